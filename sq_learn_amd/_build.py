@@ -1,0 +1,104 @@
+"""In-tree build of the native HIP layer (``sq_learn_amd/_C*.so``).
+
+Plays the role of the reference's Cython/numpy.distutils build
+(``sklearn/_build_utils/__init__.py:38-76``, ``openmp_helpers.py``): every
+``csrc/*.hip`` translation unit is compiled by ``hipcc --offload-arch=gfx950``
+(CDNA4 only - no multi-arch fatbins, no CUDA/hipify layer) and linked with
+the CPython-API marshalling module ``csrc/module.cpp`` into one extension
+that lives next to this file (so it travels with the repo snapshot to GPU
+boxes and is what the python processes load).
+
+Usage: ``python -m sq_learn_amd._build [--force] [--jobs N] [--debug]``.
+"""
+
+import argparse
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "..", "build", "sq_native")
+ARCH = os.environ.get("SQ_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def ext_path():
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(HERE, "_C" + suffix)
+
+
+def _sources():
+    hips = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+    headers = sorted(f for f in os.listdir(CSRC) if f.endswith(".h"))
+    return hips, headers
+
+
+def _newest(paths):
+    return max((os.path.getmtime(p) for p in paths), default=0.0)
+
+
+def needs_build():
+    out = ext_path()
+    if not os.path.exists(out):
+        return True
+    hips, headers = _sources()
+    srcs = [os.path.join(CSRC, f) for f in hips + headers + ["module.cpp"]] + [__file__]
+    return _newest(srcs) > os.path.getmtime(out)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("native build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(force=False, jobs=None, debug=False, verbose=False):
+    """Compile and link the extension; returns its path."""
+    out = ext_path()
+    if not force and not needs_build():
+        return out
+    os.makedirs(BUILD, exist_ok=True)
+    hips, _ = _sources()
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    common = [HIPCC, "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
+              "-Wno-unused-result", "-Wno-unused-command-line-argument"] + opt
+    py_inc = sysconfig.get_paths()["include"]
+    jobs = jobs or int(os.environ.get("MAX_JOBS", min(8, os.cpu_count() or 4)))
+
+    def compile_one(src):
+        obj = os.path.join(BUILD, src + ".o")
+        cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if src == "module.cpp":
+            cmd = [HIPCC, "-std=c++17", "-fPIC", "-O2", "-I", py_inc, "-c",
+                   os.path.join(CSRC, src), "-o", obj]
+        log = _run(cmd)
+        if verbose and log.strip():
+            print(log)
+        return obj
+
+    units = hips + ["module.cpp"]
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, units))
+    tmp = out + ".tmp"
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
+    os.replace(tmp, out)
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    path = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose)
+    print(path)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,77 @@
+"""Global configuration for sq_learn_amd.
+
+Mirrors the reference's ``sklearn/_config.py:6-150`` (``get_config`` /
+``set_config`` / ``config_context``) and adds the framework knobs that the
+MI355X build needs: the compute device, the GEMM precision
+policy for the fused distance kernels and the default counter-RNG seed.
+
+The config is process-global (one process per GPU), exactly like the
+reference; worker threads inherit it because there are none on the hot path.
+"""
+
+import os
+import threading
+from contextlib import contextmanager
+
+_global_config = {
+    # --- reference keys (sklearn/_config.py:6-11) ---
+    "assume_finite": bool(os.environ.get("SQ_ASSUME_FINITE", os.environ.get("SKLEARN_ASSUME_FINITE", False))),
+    "working_memory": int(os.environ.get("SQ_WORKING_MEMORY", os.environ.get("SKLEARN_WORKING_MEMORY", 1024))),
+    "print_changed_only": True,
+    "display": "text",
+    # --- MI355X framework keys ---
+    # 'auto' -> cuda (HIP) when a GPU is visible, else cpu
+    "device": os.environ.get("SQ_DEVICE", "auto"),
+    # precision of the distance / Gram GEMMs on GPU:
+    #   'bf16'   : bf16 operands, fp32 accumulation (MFMA 32x32x16)
+    #   'bf16x2' : data bf16, centroids split hi+lo bf16 (2 MFMA passes, ~fp32 centroid precision)
+    #   'fp32'   : fp32 operands (library GEMM + band-select kernel)
+    "gemm_precision": os.environ.get("SQ_GEMM_PRECISION", "bf16"),
+    # default seed of the counter-based (Philox) stochastic layer when an
+    # estimator is given random_state=None
+    "seed": int(os.environ.get("SQ_SEED", 0x5EED)),
+    # structured per-iteration logging (sq_learn_amd.utils.tracing)
+    "log_iterations": bool(int(os.environ.get("SQ_LOG_ITERATIONS", "0"))),
+}
+_lock = threading.Lock()
+
+
+def get_config():
+    """Return a copy of the current global configuration."""
+    return dict(_global_config)
+
+
+def set_config(assume_finite=None, working_memory=None, print_changed_only=None,
+               display=None, device=None, gemm_precision=None, seed=None,
+               log_iterations=None):
+    """Set global configuration (reference: ``sklearn/_config.py:30``)."""
+    with _lock:
+        if assume_finite is not None:
+            _global_config["assume_finite"] = assume_finite
+        if working_memory is not None:
+            _global_config["working_memory"] = working_memory
+        if print_changed_only is not None:
+            _global_config["print_changed_only"] = print_changed_only
+        if display is not None:
+            _global_config["display"] = display
+        if device is not None:
+            _global_config["device"] = device
+        if gemm_precision is not None:
+            if gemm_precision not in ("bf16", "bf16x2", "fp32"):
+                raise ValueError("gemm_precision must be 'bf16', 'bf16x2' or 'fp32'")
+            _global_config["gemm_precision"] = gemm_precision
+        if seed is not None:
+            _global_config["seed"] = int(seed)
+        if log_iterations is not None:
+            _global_config["log_iterations"] = bool(log_iterations)
+
+
+@contextmanager
+def config_context(**new_config):
+    """Temporarily change the global config (reference ``_config.py:86``)."""
+    old = get_config()
+    set_config(**new_config)
+    try:
+        yield
+    finally:
+        set_config(**old)

@@ -1,0 +1,247 @@
+"""Estimator protocol: ``BaseEstimator``, mixins and ``clone``.
+
+Behavioural parity with the reference's ``sklearn/base.py``:
+
+* ``get_params`` / ``set_params`` introspect ``__init__`` and support nested
+  ``a__b`` keys (``base.py:142-255``);
+* ``__repr__`` prints changed parameters only (``print_changed_only``);
+* pickling adds a version tag and warns on mismatch (``base.py:296-320``).
+  Unlike the reference, fitted torch tensors (possibly on a GPU) are moved to
+  host numpy in ``__getstate__``, so a model fitted on MI355X can be loaded
+  on a machine without a GPU;
+* ``_validate_data`` / ``n_features_in_`` checking (``base.py:381-451``);
+* mixins: ``ClassifierMixin.score`` (accuracy), ``RegressorMixin.score``
+  (R^2), ``ClusterMixin.fit_predict``, ``TransformerMixin.fit_transform``
+  (``base.py:482-780``).
+"""
+
+import copy
+import inspect
+import warnings
+from collections import defaultdict
+
+import numpy as np
+import torch
+
+from .exceptions import InconsistentVersionWarning
+
+
+def _framework_version():
+    from . import __version__
+    return __version__
+
+
+def clone(estimator, *, safe=True):
+    """Deep copy of an estimator's *parameters* (unfitted), reference ``base.py:30``."""
+    if isinstance(estimator, (list, tuple, set, frozenset)):
+        return type(estimator)([clone(e, safe=safe) for e in estimator])
+    if not hasattr(estimator, "get_params") or isinstance(estimator, type):
+        if not safe:
+            return copy.deepcopy(estimator)
+        raise TypeError(f"Cannot clone object '{estimator!r}' (type {type(estimator)}): "
+                        "it does not implement get_params.")
+    klass = estimator.__class__
+    params = estimator.get_params(deep=False)
+    new_params = {k: clone(v, safe=False) for k, v in params.items()}
+    new = klass(**new_params)
+    got = new.get_params(deep=False)
+    for name in new_params:
+        if got[name] is not new_params[name] and not _same_param(got[name], new_params[name]):
+            raise RuntimeError(f"Cannot clone object {estimator}, as the constructor either "
+                               f"does not set or modifies parameter {name}")
+    return new
+
+
+def _same_param(a, b):
+    try:
+        if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+            return np.array_equal(np.asarray(a), np.asarray(b))
+        return bool(a == b)
+    except Exception:  # pragma: no cover - exotic params
+        return False
+
+
+class BaseEstimator:
+    """Base class for all estimators of the framework."""
+
+    @classmethod
+    def _get_param_names(cls):
+        init = getattr(cls.__init__, "deprecated_original", cls.__init__)
+        if init is object.__init__:
+            return []
+        sig = inspect.signature(init)
+        params = [p for p in sig.parameters.values() if p.name != "self" and p.kind != p.VAR_KEYWORD]
+        for p in params:
+            if p.kind == p.VAR_POSITIONAL:
+                raise RuntimeError(f"{cls} should not have *args in __init__ ({sig}).")
+        return sorted(p.name for p in params)
+
+    def get_params(self, deep=True):
+        out = {}
+        for key in self._get_param_names():
+            value = getattr(self, key)
+            if deep and hasattr(value, "get_params") and not isinstance(value, type):
+                for k, v in value.get_params().items():
+                    out[f"{key}__{k}"] = v
+            out[key] = value
+        return out
+
+    def set_params(self, **params):
+        if not params:
+            return self
+        valid = self.get_params(deep=True)
+        nested = defaultdict(dict)
+        for key, value in params.items():
+            key, delim, sub = key.partition("__")
+            if key not in valid:
+                raise ValueError(f"Invalid parameter {key!r} for estimator {self}. "
+                                 "Check the list of available parameters with "
+                                 "`estimator.get_params().keys()`.")
+            if delim:
+                nested[key][sub] = value
+            else:
+                setattr(self, key, value)
+                valid[key] = value
+        for key, sub in nested.items():
+            valid[key].set_params(**sub)
+        return self
+
+    def __repr__(self):
+        from ._config import get_config
+        changed_only = get_config()["print_changed_only"]
+        params = self.get_params(deep=False)
+        if changed_only:
+            init_params = {}
+            try:
+                sig = inspect.signature(self.__class__.__init__)
+                init_params = {k: v.default for k, v in sig.parameters.items()}
+            except (TypeError, ValueError):  # pragma: no cover
+                pass
+            params = {k: v for k, v in params.items()
+                      if k not in init_params or not _same_param(v, init_params[k])
+                      or type(v) is not type(init_params[k])}
+        body = ", ".join(f"{k}={v!r}" for k, v in sorted(params.items()))
+        return f"{self.__class__.__name__}({body})"
+
+    # ------------------------------------------------------------------ pickle
+    def __getstate__(self):
+        state = dict(self.__dict__)
+        for k, v in list(state.items()):
+            if isinstance(v, torch.Tensor):
+                t = v.detach()
+                if t.dtype == torch.bfloat16:
+                    t = t.float()
+                state[k] = t.cpu().numpy()
+            elif k.startswith("_engine") or k.startswith("_pg"):
+                # runtime handles (process groups, kernel workspaces) are not state
+                state[k] = None
+        if type(self).__module__.startswith("sq_learn_amd."):
+            state["_sq_learn_amd_version"] = _framework_version()
+        return state
+
+    def __setstate__(self, state):
+        if type(self).__module__.startswith("sq_learn_amd."):
+            v = state.pop("_sq_learn_amd_version", "pre-0.1")
+            if v != _framework_version():
+                warnings.warn(InconsistentVersionWarning(
+                    estimator_name=self.__class__.__name__,
+                    current_version=_framework_version(), original_version=v))
+        self.__dict__.update(state)
+
+    # ----------------------------------------------------------- validation
+    def _more_tags(self):
+        return {}
+
+    def _get_tags(self):
+        tags = {"non_deterministic": False, "requires_y": False, "X_types": ["2darray"],
+                "preserves_dtype": [np.float64], "allow_nan": False, "stateless": False}
+        for base in reversed(inspect.getmro(self.__class__)):
+            if hasattr(base, "_more_tags") and "_more_tags" in vars(base):
+                tags.update(base._more_tags(self))
+        return tags
+
+    def _check_n_features(self, X, reset):
+        n = X.shape[1]
+        if reset:
+            self.n_features_in_ = n
+            return
+        if not hasattr(self, "n_features_in_"):
+            return
+        if n != self.n_features_in_:
+            raise ValueError(f"X has {n} features, but {self.__class__.__name__} "
+                             f"is expecting {self.n_features_in_} features as input.")
+
+    def _validate_data(self, X, y="no_validation", reset=True, validate_separately=False,
+                       **check_params):
+        from .utils.validation import check_array, check_X_y
+        no_y = isinstance(y, str) and y == "no_validation"
+        if no_y:
+            X = check_array(X, **check_params)
+            out = X
+        elif validate_separately:
+            cx, cy = validate_separately
+            X = check_array(X, **cx)
+            y = check_array(y, **cy)
+            out = X, y
+        else:
+            X, y = check_X_y(X, y, **check_params)
+            out = X, y
+        if check_params.get("ensure_2d", True):
+            self._check_n_features(X, reset=reset)
+        return out
+
+
+class ClassifierMixin:
+    _estimator_type = "classifier"
+
+    def score(self, X, y, sample_weight=None):
+        from .utils.metrics import accuracy_score
+        return accuracy_score(y, self.predict(X), sample_weight=sample_weight)
+
+    def _more_tags(self):
+        return {"requires_y": True}
+
+
+class RegressorMixin:
+    _estimator_type = "regressor"
+
+    def score(self, X, y, sample_weight=None):
+        from .utils.metrics import r2_score
+        return r2_score(y, self.predict(X), sample_weight=sample_weight)
+
+    def _more_tags(self):
+        return {"requires_y": True}
+
+
+class ClusterMixin:
+    _estimator_type = "clusterer"
+
+    def fit_predict(self, X, y=None, **kw):
+        self.fit(X, **kw)
+        return self.labels_
+
+
+class TransformerMixin:
+    def fit_transform(self, X, y=None, **fit_params):
+        if y is None:
+            return self.fit(X, **fit_params).transform(X)
+        return self.fit(X, y, **fit_params).transform(X)
+
+
+class DensityMixin:
+    _estimator_type = "DensityEstimator"
+
+    def score(self, X, y=None):
+        pass
+
+
+def is_classifier(est):
+    return getattr(est, "_estimator_type", None) == "classifier"
+
+
+def is_regressor(est):
+    return getattr(est, "_estimator_type", None) == "regressor"
+
+
+def is_clusterer(est):
+    return getattr(est, "_estimator_type", None) == "clusterer"

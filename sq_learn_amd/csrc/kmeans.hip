@@ -1,0 +1,662 @@
+// q-means / k-means hot loop on gfx950.
+//
+// estep_bf16 : fused distance GEMM (MFMA v_mfma_f32_32x32x16_bf16, fp32
+//              accumulation) + per-row top-2 / delta-band selection + inertia.
+//   * one workgroup = NW waves x 32 rows; each wave keeps its 32 rows of X as
+//     A fragments in VGPRs for the whole centroid sweep (X read from HBM once)
+//   * centroid tiles of 64 x d_pad bf16 stream through a 2-deep LDS ring filled
+//     by global_load_lds (LDS-DMA), XOR-swizzled (chunk ^ row&15) so the
+//     ds_read_b128 B-fragment reads are bank-conflict-free
+//   * epilogue per accumulator element: d' = ||c||^2 - 2 x.c, the centroid
+//     index packed into the low mantissa bits, then m1 = min, m2 = med3 (4 VALU)
+//   * after the sweep the 32 lanes sharing a row merge; the delta-band
+//     {j : D_ij <= min_i + delta} is resolved exactly from each lane's top-2
+//     (a lane whose 2nd-best is inside the band could hide a 3rd candidate ->
+//     the row is appended to an overflow list and re-done by band_select)
+//   * uniform choice among band members = smallest Philox key
+//     hash(seed, stream, global_row, j): shard-invariant and identical to
+//     band_select and to the torch CPU path.
+// band_select: exact selection over fp32 distance rows (fallback / generic d).
+// centroid_accumulate: label-segmented row sums (LDS counting sort per chunk,
+//              one 256-B f32 atomic row-add per (chunk, label) segment).
+// centroid_finalize: mean, empty-cluster policy, fused truncated-normal
+//              tomography noise (Utility.py:88-104), centre shift, bf16 copy
+//              and ||c||^2 for the next E-step.
+// ipe_estep : distance estimates through robust inner-product estimation
+//              (Utility.py:697-737) - median-of-Q Fejer AE per (row, centroid).
+#include "common.h"
+#include "fejer.h"
+
+namespace sq {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kBN = 64;                  // centroids per LDS tile
+constexpr float kBig = 3.0e38f;
+
+SQ_DEV float packf(float v, uint32_t keepmask, uint32_t j) {
+  return __uint_as_float((__float_as_uint(v) & keepmask) | j);
+}
+SQ_DEV float valf(float p, uint32_t keepmask) { return __uint_as_float(__float_as_uint(p) & keepmask); }
+
+SQ_DEV uint32_t band_key(const RngKey& key, long long grow, uint32_t j) {
+  unsigned long long idx = ((unsigned long long)grow << 16) | (unsigned long long)j;
+  return key.block(idx).x;
+}
+
+template <int KS, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, const float* __restrict__ cn,
+    const float* __restrict__ xn, int* __restrict__ labels, float* __restrict__ mind,
+    long long* __restrict__ ovf_rows, int* __restrict__ ovf_count, double* __restrict__ inertia,
+    long long n, int k, int k_pad, float delta, RngKey key, long long row_offset, int ovf_cap,
+    int idx_bits) {
+  constexpr int DP = KS * 16;            // padded feature count
+  constexpr int CPR = DP / 8;            // 16-B chunks per row
+  constexpr int SWZ = (CPR >= 16 ? 16 : CPR) - 1;
+  constexpr int TILE_BYTES = kBN * DP * 2;
+  constexpr int PIECES = TILE_BYTES / 1024;  // 1 KiB LDS-DMA pieces per tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* buf0 = smem;
+  unsigned char* buf1 = smem + TILE_BYTES;
+  float* cn_lds = reinterpret_cast<float*>(smem + 2 * TILE_BYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int half = lane >> 5;
+  const long long row0 = (long long)blockIdx.x * (NW * 32) + wave * 32;
+  const uint32_t keep = ~((1u << idx_bits) - 1u);
+  const int n_tiles = k_pad / kBN;
+
+  // ---- stage cn into LDS (ordinary loads, before any LDS-DMA is in flight)
+  for (int j = tid; j < k_pad; j += NW * 64) cn_lds[j] = cn[j];
+
+  // ---- issue LDS-DMA for centroid tile 0
+  auto stage = [&](int t, unsigned char* dst) {
+    const uint16_t* tile = C + (size_t)t * kBN * DP;
+    for (int p = wave; p < PIECES; p += NW) {
+      int P = p * 64 + lane;          // physical chunk written by this lane
+      int rrow = P / CPR, pc = P % CPR;
+      int lc = pc ^ (rrow & SWZ);     // logical chunk stored at (rrow, pc)
+      const uint16_t* src = tile + (size_t)rrow * DP + lc * 8;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
+    }
+  };
+  stage(0, buf0);
+
+  // ---- A fragments: this wave's 32 rows, all of K, kept in VGPRs
+  bf16x8 a[KS];
+  {
+    long long r = row0 + r32;
+    bool ok = r < n;
+    const uint16_t* xr = X + (size_t)(ok ? r : 0) * DP + half * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(xr + ks * 16);
+      a[ks] = ok ? v : (bf16x8)0;
+    }
+  }
+
+  float m1[16], m2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { m1[i] = __builtin_inff(); m2[i] = __builtin_inff(); }
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < n_tiles; ++t) {
+    unsigned char* cur = (t & 1) ? buf1 : buf0;
+    unsigned char* nxt = (t & 1) ? buf0 : buf1;
+    if (t + 1 < n_tiles) stage(t + 1, nxt);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      f32x16 acc = {0};
+      const int brow = nb * 32 + r32;
+      const unsigned char* rowp = cur + brow * (DP * 2);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        int c = ks * 2 + half;
+        int pc = c ^ (brow & SWZ);
+        bf16x8 b = *reinterpret_cast<const bf16x8*>(rowp + pc * 16);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b, acc, 0, 0, 0);
+      }
+      const uint32_t j = (uint32_t)(t * kBN + nb * 32 + r32);
+      const float cj = cn_lds[j];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float dv = __builtin_fmaf(-2.0f, acc[i], cj);
+        float pv = packf(dv, keep, j);
+        float o1 = m1[i];
+        m2[i] = __builtin_amdgcn_fmed3f(o1, pv, m2[i]);
+        m1[i] = fminf(o1, pv);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- merge the 32 lanes of each half (same rows), resolve the band
+  double my_inertia = 0.0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float M = m1[i];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) M = fminf(M, __shfl_xor(M, o, 64));
+    const int rloc = (i & 3) + 8 * (i >> 2) + 4 * half;
+    const long long grow_local = row0 + rloc;
+    const bool row_ok = grow_local < n;
+    const float mval = valf(M, keep);
+    const float thr = mval + delta;
+    const bool v1 = valf(m1[i], keep) <= thr;
+    const bool v2 = valf(m2[i], keep) <= thr;
+    unsigned long long b1 = __ballot(v1);
+    unsigned long long b2 = __ballot(v2);
+    uint32_t hb1 = (uint32_t)(b1 >> (32 * half));
+    uint32_t hb2 = (uint32_t)(b2 >> (32 * half));
+    uint32_t winner = __float_as_uint(M) & ~keep;
+    bool overflow = hb2 != 0u;
+    if (!overflow && __popc(hb1) > 1) {
+      // uniform pick among the band members: smallest Philox key
+      uint32_t jj = __float_as_uint(m1[i]) & ~keep;
+      uint32_t kk = v1 ? ((band_key(key, row_offset + grow_local, jj) & keep) | jj) : 0xFFFFFFFFu;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) kk = min(kk, (uint32_t)__shfl_xor((int)kk, o, 64));
+      winner = kk & ~keep;
+    }
+    if (r32 == (i & 31) && row_ok) {
+      float dist = fmaxf(xn[grow_local] + mval, 0.0f);
+      if (overflow) {
+        int slot = atomicAdd(ovf_count, 1);
+        if (slot < ovf_cap) ovf_rows[slot] = grow_local;
+        labels[grow_local] = -1;
+        mind[grow_local] = dist;
+      } else {
+        labels[grow_local] = (int)winner;
+        mind[grow_local] = dist;
+      }
+      my_inertia += (double)dist;
+    }
+  }
+  my_inertia = wave_sum(my_inertia);
+  if (lane == 0 && inertia) atomicAdd(inertia, my_inertia);
+}
+
+// ---------------------------------------------------------------------------
+// band_select: rows of full fp32 distances D[m][ldD] (first k valid).  One wave
+// per row.  Exact: min, band {D <= min + delta}, smallest Philox key.
+// If xn != nullptr the D rows hold ||c||^2 - 2x.c and xn is added.
+__global__ void __launch_bounds__(256) band_select_kernel(
+    const float* __restrict__ D, const long long* __restrict__ rows, const float* __restrict__ xn,
+    int* __restrict__ labels, float* __restrict__ mind, long long m, int k, long long ldD,
+    float delta, RngKey key, long long row_offset, int idx_bits) {
+  const int lane = threadIdx.x & 63;
+  const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= m) return;
+  const float* d = D + r * ldD;
+  float mn = __builtin_inff();
+  for (int j = lane; j < k; j += 64) mn = fminf(mn, d[j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+  const long long grow = rows ? rows[r] : r;
+  const float thr = mn + delta;
+  const uint32_t keep = ~((1u << idx_bits) - 1u);
+  uint32_t best = 0xFFFFFFFFu;
+  int cnt = 0;
+  for (int j = lane; j < k; j += 64) {
+    if (d[j] <= thr) {
+      ++cnt;
+      uint32_t kk = (band_key(key, row_offset + grow, (uint32_t)j) & keep) | (uint32_t)j;
+      best = min(best, kk);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    cnt += __shfl_xor(cnt, o, 64);
+  }
+  uint32_t win;
+  if (cnt <= 1) {
+    // single member: the argmin (first index at the min)
+    uint32_t am = 0xFFFFFFFFu;
+    for (int j = lane; j < k; j += 64)
+      if (d[j] == mn) am = min(am, (uint32_t)j);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = min(am, (uint32_t)__shfl_xor((int)am, o, 64));
+    win = am;
+  } else {
+    win = best & ~keep;
+  }
+  if (lane == 0) {
+    labels[grow] = (int)win;
+    float base = xn ? xn[grow] : 0.0f;
+    mind[grow] = fmaxf(base + mn, 0.0f);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// band_select_rows: fallback for rows the fused kernel flagged (a lane held
+// two band members).  Driven by the device-side count, so no host sync: the
+// grid covers the list capacity and surplus waves exit.  One wave per row,
+// lanes over centroids, full distance recomputed from the bf16 operands.
+__global__ void __launch_bounds__(256) band_select_rows_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, const float* __restrict__ cn,
+    const float* __restrict__ xn, const long long* __restrict__ rows, const int* __restrict__ count,
+    int* __restrict__ labels, long long cap, int d_pad, int k, float delta, RngKey key,
+    long long row_offset, int idx_bits) {
+  __shared__ float xs[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long slot = (long long)blockIdx.x * 4 + w;
+  long long cnt = min((long long)*count, cap);
+  if (slot >= cnt) return;
+  const long long r = rows[slot];
+  for (int c = lane; c < d_pad; c += 64) xs[w][c] = bf16_to_f32(X[(size_t)r * d_pad + c]);
+  __builtin_amdgcn_wave_barrier();
+  float mn = __builtin_inff();
+  // pass 1: min
+  for (int j = lane; j < k; j += 64) {
+    const uint16_t* cr = C + (size_t)j * d_pad;
+    float s = 0.f;
+    for (int c = 0; c < d_pad; c += 2) {
+      uint32_t v = *reinterpret_cast<const uint32_t*>(cr + c);
+      s += xs[w][c] * __uint_as_float(v << 16) + xs[w][c + 1] * __uint_as_float(v & 0xFFFF0000u);
+    }
+    float dv = cn[j] - 2.0f * s;
+    mn = fminf(mn, dv);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+  const float thr = mn + delta;
+  const uint32_t keep = ~((1u << idx_bits) - 1u);
+  uint32_t best = 0xFFFFFFFFu;
+  int nc = 0;
+  uint32_t am = 0xFFFFFFFFu;
+  for (int j = lane; j < k; j += 64) {
+    const uint16_t* cr = C + (size_t)j * d_pad;
+    float s = 0.f;
+    for (int c = 0; c < d_pad; c += 2) {
+      uint32_t v = *reinterpret_cast<const uint32_t*>(cr + c);
+      s += xs[w][c] * __uint_as_float(v << 16) + xs[w][c + 1] * __uint_as_float(v & 0xFFFF0000u);
+    }
+    float dv = cn[j] - 2.0f * s;
+    if (dv == mn) am = min(am, (uint32_t)j);
+    if (dv <= thr) {
+      ++nc;
+      best = min(best, (band_key(key, row_offset + r, (uint32_t)j) & keep) | (uint32_t)j);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    am = min(am, (uint32_t)__shfl_xor((int)am, o, 64));
+    nc += __shfl_xor(nc, o, 64);
+  }
+  if (lane == 0) labels[r] = (int)(nc <= 1 ? am : (best & ~keep));
+}
+
+// ---------------------------------------------------------------------------
+// centroid_accumulate: chunk of CH rows per workgroup (256 threads).
+template <typename T>
+SQ_DEV float4 load4(const T* p);
+template <>
+SQ_DEV float4 load4<float>(const float* p) { return *reinterpret_cast<const float4*>(p); }
+template <>
+SQ_DEV float4 load4<uint16_t>(const uint16_t* p) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+                     __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) centroid_accumulate_kernel(
+    const T* __restrict__ X, const int* __restrict__ labels, const float* __restrict__ w,
+    float* __restrict__ sums, double* __restrict__ counts, long long n, int d, int k, int CH) {
+  extern __shared__ __attribute__((aligned(16))) int sm[];
+  int* hist = sm;            // k
+  int* cursor = sm + k;      // k
+  int* perm = sm + 2 * k;    // CH
+  const int tid = threadIdx.x;
+  const long long r0 = (long long)blockIdx.x * CH;
+  const int rows = (int)min((long long)CH, n - r0);
+  for (int j = tid; j < k; j += 256) hist[j] = 0;
+  __syncthreads();
+  for (int i = tid; i < rows; i += 256) {
+    int l = labels[r0 + i];
+    if (l >= 0 && l < k) atomicAdd(&hist[l], 1);
+  }
+  __syncthreads();
+  // exclusive scan of hist -> cursor (single wave, k/64 per lane)
+  if (tid < 64) {
+    int per = (k + 63) / 64;
+    int b = tid * per, e = min(b + per, k);
+    int s = 0;
+    for (int j = b; j < e; ++j) s += hist[j];
+    int incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int v = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += v;
+    }
+    int run = incl - s;
+    for (int j = b; j < e; ++j) { cursor[j] = run; run += hist[j]; }
+  }
+  __syncthreads();
+  for (int i = tid; i < rows; i += 256) {
+    int l = labels[r0 + i];
+    if (l >= 0 && l < k) {
+      int pos = atomicAdd(&cursor[l], 1);
+      perm[pos] = i;
+    }
+  }
+  __syncthreads();
+  // cursor[l] now = end of segment l; start = end - hist[l]
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int l = wave; l < k; l += 4) {
+    int cnt = hist[l];
+    if (cnt == 0) continue;
+    int end = cursor[l], beg = end - cnt;
+    for (int c0 = lane * 4; c0 < d; c0 += 256) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int p = beg; p < end; ++p) {
+        long long r = r0 + perm[p];
+        float4 v = load4<T>(X + (size_t)r * d + c0);
+        float ww = w ? w[r] : 1.0f;
+        acc.x += ww * v.x; acc.y += ww * v.y; acc.z += ww * v.z; acc.w += ww * v.w;
+      }
+      float* dst = sums + (size_t)l * d + c0;
+      atomicAdd(dst + 0, acc.x);
+      if (c0 + 1 < d) atomicAdd(dst + 1, acc.y);
+      if (c0 + 2 < d) atomicAdd(dst + 2, acc.z);
+      if (c0 + 3 < d) atomicAdd(dst + 3, acc.w);
+    }
+    if (lane == 0) {
+      double wsum = 0.0;
+      if (w) { for (int p = beg; p < end; ++p) wsum += (double)w[r0 + perm[p]]; }
+      else wsum = (double)cnt;
+      atomicAdd(&counts[l], wsum);
+    }
+  }
+}
+
+// packed[0:k*d] = sums (f64), packed[k*d : k*d+k] = counts, packed[k*d+k] = inertia
+__global__ void __launch_bounds__(256) pack_stats_kernel(
+    const float* __restrict__ sums, const double* __restrict__ counts,
+    const double* __restrict__ inertia, double* __restrict__ packed, int k, int d) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  long long kd = (long long)k * d;
+  if (i < kd) packed[i] = (double)sums[i];
+  else if (i < kd + k) packed[i] = counts[i - kd];
+  else if (i == kd + k) packed[i] = inertia ? inertia[0] : 0.0;
+}
+
+// one workgroup per (padded) centroid row
+__global__ void __launch_bounds__(256) centroid_finalize_kernel(
+    const double* __restrict__ packed, const float* __restrict__ C_old, float* __restrict__ C_new,
+    uint16_t* __restrict__ C_bf16, float* __restrict__ cn, double* __restrict__ shift, int k, int d,
+    int d_pad, float b, float erf_b, RngKey key, int empty_policy) {
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ double red[4];
+  __shared__ float redf[4];
+  if (j >= k) {
+    for (int c = tid; c < d_pad; c += 256) C_bf16[(size_t)j * d_pad + c] = 0;
+    if (tid == 0) cn[j] = kBig;
+    return;
+  }
+  const double cntv = packed[(size_t)k * d + j];
+  double sh = 0.0;
+  float nn = 0.0f;
+  for (int c = tid; c < d_pad; c += 256) {
+    uint16_t hb = 0;
+    if (c < d) {
+      float old = C_old[(size_t)j * d + c];
+      float v;
+      if (cntv > 0.0) v = (float)(packed[(size_t)j * d + c] / cntv);
+      else v = empty_policy == 0 ? old : 0.0f;
+      if (b > 0.0f) v += trunc_normal(key.word((unsigned long long)j * d + c), b, erf_b);
+      C_new[(size_t)j * d + c] = v;
+      double df = (double)v - (double)old;
+      sh += df * df;
+      hb = f32_to_bf16_rne(v);
+      float hv = bf16_to_f32(hb);
+      nn += hv * hv;
+    }
+    C_bf16[(size_t)j * d_pad + c] = hb;
+  }
+  sh = wave_sum(sh);
+  nn = wave_sum(nn);
+  if ((tid & 63) == 0) { red[tid >> 6] = sh; redf[tid >> 6] = nn; }
+  __syncthreads();
+  if (tid == 0) {
+    atomicAdd(shift, red[0] + red[1] + red[2] + red[3]);
+    cn[j] = redf[0] + redf[1] + redf[2] + redf[3];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// IPE distances: G[m][ldG] = x_i . c_j (fp32).  One workgroup (256) per row.
+// D~_ij = |x|^2 + |c|^2 - 2 IPE(x, c); label = argmin with random tie-break.
+__global__ void __launch_bounds__(256) ipe_estep_kernel(
+    const float* __restrict__ G, const float* __restrict__ xn, const float* __restrict__ cn,
+    int* __restrict__ labels, float* __restrict__ mind, long long m, int k, long long ldG,
+    double eps, int Q, RngKey key, long long row_offset, int idx_bits) {
+  const long long r = blockIdx.x;
+  const int tid = threadIdx.x;
+  const long long grow = row_offset + r;
+  const double nx2 = (double)xn[r];
+  float best = __builtin_inff();
+  uint32_t bestk = 0xFFFFFFFFu;
+  const uint32_t keep = ~((1u << idx_bits) - 1u);
+  __shared__ float sbest[4];
+  __shared__ uint32_t skey[4];
+  double est[31];
+  for (int j = tid; j < k; j += 256) {
+    double ip = (double)G[r * ldG + j];
+    double ny2 = (double)cn[j];
+    double S = nx2 + ny2;
+    double dtil;
+    if (S <= 0.0) {
+      dtil = 0.0;
+    } else {
+      double a = (S - 2.0 * ip) / (2.0 * S);
+      if (fabs(a) <= 1e-15) a = 0.0;
+      double eps_a = eps * fmax(1.0, fabs(ip)) / S;
+      long long M = ae_bins(eps_a);
+      if (M > (1LL << 40)) M = 1LL << 40;
+      unsigned long long sid = ((unsigned long long)grow * (unsigned long long)k + j) * Q;
+      for (int q = 0; q < Q; ++q) {
+        WordStream ws(key, sid + q);
+        est[q] = ae_sample(a, M, ws);
+      }
+      double at = Q == 1 ? est[0] : median_of<31>(est, Q);
+      double s = S * (1.0 - 2.0 * at) / 2.0;
+      dtil = nx2 + ny2 - 2.0 * s;
+    }
+    float df = (float)dtil;
+    uint32_t rk = (band_key(key, grow, (uint32_t)j) & keep) | (uint32_t)j;
+    if (df < best || (df == best && rk < bestk)) { best = df; bestk = rk; }
+  }
+  // block argmin over (value, key)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ob = __shfl_xor(best, o, 64);
+    uint32_t ok = (uint32_t)__shfl_xor((int)bestk, o, 64);
+    if (ob < best || (ob == best && ok < bestk)) { best = ob; bestk = ok; }
+  }
+  if ((tid & 63) == 0) { sbest[tid >> 6] = best; skey[tid >> 6] = bestk; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (sbest[w] < best || (sbest[w] == best && skey[w] < bestk)) { best = sbest[w]; bestk = skey[w]; }
+    labels[grow - row_offset] = (int)(bestk & ~keep);
+    mind[grow - row_offset] = best;
+  }
+}
+
+}  // namespace sq
+
+using namespace sq;
+
+static int idx_bits_for(int k_pad) {
+  int b = 1;
+  while ((1 << b) < k_pad) ++b;
+  return b;
+}
+
+template <int KS, int NW>
+static int launch_estep(const void* X, const void* C, const void* cn, const void* xn, void* labels,
+                        void* mind, void* ovf_rows, void* ovf_count, void* inertia, long long n,
+                        int k, int k_pad, float delta, RngKey key, long long row_offset,
+                        int ovf_cap, hipStream_t st) {
+  constexpr int DP = KS * 16;
+  size_t lds = 2 * (size_t)kBN * DP * 2 + (size_t)k_pad * 4;
+  auto kern = estep_kernel<KS, NW>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  long long rows_per_wg = NW * 32;
+  unsigned grid = (unsigned)((n + rows_per_wg - 1) / rows_per_wg);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const uint16_t*)X,
+                     (const uint16_t*)C, (const float*)cn, (const float*)xn, (int*)labels,
+                     (float*)mind, (long long*)ovf_rows, (int*)ovf_count, (double*)inertia, n, k,
+                     k_pad, delta, key, row_offset, ovf_cap, idx_bits_for(k_pad));
+  return (int)hipGetLastError();
+}
+
+extern "C" {
+
+int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn, const void* xn,
+                  void* labels, void* mind, void* ovf_rows, void* ovf_count, void* inertia,
+                  long long n, int d, int k, int k_pad, double delta, int split, unsigned k0,
+                  unsigned k1, unsigned s0, unsigned s1, long long row_offset, int ovf_cap,
+                  void* stream) {
+  (void)Clo;
+  if (n <= 0) return 0;
+  if (split) return (int)hipErrorInvalidValue;              // bf16x2 uses the generic path
+  if (k_pad % kBN != 0 || k_pad > 32768 || k > k_pad) return (int)hipErrorInvalidValue;
+  if ((size_t)k_pad * 4 + 2 * (size_t)kBN * d * 2 > 160 * 1024) return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  hipStream_t st = (hipStream_t)stream;
+  float dl = (float)delta;
+  int nw = 4;
+  const char* env = getenv("SQ_ESTEP_NW");
+  if (env && env[0] == '8') nw = 8;
+#define ESTEP_CASE(KS)                                                                           \
+  case KS * 16:                                                                                  \
+    return nw == 8 ? launch_estep<KS, 8>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count,        \
+                                         inertia, n, k, k_pad, dl, key, row_offset, ovf_cap, st) \
+                   : launch_estep<KS, 4>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count,        \
+                                         inertia, n, k, k_pad, dl, key, row_offset, ovf_cap, st);
+  switch (d) {
+    ESTEP_CASE(1)
+    ESTEP_CASE(2)
+    ESTEP_CASE(4)
+    ESTEP_CASE(8)
+    ESTEP_CASE(16)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef ESTEP_CASE
+}
+
+int sq_band_select(const void* D, const void* rows, const void* xn, void* labels, void* mind,
+                   long long m, int k, long long ldD, double delta, unsigned k0, unsigned k1,
+                   unsigned s0, unsigned s1, long long row_offset, void* stream) {
+  if (m <= 0) return 0;
+  RngKey key{k0, k1, s0, s1};
+  int kp = ((k + 63) / 64) * 64;
+  hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)((m + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)D, (const long long*)rows,
+                     (const float*)xn, (int*)labels, (float*)mind, m, k, ldD, (float)delta, key,
+                     row_offset, idx_bits_for(kp));
+  return (int)hipGetLastError();
+}
+
+int sq_band_select_rows(const void* X, const void* C, const void* cn, const void* xn,
+                        const void* rows, const void* count, void* labels, long long cap,
+                        int d_pad, int k, int k_pad, double delta, unsigned k0, unsigned k1,
+                        unsigned s0, unsigned s1, long long row_offset, void* stream) {
+  if (cap <= 0) return 0;
+  if (d_pad > 256) return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  hipLaunchKernelGGL(band_select_rows_kernel, dim3((unsigned)((cap + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const uint16_t*)X, (const uint16_t*)C,
+                     (const float*)cn, (const float*)xn, (const long long*)rows,
+                     (const int*)count, (int*)labels, cap, d_pad, k, (float)delta, key,
+                     row_offset, idx_bits_for(k_pad));
+  return (int)hipGetLastError();
+}
+
+int sq_centroid_accumulate(const void* X, int xdtype, const void* labels, const void* weights,
+                           void* sums, void* counts, long long n, int d, int k, int chunk,
+                           void* stream) {
+  if (n <= 0) return 0;
+  if (d % 4 != 0) return (int)hipErrorInvalidValue;
+  size_t lds = (size_t)(2 * k + chunk) * 4;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  unsigned grid = (unsigned)((n + chunk - 1) / chunk);
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == 0) {
+    hipFuncSetAttribute((const void*)centroid_accumulate_kernel<float>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipLaunchKernelGGL(centroid_accumulate_kernel<float>, dim3(grid), dim3(256), lds, st,
+                       (const float*)X, (const int*)labels, (const float*)weights, (float*)sums,
+                       (double*)counts, n, d, k, chunk);
+  } else if (xdtype == 2) {
+    hipFuncSetAttribute((const void*)centroid_accumulate_kernel<uint16_t>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipLaunchKernelGGL(centroid_accumulate_kernel<uint16_t>, dim3(grid), dim3(256), lds, st,
+                       (const uint16_t*)X, (const int*)labels, (const float*)weights, (float*)sums,
+                       (double*)counts, n, d, k, chunk);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+int sq_pack_stats(const void* sums, const void* counts, const void* inertia, void* packed, int k,
+                  int d, void* stream) {
+  long long tot = (long long)k * d + k + 1;
+  hipLaunchKernelGGL(pack_stats_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)sums, (const double*)counts,
+                     (const double*)inertia, (double*)packed, k, d);
+  return (int)hipGetLastError();
+}
+
+int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
+                         void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
+                         unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
+                         void* stream) {
+  (void)C_lo;
+  RngKey key{k0, k1, s0, s1};
+  float b = (float)noise_b;
+  float eb = erff(b * 0.70710678118654752f);
+  int d_pad = d <= 16 ? 16 : (d <= 32 ? 32 : (d <= 64 ? 64 : (d <= 128 ? 128 : (d <= 256 ? 256 : ((d + 15) / 16) * 16))));
+  hipLaunchKernelGGL(centroid_finalize_kernel, dim3((unsigned)k_pad), dim3(256), 0,
+                     (hipStream_t)stream, (const double*)packed, (const float*)C_old,
+                     (float*)C_new, (uint16_t*)C_bf16, (float*)cn, (double*)shift, k, d, d_pad, b,
+                     eb, key, empty_policy);
+  return (int)hipGetLastError();
+}
+
+int sq_ipe_estep(const void* G, const void* xn, const void* cn, void* labels, void* mind,
+                 long long m, int k, long long ldG, double eps, int Q, unsigned k0, unsigned k1,
+                 unsigned s0, unsigned s1, long long row_offset, void* stream) {
+  if (m <= 0) return 0;
+  if (Q < 1 || Q > 31) return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  int kp = ((k + 63) / 64) * 64;
+  hipLaunchKernelGGL(ipe_estep_kernel, dim3((unsigned)m), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)G, (const float*)xn, (const float*)cn, (int*)labels,
+                     (float*)mind, m, k, ldG, eps, Q, key, row_offset, idx_bits_for(kp));
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,362 @@
+// Tall-skinny linear algebra for qPCA / q-means preludes (SURVEY.md §2.6
+// K13-K15) on gfx950.
+//
+// gram       : G += (X-mu)^T (X-mu) over a row range, exact fp32 MFMA
+//              (v_mfma_f32_16x16x4_f32); one pass over X, centring fused into
+//              the LDS staging; upper-triangular 64x64 output tiles, split-K
+//              over row ranges, partials combined with 256-B f32 atomics.
+// power_iter : Z += (X-mu)^T ((X-mu) Q) fused - the randomized range-finder
+//              power iteration reads X once per iteration; Y never touches HBM
+//              (phase 1 Y = Xc Q per wave -> LDS, phase 2 Z += Xc^T Y).
+// mu_sums    : all exponents of the mu(A) p-grid in one pass
+//              (row power sums -> max, column power sums) (Utility.py:196-231).
+// row_norms  : ||x_i||^2 for bf16/fp32 rows.
+#include "common.h"
+
+namespace sq {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+template <typename T> SQ_DEV float ld1(const T* p, size_t i);
+template <> SQ_DEV float ld1<float>(const float* p, size_t i) { return p[i]; }
+template <> SQ_DEV float ld1<uint16_t>(const uint16_t* p, size_t i) { return bf16_to_f32(p[i]); }
+
+// ------------------------------------------------------------------ gram
+// tile 64x64 of G (features a0.., b0..), 4 waves each 32x32 (2x2 blocks 16x16)
+// rows staged RS at a time: LDS A[RS][64+1], B[RS][64+1] fp32 (centred)
+constexpr int GT = 64;
+constexpr int GRS = 64;
+
+template <typename T>
+__global__ void __launch_bounds__(256) gram_kernel(const T* __restrict__ X, float* __restrict__ G,
+                                                   const float* __restrict__ mean, long long n,
+                                                   int d, int n_tiles_side, long long rows_per_split) {
+  __shared__ float As[GRS][GT + 1];
+  __shared__ float Bs[GRS][GT + 1];
+  // decode upper-triangular tile id
+  int tile = blockIdx.x;
+  int ta = 0;
+  while (tile >= n_tiles_side - ta) { tile -= n_tiles_side - ta; ++ta; }
+  int tb = ta + tile;
+  const int a0 = ta * GT, b0 = tb * GT;
+  const long long r_beg = (long long)blockIdx.y * rows_per_split;
+  const long long r_end = min(n, r_beg + rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wa = (wave >> 1) * 32, wb = (wave & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (long long r = r_beg; r < r_end; r += GRS) {
+    // stage (coalesced: consecutive threads -> consecutive features)
+    for (int e = tid; e < GRS * GT; e += 256) {
+      int rr = e / GT, c = e % GT;
+      long long row = r + rr;
+      float va = 0.f, vb = 0.f;
+      if (row < r_end) {
+        if (a0 + c < d) va = ld1<T>(X, (size_t)row * d + a0 + c) - mean[a0 + c];
+        if (b0 + c < d) vb = ld1<T>(X, (size_t)row * d + b0 + c) - mean[b0 + c];
+      }
+      As[rr][c] = va;
+      Bs[rr][c] = vb;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < GRS; k += 4) {
+      const int kr = k + (lane >> 4);
+      float av[2], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = As[kr][wa + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[kr][wb + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C/D map 16x16: col = lane&15, row = (lane>>4)*4 + reg
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int ra = a0 + wa + i * 16 + (lane >> 4) * 4 + g;
+        int cb = b0 + wb + j * 16 + (lane & 15);
+        if (ra < d && cb < d) atomicAdd(&G[(size_t)ra * d + cb], acc[i][j][g]);
+      }
+}
+
+// ------------------------------------------------------------ power_iter
+// 64 rows per step: wave w computes Y[16w..16w+15][0..l) = Xc Q, writes LDS;
+// then wave w accumulates Z[f in group w][0..l) += Xc^T Y over the 64 rows.
+template <typename T, int DP, int LP>
+__global__ void __launch_bounds__(256, 1) power_iter_kernel(
+    const T* __restrict__ X, const float* __restrict__ Q, float* __restrict__ Z,
+    const float* __restrict__ mean, long long n, int d, int l, long long rows_per_wg) {
+  constexpr int RS = 64;
+  constexpr int XP = DP + 1;           // padded row (bank-conflict-free column reads)
+  constexpr int YP = LP + 1;
+  constexpr int FB = DP / 16 / 4;      // f-blocks (16 wide) per wave
+  constexpr int LB = LP / 16;          // l-blocks per wave
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Xs = sm;                      // [RS][XP]
+  float* Qs = Xs + RS * XP;            // [DP][LP]
+  float* Ys = Qs + DP * LP;            // [RS][YP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < DP * LP; e += 256) {
+    int f = e / LP, c = e % LP;
+    Qs[e] = (f < d && c < l) ? Q[(size_t)f * l + c] : 0.f;
+  }
+  f32x4 z[FB][LB];
+#pragma unroll
+  for (int i = 0; i < FB; ++i)
+#pragma unroll
+    for (int j = 0; j < LB; ++j) z[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const long long r_beg = (long long)blockIdx.x * rows_per_wg;
+  const long long r_end = min(n, r_beg + rows_per_wg);
+  for (long long r = r_beg; r < r_end; r += RS) {
+    __syncthreads();
+    for (int e = tid; e < RS * DP; e += 256) {
+      int rr = e / DP, c = e % DP;
+      long long row = r + rr;
+      float v = 0.f;
+      if (row < r_end && c < d) v = ld1<T>(X, (size_t)row * d + c) - mean[c];
+      Xs[rr * XP + c] = v;
+    }
+    __syncthreads();
+    // phase 1: Y[16 rows of wave][LP]
+    {
+      f32x4 y[LB];
+#pragma unroll
+      for (int j = 0; j < LB; ++j) y[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const int yr = wave * 16 + (lane & 15);
+      for (int k = 0; k < DP; k += 4) {
+        const int kf = k + (lane >> 4);
+        float av = Xs[yr * XP + kf];
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+          float bv = Qs[kf * LP + j * 16 + (lane & 15)];
+          y[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, y[j], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < LB; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          Ys[(wave * 16 + (lane >> 4) * 4 + g) * YP + j * 16 + (lane & 15)] = y[j][g];
+    }
+    __syncthreads();
+    // phase 2: Z[f][c] += sum_rows Xc[row][f] Y[row][c]
+    for (int k = 0; k < RS; k += 4) {
+      const int kr = k + (lane >> 4);
+      float bv[LB];
+#pragma unroll
+      for (int j = 0; j < LB; ++j) bv[j] = Ys[kr * YP + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        float av = Xs[kr * XP + (wave * FB + i) * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < LB; ++j)
+          z[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], z[i][j], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FB; ++i)
+#pragma unroll
+    for (int j = 0; j < LB; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int f = (wave * FB + i) * 16 + (lane >> 4) * 4 + g;
+        int c = j * 16 + (lane & 15);
+        if (f < d && c < l) atomicAdd(&Z[(size_t)f * l + c], z[i][j][g]);
+      }
+}
+
+// ------------------------------------------------------------------ mu
+// 8 columns per thread, 32 threads per row, 2 rows per wave, 8 rows per WG step.
+constexpr int MUQ = 12;
+
+template <typename T>
+__global__ void __launch_bounds__(256) mu_sums_kernel(
+    const T* __restrict__ X, const float* __restrict__ qs, int nq, float* __restrict__ rowmax,
+    float* __restrict__ colsum, long long n, int d, long long rows_per_wg) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int sub = lane & 31;                 // thread within row group
+  const int rgrp = tid >> 5;                 // 8 row groups per WG
+  float q[MUQ];
+#pragma unroll
+  for (int i = 0; i < MUQ; ++i) q[i] = i < nq ? qs[i] : 0.f;
+  float rmax[MUQ];
+#pragma unroll
+  for (int i = 0; i < MUQ; ++i) rmax[i] = 0.f;
+  const long long r_beg = (long long)blockIdx.x * rows_per_wg;
+  const long long r_end = min(n, r_beg + rows_per_wg);
+  for (int cb = 0; cb < d; cb += 256) {
+    const int c0 = cb + sub * 8;
+    float cs[MUQ][8];
+#pragma unroll
+    for (int i = 0; i < MUQ; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[i][e] = 0.f;
+    // NOTE: for d > 256 the row sums are accumulated across column blocks in
+    // rsum_acc (per row group lane 0) - handled by the host splitting d <= 256
+    for (long long r = r_beg + rgrp; r < r_end; r += 8) {
+      float lg[8];
+      bool nz[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = (c0 + e < d) ? fabsf(ld1<T>(X, (size_t)r * d + c0 + e)) : 0.f;
+        nz[e] = v != 0.f;
+        lg[e] = __log2f(v);
+      }
+#pragma unroll
+      for (int i = 0; i < MUQ; ++i) {
+        if (i >= nq) break;
+        float rs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float p = q[i] == 0.f ? (nz[e] ? 1.f : 0.f) : (nz[e] ? exp2f(q[i] * lg[e]) : 0.f);
+          cs[i][e] += p;
+          rs += p;
+        }
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) rs += __shfl_xor(rs, o, 64);
+        rmax[i] = fmaxf(rmax[i], rs);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MUQ; ++i) {
+      if (i >= nq) break;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c0 + e < d) atomicAdd(&colsum[(size_t)i * d + c0 + e], cs[i][e]);
+    }
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int i = 0; i < MUQ; ++i)
+      if (i < nq) atomic_max_pos(&rowmax[i], rmax[i]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) row_norms_kernel(const T* __restrict__ X, float* __restrict__ out,
+                                                        long long n, int d) {
+  const int lane = threadIdx.x & 63;
+  const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    float v = ld1<T>(X, (size_t)r * d + c);
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s;
+}
+
+}  // namespace sq
+
+using namespace sq;
+
+template <typename T, int DP, int LP>
+static int launch_pi(const void* X, const void* Q, void* Z, const void* mean, long long n, int d,
+                     int l, hipStream_t st) {
+  size_t lds = ((size_t)64 * (DP + 1) + (size_t)DP * LP + (size_t)64 * (LP + 1)) * 4;
+  auto kern = power_iter_kernel<T, DP, LP>;
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  long long wgs = min(1024LL, max(1LL, (n + 1023) / 1024));
+  long long rpw = ((n + wgs - 1) / wgs + 63) / 64 * 64;
+  wgs = (n + rpw - 1) / rpw;
+  hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(256), lds, st, (const T*)X, (const float*)Q,
+                     (float*)Z, (const float*)mean, n, d, l, rpw);
+  return (int)hipGetLastError();
+}
+
+extern "C" {
+
+int sq_gram_bf16(const void* X, int xdtype, void* G, const void* mean, long long n, int d,
+                 void* stream) {
+  if (n <= 0) return 0;
+  int side = (d + GT - 1) / GT;
+  int tiles = side * (side + 1) / 2;
+  int splits = (int)max(1LL, min(2048LL / tiles, (n + 4095) / 4096));
+  long long rps = ((n + splits - 1) / splits + GRS - 1) / GRS * GRS;
+  splits = (int)((n + rps - 1) / rps);
+  dim3 grid(tiles, splits);
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == 0)
+    hipLaunchKernelGGL(gram_kernel<float>, grid, dim3(256), 0, st, (const float*)X, (float*)G,
+                       (const float*)mean, n, d, side, rps);
+  else if (xdtype == 2)
+    hipLaunchKernelGGL(gram_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)X,
+                       (float*)G, (const float*)mean, n, d, side, rps);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+int sq_power_iter(const void* X, int xdtype, const void* Q, void* Z, const void* mean, long long n,
+                  int d, int l, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (l > 64 || d > 256) return (int)hipErrorInvalidValue;
+  int DP = d <= 64 ? 64 : (d <= 128 ? 128 : 256);
+  int LP = l <= 16 ? 16 : (l <= 32 ? 32 : 64);
+#define PI_CASE(TT, D_, L_) \
+  if (DP == D_ && LP == L_) return launch_pi<TT, D_, L_>(X, Q, Z, mean, n, d, l, st);
+  if (xdtype == 0) {
+    PI_CASE(float, 64, 16) PI_CASE(float, 64, 32) PI_CASE(float, 64, 64)
+    PI_CASE(float, 128, 16) PI_CASE(float, 128, 32) PI_CASE(float, 128, 64)
+    PI_CASE(float, 256, 16) PI_CASE(float, 256, 32) PI_CASE(float, 256, 64)
+  } else if (xdtype == 2) {
+    PI_CASE(uint16_t, 64, 16) PI_CASE(uint16_t, 64, 32) PI_CASE(uint16_t, 64, 64)
+    PI_CASE(uint16_t, 128, 16) PI_CASE(uint16_t, 128, 32) PI_CASE(uint16_t, 128, 64)
+    PI_CASE(uint16_t, 256, 16) PI_CASE(uint16_t, 256, 32) PI_CASE(uint16_t, 256, 64)
+  }
+#undef PI_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+int sq_mu_sums(const void* X, int xdtype, const void* qs, int nq, void* rowmax, void* colsum,
+               long long n, int d, void* stream) {
+  if (n <= 0) return 0;
+  if (nq > MUQ || d > 256) return (int)hipErrorInvalidValue;
+  long long wgs = min(4096LL, max(1LL, (n + 255) / 256));
+  long long rpw = (n + wgs - 1) / wgs;
+  wgs = (n + rpw - 1) / rpw;
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == 0)
+    hipLaunchKernelGGL(mu_sums_kernel<float>, dim3((unsigned)wgs), dim3(256), 0, st,
+                       (const float*)X, (const float*)qs, nq, (float*)rowmax, (float*)colsum, n, d,
+                       rpw);
+  else if (xdtype == 2)
+    hipLaunchKernelGGL(mu_sums_kernel<uint16_t>, dim3((unsigned)wgs), dim3(256), 0, st,
+                       (const uint16_t*)X, (const float*)qs, nq, (float*)rowmax, (float*)colsum, n,
+                       d, rpw);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream) {
+  if (n <= 0) return 0;
+  unsigned grid = (unsigned)((n + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == 0)
+    hipLaunchKernelGGL(row_norms_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)X,
+                       (float*)out, n, d);
+  else if (xdtype == 2)
+    hipLaunchKernelGGL(row_norms_kernel<uint16_t>, dim3(grid), dim3(256), 0, st,
+                       (const uint16_t*)X, (float*)out, n, d);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

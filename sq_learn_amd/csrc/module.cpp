@@ -1,0 +1,247 @@
+// CPython extension module ``sq_learn_amd._C``: thin argument marshalling to
+// the extern "C" launchers of the .hip translation units.  Pointers arrive as
+// integers (tensor.data_ptr()), the HIP stream as the integer handle of
+// torch.cuda.current_stream(), so every launch is stream-ordered with torch
+// and capturable in a hipGraph.  No torch C++ headers: the native layer is
+// ABI-independent of the torch build.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+// qrand.hip
+__attribute__((weak)) int sq_trunc_normal_add(void*, int, long long, double, unsigned, unsigned, unsigned, unsigned,
+                        unsigned long long, void*);
+__attribute__((weak)) int sq_philox_normal(void*, int, long long, double, double, unsigned, unsigned, unsigned, unsigned,
+                     unsigned long long, void*);
+__attribute__((weak)) int sq_philox_uniform(void*, long long, unsigned, unsigned, unsigned, unsigned, unsigned long long,
+                      void*);
+__attribute__((weak)) int sq_ae_batch(const void*, const void*, void*, long long, int, unsigned, unsigned, unsigned,
+                unsigned, unsigned long long, void*);
+__attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long, unsigned, unsigned, unsigned, unsigned,
+                unsigned long long, void*);
+// kmeans.hip
+__attribute__((weak)) int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn, const void* xn,
+                  void* labels, void* mind, void* ovf_rows, void* ovf_count, void* inertia,
+                  long long n, int d, int k, int k_pad, double delta, int split, unsigned k0,
+                  unsigned k1, unsigned s0, unsigned s1, long long row_offset, int ovf_cap,
+                  void* stream);
+__attribute__((weak)) int sq_band_select(const void* D, const void* rows, const void* xn, void* labels, void* mind,
+                   long long m, int k, long long ldD, double delta, unsigned k0, unsigned k1,
+                   unsigned s0, unsigned s1, long long row_offset, void* stream);
+__attribute__((weak)) int sq_band_select_rows(const void*, const void*, const void*, const void*, const void*,
+                        const void*, void*, long long, int, int, int, double, unsigned, unsigned,
+                        unsigned, unsigned, long long, void*);
+__attribute__((weak)) int sq_centroid_accumulate(const void* X, int xdtype, const void* labels, const void* weights,
+                           void* sums, void* counts, long long n, int d, int k, int chunk,
+                           void* stream);
+__attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
+                         void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
+                         unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
+                         void* stream);
+__attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia, void* packed, int k,
+                  int d, void* stream);
+__attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void* cn, void* labels, void* mind,
+                 long long m, int k, long long ldG, double eps, int Q, unsigned k0, unsigned k1,
+                 unsigned s0, unsigned s1, long long row_offset, void* stream);
+// linalg.hip
+__attribute__((weak)) int sq_gram_bf16(const void* X, int xdtype, void* G, const void* mean, long long n, int d,
+                 void* stream);
+__attribute__((weak)) int sq_power_iter(const void* X, int xdtype, const void* Q, void* Z, const void* mean, long long n,
+                  int d, int l, void* stream);
+__attribute__((weak)) int sq_mu_sums(const void* X, int xdtype, const void* qs, int nq, void* rowmax, void* colsum,
+               long long n, int d, void* stream);
+__attribute__((weak)) int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream);
+// knn.hip
+__attribute__((weak)) int sq_knn_topk(const void* D, void* outd, void* outi, long long m, int nref, long long ldD, int kk,
+                long long col_offset, void* stream);
+}
+
+#define CHECK(fn) if (!(fn)) { PyErr_SetString(PyExc_RuntimeError, "native symbol " #fn " not built"); return nullptr; }
+static PyObject* ret(int rc) {
+  if (rc != 0) {
+    PyErr_Format(PyExc_RuntimeError, "sq_learn_amd native launch failed: %s (%d)",
+                 hipGetErrorString((hipError_t)rc), rc);
+    return nullptr;
+  }
+  Py_RETURN_NONE;
+}
+
+#define P(x) ((void*)(uintptr_t)(x))
+
+static PyObject* py_trunc_normal_add(PyObject*, PyObject* a) {
+  unsigned long long x, off, st; int dt; long long n; double b; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KiLdIIIIKK", &x, &dt, &n, &b, &k0, &k1, &s0, &s1, &off, &st)) return nullptr;
+  CHECK(sq_trunc_normal_add)
+  int rc; Py_BEGIN_ALLOW_THREADS rc = sq_trunc_normal_add(P(x), dt, n, b, k0, k1, s0, s1, off, P(st)); Py_END_ALLOW_THREADS
+  return ret(rc);
+}
+
+static PyObject* py_philox_normal(PyObject*, PyObject* a) {
+  unsigned long long x, off, st; int dt; long long n; double mu, sd; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KiLddIIIIKK", &x, &dt, &n, &mu, &sd, &k0, &k1, &s0, &s1, &off, &st)) return nullptr;
+  CHECK(sq_philox_normal)
+  return ret(sq_philox_normal(P(x), dt, n, mu, sd, k0, k1, s0, s1, off, P(st)));
+}
+
+static PyObject* py_philox_uniform(PyObject*, PyObject* a) {
+  unsigned long long x, off, st; long long n; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KLIIIIKK", &x, &n, &k0, &k1, &s0, &s1, &off, &st)) return nullptr;
+  CHECK(sq_philox_uniform)
+  return ret(sq_philox_uniform(P(x), n, k0, k1, s0, s1, off, P(st)));
+}
+
+static PyObject* py_ae_batch(PyObject*, PyObject* a) {
+  unsigned long long pa, pe, po, off, st; long long n; int Q; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKLiIIIIKK", &pa, &pe, &po, &n, &Q, &k0, &k1, &s0, &s1, &off, &st)) return nullptr;
+  CHECK(sq_ae_batch)
+  return ret(sq_ae_batch(P(pa), P(pe), P(po), n, Q, k0, k1, s0, s1, off, P(st)));
+}
+
+static PyObject* py_pe_batch(PyObject*, PyObject* a) {
+  unsigned long long pw, pm, po, off, st; long long n; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKLIIIIKK", &pw, &pm, &po, &n, &k0, &k1, &s0, &s1, &off, &st)) return nullptr;
+  CHECK(sq_pe_batch)
+  return ret(sq_pe_batch(P(pw), P(pm), P(po), n, k0, k1, s0, s1, off, P(st)));
+}
+
+static PyObject* py_estep_bf16(PyObject*, PyObject* a) {
+  unsigned long long X, C, Clo, cn, xn, lab, mind, ovr, ovc, inr, st;
+  long long n, roff; int d, k, kpad, split, cap; double delta; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKLiiidiIIIILiK", &X, &C, &Clo, &cn, &xn, &lab, &mind, &ovr,
+                        &ovc, &inr, &n, &d, &k, &kpad, &delta, &split, &k0, &k1, &s0, &s1, &roff,
+                        &cap, &st))
+    return nullptr;
+  CHECK(sq_estep_bf16)
+  return ret(sq_estep_bf16(P(X), P(C), P(Clo), P(cn), P(xn), P(lab), P(mind), P(ovr), P(ovc),
+                           P(inr), n, d, k, kpad, delta, split, k0, k1, s0, s1, roff, cap, P(st)));
+}
+
+static PyObject* py_band_select(PyObject*, PyObject* a) {
+  unsigned long long D, rows, xn, lab, mind, st; long long m, ld, roff; int k; double delta;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKLiLdIIIILK", &D, &rows, &xn, &lab, &mind, &m, &k, &ld, &delta,
+                        &k0, &k1, &s0, &s1, &roff, &st))
+    return nullptr;
+  CHECK(sq_band_select)
+  return ret(sq_band_select(P(D), P(rows), P(xn), P(lab), P(mind), m, k, ld, delta, k0, k1, s0, s1,
+                            roff, P(st)));
+}
+
+static PyObject* py_band_select_rows(PyObject*, PyObject* a) {
+  unsigned long long X, C, cn, xn, rows, cnt, lab, st; long long cap, roff; int dp, k, kp;
+  double delta; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKLiiidIIIILK", &X, &C, &cn, &xn, &rows, &cnt, &lab, &cap, &dp,
+                        &k, &kp, &delta, &k0, &k1, &s0, &s1, &roff, &st))
+    return nullptr;
+  CHECK(sq_band_select_rows)
+  return ret(sq_band_select_rows(P(X), P(C), P(cn), P(xn), P(rows), P(cnt), P(lab), cap, dp, k, kp,
+                                 delta, k0, k1, s0, s1, roff, P(st)));
+}
+
+static PyObject* py_centroid_accumulate(PyObject*, PyObject* a) {
+  unsigned long long X, lab, w, sums, counts, st; int xdt, d, k, chunk; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKKLiiiK", &X, &xdt, &lab, &w, &sums, &counts, &n, &d, &k, &chunk, &st))
+    return nullptr;
+  CHECK(sq_centroid_accumulate)
+  return ret(sq_centroid_accumulate(P(X), xdt, P(lab), P(w), P(sums), P(counts), n, d, k, chunk, P(st)));
+}
+
+static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
+  unsigned long long pk, co, cnw, cb, clo, cn, sh, st; int k, d, kpad, pol; double nb;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d, &kpad,
+                        &nb, &k0, &k1, &s0, &s1, &pol, &st))
+    return nullptr;
+  CHECK(sq_centroid_finalize)
+  return ret(sq_centroid_finalize(P(pk), P(co), P(cnw), P(cb), P(clo), P(cn), P(sh), k, d, kpad, nb,
+                                  k0, k1, s0, s1, pol, P(st)));
+}
+
+static PyObject* py_pack_stats(PyObject*, PyObject* a) {
+  unsigned long long s, c, i, p, st; int k, d;
+  if (!PyArg_ParseTuple(a, "KKKKiiK", &s, &c, &i, &p, &k, &d, &st)) return nullptr;
+  CHECK(sq_pack_stats)
+  return ret(sq_pack_stats(P(s), P(c), P(i), P(p), k, d, P(st)));
+}
+
+static PyObject* py_ipe_estep(PyObject*, PyObject* a) {
+  unsigned long long G, xn, cn, lab, mind, st; long long m, ld, roff; int k, Q; double eps;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKLiLdiIIIILK", &G, &xn, &cn, &lab, &mind, &m, &k, &ld, &eps, &Q,
+                        &k0, &k1, &s0, &s1, &roff, &st))
+    return nullptr;
+  CHECK(sq_ipe_estep)
+  return ret(sq_ipe_estep(P(G), P(xn), P(cn), P(lab), P(mind), m, k, ld, eps, Q, k0, k1, s0, s1,
+                          roff, P(st)));
+}
+
+static PyObject* py_gram(PyObject*, PyObject* a) {
+  unsigned long long X, G, mean, st; int xdt, d; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKLiK", &X, &xdt, &G, &mean, &n, &d, &st)) return nullptr;
+  CHECK(sq_gram_bf16)
+  return ret(sq_gram_bf16(P(X), xdt, P(G), P(mean), n, d, P(st)));
+}
+
+static PyObject* py_power_iter(PyObject*, PyObject* a) {
+  unsigned long long X, Q, Z, mean, st; int xdt, d, l; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKLiiK", &X, &xdt, &Q, &Z, &mean, &n, &d, &l, &st)) return nullptr;
+  CHECK(sq_power_iter)
+  return ret(sq_power_iter(P(X), xdt, P(Q), P(Z), P(mean), n, d, l, P(st)));
+}
+
+static PyObject* py_mu_sums(PyObject*, PyObject* a) {
+  unsigned long long X, qs, rm, cs, st; int xdt, nq, d; long long n;
+  if (!PyArg_ParseTuple(a, "KiKiKKLiK", &X, &xdt, &qs, &nq, &rm, &cs, &n, &d, &st)) return nullptr;
+  CHECK(sq_mu_sums)
+  return ret(sq_mu_sums(P(X), xdt, P(qs), nq, P(rm), P(cs), n, d, P(st)));
+}
+
+static PyObject* py_row_norms(PyObject*, PyObject* a) {
+  unsigned long long X, out, st; int xdt, d; long long n;
+  if (!PyArg_ParseTuple(a, "KiKLiK", &X, &xdt, &out, &n, &d, &st)) return nullptr;
+  CHECK(sq_row_norms)
+  return ret(sq_row_norms(P(X), xdt, P(out), n, d, P(st)));
+}
+
+static PyObject* py_knn_topk(PyObject*, PyObject* a) {
+  unsigned long long D, od, oi, st; long long m, ld, coff; int nref, kk;
+  if (!PyArg_ParseTuple(a, "KKKLiLiLK", &D, &od, &oi, &m, &nref, &ld, &kk, &coff, &st)) return nullptr;
+  CHECK(sq_knn_topk)
+  return ret(sq_knn_topk(P(D), P(od), P(oi), m, nref, ld, kk, coff, P(st)));
+}
+
+static PyObject* py_device_arch(PyObject*, PyObject*) {
+  hipDeviceProp_t prop;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+    Py_RETURN_NONE;
+  return Py_BuildValue("(siii)", prop.gcnArchName, prop.multiProcessorCount,
+                       (int)prop.maxSharedMemoryPerMultiProcessor, prop.warpSize);
+}
+
+static PyMethodDef methods[] = {
+    {"trunc_normal_add", py_trunc_normal_add, METH_VARARGS, "x += TN(-b,b) (Philox keyed)"},
+    {"philox_normal", py_philox_normal, METH_VARARGS, "fill with mean+std*N(0,1)"},
+    {"philox_uniform", py_philox_uniform, METH_VARARGS, "fill with U(0,1)"},
+    {"ae_batch", py_ae_batch, METH_VARARGS, "batched median-of-Q amplitude estimation"},
+    {"pe_batch", py_pe_batch, METH_VARARGS, "batched phase estimation"},
+    {"estep_bf16", py_estep_bf16, METH_VARARGS, "fused MFMA distance + delta-band E-step"},
+    {"band_select", py_band_select, METH_VARARGS, "delta-band selection over distance rows"},
+    {"band_select_rows", py_band_select_rows, METH_VARARGS, "device-driven overflow fallback"},
+    {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
+    {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},
+    {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},
+    {"ipe_estep", py_ipe_estep, METH_VARARGS, "IPE-noised distance argmin"},
+    {"gram", py_gram, METH_VARARGS, "G += (X-mean)^T (X-mean)"},
+    {"power_iter", py_power_iter, METH_VARARGS, "Z += (X-m)^T ((X-m) Q) fused"},
+    {"mu_sums", py_mu_sums, METH_VARARGS, "mu(A) power sums for a p-grid"},
+    {"row_norms", py_row_norms, METH_VARARGS, "squared row norms"},
+    {"knn_topk", py_knn_topk, METH_VARARGS, "per-row k smallest"},
+    {"device_arch", py_device_arch, METH_NOARGS, "(arch, CUs, LDS/CU, wave size)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+static struct PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_C",
+                                    "sq_learn_amd native HIP kernels (gfx950)", -1, methods};
+
+PyMODINIT_FUNC PyInit__C(void) { return PyModule_Create(&moddef); }

@@ -1,0 +1,271 @@
+"""Device-resident Lloyd / q-means iteration engine.
+
+One :class:`LloydEngine` owns every buffer of a fit on this rank's device
+and runs iterations with at most one small device->host read each
+(``[inertia, shift, overflow]`` for the convergence test).  It implements
+the reference's quantum Lloyd loop (``_dmeans.py:534-671``):
+
+    E-step   labels_estimation (``_dmeans.py:732-777``)
+               delta == 0                 : exact argmin, random tie-break
+               delta > 0, not true_dist   : uniform label in the delta-band
+               delta > 0, true_dist (IPE) : argmin of IPE-noised distances
+    M-step   _centers_update (``_dmeans.py:780-830``): cluster means, then
+               (intermediate_error) tomography with error delta/2
+    loop     best-inertia iterate, Frobenius shift <= tol, final E-step
+
+GPU fast path (d <= 256, gemm_precision 'bf16', no IPE): per iteration
+    estep_bf16 (MFMA distance GEMM + band epilogue + inertia)
+    -> band_select_rows (overflow rows, device-driven)
+    -> centroid_accumulate (segmented reduce) -> pack_stats (one fp64 bucket)
+    -> all_reduce over RCCL (C1: the only collective of the iteration)
+    -> centroid_finalize (mean + fused truncated-normal tomography noise +
+       shift + bf16 centroids and norms for the next E-step).
+Everything else (CPU tensors, IPE distances, fp32 precision, d > 256) runs
+the generic path: library GEMM distance tiles + selection kernels/torch.
+"""
+
+import math
+
+import torch
+
+from ...runtime.rng import RngKey
+from ...ops import kmeans as K
+from ...ops import linalg as L
+from ...ops.random import trunc_normal_add_
+from ...ops import _native as nat
+from ...parallel.comm import Comm
+from ...utils import tracing
+
+
+class LloydEngine:
+    def __init__(self, X, k, *, delta=0.0, true_distance_estimate=False, intermediate_error=False,
+                 true_tomography=False, tomography_kw=None, sample_weight=None, seed=0,
+                 comm=None, row_offset=0, gemm_precision="bf16", ipe_Q=13, empty_policy=0,
+                 Xb=None, xn=None):
+        self.X = X
+        self.device = X.device
+        self.n, self.d = X.shape
+        self.k = int(k)
+        self.delta = float(delta or 0.0)
+        self.ipe = bool(true_distance_estimate) and self.delta > 0
+        self.intermediate_error = bool(intermediate_error)
+        self.true_tomography = bool(true_tomography)
+        self.tomography_kw = dict(tomography_kw or {})
+        self.sample_weight = sample_weight
+        self.seed = seed
+        self.comm = comm if comm is not None else Comm(None)
+        self.row_offset = int(row_offset)
+        self.ipe_Q = int(ipe_Q)
+        self.empty_policy = int(empty_policy)
+        self.k_pad = K.pad_clusters(self.k)
+        self.d_pad = K.pad_features(self.d)
+        self.restart = 0
+        self.it = 0
+        gpu = self.device.type == "cuda"
+        self.fast = (gpu and gemm_precision == "bf16" and not self.ipe and self.d_pad <= 256
+                     and self.k_pad <= 4096)
+        self.acc_dtype = torch.float64 if not gpu else torch.float32
+        if gpu:
+            nat.native()  # fail loudly if the HIP layer is unavailable on a GPU box
+        if self.fast:
+            self._prepare_fast(Xb, xn)
+        else:
+            self._prepare_generic(xn)
+
+    # ------------------------------------------------------------ prep
+    def _prepare_fast(self, Xb, xn):
+        dev = self.device
+        if Xb is None:
+            if self.X.dtype == torch.bfloat16 and self.d == self.d_pad and self.X.is_contiguous():
+                Xb = self.X
+            else:
+                Xb = torch.zeros((self.n, self.d_pad), dtype=torch.bfloat16, device=dev)
+                Xb[:, :self.d] = self.X.to(torch.bfloat16)
+        self.Xb = Xb
+        self.xn = xn if xn is not None else L.row_norms_sq(Xb)
+        # M-step source: the original data when it is fp32 (means keep fp32
+        # precision), the bf16 copy otherwise
+        if self.X.dtype == torch.float32 and self.d % 4 == 0:
+            self.Xm = self.X.contiguous()
+        else:
+            self.Xm = Xb if self.d == self.d_pad else None
+        self.buf = K.EStepBuffers(self.n, dev)
+        self.sums = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
+        self.counts = torch.zeros(self.k, dtype=torch.float64, device=dev)
+        self.packed = torch.zeros(self.k * self.d + self.k + 1, dtype=torch.float64, device=dev)
+        self.shift = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.C = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
+        self.C_new = torch.zeros_like(self.C)
+        self.C_bf16 = torch.zeros((self.k_pad, self.d_pad), dtype=torch.bfloat16, device=dev)
+        self.cn = torch.full((self.k_pad,), K.BIG, dtype=torch.float32, device=dev)
+        self.scalars = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.weights = (self.sample_weight.to(torch.float32).contiguous()
+                        if self.sample_weight is not None else None)
+
+    def _prepare_generic(self, xn):
+        self.Xf = self.X if self.X.dtype in (torch.float32, torch.float64) else self.X.float()
+        self.xn = xn if xn is not None else (self.Xf * self.Xf).sum(1)
+        wd = torch.float64 if self.device.type == "cpu" else torch.float32
+        self.C = torch.zeros((self.k, self.d), dtype=wd, device=self.device)
+        self.labels = torch.empty(self.n, dtype=torch.int64, device=self.device)
+        self.mind = torch.empty(self.n, dtype=self.Xf.dtype, device=self.device)
+
+    # ---------------------------------------------------------- keys
+    def _key(self, purpose, it=None):
+        it = self.it if it is None else it
+        return RngKey(self.seed, purpose, (self.restart << 24) | (it & 0xFFFFFF))
+
+    # ---------------------------------------------------------- state
+    def set_centers(self, C):
+        C = C.to(self.device)
+        if self.fast:
+            self.C.copy_(C.to(torch.float32))
+            Cb, cn = K.centers_to_bf16(self.C, self.k_pad, self.d_pad)
+            self.C_bf16.copy_(Cb)
+            self.cn.copy_(cn)
+        else:
+            self.C = C.to(self.C.dtype).clone()
+
+    def centers(self):
+        return self.C
+
+    # ---------------------------------------------------------- E-step
+    def estep(self, C=None):
+        """Labels and min distances for the current (or given) centres;
+        returns (labels, mind, local_inertia_tensor)."""
+        if C is not None:
+            self.set_centers(C)
+        key = self._key("band_select")
+        if self.fast:
+            with tracing.range("estep_bf16"):
+                lab, mind = K.estep_native(self.Xb, self.C_bf16, self.cn, self.xn, self.k,
+                                           self.delta, key, self.row_offset, self.buf)
+            return lab, mind, self.buf.inertia
+        if self.ipe:
+            return self._estep_ipe(key)
+        return self._estep_generic(key)
+
+    def _chunk_rows(self):
+        wm = 1 << 28  # 256 MiB of distances per chunk
+        return max(1024, wm // (4 * max(self.k, 1)))
+
+    def _estep_generic(self, key):
+        Cw = self.C.to(self.Xf.dtype)
+        cn = (Cw * Cw).sum(1)
+        n = self.n
+        if self.device.type == "cuda":
+            labels32 = torch.empty(n, dtype=torch.int32, device=self.device)
+            mind = torch.empty(n, dtype=torch.float32, device=self.device)
+            step = self._chunk_rows()
+            for s in range(0, n, step):
+                e = min(n, s + step)
+                D = cn[None, :] - 2.0 * (self.Xf[s:e].float() @ Cw.float().T)
+                K.band_select_native(D, self.xn[s:e].float().contiguous(), self.delta, key,
+                                     self.row_offset + s, labels32[s:e], mind[s:e], k=self.k)
+            inertia = mind.double().sum().reshape(1)
+            return labels32, mind, inertia
+        lab, mind = K.estep_torch(self.Xf, Cw, self.delta, key, self.row_offset, self.k_pad,
+                                  chunk_rows=self._chunk_rows(), xn=self.xn)
+        return lab, mind, mind.double().sum().reshape(1)
+
+    def _estep_ipe(self, key):
+        eps = self.delta / 2.0
+        ipe_key = self._key("ipe")
+        if self.device.type == "cuda":
+            n = self.n
+            labels32 = torch.empty(n, dtype=torch.int32, device=self.device)
+            mind = torch.empty(n, dtype=torch.float32, device=self.device)
+            C32 = self.C.float()
+            cn = (C32 * C32).sum(1).contiguous()
+            step = max(256, min(self._chunk_rows(), 1 << 16))
+            for s in range(0, n, step):
+                e = min(n, s + step)
+                G = self.Xf[s:e].float() @ C32.T
+                K.ipe_estep_native(G, self.xn[s:e].float().contiguous(), cn, eps, self.ipe_Q,
+                                   ipe_key, self.row_offset + s, labels32[s:e], mind[s:e])
+            return labels32, mind, mind.double().sum().reshape(1)
+        lab, mind = K.ipe_estep_torch(self.Xf, self.C, eps, ipe_key, self.row_offset, self.k_pad,
+                                      Q=self.ipe_Q)
+        return lab, mind, mind.double().sum().reshape(1)
+
+    # ---------------------------------------------------------- M-step
+    def _noise_bound(self):
+        if not self.intermediate_error or self.delta <= 0 or self.true_tomography:
+            return 0.0
+        # make_gaussian_est on the flattened k x d centre matrix (Utility.py:97)
+        return (self.delta / 2.0) / math.sqrt(self.k * self.d)
+
+    def mstep(self, labels, inertia):
+        """Centroid update from labels; returns the device scalar tensor
+        [inertia, shift, overflow_count] (one D2H read by the caller)."""
+        noise_key = self._key("trunc_normal")
+        if self.fast:
+            with tracing.range("mstep"):
+                self.sums.zero_()
+                self.counts.zero_()
+                if self.Xm is not None:
+                    K.centroid_accumulate_native(self.Xm, labels, self.weights, self.sums,
+                                                 self.counts, self.k)
+                else:
+                    s, c = K.centroid_sums_torch(self.Xb[:, :self.d], labels, self.k,
+                                                 self.weights, acc_dtype=torch.float32)
+                    self.sums.copy_(s)
+                    self.counts.copy_(c)
+                K.pack_stats_native(self.sums, self.counts, inertia, self.packed, self.k, self.d)
+            with tracing.range("allreduce"):
+                self.comm.all_reduce_(self.packed)
+            with tracing.range("finalize"):
+                self.shift.zero_()
+                K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
+                                           self.shift, self.k, self.d, self._noise_bound(),
+                                           noise_key, self.empty_policy)
+                self.C, self.C_new = self.C_new, self.C
+                if self.intermediate_error and self.true_tomography and self.delta > 0:
+                    self._true_tomography_centers()
+            self.scalars[0:1].copy_(self.packed[-1:])
+            self.scalars[1:2].copy_(self.shift)
+            self.scalars[2:3].copy_(self.buf.ovf_count.to(torch.float64))
+            return self.scalars
+        # generic / CPU
+        w = self.sample_weight
+        sums, counts = K.centroid_sums_torch(self.Xf, labels, self.k, w,
+                                             acc_dtype=torch.float64 if self.device.type == "cpu"
+                                             else torch.float32)
+        packed = torch.cat([sums.reshape(-1).double(), counts.double(),
+                            inertia.double().reshape(1)])
+        self.comm.all_reduce_(packed)
+        kd = self.k * self.d
+        sums = packed[:kd].reshape(self.k, self.d)
+        counts = packed[kd:kd + self.k]
+        tot_inertia = packed[-1]
+        old = self.C
+        new = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1e-300)[:, None],
+                          old.double() if self.empty_policy == 0 else torch.zeros_like(sums))
+        new = new.to(old.dtype).contiguous()
+        b = self._noise_bound()
+        if b > 0:
+            flat = new.view(-1)
+            trunc_normal_add_(flat, b, noise_key, offset=0)
+        self.C = new
+        if self.intermediate_error and self.true_tomography and self.delta > 0:
+            self._true_tomography_centers()
+        shift = ((self.C.double() - old.double()) ** 2).sum()
+        return torch.stack([tot_inertia, shift, torch.zeros((), dtype=torch.float64,
+                                                            device=self.device)])
+
+    def _true_tomography_centers(self):
+        """Real (shot-based) tomography of the k centre rows with error delta/2,
+        replicated on every rank (seeded on the host)."""
+        from ...quantum.device import tomography_rows_torch
+        key = self._key("tomography")
+        C = self.C.double().cpu()
+        est = tomography_rows_torch(C, self.delta / 2.0, key, **self.tomography_kw)
+        self.set_centers(est.to(self.C.dtype))
+
+    # ---------------------------------------------------------- iteration
+    def step(self):
+        """One Lloyd iteration; returns (labels, scalars_tensor)."""
+        labels, mind, inertia = self.estep()
+        sc = self.mstep(labels, inertia)
+        self.it += 1
+        return labels, sc

@@ -1,0 +1,79 @@
+"""Loader for the in-tree native extension ``sq_learn_amd._C``.
+
+Policy (task contract): on a GPU tensor every op runs its HIP kernel; if the
+extension is missing or stale it is (re)built in-tree on first use, and if
+that fails the op raises - it never silently falls back to a torch
+implementation on the device.  CPU tensors use the torch reference path of
+each op (tests, the CPU oracle, gloo multi-process tests).
+"""
+
+import importlib
+import os
+import threading
+
+import torch
+
+_lock = threading.Lock()
+_mod = None
+_err = None
+
+DT_F32, DT_F64, DT_BF16 = 0, 1, 2
+
+
+def _load():
+    global _mod, _err
+    with _lock:
+        if _mod is not None:
+            return _mod
+        from .. import _build
+        try:
+            if os.environ.get("SQ_NO_AUTOBUILD", "0") != "1" and _build.needs_build():
+                _build.build()
+            _mod = importlib.import_module("sq_learn_amd._C")
+        except Exception as e:  # pragma: no cover - exercised on broken installs
+            _err = e
+            raise
+        return _mod
+
+
+def native():
+    """The extension module (builds it if needed); raises if unavailable."""
+    if _mod is not None:
+        return _mod
+    return _load()
+
+
+def available():
+    try:
+        native()
+        return True
+    except Exception:
+        return False
+
+
+def use_native(*tensors):
+    """True when the op must take the HIP path (any tensor on a GPU)."""
+    return any(isinstance(t, torch.Tensor) and t.is_cuda for t in tensors)
+
+
+def stream_handle(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return DT_F32
+    if t.dtype == torch.float64:
+        return DT_F64
+    if t.dtype == torch.bfloat16:
+        return DT_BF16
+    raise TypeError(f"unsupported dtype {t.dtype} for native op")
+
+
+def loaded_path():
+    m = native()
+    return getattr(m, "__file__", None)

@@ -1,0 +1,237 @@
+"""q-means / k-means ops: fused E-step, delta-band selection, segmented
+centroid reduction, centroid finalisation and the IPE distance path.
+
+GPU tensors run the HIP kernels of ``csrc/kmeans.hip``; CPU tensors run the
+torch twins below, which implement the same semantics and draw the same
+Philox keys (reference ``_dmeans.py:732-830``).
+"""
+
+import math
+
+import torch
+
+from ..runtime.rng import RngKey, philox4x32, MASK32
+from . import _native as nat
+from .random import amplitude_estimation_batch
+
+FAST_D = (16, 32, 64, 128, 256)
+BIG = 3.0e38
+
+
+def pad_features(d):
+    """Padded feature count used by the MFMA kernels (zero columns)."""
+    for f in FAST_D:
+        if d <= f:
+            return f
+    return ((d + 15) // 16) * 16
+
+
+def pad_clusters(k):
+    return ((k + 63) // 64) * 64
+
+
+def idx_bits(k_pad):
+    b = 1
+    while (1 << b) < k_pad:
+        b += 1
+    return b
+
+
+def band_keys(key: RngKey, grows, cols, k_pad):
+    """Selection key of (global row, centroid): philox word of block
+    (row << 16 | j), low idx_bits replaced by j (same as band_key() in HIP)."""
+    ib = idx_bits(k_pad)
+    keep = MASK32 & ~((1 << ib) - 1)
+    idx = (grows.to(torch.int64) << 16) | cols.to(torch.int64)
+    w = philox4x32(idx & MASK32, (idx >> 32) & MASK32, key.s0, key.s1, key.k0, key.k1)[0]
+    return (w & keep) | cols.to(torch.int64)
+
+
+def band_select_torch(D, grows, delta, key: RngKey, k_pad, tie_only=False):
+    """Exact delta-band selection over distance rows D [m, k] (torch).
+
+    label = uniform member of {j : D_j <= min + delta} (first argmin when the
+    band has one member).  Reference: ``_dmeans.py:742-751, 771-772``
+    (``select_labels`` -> random.choice among the qualifying indices)."""
+    mn, am = torch.min(D, dim=1)
+    thr = mn + (0.0 if tie_only else float(delta))
+    cand = D <= thr[:, None]
+    cnt = cand.sum(1)
+    labels = am.clone()
+    multi = torch.nonzero(cnt > 1).reshape(-1)
+    if multi.numel():
+        sub = cand[multi]
+        rr, cc = torch.nonzero(sub, as_tuple=True)
+        keys = band_keys(key, grows[multi][rr], cc, k_pad)
+        best = torch.full((multi.numel(),), 1 << 40, dtype=torch.int64, device=D.device)
+        best = best.scatter_reduce(0, rr, keys, reduce="amin")
+        ib = idx_bits(k_pad)
+        labels[multi] = best & ((1 << ib) - 1)
+    return labels, mn
+
+
+def distances_torch(X, C, xn=None, cn=None):
+    """Squared euclidean distances ||x||^2 + ||c||^2 - 2 x.c, clamped >= 0."""
+    if xn is None:
+        xn = (X * X).sum(1)
+    if cn is None:
+        cn = (C * C).sum(1)
+    D = xn[:, None] + cn[None, :] - 2.0 * (X @ C.T)
+    return D.clamp_(min=0.0)
+
+
+def estep_torch(X, C, delta, key, row_offset, k_pad, chunk_rows=65536, xn=None):
+    """CPU E-step (labels, min distances) over row chunks."""
+    n = X.shape[0]
+    labels = torch.empty(n, dtype=torch.int64, device=X.device)
+    mind = torch.empty(n, dtype=X.dtype, device=X.device)
+    cn = (C * C).sum(1)
+    for s in range(0, n, chunk_rows):
+        e = min(n, s + chunk_rows)
+        xb = X[s:e]
+        xnb = (xb * xb).sum(1) if xn is None else xn[s:e]
+        D = distances_torch(xb, C, xnb, cn)
+        g = torch.arange(s, e, dtype=torch.int64, device=X.device) + row_offset
+        lab, mn = band_select_torch(D, g, delta, key, k_pad)
+        labels[s:e] = lab
+        mind[s:e] = mn
+    return labels, mind
+
+
+def ipe_estep_torch(X, C, eps, key, row_offset, k_pad, Q=13, chunk_rows=256):
+    """CPU IPE E-step: D~ = |x|^2 + |c|^2 - 2 IPE(x, c) (``_dmeans.py:753-772``)."""
+    n, k = X.shape[0], C.shape[0]
+    labels = torch.empty(n, dtype=torch.int64)
+    mind = torch.empty(n, dtype=torch.float64)
+    cn = (C.double() ** 2).sum(1)
+    for s in range(0, n, chunk_rows):
+        e = min(n, s + chunk_rows)
+        xb = X[s:e].double()
+        xn = (xb * xb).sum(1)
+        G = xb @ C.double().T
+        S = xn[:, None] + cn[None, :]
+        a = (S - 2 * G) / (2 * S)
+        a = torch.where(a.abs() <= 1e-15, torch.zeros_like(a), a)
+        eps_a = eps * torch.clamp(G.abs(), min=1.0) / S
+        at = amplitude_estimation_batch(a.clamp(0, 1), eps_a, key, Q=Q,
+                                        offset=(row_offset + s) * k)
+        sv = S * (1 - 2 * at) / 2
+        Dt = xn[:, None] + cn[None, :] - 2 * sv
+        g = torch.arange(s, e, dtype=torch.int64) + row_offset
+        lab, mn = band_select_torch(Dt, g, 0.0, key, k_pad, tie_only=True)
+        labels[s:e] = lab
+        mind[s:e] = mn
+    return labels, mind
+
+
+# ----------------------------------------------------------------- native
+class EStepBuffers:
+    """Device workspace of the fused E-step (allocated once per fit)."""
+
+    def __init__(self, n, device, ovf_cap=None):
+        self.labels = torch.empty(n, dtype=torch.int32, device=device)
+        self.mind = torch.empty(n, dtype=torch.float32, device=device)
+        self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(4096, n // 16))
+        self.ovf_rows = torch.empty(self.ovf_cap, dtype=torch.int64, device=device)
+        # scalars: [ovf_count(int32)] and inertia (fp64) / shift (fp64)
+        self.ovf_count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.inertia = torch.zeros(1, dtype=torch.float64, device=device)
+
+
+def estep_native(Xb, C_bf16, cn, xn, k, delta, key: RngKey, row_offset, buf: EStepBuffers,
+                 stream=None):
+    """Fused MFMA E-step + device-driven overflow fallback (no host sync)."""
+    n, d_pad = Xb.shape
+    k_pad = C_bf16.shape[0]
+    assert Xb.dtype == torch.bfloat16 and C_bf16.dtype == torch.bfloat16
+    assert C_bf16.shape[1] == d_pad and d_pad in FAST_D and k_pad % 64 == 0
+    assert Xb.is_contiguous() and C_bf16.is_contiguous() and cn.is_contiguous()
+    st = stream if stream is not None else nat.stream_handle(Xb.device)
+    m = nat.native()
+    buf.ovf_count.zero_()
+    buf.inertia.zero_()
+    m.estep_bf16(Xb.data_ptr(), C_bf16.data_ptr(), 0, cn.data_ptr(), xn.data_ptr(),
+                 buf.labels.data_ptr(), buf.mind.data_ptr(), buf.ovf_rows.data_ptr(),
+                 buf.ovf_count.data_ptr(), buf.inertia.data_ptr(), n, d_pad, k, k_pad,
+                 float(delta), 0, key.k0, key.k1, key.s0, key.s1, int(row_offset), buf.ovf_cap, st)
+    m.band_select_rows(Xb.data_ptr(), C_bf16.data_ptr(), cn.data_ptr(), xn.data_ptr(),
+                       buf.ovf_rows.data_ptr(), buf.ovf_count.data_ptr(), buf.labels.data_ptr(),
+                       buf.ovf_cap, d_pad, k, k_pad, float(delta), key.k0, key.k1, key.s0, key.s1,
+                       int(row_offset), st)
+    return buf.labels, buf.mind
+
+
+def band_select_native(D, xn, delta, key: RngKey, row_offset, labels, mind, k=None, rows=None):
+    """Exact selection over fp32 distance rows on the GPU (generic path)."""
+    D = D.contiguous()
+    m_, kk = D.shape
+    k = kk if k is None else k
+    nat.native().band_select(D.data_ptr(), 0 if rows is None else rows.data_ptr(),
+                             0 if xn is None else xn.data_ptr(), labels.data_ptr(), mind.data_ptr(),
+                             m_, k, D.stride(0), float(delta), key.k0, key.k1, key.s0, key.s1,
+                             int(row_offset), nat.stream_handle(D.device))
+
+
+def ipe_estep_native(G, xn, cn, eps, Q, key: RngKey, row_offset, labels, mind):
+    G = G.contiguous()
+    m_, k = G.shape
+    nat.native().ipe_estep(G.data_ptr(), xn.data_ptr(), cn.data_ptr(), labels.data_ptr(),
+                           mind.data_ptr(), m_, k, G.stride(0), float(eps), int(Q), key.k0, key.k1,
+                           key.s0, key.s1, int(row_offset), nat.stream_handle(G.device))
+
+
+def centroid_accumulate_native(X, labels, weights, sums, counts, k, chunk=None):
+    n, d = X.shape
+    if chunk is None:
+        chunk = max(256, min(8192, (160 * 1024 // 4) - 2 * k - 64))
+        chunk = min(chunk, 8192)
+    assert labels.dtype == torch.int32 and sums.dtype == torch.float32 and counts.dtype == torch.float64
+    nat.native().centroid_accumulate(X.data_ptr(), nat.dtype_code(X), labels.data_ptr(),
+                                     0 if weights is None else weights.data_ptr(), sums.data_ptr(),
+                                     counts.data_ptr(), n, d, k, int(chunk),
+                                     nat.stream_handle(X.device))
+
+
+def pack_stats_native(sums, counts, inertia, packed, k, d):
+    nat.native().pack_stats(sums.data_ptr(), counts.data_ptr(),
+                            0 if inertia is None else inertia.data_ptr(), packed.data_ptr(), k, d,
+                            nat.stream_handle(sums.device))
+
+
+def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
+                             empty_policy=0):
+    k_pad = C_bf16.shape[0]
+    nat.native().centroid_finalize(packed.data_ptr(), C_old.data_ptr(), C_new.data_ptr(),
+                                   C_bf16.data_ptr(), 0, cn.data_ptr(), shift.data_ptr(), k, d,
+                                   k_pad, float(noise_b), key.k0, key.k1, key.s0, key.s1,
+                                   int(empty_policy), nat.stream_handle(packed.device))
+
+
+def centers_to_bf16(C, k_pad, d_pad):
+    """Padded bf16 copy of the centroids and fp32 ||c_bf16||^2 (BIG on pads)."""
+    k, d = C.shape
+    Cb = torch.zeros((k_pad, d_pad), dtype=torch.bfloat16, device=C.device)
+    Cb[:k, :d] = C.to(torch.bfloat16)
+    cn = torch.full((k_pad,), BIG, dtype=torch.float32, device=C.device)
+    cn[:k] = (Cb[:k].float() ** 2).sum(1)
+    return Cb, cn
+
+
+def centroid_sums_torch(X, labels, k, weights=None, acc_dtype=torch.float64):
+    """Label-segmented sums (torch index_add) -> (sums [k,d], counts [k])."""
+    d = X.shape[1]
+    sums = torch.zeros((k, d), dtype=acc_dtype, device=X.device)
+    counts = torch.zeros(k, dtype=torch.float64, device=X.device)
+    lab = labels.to(torch.int64)
+    ok = lab >= 0
+    if not bool(ok.all()):
+        lab = lab[ok]
+        X = X[ok]
+        weights = weights[ok] if weights is not None else None
+    if weights is None:
+        sums.index_add_(0, lab, X.to(acc_dtype))
+        counts.index_add_(0, lab, torch.ones_like(lab, dtype=torch.float64))
+    else:
+        sums.index_add_(0, lab, X.to(acc_dtype) * weights.to(acc_dtype)[:, None])
+        counts.index_add_(0, lab, weights.to(torch.float64))
+    return sums, counts
