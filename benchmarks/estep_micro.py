@@ -1,0 +1,49 @@
+"""Isolated E-step / M-step kernel timing (for rocprofv3 PMC runs)."""
+import argparse
+import time
+
+import torch
+
+from sq_learn_amd.ops import kmeans as K
+from sq_learn_amd.ops import linalg as L
+from sq_learn_amd.runtime.rng import RngKey
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=10_000_000)
+ap.add_argument("--d", type=int, default=256)
+ap.add_argument("--k", type=int, default=1024)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--delta", type=float, default=0.5)
+ap.add_argument("--what", default="estep", choices=["estep", "reduce", "both"])
+a = ap.parse_args()
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(0)
+C = torch.randn(a.k, a.d, device=dev, generator=g) * 3
+X = torch.empty(a.n, a.d, dtype=torch.bfloat16, device=dev)
+step = 1 << 20
+for s in range(0, a.n, step):
+    e = min(a.n, s + step)
+    lab = torch.randint(0, a.k, (e - s,), device=dev, generator=g)
+    X[s:e] = (C[lab] + torch.randn(e - s, a.d, device=dev, generator=g)).to(torch.bfloat16)
+kp, dp = K.pad_clusters(a.k), K.pad_features(a.d)
+Cb, cn = K.centers_to_bf16(C, kp, dp)
+xn = L.row_norms_sq(X)
+buf = K.EStepBuffers(a.n, dev)
+ws = K.ReduceWorkspace(a.n, a.k, dev)
+sums = torch.zeros(a.k, a.d, device=dev)
+cnt = torch.zeros(a.k, dtype=torch.float64, device=dev)
+key = RngKey(1, "band_select", 0)
+K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
+torch.cuda.synchronize()
+for name in (["estep", "reduce"] if a.what == "both" else [a.what]):
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        if name == "estep":
+            K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
+        else:
+            sums.zero_(); cnt.zero_()
+            K.centroid_reduce_native(X, buf.labels, None, sums, cnt, a.k, ws)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / a.iters * 1e3
+    fl = 2.0 * a.n * a.k * dp
+    print(f"{name}: {ms:.3f} ms  ({fl / ms / 1e9:.1f} TFLOP/s equiv)  ovf={int(buf.ovf_count.item())}")

@@ -40,6 +40,18 @@ SQ_DEV float packf(float v, uint32_t keepmask, uint32_t j) {
 }
 SQ_DEV float valf(float p, uint32_t keepmask) { return __uint_as_float(__float_as_uint(p) & keepmask); }
 
+// single-instruction min / med3: no canonicalising v_max on bit-packed inputs
+SQ_DEV float min_raw(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+SQ_DEV float med3_raw(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 SQ_DEV uint32_t band_key(const RngKey& key, long long grow, uint32_t j) {
   unsigned long long idx = ((unsigned long long)grow << 16) | (unsigned long long)j;
   return key.block(idx).x;
@@ -109,35 +121,91 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int t = 0; t < n_tiles; ++t) {
-    unsigned char* cur = (t & 1) ? buf1 : buf0;
-    unsigned char* nxt = (t & 1) ? buf0 : buf1;
-    if (t + 1 < n_tiles) stage(t + 1, nxt);
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      f32x16 acc = {0};
-      const int brow = nb * 32 + r32;
-      const unsigned char* rowp = cur + brow * (DP * 2);
+  // Cross-tile software pipeline: while the MFMAs of tile t+1 run, the VALU
+  // epilogue (distance, index packing, top-2) of tile t executes in the
+  // MFMA shadow.  Two accumulator sets (pA, pB) alternate with static names.
+  auto ldb = [&](const unsigned char* rp, int brow, int ks) -> bf16x8 {
+    int pc = (ks * 2 + half) ^ (brow & SWZ);
+    return *reinterpret_cast<const bf16x8*>(rp + pc * 16);
+  };
+  // MFMA chain of one tile (both 32-col blocks, B ring prefetched 2 ahead)
+  // interleaved with the epilogue of the previous tile (if any).
+  auto tile_step = [&](const unsigned char* cur, f32x16& n0, f32x16& n1, bool do_mfma,
+                       const f32x16& o0, const f32x16& o1acc, int t_prev, bool do_epi) {
+    const unsigned char* rowp0 = cur + r32 * (DP * 2);
+    const unsigned char* rowp1 = cur + (32 + r32) * (DP * 2);
+    const uint32_t j0 = (uint32_t)(t_prev * kBN + r32);
+    const uint32_t j1 = j0 + 32;
+    const float c0 = cn_lds[do_epi ? j0 : 0], c1 = cn_lds[do_epi ? j1 : 0];
+    if (do_mfma) {
+      f32x16 acc0 = {0}, acc1 = {0};
+      bf16x8 b0[3], b1[3];
+      b0[0] = ldb(rowp0, r32, 0);
+      b1[0] = ldb(rowp1, 32 + r32, 0);
+      if (KS > 1) { b0[1] = ldb(rowp0, r32, 1); b1[1] = ldb(rowp1, 32 + r32, 1); }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        int c = ks * 2 + half;
-        int pc = c ^ (brow & SWZ);
-        bf16x8 b = *reinterpret_cast<const bf16x8*>(rowp + pc * 16);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b, acc, 0, 0, 0);
+        if (ks + 2 < KS) {
+          b0[(ks + 2) % 3] = ldb(rowp0, r32, ks + 2);
+          b1[(ks + 2) % 3] = ldb(rowp1, 32 + r32, ks + 2);
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b0[ks % 3], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b1[ks % 3], acc1, 0, 0, 0);
       }
-      const uint32_t j = (uint32_t)(t * kBN + nb * 32 + r32);
-      const float cj = cn_lds[j];
+      n0 = acc0;
+      n1 = acc1;
+    }
+    if (do_epi) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float dv = __builtin_fmaf(-2.0f, acc[i], cj);
-        float pv = packf(dv, keep, j);
-        float o1 = m1[i];
-        m2[i] = __builtin_amdgcn_fmed3f(o1, pv, m2[i]);
-        m1[i] = fminf(o1, pv);
+        float p0 = packf(__builtin_fmaf(-2.0f, o0[i], c0), keep, j0);
+        float p1 = packf(__builtin_fmaf(-2.0f, o1acc[i], c1), keep, j1);
+        float q1 = m1[i];
+        float q2 = m2[i];
+        q2 = med3_raw(q1, p0, q2);
+        q1 = min_raw(q1, p0);
+        q2 = med3_raw(q1, p1, q2);
+        q1 = min_raw(q1, p1);
+        m1[i] = q1;
+        m2[i] = q2;
       }
     }
+    if (do_mfma && do_epi) {
+      // [2 cn reads + 4 B reads] then per k-step [2 B reads][2 MFMA][8 VALU]
+      __builtin_amdgcn_sched_group_barrier(0x100, KS > 1 ? 6 : 4, 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 2 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 128 / KS, 0);
+      }
+    }
+  };
+  auto sync_tile = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+
+  f32x16 pA0, pA1, pB0, pB1;
+  // prologue: tile 0 -> pA
+  if (n_tiles > 1) stage(1, buf1);
+  tile_step(buf0, pA0, pA1, true, pA0, pA1, 0, false);
+  sync_tile();
+  // steady state: every combined step is ONE basic block (unconditional MFMA
+  // + epilogue) so the scheduler can interleave them; static pA/pB names by
+  // unrolling two steps; the last epilogue runs alone.
+  int t = 0;
+  while (true) {
+    if (t + 1 >= n_tiles) { tile_step(buf0, pB0, pB1, false, pA0, pA1, t, true); break; }
+    if (t + 2 < n_tiles) stage(t + 2, (t & 1) ? buf1 : buf0);
+    tile_step((t & 1) ? buf0 : buf1, pB0, pB1, true, pA0, pA1, t, true);
+    sync_tile();
+    ++t;
+    if (t + 1 >= n_tiles) { tile_step(buf0, pA0, pA1, false, pB0, pB1, t, true); break; }
+    if (t + 2 < n_tiles) stage(t + 2, (t & 1) ? buf1 : buf0);
+    tile_step((t & 1) ? buf0 : buf1, pA0, pA1, true, pB0, pB1, t, true);
+    sync_tile();
+    ++t;
   }
 
   // ---- merge the 32 lanes of each half (same rows), resolve the band
@@ -383,6 +451,144 @@ __global__ void __launch_bounds__(256) centroid_accumulate_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// centroid reduction by global counting sort (replaces per-chunk LDS sorting):
+//   label_hist   : LDS histogram per chunk -> one global int atomic per label
+//   label_scan   : exclusive scan (one workgroup)
+//   label_scatter: per-chunk LDS ranks + one global cursor atomic per label
+//   segment_sum  : each workgroup owns a contiguous range of the label-sorted
+//                  permutation; each wave sums its rows (4 row loads in flight)
+//                  and flushes one 256-B f32 atomic row-add per label run.
+constexpr int kHistChunk = 8192;
+
+__global__ void __launch_bounds__(256) label_hist_kernel(const int* __restrict__ labels, long long n,
+                                                         int k, int* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) int lh[];
+  for (int j = threadIdx.x; j < k; j += 256) lh[j] = 0;
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * kHistChunk;
+  const long long r1 = min(n, r0 + kHistChunk);
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    int l = labels[r];
+    if (l >= 0 && l < k) atomicAdd(&lh[l], 1);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256)
+    if (lh[j]) atomicAdd(&hist[j], lh[j]);
+}
+
+__global__ void __launch_bounds__(1024) label_scan_kernel(const int* __restrict__ hist, int k,
+                                                          int* __restrict__ cursor) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (k + 1023) / 1024;
+  const int b = t * per, e = min(b + per, k);
+  int s = 0;
+  for (int j = b; j < e; ++j) s += hist[j];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (int j = b; j < e; ++j) { cursor[j] = run; run += hist[j]; }
+}
+
+__global__ void __launch_bounds__(256) label_scatter_kernel(const int* __restrict__ labels,
+                                                            long long n, int k,
+                                                            int* __restrict__ cursor,
+                                                            int* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) int sm2[];
+  int* lh = sm2;        // k: local counts, then local cursors
+  int* base = sm2 + k;  // k
+  for (int j = threadIdx.x; j < k; j += 256) lh[j] = 0;
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * kHistChunk;
+  const long long r1 = min(n, r0 + kHistChunk);
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    int l = labels[r];
+    if (l >= 0 && l < k) atomicAdd(&lh[l], 1);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256) {
+    int c = lh[j];
+    base[j] = c ? atomicAdd(&cursor[j], c) : 0;
+    lh[j] = 0;
+  }
+  __syncthreads();
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    int l = labels[r];
+    if (l >= 0 && l < k) {
+      int pos = base[l] + atomicAdd(&lh[l], 1);
+      perm[pos] = (int)r;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(512) segment_sum_kernel(
+    const T* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
+    const float* __restrict__ w, long long n_sorted, int d, int range,
+    float* __restrict__ sums, double* __restrict__ counts, const int* __restrict__ valid_end) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long p0 = (long long)blockIdx.x * range;
+  const long long p1 = min(min(n_sorted, (long long)*valid_end), p0 + range);
+  constexpr int U = 4;
+  for (int c0 = lane * 4; c0 < d; c0 += 256) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    double cnt = 0.0;
+    int cur = -1;
+    for (long long p = p0 + wave; p < p1; p += 8 * U) {
+      int rr[U], ll[U];
+      float4 v[U];
+      float ww[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        long long q = p + 8LL * u;
+        rr[u] = q < p1 ? perm[q] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ll[u] = rr[u] >= 0 ? labels[rr[u]] : -1;
+        v[u] = rr[u] >= 0 ? load4<T>(X + (size_t)rr[u] * d + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        ww[u] = (w && rr[u] >= 0) ? w[rr[u]] : 1.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ll[u] < 0) continue;
+        if (ll[u] != cur) {
+          if (cur >= 0) {
+            float* dst = sums + (size_t)cur * d + c0;
+            atomicAdd(dst + 0, acc.x);
+            if (c0 + 1 < d) atomicAdd(dst + 1, acc.y);
+            if (c0 + 2 < d) atomicAdd(dst + 2, acc.z);
+            if (c0 + 3 < d) atomicAdd(dst + 3, acc.w);
+            if (lane == 0 && c0 == 0) atomicAdd(&counts[cur], cnt);
+          }
+          cur = ll[u];
+          acc = make_float4(0.f, 0.f, 0.f, 0.f);
+          cnt = 0.0;
+        }
+        acc.x += ww[u] * v[u].x; acc.y += ww[u] * v[u].y;
+        acc.z += ww[u] * v[u].z; acc.w += ww[u] * v[u].w;
+        cnt += (double)ww[u];
+      }
+    }
+    if (cur >= 0) {
+      float* dst = sums + (size_t)cur * d + c0;
+      atomicAdd(dst + 0, acc.x);
+      if (c0 + 1 < d) atomicAdd(dst + 1, acc.y);
+      if (c0 + 2 < d) atomicAdd(dst + 2, acc.z);
+      if (c0 + 3 < d) atomicAdd(dst + 3, acc.w);
+      if (lane == 0 && c0 == 0) atomicAdd(&counts[cur], cnt);
+    }
+  }
+}
+
 // packed[0:k*d] = sums (f64), packed[k*d : k*d+k] = counts, packed[k*d+k] = inertia
 __global__ void __launch_bounds__(256) pack_stats_kernel(
     const float* __restrict__ sums, const double* __restrict__ counts,
@@ -618,6 +824,39 @@ int sq_centroid_accumulate(const void* X, int xdtype, const void* labels, const 
   } else {
     return (int)hipErrorInvalidValue;
   }
+  return (int)hipGetLastError();
+}
+
+int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void* weights,
+                       void* sums, void* counts, long long n, int d, int k, void* ws_hist,
+                       void* ws_cursor, void* ws_perm, void* stream) {
+  if (n <= 0) return 0;
+  if (d % 4 != 0 || k > 16384 || n > 2147483647LL) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
+  (void)hipMemsetAsync(ws_hist, 0, (size_t)k * 4, st);
+  hipLaunchKernelGGL(label_hist_kernel, dim3(chunks), dim3(256), (size_t)k * 4, st,
+                     (const int*)labels, n, k, (int*)ws_hist);
+  hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (const int*)ws_hist, k,
+                     (int*)ws_cursor);
+  hipLaunchKernelGGL(label_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
+                     (const int*)labels, n, k, (int*)ws_cursor, (int*)ws_perm);
+  // rows with label < 0 are not in the permutation: sum over the first n_valid
+  // positions; n_valid <= n and unused tail positions hold stale data, so the
+  // kernel bounds itself with the scanned total (cursor[k-1] after scatter)
+  const int range = 2048;
+  unsigned grid = (unsigned)((n + range - 1) / range);
+  if (xdtype == 0)
+    hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(grid), dim3(512), 0, st, (const float*)X,
+                       (const int*)ws_perm, (const int*)labels, (const float*)weights, n, d, range,
+                       (float*)sums, (double*)counts, (const int*)ws_cursor + (k - 1));
+  else if (xdtype == 2)
+    hipLaunchKernelGGL(segment_sum_kernel<uint16_t>, dim3(grid), dim3(512), 0, st,
+                       (const uint16_t*)X, (const int*)ws_perm, (const int*)labels,
+                       (const float*)weights, n, d, range, (float*)sums, (double*)counts,
+                       (const int*)ws_cursor + (k - 1));
+  else
+    return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

@@ -248,13 +248,34 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
 template <typename T>
 __global__ void __launch_bounds__(256) row_norms_kernel(const T* __restrict__ X, float* __restrict__ out,
                                                         long long n, int d) {
+  // 16-byte vector loads; 4 rows per wave when d <= 128 elements-per-16B*16
   const int lane = threadIdx.x & 63;
   const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
+  constexpr int V = 16 / sizeof(T);
+  const T* row = X + (size_t)r * d;
   float s = 0.f;
-  for (int c = lane; c < d; c += 64) {
-    float v = ld1<T>(X, (size_t)r * d + c);
-    s += v * v;
+  const bool aligned = ((d * sizeof(T)) % 16 == 0);
+  if (aligned) {
+    for (int c = lane * V; c < d; c += 64 * V) {
+      uint4 u = *reinterpret_cast<const uint4*>(row + c);
+      uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xFFFF0000u);
+          s += lo * lo + hi * hi;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { float v = __uint_as_float(w[i]); s += v * v; }
+      }
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) {
+      float v = ld1<T>(X, (size_t)r * d + c);
+      s += v * v;
+    }
   }
   s = wave_sum(s);
   if (lane == 0) out[r] = s;

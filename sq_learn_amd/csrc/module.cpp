@@ -35,6 +35,8 @@ __attribute__((weak)) int sq_band_select_rows(const void*, const void*, const vo
 __attribute__((weak)) int sq_centroid_accumulate(const void* X, int xdtype, const void* labels, const void* weights,
                            void* sums, void* counts, long long n, int d, int k, int chunk,
                            void* stream);
+__attribute__((weak)) int sq_centroid_reduce(const void*, int, const void*, const void*, void*, void*,
+                       long long, int, int, void*, void*, void*, void*);
 __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
                          unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
@@ -147,6 +149,16 @@ static PyObject* py_centroid_accumulate(PyObject*, PyObject* a) {
   return ret(sq_centroid_accumulate(P(X), xdt, P(lab), P(w), P(sums), P(counts), n, d, k, chunk, P(st)));
 }
 
+static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
+  unsigned long long X, lab, w, sums, counts, h, c, pm, st; int xdt, d, k; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKKLiiKKKK", &X, &xdt, &lab, &w, &sums, &counts, &n, &d, &k, &h, &c,
+                        &pm, &st))
+    return nullptr;
+  CHECK(sq_centroid_reduce)
+  return ret(sq_centroid_reduce(P(X), xdt, P(lab), P(w), P(sums), P(counts), n, d, k, P(h), P(c),
+                                P(pm), P(st)));
+}
+
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
   unsigned long long pk, co, cnw, cb, clo, cn, sh, st; int k, d, kpad, pol; double nb;
   unsigned k0, k1, s0, s1;
@@ -230,6 +242,7 @@ static PyMethodDef methods[] = {
     {"band_select", py_band_select, METH_VARARGS, "delta-band selection over distance rows"},
     {"band_select_rows", py_band_select_rows, METH_VARARGS, "device-driven overflow fallback"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
+    {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},
     {"ipe_estep", py_ipe_estep, METH_VARARGS, "IPE-noised distance argmin"},

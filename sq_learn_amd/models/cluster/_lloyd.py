@@ -90,6 +90,7 @@ class LloydEngine:
         else:
             self.Xm = Xb if self.d == self.d_pad else None
         self.buf = K.EStepBuffers(self.n, dev)
+        self.rws = K.ReduceWorkspace(self.n, self.k, dev)
         self.sums = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
         self.counts = torch.zeros(self.k, dtype=torch.float64, device=dev)
         self.packed = torch.zeros(self.k * self.d + self.k + 1, dtype=torch.float64, device=dev)
@@ -204,8 +205,8 @@ class LloydEngine:
                 self.sums.zero_()
                 self.counts.zero_()
                 if self.Xm is not None:
-                    K.centroid_accumulate_native(self.Xm, labels, self.weights, self.sums,
-                                                 self.counts, self.k)
+                    K.centroid_reduce_native(self.Xm, labels, self.weights, self.sums,
+                                             self.counts, self.k, self.rws)
                 else:
                     s, c = K.centroid_sums_torch(self.Xb[:, :self.d], labels, self.k,
                                                  self.weights, acc_dtype=torch.float32)

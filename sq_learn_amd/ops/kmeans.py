@@ -192,6 +192,26 @@ def centroid_accumulate_native(X, labels, weights, sums, counts, k, chunk=None):
                                      nat.stream_handle(X.device))
 
 
+class ReduceWorkspace:
+    """Counting-sort workspace of the segmented centroid reduction."""
+
+    def __init__(self, n, k, device):
+        self.hist = torch.zeros(k, dtype=torch.int32, device=device)
+        self.cursor = torch.zeros(k, dtype=torch.int32, device=device)
+        self.perm = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+
+
+def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorkspace):
+    """sums[l] += sum_{i: label_i = l} w_i x_i, counts[l] += sum w_i (GPU)."""
+    n, d = X.shape
+    assert labels.dtype == torch.int32 and sums.dtype == torch.float32 and counts.dtype == torch.float64
+    nat.native().centroid_reduce(X.data_ptr(), nat.dtype_code(X), labels.data_ptr(),
+                                 0 if weights is None else weights.data_ptr(), sums.data_ptr(),
+                                 counts.data_ptr(), n, d, k, ws.hist.data_ptr(),
+                                 ws.cursor.data_ptr(), ws.perm.data_ptr(),
+                                 nat.stream_handle(X.device))
+
+
 def pack_stats_native(sums, counts, inertia, packed, k, d):
     nat.native().pack_stats(sums.data_ptr(), counts.data_ptr(),
                             0 if inertia is None else inertia.data_ptr(), packed.data_ptr(), k, d,

@@ -1,0 +1,249 @@
+"""Extended math (reference ``sklearn/utils/extmath.py``): ``row_norms`` (:49),
+``squared_norm`` (:26), ``safe_sparse_dot`` (:119), ``randomized_range_finder``
+(:161), ``randomized_svd`` (:246), ``svd_flip`` (:522), ``stable_cumsum``
+(:829), ``fast_logdet`` (:81); plus the PPCA dimension MLE of
+``decomposition/_pca.py`` (``_assess_dimension`` / ``_infer_dimension``).
+
+``randomized_svd_distributed`` is the MI355X version of the randomized range
+finder over a row-sharded matrix: the Gaussian test matrix is replicated
+(Philox, same on every rank), each power iteration is ONE fused pass over
+the local rows (``(X-mu)^T ((X-mu) Q)``, csrc/linalg.hip) plus ONE d x l
+all-reduce, and the final orthonormalisation is CholeskyQR2 (two l x l
+all-reduces) instead of a tall-skinny LU/QR.  Normalising the d x l iterate
+every step spans the same subspace as sklearn's LU-normalised n x l iterate.
+"""
+
+import math
+import warnings
+
+import numpy as np
+import torch
+from scipy import linalg
+from scipy.special import gammaln
+
+from .validation import check_random_state
+
+
+def squared_norm(x):
+    x = np.ravel(x, order="K")
+    return float(np.dot(x, x))
+
+
+def row_norms(X, squared=False):
+    if isinstance(X, torch.Tensor):
+        Xf = X if X.dtype in (torch.float32, torch.float64) else X.float()
+        r = (Xf * Xf).sum(1)
+        return r if squared else torch.sqrt(r)
+    X = np.asarray(X)
+    norms = np.einsum("ij,ij->i", X, X)
+    return norms if squared else np.sqrt(norms)
+
+
+def safe_sparse_dot(a, b, *, dense_output=False):
+    out = a @ b
+    if dense_output and hasattr(out, "toarray"):
+        return out.toarray()
+    return out
+
+
+def fast_logdet(A):
+    sign, ld = np.linalg.slogdet(A)
+    return ld if sign > 0 else -np.inf
+
+
+def stable_cumsum(arr, axis=None, rtol=1e-05, atol=1e-08):
+    out = np.cumsum(arr, axis=axis, dtype=np.float64)
+    expected = np.sum(arr, axis=axis, dtype=np.float64)
+    if not np.all(np.isclose(out.take(-1, axis=axis), expected, rtol=rtol, atol=atol, equal_nan=True)):
+        warnings.warn("cumsum was found to be unstable: its last element does not correspond to sum",
+                      RuntimeWarning)
+    return out
+
+
+def svd_flip(u, v, u_based_decision=True):
+    """Deterministic signs (numpy or torch)."""
+    if isinstance(u, torch.Tensor):
+        if u_based_decision:
+            idx = torch.argmax(u.abs(), dim=0)
+            signs = torch.sign(u[idx, torch.arange(u.shape[1], device=u.device)])
+        else:
+            idx = torch.argmax(v.abs(), dim=1)
+            signs = torch.sign(v[torch.arange(v.shape[0], device=v.device), idx])
+        signs = torch.where(signs == 0, torch.ones_like(signs), signs)
+        return u * signs, v * signs[:, None]
+    if u_based_decision:
+        max_abs_cols = np.argmax(np.abs(u), axis=0)
+        signs = np.sign(u[max_abs_cols, range(u.shape[1])])
+    else:
+        max_abs_rows = np.argmax(np.abs(v), axis=1)
+        signs = np.sign(v[range(v.shape[0]), max_abs_rows])
+    signs[signs == 0] = 1
+    return u * signs, v * signs[:, np.newaxis]
+
+
+def svd_flip_distributed(U_local, Vt, comm):
+    """u-based svd_flip where U's rows are sharded: the sign of column j is
+    that of its global max-|.| entry (one gather of 2*r values per rank)."""
+    r = U_local.shape[1]
+    if U_local.shape[0]:
+        a = U_local.abs()
+        idx = torch.argmax(a, dim=0)
+        val = U_local[idx, torch.arange(r, device=U_local.device)]
+        mx = a[idx, torch.arange(r, device=U_local.device)]
+    else:
+        val = torch.zeros(r, dtype=U_local.dtype, device=U_local.device)
+        mx = torch.full((r,), -1.0, dtype=U_local.dtype, device=U_local.device)
+    both = torch.stack([mx.double(), val.double()])
+    got = comm.all_gather(both)
+    allmx = torch.stack([g[0] for g in got])   # [world, r]
+    allv = torch.stack([g[1] for g in got])
+    w = torch.argmax(allmx, dim=0)
+    signs = torch.sign(allv[w, torch.arange(r, device=allv.device)])
+    signs = torch.where(signs == 0, torch.ones_like(signs), signs)
+    s = signs.to(U_local.dtype)
+    return U_local * s, Vt * s.to(Vt.dtype)[:, None]
+
+
+# --------------------------------------------------------------- numpy path
+def randomized_range_finder(A, *, size, n_iter, power_iteration_normalizer="auto",
+                            random_state=None):
+    random_state = check_random_state(random_state)
+    Q = random_state.normal(size=(A.shape[1], size))
+    if hasattr(A, "dtype") and A.dtype.kind == "f":
+        Q = Q.astype(A.dtype, copy=False)
+    if power_iteration_normalizer == "auto":
+        power_iteration_normalizer = "none" if n_iter <= 2 else "LU"
+    for _ in range(n_iter):
+        if power_iteration_normalizer == "none":
+            Q = A @ Q
+            Q = A.T @ Q
+        elif power_iteration_normalizer == "LU":
+            Q, _ = linalg.lu(A @ Q, permute_l=True)
+            Q, _ = linalg.lu(A.T @ Q, permute_l=True)
+        elif power_iteration_normalizer == "QR":
+            Q, _ = linalg.qr(A @ Q, mode="economic")
+            Q, _ = linalg.qr(A.T @ Q, mode="economic")
+    Q, _ = linalg.qr(A @ Q, mode="economic")
+    return Q
+
+
+def randomized_svd(M, n_components, *, n_oversamples=10, n_iter="auto",
+                   power_iteration_normalizer="auto", transpose="auto", flip_sign=True,
+                   random_state=0):
+    random_state = check_random_state(random_state)
+    n_random = n_components + n_oversamples
+    n_samples, n_features = M.shape
+    if n_iter == "auto":
+        n_iter = 7 if n_components < 0.1 * min(M.shape) else 4
+    if transpose == "auto":
+        transpose = n_samples < n_features
+    if transpose:
+        M = M.T
+    Q = randomized_range_finder(M, size=n_random, n_iter=n_iter,
+                                power_iteration_normalizer=power_iteration_normalizer,
+                                random_state=random_state)
+    B = Q.T @ M
+    Uhat, s, Vt = linalg.svd(B, full_matrices=False)
+    U = Q @ Uhat
+    if flip_sign:
+        if not transpose:
+            U, Vt = svd_flip(U, Vt)
+        else:
+            U, Vt = svd_flip(U, Vt, u_based_decision=False)
+    if transpose:
+        return Vt[:n_components, :].T, s[:n_components], U[:, :n_components].T
+    return U[:, :n_components], s[:n_components], Vt[:n_components, :]
+
+
+# ------------------------------------------------------- distributed path
+def randomized_svd_distributed(X_local, mean, n_components, comm, *, n_oversamples=10,
+                               n_iter="auto", seed=0, flip_sign=True, n_rows=None, d=None):
+    """Randomized SVD of the centred row-sharded matrix (X - mean).
+
+    Returns (U_local [n_loc, k], s [k], Vt [k, d]) as tensors."""
+    from ..ops import linalg as L
+    from ..ops.random import philox_normal
+    from ..runtime.rng import RngKey
+    n_loc, dd = X_local.shape
+    d = dd if d is None else d
+    k = int(n_components)
+    l = min(k + n_oversamples, d)
+    n_glob = n_rows if n_rows is not None else n_loc
+    if n_iter == "auto":
+        n_iter = 7 if k < 0.1 * min(n_glob, d) else 4
+    dev = X_local.device
+    wdt = torch.float64 if dev.type == "cpu" else torch.float32
+    Z = philox_normal((d, l), RngKey(seed, "gaussian", 0), dtype=torch.float64, device="cpu").to(dev)
+    Z = Z.to(wdt)
+    m = mean.to(wdt).to(dev)
+    for _ in range(n_iter):
+        Zn = L.power_iter_local(X_local, Z, m).to(torch.float64)
+        comm.all_reduce_(Zn)
+        Z, _ = torch.linalg.qr(Zn)
+        Z = Z.to(wdt)
+    # Y = (X - mu) Z, CholeskyQR2 orthonormalisation
+    step = 1 << 20
+    Y = torch.empty((n_loc, l), dtype=wdt, device=dev)
+    for s in range(0, n_loc, step):
+        Y[s:s + step] = (X_local[s:s + step].to(wdt) - m) @ Z
+    R_tot = torch.eye(l, dtype=torch.float64, device=dev)
+    for _ in range(2):
+        G = (Y.T.to(torch.float64) @ Y.to(torch.float64)) if dev.type == "cpu" else (Y.T @ Y).to(torch.float64)
+        comm.all_reduce_(G)
+        G = 0.5 * (G + G.T)
+        jitter = 0.0
+        for _try in range(5):
+            try:
+                R = torch.linalg.cholesky(G + jitter * torch.eye(l, dtype=G.dtype, device=dev)).T
+                break
+            except Exception:
+                jitter = max(jitter * 10, 1e-12 * float(G.diagonal().max()))
+        Rinv = torch.linalg.inv(R)
+        Y = (Y.to(torch.float64) @ Rinv).to(wdt)
+        R_tot = R @ R_tot
+    # B = Q^T (X - mu)  (l x d)
+    B = torch.zeros((l, d), dtype=torch.float64, device=dev)
+    for s in range(0, n_loc, step):
+        B += (Y[s:s + step].T.to(torch.float64) @ (X_local[s:s + step].to(torch.float64) - m.double()))
+    comm.all_reduce_(B)
+    Uhat, sv, Vt = torch.linalg.svd(B, full_matrices=False)
+    U = (Y.to(torch.float64) @ Uhat)
+    U, Vt = U[:, :k], Vt[:k]
+    if flip_sign:
+        U, Vt = svd_flip_distributed(U, Vt, comm)
+    return U, sv[:k], Vt
+
+
+# --------------------------------------------------------- PPCA dimension
+def _assess_dimension(spectrum, rank, n_samples):
+    """Log-likelihood of a rank ``rank`` PPCA model (Minka 2000)."""
+    n_features = spectrum.shape[0]
+    if not 1 <= rank < n_features:
+        raise ValueError("the tested rank should be in [1, n_features - 1]")
+    eps = 1e-15
+    if spectrum[rank - 1] < eps:
+        return -np.inf
+    pu = -rank * np.log(2.0)
+    for i in range(1, rank + 1):
+        pu += gammaln((n_features - i + 1) / 2.0) - np.log(np.pi) * (n_features - i + 1) / 2.0
+    pl = np.sum(np.log(spectrum[:rank]))
+    pl = -pl * n_samples / 2.0
+    v = max(eps, np.sum(spectrum[rank:]) / (n_features - rank))
+    pv = -np.log(v) * n_samples * (n_features - rank) / 2.0
+    m = n_features * rank - rank * (rank + 1.0) / 2.0
+    pp = np.log(2.0 * np.pi) * (m + rank) / 2.0
+    pa = 0.0
+    spectrum_ = spectrum.copy()
+    spectrum_[rank:n_features] = v
+    for i in range(rank):
+        for j in range(i + 1, len(spectrum)):
+            pa += np.log((spectrum[i] - spectrum[j]) * (1.0 / spectrum_[j] - 1.0 / spectrum_[i])) + np.log(n_samples)
+    return pu + pl + pv + pp - pa / 2.0 - rank * np.log(n_samples) / 2.0
+
+
+def _infer_dimension(spectrum, n_samples):
+    ll = np.empty_like(spectrum)
+    ll[0] = -np.inf
+    for rank in range(1, spectrum.shape[0]):
+        ll[rank] = _assess_dimension(spectrum, rank, n_samples)
+    return int(ll.argmax())

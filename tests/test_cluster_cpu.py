@@ -1,0 +1,180 @@
+"""q-means / k-means on the CPU path: parity with sklearn at delta=0, delta-band
+semantics, tomography noise, IPE distances, estimator API."""
+import pickle
+import warnings
+
+import numpy as np
+import pytest
+import torch
+from sklearn.cluster import KMeans as SKKMeans
+from sklearn.metrics import adjusted_rand_score
+
+from sq_learn_amd.base import clone
+from sq_learn_amd.models.cluster import QMeans, KMeans, k_means, kmeans_plusplus
+from sq_learn_amd.utils.datasets import make_blobs
+
+warnings.simplefilter("ignore")
+
+
+@pytest.fixture(scope="module")
+def blobs():
+    return make_blobs(600, 5, centers=4, cluster_std=0.8, random_state=3)
+
+
+def test_kmeans_matches_sklearn_with_same_init(blobs):
+    X, y = blobs
+    init = X[[0, 10, 20, 30]]
+    ours = KMeans(n_clusters=4, init=init, n_init=1, device="cpu").fit(X)
+    ref = SKKMeans(n_clusters=4, init=init, n_init=1, algorithm="lloyd").fit(X)
+    assert np.array_equal(ours.labels_, ref.labels_)
+    np.testing.assert_allclose(ours.cluster_centers_, ref.cluster_centers_, rtol=1e-10, atol=1e-10)
+    assert abs(ours.inertia_ - ref.inertia_) < 1e-8 * ref.inertia_
+    assert ours.n_iter_ == ref.n_iter_
+    np.testing.assert_array_equal(ours.predict(X[:50]), ref.predict(X[:50]))
+    np.testing.assert_allclose(ours.transform(X[:5]), ref.transform(X[:5]), rtol=1e-10)
+    assert abs(ours.score(X) - ref.score(X)) < 1e-6 * abs(ref.score(X))
+
+
+def test_qmeans_delta0_equals_kmeans(blobs):
+    X, _ = blobs
+    init = X[[1, 11, 21, 31]]
+    q = QMeans(n_clusters=4, init=init, n_init=1, delta=0, device="cpu").fit(X)
+    k = KMeans(n_clusters=4, init=init, n_init=1, device="cpu").fit(X)
+    assert adjusted_rand_score(q.labels_, k.labels_) == 1.0
+    np.testing.assert_allclose(q.cluster_centers_, k.cluster_centers_, rtol=1e-8)
+
+
+def test_qmeans_recovers_blobs_and_prelude(blobs):
+    X, y = blobs
+    q = QMeans(n_clusters=4, delta=0.3, true_distance_estimate=False, random_state=0,
+               device="cpu").fit(X)
+    assert adjusted_rand_score(q.labels_, y) > 0.95
+    assert q.eta == pytest.approx(np.max(np.sum(X ** 2, 1)))
+    s = np.linalg.svd(X, compute_uv=False)
+    assert q.condition_number == pytest.approx(1 / s.min(), rel=1e-6)
+    from sq_learn_amd.quantum import best_mu
+    lab, mu = best_mu(X, 0, 0.1)
+    assert q.muA == pytest.approx(mu, rel=1e-9) and q.muA_norm == lab
+
+
+def test_delta_band_labels_within_band():
+    rng = np.random.RandomState(0)
+    X = rng.randn(2000, 3) * 0.5
+    init = X[:6]
+    delta = 0.4
+    q = QMeans(n_clusters=6, init=init, n_init=1, max_iter=1, delta=delta,
+               true_distance_estimate=False, device="cpu", compute_prelude=False).fit(X)
+    # one E-step on the init centres: every label must lie inside the band
+    from sq_learn_amd.models.cluster._lloyd import LloydEngine
+    Xt = torch.as_tensor(X - X.mean(0))
+    eng = LloydEngine(Xt, 6, delta=delta, seed=1)
+    eng.set_centers(torch.as_tensor(init - X.mean(0)))
+    lab, mind, _ = eng.estep()
+    D = ((Xt[:, None, :] - torch.as_tensor(init - X.mean(0))[None]) ** 2).sum(-1)
+    chosen = D[torch.arange(len(X)), lab]
+    assert torch.all(chosen <= D.min(1).values + delta + 1e-9)
+    band = (D <= D.min(1).values[:, None] + delta).sum(1)
+    assert (band > 1).float().mean() > 0.2
+    # uniform: fraction choosing the argmin ~ mean(1/|band|)
+    multi = band > 1
+    frac = (lab[multi] == D[multi].argmin(1)).double().mean().item()
+    assert abs(frac - (1.0 / band[multi].double()).mean().item()) < 0.06
+
+
+def test_intermediate_error_noise_bound(blobs):
+    X, _ = blobs
+    init = X[[0, 10, 20, 30]]
+    base = QMeans(n_clusters=4, init=init, n_init=1, max_iter=1, delta=0.5,
+                  true_distance_estimate=False, device="cpu", random_state=0,
+                  compute_prelude=False)
+    a = clone(base).set_params(intermediate_error=False).fit(X)
+    b = clone(base).set_params(intermediate_error=True, true_tomography=False).fit(X)
+    bound = (0.5 / 2) / np.sqrt(4 * 5)
+    diff = np.abs(a.cluster_centers_ - b.cluster_centers_)
+    assert diff.max() <= bound + 1e-12 and diff.max() > 0.3 * bound
+
+
+def test_intermediate_error_requires_delta(blobs):
+    X, _ = blobs
+    with pytest.raises(ValueError):
+        QMeans(n_clusters=4, delta=0, intermediate_error=True).fit(X)
+
+
+def test_true_tomography_centres(blobs):
+    X, y = blobs
+    q = QMeans(n_clusters=4, delta=0.4, true_distance_estimate=False, intermediate_error=True,
+               true_tomography=True, random_state=2, max_iter=5, device="cpu").fit(X)
+    assert adjusted_rand_score(q.labels_, y) > 0.9
+
+
+def test_ipe_distances_path():
+    X, y = make_blobs(120, 4, centers=3, cluster_std=0.5, random_state=1)
+    q = QMeans(n_clusters=3, delta=0.2, true_distance_estimate=True, random_state=0, n_init=1,
+               max_iter=5, device="cpu").fit(X)
+    assert adjusted_rand_score(q.labels_, y) > 0.9
+
+
+def test_reproducible_and_seed_sensitive(blobs):
+    X, _ = blobs
+    kw = dict(n_clusters=4, delta=1.0, true_distance_estimate=False, intermediate_error=True,
+              true_tomography=False, n_init=2, device="cpu")
+    a = QMeans(random_state=5, **kw).fit(X)
+    b = QMeans(random_state=5, **kw).fit(X)
+    c = QMeans(random_state=6, **kw).fit(X)
+    np.testing.assert_array_equal(a.cluster_centers_, b.cluster_centers_)
+    assert not np.array_equal(a.cluster_centers_, c.cluster_centers_)
+
+
+def test_predict_score_transform(blobs):
+    X, _ = blobs
+    q = QMeans(n_clusters=4, delta=0.2, true_distance_estimate=False, random_state=0,
+               device="cpu").fit(X)
+    p = q.predict(X)
+    assert p.shape == (len(X),) and p.dtype == np.int32
+    assert adjusted_rand_score(p, q.labels_) > 0.95
+    pb = q.predict(X, delta=0.5)
+    assert pb.shape == (len(X),)
+    assert q.score(X) < 0
+    t = q.transform(X[:7])
+    assert t.shape == (7, 4)
+    np.testing.assert_allclose(t.min(1) ** 2, -np.array([q.score(X[i:i + 1]) for i in range(7)]), rtol=1e-9)
+    assert q.fit_predict(X).shape == (len(X),)
+    q_rt, c_rt = q.runtime_comparison(1000, 50)
+    assert q_rt.shape == (100, 100) and c_rt.shape == (100, 100)
+
+
+def test_estimator_contract(blobs):
+    X, _ = blobs
+    q = QMeans(n_clusters=4, delta=0.2, random_state=0, true_distance_estimate=False)
+    params = q.get_params()
+    assert params["delta"] == 0.2 and params["n_clusters"] == 4
+    c = clone(q)
+    assert c.get_params() == params and c is not q
+    q.fit(X)
+    s = pickle.dumps(q)
+    q2 = pickle.loads(s)
+    np.testing.assert_array_equal(q2.cluster_centers_, q.cluster_centers_)
+    np.testing.assert_array_equal(q2.predict(X), q.predict(X))
+    assert "QMeans(" in repr(q)
+    with pytest.raises(ValueError):
+        QMeans(n_clusters=4).set_params(bogus=1)
+    with pytest.raises(ValueError):
+        q.predict(X[:, :3])
+
+
+def test_k_means_function_and_kpp(blobs):
+    X, y = blobs
+    C, lab, inertia = k_means(X, 4, random_state=0)
+    assert adjusted_rand_score(lab, y) > 0.95
+    C2, lab2, _ = k_means(X, 4, random_state=0, delta=0.1, true_distance_estimate=False)
+    assert adjusted_rand_score(lab2, y) > 0.95
+    centers, idx = kmeans_plusplus(X, 4, random_state=0)
+    assert centers.shape == (4, 5) and len(set(idx.tolist())) == 4
+    np.testing.assert_allclose(centers, X[idx])
+
+
+def test_sample_weight_affects_centres():
+    X = np.array([[0.0, 0.0], [1.0, 0.0], [10.0, 0.0], [11.0, 0.0]])
+    init = np.array([[0.0, 0.0], [10.0, 0.0]])
+    k = KMeans(n_clusters=2, init=init, n_init=1, device="cpu").fit(X, sample_weight=[1, 3, 1, 1])
+    np.testing.assert_allclose(sorted(k.cluster_centers_[:, 0]), [0.75, 10.5])

@@ -104,6 +104,24 @@ def test_centroid_accumulate(cuda):
     assert torch.allclose(sums.double(), rs, atol=1e-3)
 
 
+@pytest.mark.parametrize("dtype,d", [(torch.float32, 256), (torch.bfloat16, 256), (torch.float32, 20),
+                                     (torch.bfloat16, 512)])
+def test_centroid_reduce(cuda, dtype, d):
+    n, k = 70001, 1000
+    X = torch.randn(n, d, dtype=torch.float32, device=cuda).to(dtype)
+    lab = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
+    lab[:5000] = 3  # a big cluster
+    w = torch.rand(n, dtype=torch.float32, device=cuda)
+    ws = K.ReduceWorkspace(n, k, cuda)
+    for weights in (None, w):
+        sums = torch.zeros(k, d, dtype=torch.float32, device=cuda)
+        cnt = torch.zeros(k, dtype=torch.float64, device=cuda)
+        K.centroid_reduce_native(X, lab, weights, sums, cnt, k, ws)
+        rs, rc = K.centroid_sums_torch(X.double(), lab, k, weights)
+        assert torch.allclose(sums.double(), rs, atol=2e-3, rtol=1e-4)
+        assert torch.allclose(cnt, rc, rtol=1e-6)
+
+
 def test_finalize_noise_and_shift(cuda):
     k, d = 70, 48
     sums = torch.randn(k, d, dtype=torch.float32, device=cuda)
