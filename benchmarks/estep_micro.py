@@ -1,6 +1,10 @@
 """Isolated E-step / M-step kernel timing (for rocprofv3 PMC runs)."""
 import argparse
+import os
+import sys
 import time
+
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
 
 import torch
 

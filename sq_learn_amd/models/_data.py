@@ -122,7 +122,7 @@ def prelude_stats(data: Data, mu_start=0.0, mu_end=1.0, mu_step=0.1, condition=T
     return eta, label, mu, cond
 
 
-def best_mu_distributed(data: Data, start=0.0, end=1.0, step=0.05, fro_sq=None):
+def best_mu_distributed(data: Data, start=0.0, end=1.0, step=0.05, fro_sq=None, fro_sq_global=None):
     """``best_mu`` (``Utility.py:196-231``) over a row-sharded matrix: one
     fused power-sum pass (row-max and column sums for every exponent of the
     p-grid), then MAX / SUM all-reduces."""
@@ -140,11 +140,14 @@ def best_mu_distributed(data: Data, start=0.0, end=1.0, step=0.05, fro_sq=None):
         s2 = float(colmax[pos[round(float(2 * (1 - p)), 12)]])
         vals.append(float(np.sqrt(s1 * s2)))
     best = int(np.argmin(vals))
-    if fro_sq is None:
-        fro_sq = float((data.X.double() ** 2).sum())
-    t = torch.tensor([fro_sq], dtype=torch.float64, device=data.device)
-    data.comm.all_reduce_(t)
-    fro = float(np.sqrt(t.item()))
+    if fro_sq_global is not None:
+        fro = float(np.sqrt(fro_sq_global))
+    else:
+        if fro_sq is None:
+            fro_sq = float((data.X.double() ** 2).sum())
+        t = torch.tensor([fro_sq], dtype=torch.float64, device=data.device)
+        data.comm.all_reduce_(t)
+        fro = float(np.sqrt(t.item()))
     if vals[best] <= fro:
         return f"p={domain[best]}", vals[best]
     return "Frobenius", fro

@@ -224,7 +224,7 @@ class QPCA(_BasePCA):
         centred = type(data)(self._centred(data, mean), data.n_global, data.row_offset, data.comm,
                              data.source_kind)
         self.norm_muA, self.muA = best_mu_distributed(centred, start=0, end=1.0, step=0.1,
-                                                      fro_sq=float((S ** 2).sum()))
+                                                      fro_sq_global=float((S ** 2).sum()))
         self._data_for_tomography = data
         self._quantum_extras(centred)
         return self

@@ -1,0 +1,115 @@
+"""Row-sharded data parallelism on CPU with gloo (world_size 2 and 3): a sharded
+fit must reproduce the single-process fit (counter-based RNG keyed by global
+row -> identical draws; SURVEY.md §4 implication 3, the analogue of the
+reference's thread-count invariance test test_k_means.py:840-852)."""
+import os
+import socket
+import tempfile
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir, case):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                init_method=f"tcp://127.0.0.1:{port}")
+        import warnings
+        warnings.simplefilter("ignore")
+        from sq_learn_amd.parallel import Comm, shard_rows
+        from sq_learn_amd.utils.datasets import make_blobs
+        comm = Comm(dist.group.WORLD)
+        X, y = make_blobs(900, 6, centers=5, cluster_std=1.0, random_state=7)
+        sa = shard_rows(X, comm=comm)
+        if case == "qmeans":
+            from sq_learn_amd.models.cluster import QMeans
+            for init in ("random", "k-means++"):
+                kw = dict(n_clusters=5, delta=0.8, true_distance_estimate=False,
+                          intermediate_error=True, true_tomography=False, random_state=3,
+                          n_init=2, init=init, device="cpu")
+                ref = QMeans(**kw).fit(X)
+                got = QMeans(**kw).fit(sa)
+                np.testing.assert_allclose(got.cluster_centers_, ref.cluster_centers_, rtol=1e-9, atol=1e-9)
+                loc = torch.as_tensor(got.labels_.astype(np.int64))
+                full = torch.cat(comm.all_gather_varlen(loc)).numpy()
+                np.testing.assert_array_equal(full, ref.labels_)
+                assert abs(got.inertia_ - ref.inertia_) <= 1e-9 * ref.inertia_
+                assert got.n_iter_ == ref.n_iter_
+                assert abs(got.muA - ref.muA) < 1e-9 * ref.muA
+                assert abs(got.condition_number - ref.condition_number) < 1e-6 * ref.condition_number
+        elif case == "ipe":
+            from sq_learn_amd.models.cluster import QMeans
+            Xs = X[:120]
+            sa2 = shard_rows(Xs, comm=comm)
+            kw = dict(n_clusters=3, delta=0.3, true_distance_estimate=True, random_state=1,
+                      n_init=1, max_iter=3, init="random", device="cpu", compute_prelude=False)
+            ref = QMeans(**kw).fit(Xs)
+            got = QMeans(**kw).fit(sa2)
+            loc = torch.as_tensor(got.labels_.astype(np.int64))
+            full = torch.cat(comm.all_gather_varlen(loc)).numpy()
+            np.testing.assert_array_equal(full, ref.labels_)
+        elif case == "kmeans":
+            from sq_learn_amd.models.cluster import KMeans
+            ref = KMeans(n_clusters=5, random_state=0, n_init=1, device="cpu").fit(X)
+            got = KMeans(n_clusters=5, random_state=0, n_init=1, device="cpu").fit(sa)
+            np.testing.assert_allclose(got.cluster_centers_, ref.cluster_centers_, rtol=1e-9)
+            assert abs(got.inertia_ - ref.inertia_) <= 1e-9 * ref.inertia_
+        elif case == "pca":
+            from sq_learn_amd.models.decomposition import PCA, QPCA
+            from sq_learn_amd.models.decomposition._svd import full_svd
+            from sq_learn_amd.models._data import as_data, global_mean_var
+            rng = np.random.RandomState(0)
+            Z = rng.randn(600, 8) @ rng.randn(8, 8) + 3.0
+            sz = shard_rows(Z, comm=comm)
+            # Gram path (forced) on shards vs exact SVD of the full matrix
+            d = as_data(sz)
+            mean, _ = global_mean_var(d)
+            res = full_svd(d, mean, 4, method="gram")
+            S = np.linalg.svd(Z - Z.mean(0), compute_uv=False)
+            np.testing.assert_allclose(res.S, S, rtol=1e-8)
+            U = torch.cat(comm.all_gather_varlen(res.U_local)).numpy()
+            Uf, Sf, Vf = np.linalg.svd(Z - Z.mean(0), full_matrices=False)
+            np.testing.assert_allclose(np.abs(U), np.abs(Uf[:, :4]), atol=1e-8)
+            # randomized path
+            p = PCA(n_components=3, svd_solver="randomized", random_state=0, device="cpu").fit(sz)
+            np.testing.assert_allclose(p.singular_values_, S[:3], rtol=1e-6)
+            q = QPCA(n_components=3, svd_solver="full", random_state=0, device="cpu").fit(
+                sz, eps=0.01, theta_major=1e-3, delta=0.1, estimate_all=True, true_tomography=False)
+            qr = QPCA(n_components=3, svd_solver="full", random_state=0, device="cpu").fit(
+                Z, eps=0.01, theta_major=1e-3, delta=0.1, estimate_all=True, true_tomography=False)
+            np.testing.assert_allclose(q.singular_values_, qr.singular_values_, rtol=1e-8)
+            np.testing.assert_allclose(q.estimate_s_values, qr.estimate_s_values, rtol=1e-12)
+            assert abs(q.muA - qr.muA) < 1e-9 * qr.muA
+        with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+            f.write("ok")
+    except Exception:
+        with open(os.path.join(outdir, f"err{rank}"), "w") as f:
+            f.write(traceback.format_exc())
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world", [("qmeans", 2), ("qmeans", 3), ("kmeans", 2), ("pca", 2),
+                                        ("ipe", 2)])
+def test_sharded_matches_single_process(case, world):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d, case), nprocs=world, join=True)
+        errs = [open(os.path.join(d, f)).read() for f in os.listdir(d) if f.startswith("err")]
+        assert not errs, errs[0]
+        assert len([f for f in os.listdir(d) if f.startswith("ok")]) == world
