@@ -109,8 +109,11 @@ def main():
             torch.cuda.synchronize()
             comm.barrier()
             tq = time.perf_counter()
+            # theta: keep the top-8 estimated singular values (half the 8th)
+            theta = 0.5 * float(q.singular_values_[7])
             q = QPCA(n_components=8, svd_solver="full", device=dev)
-            q.fit(sa, eps=1e-3, theta_major=0.0, delta=0.1, estimate_all=True, true_tomography=False)
+            q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True,
+                  true_tomography=False)
             torch.cuda.synchronize()
             comm.barrier()
             tq = time.perf_counter() - tq

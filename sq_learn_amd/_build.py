@@ -9,6 +9,10 @@ that lives next to this file (so it travels with the repo snapshot to GPU
 boxes and is what the python processes load).
 
 Usage: ``python -m sq_learn_amd._build [--force] [--jobs N] [--debug]``.
+
+Tuning variants (kernel experiments only): ``--define NAME=VALUE ... --out
+PATH.so`` builds a separately named extension with extra preprocessor
+definitions; ``SQ_NATIVE_VARIANT=PATH.so`` makes the loader use it.
 """
 
 import argparse
@@ -56,21 +60,25 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force=False, jobs=None, debug=False, verbose=False):
+def build(force=False, jobs=None, debug=False, verbose=False, defines=(), out=None):
     """Compile and link the extension; returns its path."""
-    out = ext_path()
-    if not force and not needs_build():
+    variant = out is not None
+    out = out or ext_path()
+    if not variant and not force and not needs_build():
         return out
-    os.makedirs(BUILD, exist_ok=True)
+    bdir = BUILD if not variant else os.path.join(
+        BUILD, "variant_" + os.path.splitext(os.path.basename(out))[0])
+    os.makedirs(bdir, exist_ok=True)
     hips, _ = _sources()
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = [HIPCC, "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
               "-Wno-unused-result", "-Wno-unused-command-line-argument"] + opt
+    common += ["-D" + d for d in defines]
     py_inc = sysconfig.get_paths()["include"]
     jobs = jobs or int(os.environ.get("MAX_JOBS", min(8, os.cpu_count() or 4)))
 
     def compile_one(src):
-        obj = os.path.join(BUILD, src + ".o")
+        obj = os.path.join(bdir, src + ".o")
         cmd = common + ["-c", os.path.join(CSRC, src), "-o", obj]
         if src == "module.cpp":
             cmd = [HIPCC, "-std=c++17", "-fPIC", "-O2", "-I", py_inc, "-c",
@@ -95,8 +103,11 @@ def main(argv=None):
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--define", action="append", default=[])
+    ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
-    path = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose)
+    path = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose,
+                 defines=a.define, out=a.out)
     print(path)
 
 

@@ -57,109 +57,122 @@ SQ_DEV uint32_t band_key(const RngKey& key, long long grow, uint32_t j) {
   return key.block(idx).x;
 }
 
-template <int KS, int NW>
+// Centroid operand layout (written by centroid_finalize / centers_to_bf16):
+// per 64-centroid tile, CPR = (d_pad + 16) / 8 chunks of 16 B, chunk-major:
+//   elem(j, f) at ((tile * CPR + f / 8) * 64 + j % 64) * 8 + f % 8
+// holding C' = -2 c for f < d_pad and, in the augmented chunk f = d_pad ..
+// d_pad + 7, [hi, mid, lo, 0 ...] (3-way bf16 split of ||c||^2).  With the
+// constant A fragment [1, 1, 1, 0 ...] for that chunk the MFMA accumulates
+// D' = ||c||^2 - 2 x.c directly.  The tile is one contiguous 16-B-per-lane
+// LDS-DMA copy and every B-fragment read is base + constant offset: lanes of
+// a ds_read_b128 group hit 16 consecutive 16-B slots (conflict-free).
+//
+// Persistent: the grid is sized to the resident workgroups and each one walks
+// row blocks blk = blockIdx.x, + gridDim.x, ...  The centroid-tile ring runs
+// continuously across blocks (tile 0 of the next block is staged while the
+// last tiles of the current one are multiplied), and the next block's X rows
+// are loaded into the A registers as soon as the last MFMA of the current
+// block has consumed them, so their latency hides behind the epilogue and
+// the merge instead of stalling a fresh workgroup's first MFMA.
+#ifndef SQ_ESTEP_PF
+#define SQ_ESTEP_PF 1
+#endif
+template <int KSD, int NW>
 __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, const float* __restrict__ cn,
     const float* __restrict__ xn, int* __restrict__ labels, float* __restrict__ mind,
     long long* __restrict__ ovf_rows, int* __restrict__ ovf_count, double* __restrict__ inertia,
     long long n, int k, int k_pad, float delta, RngKey key, long long row_offset, int ovf_cap,
-    int idx_bits) {
-  constexpr int DP = KS * 16;            // padded feature count
-  constexpr int CPR = DP / 8;            // 16-B chunks per row
-  constexpr int SWZ = (CPR >= 16 ? 16 : CPR) - 1;
-  constexpr int TILE_BYTES = kBN * DP * 2;
+    int idx_bits, int dbg) {
+  (void)cn;
+  (void)k;
+  constexpr int KS = KSD + 1;            // data k-steps + augmented norm step
+  constexpr int DX = KSD * 16;           // X row length (padded features)
+  constexpr int CPR = KS * 2;            // 16-B chunks per centroid (incl. norms)
+  constexpr int TILE_BYTES = kBN * CPR * 16;
   constexpr int PIECES = TILE_BYTES / 1024;  // 1 KiB LDS-DMA pieces per tile
+  constexpr int ROWS = NW * 32;          // rows per block
+  constexpr int PF = SQ_ESTEP_PF;        // B-fragment prefetch distance (k-steps)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* buf0 = smem;
-  unsigned char* buf1 = smem + TILE_BYTES;
-  float* cn_lds = reinterpret_cast<float*>(smem + 2 * TILE_BYTES);
+  auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * TILE_BYTES; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31;
   const int half = lane >> 5;
-  const long long row0 = (long long)blockIdx.x * (NW * 32) + wave * 32;
   const uint32_t keep = ~((1u << idx_bits) - 1u);
   const int n_tiles = k_pad / kBN;
+  const long long nblk = (n + ROWS - 1) / ROWS;
+  long long blk = blockIdx.x;
+  if (blk >= nblk) return;
 
-  // ---- stage cn into LDS (ordinary loads, before any LDS-DMA is in flight)
-  for (int j = tid; j < k_pad; j += NW * 64) cn_lds[j] = cn[j];
-
-  // ---- issue LDS-DMA for centroid tile 0
-  auto stage = [&](int t, unsigned char* dst) {
-    const uint16_t* tile = C + (size_t)t * kBN * DP;
+  // ---- LDS-DMA of centroid tile (G mod n_tiles) into ring slot G & 1: a
+  // contiguous 16-B-per-lane copy
+  auto stage = [&](int G) {
+    const int t = (int)(G % n_tiles);
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_BYTES;
+    unsigned char* dst = buf(G);
+    if ((dbg & 2) && G > 1) return;   // ablation: no centroid staging
     for (int p = wave; p < PIECES; p += NW) {
-      int P = p * 64 + lane;          // physical chunk written by this lane
-      int rrow = P / CPR, pc = P % CPR;
-      int lc = pc ^ (rrow & SWZ);     // logical chunk stored at (rrow, pc)
-      const uint16_t* src = tile + (size_t)rrow * DP + lc * 8;
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)src,
+          (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
           (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
     }
   };
-  stage(0, buf0);
 
-  // ---- A fragments: this wave's 32 rows, all of K, kept in VGPRs
+  // ---- A fragments: this wave's 32 rows, all of K, kept in VGPRs; the
+  // augmented step is the constant [1, 1, 1, 0, ...] (k = 0..2 of the step)
   bf16x8 a[KS];
-  {
-    long long r = row0 + r32;
-    bool ok = r < n;
-    const uint16_t* xr = X + (size_t)(ok ? r : 0) * DP + half * 8;
+  auto load_a = [&](long long b) {
+    long long r = b * ROWS + wave * 32 + r32;
+    const uint16_t* xr = X + (size_t)(r < n ? r : n - 1) * DX + half * 8;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(xr + ks * 16);
-      a[ks] = ok ? v : (bf16x8)0;
-    }
+    for (int ks = 0; ks < KSD; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(xr + ks * 16);
+  };
+  {
+    bf16x8 aug = (bf16x8)0;
+    if (half == 0) { aug[0] = aug[1] = aug[2] = (short)0x3f80; }   // hi + mid + lo
+    a[KSD] = aug;
   }
 
   float m1[16], m2[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { m1[i] = __builtin_inff(); m2[i] = __builtin_inff(); }
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // Cross-tile software pipeline: while the MFMAs of tile t+1 run, the VALU
-  // epilogue (distance, index packing, top-2) of tile t executes in the
-  // MFMA shadow.  Two accumulator sets (pA, pB) alternate with static names.
-  auto ldb = [&](const unsigned char* rp, int brow, int ks) -> bf16x8 {
-    int pc = (ks * 2 + half) ^ (brow & SWZ);
-    return *reinterpret_cast<const bf16x8*>(rp + pc * 16);
+  // chunk-major tile: B fragment of (k-step ks, 32-col block nb) for this
+  // lane = base + ks * 2048 + nb * 512 (immediate offsets, no VALU math)
+  const int lane_off = (half * 64 + r32) * 16;
+  auto ldb = [&](const unsigned char* cur, int nb, int ks) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(cur + lane_off + ks * 2048 + nb * 512);
   };
-  // MFMA chain of one tile (both 32-col blocks, B ring prefetched 2 ahead)
-  // interleaved with the epilogue of the previous tile (if any).
+  // Cross-tile software pipeline: while the MFMAs of tile t+1 run, the VALU
+  // epilogue (index packing, top-2) of tile t executes in the MFMA shadow.
+  // Two accumulator sets (pA, pB) alternate with static names.
   auto tile_step = [&](const unsigned char* cur, f32x16& n0, f32x16& n1, bool do_mfma,
                        const f32x16& o0, const f32x16& o1acc, int t_prev, bool do_epi) {
-    const unsigned char* rowp0 = cur + r32 * (DP * 2);
-    const unsigned char* rowp1 = cur + (32 + r32) * (DP * 2);
     const uint32_t j0 = (uint32_t)(t_prev * kBN + r32);
     const uint32_t j1 = j0 + 32;
-    const float c0 = cn_lds[do_epi ? j0 : 0], c1 = cn_lds[do_epi ? j1 : 0];
     if (do_mfma) {
       f32x16 acc0 = {0}, acc1 = {0};
-      bf16x8 b0[3], b1[3];
-      b0[0] = ldb(rowp0, r32, 0);
-      b1[0] = ldb(rowp1, 32 + r32, 0);
-      if (KS > 1) { b0[1] = ldb(rowp0, r32, 1); b1[1] = ldb(rowp1, 32 + r32, 1); }
+      bf16x8 b0[PF + 1], b1[PF + 1];
+#pragma unroll
+      for (int q = 0; q < PF && q < KS; ++q) { b0[q] = ldb(cur, 0, q); b1[q] = ldb(cur, 1, q); }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        if (ks + 2 < KS) {
-          b0[(ks + 2) % 3] = ldb(rowp0, r32, ks + 2);
-          b1[(ks + 2) % 3] = ldb(rowp1, 32 + r32, ks + 2);
+        if (ks + PF < KS) {
+          b0[(ks + PF) % (PF + 1)] = ldb(cur, 0, ks + PF);
+          b1[(ks + PF) % (PF + 1)] = ldb(cur, 1, ks + PF);
         }
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b0[ks % 3], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b1[ks % 3], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b0[ks % (PF + 1)], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b1[ks % (PF + 1)], acc1, 0, 0, 0);
       }
       n0 = acc0;
       n1 = acc1;
     }
-    if (do_epi) {
+    if (do_epi && !(dbg & 4)) {   // dbg bit 2: ablation, no epilogue
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p0 = packf(__builtin_fmaf(-2.0f, o0[i], c0), keep, j0);
-        float p1 = packf(__builtin_fmaf(-2.0f, o1acc[i], c1), keep, j1);
+        float p0 = packf(o0[i], keep, j0);
+        float p1 = packf(o1acc[i], keep, j1);
         float q1 = m1[i];
         float q2 = m2[i];
         q2 = med3_raw(q1, p0, q2);
@@ -171,13 +184,13 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
       }
     }
     if (do_mfma && do_epi) {
-      // [2 cn reads + 4 B reads] then per k-step [2 B reads][2 MFMA][8 VALU]
-      __builtin_amdgcn_sched_group_barrier(0x100, KS > 1 ? 6 : 4, 0);
+      // [2 PF B reads] then per k-step [2 B reads][2 MFMA][~6 VALU]
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (PF < KS ? PF : KS), 0);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        if (ks + 2 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        if (ks + PF < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 128 / KS, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, (96 + KS - 1) / KS, 0);
       }
     }
   };
@@ -185,73 +198,126 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
+  auto merge2 = [](float& a1, float& a2, float b1, float b2) {
+    float lo2 = min_raw(a2, b2);
+    a2 = med3_raw(a1, b1, lo2);   // 2nd smallest of two sorted pairs
+    a1 = min_raw(a1, b1);
+  };
 
-  f32x16 pA0, pA1, pB0, pB1;
-  // prologue: tile 0 -> pA
-  if (n_tiles > 1) stage(1, buf1);
-  tile_step(buf0, pA0, pA1, true, pA0, pA1, 0, false);
+  int G = 0;   // global tile sequence number: tile G lives in buf(G)
+  stage(0);
+  load_a(blk);
   sync_tile();
-  // steady state: every combined step is ONE basic block (unconditional MFMA
-  // + epilogue) so the scheduler can interleave them; static pA/pB names by
-  // unrolling two steps; the last epilogue runs alone.
-  int t = 0;
-  while (true) {
-    if (t + 1 >= n_tiles) { tile_step(buf0, pB0, pB1, false, pA0, pA1, t, true); break; }
-    if (t + 2 < n_tiles) stage(t + 2, (t & 1) ? buf1 : buf0);
-    tile_step((t & 1) ? buf0 : buf1, pB0, pB1, true, pA0, pA1, t, true);
-    sync_tile();
-    ++t;
-    if (t + 1 >= n_tiles) { tile_step(buf0, pA0, pA1, false, pB0, pB1, t, true); break; }
-    if (t + 2 < n_tiles) stage(t + 2, (t & 1) ? buf1 : buf0);
-    tile_step((t & 1) ? buf0 : buf1, pA0, pA1, true, pB0, pB1, t, true);
-    sync_tile();
-    ++t;
-  }
-
-  // ---- merge the 32 lanes of each half (same rows), resolve the band
   double my_inertia = 0.0;
+
+  for (; blk < nblk; blk += gridDim.x) {
+    const long long row0 = blk * ROWS + wave * 32;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    float M = m1[i];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) M = fminf(M, __shfl_xor(M, o, 64));
-    const int rloc = (i & 3) + 8 * (i >> 2) + 4 * half;
-    const long long grow_local = row0 + rloc;
-    const bool row_ok = grow_local < n;
-    const float mval = valf(M, keep);
-    const float thr = mval + delta;
-    const bool v1 = valf(m1[i], keep) <= thr;
-    const bool v2 = valf(m2[i], keep) <= thr;
-    unsigned long long b1 = __ballot(v1);
-    unsigned long long b2 = __ballot(v2);
-    uint32_t hb1 = (uint32_t)(b1 >> (32 * half));
-    uint32_t hb2 = (uint32_t)(b2 >> (32 * half));
-    uint32_t winner = __float_as_uint(M) & ~keep;
-    bool overflow = hb2 != 0u;
-    if (!overflow && __popc(hb1) > 1) {
-      // uniform pick among the band members: smallest Philox key
-      uint32_t jj = __float_as_uint(m1[i]) & ~keep;
-      uint32_t kk = v1 ? ((band_key(key, row_offset + grow_local, jj) & keep) | jj) : 0xFFFFFFFFu;
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) kk = min(kk, (uint32_t)__shfl_xor((int)kk, o, 64));
-      winner = kk & ~keep;
-    }
-    if (r32 == (i & 31) && row_ok) {
-      float dist = fmaxf(xn[grow_local] + mval, 0.0f);
-      if (overflow) {
-        int slot = atomicAdd(ovf_count, 1);
-        if (slot < ovf_cap) ovf_rows[slot] = grow_local;
-        labels[grow_local] = -1;
-        mind[grow_local] = dist;
-      } else {
-        labels[grow_local] = (int)winner;
-        mind[grow_local] = dist;
+    for (int i = 0; i < 16; ++i) { m1[i] = __builtin_inff(); m2[i] = __builtin_inff(); }
+    f32x16 pA0, pA1, pB0, pB1;
+    // block prologue: tile G (landed) -> pA while tile G+1 streams in
+    stage(G + 1);
+    tile_step(buf(G), pA0, pA1, true, pA0, pA1, 0, false);
+    sync_tile();
+    // steady state: every combined step is ONE basic block (unconditional MFMA
+    // + epilogue) so the scheduler can interleave them; static pA/pB names by
+    // unrolling two steps; the block's last epilogue runs alone, after the
+    // next block's X loads were issued.
+    int t = 0;
+    while (true) {
+      if (t + 1 >= n_tiles) {
+        load_a(blk + gridDim.x);   // unconditional (clamped rows): no phi on a[]
+        tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
+        break;
       }
+      stage(G + 2);
+      tile_step(buf(G + 1), pB0, pB1, true, pA0, pA1, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+      if (t + 1 >= n_tiles) {
+        load_a(blk + gridDim.x);   // unconditional (clamped rows): no phi on a[]
+        tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pA0, pA1, true, pB0, pB1, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+    }
+    ++G;   // the block's last tile is consumed; tile G (next block) has landed
+
+    // ---- merge the 32 lanes of each half: transposed top-2 reduce-scatter.
+    // Each stage halves the rows a lane carries (xor 16, 8, 4, 2), so a lane
+    // ends with the global top-2 of row i = r32 >> 1 after 15 (not 80)
+    // shuffle-merges; xor 1 pairs the two lanes that share a row.
+    float R1[16], R2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { R1[i] = m1[i]; R2[i] = m2[i]; }
+#pragma unroll
+    for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
+      const bool hi = (r32 & o) != 0;   // keep the upper half of the rows
+#pragma unroll
+      for (int j = 0; j < c; ++j) {
+        float s1 = hi ? R1[j] : R1[c + j], s2 = hi ? R2[j] : R2[c + j];
+        float k1 = hi ? R1[c + j] : R1[j], k2 = hi ? R2[c + j] : R2[j];
+        float t1 = __shfl_xor(s1, o, 64), t2 = __shfl_xor(s2, o, 64);
+        merge2(k1, k2, t1, t2);
+        R1[j] = k1;
+        R2[j] = k2;
+      }
+    }
+    float q1 = R1[0], q2 = R2[0];
+    merge2(q1, q2, __shfl_xor(R1[0], 1, 64), __shfl_xor(R2[0], 1, 64));
+
+    const int irow = r32 >> 1;
+    const int rloc = (irow & 3) + 8 * (irow >> 2) + 4 * half;
+    const long long grow_local = row0 + rloc;
+    const bool owner = ((r32 & 1) == 0) && grow_local < n;
+    const float mval = valf(q1, keep);
+    const float thr = mval + delta;
+    const bool band2 = valf(q2, keep) <= thr;
+    if (owner) {
+      const float dist = fmaxf(xn[grow_local] + mval, 0.0f);
+      mind[grow_local] = dist;
+      if (!band2) labels[grow_local] = (int)(__float_as_uint(q1) & ~keep);
       my_inertia += (double)dist;
+    }
+    // rows with >= 2 band members (rare for small delta): exact resolution
+    // from the per-lane top-2 lists; a lane holding two members -> overflow
+    const unsigned long long slow = __ballot(owner && band2);
+    if (slow && !dbg) {   // (ablation runs skip band resolution)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const unsigned long long sel = slow & ((1ull << (2 * i)) | (1ull << (32 + 2 * i)));
+        if (!sel) continue;
+        const bool mine = (slow >> (32 * half + 2 * i)) & 1ull;
+        const float thr_i = __shfl(thr, 32 * half + 2 * i, 64);
+        const bool v1 = mine && valf(m1[i], keep) <= thr_i;
+        const bool v2 = mine && valf(m2[i], keep) <= thr_i;
+        const uint32_t hb2 = (uint32_t)(__ballot(v2) >> (32 * half));
+        const uint32_t jj = __float_as_uint(m1[i]) & ~keep;
+        const long long g = row0 + (i & 3) + 8 * (i >> 2) + 4 * half;
+        uint32_t kk = v1 ? ((band_key(key, row_offset + g, jj) & keep) | jj) : 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) kk = min(kk, (uint32_t)__shfl_xor((int)kk, o, 64));
+        if (mine && r32 == 2 * i) {
+          if (hb2 != 0u) {
+            int slot = atomicAdd(ovf_count, 1);
+            if (slot < ovf_cap) ovf_rows[slot] = g;
+            labels[g] = -1;
+          } else {
+            labels[g] = (int)(kk & ~keep);
+          }
+        }
+      }
     }
   }
   my_inertia = wave_sum(my_inertia);
   if (lane == 0 && inertia) atomicAdd(inertia, my_inertia);
+  // drain the ring's surplus prefetch before the LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -317,26 +383,33 @@ __global__ void __launch_bounds__(256) band_select_rows_kernel(
     const float* __restrict__ xn, const long long* __restrict__ rows, const int* __restrict__ count,
     int* __restrict__ labels, long long cap, int d_pad, int k, float delta, RngKey key,
     long long row_offset, int idx_bits) {
+  (void)cn;
   __shared__ float xs[4][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long slot = (long long)blockIdx.x * 4 + w;
   long long cnt = min((long long)*count, cap);
   if (slot >= cnt) return;
   const long long r = rows[slot];
+  const int cpr = d_pad / 8 + 2;   // chunk-major operand (see estep_kernel)
   for (int c = lane; c < d_pad; c += 64) xs[w][c] = bf16_to_f32(X[(size_t)r * d_pad + c]);
   __builtin_amdgcn_wave_barrier();
-  float mn = __builtin_inff();
-  // pass 1: min
-  for (int j = lane; j < k; j += 64) {
-    const uint16_t* cr = C + (size_t)j * d_pad;
+  // D'(j) = ||c_j||^2 - 2 x.c_j from the same bf16 operands the MFMA used
+  auto dist = [&](int j) -> float {
+    const uint16_t* base = C + ((size_t)(j >> 6) * cpr * 64 + (j & 63)) * 8;
     float s = 0.f;
-    for (int c = 0; c < d_pad; c += 2) {
-      uint32_t v = *reinterpret_cast<const uint32_t*>(cr + c);
-      s += xs[w][c] * __uint_as_float(v << 16) + xs[w][c + 1] * __uint_as_float(v & 0xFFFF0000u);
+    for (int ch = 0; ch < d_pad / 8; ++ch) {
+      uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)ch * 512);
+      const float* xv = &xs[w][ch * 8];
+      s += xv[0] * __uint_as_float(v.x << 16) + xv[1] * __uint_as_float(v.x & 0xFFFF0000u);
+      s += xv[2] * __uint_as_float(v.y << 16) + xv[3] * __uint_as_float(v.y & 0xFFFF0000u);
+      s += xv[4] * __uint_as_float(v.z << 16) + xv[5] * __uint_as_float(v.z & 0xFFFF0000u);
+      s += xv[6] * __uint_as_float(v.w << 16) + xv[7] * __uint_as_float(v.w & 0xFFFF0000u);
     }
-    float dv = cn[j] - 2.0f * s;
-    mn = fminf(mn, dv);
-  }
+    uint32_t nv = *reinterpret_cast<const uint32_t*>(base + (size_t)(d_pad / 8) * 512);
+    return s + __uint_as_float(nv << 16) + __uint_as_float(nv & 0xFFFF0000u);
+  };
+  float mn = __builtin_inff();
+  for (int j = lane; j < k; j += 64) mn = fminf(mn, dist(j));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
   const float thr = mn + delta;
@@ -345,13 +418,7 @@ __global__ void __launch_bounds__(256) band_select_rows_kernel(
   int nc = 0;
   uint32_t am = 0xFFFFFFFFu;
   for (int j = lane; j < k; j += 64) {
-    const uint16_t* cr = C + (size_t)j * d_pad;
-    float s = 0.f;
-    for (int c = 0; c < d_pad; c += 2) {
-      uint32_t v = *reinterpret_cast<const uint32_t*>(cr + c);
-      s += xs[w][c] * __uint_as_float(v << 16) + xs[w][c + 1] * __uint_as_float(v & 0xFFFF0000u);
-    }
-    float dv = cn[j] - 2.0f * s;
+    float dv = dist(j);
     if (dv == mn) am = min(am, (uint32_t)j);
     if (dv <= thr) {
       ++nc;
@@ -609,9 +676,15 @@ __global__ void __launch_bounds__(256) centroid_finalize_kernel(
   const int tid = threadIdx.x;
   __shared__ double red[4];
   __shared__ float redf[4];
+  // chunk-major E-step operand (see estep_kernel): -2 c, then [hi, mid, lo]
+  // of ||bf16(c)||^2 in the augmented chunk, zeros after
+  const int cpr = d_pad / 8 + 2;
+  uint16_t* Cb = C_bf16 + (size_t)(j >> 6) * cpr * 512 + (size_t)(j & 63) * 8;
+  auto at = [&](int c) -> uint16_t& { return Cb[(size_t)(c >> 3) * 512 + (c & 7)]; };
   if (j >= k) {
-    for (int c = tid; c < d_pad; c += 256) C_bf16[(size_t)j * d_pad + c] = 0;
-    if (tid == 0) cn[j] = kBig;
+    for (int c = tid; c < d_pad + 16; c += 256) at(c) = 0;
+    __syncthreads();
+    if (tid == 0) { at(d_pad) = f32_to_bf16_rne(kBig); cn[j] = kBig; }
     return;
   }
   const double cntv = packed[(size_t)k * d + j];
@@ -628,19 +701,29 @@ __global__ void __launch_bounds__(256) centroid_finalize_kernel(
       C_new[(size_t)j * d + c] = v;
       double df = (double)v - (double)old;
       sh += df * df;
-      hb = f32_to_bf16_rne(v);
-      float hv = bf16_to_f32(hb);
+      uint16_t h = f32_to_bf16_rne(v);
+      float hv = bf16_to_f32(h);
       nn += hv * hv;
+      hb = f32_to_bf16_rne(-2.0f * hv);   // exact: scaling by -2
     }
-    C_bf16[(size_t)j * d_pad + c] = hb;
+    at(c) = hb;
   }
+  for (int c = d_pad + 3 + tid; c < d_pad + 16; c += 256) at(c) = 0;
   sh = wave_sum(sh);
   nn = wave_sum(nn);
   if ((tid & 63) == 0) { red[tid >> 6] = sh; redf[tid >> 6] = nn; }
   __syncthreads();
   if (tid == 0) {
     atomicAdd(shift, red[0] + red[1] + red[2] + red[3]);
-    cn[j] = redf[0] + redf[1] + redf[2] + redf[3];
+    float t = redf[0] + redf[1] + redf[2] + redf[3];
+    cn[j] = t;
+    uint16_t hi = f32_to_bf16_rne(t);
+    float r1 = t - bf16_to_f32(hi);
+    uint16_t mid = f32_to_bf16_rne(r1);
+    uint16_t lo = f32_to_bf16_rne(r1 - bf16_to_f32(mid));
+    at(d_pad) = hi;
+    at(d_pad + 1) = mid;
+    at(d_pad + 2) = lo;
   }
 }
 
@@ -714,25 +797,42 @@ static int idx_bits_for(int k_pad) {
   return b;
 }
 
+static int estep_dbg() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("SQ_ESTEP_DBG"); v = e ? atoi(e) : 0; }
+  return v;
+}
+
 template <int KS, int NW>
 static int launch_estep(const void* X, const void* C, const void* cn, const void* xn, void* labels,
                         void* mind, void* ovf_rows, void* ovf_count, void* inertia, long long n,
                         int k, int k_pad, float delta, RngKey key, long long row_offset,
                         int ovf_cap, hipStream_t st) {
-  constexpr int DP = KS * 16;
-  size_t lds = 2 * (size_t)kBN * DP * 2 + (size_t)k_pad * 4;
+  size_t lds = 2 * (size_t)kBN * (KS + 1) * 16 * 2;   // two chunk-major tiles
   auto kern = estep_kernel<KS, NW>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
+  // persistent grid: every resident workgroup slot once (blocks are strided)
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NW * 64, lds);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
   long long rows_per_wg = NW * 32;
-  unsigned grid = (unsigned)((n + rows_per_wg - 1) / rows_per_wg);
+  long long nblk = (n + rows_per_wg - 1) / rows_per_wg;
+  static int persist = -1;
+  if (persist < 0) { const char* e = getenv("SQ_ESTEP_PERSIST"); persist = e ? atoi(e) : 1; }
+  unsigned grid = (unsigned)(nblk < resident || !persist ? nblk : resident);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const uint16_t*)X,
                      (const uint16_t*)C, (const float*)cn, (const float*)xn, (int*)labels,
                      (float*)mind, (long long*)ovf_rows, (int*)ovf_count, (double*)inertia, n, k,
-                     k_pad, delta, key, row_offset, ovf_cap, idx_bits_for(k_pad));
+                     k_pad, delta, key, row_offset, ovf_cap, idx_bits_for(k_pad), estep_dbg());
   return (int)hipGetLastError();
 }
 
@@ -747,13 +847,16 @@ int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn,
   if (n <= 0) return 0;
   if (split) return (int)hipErrorInvalidValue;              // bf16x2 uses the generic path
   if (k_pad % kBN != 0 || k_pad > 32768 || k > k_pad) return (int)hipErrorInvalidValue;
-  if ((size_t)k_pad * 4 + 2 * (size_t)kBN * d * 2 > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (2 * (size_t)kBN * (d + 16) * 2 > 160 * 1024) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   hipStream_t st = (hipStream_t)stream;
   float dl = (float)delta;
-  int nw = 4;
+  // 8 waves (2 per SIMD) share each staged centroid tile: half the LDS-DMA
+  // issue per row of the 4-wave layout (measured 5.70 vs 6.18 ms, 10M x 256,
+  // k = 1024); SQ_ESTEP_NW=4 selects the 4-wave layout.
+  int nw = 8;
   const char* env = getenv("SQ_ESTEP_NW");
-  if (env && env[0] == '8') nw = 8;
+  if (env && env[0] == '4') nw = 4;
 #define ESTEP_CASE(KS)                                                                           \
   case KS * 16:                                                                                  \
     return nw == 8 ? launch_estep<KS, 8>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count,        \

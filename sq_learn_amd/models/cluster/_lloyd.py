@@ -97,7 +97,7 @@ class LloydEngine:
         self.shift = torch.zeros(1, dtype=torch.float64, device=dev)
         self.C = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
         self.C_new = torch.zeros_like(self.C)
-        self.C_bf16 = torch.zeros((self.k_pad, self.d_pad), dtype=torch.bfloat16, device=dev)
+        self.C_bf16 = torch.zeros(K.operand_shape(self.k_pad, self.d_pad), dtype=torch.bfloat16, device=dev)
         self.cn = torch.full((self.k_pad,), K.BIG, dtype=torch.float32, device=dev)
         self.scalars = torch.zeros(3, dtype=torch.float64, device=dev)
         self.weights = (self.sample_weight.to(torch.float32).contiguous()

@@ -429,6 +429,8 @@ class QPCA(_BasePCA):
                            faster_measure_increment, check_sv_uniform_distribution=False):
         """Theorem 11 (``_qPCA.py:1025-1068``)."""
         if theta == 0:
+            if not hasattr(self, "est_theta"):
+                raise ValueError("theta_major must be > 0 (or fit with theta_estimate=True)")
             theta = self.est_theta
         est = self._sv_estimates(eps)
         mask = est >= theta

@@ -8,6 +8,7 @@ each op (tests, the CPU oracle, gloo multi-process tests).
 """
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -27,6 +28,13 @@ def _load():
             return _mod
         from .. import _build
         try:
+            variant = os.environ.get("SQ_NATIVE_VARIANT")
+            if variant:
+                # kernel-tuning experiments: a separately built extension
+                spec = importlib.util.spec_from_file_location("sq_learn_amd._C", variant)
+                _mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(_mod)
+                return _mod
             if os.environ.get("SQ_NO_AUTOBUILD", "0") != "1" and _build.needs_build():
                 _build.build()
             _mod = importlib.import_module("sq_learn_amd._C")

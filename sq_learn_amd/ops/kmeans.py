@@ -142,9 +142,9 @@ def estep_native(Xb, C_bf16, cn, xn, k, delta, key: RngKey, row_offset, buf: ESt
                  stream=None):
     """Fused MFMA E-step + device-driven overflow fallback (no host sync)."""
     n, d_pad = Xb.shape
-    k_pad = C_bf16.shape[0]
+    k_pad = C_bf16.shape[0] * 64
     assert Xb.dtype == torch.bfloat16 and C_bf16.dtype == torch.bfloat16
-    assert C_bf16.shape[1] == d_pad and d_pad in FAST_D and k_pad % 64 == 0
+    assert tuple(C_bf16.shape[1:]) == (d_pad // 8 + 2, 64, 8) and d_pad in FAST_D
     assert Xb.is_contiguous() and C_bf16.is_contiguous() and cn.is_contiguous()
     st = stream if stream is not None else nat.stream_handle(Xb.device)
     m = nat.native()
@@ -220,21 +220,53 @@ def pack_stats_native(sums, counts, inertia, packed, k, d):
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
                              empty_policy=0):
-    k_pad = C_bf16.shape[0]
+    k_pad = C_bf16.shape[0] * 64
     nat.native().centroid_finalize(packed.data_ptr(), C_old.data_ptr(), C_new.data_ptr(),
                                    C_bf16.data_ptr(), 0, cn.data_ptr(), shift.data_ptr(), k, d,
                                    k_pad, float(noise_b), key.k0, key.k1, key.s0, key.s1,
                                    int(empty_policy), nat.stream_handle(packed.device))
 
 
+def operand_shape(k_pad, d_pad):
+    """Shape of the chunk-major E-step centroid operand (csrc/kmeans.hip,
+    ``estep_kernel``): [tile][16-B chunk][centroid in tile][8 bf16]."""
+    return (k_pad // 64, d_pad // 8 + 2, 64, 8)
+
+
+def _split3_bf16(v):
+    hi = v.to(torch.bfloat16)
+    r = v - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return hi, mid, lo
+
+
 def centers_to_bf16(C, k_pad, d_pad):
-    """Padded bf16 copy of the centroids and fp32 ||c_bf16||^2 (BIG on pads)."""
+    """E-step operand of the centroids and fp32 ||bf16(c)||^2 (BIG on pads).
+
+    The operand holds -2 bf16(c) chunk-major plus an augmented chunk with the
+    3-way bf16 split of ||bf16(c)||^2 (see ``operand_shape``), exactly what
+    ``centroid_finalize`` writes on the device.
+    """
     k, d = C.shape
-    Cb = torch.zeros((k_pad, d_pad), dtype=torch.bfloat16, device=C.device)
-    Cb[:k, :d] = C.to(torch.bfloat16)
+    cb = torch.zeros((k_pad, d_pad + 16), dtype=torch.bfloat16, device=C.device)
+    h = C.to(torch.bfloat16)
+    cb[:k, :d] = (-2.0 * h.float()).to(torch.bfloat16)
     cn = torch.full((k_pad,), BIG, dtype=torch.float32, device=C.device)
-    cn[:k] = (Cb[:k].float() ** 2).sum(1)
-    return Cb, cn
+    cn[:k] = (h.float() ** 2).sum(1)
+    hi, mid, lo = _split3_bf16(cn)
+    cb[:, d_pad] = hi
+    cb[:k, d_pad + 1] = mid[:k]
+    cb[:k, d_pad + 2] = lo[:k]
+    op = cb.view(k_pad // 64, 64, d_pad // 8 + 2, 8).permute(0, 2, 1, 3).contiguous()
+    return op, cn
+
+
+def centers_from_operand(op, k, d):
+    """Inverse of ``centers_to_bf16``: the bf16-rounded centroids [k, d]."""
+    nt, cpr = op.shape[0], op.shape[1]
+    rows = op.permute(0, 2, 1, 3).reshape(nt * 64, cpr * 8)
+    return (rows[:k, :d].float() * -0.5).to(torch.bfloat16)
 
 
 def centroid_sums_torch(X, labels, k, weights=None, acc_dtype=torch.float64):

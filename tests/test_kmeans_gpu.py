@@ -34,7 +34,7 @@ def test_estep_exact_matches_fp64(cuda, d, k):
     torch.cuda.synchronize()
     # fp64 reference on the bf16-rounded operands
     Xr = Xb[:, :d].double()
-    Cr = Cb[:k, :d].double()
+    Cr = K.centers_from_operand(Cb, k, d).double()
     D = K.distances_torch(Xr, Cr)
     ref = D.argmin(1)
     got = lab.cpu().long()
@@ -50,6 +50,41 @@ def test_estep_exact_matches_fp64(cuda, d, k):
     assert torch.allclose(mind.cpu().double(), mr, rtol=2e-3, atol=1e-2)
     # inertia accumulator
     assert abs(buf.inertia.item() - mind.double().sum().item()) < 1e-3 * mind.double().sum().item()
+
+
+@pytest.mark.parametrize("d,k", [(32, 192), (256, 1024)])
+def test_estep_persistent_many_blocks(cuda, d, k):
+    """n far above the resident grid: every workgroup walks many row blocks
+    (continuous tile ring across blocks, early next-block X loads)."""
+    n = 300_001
+    g = torch.Generator(device=cuda).manual_seed(11)
+    C = torch.randn(k, d, device=cuda, generator=g) * 3
+    lab0 = torch.randint(0, k, (n,), device=cuda, generator=g)
+    dp, kp = K.pad_features(d), K.pad_clusters(k)
+    Xb = torch.zeros(n, dp, dtype=torch.bfloat16, device=cuda)
+    Xb[:, :d] = (C[lab0] + torch.randn(n, d, device=cuda, generator=g)).to(torch.bfloat16)
+    Cb, cn = K.centers_to_bf16(C, kp, dp)
+    xn = L.row_norms_sq(Xb)
+    buf = K.EStepBuffers(n, cuda)
+    key = RngKey(2, "band_select", 0)
+    lab, mind = K.estep_native(Xb, Cb, cn, xn, k, 0.0, key, 0, buf)
+    torch.cuda.synchronize()
+    Cr = K.centers_from_operand(Cb, k, d).double()
+    ok = 0
+    for s0 in range(0, n, 65536):
+        xr = Xb[s0:s0 + 65536, :d].double()
+        D = (xr * xr).sum(1, keepdim=True) + (Cr * Cr).sum(1)[None] - 2 * xr @ Cr.T
+        got = lab[s0:s0 + 65536].long()
+        ref = D.argmin(1)
+        agree = got == ref
+        ok += int(agree.sum())
+        dg = D.gather(1, got.clamp(min=0)[:, None])[:, 0]
+        dr = D.min(1).values
+        assert (got >= 0).all()
+        assert torch.all((dg - dr)[~agree] <= 1e-3 * dr[~agree].abs() + 1e-2)
+        assert torch.allclose(mind[s0:s0 + 65536].double(), dr, rtol=2e-3, atol=1e-2)
+    assert ok / n > 0.999
+    assert abs(buf.inertia.item() - mind.double().sum().item()) < 1e-4 * mind.double().sum().item()
 
 
 def test_estep_band_semantics(cuda):
@@ -68,7 +103,7 @@ def test_estep_band_semantics(cuda):
     key = RngKey(7, "band_select", 0)
     lab, mind = K.estep_native(Xg, Cb.to(cuda), cn.to(cuda), xn, k, delta, key, 0, buf)
     torch.cuda.synchronize()
-    D = K.distances_torch(Xb.double(), Cb[:k].double())
+    D = K.distances_torch(Xb.double(), K.centers_from_operand(Cb, k, d).double())
     mn = D.min(1).values
     got = lab.cpu().long()
     assert (got >= 0).all() and (got < k).all()
@@ -134,7 +169,7 @@ def test_finalize_noise_and_shift(cuda):
     Cold = torch.randn(k, d, dtype=torch.float32, device=cuda)
     Cnew = torch.empty_like(Cold)
     kp, dp = K.pad_clusters(k), K.pad_features(d)
-    Cb = torch.empty(kp, dp, dtype=torch.bfloat16, device=cuda)
+    Cb = torch.full(K.operand_shape(kp, dp), 7.0, dtype=torch.bfloat16, device=cuda)
     cn = torch.empty(kp, dtype=torch.float32, device=cuda)
     shift = torch.zeros(1, dtype=torch.float64, device=cuda)
     b = 0.05
@@ -145,8 +180,18 @@ def test_finalize_noise_and_shift(cuda):
     assert diff.abs().max().item() <= b + 1e-5
     assert diff.abs().max().item() > 0.5 * b
     assert abs(shift.item() - ((Cnew.double() - Cold.double()) ** 2).sum().item()) < 1e-3
-    assert torch.allclose(cn[:k], (Cb[:k].float() ** 2).sum(1), rtol=1e-5)
+    Ch = K.centers_from_operand(Cb, k, d)
+    assert torch.equal(Ch, Cnew.to(torch.bfloat16))
+    assert torch.allclose(cn[:k], (Ch.float() ** 2).sum(1), rtol=1e-5)
     assert (cn[k:] > 1e37).all()
+    # the device-written E-step operand equals the host-built one bit for bit
+    # (norm split may differ in the last bit of lo via the fp32 sum order)
+    ref_op, _ = K.centers_to_bf16(Cnew, kp, dp)
+    body = (slice(None), slice(0, dp // 8))
+    assert torch.equal(Cb[body], ref_op[body])
+    nb = Cb[:, dp // 8].permute(0, 1, 2).reshape(kp, 8).float()
+    assert torch.allclose(nb[:k, :3].sum(1), cn[:k], rtol=1e-6)
+    assert (nb[:, 3:] == 0).all() and (Cb[:, dp // 8 + 1] == 0).all()
 
 
 def test_ipe_estep_kernel(cuda):
