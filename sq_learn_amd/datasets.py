@@ -1,0 +1,3 @@
+"""Reference-layout import path (``sklearn.datasets``): synthetic generators."""
+from .utils.datasets import (make_blobs, make_blobs_device, make_classification,  # noqa: F401
+                             make_low_rank_device, make_low_rank_matrix)

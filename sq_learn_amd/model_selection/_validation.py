@@ -1,0 +1,207 @@
+"""``cross_validate`` / ``cross_val_score`` / ``cross_val_predict`` and a small
+``GridSearchCV`` (reference ``model_selection/_validation.py:47-280``,
+``_search.py``).
+
+The reference fans folds out over joblib worker processes
+(``_validation.py:248``).  Here a fold's fit already fills the GPU (one
+process per GPU, data resident in HBM), so folds run sequentially in this
+process; ``n_jobs`` is accepted for API compatibility and ignored.  Scoring
+strings cover the metrics this framework implements.
+"""
+
+import itertools
+import time
+import warnings
+
+import numpy as np
+
+from ..base import clone, is_classifier
+from ..exceptions import FitFailedWarning
+from ..utils import metrics as M
+from ._split import _safe_index, check_cv
+
+_SCORERS = {
+    "accuracy": (M.accuracy_score, 1.0, "predict"),
+    "r2": (M.r2_score, 1.0, "predict"),
+    "neg_mean_squared_error": (M.mean_squared_error, -1.0, "predict"),
+    "adjusted_rand_score": (M.adjusted_rand_score, 1.0, "predict"),
+}
+
+
+def get_scorer(scoring):
+    if scoring is None:
+        return lambda est, X, y: est.score(X, y) if y is not None else est.score(X)
+    if callable(scoring):
+        return scoring
+    if scoring not in _SCORERS:
+        raise ValueError(f"{scoring!r} is not a valid scoring value. Valid options are "
+                         f"{sorted(_SCORERS)}")
+    fn, sign, method = _SCORERS[scoring]
+
+    def scorer(est, X, y):
+        return sign * fn(y, getattr(est, method)(X))
+    return scorer
+
+
+def _fit_and_score(est, X, y, train, test, scorers, fit_params, return_train_score,
+                   error_score):
+    Xtr, Xte = _safe_index(X, train), _safe_index(X, test)
+    ytr, yte = _safe_index(y, train), _safe_index(y, test)
+    t0 = time.perf_counter()
+    try:
+        if ytr is None:
+            est.fit(Xtr, **fit_params)
+        else:
+            est.fit(Xtr, ytr, **fit_params)
+    except Exception as e:
+        if error_score == "raise":
+            raise
+        warnings.warn(f"Estimator fit failed. The score on this train-test partition will be "
+                      f"set to {error_score}. Details: {e!r}", FitFailedWarning)
+        nan = {k: error_score for k in scorers}
+        return {"fit_time": time.perf_counter() - t0, "score_time": 0.0, "test": nan,
+                "train": dict(nan) if return_train_score else None, "estimator": est}
+    fit_time = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    test_scores = {k: float(s(est, Xte, yte)) for k, s in scorers.items()}
+    score_time = time.perf_counter() - t1
+    train_scores = ({k: float(s(est, Xtr, ytr)) for k, s in scorers.items()}
+                    if return_train_score else None)
+    return {"fit_time": fit_time, "score_time": score_time, "test": test_scores,
+            "train": train_scores, "estimator": est}
+
+
+def cross_validate(estimator, X, y=None, *, groups=None, scoring=None, cv=None, n_jobs=None,
+                   verbose=0, fit_params=None, pre_dispatch="2*n_jobs", return_train_score=False,
+                   return_estimator=False, error_score=np.nan):
+    """Evaluate metric(s) by cross-validation (reference ``_validation.py:47``)."""
+    cv = check_cv(cv, y, classifier=is_classifier(estimator))
+    if scoring is None or callable(scoring) or isinstance(scoring, str):
+        scorers = {"score": get_scorer(scoring)}
+    elif isinstance(scoring, dict):
+        scorers = {k: get_scorer(v) for k, v in scoring.items()}
+    else:
+        scorers = {s: get_scorer(s) for s in scoring}
+    results = []
+    for train, test in cv.split(X, y, groups):
+        results.append(_fit_and_score(clone(estimator), X, y, train, test, scorers,
+                                      fit_params or {}, return_train_score, error_score))
+    out = {"fit_time": np.array([r["fit_time"] for r in results]),
+           "score_time": np.array([r["score_time"] for r in results])}
+    if return_estimator:
+        out["estimator"] = [r["estimator"] for r in results]
+    for k in scorers:
+        name = "test_score" if list(scorers) == ["score"] else f"test_{k}"
+        out[name] = np.array([r["test"][k] for r in results])
+        if return_train_score:
+            tname = "train_score" if list(scorers) == ["score"] else f"train_{k}"
+            out[tname] = np.array([r["train"][k] for r in results])
+    return out
+
+
+def cross_val_score(estimator, X, y=None, *, groups=None, scoring=None, cv=None, n_jobs=None,
+                    verbose=0, fit_params=None, pre_dispatch="2*n_jobs", error_score=np.nan):
+    r = cross_validate(estimator, X, y, groups=groups, scoring=scoring, cv=cv,
+                       fit_params=fit_params, error_score=error_score)
+    return r["test_score"]
+
+
+def cross_val_predict(estimator, X, y=None, *, groups=None, cv=None, n_jobs=None, verbose=0,
+                      fit_params=None, method="predict"):
+    cv = check_cv(cv, y, classifier=is_classifier(estimator))
+    n = len(X) if not hasattr(X, "shape") else X.shape[0]
+    preds = None
+    for train, test in cv.split(X, y, groups):
+        est = clone(estimator)
+        ytr = _safe_index(y, train)
+        est.fit(_safe_index(X, train), ytr, **(fit_params or {})) if ytr is not None else \
+            est.fit(_safe_index(X, train), **(fit_params or {}))
+        p = np.asarray(getattr(est, method)(_safe_index(X, test)))
+        if preds is None:
+            preds = np.empty((n,) + p.shape[1:], dtype=p.dtype)
+        preds[test] = p
+    return preds
+
+
+class ParameterGrid:
+    """Cartesian product of parameter lists (reference ``_search.py:49``)."""
+
+    def __init__(self, param_grid):
+        if isinstance(param_grid, dict):
+            param_grid = [param_grid]
+        self.param_grid = param_grid
+
+    def __iter__(self):
+        for p in self.param_grid:
+            items = sorted(p.items())
+            if not items:
+                yield {}
+                continue
+            keys, values = zip(*items)
+            for v in itertools.product(*values):
+                yield dict(zip(keys, v))
+
+    def __len__(self):
+        total = 0
+        for p in self.param_grid:
+            n = 1
+            for v in p.values():
+                n *= len(v)
+            total += n
+        return total
+
+
+class GridSearchCV:
+    """Exhaustive search over a parameter grid, refit on the best."""
+
+    def __init__(self, estimator, param_grid, *, scoring=None, cv=None, refit=True,
+                 return_train_score=False, error_score=np.nan, n_jobs=None, verbose=0):
+        self.estimator = estimator
+        self.param_grid = param_grid
+        self.scoring = scoring
+        self.cv = cv
+        self.refit = refit
+        self.return_train_score = return_train_score
+        self.error_score = error_score
+        self.n_jobs = n_jobs
+        self.verbose = verbose
+
+    def fit(self, X, y=None, **fit_params):
+        cands = list(ParameterGrid(self.param_grid))
+        means, stds, all_scores = [], [], []
+        for params in cands:
+            est = clone(self.estimator).set_params(**params)
+            r = cross_validate(est, X, y, scoring=self.scoring, cv=self.cv, fit_params=fit_params,
+                               error_score=self.error_score,
+                               return_train_score=self.return_train_score)
+            s = r["test_score"]
+            all_scores.append(s)
+            means.append(float(np.mean(s)))
+            stds.append(float(np.std(s)))
+        means = np.asarray(means)
+        order = np.argsort(-np.nan_to_num(means, nan=-np.inf), kind="stable")
+        ranks = np.empty(len(cands), dtype=int)
+        ranks[order] = np.arange(1, len(cands) + 1)
+        self.cv_results_ = {"params": cands, "mean_test_score": means,
+                            "std_test_score": np.asarray(stds), "rank_test_score": ranks}
+        for i in range(len(all_scores[0]) if all_scores else 0):
+            self.cv_results_[f"split{i}_test_score"] = np.array([s[i] for s in all_scores])
+        self.best_index_ = int(order[0])
+        self.best_params_ = cands[self.best_index_]
+        self.best_score_ = float(means[self.best_index_])
+        if self.refit:
+            self.best_estimator_ = clone(self.estimator).set_params(**self.best_params_)
+            if y is None:
+                self.best_estimator_.fit(X, **fit_params)
+            else:
+                self.best_estimator_.fit(X, y, **fit_params)
+        return self
+
+    def predict(self, X):
+        return self.best_estimator_.predict(X)
+
+    def score(self, X, y=None):
+        return get_scorer(self.scoring)(self.best_estimator_, X, y)
+
+    def transform(self, X):
+        return self.best_estimator_.transform(X)

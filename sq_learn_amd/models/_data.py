@@ -175,3 +175,12 @@ def gather_full(data: Data):
     if data.comm.world_size == 1:
         return data.X
     return torch.cat(data.comm.all_gather_varlen(data.X), 0)
+
+
+def check_n_features(est, data):
+    """Raise like the reference's ``_check_n_features(reset=False)``."""
+    n_in = getattr(est, "n_features_in_", None)
+    if n_in is not None and data.d != n_in:
+        raise ValueError(f"X has {data.d} features, but {type(est).__name__} is expecting "
+                         f"{n_in} features as input.")
+    return data

@@ -37,7 +37,7 @@ from ...utils.validation import check_is_fitted, check_random_state, seed_from_r
 from ...utils import tracing
 from ...runtime.device import to_numpy
 from ..._config import get_config
-from .._data import as_data, global_mean_var, prelude_stats
+from .._data import as_data, check_n_features, global_mean_var, prelude_stats
 from ._init import kmeans_plusplus, random_init
 from ._lloyd import LloydEngine
 from ...ops import kmeans as K
@@ -295,7 +295,7 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
     def transform(self, X):
         """Euclidean distances to the centres (classical path, like the reference)."""
         check_is_fitted(self)
-        data = as_data(X, device=self.device)
+        data = check_n_features(self, as_data(X, device=self.device))
         C = torch.as_tensor(self.cluster_centers_).to(data.device)
         Xf = data.X.double() if data.device.type == "cpu" else data.X.float()
         D = K.distances_torch(Xf, C.to(Xf.dtype))

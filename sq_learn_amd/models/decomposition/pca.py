@@ -162,9 +162,11 @@ class TruncatedSVD(TransformerMixin, BaseEstimator):
             U, S, Vt = res.U_local, res.S, res.Vt
         self.components_ = Vt
         X_t = U * torch.as_tensor(S, dtype=U.dtype, device=U.device)
-        Xn = data.X.double()
-        self.explained_variance_ = to_numpy(X_t.double().var(0, unbiased=False))
-        full_var = float(Xn.var(0, unbiased=False).sum())
+        # variances over all shards (one collective each)
+        from .._data import Data
+        tdata = Data(X_t.double(), data.n_global, data.row_offset, data.comm, data.source_kind)
+        self.explained_variance_ = to_numpy(global_mean_var(tdata)[1])
+        full_var = float(global_mean_var(data)[1].sum())
         self.explained_variance_ratio_ = self.explained_variance_ / full_var
         self.singular_values_ = S
         return _as_out(X_t, data.source_kind)
@@ -172,6 +174,9 @@ class TruncatedSVD(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         data = as_data(X, device=self.device)
+        if data.d != self.n_features_in_:
+            raise ValueError(f"X has {data.d} features, but TruncatedSVD is expecting "
+                             f"{self.n_features_in_} features as input.")
         out = data.X.double() @ torch.as_tensor(self.components_.T, dtype=torch.float64, device=data.device)
         return _as_out(out, data.source_kind)
 

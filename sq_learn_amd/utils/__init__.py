@@ -1,2 +1,45 @@
 """Numerical / API substrate: validation, extmath, metrics, datasets,
 model selection, tracing, checkpointing."""
+
+
+def all_estimators(type_filter=None):
+    """(name, class) of every public estimator of the framework (reference
+    ``utils/__init__.py:1098``: crawls the package for ``BaseEstimator``
+    subclasses).  ``type_filter``: 'classifier', 'regressor', 'cluster',
+    'transformer' or a list of them."""
+    import importlib
+    import inspect
+    import pkgutil
+
+    import sq_learn_amd
+    from ..base import (BaseEstimator, ClassifierMixin, ClusterMixin, RegressorMixin,
+                        TransformerMixin)
+
+    found = {}
+    for mod in pkgutil.walk_packages(sq_learn_amd.__path__, "sq_learn_amd."):
+        name = mod.name
+        if any(p.startswith("_") for p in name.split(".")[1:]) or ".tests" in name:
+            continue
+        try:
+            m = importlib.import_module(name)
+        except Exception:  # pragma: no cover - optional deps
+            continue
+        for cname, cls in inspect.getmembers(m, inspect.isclass):
+            if (issubclass(cls, BaseEstimator) and cls is not BaseEstimator
+                    and not cname.startswith("_") and cls.__module__.startswith("sq_learn_amd")
+                    and not inspect.isabstract(cls)):
+                found[cls] = cname
+    items = sorted(((n, c) for c, n in found.items()), key=lambda t: (t[0], t[1].__module__))
+    # aliases (qMeans_ = QMeans) collapse to one entry per class
+    seen, out = set(), []
+    for n, c in items:
+        if c in seen:
+            continue
+        seen.add(c)
+        out.append((n, c))
+    if type_filter is None:
+        return out
+    filters = [type_filter] if isinstance(type_filter, str) else list(type_filter)
+    mix = {"classifier": ClassifierMixin, "regressor": RegressorMixin,
+           "cluster": ClusterMixin, "transformer": TransformerMixin}
+    return [(n, c) for n, c in out if any(issubclass(c, mix[f]) for f in filters)]

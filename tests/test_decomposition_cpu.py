@@ -1,0 +1,146 @@
+"""PCA / TruncatedSVD / qPCA on the CPU path (torch fp64) vs scikit-learn and
+the reference's semantics (``_qPCA.py``)."""
+import pickle
+
+import numpy as np
+import pytest
+
+sk_decomp = pytest.importorskip("sklearn.decomposition")
+
+from sq_learn_amd.models.decomposition import PCA, QPCA, TruncatedSVD
+from sq_learn_amd.utils.datasets import make_low_rank_matrix
+from sq_learn_amd.base import clone
+
+
+@pytest.fixture(scope="module")
+def X():
+    rng = np.random.RandomState(0)
+    A = make_low_rank_matrix(400, 30, effective_rank=8, tail_strength=0.2, random_state=0)
+    return A * 10 + rng.randn(1, 30)
+
+
+@pytest.mark.parametrize("solver", ["full", "randomized"])
+@pytest.mark.parametrize("n_components", [5, 0.9])
+def test_pca_matches_sklearn(X, solver, n_components):
+    if solver == "randomized" and not isinstance(n_components, int):
+        pytest.skip("randomized needs an int n_components")
+    ours = PCA(n_components=n_components, svd_solver=solver, random_state=0).fit(X)
+    ref = sk_decomp.PCA(n_components=n_components, svd_solver=solver, random_state=0).fit(X)
+    assert ours.n_components_ == ref.n_components_
+    np.testing.assert_allclose(ours.explained_variance_, ref.explained_variance_, rtol=1e-6)
+    np.testing.assert_allclose(ours.explained_variance_ratio_, ref.explained_variance_ratio_,
+                               rtol=1e-6)
+    np.testing.assert_allclose(ours.singular_values_, ref.singular_values_, rtol=1e-6)
+    # sign conventions differ across sklearn versions (u- vs v-based flip)
+    np.testing.assert_allclose(np.abs(ours.components_), np.abs(ref.components_), atol=1e-6)
+    np.testing.assert_allclose(np.abs(ours.transform(X)), np.abs(ref.transform(X)), atol=1e-6)
+    np.testing.assert_allclose(ours.noise_variance_, ref.noise_variance_, rtol=1e-6)
+
+
+def test_pca_inverse_transform_and_covariance(X):
+    p = PCA(n_components=30).fit(X)
+    np.testing.assert_allclose(p.inverse_transform(p.transform(X)), X, atol=1e-8)
+    ref = sk_decomp.PCA(n_components=8).fit(X)
+    ours = PCA(n_components=8).fit(X)
+    np.testing.assert_allclose(ours.get_covariance(), ref.get_covariance(), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(ours.get_precision(), ref.get_precision(), rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(ours.score(X), ref.score(X), rtol=1e-8)
+
+
+def test_pca_whiten(X):
+    ours = PCA(n_components=5, whiten=True).fit(X)
+    ref = sk_decomp.PCA(n_components=5, whiten=True).fit(X)
+    np.testing.assert_allclose(np.abs(ours.transform(X)), np.abs(ref.transform(X)), atol=1e-6)
+
+
+def test_truncated_svd_matches_sklearn(X):
+    ours = TruncatedSVD(n_components=6, algorithm="randomized", n_iter=7, random_state=0).fit(X)
+    ref = sk_decomp.TruncatedSVD(n_components=6, algorithm="randomized", n_iter=7,
+                                 random_state=0).fit(X)
+    np.testing.assert_allclose(ours.singular_values_, ref.singular_values_, rtol=1e-6)
+    np.testing.assert_allclose(ours.explained_variance_ratio_, ref.explained_variance_ratio_,
+                               rtol=1e-5)
+
+
+def test_qpca_classical_equals_pca(X):
+    q = QPCA(n_components=6, svd_solver="full").fit(X)
+    p = PCA(n_components=6, svd_solver="full").fit(X)
+    np.testing.assert_allclose(q.singular_values_, p.singular_values_, rtol=1e-10)
+    np.testing.assert_allclose(q.components_, p.components_, atol=1e-10)
+    np.testing.assert_allclose(q.transform(X), p.transform(X), atol=1e-8)
+    # reference extras: left singular vectors (k x n), frob norm, muA
+    assert q.left_sv.shape == (6, X.shape[0])
+    assert np.isclose(q.frob_norm, np.linalg.norm(X - X.mean(0)))
+    assert 0 < q.muA <= q.frob_norm + 1e-9
+
+
+def test_qpca_topk_extractors_bounded_noise(X):
+    q = QPCA(n_components=10, svd_solver="full", random_state=3)
+    sv_full = PCA(svd_solver="full").fit(X).singular_values_
+    theta = 0.5 * sv_full[5]
+    q.fit(X, eps=1e-3, theta_major=theta, delta=0.05, estimate_all=True, true_tomography=False)
+    assert q.topk >= 1
+    k = q.topk
+    # singular value estimates are eps-close (relative to muA) to the true ones
+    assert np.all(np.abs(q.estimate_s_values - q.top_k_true_singular_value) <= 2e-3 * q.muA + 1e-9)
+    # Gaussian tomography: the whole matrix error within delta (Frobenius budget)
+    err = np.linalg.norm(np.asarray(q.estimate_right_sv) - q.topk_right_singular_vectors)
+    assert err <= 0.05 + 1e-12
+    assert np.asarray(q.estimate_right_sv).shape == (k, X.shape[1])
+    assert q.estimate_fs_ratio.shape == (k,)
+
+
+def test_qpca_true_tomography_unit_rows(X):
+    q = QPCA(n_components=4, svd_solver="full", random_state=1)
+    theta = 0.5 * PCA(svd_solver="full").fit(X).singular_values_[3]
+    q.fit(X, eps=1e-3, theta_major=theta, delta=0.3, estimate_all=True, true_tomography=True)
+    est = np.asarray(q.estimate_right_sv)
+    # real tomography returns unit-norm rows (reference Q4 semantics)
+    np.testing.assert_allclose(np.linalg.norm(est, axis=1), 1.0, atol=1e-8)
+    # and each row within delta of the true vector with high probability
+    d = np.linalg.norm(est - q.topk_right_singular_vectors, axis=1)
+    assert np.all(d <= 0.3 * 1.5)
+
+
+def test_qpca_theta_estimate_and_retained_variance(X):
+    q = QPCA(n_components=0.8, svd_solver="full", random_state=2)
+    q.fit(X, eps=1e-2, eps_theta=1.0, eta=0.1, p=0.8, theta_estimate=True,
+          quantum_retained_variance=True, theta_major=0.0)
+    assert q.est_theta >= 0
+    assert 0.0 <= q.p_ <= 1.0
+
+
+def test_qpca_quantum_transform_representation(X):
+    q = QPCA(n_components=5, svd_solver="full", random_state=4).fit(X)
+    Y = q.transform(X)
+    r = q.transform(X, classic_transform=False, epsilon_delta=0.1, quantum_representation=True,
+                    norm="est_representation", psi=0, true_tomography=False)
+    A, eps_used, f = r["quantum_representation_results"]
+    assert np.asarray(A).shape == Y.shape
+    assert np.isclose(eps_used, np.sqrt(5) * 0.1)
+    assert f <= eps_used + 1e-12
+
+
+def test_qpca_runtime_comparison_shapes(X):
+    q = QPCA(n_components=5, svd_solver="full", random_state=4)
+    theta = 0.5 * PCA(svd_solver="full").fit(X).singular_values_[4]
+    q.fit(X, eps=1e-2, theta_major=theta, delta=0.1, estimate_all=True, true_tomography=False)
+    qr, cr = q.runtime_comparison(10_000, 100)
+    assert qr.shape == cr.shape == (100, 100)
+    assert np.all(np.isfinite(qr))
+
+
+def test_pickle_and_clone(X):
+    q = QPCA(n_components=3, svd_solver="full").fit(X)
+    q2 = pickle.loads(pickle.dumps(q))
+    np.testing.assert_allclose(q2.transform(X), q.transform(X))
+    c = clone(q)
+    assert c.get_params() == q.get_params()
+    assert not hasattr(c, "components_")
+
+
+def test_fit_kwargs_validation(X):
+    with pytest.raises(TypeError):
+        QPCA(n_components=2).fit(X, not_a_knob=1)
+    with pytest.raises(ValueError):
+        QPCA(n_components=2).fit(X, quantum_retained_variance=True, eps=0.0)
