@@ -20,6 +20,10 @@ __attribute__((weak)) int sq_ae_batch(const void*, const void*, void*, long long
                 unsigned, unsigned long long, void*);
 __attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long, unsigned, unsigned, unsigned, unsigned,
                 unsigned long long, void*);
+// failure.hip
+__attribute__((weak)) int sq_failure_inject(void*, long long, int, double, int, unsigned, unsigned,
+                                            unsigned, unsigned, unsigned, unsigned, unsigned,
+                                            unsigned, long long, void*, void*);
 // kmeans.hip
 __attribute__((weak)) int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn, const void* xn,
                   void* labels, void* mind, void* ovf_rows, void* ovf_count, void* inertia,
@@ -128,6 +132,17 @@ static PyObject* py_band_select(PyObject*, PyObject* a) {
   CHECK(sq_band_select)
   return ret(sq_band_select(P(D), P(rows), P(xn), P(lab), P(mind), m, k, ld, delta, k0, k1, s0, s1,
                             roff, P(st)));
+}
+
+static PyObject* py_failure_inject(PyObject*, PyObject* a) {
+  unsigned long long lab, cnt, st; long long n, roff; int k, R; double p;
+  unsigned k0, k1, s0, s1, t0, t1, u0, u1;
+  if (!PyArg_ParseTuple(a, "KLidiIIIIIIIILKK", &lab, &n, &k, &p, &R, &k0, &k1, &s0, &s1, &t0, &t1,
+                        &u0, &u1, &roff, &cnt, &st))
+    return nullptr;
+  CHECK(sq_failure_inject)
+  return ret(sq_failure_inject(P(lab), n, k, p, R, k0, k1, s0, s1, t0, t1, u0, u1, roff, P(cnt),
+                               P(st)));
 }
 
 static PyObject* py_band_select_rows(PyObject*, PyObject* a) {
@@ -241,6 +256,7 @@ static PyMethodDef methods[] = {
     {"estep_bf16", py_estep_bf16, METH_VARARGS, "fused MFMA distance + delta-band E-step"},
     {"band_select", py_band_select, METH_VARARGS, "delta-band selection over distance rows"},
     {"band_select_rows", py_band_select_rows, METH_VARARGS, "device-driven overflow fallback"},
+    {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},

@@ -32,6 +32,7 @@ from ...runtime.rng import RngKey
 from ...ops import kmeans as K
 from ...ops import linalg as L
 from ...ops.random import trunc_normal_add_
+from ...ops.failure import failure_inject_
 from ...ops import _native as nat
 from ...parallel.comm import Comm
 from ...utils import tracing
@@ -41,7 +42,7 @@ class LloydEngine:
     def __init__(self, X, k, *, delta=0.0, true_distance_estimate=False, intermediate_error=False,
                  true_tomography=False, tomography_kw=None, sample_weight=None, seed=0,
                  comm=None, row_offset=0, gemm_precision="bf16", ipe_Q=13, empty_policy=0,
-                 Xb=None, xn=None):
+                 Xb=None, xn=None, failure_prob=0.0, failure_attempts=1):
         self.X = X
         self.device = X.device
         self.n, self.d = X.shape
@@ -61,6 +62,10 @@ class LloydEngine:
         self.d_pad = K.pad_features(self.d)
         self.restart = 0
         self.it = 0
+        self.failure_prob = float(failure_prob or 0.0)
+        self.failure_attempts = max(1, int(failure_attempts))
+        # [estimations made, corrupted rows] over the engine's lifetime (device)
+        self.failure_counters = torch.zeros(2, dtype=torch.int64, device=X.device)
         gpu = self.device.type == "cuda"
         self.fast = (gpu and gemm_precision == "bf16" and not self.ipe and self.d_pad <= 256
                      and self.k_pad <= 4096)
@@ -129,6 +134,16 @@ class LloydEngine:
 
     def centers(self):
         return self.C
+
+    def checkpoint_tensors(self):
+        """Derived device state that must round-trip bit-exactly on resume
+        (the E-step operand written by ``centroid_finalize``)."""
+        return {"C_bf16": self.C_bf16, "cn": self.cn} if self.fast else {}
+
+    def restore_tensors(self, d):
+        if self.fast and "C_bf16" in d:
+            self.C_bf16.copy_(d["C_bf16"].to(self.device))
+            self.cn.copy_(d["cn"].to(self.device))
 
     # ---------------------------------------------------------- E-step
     def estep(self, C=None):
@@ -267,6 +282,10 @@ class LloydEngine:
     def step(self):
         """One Lloyd iteration; returns (labels, scalars_tensor)."""
         labels, mind, inertia = self.estep()
+        if self.failure_prob > 0:
+            # SURVEY.md §5.3: Bernoulli estimation failures (+ resampling)
+            failure_inject_(labels, self.k, self.failure_prob, self.failure_attempts,
+                            self._key("failure"), self.row_offset, self.failure_counters)
         sc = self.mstep(labels, inertia)
         self.it += 1
         return labels, sc

@@ -38,6 +38,7 @@ from ...utils import tracing
 from ...runtime.device import to_numpy
 from ..._config import get_config
 from .._data import as_data, check_n_features, global_mean_var, prelude_stats
+from ...utils.checkpoint import Checkpointer, rs_state_from_tensors, rs_state_to_tensors
 from ._init import kmeans_plusplus, random_init
 from ._lloyd import LloydEngine
 from ...ops import kmeans as K
@@ -68,7 +69,8 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                  true_tomography=True, stop_when_reached_accuracy=True, multiprocess=False,
                  true_distance_estimate=True, device=None, gemm_precision=None,
                  compute_prelude=True, ipe_Q=None, preserve_norm_tomography=True,
-                 empty_cluster="keep"):
+                 empty_cluster="keep", failure_prob=0.0, failure_policy="ignore",
+                 failure_max_attempts=3, checkpoint_dir=None, checkpoint_every=10):
         self.n_clusters = n_clusters
         self.init = init
         self.n_init = n_init
@@ -92,6 +94,11 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         self.ipe_Q = ipe_Q
         self.preserve_norm_tomography = preserve_norm_tomography
         self.empty_cluster = empty_cluster
+        self.failure_prob = failure_prob
+        self.failure_policy = failure_policy
+        self.failure_max_attempts = failure_max_attempts
+        self.checkpoint_dir = checkpoint_dir
+        self.checkpoint_every = checkpoint_every
 
     # ------------------------------------------------------------ checks
     def _check_params(self, data):
@@ -121,6 +128,12 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             self._n_init = 1
         if self.empty_cluster not in ("keep", "zero"):
             raise ValueError("empty_cluster must be 'keep' or 'zero'")
+        if not 0.0 <= float(self.failure_prob) < 1.0:
+            raise ValueError(f"failure_prob must be in [0, 1), got {self.failure_prob}")
+        if self.failure_policy not in ("ignore", "resample"):
+            raise ValueError("failure_policy must be 'ignore' or 'resample'")
+        if self.failure_policy == "resample" and int(self.failure_max_attempts) < 1:
+            raise ValueError("failure_max_attempts must be >= 1")
 
     def _delta(self):
         return 0.0 if self.delta is None else float(self.delta)
@@ -188,17 +201,59 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                              true_tomography=self.true_tomography, tomography_kw=tomo_kw,
                              sample_weight=sw, seed=seed, comm=comm, row_offset=data.row_offset,
                              gemm_precision=self._precision(), ipe_Q=Q,
-                             empty_policy=0 if self.empty_cluster == "keep" else 1)
+                             empty_policy=0 if self.empty_cluster == "keep" else 1,
+                             failure_prob=float(self.failure_prob),
+                             failure_attempts=(int(self.failure_max_attempts)
+                                               if self.failure_policy == "resample" else 1))
         xn = engine.xn
-        best = None
-        for restart in range(self._n_init):
+        # iteration-level checkpoint / resume
+        ckpt = Checkpointer(self.checkpoint_dir, comm, tag=type(self).__name__,
+                            every=self.checkpoint_every)
+        fingerprint = torch.cat([torch.tensor([float(data.n_global), float(data.d),
+                                               float(self.n_clusters), float(seed % (1 << 52)),
+                                               delta, float(self._n_init)], dtype=torch.float64),
+                                 mean.double().cpu()])
+        resume = ckpt.load()
+        if resume is not None and not torch.equal(resume[0]["fingerprint"], fingerprint):
+            warnings.warn("checkpoint in checkpoint_dir does not match this fit; starting over")
+            resume = None
+        best, start_restart = None, 0
+        if resume is not None:
+            st, loc = resume
+            start_restart = int(st["restart"])
+            if bool(st["has_best"]):
+                best = (loc["best_labels"].to(data.device), float(st["best_inertia"]),
+                        st["best_centers"].to(data.device), int(st["best_n_iter"]))
+            rs_state_from_tensors(rs, st)
+            if comm.rank == 0 and "failure_counters" in st:
+                engine.failure_counters.copy_(st["failure_counters"].to(engine.device))
+            self.resumed_from_ = (start_restart, int(st["it"]))
+        self._ckpt_ctx = dict(ckpt=ckpt, fingerprint=fingerprint, rs=rs)
+        for restart in range(start_restart, self._n_init):
             engine.restart = restart
             engine.it = 0
-            C0 = self._init_centroids(data_c, self.init, rs, xn, mean)
-            labels, inertia, centers, n_iter = self._run_lloyd(engine, C0)
+            if resume is not None and restart == start_restart:
+                st, loc = resume
+                C0 = st["C"].to(data.device)
+                engine.it = int(st["it"])
+                inner = dict(best_inertia=st["r_best_inertia"], best_centers=st["r_best_centers"],
+                             best_labels=loc.get("r_best_labels"), shift=float(st["shift"]),
+                             engine={k[7:]: v for k, v in st.items() if k.startswith("engine_")})
+            else:
+                C0 = self._init_centroids(data_c, self.init, rs, xn, mean)
+                inner = None
+            self._ckpt_ctx["outer_best"] = best
+            labels, inertia, centers, n_iter = self._run_lloyd(engine, C0, resume=inner)
             if best is None or inertia < best[1]:
                 best = (labels, inertia, centers, n_iter)
+        ckpt.clear()
+        del self._ckpt_ctx   # holds the communicator: not estimator state
         labels, inertia, centers, n_iter = best
+        cnt = engine.failure_counters.clone()
+        comm.all_reduce_(cnt)
+        counters = cnt.tolist()
+        self.n_estimations_ = int(counters[0])
+        self.n_failed_rows_ = int(counters[1])
         centers = centers.double() + mean.to(centers.device)
         self.cluster_centers_ = to_numpy(centers)
         self._labels_t = labels
@@ -227,14 +282,44 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         comm.all_reduce_(present, op="max")
         return int(present.sum().item())
 
-    def _run_lloyd(self, engine, C0):
+    def _save_checkpoint(self, engine, it, shift, best_inertia, best_centers, best_labels):
+        ctx = self._ckpt_ctx
+        outer = ctx.get("outer_best")
+        state = dict(fingerprint=ctx["fingerprint"], restart=engine.restart, it=it + 1,
+                     C=engine.centers().double(), shift=float(shift),
+                     r_best_inertia=float(best_inertia), r_best_centers=best_centers.double(),
+                     has_best=outer is not None,
+                     best_inertia=float(outer[1]) if outer is not None else 0.0,
+                     best_centers=(outer[2].double() if outer is not None
+                                   else torch.zeros(1, dtype=torch.float64)),
+                     best_n_iter=int(outer[3]) if outer is not None else 0,
+                     **rs_state_to_tensors(ctx["rs"]))
+        state.update({f"engine_{k}": v for k, v in engine.checkpoint_tensors().items()})
+        cnt = engine.failure_counters.clone()
+        engine.comm.all_reduce_(cnt)   # fit-wide totals, like the attributes
+        state["failure_counters"] = cnt
+        local = dict(r_best_labels=best_labels.to(torch.int32))
+        if outer is not None:
+            local["best_labels"] = outer[0].to(torch.int32)
+        ctx["ckpt"].save(state, local)
+
+    def _run_lloyd(self, engine, C0, resume=None):
         """One restart of the quantum Lloyd loop (``_dmeans.py:594-671``)."""
         engine.set_centers(C0)
         log = tracing.IterationLog(type(self).__name__, self.verbose, engine.comm)
         best_inertia, best_centers, best_labels = None, None, None
         shift = 0.0
-        it = 0
-        for it in range(self.max_iter):
+        first = 0
+        if resume is not None:
+            first = engine.it
+            engine.restore_tensors(resume["engine"])
+            best_inertia = float(resume["best_inertia"])
+            best_centers = resume["best_centers"].to(engine.device).to(engine.centers().dtype)
+            best_labels = resume["best_labels"].to(engine.device)
+            shift = resume["shift"]
+        ckpt = getattr(self, "_ckpt_ctx", {}).get("ckpt")
+        it = first - 1
+        for it in range(first, self.max_iter):
             labels, sc = engine.step()
             vals = sc.tolist()  # the single D2H read of the iteration
             inertia, shift = vals[0], vals[1]
@@ -248,6 +333,9 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                 best_labels = labels.clone()
             if shift <= self._tol:
                 break
+            if ckpt is not None and ckpt.due(it):
+                self._save_checkpoint(engine, it, shift, best_inertia, best_centers, best_labels)
+        it = max(it, first)
         if shift > 0:
             labels, _, inertia_t = engine.estep(best_centers)
             best_labels = labels.clone()

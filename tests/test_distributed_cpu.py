@@ -95,6 +95,41 @@ def _worker(rank, world, port, outdir, case):
             np.testing.assert_allclose(q.singular_values_, qr.singular_values_, rtol=1e-8)
             np.testing.assert_allclose(q.estimate_s_values, qr.estimate_s_values, rtol=1e-12)
             assert abs(q.muA - qr.muA) < 1e-9 * qr.muA
+        elif case == "resume":
+            # sharded fit with failures, crashed mid-fit on every rank, then
+            # resumed from the per-rank checkpoint: identical to an
+            # uninterrupted single-process fit
+            from sq_learn_amd.models.cluster import QMeans
+            from sq_learn_amd.models.cluster._lloyd import LloydEngine
+            kw = dict(n_clusters=5, delta=0.5, true_distance_estimate=False, random_state=2,
+                      n_init=2, max_iter=10, tol=0.0, device="cpu", failure_prob=0.1,
+                      failure_policy="resample", failure_max_attempts=2, checkpoint_every=3)
+            ref = QMeans(**kw).fit(X)
+            ck = os.path.join(outdir, "ck")
+            orig = LloydEngine.step
+            calls = {"n": 0}
+
+            def crashing(self):
+                calls["n"] += 1
+                if calls["n"] > 13:
+                    raise KeyboardInterrupt
+                return orig(self)
+            LloydEngine.step = crashing
+            try:
+                QMeans(checkpoint_dir=ck, **kw).fit(sa)
+                raise AssertionError("expected the simulated crash")
+            except KeyboardInterrupt:
+                pass
+            finally:
+                LloydEngine.step = orig
+            got = QMeans(checkpoint_dir=ck, **kw).fit(sa)
+            assert got.resumed_from_ == (1, 3)
+            np.testing.assert_allclose(got.cluster_centers_, ref.cluster_centers_, rtol=1e-9,
+                                       atol=1e-9)
+            loc = torch.as_tensor(got.labels_.astype(np.int64))
+            full = torch.cat(comm.all_gather_varlen(loc)).numpy()
+            np.testing.assert_array_equal(full, ref.labels_)
+            assert got.n_failed_rows_ > 0
         with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
             f.write("ok")
     except Exception:
@@ -106,7 +141,7 @@ def _worker(rank, world, port, outdir, case):
 
 
 @pytest.mark.parametrize("case,world", [("qmeans", 2), ("qmeans", 3), ("kmeans", 2), ("pca", 2),
-                                        ("ipe", 2)])
+                                        ("ipe", 2), ("resume", 2)])
 def test_sharded_matches_single_process(case, world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, case), nprocs=world, join=True)
