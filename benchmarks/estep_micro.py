@@ -33,8 +33,8 @@ kp, dp = K.pad_clusters(a.k), K.pad_features(a.d)
 Cb, cn = K.centers_to_bf16(C, kp, dp)
 xn = L.row_norms_sq(X)
 buf = K.EStepBuffers(a.n, dev)
-ws = K.ReduceWorkspace(a.n, a.k, dev)
-sums = torch.zeros(a.k, a.d, device=dev)
+ws = K.ReduceWorkspace(a.n, a.k, dev).set_scale(float(X.float().abs().max()), a.n)
+sums = torch.zeros(a.k, a.d, dtype=torch.float64, device=dev)
 cnt = torch.zeros(a.k, dtype=torch.float64, device=dev)
 key = RngKey(1, "band_select", 0)
 K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)

@@ -314,8 +314,10 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
       }
     }
   }
+  // per-wave partial (no float atomics: the launcher sums the partials in a
+  // fixed order, so the inertia is bit-reproducible)
   my_inertia = wave_sum(my_inertia);
-  if (lane == 0 && inertia) atomicAdd(inertia, my_inertia);
+  if (lane == 0) inertia[(size_t)blockIdx.x * NW + wave] = my_inertia;
   // drain the ring's surplus prefetch before the LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -596,19 +598,37 @@ __global__ void __launch_bounds__(256) label_scatter_kernel(const int* __restric
   }
 }
 
+// Deterministic segmented sums: every contribution is quantised to an
+// integer multiple of 2^qexp (x * 2^-qexp rounded in fp32: exact scaling by a
+// power of two, then v_rndne) and accumulated in fp64.  The host picks qexp
+// so that max|x| * n * 2^-qexp <= 2^52: every partial and total sum is then
+// an integer below 2^53, exactly representable, so fp64 addition is exact
+// and therefore associative - the result is independent of the (atomic,
+// arbitrary) order of the permutation and the flushes.  A fit is thus
+// bit-reproducible run to run and across checkpoint/resume, at a rounding
+// of at most 2^qexp / 2 per element (~1e-7 absolute for |x| <= 100 at 10M
+// rows, below bf16/fp32 input precision).
 template <typename T>
 __global__ void __launch_bounds__(512) segment_sum_kernel(
     const T* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
-    const float* __restrict__ w, long long n_sorted, int d, int range,
-    float* __restrict__ sums, double* __restrict__ counts, const int* __restrict__ valid_end) {
+    const float* __restrict__ w, long long n_sorted, int d, int range, float xscale,
+    float wscale, double* __restrict__ sums, double* __restrict__ counts,
+    const int* __restrict__ valid_end) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long long p0 = (long long)blockIdx.x * range;
   const long long p1 = min(min(n_sorted, (long long)*valid_end), p0 + range);
   constexpr int U = 4;
   for (int c0 = lane * 4; c0 < d; c0 += 256) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    double cnt = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, cnt = 0.0;
     int cur = -1;
+    auto flush = [&]() {
+      double* dst = sums + (size_t)cur * d + c0;
+      if (a0 != 0.0) atomicAdd(dst + 0, a0);
+      if (a1 != 0.0 && c0 + 1 < d) atomicAdd(dst + 1, a1);
+      if (a2 != 0.0 && c0 + 2 < d) atomicAdd(dst + 2, a2);
+      if (a3 != 0.0 && c0 + 3 < d) atomicAdd(dst + 3, a3);
+      if (lane == 0 && c0 == 0) atomicAdd(&counts[cur], cnt);
+    };
     for (long long p = p0 + wave; p < p1; p += 8 * U) {
       int rr[U], ll[U];
       float4 v[U];
@@ -628,42 +648,47 @@ __global__ void __launch_bounds__(512) segment_sum_kernel(
       for (int u = 0; u < U; ++u) {
         if (ll[u] < 0) continue;
         if (ll[u] != cur) {
-          if (cur >= 0) {
-            float* dst = sums + (size_t)cur * d + c0;
-            atomicAdd(dst + 0, acc.x);
-            if (c0 + 1 < d) atomicAdd(dst + 1, acc.y);
-            if (c0 + 2 < d) atomicAdd(dst + 2, acc.z);
-            if (c0 + 3 < d) atomicAdd(dst + 3, acc.w);
-            if (lane == 0 && c0 == 0) atomicAdd(&counts[cur], cnt);
-          }
+          if (cur >= 0) flush();
           cur = ll[u];
-          acc = make_float4(0.f, 0.f, 0.f, 0.f);
-          cnt = 0.0;
+          a0 = a1 = a2 = a3 = cnt = 0.0;
         }
-        acc.x += ww[u] * v[u].x; acc.y += ww[u] * v[u].y;
-        acc.z += ww[u] * v[u].z; acc.w += ww[u] * v[u].w;
-        cnt += (double)ww[u];
+        const float s = ww[u] * xscale;   // exact when unweighted (power of 2)
+        a0 += (double)rintf(v[u].x * s);
+        a1 += (double)rintf(v[u].y * s);
+        a2 += (double)rintf(v[u].z * s);
+        a3 += (double)rintf(v[u].w * s);
+        cnt += w ? (double)rintf(ww[u] * wscale) : 1.0;
       }
     }
-    if (cur >= 0) {
-      float* dst = sums + (size_t)cur * d + c0;
-      atomicAdd(dst + 0, acc.x);
-      if (c0 + 1 < d) atomicAdd(dst + 1, acc.y);
-      if (c0 + 2 < d) atomicAdd(dst + 2, acc.z);
-      if (c0 + 3 < d) atomicAdd(dst + 3, acc.w);
-      if (lane == 0 && c0 == 0) atomicAdd(&counts[cur], cnt);
-    }
+    if (cur >= 0) flush();
   }
 }
 
-// packed[0:k*d] = sums (f64), packed[k*d : k*d+k] = counts, packed[k*d+k] = inertia
+// deterministic sum of n doubles (fixed thread order + fixed tree): one WG
+__global__ void __launch_bounds__(256) sum_partials_kernel(const double* __restrict__ part,
+                                                           int n, double* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// packed[0:k*d] = sums (f64), packed[k*d : k*d+k] = counts, packed[k*d+k] = inertia;
+// sums/counts arrive as integer multiples of the quanta xq / wq
 __global__ void __launch_bounds__(256) pack_stats_kernel(
-    const float* __restrict__ sums, const double* __restrict__ counts,
-    const double* __restrict__ inertia, double* __restrict__ packed, int k, int d) {
+    const double* __restrict__ sums, const double* __restrict__ counts,
+    const double* __restrict__ inertia, double* __restrict__ packed, int k, int d, double xq,
+    double wq) {
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   long long kd = (long long)k * d;
-  if (i < kd) packed[i] = (double)sums[i];
-  else if (i < kd + k) packed[i] = counts[i - kd];
+  if (i < kd) packed[i] = (double)sums[i] * xq;
+  else if (i < kd + k) packed[i] = (double)counts[i - kd] * wq;
   else if (i == kd + k) packed[i] = inertia ? inertia[0] : 0.0;
 }
 
@@ -805,9 +830,9 @@ static int estep_dbg() {
 
 template <int KS, int NW>
 static int launch_estep(const void* X, const void* C, const void* cn, const void* xn, void* labels,
-                        void* mind, void* ovf_rows, void* ovf_count, void* inertia, long long n,
-                        int k, int k_pad, float delta, RngKey key, long long row_offset,
-                        int ovf_cap, hipStream_t st) {
+                        void* mind, void* ovf_rows, void* ovf_count, void* inertia,
+                        void* part, int part_cap, long long n, int k, int k_pad, float delta,
+                        RngKey key, long long row_offset, int ovf_cap, hipStream_t st) {
   size_t lds = 2 * (size_t)kBN * (KS + 1) * 16 * 2;   // two chunk-major tiles
   auto kern = estep_kernel<KS, NW>;
   static bool attr_set = false;
@@ -829,23 +854,26 @@ static int launch_estep(const void* X, const void* C, const void* cn, const void
   static int persist = -1;
   if (persist < 0) { const char* e = getenv("SQ_ESTEP_PERSIST"); persist = e ? atoi(e) : 1; }
   unsigned grid = (unsigned)(nblk < resident || !persist ? nblk : resident);
+  if ((long long)grid * NW > part_cap) grid = (unsigned)(part_cap / NW);   // still persistent
+  if (grid == 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const uint16_t*)X,
                      (const uint16_t*)C, (const float*)cn, (const float*)xn, (int*)labels,
-                     (float*)mind, (long long*)ovf_rows, (int*)ovf_count, (double*)inertia, n, k,
+                     (float*)mind, (long long*)ovf_rows, (int*)ovf_count, (double*)part, n, k,
                      k_pad, delta, key, row_offset, ovf_cap, idx_bits_for(k_pad), estep_dbg());
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, (const double*)part,
+                     (int)grid * NW, (double*)inertia);
   return (int)hipGetLastError();
 }
 
 extern "C" {
 
-int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn, const void* xn,
+int sq_estep_bf16(const void* X, const void* C, void* part, const void* cn, const void* xn,
                   void* labels, void* mind, void* ovf_rows, void* ovf_count, void* inertia,
-                  long long n, int d, int k, int k_pad, double delta, int split, unsigned k0,
+                  long long n, int d, int k, int k_pad, double delta, int part_cap, unsigned k0,
                   unsigned k1, unsigned s0, unsigned s1, long long row_offset, int ovf_cap,
                   void* stream) {
-  (void)Clo;
   if (n <= 0) return 0;
-  if (split) return (int)hipErrorInvalidValue;              // bf16x2 uses the generic path
+  if (part_cap < 8) return (int)hipErrorInvalidValue;
   if (k_pad % kBN != 0 || k_pad > 32768 || k > k_pad) return (int)hipErrorInvalidValue;
   if (2 * (size_t)kBN * (d + 16) * 2 > 160 * 1024) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
@@ -860,9 +888,11 @@ int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn,
 #define ESTEP_CASE(KS)                                                                           \
   case KS * 16:                                                                                  \
     return nw == 8 ? launch_estep<KS, 8>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count,        \
-                                         inertia, n, k, k_pad, dl, key, row_offset, ovf_cap, st) \
+                                         inertia, part, part_cap, n, k, k_pad, dl, key,         \
+                                         row_offset, ovf_cap, st)                               \
                    : launch_estep<KS, 4>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count,        \
-                                         inertia, n, k, k_pad, dl, key, row_offset, ovf_cap, st);
+                                         inertia, part, part_cap, n, k, k_pad, dl, key,         \
+                                         row_offset, ovf_cap, st);
   switch (d) {
     ESTEP_CASE(1)
     ESTEP_CASE(2)
@@ -931,10 +961,11 @@ int sq_centroid_accumulate(const void* X, int xdtype, const void* labels, const 
 }
 
 int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void* weights,
-                       void* sums, void* counts, long long n, int d, int k, void* ws_hist,
-                       void* ws_cursor, void* ws_perm, void* stream) {
+                       void* sums, void* counts, long long n, int d, int k, int xexp, int wexp,
+                       void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
   if (n <= 0) return 0;
   if (d % 4 != 0 || k > 16384 || n > 2147483647LL) return (int)hipErrorInvalidValue;
+  if (xexp < -120 || xexp > 120 || wexp < -120 || wexp > 120) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
   (void)hipMemsetAsync(ws_hist, 0, (size_t)k * 4, st);
@@ -949,26 +980,34 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
   // kernel bounds itself with the scanned total (cursor[k-1] after scatter)
   const int range = 2048;
   unsigned grid = (unsigned)((n + range - 1) / range);
+  const float xs = ldexpf(1.0f, -xexp), wsc = ldexpf(1.0f, -wexp);
   if (xdtype == 0)
     hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(grid), dim3(512), 0, st, (const float*)X,
                        (const int*)ws_perm, (const int*)labels, (const float*)weights, n, d, range,
-                       (float*)sums, (double*)counts, (const int*)ws_cursor + (k - 1));
+                       xs, wsc, (double*)sums, (double*)counts, (const int*)ws_cursor + (k - 1));
   else if (xdtype == 2)
     hipLaunchKernelGGL(segment_sum_kernel<uint16_t>, dim3(grid), dim3(512), 0, st,
                        (const uint16_t*)X, (const int*)ws_perm, (const int*)labels,
-                       (const float*)weights, n, d, range, (float*)sums, (double*)counts,
-                       (const int*)ws_cursor + (k - 1));
+                       (const float*)weights, n, d, range, xs, wsc, (double*)sums,
+                       (double*)counts, (const int*)ws_cursor + (k - 1));
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 
 int sq_pack_stats(const void* sums, const void* counts, const void* inertia, void* packed, int k,
-                  int d, void* stream) {
+                  int d, int xexp, int wexp, void* stream) {
   long long tot = (long long)k * d + k + 1;
   hipLaunchKernelGGL(pack_stats_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, (const float*)sums, (const double*)counts,
-                     (const double*)inertia, (double*)packed, k, d);
+                     (hipStream_t)stream, (const double*)sums, (const double*)counts,
+                     (const double*)inertia, (double*)packed, k, d, ldexp(1.0, xexp),
+                     ldexp(1.0, wexp));
+  return (int)hipGetLastError();
+}
+
+int sq_sum_partials(const void* part, int n, void* out, void* stream) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                     (const double*)part, n, (double*)out);
   return (int)hipGetLastError();
 }
 

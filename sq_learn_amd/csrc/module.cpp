@@ -25,11 +25,11 @@ __attribute__((weak)) int sq_failure_inject(void*, long long, int, double, int, 
                                             unsigned, unsigned, unsigned, unsigned, unsigned,
                                             unsigned, long long, void*, void*);
 // kmeans.hip
-__attribute__((weak)) int sq_estep_bf16(const void* X, const void* C, const void* Clo, const void* cn, const void* xn,
-                  void* labels, void* mind, void* ovf_rows, void* ovf_count, void* inertia,
-                  long long n, int d, int k, int k_pad, double delta, int split, unsigned k0,
-                  unsigned k1, unsigned s0, unsigned s1, long long row_offset, int ovf_cap,
-                  void* stream);
+__attribute__((weak)) int sq_estep_bf16(const void* X, const void* C, void* inertia_part, const void* cn,
+                  const void* xn, void* labels, void* mind, void* ovf_rows, void* ovf_count,
+                  void* inertia, long long n, int d, int k, int k_pad, double delta, int part_cap,
+                  unsigned k0, unsigned k1, unsigned s0, unsigned s1, long long row_offset,
+                  int ovf_cap, void* stream);
 __attribute__((weak)) int sq_band_select(const void* D, const void* rows, const void* xn, void* labels, void* mind,
                    long long m, int k, long long ldD, double delta, unsigned k0, unsigned k1,
                    unsigned s0, unsigned s1, long long row_offset, void* stream);
@@ -40,13 +40,13 @@ __attribute__((weak)) int sq_centroid_accumulate(const void* X, int xdtype, cons
                            void* sums, void* counts, long long n, int d, int k, int chunk,
                            void* stream);
 __attribute__((weak)) int sq_centroid_reduce(const void*, int, const void*, const void*, void*, void*,
-                       long long, int, int, void*, void*, void*, void*);
+                       long long, int, int, int, int, void*, void*, void*, void*);
 __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
                          unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
                          void* stream);
-__attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia, void* packed, int k,
-                  int d, void* stream);
+__attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia,
+                                        void* packed, int k, int d, int xexp, int wexp, void*);
 __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void* cn, void* labels, void* mind,
                  long long m, int k, long long ldG, double eps, int Q, unsigned k0, unsigned k1,
                  unsigned s0, unsigned s1, long long row_offset, void* stream);
@@ -112,15 +112,15 @@ static PyObject* py_pe_batch(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_estep_bf16(PyObject*, PyObject* a) {
-  unsigned long long X, C, Clo, cn, xn, lab, mind, ovr, ovc, inr, st;
-  long long n, roff; int d, k, kpad, split, cap; double delta; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKKKKLiiidiIIIILiK", &X, &C, &Clo, &cn, &xn, &lab, &mind, &ovr,
-                        &ovc, &inr, &n, &d, &k, &kpad, &delta, &split, &k0, &k1, &s0, &s1, &roff,
+  unsigned long long X, C, part, cn, xn, lab, mind, ovr, ovc, inr, st;
+  long long n, roff; int d, k, kpad, pcap, cap; double delta; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKLiiidiIIIILiK", &X, &C, &part, &cn, &xn, &lab, &mind, &ovr,
+                        &ovc, &inr, &n, &d, &k, &kpad, &delta, &pcap, &k0, &k1, &s0, &s1, &roff,
                         &cap, &st))
     return nullptr;
   CHECK(sq_estep_bf16)
-  return ret(sq_estep_bf16(P(X), P(C), P(Clo), P(cn), P(xn), P(lab), P(mind), P(ovr), P(ovc),
-                           P(inr), n, d, k, kpad, delta, split, k0, k1, s0, s1, roff, cap, P(st)));
+  return ret(sq_estep_bf16(P(X), P(C), P(part), P(cn), P(xn), P(lab), P(mind), P(ovr), P(ovc),
+                           P(inr), n, d, k, kpad, delta, pcap, k0, k1, s0, s1, roff, cap, P(st)));
 }
 
 static PyObject* py_band_select(PyObject*, PyObject* a) {
@@ -165,13 +165,13 @@ static PyObject* py_centroid_accumulate(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
-  unsigned long long X, lab, w, sums, counts, h, c, pm, st; int xdt, d, k; long long n;
-  if (!PyArg_ParseTuple(a, "KiKKKKLiiKKKK", &X, &xdt, &lab, &w, &sums, &counts, &n, &d, &k, &h, &c,
-                        &pm, &st))
+  unsigned long long X, lab, w, sums, counts, h, c, pm, st; int xdt, d, k, xe, we; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKKLiiiiKKKK", &X, &xdt, &lab, &w, &sums, &counts, &n, &d, &k, &xe,
+                        &we, &h, &c, &pm, &st))
     return nullptr;
   CHECK(sq_centroid_reduce)
-  return ret(sq_centroid_reduce(P(X), xdt, P(lab), P(w), P(sums), P(counts), n, d, k, P(h), P(c),
-                                P(pm), P(st)));
+  return ret(sq_centroid_reduce(P(X), xdt, P(lab), P(w), P(sums), P(counts), n, d, k, xe, we, P(h),
+                                P(c), P(pm), P(st)));
 }
 
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
@@ -186,10 +186,10 @@ static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_pack_stats(PyObject*, PyObject* a) {
-  unsigned long long s, c, i, p, st; int k, d;
-  if (!PyArg_ParseTuple(a, "KKKKiiK", &s, &c, &i, &p, &k, &d, &st)) return nullptr;
+  unsigned long long s, c, i, p, st; int k, d, xe, we;
+  if (!PyArg_ParseTuple(a, "KKKKiiiiK", &s, &c, &i, &p, &k, &d, &xe, &we, &st)) return nullptr;
   CHECK(sq_pack_stats)
-  return ret(sq_pack_stats(P(s), P(c), P(i), P(p), k, d, P(st)));
+  return ret(sq_pack_stats(P(s), P(c), P(i), P(p), k, d, xe, we, P(st)));
 }
 
 static PyObject* py_ipe_estep(PyObject*, PyObject* a) {

@@ -89,14 +89,24 @@ class LloydEngine:
         self.Xb = Xb
         self.xn = xn if xn is not None else L.row_norms_sq(Xb)
         # M-step source: the original data when it is fp32 (means keep fp32
-        # precision), the bf16 copy otherwise
+        # precision), the padded bf16 copy otherwise
         if self.X.dtype == torch.float32 and self.d % 4 == 0:
             self.Xm = self.X.contiguous()
         else:
-            self.Xm = Xb if self.d == self.d_pad else None
+            self.Xm = Xb
+        self.dm = self.Xm.shape[1]
         self.buf = K.EStepBuffers(self.n, dev)
-        self.rws = K.ReduceWorkspace(self.n, self.k, dev)
-        self.sums = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
+        # deterministic fixed-point reduction: one global quantum for all ranks
+        mx = torch.stack([self.Xm.abs().max().float() if self.n else torch.zeros((), device=dev),
+                          (self.sample_weight.abs().max().float() if self.sample_weight is not None
+                           and self.n else torch.zeros((), device=dev))]).double()
+        nrows = torch.tensor([float(self.n)], dtype=torch.float64, device=dev)
+        self.comm.all_reduce_(mx, op="max")
+        self.comm.all_reduce_(nrows)
+        mxl = mx.tolist()
+        self.rws = K.ReduceWorkspace(self.n, self.k, dev).set_scale(
+            mxl[0], int(nrows.item()), mxl[1] if self.sample_weight is not None else None)
+        self.sums = torch.zeros((self.k, self.dm), dtype=torch.float64, device=dev)
         self.counts = torch.zeros(self.k, dtype=torch.float64, device=dev)
         self.packed = torch.zeros(self.k * self.d + self.k + 1, dtype=torch.float64, device=dev)
         self.shift = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -219,15 +229,11 @@ class LloydEngine:
             with tracing.range("mstep"):
                 self.sums.zero_()
                 self.counts.zero_()
-                if self.Xm is not None:
-                    K.centroid_reduce_native(self.Xm, labels, self.weights, self.sums,
-                                             self.counts, self.k, self.rws)
-                else:
-                    s, c = K.centroid_sums_torch(self.Xb[:, :self.d], labels, self.k,
-                                                 self.weights, acc_dtype=torch.float32)
-                    self.sums.copy_(s)
-                    self.counts.copy_(c)
-                K.pack_stats_native(self.sums, self.counts, inertia, self.packed, self.k, self.d)
+                K.centroid_reduce_native(self.Xm, labels, self.weights, self.sums,
+                                         self.counts, self.k, self.rws)
+                sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
+                K.pack_stats_native(sums, self.counts, inertia, self.packed, self.k, self.d,
+                                    self.rws, weighted=self.weights is not None)
             with tracing.range("allreduce"):
                 self.comm.all_reduce_(self.packed)
             with tracing.range("finalize"):
@@ -244,11 +250,34 @@ class LloydEngine:
             return self.scalars
         # generic / CPU
         w = self.sample_weight
-        sums, counts = K.centroid_sums_torch(self.Xf, labels, self.k, w,
-                                             acc_dtype=torch.float64 if self.device.type == "cpu"
-                                             else torch.float32)
-        packed = torch.cat([sums.reshape(-1).double(), counts.double(),
-                            inertia.double().reshape(1)])
+        if self.device.type == "cuda" and self.Xf.dtype == torch.float32 and self.d % 4 == 0:
+            # deterministic fixed-point segmented reduce (same kernel as the fast path)
+            if not hasattr(self, "_g_rws"):
+                mx = torch.stack([self.Xf.abs().max(), w.abs().max().float() if w is not None
+                                  else torch.zeros((), device=self.device)]).double()
+                nr = torch.tensor([float(self.n)], dtype=torch.float64, device=self.device)
+                self.comm.all_reduce_(mx, op="max")
+                self.comm.all_reduce_(nr)
+                mxl = mx.tolist()
+                self._g_rws = K.ReduceWorkspace(self.n, self.k, self.device).set_scale(
+                    mxl[0], int(nr.item()), mxl[1] if w is not None else None)
+                self._g_sums = torch.zeros((self.k, self.d), dtype=torch.float64,
+                                           device=self.device)
+                self._g_counts = torch.zeros(self.k, dtype=torch.float64, device=self.device)
+                self._g_w = w.to(torch.float32).contiguous() if w is not None else None
+            self._g_sums.zero_()
+            self._g_counts.zero_()
+            K.centroid_reduce_native(self.Xf, labels.to(torch.int32), self._g_w, self._g_sums,
+                                     self._g_counts, self.k, self._g_rws)
+            packed = torch.empty(self.k * self.d + self.k + 1, dtype=torch.float64,
+                                 device=self.device)
+            K.pack_stats_native(self._g_sums, self._g_counts, inertia.double().reshape(1), packed,
+                                self.k, self.d, self._g_rws, weighted=w is not None)
+        else:
+            sums, counts = K.centroid_sums_torch(self.Xf, labels, self.k, w,
+                                                 acc_dtype=torch.float64)
+            packed = torch.cat([sums.reshape(-1).double(), counts.double(),
+                                inertia.double().reshape(1)])
         self.comm.all_reduce_(packed)
         kd = self.k * self.d
         sums = packed[:kd].reshape(self.k, self.d)

@@ -136,6 +136,9 @@ class EStepBuffers:
         # scalars: [ovf_count(int32)] and inertia (fp64) / shift (fp64)
         self.ovf_count = torch.zeros(1, dtype=torch.int32, device=device)
         self.inertia = torch.zeros(1, dtype=torch.float64, device=device)
+        # per-wave inertia partials (summed in a fixed order: reproducible)
+        self.part_cap = n // 32 + 64
+        self.inertia_part = torch.zeros(self.part_cap, dtype=torch.float64, device=device)
 
 
 def estep_native(Xb, C_bf16, cn, xn, k, delta, key: RngKey, row_offset, buf: EStepBuffers,
@@ -146,14 +149,15 @@ def estep_native(Xb, C_bf16, cn, xn, k, delta, key: RngKey, row_offset, buf: ESt
     assert Xb.dtype == torch.bfloat16 and C_bf16.dtype == torch.bfloat16
     assert tuple(C_bf16.shape[1:]) == (d_pad // 8 + 2, 64, 8) and d_pad in FAST_D
     assert Xb.is_contiguous() and C_bf16.is_contiguous() and cn.is_contiguous()
+    assert buf.labels.numel() >= n and buf.part_cap >= 8
     st = stream if stream is not None else nat.stream_handle(Xb.device)
     m = nat.native()
     buf.ovf_count.zero_()
-    buf.inertia.zero_()
-    m.estep_bf16(Xb.data_ptr(), C_bf16.data_ptr(), 0, cn.data_ptr(), xn.data_ptr(),
-                 buf.labels.data_ptr(), buf.mind.data_ptr(), buf.ovf_rows.data_ptr(),
+    m.estep_bf16(Xb.data_ptr(), C_bf16.data_ptr(), buf.inertia_part.data_ptr(), cn.data_ptr(),
+                 xn.data_ptr(), buf.labels.data_ptr(), buf.mind.data_ptr(), buf.ovf_rows.data_ptr(),
                  buf.ovf_count.data_ptr(), buf.inertia.data_ptr(), n, d_pad, k, k_pad,
-                 float(delta), 0, key.k0, key.k1, key.s0, key.s1, int(row_offset), buf.ovf_cap, st)
+                 float(delta), int(buf.part_cap), key.k0, key.k1, key.s0, key.s1, int(row_offset),
+                 buf.ovf_cap, st)
     m.band_select_rows(Xb.data_ptr(), C_bf16.data_ptr(), cn.data_ptr(), xn.data_ptr(),
                        buf.ovf_rows.data_ptr(), buf.ovf_count.data_ptr(), buf.labels.data_ptr(),
                        buf.ovf_cap, d_pad, k, k_pad, float(delta), key.k0, key.k1, key.s0, key.s1,
@@ -192,30 +196,57 @@ def centroid_accumulate_native(X, labels, weights, sums, counts, k, chunk=None):
                                      nat.stream_handle(X.device))
 
 
-class ReduceWorkspace:
-    """Counting-sort workspace of the segmented centroid reduction."""
+def fixed_point_exp(max_abs, n_rows):
+    """Exponent e of the 2^e quantum of the deterministic segmented sums:
+    the smallest power of two with max|x| * n / 2^e <= 2^52, so every sum
+    is an integer multiple of 2^e below 2^53 quanta (exact in fp64 in any
+    addition order); clamped to the kernel's range."""
+    bound = float(max_abs) * max(int(n_rows), 1)
+    if not math.isfinite(bound):
+        raise ValueError("non-finite values in the data: cannot reduce centroids")
+    if bound <= 0.0:
+        return -120
+    e = math.ceil(math.log2(bound)) - 52
+    return int(min(max(e, -120), 120))
 
-    def __init__(self, n, k, device):
+
+class ReduceWorkspace:
+    """Counting-sort workspace of the segmented centroid reduction, plus the
+    fixed-point exponents (``xexp`` for the data, ``wexp`` for the weights;
+    0 when unweighted, counts then being exact integers)."""
+
+    def __init__(self, n, k, device, xexp=-30, wexp=0):
         self.hist = torch.zeros(k, dtype=torch.int32, device=device)
         self.cursor = torch.zeros(k, dtype=torch.int32, device=device)
         self.perm = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+        self.xexp = int(xexp)
+        self.wexp = int(wexp)
+
+    def set_scale(self, max_abs_x, n_rows, max_w=None):
+        self.xexp = fixed_point_exp(max_abs_x * (max_w if max_w is not None else 1.0), n_rows)
+        self.wexp = 0 if max_w is None else fixed_point_exp(max_w, n_rows)
+        return self
 
 
 def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorkspace):
-    """sums[l] += sum_{i: label_i = l} w_i x_i, counts[l] += sum w_i (GPU)."""
+    """sums[l] += sum_{i: label_i = l} w_i x_i, counts[l] += sum w_i (GPU),
+    in units of the quanta 2^ws.xexp / 2^ws.wexp (exact integer-valued fp64,
+    order-independent: bit-reproducible).  ``pack_stats_native`` rescales."""
     n, d = X.shape
-    assert labels.dtype == torch.int32 and sums.dtype == torch.float32 and counts.dtype == torch.float64
+    assert labels.dtype == torch.int32 and sums.dtype == torch.float64 and counts.dtype == torch.float64
+    assert sums.numel() >= k * d and counts.numel() >= k and labels.numel() >= n
     nat.native().centroid_reduce(X.data_ptr(), nat.dtype_code(X), labels.data_ptr(),
                                  0 if weights is None else weights.data_ptr(), sums.data_ptr(),
-                                 counts.data_ptr(), n, d, k, ws.hist.data_ptr(),
+                                 counts.data_ptr(), n, d, k, ws.xexp,
+                                 ws.wexp if weights is not None else 0, ws.hist.data_ptr(),
                                  ws.cursor.data_ptr(), ws.perm.data_ptr(),
                                  nat.stream_handle(X.device))
 
 
-def pack_stats_native(sums, counts, inertia, packed, k, d):
+def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, weighted=False):
     nat.native().pack_stats(sums.data_ptr(), counts.data_ptr(),
                             0 if inertia is None else inertia.data_ptr(), packed.data_ptr(), k, d,
-                            nat.stream_handle(sums.device))
+                            ws.xexp, ws.wexp if weighted else 0, nat.stream_handle(sums.device))
 
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,

@@ -147,24 +147,43 @@ def test_centroid_reduce(cuda, dtype, d):
     lab = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
     lab[:5000] = 3  # a big cluster
     w = torch.rand(n, dtype=torch.float32, device=cuda)
-    ws = K.ReduceWorkspace(n, k, cuda)
+    packed = torch.zeros(k * d + k + 1, dtype=torch.float64, device=cuda)
     for weights in (None, w):
-        sums = torch.zeros(k, d, dtype=torch.float32, device=cuda)
-        cnt = torch.zeros(k, dtype=torch.float64, device=cuda)
-        K.centroid_reduce_native(X, lab, weights, sums, cnt, k, ws)
+        ws = K.ReduceWorkspace(n, k, cuda).set_scale(float(X.float().abs().max()), n,
+                                                     None if weights is None else 1.0)
+        outs = []
+        for rep in range(2):
+            sums = torch.zeros(k, d, dtype=torch.float64, device=cuda)
+            cnt = torch.zeros(k, dtype=torch.float64, device=cuda)
+            K.centroid_reduce_native(X, lab, weights, sums, cnt, k, ws)
+            outs.append((sums.clone(), cnt.clone()))
+        # exact integer-valued accumulation: bit-identical run to run
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        K.pack_stats_native(outs[0][0], outs[0][1], None, packed, k, d, ws,
+                            weighted=weights is not None)
         rs, rc = K.centroid_sums_torch(X.double(), lab, k, weights)
-        assert torch.allclose(sums.double(), rs, atol=2e-3, rtol=1e-4)
-        assert torch.allclose(cnt, rc, rtol=1e-6)
+        got_s = packed[:k * d].reshape(k, d)
+        got_c = packed[k * d:k * d + k]
+        # error: fp32 product w*x per element, then a 2^-30-ish quantum
+        assert torch.allclose(got_s, rs, atol=1e-4, rtol=1e-6)
+        assert torch.allclose(got_c, rc, rtol=1e-6, atol=1e-6)
+        if weights is None:
+            assert torch.equal(got_c, rc)
 
 
 def test_finalize_noise_and_shift(cuda):
     k, d = 70, 48
-    sums = torch.randn(k, d, dtype=torch.float32, device=cuda)
-    cnt = torch.randint(1, 5, (k,), device=cuda).double()
-    cnt[3] = 0
+    ws = K.ReduceWorkspace(1, k, cuda, xexp=-20)
+    sums_f = torch.randn(k, d, dtype=torch.float64, device=cuda)
+    sums_i = torch.round(sums_f * 2.0 ** 20)
+    sums = (sums_i.double() * 2.0 ** -20).float()
+    cnt_i = torch.randint(1, 5, (k,), device=cuda).double()
+    cnt_i[3] = 0
+    cnt = cnt_i.double()
     inertia = torch.tensor([5.0], dtype=torch.float64, device=cuda)
     packed = torch.zeros(k * d + k + 1, dtype=torch.float64, device=cuda)
-    K.pack_stats_native(sums, cnt, inertia, packed, k, d)
+    K.pack_stats_native(sums_i, cnt_i, inertia, packed, k, d, ws)
+    assert torch.equal(packed[:k * d].reshape(k, d), sums_i.double() * 2.0 ** -20)
     assert packed[-1].item() == 5.0
     Cold = torch.randn(k, d, dtype=torch.float32, device=cuda)
     Cnew = torch.empty_like(Cold)
