@@ -45,6 +45,29 @@ def parse():
     return ap.parse_args()
 
 
+def _qpca_extra(extra, name, sa, comm, dev, solver, n_components=16):
+    """Wall-clock of a QPCA fit with the quantum extras of ``_qPCA.py:357-465``
+    (CPE singular values, Theorem 11 top-k extraction + Gaussian tomography);
+    one untimed warm fit first.  Never breaks the headline line."""
+    try:
+        from sq_learn_amd.models.decomposition import QPCA
+        q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev).fit(sa)
+        theta = 0.5 * float(q.singular_values_[n_components - 1])
+        torch.cuda.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev)
+        q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True,
+              true_tomography=False)
+        torch.cuda.synchronize()
+        comm.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        comm.all_reduce_(el, op="max")
+        extra[name] = float(el.item())
+    except Exception as e:  # qPCA must not break the headline line
+        extra[name + "_error"] = repr(e)[:200]
+
+
 def main():
     a = parse()
     from sq_learn_amd.parallel.comm import init_distributed, shard_bounds, Comm
@@ -98,30 +121,23 @@ def main():
     extra = {"inertia_last": last[0] if last else None, "overflow_rows_last": ovf,
              "rows_per_gpu": stop - start, "delta": a.delta, "k": a.k, "d": a.d}
     if not a.no_qpca:
-        try:
-            from sq_learn_amd.models.decomposition import QPCA
-            from sq_learn_amd.parallel.sharding import ShardedArray
-            del eng
-            torch.cuda.empty_cache()
-            sa = ShardedArray(X, a.n, start, comm)
-            q = QPCA(n_components=8, svd_solver="full", device=dev)
-            q.fit(sa)            # warm (kernel load, allocator)
-            torch.cuda.synchronize()
-            comm.barrier()
-            tq = time.perf_counter()
-            # theta: keep the top-8 estimated singular values (half the 8th)
-            theta = 0.5 * float(q.singular_values_[7])
-            q = QPCA(n_components=8, svd_solver="full", device=dev)
-            q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True,
-                  true_tomography=False)
-            torch.cuda.synchronize()
-            comm.barrier()
-            tq = time.perf_counter() - tq
-            e2 = torch.tensor([tq], dtype=torch.float64, device=dev)
-            comm.all_reduce_(e2, op="max")
-            extra["qpca_full_fit_s"] = float(e2.item())
-        except Exception as e:  # qPCA must not break the headline line
-            extra["qpca_error"] = repr(e)[:200]
+        del eng
+        torch.cuda.empty_cache()
+        from sq_learn_amd.parallel.sharding import ShardedArray
+        # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
+        _qpca_extra(extra, "qpca_10Mx256_full_fit_s", ShardedArray(X, a.n, start, comm), comm,
+                    dev, "full")
+        del X
+        torch.cuda.empty_cache()
+        # BASELINE config 2: qPCA 1M x 512 bf16 (low-rank + tail), full and randomized
+        from sq_learn_amd.utils.datasets import make_low_rank_device
+        n2, d2 = 1_000_000, 512
+        s2, e2 = shard_bounds(n2, rank, comm.world_size)
+        X2 = make_low_rank_device(n2, d2, effective_rank=32, tail_strength=0.3, seed=a.seed,
+                                  device=dev, dtype=torch.bfloat16, row_range=(s2, e2))
+        sa2 = ShardedArray(X2, n2, s2, comm)
+        _qpca_extra(extra, "qpca_1Mx512_full_fit_s", sa2, comm, dev, "full")
+        _qpca_extra(extra, "qpca_1Mx512_randomized_fit_s", sa2, comm, dev, "randomized")
 
     if rank == 0:
         out = {

@@ -57,6 +57,60 @@ SQ_DEV uint32_t band_key(const RngKey& key, long long grow, uint32_t j) {
   return key.block(idx).x;
 }
 
+// ---------------------------------------------------------------------------
+// delta-band selection rule (shared by every kernel and the torch twin
+// ops/kmeans.py band_select_torch):  members M = {j : D_j <= min + delta},
+// c = |M|, ordered by kappa(j) = (j mod 32, j div 32); the label is the
+// member of rank r = floor(u * c), u = u01(word g of key) - ONE Philox word
+// per row (not per member), so the band resolution costs a few wave ops.
+SQ_DEV float band_u(const RngKey& key, long long grow) {
+  return u01(key.word((unsigned long long)grow));
+}
+SQ_DEV int band_rank(float u, int c) {
+  int r = (int)(u * (float)c);
+  return r < c ? r : c - 1;
+}
+// position of the (r+1)-th set bit of m (r < popcount(m))
+SQ_DEV int nth_set_bit(unsigned long long m, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w > 0; w >>= 1) {
+    const unsigned long long lo = m & ((1ull << w) - 1ull);
+    const int c = __popcll(lo);
+    if (r >= c) { r -= c; m >>= w; pos += w; } else { m = lo; }
+  }
+  return pos;
+}
+// One wave picks the band member of rank r for one row; lanes scan
+// j = lane + 64 t.  dist(j) must be a pure function (called in two passes).
+template <typename DistF>
+SQ_DEV int band_pick_wave(DistF dist, int k, float thr, float u, int lane) {
+  int c = 0;
+  for (int j = lane; j < k; j += 64) c += dist(j) <= thr ? 1 : 0;
+  const int cr = c + __shfl_xor(c, 32, 64);          // count of class rho = lane & 31
+  int incl = cr;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    const int v = __shfl_up(incl, o, 32);
+    if ((lane & 31) >= o) incl += v;
+  }
+  const int total = __shfl(incl, 31, 64);
+  if (total == 0) return -1;
+  const int r = band_rank(u, total);
+  const unsigned long long hit = __ballot(lane < 32 && incl > r);
+  const int rho = __ffsll((long long)hit) - 1;
+  int rr = r - __shfl(incl - cr, rho, 64);
+  for (int base = 0;; base += 64) {                  // members of class rho in j order
+    const int j = rho + 32 * (base + lane);
+    const bool mem = j < k && dist(j) <= thr;
+    const unsigned long long b = __ballot(mem);
+    const int cnt = __popcll(b);
+    if (rr < cnt) return rho + 32 * (base + nth_set_bit(b, rr));
+    rr -= cnt;
+    if (rho + 32 * base >= k) return -1;             // unreachable for a consistent dist
+  }
+}
+
 // Centroid operand layout (written by centroid_finalize / centers_to_bf16):
 // per 64-centroid tile, CPR = (d_pad + 16) / 8 chunks of 16 B, chunk-major:
 //   elem(j, f) at ((tile * CPR + f / 8) * 64 + j % 64) * 8 + f % 8
@@ -79,12 +133,11 @@ SQ_DEV uint32_t band_key(const RngKey& key, long long grow, uint32_t j) {
 #endif
 template <int KSD, int NW>
 __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
-    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, const float* __restrict__ cn,
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, float* __restrict__ ovf_thr,
     const float* __restrict__ xn, int* __restrict__ labels, float* __restrict__ mind,
     long long* __restrict__ ovf_rows, int* __restrict__ ovf_count, double* __restrict__ inertia,
     long long n, int k, int k_pad, float delta, RngKey key, long long row_offset, int ovf_cap,
     int idx_bits, int dbg) {
-  (void)cn;
   (void)k;
   constexpr int KS = KSD + 1;            // data k-steps + augmented norm step
   constexpr int DX = KSD * 16;           // X row length (padded features)
@@ -284,31 +337,36 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
       if (!band2) labels[grow_local] = (int)(__float_as_uint(q1) & ~keep);
       my_inertia += (double)dist;
     }
-    // rows with >= 2 band members (rare for small delta): exact resolution
-    // from the per-lane top-2 lists; a lane holding two members -> overflow
+    // rows with >= 2 band members: rank rule over the per-lane top-2 lists
+    // (lane r32 holds the candidates j = r32 mod 32, so lane order is kappa
+    // order); a lane holding two members -> exact fallback (overflow list)
     const unsigned long long slow = __ballot(owner && band2);
     if (slow && !dbg) {   // (ablation runs skip band resolution)
+      const float urow = band_u(key, row_offset + grow_local);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const unsigned long long sel = slow & ((1ull << (2 * i)) | (1ull << (32 + 2 * i)));
         if (!sel) continue;
-        const bool mine = (slow >> (32 * half + 2 * i)) & 1ull;
-        const float thr_i = __shfl(thr, 32 * half + 2 * i, 64);
+        const int src = 32 * half + 2 * i;
+        const bool mine = (slow >> src) & 1ull;
+        const float thr_i = __shfl(thr, src, 64);
+        const float u_i = __shfl(urow, src, 64);
         const bool v1 = mine && valf(m1[i], keep) <= thr_i;
         const bool v2 = mine && valf(m2[i], keep) <= thr_i;
+        const uint32_t hb1 = (uint32_t)(__ballot(v1) >> (32 * half));
         const uint32_t hb2 = (uint32_t)(__ballot(v2) >> (32 * half));
-        const uint32_t jj = __float_as_uint(m1[i]) & ~keep;
-        const long long g = row0 + (i & 3) + 8 * (i >> 2) + 4 * half;
-        uint32_t kk = v1 ? ((band_key(key, row_offset + g, jj) & keep) | jj) : 0xFFFFFFFFu;
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) kk = min(kk, (uint32_t)__shfl_xor((int)kk, o, 64));
+        const int c = __popc(hb1);
+        const int pick = hb2 == 0u && c > 0 ? nth_set_bit(hb1, band_rank(u_i, c)) : 0;
+        const uint32_t jsel = (uint32_t)__shfl((int)(__float_as_uint(m1[i]) & ~keep),
+                                               32 * half + pick, 64);
         if (mine && r32 == 2 * i) {
+          const long long g = row0 + (i & 3) + 8 * (i >> 2) + 4 * half;
           if (hb2 != 0u) {
             int slot = atomicAdd(ovf_count, 1);
-            if (slot < ovf_cap) ovf_rows[slot] = g;
+            if (slot < ovf_cap) { ovf_rows[slot] = g; ovf_thr[slot] = thr_i; }
             labels[g] = -1;
           } else {
-            labels[g] = (int)(kk & ~keep);
+            labels[g] = (int)jsel;
           }
         }
       }
@@ -324,7 +382,8 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
 
 // ---------------------------------------------------------------------------
 // band_select: rows of full fp32 distances D[m][ldD] (first k valid).  One wave
-// per row.  Exact: min, band {D <= min + delta}, smallest Philox key.
+// per row.  Exact: min, band {D <= min + delta}, member of rank floor(u c)
+// in kappa order (band_pick_wave).
 // If xn != nullptr the D rows hold ||c||^2 - 2x.c and xn is added.
 __global__ void __launch_bounds__(256) band_select_kernel(
     const float* __restrict__ D, const long long* __restrict__ rows, const float* __restrict__ xn,
@@ -340,33 +399,10 @@ __global__ void __launch_bounds__(256) band_select_kernel(
   for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
   const long long grow = rows ? rows[r] : r;
   const float thr = mn + delta;
-  const uint32_t keep = ~((1u << idx_bits) - 1u);
-  uint32_t best = 0xFFFFFFFFu;
-  int cnt = 0;
-  for (int j = lane; j < k; j += 64) {
-    if (d[j] <= thr) {
-      ++cnt;
-      uint32_t kk = (band_key(key, row_offset + grow, (uint32_t)j) & keep) | (uint32_t)j;
-      best = min(best, kk);
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
-    cnt += __shfl_xor(cnt, o, 64);
-  }
-  uint32_t win;
-  if (cnt <= 1) {
-    // single member: the argmin (first index at the min)
-    uint32_t am = 0xFFFFFFFFu;
-    for (int j = lane; j < k; j += 64)
-      if (d[j] == mn) am = min(am, (uint32_t)j);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) am = min(am, (uint32_t)__shfl_xor((int)am, o, 64));
-    win = am;
-  } else {
-    win = best & ~keep;
-  }
+  (void)idx_bits;
+  auto dist = [&](int j) -> float { return d[j]; };
+  const uint32_t win =
+      (uint32_t)band_pick_wave(dist, k, thr, band_u(key, row_offset + grow), lane);
   if (lane == 0) {
     labels[grow] = (int)win;
     float base = xn ? xn[grow] : 0.0f;
@@ -381,18 +417,20 @@ __global__ void __launch_bounds__(256) band_select_kernel(
 // grid covers the list capacity and surplus waves exit.  One wave per row,
 // lanes over centroids, full distance recomputed from the bf16 operands.
 __global__ void __launch_bounds__(256) band_select_rows_kernel(
-    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, const float* __restrict__ cn,
-    const float* __restrict__ xn, const long long* __restrict__ rows, const int* __restrict__ count,
-    int* __restrict__ labels, long long cap, int d_pad, int k, float delta, RngKey key,
-    long long row_offset, int idx_bits) {
-  (void)cn;
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C,
+    const float* __restrict__ thr_list, const float* __restrict__ xn,
+    const long long* __restrict__ rows, const int* __restrict__ count, int* __restrict__ labels,
+    long long cap, int d_pad, int k, float delta, RngKey key, long long row_offset, int idx_bits) {
+  (void)xn;
   __shared__ float xs[4][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long long slot = (long long)blockIdx.x * 4 + w;
-  long long cnt = min((long long)*count, cap);
-  if (slot >= cnt) return;
-  const long long r = rows[slot];
+  const long long cnt = min((long long)*count, cap);
   const int cpr = d_pad / 8 + 2;   // chunk-major operand (see estep_kernel)
+  // grid-stride over the device-side list (any length up to cap)
+  for (long long slot = (long long)blockIdx.x * 4 + w; slot < cnt;
+       slot += (long long)gridDim.x * 4) {
+  const long long r = rows[slot];
+  __builtin_amdgcn_wave_barrier();
   for (int c = lane; c < d_pad; c += 64) xs[w][c] = bf16_to_f32(X[(size_t)r * d_pad + c]);
   __builtin_amdgcn_wave_barrier();
   // D'(j) = ||c_j||^2 - 2 x.c_j from the same bf16 operands the MFMA used
@@ -410,30 +448,22 @@ __global__ void __launch_bounds__(256) band_select_rows_kernel(
     uint32_t nv = *reinterpret_cast<const uint32_t*>(base + (size_t)(d_pad / 8) * 512);
     return s + __uint_as_float(nv << 16) + __uint_as_float(nv & 0xFFFF0000u);
   };
-  float mn = __builtin_inff();
-  for (int j = lane; j < k; j += 64) mn = fminf(mn, dist(j));
+  // threshold from the fused kernel (its MFMA min + delta): no min pass;
+  // if rounding of this recomputation leaves the band empty, use our own min
+  float thr = thr_list[slot];
+  (void)idx_bits;
+  const float u = band_u(key, row_offset + r);
+  int win = band_pick_wave(dist, k, thr, u, lane);
+  if (win < 0) {
+    float mn = __builtin_inff();
+    for (int j = lane; j < k; j += 64) mn = fminf(mn, dist(j));
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
-  const float thr = mn + delta;
-  const uint32_t keep = ~((1u << idx_bits) - 1u);
-  uint32_t best = 0xFFFFFFFFu;
-  int nc = 0;
-  uint32_t am = 0xFFFFFFFFu;
-  for (int j = lane; j < k; j += 64) {
-    float dv = dist(j);
-    if (dv == mn) am = min(am, (uint32_t)j);
-    if (dv <= thr) {
-      ++nc;
-      best = min(best, (band_key(key, row_offset + r, (uint32_t)j) & keep) | (uint32_t)j);
-    }
+    for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+    thr = mn + delta;
+    win = band_pick_wave(dist, k, thr, u, lane);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
-    am = min(am, (uint32_t)__shfl_xor((int)am, o, 64));
-    nc += __shfl_xor(nc, o, 64);
+  if (lane == 0) labels[r] = win;
   }
-  if (lane == 0) labels[r] = (int)(nc <= 1 ? am : (best & ~keep));
 }
 
 // ---------------------------------------------------------------------------
@@ -857,7 +887,7 @@ static int launch_estep(const void* X, const void* C, const void* cn, const void
   if ((long long)grid * NW > part_cap) grid = (unsigned)(part_cap / NW);   // still persistent
   if (grid == 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const uint16_t*)X,
-                     (const uint16_t*)C, (const float*)cn, (const float*)xn, (int*)labels,
+                     (const uint16_t*)C, (float*)cn, (const float*)xn, (int*)labels,
                      (float*)mind, (long long*)ovf_rows, (int*)ovf_count, (double*)part, n, k,
                      k_pad, delta, key, row_offset, ovf_cap, idx_bits_for(k_pad), estep_dbg());
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, (const double*)part,
@@ -925,9 +955,12 @@ int sq_band_select_rows(const void* X, const void* C, const void* cn, const void
   if (cap <= 0) return 0;
   if (d_pad > 256) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
-  hipLaunchKernelGGL(band_select_rows_kernel, dim3((unsigned)((cap + 3) / 4)), dim3(256), 0,
+  const long long blocks = (cap + 3) / 4;
+  hipLaunchKernelGGL(band_select_rows_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
+                     dim3(256), 0,
                      (hipStream_t)stream, (const uint16_t*)X, (const uint16_t*)C,
-                     (const float*)cn, (const float*)xn, (const long long*)rows,
+                     (const float*)cn /* per-slot thresholds */, (const float*)xn,
+                     (const long long*)rows,
                      (const int*)count, (int*)labels, cap, d_pad, k, (float)delta, key,
                      row_offset, idx_bits_for(k_pad));
   return (int)hipGetLastError();

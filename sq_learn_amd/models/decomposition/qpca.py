@@ -484,9 +484,14 @@ class QPCA(_BasePCA):
 
     # ----------------------------------------------------------- transform
     def transform(self, X, classic_transform=True, epsilon_delta=0, quantum_representation=False,
-                  norm="None", psi=0, true_tomography=True, use_classical_components=True):
+                  norm="None", psi=0, true_tomography=True, use_classical_components=True,
+                  tomography=None):
         """Classical projection, or the quantum representation of the projected
-        data (``_qPCA.py:773-846``)."""
+        data (``_qPCA.py:773-846``).  ``tomography=`` is accepted as an alias
+        of ``true_tomography`` (the reference's driver passes it,
+        ``MnistTrial.py:19``, and crashes with TypeError there)."""
+        if tomography is not None:
+            true_tomography = bool(tomography)
         if classic_transform:
             if epsilon_delta != 0 or quantum_representation or (norm not in ("None", None)) or psi != 0:
                 warnings.warn("Warning! You are using the classical transform, so the quantum "

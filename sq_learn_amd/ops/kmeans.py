@@ -47,12 +47,50 @@ def band_keys(key: RngKey, grows, cols, k_pad):
     return (w & keep) | cols.to(torch.int64)
 
 
-def band_select_torch(D, grows, delta, key: RngKey, k_pad, tie_only=False):
-    """Exact delta-band selection over distance rows D [m, k] (torch).
+def band_u(key: RngKey, grows):
+    """Per-row uniform of the band rule: u01(Philox word g) (fp32, exact twin
+    of ``band_u`` in csrc/kmeans.hip)."""
+    g = grows.to(torch.int64)
+    w = philox4x32((g >> 2) & MASK32, (g >> 34) & MASK32, key.s0, key.s1, key.k0, key.k1)
+    word = torch.stack(w, 1).gather(1, (g & 3)[:, None])[:, 0]
+    return ((word >> 8).to(torch.float32) + 0.5) * (1.0 / 16777216.0)
 
-    label = uniform member of {j : D_j <= min + delta} (first argmin when the
-    band has one member).  Reference: ``_dmeans.py:742-751, 771-772``
-    (``select_labels`` -> random.choice among the qualifying indices)."""
+
+def band_select_torch(D, grows, delta, key: RngKey, k_pad, tie_only=False):
+    """Exact delta-band selection over distance rows D [m, k] (torch twin of
+    the HIP kernels; csrc/kmeans.hip ``band_pick_wave``).
+
+    members M = {j : D_j <= min + delta}; ordered by kappa(j) = (j mod 32,
+    j div 32); label = member of rank floor(u * |M|) with one Philox uniform
+    per row -> a uniform choice among the qualifying indices, like the
+    reference's ``random.choice`` (``_dmeans.py:742-751, 771-772``)."""
+    if tie_only:
+        return _band_select_minkey_torch(D, grows, delta, key, k_pad, tie_only=True)
+    mn, am = torch.min(D, dim=1)
+    thr = mn + float(delta)
+    cand = D <= thr[:, None]
+    cnt = cand.sum(1)
+    labels = am.clone()
+    multi = torch.nonzero(cnt > 1).reshape(-1)
+    if multi.numel():
+        k = D.shape[1]
+        j = torch.arange(k, dtype=torch.int64, device=D.device)
+        kappa = ((j & 31) << 20) | (j >> 5)
+        sub = cand[multi]
+        kap = torch.where(sub, kappa[None, :], torch.full_like(kappa, 1 << 40)[None, :])
+        srt = torch.sort(kap, dim=1).values
+        c = cnt[multi]
+        u = band_u(key, grows[multi].to(D.device))
+        r = torch.floor(u * c.to(torch.float32)).to(torch.int64)
+        r = torch.minimum(r, c - 1)
+        ch = srt.gather(1, r[:, None])[:, 0]
+        labels[multi] = ((ch & 0xFFFFF) << 5) | (ch >> 20)
+    return labels, mn
+
+
+def _band_select_minkey_torch(D, grows, delta, key: RngKey, k_pad, tie_only=False):
+    """Tie-break by the smallest per-(row, centroid) Philox key (the IPE
+    kernel's rule, ``ipe_estep_kernel``)."""
     mn, am = torch.min(D, dim=1)
     thr = mn + (0.0 if tie_only else float(delta))
     cand = D <= thr[:, None]
@@ -131,8 +169,11 @@ class EStepBuffers:
     def __init__(self, n, device, ovf_cap=None):
         self.labels = torch.empty(n, dtype=torch.int32, device=device)
         self.mind = torch.empty(n, dtype=torch.float32, device=device)
-        self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(4096, n // 16))
+        # every row may overflow (wide bands): the list holds all n rows, so no
+        # row is ever dropped; the fallback kernel strides over the live count
+        self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(n, 1))
         self.ovf_rows = torch.empty(self.ovf_cap, dtype=torch.int64, device=device)
+        self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
         # scalars: [ovf_count(int32)] and inertia (fp64) / shift (fp64)
         self.ovf_count = torch.zeros(1, dtype=torch.int32, device=device)
         self.inertia = torch.zeros(1, dtype=torch.float64, device=device)
@@ -153,12 +194,12 @@ def estep_native(Xb, C_bf16, cn, xn, k, delta, key: RngKey, row_offset, buf: ESt
     st = stream if stream is not None else nat.stream_handle(Xb.device)
     m = nat.native()
     buf.ovf_count.zero_()
-    m.estep_bf16(Xb.data_ptr(), C_bf16.data_ptr(), buf.inertia_part.data_ptr(), cn.data_ptr(),
+    m.estep_bf16(Xb.data_ptr(), C_bf16.data_ptr(), buf.inertia_part.data_ptr(), buf.ovf_thr.data_ptr(),
                  xn.data_ptr(), buf.labels.data_ptr(), buf.mind.data_ptr(), buf.ovf_rows.data_ptr(),
                  buf.ovf_count.data_ptr(), buf.inertia.data_ptr(), n, d_pad, k, k_pad,
                  float(delta), int(buf.part_cap), key.k0, key.k1, key.s0, key.s1, int(row_offset),
                  buf.ovf_cap, st)
-    m.band_select_rows(Xb.data_ptr(), C_bf16.data_ptr(), cn.data_ptr(), xn.data_ptr(),
+    m.band_select_rows(Xb.data_ptr(), C_bf16.data_ptr(), buf.ovf_thr.data_ptr(), xn.data_ptr(),
                        buf.ovf_rows.data_ptr(), buf.ovf_count.data_ptr(), buf.labels.data_ptr(),
                        buf.ovf_cap, d_pad, k, k_pad, float(delta), key.k0, key.k1, key.s0, key.s1,
                        int(row_offset), st)

@@ -119,7 +119,8 @@ def test_estep_band_semantics(cuda):
     assert abs(frac_argmin - expect) < 0.05, (frac_argmin, expect)
     # torch CPU selection with the same keys agrees on the large majority
     lab_cpu, _ = K.band_select_torch(D.float(), torch.arange(n), delta, key, kp)
-    assert (lab_cpu == got).float().mean() > 0.97
+    # same rank rule and Philox words: identical except fp near-ties at the band edge
+    assert (lab_cpu == got).float().mean() > 0.995
 
 
 def test_centroid_accumulate(cuda):
