@@ -179,70 +179,135 @@ __global__ void __launch_bounds__(256, 1) power_iter_kernel(
 }
 
 // ------------------------------------------------------------------ mu
-// 8 columns per thread, 32 threads per row, 2 rows per wave, 8 rows per WG step.
+// Power sums of |a|^q for a p-grid of exponents (mu(A), Utility.py:196-231):
+// rowmax[i] = max_r sum_c |a_rc|^q_i, colsum[i][c] = sum_r |a_rc|^q_i.
+// Lanes own 8 consecutive columns; LPR = ceil(d/8) (power of two) lanes per
+// row, so a wave covers 64/LPR rows at once (no idle lanes for d < 256).
+// One v_log per element, one v_exp per (element, exponent); row sums by
+// log2(LPR) xor-shuffles; column sums reduced in LDS per workgroup and
+// written as per-WG partials, summed by mu_colsum_kernel in a fixed order
+// (no float atomics: deterministic).
 constexpr int MUQ = 12;
 
 template <typename T>
+SQ_DEV void ld8abs(const T* p, bool full, int valid, float v[8]);
+template <>
+SQ_DEV void ld8abs<uint16_t>(const uint16_t* p, bool full, int valid, float v[8]) {
+  if (full) {
+    uint4 u = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] = fabsf(__uint_as_float(w[e] << 16));
+      v[2 * e + 1] = fabsf(__uint_as_float(w[e] & 0xFFFF0000u));
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(bf16_to_f32(p[e])) : 0.f;
+  }
+}
+template <>
+SQ_DEV void ld8abs<float>(const float* p, bool full, int valid, float v[8]) {
+  if (full) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = fabsf(a.x); v[1] = fabsf(a.y); v[2] = fabsf(a.z); v[3] = fabsf(a.w);
+    v[4] = fabsf(b.x); v[5] = fabsf(b.y); v[6] = fabsf(b.z); v[7] = fabsf(b.w);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(p[e]) : 0.f;
+  }
+}
+
+template <typename T, int LPR>
 __global__ void __launch_bounds__(256) mu_sums_kernel(
     const T* __restrict__ X, const float* __restrict__ qs, int nq, float* __restrict__ rowmax,
-    float* __restrict__ colsum, long long n, int d, long long rows_per_wg) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int sub = lane & 31;                 // thread within row group
-  const int rgrp = tid >> 5;                 // 8 row groups per WG
+    float* __restrict__ part, long long n, int d, long long rows_per_wg) {
+  constexpr int RPW = 64 / LPR;              // rows per wave step
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int vl = lane % LPR;                  // column group of this lane
+  const int sg = (wave * 64 + lane) / LPR;    // row slot within the WG (0 .. 4*RPW-1)
+  const int c0 = vl * 8;
+  const bool vec = ((d % 8) == 0) && (c0 + 8 <= d);
+  const int valid = d - c0;
   float q[MUQ];
 #pragma unroll
   for (int i = 0; i < MUQ; ++i) q[i] = i < nq ? qs[i] : 0.f;
-  float rmax[MUQ];
+  float cs[MUQ][8], rmax[MUQ];
 #pragma unroll
-  for (int i = 0; i < MUQ; ++i) rmax[i] = 0.f;
+  for (int i = 0; i < MUQ; ++i) {
+    rmax[i] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[i][e] = 0.f;
+  }
   const long long r_beg = (long long)blockIdx.x * rows_per_wg;
   const long long r_end = min(n, r_beg + rows_per_wg);
-  for (int cb = 0; cb < d; cb += 256) {
-    const int c0 = cb + sub * 8;
-    float cs[MUQ][8];
+  for (long long r = r_beg + sg; r < r_end; r += 4 * RPW) {
+    float v[8], lg[8];
+    if (c0 < d) ld8abs<T>(X + (size_t)r * d + c0, vec, valid, v);
+    else {
 #pragma unroll
-    for (int i = 0; i < MUQ; ++i)
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) cs[i][e] = 0.f;
-    // NOTE: for d > 256 the row sums are accumulated across column blocks in
-    // rsum_acc (per row group lane 0) - handled by the host splitting d <= 256
-    for (long long r = r_beg + rgrp; r < r_end; r += 8) {
-      float lg[8];
-      bool nz[8];
+    for (int e = 0; e < 8; ++e) lg[e] = __builtin_amdgcn_logf(v[e]);   // log2, -inf at 0
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = (c0 + e < d) ? fabsf(ld1<T>(X, (size_t)r * d + c0 + e)) : 0.f;
-        nz[e] = v != 0.f;
-        lg[e] = __log2f(v);
-      }
-#pragma unroll
-      for (int i = 0; i < MUQ; ++i) {
-        if (i >= nq) break;
+    for (int i = 0; i < MUQ; ++i) {
+      if (i < nq) {
         float rs = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float p = q[i] == 0.f ? (nz[e] ? 1.f : 0.f) : (nz[e] ? exp2f(q[i] * lg[e]) : 0.f);
-          cs[i][e] += p;
-          rs += p;
+          // |a|^0 counts nonzeros; exp2(q * -inf) = 0 for q > 0
+          const float pw = q[i] == 0.f ? (v[e] != 0.f ? 1.f : 0.f)
+                                        : __builtin_amdgcn_exp2f(q[i] * lg[e]);
+          cs[i][e] += pw;
+          rs += pw;
         }
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) rs += __shfl_xor(rs, o, 64);
+        for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
         rmax[i] = fmaxf(rmax[i], rs);
       }
     }
+  }
+  // row maxima: one atomic per exponent per wave (max is order-independent)
 #pragma unroll
-    for (int i = 0; i < MUQ; ++i) {
-      if (i >= nq) break;
+  for (int i = 0; i < MUQ; ++i) {
+    if (i < nq) {
+      float m = rmax[i];
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (c0 + e < d) atomicAdd(&colsum[(size_t)i * d + c0 + e], cs[i][e]);
+      for (int o = LPR; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      if (lane == 0) atomic_max_pos(&rowmax[i], m);
     }
   }
-  if (sub == 0) {
+  // column sums: reduce the 4*RPW row slots sharing a column group in LDS
+  for (int i = 0; i < nq; ++i) {
 #pragma unroll
-    for (int i = 0; i < MUQ; ++i)
-      if (i < nq) atomic_max_pos(&rowmax[i], rmax[i]);
+    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = cs[i][e];
+    __syncthreads();
+    if (sg == 0) {               // threads 0..LPR-1: one per column group
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < 4 * RPW; ++s2) {
+        const int t = s2 * LPR + vl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += red[t * 8 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c0 + e < d) part[((size_t)blockIdx.x * nq + i) * d + c0 + e] = acc[e];
+    }
+    __syncthreads();
   }
+}
+
+// colsum[i][c] = sum over WGs of part[wg][i][c] (fixed order)
+__global__ void __launch_bounds__(256) mu_colsum_kernel(const float* __restrict__ part, int wgs,
+                                                        int nq, int d, float* __restrict__ colsum) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nq * d) return;
+  float s = 0.f;
+  for (int w = 0; w < wgs; ++w) s += part[(size_t)w * nq * d + idx];
+  colsum[idx] = s;
 }
 
 template <typename T>
@@ -345,23 +410,34 @@ int sq_power_iter(const void* X, int xdtype, const void* Q, void* Z, const void*
 }
 
 int sq_mu_sums(const void* X, int xdtype, const void* qs, int nq, void* rowmax, void* colsum,
-               long long n, int d, void* stream) {
+               void* part, int part_wgs, long long n, int d, void* stream) {
   if (n <= 0) return 0;
-  if (nq > MUQ || d > 256) return (int)hipErrorInvalidValue;
-  long long wgs = min(4096LL, max(1LL, (n + 255) / 256));
+  if (nq > MUQ || d > 256 || part_wgs < 1) return (int)hipErrorInvalidValue;
+  long long wgs = min((long long)part_wgs, max(1LL, (n + 255) / 256));
   long long rpw = (n + wgs - 1) / wgs;
   wgs = (n + rpw - 1) / rpw;
   hipStream_t st = (hipStream_t)stream;
-  if (xdtype == 0)
-    hipLaunchKernelGGL(mu_sums_kernel<float>, dim3((unsigned)wgs), dim3(256), 0, st,
-                       (const float*)X, (const float*)qs, nq, (float*)rowmax, (float*)colsum, n, d,
-                       rpw);
-  else if (xdtype == 2)
-    hipLaunchKernelGGL(mu_sums_kernel<uint16_t>, dim3((unsigned)wgs), dim3(256), 0, st,
-                       (const uint16_t*)X, (const float*)qs, nq, (float*)rowmax, (float*)colsum, n,
-                       d, rpw);
-  else
+  int lpr = 1;
+  while (lpr * 8 < d) lpr <<= 1;
+#define MU_CASE(T, L)                                                                          \
+  case L:                                                                                      \
+    hipLaunchKernelGGL((mu_sums_kernel<T, L>), dim3((unsigned)wgs), dim3(256), 0, st,          \
+                       (const T*)X, (const float*)qs, nq, (float*)rowmax, (float*)part, n, d,  \
+                       rpw);                                                                   \
+    break;
+  if (xdtype == 0) {
+    switch (lpr) { MU_CASE(float, 1) MU_CASE(float, 2) MU_CASE(float, 4) MU_CASE(float, 8)
+                   MU_CASE(float, 16) MU_CASE(float, 32) default: return (int)hipErrorInvalidValue; }
+  } else if (xdtype == 2) {
+    switch (lpr) { MU_CASE(uint16_t, 1) MU_CASE(uint16_t, 2) MU_CASE(uint16_t, 4)
+                   MU_CASE(uint16_t, 8) MU_CASE(uint16_t, 16) MU_CASE(uint16_t, 32)
+                   default: return (int)hipErrorInvalidValue; }
+  } else {
     return (int)hipErrorInvalidValue;
+  }
+#undef MU_CASE
+  hipLaunchKernelGGL(mu_colsum_kernel, dim3((unsigned)((nq * d + 255) / 256)), dim3(256), 0, st,
+                     (const float*)part, (int)wgs, nq, d, (float*)colsum);
   return (int)hipGetLastError();
 }
 

@@ -55,8 +55,8 @@ __attribute__((weak)) int sq_gram_bf16(const void* X, int xdtype, void* G, const
                  void* stream);
 __attribute__((weak)) int sq_power_iter(const void* X, int xdtype, const void* Q, void* Z, const void* mean, long long n,
                   int d, int l, void* stream);
-__attribute__((weak)) int sq_mu_sums(const void* X, int xdtype, const void* qs, int nq, void* rowmax, void* colsum,
-               long long n, int d, void* stream);
+__attribute__((weak)) int sq_mu_sums(const void*, int, const void*, int, void*, void*, void*, int,
+                                     long long, int, void*);
 __attribute__((weak)) int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream);
 // knn.hip
 __attribute__((weak)) int sq_knn_topk(const void* D, void* outd, void* outi, long long m, int nref, long long ldD, int kk,
@@ -218,10 +218,11 @@ static PyObject* py_power_iter(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_mu_sums(PyObject*, PyObject* a) {
-  unsigned long long X, qs, rm, cs, st; int xdt, nq, d; long long n;
-  if (!PyArg_ParseTuple(a, "KiKiKKLiK", &X, &xdt, &qs, &nq, &rm, &cs, &n, &d, &st)) return nullptr;
+  unsigned long long X, qs, rm, cs, part, st; int xdt, nq, pw, d; long long n;
+  if (!PyArg_ParseTuple(a, "KiKiKKKiLiK", &X, &xdt, &qs, &nq, &rm, &cs, &part, &pw, &n, &d, &st))
+    return nullptr;
   CHECK(sq_mu_sums)
-  return ret(sq_mu_sums(P(X), xdt, P(qs), nq, P(rm), P(cs), n, d, P(st)));
+  return ret(sq_mu_sums(P(X), xdt, P(qs), nq, P(rm), P(cs), P(part), pw, n, d, P(st)));
 }
 
 static PyObject* py_row_norms(PyObject*, PyObject* a) {

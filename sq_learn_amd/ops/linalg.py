@@ -85,8 +85,11 @@ def mu_power_sums_local(X, exponents):
         qd = q.to(X.device)
         rowmax = torch.zeros(nq, dtype=torch.float32, device=X.device)
         colsum = torch.zeros((nq, d), dtype=torch.float32, device=X.device)
+        wgs = 1024   # per-WG partials, summed in a fixed order (deterministic)
+        part = torch.empty((wgs, nq, d), dtype=torch.float32, device=X.device)
         nat.native().mu_sums(X.data_ptr(), nat.dtype_code(X), qd.data_ptr(), nq, rowmax.data_ptr(),
-                             colsum.data_ptr(), n, d, nat.stream_handle(X.device))
+                             colsum.data_ptr(), part.data_ptr(), wgs, n, d,
+                             nat.stream_handle(X.device))
         return rowmax.double(), colsum.double()
     A = X.abs().to(torch.float64)
     rowmax = torch.zeros(nq, dtype=torch.float64, device=X.device)

@@ -261,3 +261,19 @@ def test_gram_power_mu_rownorm(cuda):
     assert torch.allclose(cs.cpu(), cs2, rtol=1e-4)
     rn = L.row_norms_sq(X.to(torch.bfloat16))
     assert torch.allclose(rn.double().cpu(), (X.to(torch.bfloat16).double() ** 2).sum(1).cpu(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("d,dtype", [(32, torch.bfloat16), (30, torch.float32), (128, torch.bfloat16),
+                                     (256, torch.float32), (5, torch.float32)])
+def test_mu_power_sums_shapes(cuda, d, dtype):
+    n = 50_003
+    X = (torch.randn(n, d, device=cuda) * 3).to(dtype)
+    X[::7, 0] = 0   # zeros: q = 0 counts nonzeros
+    exps = [0.0, 0.1, 0.2, 1.0, 1.8, 1.9, 2.0]
+    rm, cs = L.mu_power_sums_local(X, exps)
+    rm2, cs2 = L.mu_power_sums_local(X.float().cpu(), exps)
+    assert torch.allclose(rm.cpu(), rm2, rtol=2e-4)
+    assert torch.allclose(cs.cpu(), cs2, rtol=2e-4)
+    # deterministic (no float atomics in the column sums)
+    rm3, cs3 = L.mu_power_sums_local(X, exps)
+    assert torch.equal(cs, cs3) and torch.equal(rm, rm3)
