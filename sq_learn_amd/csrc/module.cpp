@@ -20,6 +20,10 @@ __attribute__((weak)) int sq_ae_batch(const void*, const void*, void*, long long
                 unsigned, unsigned long long, void*);
 __attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long, unsigned, unsigned, unsigned, unsigned,
                 unsigned long long, void*);
+// tomography.hip
+__attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int, int, const void*,
+                                        void*, void*, int, unsigned, unsigned, unsigned, unsigned,
+                                        long long, void*);
 // failure.hip
 __attribute__((weak)) int sq_failure_inject(void*, long long, int, double, int, unsigned, unsigned,
                                             unsigned, unsigned, unsigned, unsigned, unsigned,
@@ -132,6 +136,17 @@ static PyObject* py_band_select(PyObject*, PyObject* a) {
   CHECK(sq_band_select)
   return ret(sq_band_select(P(D), P(rows), P(xn), P(lab), P(mind), m, k, ld, delta, k0, k1, s0, s1,
                             roff, P(st)));
+}
+
+static PyObject* py_tomography(PyObject*, PyObject* a) {
+  unsigned long long V, sched, first, err, out, st; int r, d, T, mode, ninf; long long roff;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KiiKiiKKKiIIIILK", &V, &r, &d, &sched, &T, &mode, &first, &err, &out,
+                        &ninf, &k0, &k1, &s0, &s1, &roff, &st))
+    return nullptr;
+  CHECK(sq_tomography)
+  return ret(sq_tomography(P(V), r, d, P(sched), T, mode, P(first), P(err), P(out), ninf, k0, k1,
+                           s0, s1, roff, P(st)));
 }
 
 static PyObject* py_failure_inject(PyObject*, PyObject* a) {
@@ -258,6 +273,7 @@ static PyMethodDef methods[] = {
     {"band_select", py_band_select, METH_VARARGS, "delta-band selection over distance rows"},
     {"band_select_rows", py_band_select_rows, METH_VARARGS, "device-driven overflow fallback"},
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
+    {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},

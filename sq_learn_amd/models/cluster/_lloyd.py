@@ -300,10 +300,11 @@ class LloydEngine:
 
     def _true_tomography_centers(self):
         """Real (shot-based) tomography of the k centre rows with error delta/2,
-        replicated on every rank (seeded on the host)."""
+        replicated on every rank (Philox-keyed: identical everywhere); on the
+        GPU one batched HIP launch pair (csrc/tomography.hip), no host trip."""
         from ...quantum.device import tomography_rows_torch
         key = self._key("tomography")
-        C = self.C.double().cpu()
+        C = self.C.double()
         est = tomography_rows_torch(C, self.delta / 2.0, key, **self.tomography_kw)
         self.set_centers(est.to(self.C.dtype))
 

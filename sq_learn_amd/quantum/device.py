@@ -82,6 +82,12 @@ def tomography_rows_torch(A, delta, key: RngKey, norm="L2", N=None,
     else:
         sched = np.array([int(N)], dtype=np.int64)
     T = len(sched)
+    if dev.type == "cuda" and d + 1 <= 512:
+        out = _tomography_rows_native(V.contiguous(), sched, delta, key, norm,
+                                      incremental_measure and stop_when_reached_accuracy)
+        if preserve_norm:
+            out = out * nrm[:, None]
+        return out[0] if squeeze else out
     shots = torch.as_tensor(sched, dtype=torch.float64, device=dev)
     # batch = rows x checkpoints
     Vb = V[:, None, :].expand(r, T, d).reshape(r * T, d)
@@ -107,6 +113,33 @@ def tomography_rows_torch(A, delta, key: RngKey, norm="L2", N=None,
     if preserve_norm:
         out = out * nrm[:, None]
     return out[0] if squeeze else out
+
+
+def _tomography_rows_native(V, sched, delta, key: RngKey, norm, stop):
+    """HIP path (csrc/tomography.hip): errors of every checkpoint in one
+    launch, first passing checkpoint per row on the device, then the chosen
+    estimates regenerated (same Philox words) in a second launch."""
+    from ..ops import _native as nat
+    r, d = V.shape
+    T = len(sched)
+    dev = V.device
+    sch = torch.as_tensor(np.asarray(sched, dtype=np.int64), device=dev)
+    err = torch.empty((r, T), dtype=torch.float64, device=dev)
+    out = torch.empty((r, d), dtype=torch.float64, device=dev)
+    st = nat.stream_handle(dev)
+    ninf = 0 if norm == "L2" else 1
+    m = nat.native()
+    if stop and T > 1:
+        m.tomography(V.data_ptr(), r, d, sch.data_ptr(), T, 0, 0, err.data_ptr(), 0, ninf,
+                     key.k0, key.k1, key.s0, key.s1, 0, st)
+        ok = err <= float(delta)
+        first = torch.where(ok.any(1), ok.to(torch.int8).argmax(1),
+                            torch.full((r,), T - 1, device=dev)).to(torch.int32).contiguous()
+    else:
+        first = torch.full((r,), T - 1, dtype=torch.int32, device=dev)
+    m.tomography(V.data_ptr(), r, d, sch.data_ptr(), T, 1, first.data_ptr(), 0, out.data_ptr(),
+                 ninf, key.k0, key.k1, key.s0, key.s1, 0, st)
+    return out
 
 
 def tomography(A, noise, key: RngKey, true_tomography=True, preserve_norm=False, **kw):

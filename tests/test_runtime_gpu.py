@@ -57,3 +57,35 @@ def test_gpu_fit_checkpoint_resume(cuda, tmp_path):
     np.testing.assert_array_equal(got.cluster_centers_, ref.cluster_centers_)
     np.testing.assert_array_equal(got.labels_, ref.labels_)
     assert got.n_failed_rows_ > 0
+
+
+def test_tomography_kernel_matches_law(cuda):
+    """HIP tomography (K12) vs the torch implementation of the same law."""
+    from sq_learn_amd.quantum import device as QD
+    g = torch.Generator().manual_seed(0)
+    d, rows = 64, 3000
+    v = torch.randn(d, generator=g, dtype=torch.float64)
+    v /= v.norm()
+    A = v[None, :].repeat(rows, 1)
+    key = RngKey(5, "tomography", 1)
+    # fixed N (no schedule): magnitudes are unbiased, norms are exactly 1
+    N = 4000
+    est = QD.tomography_rows_torch(A.to(cuda), 0.3, key, N=N, incremental_measure=False)
+    torch.cuda.synchronize()
+    est = est.cpu()
+    assert torch.allclose(est.norm(dim=1), torch.ones(rows, dtype=torch.float64), atol=1e-12)
+    m2 = (est ** 2).mean(0)
+    assert torch.allclose(m2, v ** 2, atol=4 * (v ** 2 / N / rows).sqrt().max().item() + 1e-4)
+    big = v.abs() > 0.15
+    assert (torch.sign(est[:, big]) == torch.sign(v[big])).double().mean() > 0.99
+    # incremental schedule + stopping rule: errors within delta, same law as torch
+    e_gpu = QD.tomography_rows_torch(A.to(cuda), 0.3, key).cpu()
+    e_cpu = QD.tomography_rows_torch(A[:500], 0.3, key)
+    err_g = (e_gpu - A).norm(dim=1)
+    err_c = (e_cpu - A[:500]).norm(dim=1)
+    assert (err_g <= 0.3 + 1e-12).double().mean() > 0.99
+    assert abs(err_g.mean().item() - err_c.mean().item()) < 0.03
+    # deterministic, and distinct rows get distinct draws
+    e2 = QD.tomography_rows_torch(A.to(cuda), 0.3, key).cpu()
+    assert torch.equal(e_gpu, e2)
+    assert not torch.equal(e_gpu[0], e_gpu[1])
