@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(256) centroid_finalize_kernel(
   if ((tid & 63) == 0) { red[tid >> 6] = sh; redf[tid >> 6] = nn; }
   __syncthreads();
   if (tid == 0) {
-    atomicAdd(shift, red[0] + red[1] + red[2] + red[3]);
+    shift[j] = red[0] + red[1] + red[2] + red[3];   // per-centroid part (fixed-order sum)
     float t = redf[0] + redf[1] + redf[2] + redf[3];
     cn[j] = t;
     uint16_t hi = f32_to_bf16_rne(t);
@@ -1045,18 +1045,20 @@ int sq_sum_partials(const void* part, int n, void* out, void* stream) {
 }
 
 int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
-                         void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
-                         unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
-                         void* stream) {
-  (void)C_lo;
+                         void* shift_part, void* cn, void* shift, int k, int d, int k_pad,
+                         double noise_b, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
+                         int empty_policy, void* stream) {
+  if (!shift_part) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   float b = (float)noise_b;
   float eb = erff(b * 0.70710678118654752f);
   int d_pad = d <= 16 ? 16 : (d <= 32 ? 32 : (d <= 64 ? 64 : (d <= 128 ? 128 : (d <= 256 ? 256 : ((d + 15) / 16) * 16))));
   hipLaunchKernelGGL(centroid_finalize_kernel, dim3((unsigned)k_pad), dim3(256), 0,
                      (hipStream_t)stream, (const double*)packed, (const float*)C_old,
-                     (float*)C_new, (uint16_t*)C_bf16, (float*)cn, (double*)shift, k, d, d_pad, b,
-                     eb, key, empty_policy);
+                     (float*)C_new, (uint16_t*)C_bf16, (float*)cn, (double*)shift_part, k, d,
+                     d_pad, b, eb, key, empty_policy);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                     (const double*)shift_part, k, (double*)shift);
   return (int)hipGetLastError();
 }
 

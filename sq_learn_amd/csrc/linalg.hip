@@ -4,7 +4,8 @@
 // gram       : G += (X-mu)^T (X-mu) over a row range, exact fp32 MFMA
 //              (v_mfma_f32_16x16x4_f32); one pass over X, centring fused into
 //              the LDS staging; upper-triangular 64x64 output tiles, split-K
-//              over row ranges, partials combined with 256-B f32 atomics.
+//              over row ranges, per-split partial tiles summed in a fixed
+//              order (no float atomics: deterministic).
 // power_iter : Z += (X-mu)^T ((X-mu) Q) fused - the randomized range-finder
 //              power iteration reads X once per iteration; Y never touches HBM
 //              (phase 1 Y = Xc Q per wave -> LDS, phase 2 Z += Xc^T Y).
@@ -27,10 +28,40 @@ template <> SQ_DEV float ld1<uint16_t>(const uint16_t* p, size_t i) { return bf1
 constexpr int GT = 64;
 constexpr int GRS = 64;
 
+template <typename T> SQ_DEV void ld4(const T* p, float v[4]);
+template <> SQ_DEV void ld4<float>(const float* p, float v[4]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+template <> SQ_DEV void ld4<uint16_t>(const uint16_t* p, float v[4]) {
+  uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+}
+
+// G (upper tiles, then mirrored on the host) = sum over splits, fixed order
+__global__ void __launch_bounds__(256) gram_reduce_kernel(const float* __restrict__ part,
+                                                          int splits, int tiles, int side, int d,
+                                                          float* __restrict__ G) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)tiles * GT * GT) return;
+  const int tile0 = (int)(idx / (GT * GT));
+  const int e = (int)(idx % (GT * GT));
+  int tile = tile0, ta = 0;
+  while (tile >= side - ta) { tile -= side - ta; ++ta; }
+  const int tb = ta + tile;
+  const int ra = ta * GT + e / GT, cb = tb * GT + e % GT;
+  if (ra >= d || cb >= d) return;
+  float s = 0.f;
+  for (int sp = 0; sp < splits; ++sp) s += part[((size_t)sp * tiles + tile0) * GT * GT + e];
+  G[(size_t)ra * d + cb] = s;
+}
+
 template <typename T>
-__global__ void __launch_bounds__(256) gram_kernel(const T* __restrict__ X, float* __restrict__ G,
+__global__ void __launch_bounds__(256) gram_kernel(const T* __restrict__ X, float* __restrict__ part,
                                                    const float* __restrict__ mean, long long n,
                                                    int d, int n_tiles_side, long long rows_per_split) {
+  const bool vec4 = (d % 4) == 0;
   __shared__ float As[GRS][GT + 1];
   __shared__ float Bs[GRS][GT + 1];
   // decode upper-triangular tile id
@@ -49,17 +80,34 @@ __global__ void __launch_bounds__(256) gram_kernel(const T* __restrict__ X, floa
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (long long r = r_beg; r < r_end; r += GRS) {
-    // stage (coalesced: consecutive threads -> consecutive features)
-    for (int e = tid; e < GRS * GT; e += 256) {
-      int rr = e / GT, c = e % GT;
-      long long row = r + rr;
-      float va = 0.f, vb = 0.f;
+    // stage: 4 consecutive features per thread (vector loads when aligned)
+    for (int e = tid * 4; e < GRS * GT; e += 256 * 4) {
+      const int rr = e / GT, c = e % GT;
+      const long long row = r + rr;
+      float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
       if (row < r_end) {
-        if (a0 + c < d) va = ld1<T>(X, (size_t)row * d + a0 + c) - mean[a0 + c];
-        if (b0 + c < d) vb = ld1<T>(X, (size_t)row * d + b0 + c) - mean[b0 + c];
+        const T* xr = X + (size_t)row * d;
+        if (vec4 && a0 + c + 4 <= d) {
+          ld4<T>(xr + a0 + c, va);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) va[q] -= mean[a0 + c + q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (a0 + c + q < d) va[q] = ld1<T>(xr, a0 + c + q) - mean[a0 + c + q];
+        }
+        if (vec4 && b0 + c + 4 <= d) {
+          ld4<T>(xr + b0 + c, vb);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) vb[q] -= mean[b0 + c + q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (b0 + c + q < d) vb[q] = ld1<T>(xr, b0 + c + q) - mean[b0 + c + q];
+        }
       }
-      As[rr][c] = va;
-      Bs[rr][c] = vb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { As[rr][c + q] = va[q]; Bs[rr][c + q] = vb[q]; }
     }
     __syncthreads();
 #pragma unroll 4
@@ -85,9 +133,11 @@ __global__ void __launch_bounds__(256) gram_kernel(const T* __restrict__ X, floa
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        int ra = a0 + wa + i * 16 + (lane >> 4) * 4 + g;
-        int cb = b0 + wb + j * 16 + (lane & 15);
-        if (ra < d && cb < d) atomicAdd(&G[(size_t)ra * d + cb], acc[i][j][g]);
+        // per-split partial tile (no atomics); gram_reduce_kernel sums the
+        // splits in a fixed order -> deterministic Gram matrix
+        const int la = wa + i * 16 + (lane >> 4) * 4 + g;
+        const int lb = wb + j * 16 + (lane & 15);
+        part[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * GT + la) * GT + lb] = acc[i][j][g];
       }
 }
 
@@ -174,8 +224,18 @@ __global__ void __launch_bounds__(256, 1) power_iter_kernel(
       for (int g = 0; g < 4; ++g) {
         int f = (wave * FB + i) * 16 + (lane >> 4) * 4 + g;
         int c = j * 16 + (lane & 15);
-        if (f < d && c < l) atomicAdd(&Z[(size_t)f * l + c], z[i][j][g]);
+        // per-WG partial (no atomics): summed in a fixed order by pi_reduce_kernel
+        if (f < d && c < l) Z[((size_t)blockIdx.x * d + f) * l + c] = z[i][j][g];
       }
+}
+
+__global__ void __launch_bounds__(256) pi_reduce_kernel(const float* __restrict__ part, int wgs,
+                                                        int dl, float* __restrict__ Z) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= dl) return;
+  float s = 0.f;
+  for (int w = 0; w < wgs; ++w) s += part[(size_t)w * dl + idx];
+  Z[idx] = s;
 }
 
 // ------------------------------------------------------------------ mu
@@ -352,50 +412,57 @@ using namespace sq;
 
 template <typename T, int DP, int LP>
 static int launch_pi(const void* X, const void* Q, void* Z, const void* mean, long long n, int d,
-                     int l, hipStream_t st) {
+                     int l, void* part, int part_wgs, hipStream_t st) {
   size_t lds = ((size_t)64 * (DP + 1) + (size_t)DP * LP + (size_t)64 * (LP + 1)) * 4;
   auto kern = power_iter_kernel<T, DP, LP>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  long long wgs = min(1024LL, max(1LL, (n + 1023) / 1024));
+  long long wgs = min((long long)part_wgs, max(1LL, (n + 1023) / 1024));
   long long rpw = ((n + wgs - 1) / wgs + 63) / 64 * 64;
   wgs = (n + rpw - 1) / rpw;
   hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(256), lds, st, (const T*)X, (const float*)Q,
-                     (float*)Z, (const float*)mean, n, d, l, rpw);
+                     (float*)part, (const float*)mean, n, d, l, rpw);
+  hipLaunchKernelGGL(pi_reduce_kernel, dim3((unsigned)((d * l + 255) / 256)), dim3(256), 0, st,
+                     (const float*)part, (int)wgs, d * l, (float*)Z);
   return (int)hipGetLastError();
 }
 
 extern "C" {
 
 int sq_gram_bf16(const void* X, int xdtype, void* G, const void* mean, long long n, int d,
-                 void* stream) {
+                 void* part, long long part_cap, void* stream) {
   if (n <= 0) return 0;
   int side = (d + GT - 1) / GT;
   int tiles = side * (side + 1) / 2;
   int splits = (int)max(1LL, min(2048LL / tiles, (n + 4095) / 4096));
+  splits = (int)min((long long)splits, max(1LL, part_cap / ((long long)tiles * GT * GT)));
   long long rps = ((n + splits - 1) / splits + GRS - 1) / GRS * GRS;
   splits = (int)((n + rps - 1) / rps);
+  if ((long long)splits * tiles * GT * GT > part_cap) return (int)hipErrorInvalidValue;
   dim3 grid(tiles, splits);
   hipStream_t st = (hipStream_t)stream;
   if (xdtype == 0)
-    hipLaunchKernelGGL(gram_kernel<float>, grid, dim3(256), 0, st, (const float*)X, (float*)G,
+    hipLaunchKernelGGL(gram_kernel<float>, grid, dim3(256), 0, st, (const float*)X, (float*)part,
                        (const float*)mean, n, d, side, rps);
   else if (xdtype == 2)
     hipLaunchKernelGGL(gram_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)X,
-                       (float*)G, (const float*)mean, n, d, side, rps);
+                       (float*)part, (const float*)mean, n, d, side, rps);
   else
     return (int)hipErrorInvalidValue;
+  long long tot = (long long)tiles * GT * GT;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                     (const float*)part, splits, tiles, side, d, (float*)G);
   return (int)hipGetLastError();
 }
 
 int sq_power_iter(const void* X, int xdtype, const void* Q, void* Z, const void* mean, long long n,
-                  int d, int l, void* stream) {
+                  int d, int l, void* part, int part_wgs, void* stream) {
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (l > 64 || d > 256) return (int)hipErrorInvalidValue;
+  if (l > 64 || d > 256 || part_wgs < 1) return (int)hipErrorInvalidValue;
   int DP = d <= 64 ? 64 : (d <= 128 ? 128 : 256);
   int LP = l <= 16 ? 16 : (l <= 32 ? 32 : 64);
 #define PI_CASE(TT, D_, L_) \
-  if (DP == D_ && LP == L_) return launch_pi<TT, D_, L_>(X, Q, Z, mean, n, d, l, st);
+  if (DP == D_ && LP == L_) return launch_pi<TT, D_, L_>(X, Q, Z, mean, n, d, l, part, part_wgs, st);
   if (xdtype == 0) {
     PI_CASE(float, 64, 16) PI_CASE(float, 64, 32) PI_CASE(float, 64, 64)
     PI_CASE(float, 128, 16) PI_CASE(float, 128, 32) PI_CASE(float, 128, 64)

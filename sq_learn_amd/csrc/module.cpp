@@ -55,10 +55,10 @@ __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void
                  long long m, int k, long long ldG, double eps, int Q, unsigned k0, unsigned k1,
                  unsigned s0, unsigned s1, long long row_offset, void* stream);
 // linalg.hip
-__attribute__((weak)) int sq_gram_bf16(const void* X, int xdtype, void* G, const void* mean, long long n, int d,
-                 void* stream);
-__attribute__((weak)) int sq_power_iter(const void* X, int xdtype, const void* Q, void* Z, const void* mean, long long n,
-                  int d, int l, void* stream);
+__attribute__((weak)) int sq_gram_bf16(const void*, int, void*, const void*, long long, int, void*,
+                                       long long, void*);
+__attribute__((weak)) int sq_power_iter(const void*, int, const void*, void*, const void*, long long,
+                                        int, int, void*, int, void*);
 __attribute__((weak)) int sq_mu_sums(const void*, int, const void*, int, void*, void*, void*, int,
                                      long long, int, void*);
 __attribute__((weak)) int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream);
@@ -219,17 +219,19 @@ static PyObject* py_ipe_estep(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_gram(PyObject*, PyObject* a) {
-  unsigned long long X, G, mean, st; int xdt, d; long long n;
-  if (!PyArg_ParseTuple(a, "KiKKLiK", &X, &xdt, &G, &mean, &n, &d, &st)) return nullptr;
+  unsigned long long X, G, mean, part, st; int xdt, d; long long n, cap;
+  if (!PyArg_ParseTuple(a, "KiKKLiKLK", &X, &xdt, &G, &mean, &n, &d, &part, &cap, &st))
+    return nullptr;
   CHECK(sq_gram_bf16)
-  return ret(sq_gram_bf16(P(X), xdt, P(G), P(mean), n, d, P(st)));
+  return ret(sq_gram_bf16(P(X), xdt, P(G), P(mean), n, d, P(part), cap, P(st)));
 }
 
 static PyObject* py_power_iter(PyObject*, PyObject* a) {
-  unsigned long long X, Q, Z, mean, st; int xdt, d, l; long long n;
-  if (!PyArg_ParseTuple(a, "KiKKKLiiK", &X, &xdt, &Q, &Z, &mean, &n, &d, &l, &st)) return nullptr;
+  unsigned long long X, Q, Z, mean, part, st; int xdt, d, l, pw; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKLiiKiK", &X, &xdt, &Q, &Z, &mean, &n, &d, &l, &part, &pw, &st))
+    return nullptr;
   CHECK(sq_power_iter)
-  return ret(sq_power_iter(P(X), xdt, P(Q), P(Z), P(mean), n, d, l, P(st)));
+  return ret(sq_power_iter(P(X), xdt, P(Q), P(Z), P(mean), n, d, l, P(part), pw, P(st)));
 }
 
 static PyObject* py_mu_sums(PyObject*, PyObject* a) {

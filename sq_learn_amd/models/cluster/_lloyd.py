@@ -110,6 +110,7 @@ class LloydEngine:
         self.counts = torch.zeros(self.k, dtype=torch.float64, device=dev)
         self.packed = torch.zeros(self.k * self.d + self.k + 1, dtype=torch.float64, device=dev)
         self.shift = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.shift_part = torch.zeros(self.k, dtype=torch.float64, device=dev)
         self.C = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
         self.C_new = torch.zeros_like(self.C)
         self.C_bf16 = torch.zeros(K.operand_shape(self.k_pad, self.d_pad), dtype=torch.bfloat16, device=dev)
@@ -237,10 +238,10 @@ class LloydEngine:
             with tracing.range("allreduce"):
                 self.comm.all_reduce_(self.packed)
             with tracing.range("finalize"):
-                self.shift.zero_()
                 K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
                                            self.shift, self.k, self.d, self._noise_bound(),
-                                           noise_key, self.empty_policy)
+                                           noise_key, self.empty_policy,
+                                           shift_part=self.shift_part)
                 self.C, self.C_new = self.C_new, self.C
                 if self.intermediate_error and self.true_tomography and self.delta > 0:
                     self._true_tomography_centers()

@@ -291,12 +291,18 @@ def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, 
 
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
-                             empty_policy=0):
+                             empty_policy=0, shift_part=None):
+    """shift[0] = sum_j ||c_j' - c_j||^2 (per-centroid parts summed in a fixed
+    order: deterministic); ``shift_part`` is a k-double workspace."""
     k_pad = C_bf16.shape[0] * 64
+    if shift_part is None:
+        shift_part = torch.empty(max(k, 1), dtype=torch.float64, device=packed.device)
+    assert shift_part.numel() >= k and shift_part.dtype == torch.float64
     nat.native().centroid_finalize(packed.data_ptr(), C_old.data_ptr(), C_new.data_ptr(),
-                                   C_bf16.data_ptr(), 0, cn.data_ptr(), shift.data_ptr(), k, d,
-                                   k_pad, float(noise_b), key.k0, key.k1, key.s0, key.s1,
-                                   int(empty_policy), nat.stream_handle(packed.device))
+                                   C_bf16.data_ptr(), shift_part.data_ptr(), cn.data_ptr(),
+                                   shift.data_ptr(), k, d, k_pad, float(noise_b), key.k0, key.k1,
+                                   key.s0, key.s1, int(empty_policy),
+                                   nat.stream_handle(packed.device))
 
 
 def operand_shape(k_pad, d_pad):

@@ -38,8 +38,12 @@ def gram_local(X, mean):
         X = X.contiguous()
         G = torch.zeros((d, d), dtype=torch.float32, device=X.device)
         m = mean.to(torch.float32).contiguous()
+        # per-split partial tiles, reduced in a fixed order (deterministic)
+        side = (d + 63) // 64
+        cap = max(1, 2048 // (side * (side + 1) // 2)) * (side * (side + 1) // 2) * 64 * 64
+        part = torch.empty(cap, dtype=torch.float32, device=X.device)
         nat.native().gram(X.data_ptr(), nat.dtype_code(X), G.data_ptr(), m.data_ptr(), n, d,
-                          nat.stream_handle(X.device))
+                          part.data_ptr(), cap, nat.stream_handle(X.device))
         # kernel fills the upper triangle tiles; mirror
         iu = torch.triu_indices(d, d, 1, device=X.device)
         G[iu[1], iu[0]] = G[iu[0], iu[1]]
@@ -57,8 +61,11 @@ def power_iter_local(X, Q, mean):
         Z = torch.zeros((d, l), dtype=torch.float32, device=X.device)
         Qc = Q.to(torch.float32).contiguous()
         m = mean.to(torch.float32).contiguous()
+        wgs = 256   # per-WG partials summed in a fixed order (deterministic)
+        part = torch.empty((wgs, d, l), dtype=torch.float32, device=X.device)
         nat.native().power_iter(X.data_ptr(), nat.dtype_code(X), Qc.data_ptr(), Z.data_ptr(),
-                                m.data_ptr(), n, d, l, nat.stream_handle(X.device))
+                                m.data_ptr(), n, d, l, part.data_ptr(), wgs,
+                                nat.stream_handle(X.device))
         return Z
     acc = torch.float64 if X.device.type == "cpu" else torch.float32
     Z = torch.zeros((d, l), dtype=acc, device=X.device)

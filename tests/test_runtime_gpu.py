@@ -89,3 +89,26 @@ def test_tomography_kernel_matches_law(cuda):
     e2 = QD.tomography_rows_torch(A.to(cuda), 0.3, key).cpu()
     assert torch.equal(e_gpu, e2)
     assert not torch.equal(e_gpu[0], e_gpu[1])
+
+
+def test_gpu_fits_are_bit_reproducible(cuda):
+    """No float atomics feed any fitted quantity: two fits are identical."""
+    from sq_learn_amd.cluster import QMeans
+    from sq_learn_amd.decomposition import QPCA
+    from sq_learn_amd.ops import linalg as L
+    from sq_learn_amd.utils.datasets import make_blobs_device
+    X, _ = make_blobs_device(200_000, 64, centers=50, seed=3, device=cuda, dtype=torch.bfloat16)
+    kw = dict(n_clusters=50, n_init=1, max_iter=6, tol=0.0, delta=0.3, random_state=0,
+              true_distance_estimate=False, intermediate_error=True, true_tomography=True)
+    a = QMeans(**kw).fit(X)
+    b = QMeans(**kw).fit(X)
+    np.testing.assert_array_equal(a.cluster_centers_, b.cluster_centers_)
+    np.testing.assert_array_equal(a.labels_, b.labels_)
+    assert a.inertia_ == b.inertia_ and a.muA == b.muA
+    mean = X.float().mean(0)
+    assert torch.equal(L.gram_local(X, mean), L.gram_local(X, mean))
+    Q = torch.randn(64, 24, device=cuda)
+    assert torch.equal(L.power_iter_local(X, Q, mean), L.power_iter_local(X, Q, mean))
+    p1 = QPCA(n_components=8, svd_solver="randomized", random_state=0, device=cuda).fit(X)
+    p2 = QPCA(n_components=8, svd_solver="randomized", random_state=0, device=cuda).fit(X)
+    np.testing.assert_array_equal(p1.singular_values_, p2.singular_values_)
