@@ -23,7 +23,7 @@ import sysconfig
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CSRC = os.path.join(HERE, "csrc")
+CSRC = os.environ.get("SQ_CSRC_DIR", os.path.join(HERE, "csrc"))   # override: A/B kernel variants
 BUILD = os.path.join(HERE, "..", "build", "sq_native")
 ARCH = os.environ.get("SQ_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
