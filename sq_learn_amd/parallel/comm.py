@@ -39,7 +39,9 @@ def init_distributed(backend=None, timeout_s=600, device=None):
         return Comm(None)
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # SQ_DIST_BACKEND=gloo rehearses multi-rank GPU runs on one device
+            backend = os.environ.get("SQ_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
