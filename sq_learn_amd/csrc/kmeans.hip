@@ -131,6 +131,15 @@ SQ_DEV int band_pick_wave(DistF dist, int k, float thr, float u, int lane) {
 #ifndef SQ_ESTEP_PF
 #define SQ_ESTEP_PF 1
 #endif
+#ifndef SQ_ESTEP_PAIR
+#define SQ_ESTEP_PAIR 0
+#endif
+// compile-time ablations (timing experiments only; results invalid):
+// bit 1 = no centroid staging after tile 1, bit 2 = no top-2 epilogue.
+// Compile-time so that no runtime branch splits the pipelined basic block.
+#ifndef SQ_ESTEP_ABLATE
+#define SQ_ESTEP_ABLATE 0
+#endif
 template <int KSD, int NW>
 __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, float* __restrict__ ovf_thr,
@@ -138,6 +147,7 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     long long* __restrict__ ovf_rows, int* __restrict__ ovf_count, double* __restrict__ inertia,
     long long n, int k, int k_pad, float delta, RngKey key, long long row_offset, int ovf_cap,
     int idx_bits, int dbg) {
+  (void)dbg;
   (void)k;
   constexpr int KS = KSD + 1;            // data k-steps + augmented norm step
   constexpr int DX = KSD * 16;           // X row length (padded features)
@@ -147,7 +157,10 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
   constexpr int ROWS = NW * 32;          // rows per block
   constexpr int PF = SQ_ESTEP_PF;        // B-fragment prefetch distance (k-steps)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * TILE_BYTES; };
+  // ring of RING tile slots; PAIR mode stages two tiles per DMA round and
+  // synchronises the workgroup once per two tiles (half the barriers)
+  constexpr int RING = SQ_ESTEP_PAIR ? 4 : 2;
+  auto buf = [&](int g) -> unsigned char* { return smem + (g & (RING - 1)) * TILE_BYTES; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -166,7 +179,7 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     const int t = (int)(G % n_tiles);
     const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_BYTES;
     unsigned char* dst = buf(G);
-    if ((dbg & 2) && G > 1) return;   // ablation: no centroid staging
+    if ((SQ_ESTEP_ABLATE & 2) && G > 1) return;   // ablation: no centroid staging
     for (int p = wave; p < PIECES; p += NW) {
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
@@ -204,7 +217,25 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
                        const f32x16& o0, const f32x16& o1acc, int t_prev, bool do_epi) {
     const uint32_t j0 = (uint32_t)(t_prev * kBN + r32);
     const uint32_t j1 = j0 + 32;
+    const bool epi = do_epi && !(SQ_ESTEP_ABLATE & 4);
+    // top-2 update of row i of the previous tile (3 VALU per value)
+    auto epi_row = [&](int i) {
+      float p0 = packf(o0[i], keep, j0);
+      float p1 = packf(o1acc[i], keep, j1);
+      float q1 = m1[i];
+      float q2 = m2[i];
+      q2 = med3_raw(q1, p0, q2);
+      q1 = min_raw(q1, p0);
+      q2 = med3_raw(q1, p1, q2);
+      q1 = min_raw(q1, p1);
+      m1[i] = q1;
+      m2[i] = q2;
+    };
     if (do_mfma) {
+      // explicit software pipeline: the source order IS the schedule
+      // (sched_barrier after every k-step): B reads PF k-steps ahead, the two
+      // MFMAs of the k-step, then the slice of the previous tile's epilogue
+      // that runs in their shadow
       f32x16 acc0 = {0}, acc1 = {0};
       bf16x8 b0[PF + 1], b1[PF + 1];
 #pragma unroll
@@ -217,34 +248,17 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
         }
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b0[ks % (PF + 1)], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks], b1[ks % (PF + 1)], acc1, 0, 0, 0);
+        if (epi) {
+#pragma unroll
+          for (int i = (ks * 16) / KS; i < ((ks + 1) * 16) / KS; ++i) epi_row(i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       n0 = acc0;
       n1 = acc1;
-    }
-    if (do_epi && !(dbg & 4)) {   // dbg bit 2: ablation, no epilogue
+    } else if (epi) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p0 = packf(o0[i], keep, j0);
-        float p1 = packf(o1acc[i], keep, j1);
-        float q1 = m1[i];
-        float q2 = m2[i];
-        q2 = med3_raw(q1, p0, q2);
-        q1 = min_raw(q1, p0);
-        q2 = med3_raw(q1, p1, q2);
-        q1 = min_raw(q1, p1);
-        m1[i] = q1;
-        m2[i] = q2;
-      }
-    }
-    if (do_mfma && do_epi) {
-      // [2 PF B reads] then per k-step [2 B reads][2 MFMA][~6 VALU]
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (PF < KS ? PF : KS), 0);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        if (ks + PF < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, (96 + KS - 1) / KS, 0);
-      }
+      for (int i = 0; i < 16; ++i) epi_row(i);
     }
   };
   auto sync_tile = [&]() {
@@ -257,8 +271,21 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     a1 = min_raw(a1, b1);
   };
 
+  // hooks around the MFMA of tile Gc: issue the next DMA, then synchronise
+  auto pre_tile = [&](int Gc) {
+    if (SQ_ESTEP_PAIR) {
+      if ((Gc & 1) == 0) { stage(Gc + 2); stage(Gc + 3); }
+    } else {
+      stage(Gc + 1);
+    }
+  };
+  auto post_tile = [&](int Gc) {
+    if (!SQ_ESTEP_PAIR || (Gc & 1)) sync_tile();
+  };
+
   int G = 0;   // global tile sequence number: tile G lives in buf(G)
   stage(0);
+  if (SQ_ESTEP_PAIR) stage(1);
   load_a(blk);
   sync_tile();
   double my_inertia = 0.0;
@@ -269,9 +296,9 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     for (int i = 0; i < 16; ++i) { m1[i] = __builtin_inff(); m2[i] = __builtin_inff(); }
     f32x16 pA0, pA1, pB0, pB1;
     // block prologue: tile G (landed) -> pA while tile G+1 streams in
-    stage(G + 1);
+    pre_tile(G);
     tile_step(buf(G), pA0, pA1, true, pA0, pA1, 0, false);
-    sync_tile();
+    post_tile(G);
     // steady state: every combined step is ONE basic block (unconditional MFMA
     // + epilogue) so the scheduler can interleave them; static pA/pB names by
     // unrolling two steps; the block's last epilogue runs alone, after the
@@ -283,9 +310,9 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
         tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
         break;
       }
-      stage(G + 2);
+      pre_tile(G + 1);
       tile_step(buf(G + 1), pB0, pB1, true, pA0, pA1, t, true);
-      sync_tile();
+      post_tile(G + 1);
       ++t;
       ++G;
       if (t + 1 >= n_tiles) {
@@ -293,9 +320,9 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
         tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
         break;
       }
-      stage(G + 2);
+      pre_tile(G + 1);
       tile_step(buf(G + 1), pA0, pA1, true, pB0, pB1, t, true);
-      sync_tile();
+      post_tile(G + 1);
       ++t;
       ++G;
     }
@@ -341,7 +368,7 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
     // (lane r32 holds the candidates j = r32 mod 32, so lane order is kappa
     // order); a lane holding two members -> exact fallback (overflow list)
     const unsigned long long slow = __ballot(owner && band2);
-    if (slow && !dbg) {   // (ablation runs skip band resolution)
+    if (slow && !SQ_ESTEP_ABLATE) {   // (ablation runs skip band resolution)
       const float urow = band_u(key, row_offset + grow_local);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -377,6 +404,253 @@ __global__ void __launch_bounds__(NW * 64, 2) estep_kernel(
   my_inertia = wave_sum(my_inertia);
   if (lane == 0) inertia[(size_t)blockIdx.x * NW + wave] = my_inertia;
   // drain the ring's surplus prefetch before the LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// estep64: the same E-step with 64 rows per wave (two 32-row MFMA blocks
+// sharing every B fragment) at one wave per SIMD (up to 512 registers):
+// half the LDS traffic per MFMA, room for a 3-deep B ring and for both
+// accumulator sets of the cross-tile pipeline, so the top-2 epilogue of tile
+// t can actually be interleaved with the MFMAs of tile t+1 (the 32-row
+// kernel runs at the 256-register limit of two waves per SIMD and the
+// compiler serialises both).  4 waves per workgroup, 256 rows per block.
+struct Acc4 {
+  f32x16 v[2][2];   // [row block][column block]
+};
+
+template <int KSD>
+__global__ void __launch_bounds__(256, 1) estep64_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ C, float* __restrict__ ovf_thr,
+    const float* __restrict__ xn, int* __restrict__ labels, float* __restrict__ mind,
+    long long* __restrict__ ovf_rows, int* __restrict__ ovf_count, double* __restrict__ inertia,
+    long long n, int k, int k_pad, float delta, RngKey key, long long row_offset, int ovf_cap,
+    int idx_bits, int dbg) {
+  (void)k;
+  constexpr int NW = 4;
+  constexpr int KS = KSD + 1;
+  constexpr int DX = KSD * 16;
+  constexpr int CPR = KS * 2;
+  constexpr int TILE_BYTES = kBN * CPR * 16;
+  constexpr int PIECES = TILE_BYTES / 1024;
+  constexpr int ROWS = NW * 64;
+  constexpr int PF = SQ_ESTEP_PF + 1;    // B prefetch distance (k-steps)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * TILE_BYTES; };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int half = lane >> 5;
+  const uint32_t keep = ~((1u << idx_bits) - 1u);
+  const int n_tiles = k_pad / kBN;
+  const long long nblk = (n + ROWS - 1) / ROWS;
+  long long blk = blockIdx.x;
+  if (blk >= nblk) return;
+  (void)dbg;
+
+  auto stage = [&](int G) {
+    const int t = (int)(G % n_tiles);
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_BYTES;
+    unsigned char* dst = buf(G);
+    if ((SQ_ESTEP_ABLATE & 2) && G > 1) return;
+    for (int p = wave; p < PIECES; p += NW) {
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
+    }
+  };
+
+  bf16x8 a0[KSD], a1[KSD];
+  auto load_a = [&](long long b) {
+    const long long r = b * ROWS + wave * 64 + r32;
+    const uint16_t* x0 = X + (size_t)(r < n ? r : n - 1) * DX + half * 8;
+    const uint16_t* x1 = X + (size_t)(r + 32 < n ? r + 32 : n - 1) * DX + half * 8;
+#pragma unroll
+    for (int ks = 0; ks < KSD; ++ks) {
+      a0[ks] = *reinterpret_cast<const bf16x8*>(x0 + ks * 16);
+      a1[ks] = *reinterpret_cast<const bf16x8*>(x1 + ks * 16);
+    }
+  };
+  bf16x8 aug = (bf16x8)0;
+  if (half == 0) { aug[0] = aug[1] = aug[2] = (short)0x3f80; }
+
+  float m1[2][16], m2[2][16];
+  const int lane_off = (half * 64 + r32) * 16;
+  auto ldb = [&](const unsigned char* cur, int nb, int ks) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(cur + lane_off + ks * 2048 + nb * 512);
+  };
+  auto tile_step = [&](const unsigned char* cur, Acc4& nacc, bool do_mfma, const Acc4& oacc,
+                       int t_prev, bool do_epi) {
+    const uint32_t j0 = (uint32_t)(t_prev * kBN + r32);
+    const uint32_t j1 = j0 + 32;
+    const bool epi = do_epi && !(SQ_ESTEP_ABLATE & 4);
+    auto epi_row = [&](int q) {   // q = rb * 16 + i
+      const int rb = q >> 4, i = q & 15;
+      float p0 = packf(oacc.v[rb][0][i], keep, j0);
+      float p1 = packf(oacc.v[rb][1][i], keep, j1);
+      float q1 = m1[rb][i];
+      float q2 = m2[rb][i];
+      q2 = med3_raw(q1, p0, q2);
+      q1 = min_raw(q1, p0);
+      q2 = med3_raw(q1, p1, q2);
+      q1 = min_raw(q1, p1);
+      m1[rb][i] = q1;
+      m2[rb][i] = q2;
+    };
+    if (do_mfma) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) nacc.v[rb][nb] = (f32x16){0};
+      bf16x8 b0[PF + 1], b1[PF + 1];
+#pragma unroll
+      for (int q = 0; q < PF && q < KS; ++q) { b0[q] = ldb(cur, 0, q); b1[q] = ldb(cur, 1, q); }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + PF < KS) {
+          b0[(ks + PF) % (PF + 1)] = ldb(cur, 0, ks + PF);
+          b1[(ks + PF) % (PF + 1)] = ldb(cur, 1, ks + PF);
+        }
+        const bf16x8 A0 = ks < KSD ? a0[ks] : aug;
+        const bf16x8 A1 = ks < KSD ? a1[ks] : aug;
+        const bf16x8 B0 = b0[ks % (PF + 1)], B1 = b1[ks % (PF + 1)];
+        nacc.v[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0, nacc.v[0][0], 0, 0, 0);
+        nacc.v[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0, nacc.v[1][0], 0, 0, 0);
+        nacc.v[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1, nacc.v[0][1], 0, 0, 0);
+        nacc.v[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1, nacc.v[1][1], 0, 0, 0);
+        if (epi) {
+#pragma unroll
+          for (int q = (ks * 32) / KS; q < ((ks + 1) * 32) / KS; ++q) epi_row(q);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if (epi) {
+#pragma unroll
+      for (int q = 0; q < 32; ++q) epi_row(q);
+    }
+  };
+  auto sync_tile = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  auto merge2 = [](float& x1, float& x2, float y1, float y2) {
+    float lo2 = min_raw(x2, y2);
+    x2 = med3_raw(x1, y1, lo2);
+    x1 = min_raw(x1, y1);
+  };
+
+  int G = 0;
+  stage(0);
+  load_a(blk);
+  sync_tile();
+  double my_inertia = 0.0;
+
+  for (; blk < nblk; blk += gridDim.x) {
+    const long long row0 = blk * ROWS + wave * 64;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { m1[rb][i] = __builtin_inff(); m2[rb][i] = __builtin_inff(); }
+    Acc4 pA, pB;
+    stage(G + 1);
+    tile_step(buf(G), pA, true, pA, 0, false);
+    sync_tile();
+    int t = 0;
+    while (true) {
+      if (t + 1 >= n_tiles) {
+        load_a(blk + gridDim.x);
+        tile_step(smem, pB, false, pA, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pB, true, pA, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+      if (t + 1 >= n_tiles) {
+        load_a(blk + gridDim.x);
+        tile_step(smem, pA, false, pB, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pA, true, pB, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+    }
+    ++G;
+
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const long long rowb = row0 + rb * 32;
+      float R1[16], R2[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { R1[i] = m1[rb][i]; R2[i] = m2[rb][i]; }
+#pragma unroll
+      for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
+        const bool hi = (r32 & o) != 0;
+#pragma unroll
+        for (int j = 0; j < c; ++j) {
+          float s1 = hi ? R1[j] : R1[c + j], s2 = hi ? R2[j] : R2[c + j];
+          float k1 = hi ? R1[c + j] : R1[j], k2 = hi ? R2[c + j] : R2[j];
+          float t1 = __shfl_xor(s1, o, 64), t2 = __shfl_xor(s2, o, 64);
+          merge2(k1, k2, t1, t2);
+          R1[j] = k1;
+          R2[j] = k2;
+        }
+      }
+      float q1 = R1[0], q2 = R2[0];
+      merge2(q1, q2, __shfl_xor(R1[0], 1, 64), __shfl_xor(R2[0], 1, 64));
+      const int irow = r32 >> 1;
+      const int rloc = (irow & 3) + 8 * (irow >> 2) + 4 * half;
+      const long long grow_local = rowb + rloc;
+      const bool owner = ((r32 & 1) == 0) && grow_local < n;
+      const float mval = valf(q1, keep);
+      const float thr = mval + delta;
+      const bool band2 = valf(q2, keep) <= thr;
+      if (owner) {
+        const float dist = fmaxf(xn[grow_local] + mval, 0.0f);
+        mind[grow_local] = dist;
+        if (!band2) labels[grow_local] = (int)(__float_as_uint(q1) & ~keep);
+        my_inertia += (double)dist;
+      }
+      const unsigned long long slow = __ballot(owner && band2);
+      if (slow && !SQ_ESTEP_ABLATE) {
+        const float urow = band_u(key, row_offset + grow_local);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const unsigned long long sel = slow & ((1ull << (2 * i)) | (1ull << (32 + 2 * i)));
+          if (!sel) continue;
+          const int src = 32 * half + 2 * i;
+          const bool mine = (slow >> src) & 1ull;
+          const float thr_i = __shfl(thr, src, 64);
+          const float u_i = __shfl(urow, src, 64);
+          const bool v1 = mine && valf(m1[rb][i], keep) <= thr_i;
+          const bool v2 = mine && valf(m2[rb][i], keep) <= thr_i;
+          const uint32_t hb1 = (uint32_t)(__ballot(v1) >> (32 * half));
+          const uint32_t hb2 = (uint32_t)(__ballot(v2) >> (32 * half));
+          const int c = __popc(hb1);
+          const int pick = hb2 == 0u && c > 0 ? nth_set_bit(hb1, band_rank(u_i, c)) : 0;
+          const uint32_t jsel = (uint32_t)__shfl((int)(__float_as_uint(m1[rb][i]) & ~keep),
+                                                 32 * half + pick, 64);
+          if (mine && r32 == 2 * i) {
+            const long long g = rowb + (i & 3) + 8 * (i >> 2) + 4 * half;
+            if (hb2 != 0u) {
+              int slot = atomicAdd(ovf_count, 1);
+              if (slot < ovf_cap) { ovf_rows[slot] = g; ovf_thr[slot] = thr_i; }
+              labels[g] = -1;
+            } else {
+              labels[g] = (int)jsel;
+            }
+          }
+        }
+      }
+    }
+  }
+  my_inertia = wave_sum(my_inertia);
+  if (lane == 0) inertia[(size_t)blockIdx.x * NW + wave] = my_inertia;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -962,7 +1236,7 @@ static int launch_estep(const void* X, const void* C, const void* cn, const void
                         void* mind, void* ovf_rows, void* ovf_count, void* inertia,
                         void* part, int part_cap, long long n, int k, int k_pad, float delta,
                         RngKey key, long long row_offset, int ovf_cap, hipStream_t st) {
-  size_t lds = 2 * (size_t)kBN * (KS + 1) * 16 * 2;   // two chunk-major tiles
+  size_t lds = (SQ_ESTEP_PAIR ? 4 : 2) * (size_t)kBN * (KS + 1) * 16 * 2;   // tile ring
   auto kern = estep_kernel<KS, NW>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -994,6 +1268,41 @@ static int launch_estep(const void* X, const void* C, const void* cn, const void
   return (int)hipGetLastError();
 }
 
+template <int KS>
+static int launch_estep64(const void* X, const void* C, const void* cn, const void* xn,
+                          void* labels, void* mind, void* ovf_rows, void* ovf_count, void* inertia,
+                          void* part, int part_cap, long long n, int k, int k_pad, float delta,
+                          RngKey key, long long row_offset, int ovf_cap, hipStream_t st) {
+  constexpr int NW = 4;
+  size_t lds = 2 * (size_t)kBN * (KS + 1) * 16 * 2;
+  auto kern = estep64_kernel<KS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NW * 64, lds);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  long long rows_per_wg = NW * 64;
+  long long nblk = (n + rows_per_wg - 1) / rows_per_wg;
+  unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
+  if ((long long)grid * NW > part_cap) grid = (unsigned)(part_cap / NW);
+  if (grid == 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const uint16_t*)X,
+                     (const uint16_t*)C, (float*)cn, (const float*)xn, (int*)labels,
+                     (float*)mind, (long long*)ovf_rows, (int*)ovf_count, (double*)part, n, k,
+                     k_pad, delta, key, row_offset, ovf_cap, idx_bits_for(k_pad), estep_dbg());
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, (const double*)part,
+                     (int)grid * NW, (double*)inertia);
+  return (int)hipGetLastError();
+}
+
 extern "C" {
 
 int sq_estep_bf16(const void* X, const void* C, void* part, const void* cn, const void* xn,
@@ -1004,7 +1313,7 @@ int sq_estep_bf16(const void* X, const void* C, void* part, const void* cn, cons
   if (n <= 0) return 0;
   if (part_cap < 8) return (int)hipErrorInvalidValue;
   if (k_pad % kBN != 0 || k_pad > 32768 || k > k_pad) return (int)hipErrorInvalidValue;
-  if (2 * (size_t)kBN * (d + 16) * 2 > 160 * 1024) return (int)hipErrorInvalidValue;
+  if ((SQ_ESTEP_PAIR ? 4 : 2) * (size_t)kBN * (d + 16) * 2 > 160 * 1024) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   hipStream_t st = (hipStream_t)stream;
   float dl = (float)delta;
@@ -1014,8 +1323,14 @@ int sq_estep_bf16(const void* X, const void* C, void* part, const void* cn, cons
   int nw = 8;
   const char* env = getenv("SQ_ESTEP_NW");
   if (env && env[0] == '4') nw = 4;
+  static int rows64 = -1;
+  if (rows64 < 0) { const char* e = getenv("SQ_ESTEP_ROWS"); rows64 = (e && atoi(e) == 64) ? 1 : 0; }
+  if (rows64) nw = 64;   // estep64_kernel
 #define ESTEP_CASE(KS)                                                                           \
   case KS * 16:                                                                                  \
+    if (nw == 64)                                                                              \
+      return launch_estep64<KS>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count, inertia, part, \
+                                part_cap, n, k, k_pad, dl, key, row_offset, ovf_cap, st);        \
     return nw == 8 ? launch_estep<KS, 8>(X, C, cn, xn, labels, mind, ovf_rows, ovf_count,        \
                                          inertia, part, part_cap, n, k, k_pad, dl, key,         \
                                          row_offset, ovf_cap, st)                               \
