@@ -24,6 +24,10 @@ __attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long
 __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int, int, const void*,
                                         void*, void*, int, unsigned, unsigned, unsigned, unsigned,
                                         long long, void*);
+// elkan.hip
+__attribute__((weak)) int sq_elkan_step(const void*, const void*, const void*, const void*,
+                                        const void*, void*, void*, void*, long long, int, int,
+                                        int, int, void*);
 // failure.hip
 __attribute__((weak)) int sq_failure_inject(void*, long long, int, double, int, unsigned, unsigned,
                                             unsigned, unsigned, unsigned, unsigned, unsigned,
@@ -147,6 +151,16 @@ static PyObject* py_tomography(PyObject*, PyObject* a) {
   CHECK(sq_tomography)
   return ret(sq_tomography(P(V), r, d, P(sched), T, mode, P(first), P(err), P(out), ninf, k0, k1,
                            s0, s1, roff, P(st)));
+}
+
+static PyObject* py_elkan_step(PyObject*, PyObject* a) {
+  unsigned long long X, C, hcc, sn, sh, lab, up, lo, st; long long n; int d, k, dt, init;
+  if (!PyArg_ParseTuple(a, "KKKKKKKKLiiiiK", &X, &C, &hcc, &sn, &sh, &lab, &up, &lo, &n, &d, &k,
+                        &dt, &init, &st))
+    return nullptr;
+  CHECK(sq_elkan_step)
+  return ret(sq_elkan_step(P(X), P(C), P(hcc), P(sn), P(sh), P(lab), P(up), P(lo), n, d, k, dt,
+                           init, P(st)));
 }
 
 static PyObject* py_failure_inject(PyObject*, PyObject* a) {
@@ -274,6 +288,7 @@ static PyMethodDef methods[] = {
     {"estep_bf16", py_estep_bf16, METH_VARARGS, "fused MFMA distance + delta-band E-step"},
     {"band_select", py_band_select, METH_VARARGS, "delta-band selection over distance rows"},
     {"band_select_rows", py_band_select_rows, METH_VARARGS, "device-driven overflow fallback"},
+    {"elkan_step", py_elkan_step, METH_VARARGS, "Elkan bounded k-means assignment"},
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},

@@ -5,8 +5,12 @@ fit :842-936), ``k_means`` (:265), ``kmeans_plusplus`` (:1725).  Lloyd
 semantics follow the reference exactly: strict convergence when labels stop
 changing, else centre shift <= tol (tol scaled by the mean feature variance),
 a final E-step when not strictly converged, inertia on the final
-(labels, centres).  'elkan' is accepted and runs Lloyd (on MI355X the fused
-MFMA assignment beats triangle-inequality bounds at d >= 64).
+(labels, centres).  ``algorithm='elkan'`` runs the triangle-inequality
+engine (``_elkan.py``, HIP kernel ``csrc/elkan.hip``; exact fp32/fp64
+distances); 'auto' / 'full' / 'lloyd' run the fused MFMA Lloyd engine,
+which on MI355X beats bounds at d >= 64.  The reference's
+'auto' picks Elkan for dense data: the labels agree (both are the exact
+argmin), only the cost differs.
 Empty clusters keep their previous centre (the reference relocates the
 farthest points).
 """
@@ -24,6 +28,7 @@ from ..._config import get_config
 from .._data import as_data, global_mean_var, Data
 from ._init import kmeans_plusplus as _kpp, random_init
 from ._lloyd import LloydEngine
+from ._elkan import ElkanEngine
 from ...ops import kmeans as K
 
 
@@ -86,9 +91,18 @@ class KMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         sw = None
         if sample_weight is not None:
             sw = torch.as_tensor(np.asarray(to_numpy(sample_weight), dtype=np.float64)).to(Xc.device)
-        eng = LloydEngine(Xc, self.n_clusters, delta=0.0, sample_weight=sw, seed=seed,
-                          comm=data.comm, row_offset=data.row_offset,
-                          gemm_precision=self._precision())
+        algo = self.algorithm
+        if algo == "elkan" and self.n_clusters == 1:
+            warnings.warn("algorithm='elkan' doesn't make sense for a single cluster. Using "
+                          "'full' instead.", RuntimeWarning, stacklevel=2)
+            algo = "full"
+        if algo == "elkan":
+            eng = ElkanEngine(Xc, self.n_clusters, sample_weight=sw, seed=seed,
+                              comm=data.comm, row_offset=data.row_offset)
+        else:
+            eng = LloydEngine(Xc, self.n_clusters, delta=0.0, sample_weight=sw, seed=seed,
+                              comm=data.comm, row_offset=data.row_offset,
+                              gemm_precision=self._precision())
         best = None
         for r in range(n_init):
             eng.restart, eng.it = r, 0

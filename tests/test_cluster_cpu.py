@@ -178,3 +178,48 @@ def test_sample_weight_affects_centres():
     init = np.array([[0.0, 0.0], [10.0, 0.0]])
     k = KMeans(n_clusters=2, init=init, n_init=1, device="cpu").fit(X, sample_weight=[1, 3, 1, 1])
     np.testing.assert_allclose(sorted(k.cluster_centers_[:, 0]), [0.75, 10.5])
+
+
+@pytest.mark.parametrize("k,d", [(12, 16), (70, 5)])
+def test_kmeans_elkan_matches_sklearn_elkan(k, d):
+    """algorithm='elkan' (bounded engine, torch twin on CPU) follows the same
+    Lloyd trajectory as sklearn's Elkan: same labels, centres, n_iter."""
+    from sklearn.datasets import make_blobs as skblobs
+    X, _ = skblobs(3000, d, centers=k, random_state=1, cluster_std=2.5)
+    init = X[:k].copy()
+    ours = KMeans(k, init=init, n_init=1, algorithm="elkan", max_iter=60).fit(X)
+    full = KMeans(k, init=init, n_init=1, algorithm="full", max_iter=60).fit(X)
+    ref = SKKMeans(k, init=init, n_init=1, algorithm="elkan", max_iter=60).fit(X)
+    assert ours.n_iter_ == ref.n_iter_ == full.n_iter_
+    np.testing.assert_array_equal(ours.labels_, ref.labels_)
+    np.testing.assert_allclose(ours.cluster_centers_, ref.cluster_centers_, atol=1e-10)
+    assert abs(ours.inertia_ - ref.inertia_) <= 1e-9 * ref.inertia_
+
+
+def test_elkan_bounds_invariants():
+    """After every bounded step: upper >= d(x, c_label) and lower[j] <= d(x, c_j)."""
+    from sq_learn_amd.ops import elkan as E
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(800, 7, generator=g, dtype=torch.float64)
+    C = X[:9].clone()
+    n, k = X.shape[0], C.shape[0]
+    lab = torch.zeros(n, dtype=torch.int32)
+    up = torch.zeros(n, dtype=torch.float64)
+    lo = torch.zeros(n, k, dtype=torch.float64)
+    sh = torch.zeros(k, dtype=torch.float64)
+    for it in range(6):
+        hcc, sn = E.centre_geometry(C)
+        E.elkan_step_torch(X, C, hcc, sn, sh, lab, up, lo, init=(it == 0))
+        D = torch.cdist(X, C, compute_mode="donot_use_mm_for_euclid_dist")
+        assert torch.equal(lab.long(), D.argmin(1))
+        assert bool((up >= D.gather(1, lab.long()[:, None])[:, 0] - 1e-12).all())
+        assert bool((lo <= D + 1e-12).all())
+        newC = torch.stack([X[lab.long() == j].mean(0) for j in range(k)])
+        sh = E.centre_shift(C, newC)
+        C = newC
+
+
+def test_elkan_single_cluster_warns():
+    X = np.random.RandomState(0).randn(50, 3)
+    with pytest.warns(RuntimeWarning, match="single cluster"):
+        KMeans(1, algorithm="elkan", n_init=1).fit(X)
