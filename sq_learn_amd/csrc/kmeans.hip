@@ -688,55 +688,68 @@ __global__ void __launch_bounds__(256) band_select_kernel(
 // ---------------------------------------------------------------------------
 // band_select_rows: fallback for rows the fused kernel flagged (a lane held
 // two band members).  Driven by the device-side count, so no host sync: the
-// grid covers the list capacity and surplus waves exit.  One wave per row,
-// lanes over centroids, full distance recomputed from the bf16 operands.
+// grid covers min(list capacity, 2048) workgroups and surplus ones exit.
+// One 256-thread workgroup per row: every thread computes k/256 distances
+// from the bf16 operands (x broadcast from LDS, centroid chunks coalesced
+// across threads, 4 independent accumulators per distance), the k distances
+// are staged in LDS, and wave 0 runs the exact band pick on them.  Distances
+// are computed once, so the count and pick passes see the same values.
+constexpr int kRowsMaxK = 4096;
 __global__ void __launch_bounds__(256) band_select_rows_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ C,
-    const float* __restrict__ thr_list, const float* __restrict__ xn,
-    const long long* __restrict__ rows, const int* __restrict__ count, int* __restrict__ labels,
-    long long cap, int d_pad, int k, float delta, RngKey key, long long row_offset, int idx_bits) {
-  (void)xn;
-  __shared__ float xs[4][256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float* __restrict__ thr_list, const long long* __restrict__ rows,
+    const int* __restrict__ count, int* __restrict__ labels, long long cap, int d_pad, int k,
+    float delta, RngKey key, long long row_offset) {
+  __shared__ float xs[256];
+  __shared__ float ds[kRowsMaxK];
+  const int tid = threadIdx.x, lane = tid & 63;
   const long long cnt = min((long long)*count, cap);
-  const int cpr = d_pad / 8 + 2;   // chunk-major operand (see estep_kernel)
-  // grid-stride over the device-side list (any length up to cap)
-  for (long long slot = (long long)blockIdx.x * 4 + w; slot < cnt;
-       slot += (long long)gridDim.x * 4) {
-  const long long r = rows[slot];
-  __builtin_amdgcn_wave_barrier();
-  for (int c = lane; c < d_pad; c += 64) xs[w][c] = bf16_to_f32(X[(size_t)r * d_pad + c]);
-  __builtin_amdgcn_wave_barrier();
-  // D'(j) = ||c_j||^2 - 2 x.c_j from the same bf16 operands the MFMA used
-  auto dist = [&](int j) -> float {
-    const uint16_t* base = C + ((size_t)(j >> 6) * cpr * 64 + (j & 63)) * 8;
-    float s = 0.f;
-    for (int ch = 0; ch < d_pad / 8; ++ch) {
-      uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)ch * 512);
-      const float* xv = &xs[w][ch * 8];
-      s += xv[0] * __uint_as_float(v.x << 16) + xv[1] * __uint_as_float(v.x & 0xFFFF0000u);
-      s += xv[2] * __uint_as_float(v.y << 16) + xv[3] * __uint_as_float(v.y & 0xFFFF0000u);
-      s += xv[4] * __uint_as_float(v.z << 16) + xv[5] * __uint_as_float(v.z & 0xFFFF0000u);
-      s += xv[6] * __uint_as_float(v.w << 16) + xv[7] * __uint_as_float(v.w & 0xFFFF0000u);
+  const int nch = d_pad / 8;
+  const int cpr = nch + 2;   // chunk-major operand (see estep_kernel)
+  for (long long slot = blockIdx.x; slot < cnt; slot += gridDim.x) {
+    const long long r = rows[slot];
+    __syncthreads();
+    if (tid < d_pad) xs[tid] = bf16_to_f32(X[(size_t)r * d_pad + tid]);
+    __syncthreads();
+    // D'(j) = ||c_j||^2 - 2 x.c_j
+    for (int j = tid; j < k; j += 256) {
+      const uint16_t* base = C + ((size_t)(j >> 6) * cpr * 64 + (j & 63)) * 8;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 4
+      for (int ch = 0; ch < nch; ++ch) {
+        const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)ch * 512);
+        const float* xv = &xs[ch * 8];
+        a0 = fmaf(xv[0], __uint_as_float(v.x << 16), a0);
+        a1 = fmaf(xv[1], __uint_as_float(v.x & 0xFFFF0000u), a1);
+        a2 = fmaf(xv[2], __uint_as_float(v.y << 16), a2);
+        a3 = fmaf(xv[3], __uint_as_float(v.y & 0xFFFF0000u), a3);
+        a0 = fmaf(xv[4], __uint_as_float(v.z << 16), a0);
+        a1 = fmaf(xv[5], __uint_as_float(v.z & 0xFFFF0000u), a1);
+        a2 = fmaf(xv[6], __uint_as_float(v.w << 16), a2);
+        a3 = fmaf(xv[7], __uint_as_float(v.w & 0xFFFF0000u), a3);
+      }
+      const uint32_t nv = *reinterpret_cast<const uint32_t*>(base + (size_t)nch * 512);
+      ds[j] = ((a0 + a1) + (a2 + a3)) + (__uint_as_float(nv << 16) +
+                                         __uint_as_float(nv & 0xFFFF0000u));
     }
-    uint32_t nv = *reinterpret_cast<const uint32_t*>(base + (size_t)(d_pad / 8) * 512);
-    return s + __uint_as_float(nv << 16) + __uint_as_float(nv & 0xFFFF0000u);
-  };
-  // threshold from the fused kernel (its MFMA min + delta): no min pass;
-  // if rounding of this recomputation leaves the band empty, use our own min
-  float thr = thr_list[slot];
-  (void)idx_bits;
-  const float u = band_u(key, row_offset + r);
-  int win = band_pick_wave(dist, k, thr, u, lane);
-  if (win < 0) {
-    float mn = __builtin_inff();
-    for (int j = lane; j < k; j += 64) mn = fminf(mn, dist(j));
+    __syncthreads();
+    if (tid < 64) {
+      auto dist = [&](int j) -> float { return ds[j]; };
+      // threshold from the fused kernel (its MFMA min + delta); if rounding of
+      // this recomputation leaves the band empty, use our own min
+      float thr = thr_list[slot];
+      const float u = band_u(key, row_offset + r);
+      int win = band_pick_wave(dist, k, thr, u, lane);
+      if (win < 0) {
+        float mn = __builtin_inff();
+        for (int j = lane; j < k; j += 64) mn = fminf(mn, ds[j]);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
-    thr = mn + delta;
-    win = band_pick_wave(dist, k, thr, u, lane);
-  }
-  if (lane == 0) labels[r] = win;
+        for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+        thr = mn + delta;
+        win = band_pick_wave(dist, k, thr, u, lane);
+      }
+      if (lane == 0) labels[r] = win;
+    }
   }
 }
 
@@ -835,9 +848,19 @@ __global__ void __launch_bounds__(256) centroid_accumulate_kernel(
 //                  and flushes one 256-B f32 atomic row-add per label run.
 constexpr int kHistChunk = 8192;
 
+// Also zeroes the reduce outputs (sums: nz1 doubles, counts: nz2) grid-stride,
+// so the segmented sums that follow need no separate memset launches.
 __global__ void __launch_bounds__(256) label_hist_kernel(const int* __restrict__ labels, long long n,
-                                                         int k, int* __restrict__ hist) {
+                                                         int k, int* __restrict__ hist,
+                                                         double* __restrict__ z1, long long nz1,
+                                                         double* __restrict__ z2, int nz2) {
   extern __shared__ __attribute__((aligned(16))) int lh[];
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nz1;
+       i += (long long)gridDim.x * 256)
+    z1[i] = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nz2;
+       i += (long long)gridDim.x * 256)
+    z2[i] = 0.0;
   for (int j = threadIdx.x; j < k; j += 256) lh[j] = 0;
   __syncthreads();
   const long long r0 = (long long)blockIdx.x * kHistChunk;
@@ -851,7 +874,9 @@ __global__ void __launch_bounds__(256) label_hist_kernel(const int* __restrict__
     if (lh[j]) atomicAdd(&hist[j], lh[j]);
 }
 
-__global__ void __launch_bounds__(1024) label_scan_kernel(const int* __restrict__ hist, int k,
+// Exclusive scan of the histogram into the scatter cursors; the histogram is
+// zeroed after use (it is only consumed here), ready for the next reduce.
+__global__ void __launch_bounds__(1024) label_scan_kernel(int* __restrict__ hist, int k,
                                                           int* __restrict__ cursor) {
   __shared__ int part[1024];
   const int t = threadIdx.x;
@@ -868,7 +893,7 @@ __global__ void __launch_bounds__(1024) label_scan_kernel(const int* __restrict_
     __syncthreads();
   }
   int run = part[t] - s;
-  for (int j = b; j < e; ++j) { cursor[j] = run; run += hist[j]; }
+  for (int j = b; j < e; ++j) { cursor[j] = run; run += hist[j]; hist[j] = 0; }
 }
 
 __global__ void __launch_bounds__(256) label_scatter_kernel(const int* __restrict__ labels,
@@ -915,6 +940,9 @@ __global__ void __launch_bounds__(256) label_scatter_kernel(const int* __restric
 // Large-d variant (a row spans the whole wave: 4 values per lane, 8-B/16-B
 // loads); measured faster than the chunked variant below at d = 256 bf16
 // (1.55 vs 1.84 ms, 10M rows), slower at small d (1.21 vs 0.85 ms, d = 32).
+#ifndef SQ_SEG_U
+#define SQ_SEG_U 4   // rows in flight per wave (perm -> label/row gathers)
+#endif
 template <typename T>
 __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
     const T* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
@@ -924,7 +952,7 @@ __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long long p0 = (long long)blockIdx.x * range;
   const long long p1 = min(min(n_sorted, (long long)*valid_end), p0 + range);
-  constexpr int U = 4;
+  constexpr int U = SQ_SEG_U;
   for (int c0 = lane * 4; c0 < d; c0 += 256) {
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, cnt = 0.0;
     int cur = -1;
@@ -1080,6 +1108,37 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const double* __restr
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// Iteration scalars for the host convergence test in one launch:
+// scalars = [inertia (packed tail, after the all-reduce), shift (per-centroid
+// parts summed in the same fixed order as sum_partials_kernel), overflow
+// rows]; the overflow counter is reset for the next E-step.
+__global__ void __launch_bounds__(256) iter_scalars_kernel(const double* __restrict__ part, int n,
+                                                           double* __restrict__ shift,
+                                                           const double* __restrict__ inertia,
+                                                           int* __restrict__ ovf_count,
+                                                           double* __restrict__ scalars) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    shift[0] = red[0];
+    scalars[0] = inertia[0];
+    scalars[1] = red[0];
+    if (ovf_count) {
+      scalars[2] = (double)ovf_count[0];
+      ovf_count[0] = 0;
+    } else {
+      scalars[2] = 0.0;
+    }
+  }
 }
 
 // packed[0:k*d] = sums (f64), packed[k*d : k*d+k] = counts, packed[k*d+k] = inertia;
@@ -1368,15 +1427,15 @@ int sq_band_select_rows(const void* X, const void* C, const void* cn, const void
                         unsigned s0, unsigned s1, long long row_offset, void* stream) {
   if (cap <= 0) return 0;
   if (d_pad > 256) return (int)hipErrorInvalidValue;
+  if (k > kRowsMaxK) return (int)hipErrorInvalidValue;
+  (void)xn;
+  (void)k_pad;
   RngKey key{k0, k1, s0, s1};
-  const long long blocks = (cap + 3) / 4;
-  hipLaunchKernelGGL(band_select_rows_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
-                     dim3(256), 0,
-                     (hipStream_t)stream, (const uint16_t*)X, (const uint16_t*)C,
-                     (const float*)cn /* per-slot thresholds */, (const float*)xn,
-                     (const long long*)rows,
+  hipLaunchKernelGGL(band_select_rows_kernel, dim3((unsigned)(cap < 2048 ? cap : 2048)),
+                     dim3(256), 0, (hipStream_t)stream, (const uint16_t*)X, (const uint16_t*)C,
+                     (const float*)cn /* per-slot thresholds */, (const long long*)rows,
                      (const int*)count, (int*)labels, cap, d_pad, k, (float)delta, key,
-                     row_offset, idx_bits_for(k_pad));
+                     row_offset);
   return (int)hipGetLastError();
 }
 
@@ -1415,10 +1474,11 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
   if (xexp < -120 || xexp > 120 || wexp < -120 || wexp > 120) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
-  (void)hipMemsetAsync(ws_hist, 0, (size_t)k * 4, st);
+  // ws_hist is all-zero on entry (zeroed at allocation, re-zeroed by the scan)
   hipLaunchKernelGGL(label_hist_kernel, dim3(chunks), dim3(256), (size_t)k * 4, st,
-                     (const int*)labels, n, k, (int*)ws_hist);
-  hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (const int*)ws_hist, k,
+                     (const int*)labels, n, k, (int*)ws_hist, (double*)sums, (long long)k * d,
+                     (double*)counts, k);
+  hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)ws_hist, k,
                      (int*)ws_cursor);
   hipLaunchKernelGGL(label_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
                      (const int*)labels, n, k, (int*)ws_cursor, (int*)ws_perm);
@@ -1492,7 +1552,7 @@ int sq_sum_partials(const void* part, int n, void* out, void* stream) {
 int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* shift_part, void* cn, void* shift, int k, int d, int k_pad,
                          double noise_b, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
-                         int empty_policy, void* stream) {
+                         int empty_policy, void* scalars, void* ovf_count, void* stream) {
   if (!shift_part) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   float b = (float)noise_b;
@@ -1502,8 +1562,14 @@ int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, voi
                      (hipStream_t)stream, (const double*)packed, (const float*)C_old,
                      (float*)C_new, (uint16_t*)C_bf16, (float*)cn, (double*)shift_part, k, d,
                      d_pad, b, eb, key, empty_policy);
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
-                     (const double*)shift_part, k, (double*)shift);
+  if (scalars)
+    hipLaunchKernelGGL(iter_scalars_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                       (const double*)shift_part, k, (double*)shift,
+                       (const double*)packed + (long long)k * d + k, (int*)ovf_count,
+                       (double*)scalars);
+  else
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                       (const double*)shift_part, k, (double*)shift);
   return (int)hipGetLastError();
 }
 

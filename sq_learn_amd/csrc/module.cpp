@@ -52,7 +52,7 @@ __attribute__((weak)) int sq_centroid_reduce(const void*, int, const void*, cons
 __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
                          unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
-                         void* stream);
+                         void* scalars, void* ovf_count, void* stream);
 __attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia,
                                         void* packed, int k, int d, int xexp, int wexp, void*);
 __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void* cn, void* labels, void* mind,
@@ -204,14 +204,14 @@ static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
-  unsigned long long pk, co, cnw, cb, clo, cn, sh, st; int k, d, kpad, pol; double nb;
+  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, st; int k, d, kpad, pol; double nb;
   unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d, &kpad,
-                        &nb, &k0, &k1, &s0, &s1, &pol, &st))
+  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
+                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &st))
     return nullptr;
   CHECK(sq_centroid_finalize)
   return ret(sq_centroid_finalize(P(pk), P(co), P(cnw), P(cb), P(clo), P(cn), P(sh), k, d, kpad, nb,
-                                  k0, k1, s0, s1, pol, P(st)));
+                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(st)));
 }
 
 static PyObject* py_pack_stats(PyObject*, PyObject* a) {

@@ -228,8 +228,6 @@ class LloydEngine:
         noise_key = self._key("trunc_normal")
         if self.fast:
             with tracing.range("mstep"):
-                self.sums.zero_()
-                self.counts.zero_()
                 K.centroid_reduce_native(self.Xm, labels, self.weights, self.sums,
                                          self.counts, self.k, self.rws)
                 sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
@@ -241,13 +239,12 @@ class LloydEngine:
                 K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
                                            self.shift, self.k, self.d, self._noise_bound(),
                                            noise_key, self.empty_policy,
-                                           shift_part=self.shift_part)
+                                           shift_part=self.shift_part, scalars=self.scalars,
+                                           buf=self.buf)
                 self.C, self.C_new = self.C_new, self.C
                 if self.intermediate_error and self.true_tomography and self.delta > 0:
                     self._true_tomography_centers()
-            self.scalars[0:1].copy_(self.packed[-1:])
-            self.scalars[1:2].copy_(self.shift)
-            self.scalars[2:3].copy_(self.buf.ovf_count.to(torch.float64))
+                    self.scalars[1:2].copy_(((self.C.double() - self.C_new.double()) ** 2).sum())
             return self.scalars
         # generic / CPU
         w = self.sample_weight
@@ -266,8 +263,6 @@ class LloydEngine:
                                            device=self.device)
                 self._g_counts = torch.zeros(self.k, dtype=torch.float64, device=self.device)
                 self._g_w = w.to(torch.float32).contiguous() if w is not None else None
-            self._g_sums.zero_()
-            self._g_counts.zero_()
             K.centroid_reduce_native(self.Xf, labels.to(torch.int32), self._g_w, self._g_sums,
                                      self._g_counts, self.k, self._g_rws)
             packed = torch.empty(self.k * self.d + self.k + 1, dtype=torch.float64,

@@ -176,6 +176,9 @@ class EStepBuffers:
         self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
         # scalars: [ovf_count(int32)] and inertia (fp64) / shift (fp64)
         self.ovf_count = torch.zeros(1, dtype=torch.int32, device=device)
+        # True while ovf_count is known to be zero (fresh, or reset on the
+        # device by the iteration-scalars launch): the E-step skips its memset
+        self.ovf_clean = True
         self.inertia = torch.zeros(1, dtype=torch.float64, device=device)
         # per-wave inertia partials (summed in a fixed order: reproducible)
         self.part_cap = n // 32 + 64
@@ -193,7 +196,9 @@ def estep_native(Xb, C_bf16, cn, xn, k, delta, key: RngKey, row_offset, buf: ESt
     assert buf.labels.numel() >= n and buf.part_cap >= 8
     st = stream if stream is not None else nat.stream_handle(Xb.device)
     m = nat.native()
-    buf.ovf_count.zero_()
+    if not buf.ovf_clean:
+        buf.ovf_count.zero_()
+    buf.ovf_clean = False
     m.estep_bf16(Xb.data_ptr(), C_bf16.data_ptr(), buf.inertia_part.data_ptr(), buf.ovf_thr.data_ptr(),
                  xn.data_ptr(), buf.labels.data_ptr(), buf.mind.data_ptr(), buf.ovf_rows.data_ptr(),
                  buf.ovf_count.data_ptr(), buf.inertia.data_ptr(), n, d_pad, k, k_pad,
@@ -270,7 +275,8 @@ class ReduceWorkspace:
 
 
 def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorkspace):
-    """sums[l] += sum_{i: label_i = l} w_i x_i, counts[l] += sum w_i (GPU),
+    """sums[l] = sum_{i: label_i = l} w_i x_i, counts[l] = sum w_i (GPU; the
+    outputs are overwritten - zeroed inside the histogram launch),
     in units of the quanta 2^ws.xexp / 2^ws.wexp (exact integer-valued fp64,
     order-independent: bit-reproducible).  ``pack_stats_native`` rescales."""
     n, d = X.shape
@@ -291,9 +297,13 @@ def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, 
 
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
-                             empty_policy=0, shift_part=None):
+                             empty_policy=0, shift_part=None, scalars=None, buf=None):
     """shift[0] = sum_j ||c_j' - c_j||^2 (per-centroid parts summed in a fixed
-    order: deterministic); ``shift_part`` is a k-double workspace."""
+    order: deterministic); ``shift_part`` is a k-double workspace.
+
+    With ``scalars`` (3 doubles) the same launch also writes the iteration's
+    [inertia, shift, overflow rows] (inertia from the packed bucket, overflow
+    count from ``buf``, an :class:`EStepBuffers`, whose counter it resets)."""
     k_pad = C_bf16.shape[0] * 64
     if shift_part is None:
         shift_part = torch.empty(max(k, 1), dtype=torch.float64, device=packed.device)
@@ -302,7 +312,11 @@ def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, nois
                                    C_bf16.data_ptr(), shift_part.data_ptr(), cn.data_ptr(),
                                    shift.data_ptr(), k, d, k_pad, float(noise_b), key.k0, key.k1,
                                    key.s0, key.s1, int(empty_policy),
+                                   0 if scalars is None else scalars.data_ptr(),
+                                   0 if buf is None else buf.ovf_count.data_ptr(),
                                    nat.stream_handle(packed.device))
+    if scalars is not None and buf is not None:
+        buf.ovf_clean = True
 
 
 def operand_shape(k_pad, d_pad):
