@@ -5,7 +5,7 @@ names="$@"
 what=${AB_WHAT:-estep}   # estep | reduce ; AB_ARGS: extra micro-benchmark flags
 for rep in 1 2; do
   for v in cur $names; do
-    unset SQ_NATIVE_VARIANT SQ_ESTEP_ROWS SQ_ESTEP_NW
+    unset SQ_NATIVE_VARIANT SQ_ESTEP_ROWS SQ_ESTEP_NW SQ_SEG_HALF SQ_SEG_RANGE
     case $v in
       cur) ;;
       env:*) export "${v#env:}" ;;

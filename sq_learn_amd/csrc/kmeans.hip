@@ -999,6 +999,71 @@ __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
   }
 }
 
+// bf16 half-wave variant: 16-B loads (8 values per lane), a row spans 32
+// lanes, so each wave instruction gathers two rows; every half-wave owns a
+// contiguous slice of the workgroup's positions (fewer label runs touched,
+// hence fewer flushes, than a strided split).
+__global__ void __launch_bounds__(512) segment_sum_rows_half_kernel(
+    const uint16_t* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
+    const float* __restrict__ w, long long n_sorted, int d, int range, float xscale,
+    float wscale, double* __restrict__ sums, double* __restrict__ counts,
+    const int* __restrict__ valid_end) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int hw = wave * 2 + (lane >> 5), hl = lane & 31;
+  const long long pe = min(n_sorted, (long long)*valid_end);
+  const int sub = range / 16;
+  const long long s0 = (long long)blockIdx.x * range + (long long)hw * sub;
+  const long long s1 = min(pe, s0 + sub);
+  constexpr int U = SQ_SEG_U;
+  for (int c0 = hl * 8; c0 < d; c0 += 256) {
+    double a[8], cnt = 0.0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.0;
+    int cur = -1;
+    auto flush = [&]() {
+      double* dst = sums + (size_t)cur * d + c0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (a[e] != 0.0 && c0 + e < d) atomicAdd(dst + e, a[e]);
+      if (hl == 0 && c0 == 0) atomicAdd(&counts[cur], cnt);
+    };
+    for (long long p = s0; p < s1; p += U) {
+      int rr[U], ll[U];
+      uint4 v[U];
+      float ww[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) rr[u] = p + u < s1 ? perm[p + u] : -1;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ll[u] = rr[u] >= 0 ? labels[rr[u]] : -1;
+        v[u] = rr[u] >= 0 && c0 < d ? *reinterpret_cast<const uint4*>(X + (size_t)rr[u] * d + c0)
+                                    : make_uint4(0u, 0u, 0u, 0u);
+        ww[u] = (w && rr[u] >= 0) ? w[rr[u]] : 1.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ll[u] < 0) continue;
+        if (ll[u] != cur) {
+          if (cur >= 0) flush();
+          cur = ll[u];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] = 0.0;
+          cnt = 0.0;
+        }
+        const float s = ww[u] * xscale;   // exact when unweighted (power of 2)
+        const uint32_t q[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[2 * e] += (double)rintf(__uint_as_float(q[e] << 16) * s);
+          a[2 * e + 1] += (double)rintf(__uint_as_float(q[e] & 0xFFFF0000u) * s);
+        }
+        cnt += w ? (double)rintf(ww[u] * wscale) : 1.0;
+      }
+    }
+    if (cur >= 0) flush();
+  }
+}
+
 // 16-byte chunk loads: 8 bf16 or 4 fp32 values
 template <typename T> struct Chunk16;
 template <> struct Chunk16<uint16_t> {
@@ -1466,6 +1531,21 @@ int sq_centroid_accumulate(const void* X, int xdtype, const void* labels, const 
   return (int)hipGetLastError();
 }
 
+// A/B knobs (read once): SQ_SEG_HALF=0/1 bf16 half-wave rows, SQ_SEG_RANGE
+// positions per workgroup of the large-d segmented sum (multiple of 16)
+static int seg_half() {
+  static int v = [] { const char* e = getenv("SQ_SEG_HALF"); return e ? atoi(e) : 0; }();
+  return v;
+}
+static int seg_range() {
+  static int v = [] {
+    const char* e = getenv("SQ_SEG_RANGE");
+    int r = e ? atoi(e) : 2048;
+    return r < 64 ? 64 : (r / 16) * 16;
+  }();
+  return v;
+}
+
 int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void* weights,
                        void* sums, void* counts, long long n, int d, int k, int xexp, int wexp,
                        void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
@@ -1489,11 +1569,16 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
   const int V = xdtype == 2 ? 8 : 4;
   if (d / V >= 32 || d % V != 0) {
     // whole-wave rows (large d, or d not a multiple of the 16-B chunk)
-    const int range = 2048;
+    const int range = seg_range();
     unsigned grid = (unsigned)((n + range - 1) / range);
     if (xdtype == 0)
       hipLaunchKernelGGL(segment_sum_rows_kernel<float>, dim3(grid), dim3(512), 0, st,
                          (const float*)X, (const int*)ws_perm, (const int*)labels,
+                         (const float*)weights, n, d, range, xs, wsc, (double*)sums,
+                         (double*)counts, (const int*)ws_cursor + (k - 1));
+    else if (xdtype == 2 && d % 8 == 0 && seg_half())
+      hipLaunchKernelGGL(segment_sum_rows_half_kernel, dim3(grid), dim3(512), 0, st,
+                         (const uint16_t*)X, (const int*)ws_perm, (const int*)labels,
                          (const float*)weights, n, d, range, xs, wsc, (double*)sums,
                          (double*)counts, (const int*)ws_cursor + (k - 1));
     else if (xdtype == 2)
