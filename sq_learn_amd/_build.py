@@ -10,6 +10,10 @@ boxes and is what the python processes load).
 
 Usage: ``python -m sq_learn_amd._build [--force] [--jobs N] [--debug]``.
 
+The host-native library (``csrc/host/*.cpp``: hashing, isotonic PAVA, graph
+searches, svmlight parsing, DBSCAN expansion, ...) is built alongside with
+the host C++ compiler into ``_sq_host.so`` (``build_host``).
+
 Tuning variants (kernel experiments only): ``--define NAME=VALUE ... --out
 PATH.so`` builds a separately named extension with extra preprocessor
 definitions; ``SQ_NATIVE_VARIANT=PATH.so`` makes the loader use it.
@@ -97,6 +101,39 @@ def build(force=False, jobs=None, debug=False, verbose=False, defines=(), out=No
     return out
 
 
+HOST_SRC = os.path.join(CSRC, "host")
+CXX = os.environ.get("CXX", "g++")
+
+
+def host_path():
+    return os.path.join(HERE, "_sq_host.so")
+
+
+def _host_sources():
+    return sorted(os.path.join(HOST_SRC, f) for f in os.listdir(HOST_SRC)
+                  if f.endswith((".cpp", ".h")))
+
+
+def host_needs_build():
+    out = host_path()
+    return not os.path.exists(out) or _newest(_host_sources() + [__file__]) > os.path.getmtime(out)
+
+
+def build_host(force=False, debug=False):
+    """Host-native library (``csrc/host/*.cpp`` -> ``_sq_host.so``, loaded
+    with ctypes): C++17 + OpenMP, no HIP dependency."""
+    out = host_path()
+    if not force and not host_needs_build():
+        return out
+    srcs = [f for f in _host_sources() if f.endswith(".cpp")]
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    tmp = out + ".tmp"
+    _run([CXX, "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", HOST_SRC] + opt + srcs
+         + ["-o", tmp])
+    os.replace(tmp, out)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
@@ -108,6 +145,8 @@ def main(argv=None):
     a = ap.parse_args(argv)
     path = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose,
                  defines=a.define, out=a.out)
+    if a.out is None:
+        print(build_host(force=a.force, debug=a.debug))
     print(path)
 
 

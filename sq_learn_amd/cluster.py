@@ -1,3 +1,4 @@
 """Reference-layout import path (``sklearn.cluster``): q-means and k-means."""
 from .models.cluster import KMeans, LloydEngine, QMeans, k_means, kmeans_plusplus, qMeans_  # noqa: F401
 from .models.cluster.minibatch import MiniBatchKMeans  # noqa: F401
+from .models.cluster.dbscan import DBSCAN, dbscan  # noqa: F401

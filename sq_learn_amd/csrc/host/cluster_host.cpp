@@ -1,0 +1,82 @@
+// Host kernels for clustering utilities:
+//   * DBSCAN cluster expansion (reference ``cluster/_dbscan_inner.pyx:21``):
+//     depth-first growth from each unlabelled core sample over the
+//     precomputed radius-neighbourhood graph (CSR), non-core samples are
+//     border points that join the first cluster reaching them;
+//   * expected mutual information of a contingency table under the
+//     hypergeometric model (reference
+//     ``metrics/cluster/_expected_mutual_info_fast.pyx``), OpenMP over rows.
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "host.h"
+
+extern "C" {
+
+void sqh_dbscan_inner(const uint8_t* is_core, const int64_t* indptr, const int64_t* indices,
+                      long long n, int64_t* labels) {
+  std::vector<int64_t> stack;
+  int64_t label = 0;
+  for (long long s = 0; s < n; ++s) {
+    if (labels[s] != -1 || !is_core[s]) continue;
+    int64_t i = s;
+    while (true) {
+      if (labels[i] == -1) {
+        labels[i] = label;
+        if (is_core[i]) {
+          for (int64_t e = indptr[i]; e < indptr[i + 1]; ++e) {
+            const int64_t v = indices[e];
+            if (labels[v] == -1) stack.push_back(v);
+          }
+        }
+      }
+      if (stack.empty()) break;
+      i = stack.back();
+      stack.pop_back();
+    }
+    ++label;
+  }
+}
+
+// a: row sums (R), b: column sums (C), N: total.  Returns E[MI] in nats.
+double sqh_expected_mutual_info(const int64_t* a, long long R, const int64_t* b, long long C,
+                                long long N) {
+  if (N <= 1) return 0.0;
+  long long maxab = 0;
+  for (long long i = 0; i < R; ++i) maxab = std::max<long long>(maxab, a[i]);
+  for (long long j = 0; j < C; ++j) maxab = std::max<long long>(maxab, b[j]);
+  // log(nij / N) and lgamma(nij + 1) tables for nij = 0 .. maxab
+  std::vector<double> log_nij(maxab + 1), gln_nij(maxab + 1);
+  for (long long v = 0; v <= maxab; ++v) {
+    log_nij[v] = v > 0 ? std::log((double)v) : 0.0;
+    gln_nij[v] = std::lgamma((double)v + 1.0);
+  }
+  const double logN = std::log((double)N);
+  const double gln_N = std::lgamma((double)N + 1.0);
+  double emi = 0.0;
+#pragma omp parallel for reduction(+ : emi) schedule(dynamic)
+  for (long long i = 0; i < R; ++i) {
+    const double ai = (double)a[i];
+    const double gln_a = std::lgamma(ai + 1.0), gln_Na = std::lgamma((double)N - ai + 1.0);
+    for (long long j = 0; j < C; ++j) {
+      const double bj = (double)b[j];
+      const double gln_b = std::lgamma(bj + 1.0), gln_Nb = std::lgamma((double)N - bj + 1.0);
+      const long long lo = std::max<long long>(1, a[i] - N + b[j]);
+      const long long hi = std::min<long long>(a[i], b[j]) + 1;
+      const double log_ab = std::log(ai) + std::log(bj);
+      for (long long nij = lo; nij < hi; ++nij) {
+        const double term1 = (double)nij / (double)N;
+        const double term2 = logN + log_nij[nij] - log_ab;
+        const double gln = gln_a + gln_b + gln_Na + gln_Nb - gln_N - gln_nij[nij] -
+                           std::lgamma(ai - (double)nij + 1.0) -
+                           std::lgamma(bj - (double)nij + 1.0) -
+                           std::lgamma((double)N - ai - bj + (double)nij + 1.0);
+        emi += term1 * term2 * std::exp(gln);
+      }
+    }
+  }
+  return emi;
+}
+
+}  // extern "C"

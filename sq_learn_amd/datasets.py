@@ -1,3 +1,4 @@
 """Reference-layout import path (``sklearn.datasets``): synthetic generators."""
 from .utils.datasets import (make_blobs, make_blobs_device, make_classification,  # noqa: F401
                              make_low_rank_device, make_low_rank_matrix)
+from .utils.svmlight import dump_svmlight_file, load_svmlight_file, load_svmlight_files  # noqa: F401

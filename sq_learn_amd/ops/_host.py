@@ -1,0 +1,73 @@
+"""Loader for the host-native library ``sq_learn_amd/_sq_host.so``
+(``csrc/host/*.cpp``), bound with ctypes.
+
+Same policy as the device layer (``_native.py``): the library is (re)built
+in-tree when missing or stale and every op that has a host kernel calls it
+- there is no Python re-implementation to fall back to.  ctypes releases
+the GIL for the duration of each call.
+"""
+
+import ctypes
+import threading
+
+import numpy as np
+
+_lock = threading.Lock()
+_lib = None
+
+_P = ctypes.c_void_p
+_LL = ctypes.c_longlong
+_I = ctypes.c_int
+_U = ctypes.c_uint32
+_D = ctypes.c_double
+_F = ctypes.c_float
+
+_SIGS = {
+    "sqh_murmur_i32": (None, [_P, _LL, _U, _P]),
+    "sqh_murmur_bytes": (None, [_P, _P, _LL, _U, _P]),
+    "sqh_hash_features": (None, [_P, _P, _P, _LL, _LL, _I, _U, _P, _P]),
+    "sqh_pava_f64": (None, [_P, _P, _LL]),
+    "sqh_pava_f32": (None, [_P, _P, _LL]),
+    "sqh_make_unique_f64": (_LL, [_P, _P, _P, _LL, _D, _P, _P, _P]),
+    "sqh_make_unique_f32": (_LL, [_P, _P, _P, _LL, _F, _P, _P, _P]),
+    "sqh_floyd_warshall": (None, [_P, _LL, _I]),
+    "sqh_dijkstra": (None, [_P, _P, _P, _P, _P, _P, _LL, _I, _P]),
+    "sqh_svml_parse": (_P, [_P, _LL, _I, _I, _I, _LL, _LL]),
+    "sqh_svml_error": (ctypes.c_char_p, [_P]),
+    "sqh_svml_sizes": (None, [_P, _P]),
+    "sqh_svml_copy": (None, [_P, _P, _P, _P, _P, _P, _P]),
+    "sqh_svml_free": (None, [_P]),
+    "sqh_dbscan_inner": (None, [_P, _P, _P, _LL, _P]),
+    "sqh_expected_mutual_info": (_D, [_P, _LL, _P, _LL, _LL]),
+}
+
+
+def lib():
+    """The loaded host library (built on first use if missing or stale)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            from .. import _build
+            if _build.host_needs_build():
+                _build.build_host()
+            h = ctypes.CDLL(_build.host_path())
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def ptr(a):
+    """Raw data pointer of a C-contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "host kernels take C-contiguous arrays"
+    return a.ctypes.data
+
+
+def carray(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)

@@ -1,0 +1,217 @@
+"""Host-native library (csrc/host/*.cpp via ops/_host.py) against the
+installed upstream scikit-learn / scipy implementations of the same
+functions (the reference is a scikit-learn fork: these are its untouched
+upstream components)."""
+import io
+import warnings
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import sklearn
+import sklearn.metrics as skm
+from sklearn.cluster import DBSCAN as SKDBSCAN
+from sklearn.datasets import dump_svmlight_file as sk_dump, load_svmlight_file as sk_load
+from sklearn.feature_extraction import FeatureHasher as SKFeatureHasher
+from sklearn.isotonic import IsotonicRegression as SKIso, isotonic_regression as sk_iso
+from sklearn.utils import murmurhash3_32 as sk_murmur
+from scipy.sparse.csgraph import shortest_path
+
+from sq_learn_amd.cluster import DBSCAN, dbscan
+from sq_learn_amd.feature_extraction import FeatureHasher
+from sq_learn_amd.isotonic import IsotonicRegression, check_increasing, isotonic_regression
+from sq_learn_amd import metrics as M
+from sq_learn_amd.ops import _host
+from sq_learn_amd.utils.graph import graph_shortest_path, single_source_shortest_path_length
+from sq_learn_amd.utils.murmurhash import murmurhash3_32
+from sq_learn_amd.utils.svmlight import dump_svmlight_file, load_svmlight_file, load_svmlight_files
+
+
+def test_host_library_loads():
+    lib = _host.lib()
+    assert lib.sqh_pava_f64 is not None
+
+
+# ------------------------------------------------------------------ hashing
+@pytest.mark.parametrize("seed", [0, 1, 2 ** 31, 2 ** 32 - 1])
+@pytest.mark.parametrize("positive", [True, False])
+def test_murmurhash_int_and_str(seed, positive):
+    for k in [0, 1, -1, 42, 2 ** 31 - 1, -2 ** 31]:
+        assert murmurhash3_32(k, seed=seed, positive=positive) == sk_murmur(k, seed=seed,
+                                                                            positive=positive)
+    for s in ["", "a", "ab", "abc", "abcd", "abcde", "hello world", "café", b"\x00\xff"]:
+        assert murmurhash3_32(s, seed=seed, positive=positive) == sk_murmur(s, seed=seed,
+                                                                            positive=positive)
+
+
+def test_murmurhash_arrays():
+    rs = np.random.RandomState(0)
+    a = rs.randint(-2 ** 31, 2 ** 31 - 1, 257).astype(np.int32)
+    np.testing.assert_array_equal(murmurhash3_32(a, 7), sk_murmur(a, 7))
+    np.testing.assert_array_equal(murmurhash3_32(a, 7, positive=True), sk_murmur(a, 7, positive=True))
+    strs = np.array(["x%d" % i for i in range(50)], dtype=object)
+    np.testing.assert_array_equal(murmurhash3_32(strs, 3), [sk_murmur(str(v), 3) for v in strs])
+
+
+@pytest.mark.parametrize("input_type,alt", [("dict", True), ("pair", False), ("string", True)])
+def test_feature_hasher(input_type, alt):
+    rs = np.random.RandomState(1)
+    words = ["w%d" % i for i in range(40)]
+    if input_type == "dict":
+        raw = [{w: float(rs.randint(-3, 4)) for w in rs.choice(words, 6)} for _ in range(30)]
+        raw[0]["cat"] = "meow"
+    elif input_type == "pair":
+        raw = [[(w, float(rs.rand())) for w in rs.choice(words, 5)] for _ in range(30)]
+    else:
+        raw = [list(rs.choice(words, 7)) for _ in range(30)]
+    for nf in (1, 16, 2 ** 20):
+        A = FeatureHasher(nf, input_type=input_type, alternate_sign=alt).transform(raw)
+        B = SKFeatureHasher(nf, input_type=input_type, alternate_sign=alt).transform(raw)
+        assert A.shape == B.shape and abs(A - B).sum() == 0
+    with pytest.raises(ValueError):
+        FeatureHasher(8).transform([])
+
+
+# ----------------------------------------------------------------- isotonic
+@pytest.mark.parametrize("n", [1, 2, 5, 100, 2000])
+def test_isotonic_regression_function(n):
+    rs = np.random.RandomState(n)
+    y = rs.randn(n).cumsum() + 3 * rs.randn(n)
+    w = rs.rand(n) + 0.1
+    for inc in (True, False):
+        np.testing.assert_allclose(isotonic_regression(y, sample_weight=w, increasing=inc),
+                                   sk_iso(y, sample_weight=w, increasing=inc), atol=1e-12)
+    np.testing.assert_allclose(isotonic_regression(y, y_min=-1, y_max=1), sk_iso(y, y_min=-1, y_max=1))
+    y32 = y.astype(np.float32)
+    assert isotonic_regression(y32).dtype == np.float32
+
+
+@pytest.mark.parametrize("oob", ["nan", "clip"])
+@pytest.mark.parametrize("increasing", [True, False, "auto"])
+def test_isotonic_estimator(oob, increasing):
+    rs = np.random.RandomState(2)
+    X = rs.randint(0, 40, 300).astype(float)            # duplicates exercise _make_unique
+    y = 0.2 * X + rs.randn(300)
+    w = rs.rand(300)
+    w[:10] = 0.0
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        a = IsotonicRegression(out_of_bounds=oob, increasing=increasing).fit(X, y, sample_weight=w)
+        b = SKIso(out_of_bounds=oob, increasing=increasing).fit(X, y, sample_weight=w)
+    np.testing.assert_allclose(a.X_thresholds_, b.X_thresholds_)
+    np.testing.assert_allclose(a.y_thresholds_, b.y_thresholds_, atol=1e-12)
+    T = np.linspace(-5, 45, 101)
+    np.testing.assert_allclose(a.predict(T), b.predict(T), atol=1e-12, equal_nan=True)
+    assert a.increasing_ == b.increasing_
+    assert check_increasing(X, y)
+
+
+# -------------------------------------------------------------- graph paths
+@pytest.mark.parametrize("N,dens", [(1, 1.0), (9, 0.5), (80, 0.05), (80, 0.7)])
+@pytest.mark.parametrize("directed", [True, False])
+def test_graph_shortest_path(N, dens, directed):
+    rs = np.random.RandomState(N)
+    A = rs.rand(N, N) * (rs.rand(N, N) < dens)
+    ref = shortest_path(sp.csr_matrix(A), directed=directed)
+    ref[np.isinf(ref)] = 0
+    for method in ("FW", "D", "auto"):
+        np.testing.assert_allclose(graph_shortest_path(A, directed=directed, method=method), ref,
+                                   atol=1e-12)
+    np.testing.assert_allclose(graph_shortest_path(sp.csr_matrix(A), directed=directed,
+                                                   method="D"), ref, atol=1e-12)
+    with pytest.raises(ValueError):
+        graph_shortest_path(A, method="X")
+
+
+def test_single_source_shortest_path_length():
+    A = np.array([[0, 1, 0, 0], [1, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 0]])
+    assert single_source_shortest_path_length(A, 0) == {0: 0, 1: 1, 2: 2}
+    assert single_source_shortest_path_length(A, 0, cutoff=1) == {0: 0, 1: 1}
+
+
+# ----------------------------------------------------------------- svmlight
+@pytest.mark.parametrize("zero_based", [True, False])
+def test_svmlight_roundtrip_vs_sklearn(zero_based):
+    rs = np.random.RandomState(0)
+    X = sp.random(40, 25, density=0.25, random_state=0, format="csr")
+    y = rs.randint(0, 4, 40).astype(float)
+    q = rs.randint(0, 3, 40)
+    ours, ref = io.BytesIO(), io.BytesIO()
+    dump_svmlight_file(X, y, ours, zero_based=zero_based, query_id=q, comment="c")
+    sk_dump(X, y, ref, zero_based=zero_based, query_id=q, comment="c")
+    body = lambda b: [ln for ln in b.getvalue().splitlines() if not ln.startswith(b"#")]
+    assert body(ours) == body(ref)
+    for zb in ("auto", zero_based):
+        A = load_svmlight_file(io.BytesIO(ref.getvalue()), zero_based=zb, query_id=True)
+        B = sk_load(io.BytesIO(ref.getvalue()), zero_based=zb, query_id=True)
+        assert A[0].shape == B[0].shape and (A[0] != B[0]).nnz == 0
+        np.testing.assert_array_equal(A[1], B[1])
+        np.testing.assert_array_equal(A[2], B[2])
+
+
+def test_svmlight_offsets_multilabel_errors(tmp_path):
+    X = sp.random(60, 12, density=0.3, random_state=1, format="csr")
+    y = np.arange(60, dtype=float)
+    raw = io.BytesIO()
+    sk_dump(X, y, raw)
+    raw = raw.getvalue()
+    for off, ln in [(0, 100), (57, 200), (300, -1), (0, -1)]:
+        A = load_svmlight_file(io.BytesIO(raw), n_features=12, offset=off, length=ln)
+        B = sk_load(io.BytesIO(raw), n_features=12, offset=off, length=ln)
+        assert (A[0] != B[0]).nnz == 0
+        np.testing.assert_array_equal(A[1], B[1])
+    ml = b"1,3 1:2.5 4:1\n2 2:1 # comment\n 3:4\n\n"
+    A = load_svmlight_file(io.BytesIO(ml), multilabel=True)
+    B = sk_load(io.BytesIO(ml), multilabel=True)
+    assert A[1] == B[1] and (A[0] != B[0]).nnz == 0
+    for bad in [b"1 3:1 2:1\n", b"1 0:1\n", b"1 -1:1\n", b"abc 1:1\n"]:
+        with pytest.raises(ValueError):
+            load_svmlight_file(io.BytesIO(bad), zero_based=False)
+    p = tmp_path / "d.svm"
+    p.write_bytes(raw)
+    Xa, ya, Xb, yb = load_svmlight_files([str(p), str(p)])
+    assert Xa.shape == Xb.shape and np.array_equal(ya, yb)
+
+
+# ---------------------------------------------------------- cluster metrics
+@pytest.mark.parametrize("n,k1,k2", [(10, 2, 3), (500, 6, 9), (3000, 25, 30), (40, 1, 1)])
+def test_supervised_cluster_metrics(n, k1, k2):
+    rs = np.random.RandomState(n)
+    a, b = rs.randint(0, k1, n), rs.randint(0, k2, n)
+    for f in ("adjusted_mutual_info_score", "normalized_mutual_info_score", "mutual_info_score",
+              "rand_score", "fowlkes_mallows_score", "homogeneity_score", "completeness_score",
+              "v_measure_score"):
+        assert abs(getattr(M, f)(a, b) - getattr(skm, f)(a, b)) < 1e-10, f
+    for am in ("min", "geometric", "arithmetic", "max"):
+        assert abs(M.adjusted_mutual_info_score(a, b, average_method=am)
+                   - skm.adjusted_mutual_info_score(a, b, average_method=am)) < 1e-10
+
+
+def test_unsupervised_cluster_metrics():
+    rs = np.random.RandomState(3)
+    X, lab = rs.randn(300, 4), rs.randint(0, 4, 300)
+    np.testing.assert_allclose(M.silhouette_samples(X, lab), skm.silhouette_samples(X, lab),
+                               atol=1e-12)
+    D = skm.pairwise_distances(X)
+    assert abs(M.silhouette_score(D, lab, metric="precomputed") - skm.silhouette_score(X, lab)) < 1e-12
+    assert abs(M.calinski_harabasz_score(X, lab) - skm.calinski_harabasz_score(X, lab)) < 1e-9
+    assert abs(M.davies_bouldin_score(X, lab) - skm.davies_bouldin_score(X, lab)) < 1e-12
+
+
+# ------------------------------------------------------------------- DBSCAN
+@pytest.mark.parametrize("metric", ["euclidean", "manhattan", "precomputed"])
+def test_dbscan_matches_sklearn(metric):
+    from sklearn.datasets import make_moons
+    X, _ = make_moons(500, noise=0.08, random_state=0)
+    w = np.random.RandomState(0).rand(500) * 2
+    for eps, ms in [(0.15, 5), (0.1, 10)]:
+        Xin = skm.pairwise_distances(X) if metric == "precomputed" else X
+        sk_metric = "euclidean" if metric == "precomputed" else metric
+        for sw in (None, w):
+            a = DBSCAN(eps=eps, min_samples=ms, metric=metric).fit(Xin, sample_weight=sw)
+            b = SKDBSCAN(eps=eps, min_samples=ms, metric=sk_metric).fit(X, sample_weight=sw)
+            np.testing.assert_array_equal(a.labels_, b.labels_)
+            np.testing.assert_array_equal(a.core_sample_indices_, b.core_sample_indices_)
+    core, labels = dbscan(X, eps=0.15, min_samples=5)
+    assert labels.max() >= 1 and len(core) > 0
