@@ -24,6 +24,9 @@ __attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long
 __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int, int, const void*,
                                         void*, void*, int, unsigned, unsigned, unsigned, unsigned,
                                         long long, void*);
+// pairwise_fast.hip
+__attribute__((weak)) int sq_pairwise_reduce(const void*, const void*, void*, int, int, int, int,
+                                             double, int, void*);
 // elkan.hip
 __attribute__((weak)) int sq_elkan_step(const void*, const void*, const void*, const void*,
                                         const void*, void*, void*, void*, long long, int, int,
@@ -151,6 +154,14 @@ static PyObject* py_tomography(PyObject*, PyObject* a) {
   CHECK(sq_tomography)
   return ret(sq_tomography(P(V), r, d, P(sched), T, mode, P(first), P(err), P(out), ninf, k0, k1,
                            s0, s1, roff, P(st)));
+}
+
+static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {
+  unsigned long long X, Y, out, st; int n, m, d, op, dt; double p;
+  if (!PyArg_ParseTuple(a, "KKKiiiidiK", &X, &Y, &out, &n, &m, &d, &op, &p, &dt, &st))
+    return nullptr;
+  CHECK(sq_pairwise_reduce)
+  return ret(sq_pairwise_reduce(P(X), P(Y), P(out), n, m, d, op, p, dt, P(st)));
 }
 
 static PyObject* py_elkan_step(PyObject*, PyObject* a) {
@@ -288,6 +299,7 @@ static PyMethodDef methods[] = {
     {"estep_bf16", py_estep_bf16, METH_VARARGS, "fused MFMA distance + delta-band E-step"},
     {"band_select", py_band_select, METH_VARARGS, "delta-band selection over distance rows"},
     {"band_select_rows", py_band_select_rows, METH_VARARGS, "device-driven overflow fallback"},
+    {"pairwise_reduce", py_pairwise_reduce, METH_VARARGS, "L1 / chi2 / chebyshev / minkowski tiles"},
     {"elkan_step", py_elkan_step, METH_VARARGS, "Elkan bounded k-means assignment"},
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},

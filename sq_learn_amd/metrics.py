@@ -11,3 +11,10 @@ from .utils.cluster_metrics import (adjusted_mutual_info_score, calinski_harabas
                                     normalized_mutual_info_score, pair_confusion_matrix,
                                     rand_score, silhouette_samples, silhouette_score,
                                     v_measure_score)
+from .utils.pairwise import (PAIRWISE_DISTANCE_FUNCTIONS, PAIRWISE_KERNEL_FUNCTIONS,  # noqa: F401
+                             additive_chi2_kernel, chi2_kernel, cosine_distances,
+                             cosine_similarity, haversine_distances, laplacian_kernel,
+                             manhattan_distances, paired_cosine_distances, paired_distances,
+                             paired_euclidean_distances, paired_manhattan_distances,
+                             pairwise_distances, pairwise_distances_argmin,
+                             pairwise_distances_argmin_min)

@@ -39,6 +39,9 @@ _SIGS = {
     "sqh_svml_free": (None, [_P]),
     "sqh_dbscan_inner": (None, [_P, _P, _P, _LL, _P]),
     "sqh_expected_mutual_info": (_D, [_P, _LL, _P, _LL, _LL]),
+    "sqh_sparse_manhattan": (None, [_P, _P, _P, _P, _P, _P, _LL, _LL, _P]),
+    "sqh_cholesky_delete": (None, [_P, _LL, _LL, _LL]),
+    "sqh_csr_poly": (_LL, [_P, _P, _P, _LL, _LL, _I, _I, _P, _P, _P]),
 }
 
 

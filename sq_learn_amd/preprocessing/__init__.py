@@ -208,3 +208,6 @@ class Normalizer(TransformerMixin, BaseEstimator):
 
 
 __all__ = ["StandardScaler", "MinMaxScaler", "Normalizer", "normalize"]
+
+
+from ._polynomial import PolynomialFeatures  # noqa: E402,F401

@@ -79,6 +79,8 @@ def to_tensor(x, device=None, dtype=None, copy=False):
             copy = False
         return t.clone() if copy else t
     arr = np.asarray(x)
+    if any(st < 0 for st in arr.strides):
+        arr = np.ascontiguousarray(arr)   # torch rejects negative strides
     if dtype is None:
         if arr.dtype.kind in "fc":
             dtype = resolve_dtype(arr.dtype) if arr.dtype in (np.float32, np.float64, np.float16) else torch.float64

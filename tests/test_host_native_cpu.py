@@ -215,3 +215,71 @@ def test_dbscan_matches_sklearn(metric):
             np.testing.assert_array_equal(a.core_sample_indices_, b.core_sample_indices_)
     core, labels = dbscan(X, eps=0.15, min_samples=5)
     assert labels.max() >= 1 and len(core) > 0
+
+
+# ------------------------------------------------- pairwise / arrayfuncs
+def test_pairwise_metrics_match_sklearn():
+    import sklearn.metrics.pairwise as S
+    from sq_learn_amd.utils import pairwise as P
+    rs = np.random.RandomState(0)
+    A, B = rs.rand(37, 9), rs.rand(29, 9)
+    close = lambda a, b: np.testing.assert_allclose(np.asarray(a), np.asarray(b), atol=1e-12)
+    close(P.manhattan_distances(A, B), S.manhattan_distances(A, B))
+    As, Bs = sp.csr_matrix(A * (A > 0.5)), sp.csr_matrix(B * (B > 0.5))
+    close(P.manhattan_distances(As, Bs), S.manhattan_distances(As, Bs))
+    close(P.cosine_similarity(A, B), S.cosine_similarity(A, B))
+    close(P.cosine_distances(A), S.cosine_distances(A))
+    close(P.additive_chi2_kernel(A, B), S.additive_chi2_kernel(A, B))
+    close(P.chi2_kernel(A, B, gamma=0.5), S.chi2_kernel(A, B, gamma=0.5))
+    close(P.laplacian_kernel(A, B), S.laplacian_kernel(A, B))
+    H = rs.rand(5, 2)
+    close(P.haversine_distances(H), S.haversine_distances(H))
+    for m in ["euclidean", "manhattan", "cosine", "chebyshev", "sqeuclidean", "braycurtis"]:
+        close(P.pairwise_distances(A, B, metric=m), S.pairwise_distances(A, B, metric=m))
+    close(P.pairwise_distances(A, B, metric="minkowski", p=3),
+          S.pairwise_distances(A, B, metric="minkowski", p=3))
+    a1, v1 = P.pairwise_distances_argmin_min(A, B)
+    a2, v2 = S.pairwise_distances_argmin_min(A, B)
+    np.testing.assert_array_equal(a1, a2)
+    close(v1, v2)
+    for m in ["euclidean", "manhattan", "cosine"]:
+        close(P.paired_distances(A, A[::-1], metric=m), S.paired_distances(A, A[::-1], metric=m))
+    with pytest.raises(ValueError):
+        P.additive_chi2_kernel(-A)
+
+
+def test_arrayfuncs():
+    from sklearn.utils.arrayfuncs import cholesky_delete as sk_cd, min_pos as sk_mp
+    from sq_learn_amd.utils.arrayfuncs import cholesky_delete, log_logistic, min_pos
+    rs = np.random.RandomState(0)
+    A = rs.randn(8, 8)
+    L = np.linalg.cholesky(A @ A.T + 8 * np.eye(8))
+    for g in range(8):
+        a, b = L.copy(), L.copy()
+        cholesky_delete(a, g)
+        sk_cd(b, g)
+        np.testing.assert_allclose(a, b, atol=1e-13)
+    x = rs.randn(100)
+    assert min_pos(x) == sk_mp(x) and min_pos(-np.abs(x)) == sk_mp(-np.abs(x))
+    z = rs.randn(5, 7) * 50
+    np.testing.assert_allclose(log_logistic(z), -np.logaddexp(0, -z), atol=1e-14)
+
+
+@pytest.mark.parametrize("degree", [1, 2, 3, 4])
+@pytest.mark.parametrize("interaction_only", [False, True])
+@pytest.mark.parametrize("include_bias", [True, False])
+def test_polynomial_features_dense_and_csr(degree, interaction_only, include_bias):
+    from sklearn.preprocessing import PolynomialFeatures as SKPoly
+    from sq_learn_amd.preprocessing import PolynomialFeatures
+    rs = np.random.RandomState(degree)
+    X = rs.randn(20, 5)
+    Xs = sp.random(30, 7, density=0.4, random_state=1, format="csr")
+    kw = dict(interaction_only=interaction_only, include_bias=include_bias)
+    a, b = PolynomialFeatures(degree, **kw).fit(X), SKPoly(degree, **kw).fit(X)
+    np.testing.assert_allclose(a.transform(X), b.transform(X), atol=1e-12)
+    np.testing.assert_array_equal(a.powers_, b.powers_)
+    assert a.n_output_features_ == b.n_output_features_
+    A = PolynomialFeatures(degree, **kw).fit(Xs).transform(Xs)
+    B = SKPoly(degree, **kw).fit(Xs).transform(Xs)
+    assert sp.issparse(A) == sp.issparse(B) and A.shape == B.shape
+    assert abs(A - B).max() < 1e-12
