@@ -106,7 +106,15 @@ class PolynomialFeatures(TransformerMixin, BaseEstimator):
                 for d in range(1, self.degree + 1):
                     blocks.append(_csr_degree(Xc, F, d, self.interaction_only))
                 return sp.hstack(blocks, format="csr").astype(X.dtype)
-            X = X.toarray()
+            # higher degrees: column products on CSC (stays sparse)
+            Xc = sp.csc_matrix(X)
+            cols = []
+            for c in _combinations(F, self.degree, self.interaction_only, self.include_bias):
+                col = sp.csc_matrix(np.ones((Xc.shape[0], 1)), dtype=Xc.dtype)
+                for j in c:
+                    col = col.multiply(Xc[:, j])
+                cols.append(sp.csc_matrix(col))
+            return sp.hstack(cols, format="csr")
         numpy_in = not isinstance(X, torch.Tensor)
         Xt = torch.as_tensor(check_array(X, dtype=[np.float64, np.float32])) if numpy_in else X
         if not Xt.is_floating_point():
