@@ -2,3 +2,5 @@
 from .models.cluster import KMeans, LloydEngine, QMeans, k_means, kmeans_plusplus, qMeans_  # noqa: F401
 from .models.cluster.minibatch import MiniBatchKMeans  # noqa: F401
 from .models.cluster.dbscan import DBSCAN, dbscan  # noqa: F401
+from .models.cluster.hierarchical import (AgglomerativeClustering, FeatureAgglomeration,  # noqa: F401
+                                          linkage_tree, ward_tree)

@@ -1,0 +1,251 @@
+"""Agglomerative clustering (reference ``cluster/_agglomerative.py`` +
+``_hierarchical_fast.pyx``).
+
+Pairwise distances are computed on the data's device (exact difference
+form, no norm expansion, so merge heights match a float64 pdist), reduced
+to the condensed upper triangle, and handed to the host-native linkage core
+``sqh_linkage`` (``csrc/host/hier_host.cpp``: nearest-neighbour chain with
+Lance-Williams updates, Prim's MST for single linkage, stable height sort,
+union-find relabelling).  Trees are unstructured (no ``connectivity``
+graph): a connectivity-constrained build raises ``NotImplementedError``.
+"""
+
+from heapq import heappush, heappushpop
+
+import numpy as np
+import torch
+
+from ...base import BaseEstimator, ClusterMixin, TransformerMixin
+from ...ops import _host
+from ...runtime.device import resolve_device, to_tensor
+from ...utils.validation import check_array, check_is_fitted
+
+_METHODS = {"single": 0, "complete": 1, "average": 2, "weighted": 3, "ward": 4}
+
+
+def _condensed(X, affinity, device=None):
+    """float64 condensed distance vector (n(n-1)/2) for the affinity."""
+    if affinity == "precomputed":
+        D = np.asarray(X, dtype=np.float64)
+        iu = np.triu_indices(D.shape[0], k=1)
+        return np.ascontiguousarray(D[iu])
+    if callable(affinity):
+        D = np.asarray(affinity(np.asarray(X)), dtype=np.float64)
+        iu = np.triu_indices(D.shape[0], k=1)
+        return np.ascontiguousarray(D[iu])
+    Xt = X if isinstance(X, torch.Tensor) else to_tensor(np.asarray(X, dtype=np.float64),
+                                                         resolve_device(device))
+    Xt = Xt.to(torch.float64)
+    n = Xt.shape[0]
+    if affinity in ("euclidean", "l2"):
+        D = torch.cdist(Xt, Xt, compute_mode="donot_use_mm_for_euclid_dist")
+    elif affinity in ("l1", "manhattan", "cityblock"):
+        D = torch.cdist(Xt, Xt, p=1.0)
+    elif affinity == "cosine":
+        nrm = torch.linalg.vector_norm(Xt, dim=1, keepdim=True)
+        D = (1.0 - (Xt / nrm) @ (Xt / nrm).T).clamp_(min=0)
+    else:
+        from scipy.spatial.distance import pdist
+        return np.ascontiguousarray(pdist(np.asarray(Xt.cpu()), metric=affinity))
+    iu = torch.triu_indices(n, n, offset=1, device=D.device)
+    return np.ascontiguousarray(D[iu[0], iu[1]].cpu().numpy())
+
+
+def _linkage_matrix(cond, n, method, ordered_children=True):
+    Z = np.zeros((max(n - 1, 0), 4), dtype=np.float64)
+    if n > 1:
+        rc = _host.lib().sqh_linkage(_host.ptr(cond), n, _METHODS[method],
+                                     int(ordered_children), _host.ptr(Z))
+        if rc != 0:
+            raise ValueError("Unknown linkage type %s" % method)
+    return Z
+
+
+def ward_tree(X, *, connectivity=None, n_clusters=None, return_distance=False, device=None):
+    """(children, n_connected_components, n_leaves, parents[, distances])."""
+    if connectivity is not None:
+        raise NotImplementedError("connectivity-constrained trees are not implemented")
+    X = X if isinstance(X, torch.Tensor) else check_array(X)
+    n = X.shape[0]
+    if n_clusters is not None:
+        import warnings
+        warnings.warn("Partial build of the tree is implemented only for structured clustering "
+                      "(i.e. with explicit connectivity). The algorithm will build the full "
+                      "tree and only retain the lower branches required for the specified "
+                      "number of clusters", stacklevel=2)
+    Z = _linkage_matrix(_condensed(X, "euclidean", device), n, "ward")
+    children = Z[:, :2].astype(np.intp)
+    if return_distance:
+        return children, 1, n, None, Z[:, 2]
+    return children, 1, n, None
+
+
+def linkage_tree(X, connectivity=None, n_clusters=None, linkage="complete",
+                 affinity="euclidean", return_distance=False, device=None):
+    if connectivity is not None:
+        raise NotImplementedError("connectivity-constrained trees are not implemented")
+    if linkage not in ("average", "complete", "single"):
+        raise ValueError("Unknown linkage option, linkage should be one of %s, but %s was given"
+                         % (("average", "complete", "single"), linkage))
+    if affinity == "precomputed":
+        X = check_array(X)
+        if X.shape[0] != X.shape[1]:
+            raise ValueError("Distance matrix should be square, Got matrix of shape {X.shape}")
+    n = X.shape[0]
+    # the reference labels single-linkage MST edges without ordering the
+    # children for its own (non-scipy) metrics
+    mst_path = linkage == "single" and affinity in ("euclidean", "l2", "l1", "manhattan",
+                                                    "cityblock", "chebyshev", "minkowski")
+    Z = _linkage_matrix(_condensed(X, affinity, device), n, linkage,
+                        ordered_children=not mst_path)
+    children = Z[:, :2].astype(np.intp)
+    if return_distance:
+        return children, 1, n, None, Z[:, 2]
+    return children, 1, n, None
+
+
+def _complete_linkage(*a, **k):
+    return linkage_tree(*a, linkage="complete", **k)
+
+
+def _average_linkage(*a, **k):
+    return linkage_tree(*a, linkage="average", **k)
+
+
+def _single_linkage(*a, **k):
+    return linkage_tree(*a, linkage="single", **k)
+
+
+_TREE_BUILDERS = dict(ward=ward_tree, complete=_complete_linkage, average=_average_linkage,
+                      single=_single_linkage)
+
+
+def _hc_get_descendent(node, children, n_leaves):
+    ind = [node]
+    if node < n_leaves:
+        return ind
+    descendent = []
+    while ind:
+        i = ind.pop()
+        if i < n_leaves:
+            descendent.append(i)
+        else:
+            ind.extend(children[i - n_leaves])
+    return descendent
+
+
+def _hc_cut(n_clusters, children, n_leaves):
+    if n_clusters > n_leaves:
+        raise ValueError("Cannot extract more clusters than samples: %s clusters where given "
+                         "for a tree with %s leaves." % (n_clusters, n_leaves))
+    nodes = [-(max(children[-1]) + 1)]
+    for _ in range(n_clusters - 1):
+        these = children[-nodes[0] - n_leaves]
+        heappush(nodes, -these[0])
+        heappushpop(nodes, -these[1])
+    label = np.zeros(n_leaves, dtype=np.intp)
+    for i, node in enumerate(nodes):
+        label[_hc_get_descendent(-node, children, n_leaves)] = i
+    return label
+
+
+class AgglomerativeClustering(ClusterMixin, BaseEstimator):
+    """Recursively merges the pair of clusters that minimally increases a
+    linkage distance (n_clusters or distance_threshold; linkage ward /
+    complete / average / single)."""
+
+    def __init__(self, n_clusters=2, *, affinity="euclidean", memory=None, connectivity=None,
+                 compute_full_tree="auto", linkage="ward", distance_threshold=None,
+                 compute_distances=False, device=None):
+        self.n_clusters = n_clusters
+        self.distance_threshold = distance_threshold
+        self.memory = memory
+        self.connectivity = connectivity
+        self.compute_full_tree = compute_full_tree
+        self.linkage = linkage
+        self.affinity = affinity
+        self.compute_distances = compute_distances
+        self.device = device
+
+    def fit(self, X, y=None):
+        if not isinstance(X, torch.Tensor):
+            X = check_array(X, ensure_min_samples=2)
+        self.n_features_in_ = X.shape[1]
+        if self.n_clusters is not None and self.n_clusters <= 0:
+            raise ValueError("n_clusters should be an integer greater than 0. %s was provided."
+                             % str(self.n_clusters))
+        if not ((self.n_clusters is None) ^ (self.distance_threshold is None)):
+            raise ValueError("Exactly one of n_clusters and distance_threshold has to be set, "
+                             "and the other needs to be None.")
+        if self.distance_threshold is not None and not self.compute_full_tree:
+            raise ValueError("compute_full_tree must be True if distance_threshold is set.")
+        if self.linkage == "ward" and self.affinity != "euclidean":
+            raise ValueError("%s was provided as affinity. Ward can only work with euclidean "
+                             "distances." % (self.affinity,))
+        if self.linkage not in _TREE_BUILDERS:
+            raise ValueError("Unknown linkage type %s. Valid options are %s"
+                             % (self.linkage, _TREE_BUILDERS.keys()))
+        if self.connectivity is not None:
+            raise NotImplementedError("connectivity-constrained agglomeration is not implemented")
+        kwargs = {} if self.linkage == "ward" else {"affinity": self.affinity}
+        return_distance = self.distance_threshold is not None or self.compute_distances
+        out = _TREE_BUILDERS[self.linkage](X, connectivity=None, n_clusters=None,
+                                           return_distance=return_distance, device=self.device,
+                                           **kwargs)
+        self.children_, self.n_connected_components_, self.n_leaves_, _ = out[:4]
+        if return_distance:
+            self.distances_ = out[-1]
+        if self.distance_threshold is not None:
+            self.n_clusters_ = int(np.count_nonzero(self.distances_ >= self.distance_threshold)) + 1
+        else:
+            self.n_clusters_ = self.n_clusters
+        self.labels_ = _hc_cut(self.n_clusters_, self.children_, self.n_leaves_)
+        return self
+
+    def fit_predict(self, X, y=None):
+        return self.fit(X).labels_
+
+
+class FeatureAgglomeration(AgglomerativeClustering, TransformerMixin):
+    """Agglomerates features: clusters the columns, then pools each cluster
+    (``pooling_func``, default mean)."""
+
+    def __init__(self, n_clusters=2, *, affinity="euclidean", memory=None, connectivity=None,
+                 compute_full_tree="auto", linkage="ward", pooling_func=np.mean,
+                 distance_threshold=None, compute_distances=False, device=None):
+        super().__init__(n_clusters=n_clusters, memory=memory, connectivity=connectivity,
+                         compute_full_tree=compute_full_tree, linkage=linkage, affinity=affinity,
+                         distance_threshold=distance_threshold,
+                         compute_distances=compute_distances, device=device)
+        self.pooling_func = pooling_func
+
+    def fit(self, X, y=None, **params):
+        X = check_array(X, ensure_min_features=2)
+        super().fit(X.T)
+        self.n_features_in_ = X.shape[1]
+        return self
+
+    @property
+    def fit_predict(self):
+        raise AttributeError
+
+    def transform(self, X):
+        check_is_fitted(self)
+        X = check_array(X)
+        if X.shape[1] != self.n_features_in_:
+            raise ValueError(f"X has {X.shape[1]} features, but FeatureAgglomeration is "
+                             f"expecting {self.n_features_in_} features as input.")
+        if self.pooling_func == np.mean:
+            size = np.bincount(self.labels_)
+            n_samples = X.shape[0]
+            nX = np.array([np.bincount(self.labels_, X[i, :]) / size for i in range(n_samples)])
+        else:
+            nX = [self.pooling_func(X[:, self.labels_ == l], axis=1)
+                  for l in np.unique(self.labels_)]
+            nX = np.array(nX).T
+        return nX
+
+    def inverse_transform(self, Xred):
+        check_is_fitted(self)
+        unil, inverse = np.unique(self.labels_, return_inverse=True)
+        return Xred[..., inverse]

@@ -42,6 +42,7 @@ _SIGS = {
     "sqh_sparse_manhattan": (None, [_P, _P, _P, _P, _P, _P, _LL, _LL, _P]),
     "sqh_cholesky_delete": (None, [_P, _LL, _LL, _LL]),
     "sqh_csr_poly": (_LL, [_P, _P, _P, _LL, _LL, _I, _I, _P, _P, _P]),
+    "sqh_linkage": (_I, [_P, _LL, _I, _I, _P]),
 }
 
 

@@ -283,3 +283,41 @@ def test_polynomial_features_dense_and_csr(degree, interaction_only, include_bia
     B = SKPoly(degree, **kw).fit(Xs).transform(Xs)
     assert sp.issparse(A) == sp.issparse(B) and A.shape == B.shape
     assert abs(A - B).max() < 1e-12
+
+
+# ------------------------------------------------------------ hierarchical
+@pytest.mark.parametrize("linkage,affinity", [("ward", "euclidean"), ("complete", "euclidean"),
+                                              ("complete", "manhattan"), ("average", "cosine"),
+                                              ("average", "euclidean"), ("single", "euclidean"),
+                                              ("single", "manhattan"), ("single", "cosine")])
+def test_agglomerative_matches_sklearn(linkage, affinity):
+    from sklearn.cluster import AgglomerativeClustering as SKAgg
+    from sq_learn_amd.cluster import AgglomerativeClustering
+    X = np.random.RandomState(0).randn(120, 4)
+    kw = {} if linkage == "ward" else {"affinity": affinity}
+    skkw = {} if linkage == "ward" else {"metric": affinity}
+    a = AgglomerativeClustering(5, linkage=linkage, compute_distances=True, **kw).fit(X)
+    b = SKAgg(5, linkage=linkage, compute_distances=True, **skkw).fit(X)
+    np.testing.assert_array_equal(a.children_, b.children_)
+    np.testing.assert_allclose(a.distances_, b.distances_, atol=1e-12)
+    np.testing.assert_array_equal(a.labels_, b.labels_)
+
+
+def test_agglomerative_threshold_precomputed_and_features():
+    from sklearn.cluster import AgglomerativeClustering as SKAgg, FeatureAgglomeration as SKFA
+    from sq_learn_amd.cluster import AgglomerativeClustering, FeatureAgglomeration
+    X = np.random.RandomState(1).randn(90, 6)
+    a = AgglomerativeClustering(None, distance_threshold=3.0).fit(X)
+    b = SKAgg(None, distance_threshold=3.0).fit(X)
+    assert a.n_clusters_ == b.n_clusters_
+    np.testing.assert_array_equal(a.labels_, b.labels_)
+    D = skm.pairwise_distances(X)
+    a = AgglomerativeClustering(4, affinity="precomputed", linkage="average").fit(D)
+    b = SKAgg(4, metric="precomputed", linkage="average").fit(D)
+    np.testing.assert_array_equal(a.labels_, b.labels_)
+    fa, fb = FeatureAgglomeration(3).fit(X), SKFA(3).fit(X)
+    np.testing.assert_allclose(fa.transform(X), fb.transform(X))
+    np.testing.assert_allclose(fa.inverse_transform(fa.transform(X)),
+                               fb.inverse_transform(fb.transform(X)))
+    with pytest.raises(ValueError):
+        AgglomerativeClustering(2, linkage="ward", affinity="manhattan").fit(X)
