@@ -1,0 +1,10 @@
+"""Linear models (reference ``sklearn.linear_model``)."""
+from ._base import LinearRegression
+from ._coordinate_descent import (ElasticNet, ElasticNetCV, Lasso, LassoCV, enet_path,
+                                  lasso_path)
+from ._logistic import LogisticRegression
+from ._ridge import Ridge, RidgeClassifier, RidgeClassifierCV, RidgeCV, ridge_regression
+
+__all__ = ["LinearRegression", "ElasticNet", "ElasticNetCV", "Lasso", "LassoCV", "enet_path",
+           "lasso_path", "Ridge", "RidgeClassifier", "RidgeClassifierCV", "RidgeCV",
+           "ridge_regression", "LogisticRegression"]
