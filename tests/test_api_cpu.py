@@ -3,6 +3,7 @@ MiniBatchKMeans, IncrementalPCA, pairwise/metrics parity with scikit-learn,
 and an estimator-contract sweep over ``all_estimators()`` (the analogue of
 the reference's ``test_common.py`` / ``estimator_checks.py``; SURVEY.md §4
 item 4)."""
+import inspect
 import pickle
 import warnings
 
@@ -227,6 +228,10 @@ def _fit(est):
         return est.fit(X, np.where(y == 0, -1.0, 1.0))
     if name in ("KNeighborsClassifier", "KNeighborsRegressor", "Pipeline"):
         return est.fit(X, y)
+    yp = inspect.signature(est.fit).parameters.get("y")
+    if yp is not None and yp.default is inspect.Parameter.empty:
+        return est.fit(X, y.astype(float) if getattr(est, "_estimator_type", "") == "regressor"
+                       else y)
     return est.fit(X)
 
 
