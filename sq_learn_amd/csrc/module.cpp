@@ -27,6 +27,13 @@ __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int,
 // pairwise_fast.hip
 __attribute__((weak)) int sq_pairwise_reduce(const void*, const void*, void*, int, int, int, int,
                                              double, int, void*);
+// forest.hip
+__attribute__((weak)) int sq_forest_apply(const void*, const void*, const void*, const void*,
+                                          const void*, int, const void*, long long, int, void*,
+                                          void*);
+__attribute__((weak)) int sq_forest_predict(const void*, const void*, const void*, const void*,
+                                            const void*, const void*, int, const void*, int,
+                                            const void*, long long, int, double, void*, void*);
 // elkan.hip
 __attribute__((weak)) int sq_elkan_step(const void*, const void*, const void*, const void*,
                                         const void*, void*, void*, void*, long long, int, int,
@@ -164,6 +171,24 @@ static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {
   return ret(sq_pairwise_reduce(P(X), P(Y), P(out), n, m, d, op, p, dt, P(st)));
 }
 
+static PyObject* py_forest_apply(PyObject*, PyObject* a) {
+  unsigned long long l, r, f, t, o, X, out, st; int T, d; long long n;
+  if (!PyArg_ParseTuple(a, "KKKKKiKLiKK", &l, &r, &f, &t, &o, &T, &X, &n, &d, &out, &st))
+    return nullptr;
+  CHECK(sq_forest_apply)
+  return ret(sq_forest_apply(P(l), P(r), P(f), P(t), P(o), T, P(X), n, d, P(out), P(st)));
+}
+
+static PyObject* py_forest_predict(PyObject*, PyObject* a) {
+  unsigned long long l, r, f, t, ml, o, v, X, out, st; int T, s_act, d; long long n; double sc;
+  if (!PyArg_ParseTuple(a, "KKKKKKiKiKLidKK", &l, &r, &f, &t, &ml, &o, &T, &v, &s_act, &X, &n, &d,
+                        &sc, &out, &st))
+    return nullptr;
+  CHECK(sq_forest_predict)
+  return ret(sq_forest_predict(P(l), P(r), P(f), P(t), P(ml), P(o), T, P(v), s_act, P(X), n, d,
+                               sc, P(out), P(st)));
+}
+
 static PyObject* py_elkan_step(PyObject*, PyObject* a) {
   unsigned long long X, C, hcc, sn, sh, lab, up, lo, st; long long n; int d, k, dt, init;
   if (!PyArg_ParseTuple(a, "KKKKKKKKLiiiiK", &X, &C, &hcc, &sn, &sh, &lab, &up, &lo, &n, &d, &k,
@@ -291,6 +316,8 @@ static PyObject* py_device_arch(PyObject*, PyObject*) {
 }
 
 static PyMethodDef methods[] = {
+    {"forest_apply", py_forest_apply, METH_VARARGS, "leaf ids of (row, tree) pairs"},
+    {"forest_predict", py_forest_predict, METH_VARARGS, "sum of leaf values over trees"},
     {"trunc_normal_add", py_trunc_normal_add, METH_VARARGS, "x += TN(-b,b) (Philox keyed)"},
     {"philox_normal", py_philox_normal, METH_VARARGS, "fill with mean+std*N(0,1)"},
     {"philox_uniform", py_philox_uniform, METH_VARARGS, "fill with U(0,1)"},

@@ -45,6 +45,11 @@ _SIGS = {
     "sqh_linkage": (_I, [_P, _LL, _I, _I, _P]),
     "sqh_enet_cd_dense": (None, [_P, _D, _D, _P, _P, _LL, _LL, _I, _D, _U, _I, _I, _P]),
     "sqh_enet_cd_gram": (None, [_P, _D, _D, _P, _P, _D, _LL, _I, _D, _U, _I, _I, _P]),
+    "sqh_forest_build": (None, [_P, _P, _P, _LL, _LL, _I, _P, _LL, _P, _P, _I, _I, _P]),
+    "sqh_tree_sizes": (None, [_P, _P]),
+    "sqh_tree_copy": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "sqh_tree_free": (None, [_P]),
+    "sqh_forest_apply": (None, [_P, _P, _P, _P, _P, _I, _P, _LL, _LL, _P]),
 }
 
 
