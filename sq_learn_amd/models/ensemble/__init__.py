@@ -1,6 +1,11 @@
 """Ensembles (reference ``sklearn.ensemble``)."""
+from ._hist_gradient_boosting import (HistGradientBoostingClassifier,
+                                      HistGradientBoostingRegressor)
+from ._gb import GradientBoostingClassifier, GradientBoostingRegressor
 from ._forest import (ExtraTreesClassifier, ExtraTreesRegressor, RandomForestClassifier,
                       RandomForestRegressor, RandomTreesEmbedding)
 
 __all__ = ["RandomForestClassifier", "RandomForestRegressor", "ExtraTreesClassifier",
-           "ExtraTreesRegressor", "RandomTreesEmbedding"]
+           "ExtraTreesRegressor", "RandomTreesEmbedding", "GradientBoostingClassifier",
+           "GradientBoostingRegressor", "HistGradientBoostingClassifier",
+           "HistGradientBoostingRegressor"]

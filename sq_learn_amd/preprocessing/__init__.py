@@ -211,3 +211,16 @@ __all__ = ["StandardScaler", "MinMaxScaler", "Normalizer", "normalize"]
 
 
 from ._polynomial import PolynomialFeatures  # noqa: E402,F401
+from ._encoders import (LabelBinarizer, LabelEncoder, MultiLabelBinarizer,  # noqa: E402,F401
+                        OneHotEncoder, OrdinalEncoder, label_binarize)
+from ._data_extra import (Binarizer, FunctionTransformer, KBinsDiscretizer,  # noqa: E402,F401
+                          KernelCenterer, MaxAbsScaler, PowerTransformer, QuantileTransformer,
+                          RobustScaler, SplineTransformer, add_dummy_feature, binarize,
+                          maxabs_scale, power_transform, quantile_transform, robust_scale)
+
+__all__ += ["PolynomialFeatures", "LabelBinarizer", "LabelEncoder", "MultiLabelBinarizer",
+            "OneHotEncoder", "OrdinalEncoder", "label_binarize", "Binarizer",
+            "FunctionTransformer", "KBinsDiscretizer", "KernelCenterer", "MaxAbsScaler",
+            "PowerTransformer", "QuantileTransformer", "RobustScaler", "SplineTransformer",
+            "add_dummy_feature", "binarize", "maxabs_scale", "power_transform",
+            "quantile_transform", "robust_scale"]

@@ -217,9 +217,14 @@ def _instance(cls):
     return cls(**kw)
 
 
+_LABEL_TRANSFORMERS = ("LabelEncoder", "LabelBinarizer", "MultiLabelBinarizer")
+
+
 def _fit(est):
     X, y = _DATA
     name = type(est).__name__
+    if name in _LABEL_TRANSFORMERS:
+        return est.fit([[v] for v in y] if name == "MultiLabelBinarizer" else y)
     if name == "IsotonicRegression":
         return est.fit(X[:, 0], X[:, 1])
     if name == "FeatureHasher":
@@ -252,7 +257,11 @@ def test_estimator_contract(name, cls):
         _fit(est)
     # fitted attributes survive a pickle round trip (checkpoint compatibility)
     est2 = pickle.loads(pickle.dumps(est))
-    X, _ = _DATA
+    X, y = _DATA
+    if name in _LABEL_TRANSFORMERS:
+        yy = [[v] for v in y] if name == "MultiLabelBinarizer" else y
+        np.testing.assert_array_equal(est.transform(yy), est2.transform(yy))
+        return
     if name == "IsotonicRegression":
         X = X[:, 0]
     elif name == "FeatureHasher":
