@@ -55,6 +55,11 @@ _SIGS = {
     "sqh_hgb_size": (_LL, [_P]),
     "sqh_hgb_copy": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LL]),
     "sqh_hgb_free": (None, [_P]),
+    "sqh_svm_solve": (None, [_P, _LL, _P, _P, _P, _P, _LL, _D, _LL, _I, _P, _P]),
+    "sqh_linear_svc_dual": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _I, _P, _P, _P]),
+    "sqh_linear_svr_dual": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _D, _I, _P, _P]),
+    "sqh_mt_new": (_P, [_U]),
+    "sqh_mt_free": (None, [_P]),
     "sqh_hgb_predict": (None, [_P, _LL, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
 }
 

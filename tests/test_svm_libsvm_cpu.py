@@ -1,0 +1,81 @@
+"""Kernel SVMs (libsvm SMO) and linear SVMs (liblinear dual
+CD, N10-N11) against scikit-learn (the reference's upstream solvers)."""
+import warnings
+
+import numpy as np
+import pytest
+
+sk = pytest.importorskip("sklearn")
+import sklearn.svm as sks  # noqa: E402
+from sklearn.datasets import make_classification, make_regression  # noqa: E402
+
+from sq_learn_amd.models.svm import (SVC, SVR, LinearSVC, LinearSVR, NuSVC, NuSVR,  # noqa: E402
+                                     OneClassSVM)
+
+X3, y3 = make_classification(240, 6, n_informative=4, n_classes=3, random_state=0)
+X2, y2 = make_classification(240, 6, n_informative=4, random_state=1)
+Xr, yr = make_regression(240, 5, noise=2.0, random_state=0)
+
+
+@pytest.mark.parametrize("data", [(X2, y2), (X3, y3)])
+@pytest.mark.parametrize("kw", [dict(kernel="rbf"), dict(kernel="linear", C=0.5),
+                                dict(kernel="poly", degree=2),
+                                dict(kernel="rbf", class_weight="balanced")])
+def test_svc_matches_libsvm(data, kw):
+    X, y = data
+    a, b = SVC(**kw).fit(X, y), sks.SVC(**kw).fit(X, y)
+    np.testing.assert_array_equal(a.support_, b.support_)
+    np.testing.assert_array_equal(a.n_support_, b.n_support_)
+    np.testing.assert_allclose(a.decision_function(X), b.decision_function(X), atol=5e-3)
+    assert (a.predict(X) == b.predict(X)).mean() > 0.99
+
+
+def test_nu_and_regression_svms_match_libsvm():
+    a, b = NuSVC(nu=0.3).fit(X3, y3), sks.NuSVC(nu=0.3).fit(X3, y3)
+    np.testing.assert_array_equal(a.support_, b.support_)
+    np.testing.assert_allclose(a.decision_function(X3), b.decision_function(X3), atol=5e-3)
+    for ours, ref, kw in [(SVR, sks.SVR, dict(C=10.0, epsilon=0.5)),
+                          (NuSVR, sks.NuSVR, dict(C=10.0, nu=0.3))]:
+        a, b = ours(**kw).fit(Xr, yr), ref(**kw).fit(Xr, yr)
+        np.testing.assert_array_equal(a.support_, b.support_)
+        np.testing.assert_allclose(a.predict(Xr), b.predict(Xr), rtol=1e-4, atol=1e-3)
+    a, b = OneClassSVM(nu=0.2).fit(Xr), sks.OneClassSVM(nu=0.2).fit(Xr)
+    np.testing.assert_array_equal(a.support_, b.support_)
+    np.testing.assert_allclose(a.decision_function(Xr), b.decision_function(Xr), atol=1e-6)
+    np.testing.assert_array_equal(a.predict(Xr), b.predict(Xr))
+
+
+def test_svc_probability_is_calibrated():
+    a = SVC(probability=True, random_state=0).fit(X3, y3)
+    p = a.predict_proba(X3)
+    np.testing.assert_allclose(p.sum(1), 1.0, atol=1e-6)
+    assert (p.argmax(1) == a.predict(X3)).mean() > 0.9
+
+
+@pytest.mark.parametrize("data", [(X2, y2), (X3, y3)])
+@pytest.mark.parametrize("kw", [dict(dual=True), dict(dual=True, loss="hinge"),
+                                dict(dual=True, C=0.1, class_weight="balanced"),
+                                dict(dual=True, fit_intercept=False)])
+def test_linear_svc_dual_is_bit_compatible(data, kw):
+    X, y = data
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        a = LinearSVC(random_state=0, **kw).fit(X, y)
+        b = sks.LinearSVC(random_state=0, **kw).fit(X, y)
+    np.testing.assert_allclose(a.coef_, b.coef_, atol=1e-10)
+    np.testing.assert_allclose(a.intercept_, b.intercept_, atol=1e-10)
+    assert a.n_iter_ == b.n_iter_
+
+
+def test_linear_svc_primal_and_svr():
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for kw in [dict(dual=False), dict(penalty="l1", dual=False, tol=1e-8, max_iter=100000)]:
+            a = LinearSVC(random_state=0, **kw).fit(X2, y2)
+            b = sks.LinearSVC(random_state=0, **kw).fit(X2, y2)
+            np.testing.assert_allclose(a.coef_, b.coef_, atol=1e-3)
+        for kw in [dict(), dict(epsilon=1.0, C=0.5)]:
+            a = LinearSVR(random_state=0, **kw).fit(Xr, yr)
+            b = sks.LinearSVR(random_state=0, dual=True, **kw).fit(Xr, yr)
+            np.testing.assert_allclose(a.coef_, b.coef_, atol=1e-10)
+            assert a.n_iter_ == b.n_iter_
