@@ -241,10 +241,11 @@ class LinearSVR(RegressorMixin, BaseEstimator):
             raise ValueError("loss='%s' is not supported" % self.loss)
         if self.dual:
             w = np.zeros(Xa.shape[1])
+            stream = _MTStream(seed)     # must outlive the native call
             it = _host.lib().sqh_linear_svr_dual(
                 Xa.ctypes.data, Xa.shape[0], Xa.shape[1], y.ctypes.data, Cvec.ctypes.data,
                 int(self.loss == "epsilon_insensitive"), float(self.epsilon), float(self.tol),
-                int(self.max_iter), _MTStream(seed).h, w.ctypes.data)
+                int(self.max_iter), stream.h, w.ctypes.data)
         else:
             eps = self.epsilon
 
