@@ -50,3 +50,7 @@ class DistributedError(RuntimeError):
 
 class NumericalGuardError(FloatingPointError):
     """The per-iteration NaN/inf guard tripped."""
+
+
+class UndefinedMetricWarning(UserWarning):
+    """A metric is ill-defined (e.g. no positive predictions for precision)."""

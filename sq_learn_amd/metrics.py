@@ -18,3 +18,20 @@ from .utils.pairwise import (PAIRWISE_DISTANCE_FUNCTIONS, PAIRWISE_KERNEL_FUNCTI
                              paired_euclidean_distances, paired_manhattan_distances,
                              pairwise_distances, pairwise_distances_argmin,
                              pairwise_distances_argmin_min)
+from .utils.metrics_extra import (SCORERS, auc, average_precision_score,  # noqa: F401,E402
+                                  balanced_accuracy_score, brier_score_loss, check_scoring,
+                                  classification_report, cohen_kappa_score, coverage_error,
+                                  dcg_score, det_curve, explained_variance_score, f1_score,
+                                  fbeta_score, hamming_loss, hinge_loss, jaccard_score,
+                                  label_ranking_average_precision_score, label_ranking_loss,
+                                  log_loss, make_scorer, matthews_corrcoef, max_error,
+                                  mean_absolute_error, mean_absolute_percentage_error,
+                                  mean_gamma_deviance, mean_pinball_loss, mean_poisson_deviance,
+                                  mean_squared_log_error, mean_tweedie_deviance,
+                                  median_absolute_error, multilabel_confusion_matrix, ndcg_score,
+                                  precision_recall_curve, precision_recall_fscore_support,
+                                  precision_score, recall_score, roc_auc_score, roc_curve,
+                                  top_k_accuracy_score, zero_one_loss)
+from .utils.metrics_extra import get_scorer_ext as get_scorer  # noqa: F401,E402
+from .utils.metrics_extra import mean_squared_error_ext as mean_squared_error  # noqa: F401,E402,F811
+from .utils.metrics_extra import r2_score_ext as r2_score  # noqa: F401,E402,F811
