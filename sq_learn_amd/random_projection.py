@@ -1,0 +1,3 @@
+"""Reference-layout import path (``sklearn.random_projection``)."""
+from .kernel_approximation import (GaussianRandomProjection, SparseRandomProjection,  # noqa: F401
+                                   johnson_lindenstrauss_min_dim)
