@@ -82,7 +82,11 @@ class KMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                           f"KMeans instead of n_init={n_init}.", RuntimeWarning, stacklevel=2)
             n_init = 1
         rs = check_random_state(self.random_state)
-        seed = seed_from_random_state(self.random_state)
+        # A RandomState object must reach k-means++ unconsumed (reference
+        # _kmeans.py:869 hands it straight to _init_centroids), so the
+        # stochastic-layer seed is read from its state instead of drawn.
+        seed = (int(rs.get_state()[1][0]) if isinstance(self.random_state, np.random.RandomState)
+                else seed_from_random_state(self.random_state))
         mean, var = global_mean_var(data)
         tol = float(var.mean()) * self.tol
         Xc = data.X - mean.to(data.X.device).to(data.X.dtype) if data.X.dtype != torch.bfloat16 \

@@ -1,5 +1,6 @@
 """Linear models (reference ``sklearn.linear_model``)."""
 from ._base import LinearRegression
+from ._bayes import ARDRegression, BayesianRidge
 from ._coordinate_descent import (ElasticNet, ElasticNetCV, Lasso, LassoCV, enet_path,
                                   lasso_path)
 from ._logistic import LogisticRegression
@@ -7,4 +8,4 @@ from ._ridge import Ridge, RidgeClassifier, RidgeClassifierCV, RidgeCV, ridge_re
 
 __all__ = ["LinearRegression", "ElasticNet", "ElasticNetCV", "Lasso", "LassoCV", "enet_path",
            "lasso_path", "Ridge", "RidgeClassifier", "RidgeClassifierCV", "RidgeCV",
-           "ridge_regression", "LogisticRegression"]
+           "ridge_regression", "LogisticRegression", "ARDRegression", "BayesianRidge"]
