@@ -235,6 +235,19 @@ class DensityMixin:
         pass
 
 
+class OutlierMixin:
+    """Outlier detectors: ``fit_predict`` returns +1 inliers / -1 outliers
+    (reference sklearn/base.py:OutlierMixin)."""
+    _estimator_type = "outlier_detector"
+
+    def fit_predict(self, X, y=None):
+        return self.fit(X).predict(X)
+
+
+def is_outlier_detector(est):
+    return getattr(est, "_estimator_type", None) == "outlier_detector"
+
+
 def is_classifier(est):
     return getattr(est, "_estimator_type", None) == "classifier"
 

@@ -4,8 +4,12 @@ from ._bayes import ARDRegression, BayesianRidge
 from ._coordinate_descent import (ElasticNet, ElasticNetCV, Lasso, LassoCV, enet_path,
                                   lasso_path)
 from ._logistic import LogisticRegression
+from ._stochastic_gradient import (PassiveAggressiveClassifier, PassiveAggressiveRegressor,
+                                   Perceptron, SGDClassifier, SGDOneClassSVM, SGDRegressor)
 from ._ridge import Ridge, RidgeClassifier, RidgeClassifierCV, RidgeCV, ridge_regression
 
 __all__ = ["LinearRegression", "ElasticNet", "ElasticNetCV", "Lasso", "LassoCV", "enet_path",
            "lasso_path", "Ridge", "RidgeClassifier", "RidgeClassifierCV", "RidgeCV",
-           "ridge_regression", "LogisticRegression", "ARDRegression", "BayesianRidge"]
+           "ridge_regression", "LogisticRegression", "ARDRegression", "BayesianRidge", "SGDClassifier", "SGDRegressor",
+           "SGDOneClassSVM", "Perceptron", "PassiveAggressiveClassifier",
+           "PassiveAggressiveRegressor"]
