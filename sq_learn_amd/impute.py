@@ -49,6 +49,7 @@ class MissingIndicator(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _arr(X)
+        self._check_n_features(X, reset=False)
         m = _mask(X, self.missing_values)
         if self.features == "missing-only":
             new = np.setdiff1d(np.flatnonzero(m.any(axis=0)), self.features_)
@@ -179,6 +180,7 @@ class KNNImputer(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _arr(X).copy()
+        self._check_n_features(X, reset=False)
         m = _mask(X, self.missing_values)
         Xo = X.copy()
         rows = np.flatnonzero(m[:, self._valid_mask].any(axis=1))
@@ -313,6 +315,7 @@ class IterativeImputer(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _arr(X)
+        self._check_n_features(X, reset=False)
         mask = _mask(X, self.missing_values)[:, self._valid]
         Xt = self.initial_imputer_.transform(X)
         for f, others, e in self.imputation_sequence_:

@@ -59,6 +59,7 @@ class RBFSampler(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _dense(X)
+        self._check_n_features(X, reset=False)
         _nf(self, X)
         proj = _mm(X, self.random_weights_) + self.random_offset_
         return np.cos(proj) * np.sqrt(2.0) / np.sqrt(self.n_components)
@@ -82,6 +83,7 @@ class SkewedChi2Sampler(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _dense(X)
+        self._check_n_features(X, reset=False)
         if (X <= -self.skewedness).any():
             raise ValueError("X may not contain entries smaller than -skewedness.")
         proj = _mm(np.log(X + self.skewedness), self.random_weights_) + self.random_offset_
@@ -113,6 +115,7 @@ class AdditiveChi2Sampler(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _dense(X)
+        self._check_n_features(X, reset=False)
         if (X < 0).any():
             raise ValueError("Negative values in data passed to X in AdditiveChi2Sampler.fit")
         nz = X > 0
@@ -182,6 +185,7 @@ class Nystroem(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _dense(X)
+        self._check_n_features(X, reset=False)
         return _mm(self._k(X, self.components_), self.normalization_.T)
 
 
@@ -205,6 +209,7 @@ class PolynomialCountSketch(TransformerMixin, BaseEstimator):
     def transform(self, X):
         check_is_fitted(self)
         X = _dense(X) * np.sqrt(self.gamma)
+        self._check_n_features(X, reset=False)
         if self.coef0 != 0:
             X = np.hstack([X, np.full((X.shape[0], 1), np.sqrt(self.coef0))])
         count_sketches = np.zeros((X.shape[0], self.degree, self.n_components), dtype=np.complex128)

@@ -1,6 +1,6 @@
-"""``cross_validate`` / ``cross_val_score`` / ``cross_val_predict`` and a small
-``GridSearchCV`` (reference ``model_selection/_validation.py:47-280``,
-``_search.py``).
+"""``cross_validate`` / ``cross_val_score`` / ``cross_val_predict``
+(reference ``model_selection/_validation.py:47-280``); searches live in
+``_search.py``.
 
 The reference fans folds out over joblib worker processes
 (``_validation.py:248``).  Here a fold's fit already fills the GPU (one
@@ -9,7 +9,6 @@ process; ``n_jobs`` is accepted for API compatibility and ignored.  Scoring
 strings cover the metrics this framework implements.
 """
 
-import itertools
 import time
 import warnings
 
@@ -28,19 +27,31 @@ _SCORERS = {
 }
 
 
+class _PassthroughScorer:
+    """est.score (picklable, so fitted searches can be checkpointed)."""
+
+    def __call__(self, est, X, y=None):
+        return est.score(X, y) if y is not None else est.score(X)
+
+
+class _SimpleScorer:
+    def __init__(self, name):
+        self.name = name
+
+    def __call__(self, est, X, y):
+        fn, sign, method = _SCORERS[self.name]
+        return sign * fn(y, getattr(est, method)(X))
+
+
 def get_scorer(scoring):
     if scoring is None:
-        return lambda est, X, y: est.score(X, y) if y is not None else est.score(X)
+        return _PassthroughScorer()
     if callable(scoring):
         return scoring
     if scoring not in _SCORERS:
-        raise ValueError(f"{scoring!r} is not a valid scoring value. Valid options are "
-                         f"{sorted(_SCORERS)}")
-    fn, sign, method = _SCORERS[scoring]
-
-    def scorer(est, X, y):
-        return sign * fn(y, getattr(est, method)(X))
-    return scorer
+        from ..utils.metrics_extra import get_scorer_ext
+        return get_scorer_ext(scoring)
+    return _SimpleScorer(scoring)
 
 
 def _fit_and_score(est, X, y, train, test, scorers, fit_params, return_train_score,
@@ -63,9 +74,19 @@ def _fit_and_score(est, X, y, train, test, scorers, fit_params, return_train_sco
                 "train": dict(nan) if return_train_score else None, "estimator": est}
     fit_time = time.perf_counter() - t0
     t1 = time.perf_counter()
-    test_scores = {k: float(s(est, Xte, yte)) for k, s in scorers.items()}
+    def score(s, Xs, ys):
+        try:
+            return float(s(est, Xs, ys))
+        except Exception as e:
+            if error_score == "raise":
+                raise
+            warnings.warn(f"Scoring failed. The score on this train-test partition for these "
+                          f"parameters will be set to {error_score}. Details: {e!r}",
+                          UserWarning)
+            return error_score
+    test_scores = {k: score(s, Xte, yte) for k, s in scorers.items()}
     score_time = time.perf_counter() - t1
-    train_scores = ({k: float(s(est, Xtr, ytr)) for k, s in scorers.items()}
+    train_scores = ({k: score(s, Xtr, ytr) for k, s in scorers.items()}
                     if return_train_score else None)
     return {"fit_time": fit_time, "score_time": score_time, "test": test_scores,
             "train": train_scores, "estimator": est}
@@ -121,87 +142,3 @@ def cross_val_predict(estimator, X, y=None, *, groups=None, cv=None, n_jobs=None
             preds = np.empty((n,) + p.shape[1:], dtype=p.dtype)
         preds[test] = p
     return preds
-
-
-class ParameterGrid:
-    """Cartesian product of parameter lists (reference ``_search.py:49``)."""
-
-    def __init__(self, param_grid):
-        if isinstance(param_grid, dict):
-            param_grid = [param_grid]
-        self.param_grid = param_grid
-
-    def __iter__(self):
-        for p in self.param_grid:
-            items = sorted(p.items())
-            if not items:
-                yield {}
-                continue
-            keys, values = zip(*items)
-            for v in itertools.product(*values):
-                yield dict(zip(keys, v))
-
-    def __len__(self):
-        total = 0
-        for p in self.param_grid:
-            n = 1
-            for v in p.values():
-                n *= len(v)
-            total += n
-        return total
-
-
-class GridSearchCV:
-    """Exhaustive search over a parameter grid, refit on the best."""
-
-    def __init__(self, estimator, param_grid, *, scoring=None, cv=None, refit=True,
-                 return_train_score=False, error_score=np.nan, n_jobs=None, verbose=0):
-        self.estimator = estimator
-        self.param_grid = param_grid
-        self.scoring = scoring
-        self.cv = cv
-        self.refit = refit
-        self.return_train_score = return_train_score
-        self.error_score = error_score
-        self.n_jobs = n_jobs
-        self.verbose = verbose
-
-    def fit(self, X, y=None, **fit_params):
-        cands = list(ParameterGrid(self.param_grid))
-        means, stds, all_scores = [], [], []
-        for params in cands:
-            est = clone(self.estimator).set_params(**params)
-            r = cross_validate(est, X, y, scoring=self.scoring, cv=self.cv, fit_params=fit_params,
-                               error_score=self.error_score,
-                               return_train_score=self.return_train_score)
-            s = r["test_score"]
-            all_scores.append(s)
-            means.append(float(np.mean(s)))
-            stds.append(float(np.std(s)))
-        means = np.asarray(means)
-        order = np.argsort(-np.nan_to_num(means, nan=-np.inf), kind="stable")
-        ranks = np.empty(len(cands), dtype=int)
-        ranks[order] = np.arange(1, len(cands) + 1)
-        self.cv_results_ = {"params": cands, "mean_test_score": means,
-                            "std_test_score": np.asarray(stds), "rank_test_score": ranks}
-        for i in range(len(all_scores[0]) if all_scores else 0):
-            self.cv_results_[f"split{i}_test_score"] = np.array([s[i] for s in all_scores])
-        self.best_index_ = int(order[0])
-        self.best_params_ = cands[self.best_index_]
-        self.best_score_ = float(means[self.best_index_])
-        if self.refit:
-            self.best_estimator_ = clone(self.estimator).set_params(**self.best_params_)
-            if y is None:
-                self.best_estimator_.fit(X, **fit_params)
-            else:
-                self.best_estimator_.fit(X, y, **fit_params)
-        return self
-
-    def predict(self, X):
-        return self.best_estimator_.predict(X)
-
-    def score(self, X, y=None):
-        return get_scorer(self.scoring)(self.best_estimator_, X, y)
-
-    def transform(self, X):
-        return self.best_estimator_.transform(X)

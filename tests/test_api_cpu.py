@@ -214,7 +214,28 @@ def _instance(cls):
         kw = {"n_components": 3}
     elif name == "Pipeline":
         return Pipeline([("sc", StandardScaler()), ("knn", KNeighborsClassifier(3))])
+    elif name in ("GaussianRandomProjection", "SparseRandomProjection", "SelectKBest"):
+        kw = {"n_components": 3} if name != "SelectKBest" else {"k": 3}
+    elif name in ("GridSearchCV", "HalvingGridSearchCV"):
+        return cls(KNeighborsClassifier(), {"n_neighbors": [1, 3]}, cv=3)
+    elif name in ("RandomizedSearchCV", "HalvingRandomSearchCV"):
+        return cls(KNeighborsClassifier(), {"n_neighbors": [1, 3, 5]}, cv=3, random_state=0)
+    params = inspect.signature(cls.__init__).parameters
+    for arg in ("estimator", "base_estimator"):
+        if arg in params and params[arg].default is inspect.Parameter.empty:
+            from sq_learn_amd.linear_model import LogisticRegression
+            kw[arg] = LogisticRegression()
     return cls(**kw)
+
+
+# estimators that only accept non-negative features
+_NONNEG = ("CategoricalNB", "ComplementNB", "MultinomialNB", "AdditiveChi2Sampler",
+           "SkewedChi2Sampler")
+
+
+def _X(name):
+    X = _DATA[0]
+    return np.round(np.abs(X) * 2) if name in _NONNEG else X
 
 
 _LABEL_TRANSFORMERS = ("LabelEncoder", "LabelBinarizer", "MultiLabelBinarizer")
@@ -223,6 +244,7 @@ _LABEL_TRANSFORMERS = ("LabelEncoder", "LabelBinarizer", "MultiLabelBinarizer")
 def _fit(est):
     X, y = _DATA
     name = type(est).__name__
+    X = _X(name)
     if name in _LABEL_TRANSFORMERS:
         return est.fit([[v] for v in y] if name == "MultiLabelBinarizer" else y)
     if name == "IsotonicRegression":
@@ -231,7 +253,8 @@ def _fit(est):
         return est.fit()
     if name in ("LSSVC", "QLSSVC"):
         return est.fit(X, np.where(y == 0, -1.0, 1.0))
-    if name in ("KNeighborsClassifier", "KNeighborsRegressor", "Pipeline"):
+    if name in ("KNeighborsClassifier", "KNeighborsRegressor", "Pipeline") or \
+            "estimator" in est.get_params(deep=False):
         return est.fit(X, y)
     yp = inspect.signature(est.fit).parameters.get("y")
     if yp is not None and yp.default is inspect.Parameter.empty:
@@ -257,7 +280,7 @@ def test_estimator_contract(name, cls):
         _fit(est)
     # fitted attributes survive a pickle round trip (checkpoint compatibility)
     est2 = pickle.loads(pickle.dumps(est))
-    X, y = _DATA
+    X, y = _X(name), _DATA[1]
     if name in _LABEL_TRANSFORMERS:
         yy = [[v] for v in y] if name == "MultiLabelBinarizer" else y
         np.testing.assert_array_equal(est.transform(yy), est2.transform(yy))
