@@ -227,12 +227,66 @@ class TransformerMixin:
             return self.fit(X, **fit_params).transform(X)
         return self.fit(X, y, **fit_params).transform(X)
 
+    def get_feature_names_out(self, input_features=None):
+        """Output feature names: ``<classname><i>`` for projecting
+        transformers (those with ``components_`` / ``_n_features_out``),
+        otherwise one-to-one with the input names."""
+        n_out = getattr(self, "_n_features_out", None)
+        comps = getattr(self, "components_", None)
+        if n_out is None and comps is not None and hasattr(comps, "shape"):
+            n_out = comps.shape[0]
+        if n_out is not None:
+            prefix = type(self).__name__.lower()
+            return np.asarray([f"{prefix}{i}" for i in range(n_out)], dtype=object)
+        if input_features is not None:
+            return np.asarray(input_features, dtype=object)
+        names = getattr(self, "feature_names_in_", None)
+        if names is not None:
+            return np.asarray(names, dtype=object)
+        n = getattr(self, "n_features_in_", None)
+        if n is None:
+            raise AttributeError(f"{type(self).__name__} is not fitted; call fit first.")
+        return np.asarray([f"x{i}" for i in range(n)], dtype=object)
+
 
 class DensityMixin:
     _estimator_type = "DensityEstimator"
 
     def score(self, X, y=None):
         pass
+
+
+class MetaEstimatorMixin:
+    """Marker for estimators wrapping a sub-estimator."""
+    _required_parameters = ["estimator"]
+
+
+class MultiOutputMixin:
+    """Marker: supports multi-output targets."""
+
+    def _more_tags(self):
+        return {"multioutput": True}
+
+
+class BiclusterMixin:
+    """Row/column index helpers for biclustering estimators."""
+
+    @property
+    def biclusters_(self):
+        return self.rows_, self.columns_
+
+    def get_indices(self, i):
+        import numpy as np
+        return np.nonzero(self.rows_[i])[0], np.nonzero(self.columns_[i])[0]
+
+    def get_shape(self, i):
+        r, c = self.get_indices(i)
+        return len(r), len(c)
+
+    def get_submatrix(self, i, data):
+        import numpy as np
+        r, c = self.get_indices(i)
+        return np.asarray(data)[r[:, None], c]
 
 
 class OutlierMixin:

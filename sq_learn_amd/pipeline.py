@@ -204,3 +204,99 @@ def make_pipeline(*steps, memory=None, verbose=False):
 
 
 __all__ = ["Pipeline", "make_pipeline", "clone"]
+
+
+from .utils.metaestimators import _BaseComposition  # noqa: E402
+
+
+class FeatureUnion(_BaseComposition):
+    """Concatenate the outputs of several transformers fitted on the same
+    input (reference ``pipeline.py:FeatureUnion``)."""
+
+    def __init__(self, transformer_list, *, n_jobs=None, transformer_weights=None,
+                 verbose=False):
+        self.transformer_list = transformer_list
+        self.n_jobs = n_jobs
+        self.transformer_weights = transformer_weights
+        self.verbose = verbose
+
+    def get_params(self, deep=True):
+        return self._get_params("transformer_list", deep=deep)
+
+    def set_params(self, **kwargs):
+        self._set_params("transformer_list", **kwargs)
+        return self
+
+    def _iter(self):
+        w = self.transformer_weights or {}
+        for name, t in self.transformer_list:
+            if t == "drop" or t is None:
+                continue
+            yield name, t, w.get(name)
+
+    def _validate(self):
+        names = [n for n, _ in self.transformer_list]
+        if len(set(names)) != len(names):
+            raise ValueError(f"Names provided are not unique: {names}")
+        for _, t in self.transformer_list:
+            if t in ("drop", "passthrough") or t is None:
+                continue
+            if not (hasattr(t, "fit") or hasattr(t, "fit_transform")) or not hasattr(t, "transform"):
+                raise TypeError("All estimators should implement fit and transform. '%s' (type %s) "
+                                "doesn't" % (t, type(t)))
+
+    @staticmethod
+    def _stack(Xs, n):
+        import numpy as np
+        import scipy.sparse as sp
+        if not Xs:
+            return np.zeros((n, 0))
+        if any(sp.issparse(x) for x in Xs):
+            return sp.hstack([sp.csr_matrix(x) for x in Xs]).tocsr()
+        return np.hstack([np.asarray(x) for x in Xs])
+
+    def fit(self, X, y=None, **fit_params):
+        self.fit_transform(X, y, **fit_params)
+        return self
+
+    def fit_transform(self, X, y=None, **fit_params):
+        import numpy as np
+        self._validate()
+        outs, fitted = [], []
+        for name, t, w in self._iter():
+            if t == "passthrough":
+                out, est = np.asarray(X), "passthrough"
+            else:
+                est = clone(t)
+                out = est.fit_transform(X, y, **fit_params) if hasattr(est, "fit_transform") \
+                    else est.fit(X, y, **fit_params).transform(X)
+            outs.append(out * w if w is not None else out)
+            fitted.append((name, est))
+        dropped = [(n, t) for n, t in self.transformer_list if t == "drop" or t is None]
+        self.transformer_list = fitted + dropped if dropped else fitted
+        if hasattr(X, "shape"):
+            self.n_features_in_ = X.shape[1]
+        return self._stack(outs, len(X) if not hasattr(X, "shape") else X.shape[0])
+
+    def transform(self, X):
+        import numpy as np
+        outs = []
+        for name, t, w in self._iter():
+            out = np.asarray(X) if t == "passthrough" else t.transform(X)
+            outs.append(out * w if w is not None else out)
+        return self._stack(outs, len(X) if not hasattr(X, "shape") else X.shape[0])
+
+    def get_feature_names_out(self, input_features=None):
+        import numpy as np
+        out = []
+        for name, t, _ in self._iter():
+            out += [f"{name}__{f}" for f in t.get_feature_names_out(input_features)]
+        return np.asarray(out, dtype=object)
+
+    @property
+    def named_transformers(self):
+        return dict(self.transformer_list)
+
+
+def make_union(*transformers, n_jobs=None, verbose=False):
+    return FeatureUnion(_name_estimators(transformers), n_jobs=n_jobs, verbose=verbose)

@@ -216,6 +216,10 @@ def _instance(cls):
         return Pipeline([("sc", StandardScaler()), ("knn", KNeighborsClassifier(3))])
     elif name in ("GaussianRandomProjection", "SparseRandomProjection", "SelectKBest"):
         kw = {"n_components": 3} if name != "SelectKBest" else {"k": 3}
+    elif name == "ColumnTransformer":
+        return cls([("sc", StandardScaler(), [0, 1, 2])], remainder="passthrough")
+    elif name == "FeatureUnion":
+        return cls([("sc", StandardScaler()), ("sc2", StandardScaler(with_mean=False))])
     elif name in ("GridSearchCV", "HalvingGridSearchCV"):
         return cls(KNeighborsClassifier(), {"n_neighbors": [1, 3]}, cv=3)
     elif name in ("RandomizedSearchCV", "HalvingRandomSearchCV"):
@@ -223,14 +227,18 @@ def _instance(cls):
     params = inspect.signature(cls.__init__).parameters
     for arg in ("estimator", "base_estimator"):
         if arg in params and params[arg].default is inspect.Parameter.empty:
-            from sq_learn_amd.linear_model import LogisticRegression
-            kw[arg] = LogisticRegression()
+            from sq_learn_amd.linear_model import LogisticRegression, Ridge
+            kw[arg] = Ridge() if "Regressor" in name else LogisticRegression()
     return cls(**kw)
 
 
 # estimators that only accept non-negative features
 _NONNEG = ("CategoricalNB", "ComplementNB", "MultinomialNB", "AdditiveChi2Sampler",
            "SkewedChi2Sampler")
+
+
+_MULTI_OUTPUT = ("MultiOutputClassifier", "MultiOutputRegressor", "ClassifierChain",
+                 "RegressorChain")
 
 
 def _X(name):
@@ -253,8 +261,11 @@ def _fit(est):
         return est.fit()
     if name in ("LSSVC", "QLSSVC"):
         return est.fit(X, np.where(y == 0, -1.0, 1.0))
+    if name in _MULTI_OUTPUT:
+        return est.fit(X, np.c_[y, 1 - y])
     if name in ("KNeighborsClassifier", "KNeighborsRegressor", "Pipeline") or \
-            "estimator" in est.get_params(deep=False):
+            "estimator" in est.get_params(deep=False) or \
+            "regressor" in est.get_params(deep=False):
         return est.fit(X, y)
     yp = inspect.signature(est.fit).parameters.get("y")
     if yp is not None and yp.default is inspect.Parameter.empty:
