@@ -43,3 +43,4 @@ def all_estimators(type_filter=None):
     mix = {"classifier": ClassifierMixin, "regressor": RegressorMixin,
            "cluster": ClusterMixin, "transformer": TransformerMixin}
     return [(n, c) for n, c in out if any(issubclass(c, mix[f]) for f in filters)]
+from ._bunch import Bunch  # noqa: E402,F401

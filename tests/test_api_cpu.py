@@ -238,7 +238,7 @@ _NONNEG = ("CategoricalNB", "ComplementNB", "MultinomialNB", "AdditiveChi2Sample
 
 
 _MULTI_OUTPUT = ("MultiOutputClassifier", "MultiOutputRegressor", "ClassifierChain",
-                 "RegressorChain")
+                 "RegressorChain", "CCA", "PLSCanonical", "PLSSVD")
 
 
 def _X(name):
@@ -267,7 +267,8 @@ def _fit(est):
             "estimator" in est.get_params(deep=False) or \
             "regressor" in est.get_params(deep=False):
         return est.fit(X, y)
-    yp = inspect.signature(est.fit).parameters.get("y")
+    sig = inspect.signature(est.fit).parameters
+    yp = sig.get("y", sig.get("Y"))
     if yp is not None and yp.default is inspect.Parameter.empty:
         return est.fit(X, y.astype(float) if getattr(est, "_estimator_type", "") == "regressor"
                        else y)
