@@ -51,7 +51,7 @@ def test_matrix_generators():
     b = M.make_sparse_coded_signal(10, n_components=8, n_features=6, n_nonzero_coefs=3,
                                    random_state=0)
     for x, y in zip(a, b):   # sklearn>=1.3 returns the transposed layout
-        assert np.allclose(x, y) or np.allclose(x, y.T)
+        assert (x.shape == y.shape and np.allclose(x, y)) or np.allclose(x, y.T)
     p = M.make_sparse_spd_matrix(8, alpha=0.5, norm_diag=True, random_state=0)
     assert np.allclose(p, p.T) and np.all(np.linalg.eigvalsh(p) > 0)
 
@@ -60,7 +60,8 @@ def test_matrix_generators():
                                     "load_diabetes", "load_linnerud"])
 def test_toy_loaders(loader):
     a, b = getattr(S, loader)(), getattr(M, loader)()
-    np.testing.assert_allclose(b.data, a.data, atol=1e-6)
+    # sklearn>=1.1 re-derives the scaled diabetes features (~1e-5 drift)
+    np.testing.assert_allclose(b.data, a.data, atol=2e-5)
     np.testing.assert_allclose(b.target, a.target)
     assert list(a.feature_names) == list(b.feature_names)
     fa, fb = getattr(S, loader)(as_frame=True).frame, getattr(M, loader)(as_frame=True).frame
