@@ -44,12 +44,28 @@ class _NeighborsBase(BaseEstimator):
         self._xn = (self._X * self._X).sum(1)
         self.n_features_in_ = self._X.shape[1]
         self.n_samples_fit_ = self._X.shape[0]
-        if self.metric not in ("euclidean", "minkowski", "l2") or (self.metric == "minkowski" and self.p != 2):
-            raise ValueError("only the euclidean metric is implemented on the GPU path")
+        # euclidean + auto/brute -> device GEMM + top-k; anything else (other
+        # metrics, explicit kd_tree / ball_tree) -> host trees / pairwise
+        from ._extra import _HostEngine, _is_euclidean
+        euclid = _is_euclidean(self.metric, getattr(self, "p", 2), self.metric_params)
+        algo = getattr(self, "algorithm", "auto")
+        self._host = None
+        if not euclid or algo in ("kd_tree", "ball_tree"):
+            self._host = _HostEngine(to_numpy(Xt).astype(np.float64), algo, self.metric,
+                                     getattr(self, "p", 2), self.metric_params,
+                                     getattr(self, "leaf_size", 30))
+        self._fit_method = self._host.method if self._host is not None else "brute"
+        self.effective_metric_ = "euclidean" if euclid else self.metric
         return self
 
     def kneighbors(self, X=None, n_neighbors=None, return_distance=True):
         check_is_fitted(self, "_X")
+        if X is not None and np.shape(X)[-1] != self.n_features_in_:
+            raise ValueError(f"X has {np.shape(X)[-1]} features, but {type(self).__name__} is "
+                             f"expecting {self.n_features_in_} features as input.")
+        if getattr(self, "_host", None) is not None:
+            k = self.n_neighbors if n_neighbors is None else n_neighbors
+            return self._host.kneighbors(X, k, return_distance)
         k = self.n_neighbors if n_neighbors is None else n_neighbors
         dev = self._X.device
         query_is_train = X is None

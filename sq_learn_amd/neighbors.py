@@ -1,2 +1,3 @@
 """Reference-layout import path (``sklearn.neighbors``)."""
-from .models.neighbors import KNeighborsClassifier, KNeighborsRegressor, NearestNeighbors  # noqa: F401
+from .models.neighbors import *  # noqa: F401,F403
+from .models.neighbors import __all__  # noqa: F401

@@ -61,6 +61,14 @@ _SIGS = {
     "sqh_mt_new": (_P, [_U]),
     "sqh_sgd_plain": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _U, _P]),
     "sqh_mt_free": (None, [_P]),
+    "sqh_btree_build": (_P, [_P, _LL, _I, _I, _I, _D]),
+    "sqh_btree_free": (None, [_P]),
+    "sqh_btree_info": (None, [_P, _P]),
+    "sqh_btree_copy": (None, [_P, _P, _P, _P, _P, _P, _P]),
+    "sqh_btree_knn": (None, [_P, _P, _LL, _I, _P, _P, _I]),
+    "sqh_btree_radius": (_P, [_P, _P, _LL, _P, _I, _I, _I, _P, _I]),
+    "sqh_radius_copy": (None, [_P, _P, _P]),
+    "sqh_radius_free": (None, [_P]),
     "sqh_hgb_predict": (None, [_P, _LL, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
 }
 
