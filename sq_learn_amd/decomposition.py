@@ -1,3 +1,6 @@
 """Reference-layout import path (``sklearn.decomposition``)."""
 from .models.decomposition import PCA, QPCA, TruncatedSVD, qPCA  # noqa: F401
 from .models.decomposition.incremental import IncrementalPCA  # noqa: F401
+from .models.decomposition._extra import (NMF, FactorAnalysis, FastICA, KernelPCA,  # noqa: F401
+                                           LatentDirichletAllocation, fastica,
+                                           non_negative_factorization)

@@ -234,7 +234,7 @@ def _instance(cls):
 
 # estimators that only accept non-negative features
 _NONNEG = ("CategoricalNB", "ComplementNB", "MultinomialNB", "AdditiveChi2Sampler",
-           "SkewedChi2Sampler")
+           "SkewedChi2Sampler", "NMF", "LatentDirichletAllocation")
 
 
 _MULTI_OUTPUT = ("MultiOutputClassifier", "MultiOutputRegressor", "ClassifierChain",

@@ -1,0 +1,73 @@
+"""Device (MI355X) paths of the estimators whose heavy algebra runs in
+torch on the resolved device: Gaussian mixture EM, label spreading,
+kernel density, NCA, Bayesian ridge, PLSSVD.  Compared with scikit-learn
+(fp64 on the GPU, so tolerances stay tight)."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+pytest.importorskip("sklearn")
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        yield
+
+
+def test_device_resolution():
+    from sq_learn_amd.runtime.device import resolve_device
+    assert resolve_device(None).type == "cuda"
+
+
+def test_gmm_labelspreading_kde_on_device():
+    import sklearn.mixture as SM
+    import sklearn.neighbors as SN
+    import sklearn.semi_supervised as SS
+    from sklearn.datasets import make_blobs
+
+    import sq_learn_amd.mixture as MM
+    import sq_learn_amd.neighbors as MN
+    import sq_learn_amd.semi_supervised as MS
+    X, y = make_blobs(600, 4, centers=4, random_state=0)
+    for cov in ["full", "diag"]:
+        a = SM.GaussianMixture(4, covariance_type=cov, random_state=0, init_params="random").fit(X)
+        b = MM.GaussianMixture(4, covariance_type=cov, random_state=0, init_params="random").fit(X)
+        np.testing.assert_allclose(b.means_, a.means_, atol=1e-6)
+    ys = y.copy()
+    ys[np.random.RandomState(0).rand(len(y)) < 0.8] = -1
+    Xs = X / X.std(0) / 3
+    a = SS.LabelSpreading(gamma=1).fit(Xs, ys)
+    b = MS.LabelSpreading(gamma=1).fit(Xs, ys)
+    np.testing.assert_allclose(b.label_distributions_, a.label_distributions_, atol=1e-10)
+    a = SN.KernelDensity(bandwidth=0.7).fit(X).score_samples(X[:50])
+    b = MN.KernelDensity(bandwidth=0.7).fit(X).score_samples(X[:50])
+    np.testing.assert_allclose(b, a, atol=1e-9)
+
+
+def test_nca_bayes_pls_on_device():
+    import sklearn.cross_decomposition as SCD
+    import sklearn.linear_model as SL
+    import sklearn.neighbors as SN
+    from sklearn.datasets import make_classification
+
+    import sq_learn_amd.cross_decomposition as MCD
+    import sq_learn_amd.linear_model as ML
+    import sq_learn_amd.neighbors as MN
+    X, y = make_classification(200, 6, n_informative=4, n_classes=3, random_state=0)
+    a = SN.NeighborhoodComponentsAnalysis(n_components=2, init="identity").fit(X, y)
+    b = MN.NeighborhoodComponentsAnalysis(n_components=2, init="identity").fit(X, y)
+    # L-BFGS stops at a slightly different point under device fp order
+    assert np.abs(a.components_ - b.components_).max() / np.abs(a.components_).max() < 1e-2
+    yr = X[:, 0] * 2 - X[:, 1]
+    np.testing.assert_allclose(ML.BayesianRidge().fit(X, yr).coef_,
+                               SL.BayesianRidge().fit(X, yr).coef_, atol=1e-9)
+    Y = np.c_[yr, X[:, 2]]
+    np.testing.assert_allclose(np.abs(MCD.PLSSVD(2).fit(X, Y).transform(X)),
+                               np.abs(SCD.PLSSVD(2).fit(X, Y).transform(X)), atol=1e-9)
