@@ -6,6 +6,8 @@ from ._coordinate_descent import (ElasticNet, ElasticNetCV, Lasso, LassoCV, enet
 from ._logistic import LogisticRegression
 from ._stochastic_gradient import (PassiveAggressiveClassifier, PassiveAggressiveRegressor,
                                    Perceptron, SGDClassifier, SGDOneClassSVM, SGDRegressor)
+from ._lm_extra import *  # noqa: F401,F403
+from ._lm_extra import __all__ as _extra_all
 from ._ridge import Ridge, RidgeClassifier, RidgeClassifierCV, RidgeCV, ridge_regression
 
 __all__ = ["LinearRegression", "ElasticNet", "ElasticNetCV", "Lasso", "LassoCV", "enet_path",
@@ -13,3 +15,4 @@ __all__ = ["LinearRegression", "ElasticNet", "ElasticNetCV", "Lasso", "LassoCV",
            "ridge_regression", "LogisticRegression", "ARDRegression", "BayesianRidge", "SGDClassifier", "SGDRegressor",
            "SGDOneClassSVM", "Perceptron", "PassiveAggressiveClassifier",
            "PassiveAggressiveRegressor"]
+__all__ = __all__ + list(_extra_all)

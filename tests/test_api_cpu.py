@@ -238,7 +238,8 @@ _NONNEG = ("CategoricalNB", "ComplementNB", "MultinomialNB", "AdditiveChi2Sample
 
 
 _MULTI_OUTPUT = ("MultiOutputClassifier", "MultiOutputRegressor", "ClassifierChain",
-                 "RegressorChain", "CCA", "PLSCanonical", "PLSSVD")
+                 "RegressorChain", "CCA", "PLSCanonical", "PLSSVD", "MultiTaskElasticNet",
+                 "MultiTaskLasso", "MultiTaskElasticNetCV", "MultiTaskLassoCV")
 
 
 def _X(name):
@@ -263,6 +264,8 @@ def _fit(est):
         return est.fit(X, np.where(y == 0, -1.0, 1.0))
     if name in _MULTI_OUTPUT:
         return est.fit(X, np.c_[y, 1 - y])
+    if name in ("GammaRegressor", "PoissonRegressor", "TweedieRegressor"):
+        return est.fit(X, y + 1.0)
     if name in ("KNeighborsClassifier", "KNeighborsRegressor", "Pipeline") or \
             "estimator" in est.get_params(deep=False) or \
             "regressor" in est.get_params(deep=False):
