@@ -9,3 +9,10 @@ __all__ = ["RandomForestClassifier", "RandomForestRegressor", "ExtraTreesClassif
            "ExtraTreesRegressor", "RandomTreesEmbedding", "GradientBoostingClassifier",
            "GradientBoostingRegressor", "HistGradientBoostingClassifier",
            "HistGradientBoostingRegressor"]
+from ._meta import (AdaBoostClassifier, AdaBoostRegressor, BaggingClassifier,  # noqa: E402
+                    BaggingRegressor, IsolationForest, StackingClassifier, StackingRegressor,
+                    VotingClassifier, VotingRegressor)
+
+__all__ += ["BaggingClassifier", "BaggingRegressor", "IsolationForest", "AdaBoostClassifier",
+            "AdaBoostRegressor", "VotingClassifier", "VotingRegressor", "StackingClassifier",
+            "StackingRegressor"]

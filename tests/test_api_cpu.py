@@ -220,6 +220,12 @@ def _instance(cls):
         return cls([("sc", StandardScaler(), [0, 1, 2])], remainder="passthrough")
     elif name == "FeatureUnion":
         return cls([("sc", StandardScaler()), ("sc2", StandardScaler(with_mean=False))])
+    elif name in ("VotingClassifier", "StackingClassifier"):
+        from sq_learn_amd.naive_bayes import GaussianNB
+        return cls([("a", GaussianNB()), ("b", KNeighborsClassifier(3))])
+    elif name in ("VotingRegressor", "StackingRegressor"):
+        from sq_learn_amd.linear_model import Ridge
+        return cls([("a", Ridge()), ("b", Ridge(alpha=10.0))])
     elif name in ("GridSearchCV", "HalvingGridSearchCV"):
         return cls(KNeighborsClassifier(), {"n_neighbors": [1, 3]}, cv=3)
     elif name in ("RandomizedSearchCV", "HalvingRandomSearchCV"):
