@@ -4,3 +4,8 @@ from .models.cluster.minibatch import MiniBatchKMeans  # noqa: F401
 from .models.cluster.dbscan import DBSCAN, dbscan  # noqa: F401
 from .models.cluster.hierarchical import (AgglomerativeClustering, FeatureAgglomeration,  # noqa: F401
                                           linkage_tree, ward_tree)
+from .models.cluster._extra import (OPTICS, AffinityPropagation, Birch, MeanShift,  # noqa: F401
+                                     SpectralClustering, affinity_propagation,
+                                     cluster_optics_dbscan, cluster_optics_xi,
+                                     compute_optics_graph, estimate_bandwidth, get_bin_seeds,
+                                     mean_shift, spectral_clustering)

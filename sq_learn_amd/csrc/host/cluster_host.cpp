@@ -80,3 +80,61 @@ double sqh_expected_mutual_info(const int64_t* a, long long R, const int64_t* b,
 }
 
 }  // extern "C"
+
+// OPTICS ordering (reference cluster/_optics.py:compute_optics_graph and
+// _set_reach_dist): repeatedly take the unprocessed point of smallest
+// reachability (first index on ties) and relax the reachability of the
+// unprocessed points within max_eps of it.  Distances are minkowski-p on
+// the fly (p = inf for chebyshev); reachabilities are rounded to 15
+// decimals exactly like np.around, so the ordering matches the reference.
+extern "C" void sqh_optics_order(const double* X, int64_t n, int64_t d, const double* core,
+                                 double max_eps, double p, double* reach, int64_t* pred,
+                                 int64_t* ordering) {
+  std::vector<uint8_t> done(n, 0);
+  for (int64_t i = 0; i < n; ++i) { reach[i] = INFINITY; pred[i] = -1; }
+  auto rnd = [](double v) {
+    if (!std::isfinite(v)) return v;
+    double y = v * 1e15;
+    if (std::fabs(y) >= 4503599627370496.0) return v;
+    return std::nearbyint(y) / 1e15;
+  };
+  for (int64_t step = 0; step < n; ++step) {
+    int64_t pt = -1;
+    double best = INFINITY;
+    for (int64_t j = 0; j < n; ++j) {
+      if (done[j]) continue;
+      if (pt < 0 || reach[j] < best) { pt = j; best = reach[j]; }
+    }
+    done[pt] = 1;
+    ordering[step] = pt;
+    if (!std::isfinite(core[pt])) continue;
+    const double* xp = X + pt * d;
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < n; ++j) {
+      if (done[j]) continue;
+      const double* xj = X + j * d;
+      double s = 0.0;
+      if (std::isinf(p)) {
+        for (int64_t k = 0; k < d; ++k) s = std::max(s, std::fabs(xp[k] - xj[k]));
+      } else if (p == 2.0) {
+        // the reference's euclidean_distances expansion: -2 x.y + |x|^2 + |y|^2
+        double dot = 0.0, xx = 0.0, yy = 0.0;
+        for (int64_t k = 0; k < d; ++k) {
+          dot += xp[k] * xj[k];
+          xx += xp[k] * xp[k];
+          yy += xj[k] * xj[k];
+        }
+        s = -2.0 * dot + xx + yy;
+        s = std::sqrt(std::max(s, 0.0));
+      } else if (p == 1.0) {
+        for (int64_t k = 0; k < d; ++k) s += std::fabs(xp[k] - xj[k]);
+      } else {
+        for (int64_t k = 0; k < d; ++k) s += std::pow(std::fabs(xp[k] - xj[k]), p);
+        s = std::pow(s, 1.0 / p);
+      }
+      if (s > max_eps) continue;
+      double rd = rnd(std::max(s, core[pt]));
+      if (rd < reach[j]) { reach[j] = rd; pred[j] = pt; }
+    }
+  }
+}

