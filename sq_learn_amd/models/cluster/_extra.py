@@ -515,7 +515,11 @@ class Birch(ClusterMixin, TransformerMixin, BaseEstimator):
 
     def transform(self, X):
         check_is_fitted(self, "subcluster_centers_")
-        return np.sqrt(_sq_dists(_dense(X), self.subcluster_centers_))
+        X = _dense(X)
+        if X.shape[1] != self.n_features_in_:
+            raise ValueError("X has %d features, but Birch is expecting %d features as input."
+                             % (X.shape[1], self.n_features_in_))
+        return np.sqrt(_sq_dists(X, self.subcluster_centers_))
 
 
 # ------------------------------------------------------------------- OPTICS
