@@ -71,6 +71,8 @@ class KernelPCA(TransformerMixin, BaseEstimator):
 
     def _get_kernel(self, X, Y=None):
         from ...metrics import pairwise_kernels
+        if self.kernel == "precomputed":
+            return np.asarray(X, dtype=np.float64)
         if callable(self.kernel):
             params = self.kernel_params or {}
         else:

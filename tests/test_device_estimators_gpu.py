@@ -73,3 +73,15 @@ def test_nca_bayes_pls_on_device():
     Y = np.c_[yr, X[:, 2]]
     np.testing.assert_allclose(np.abs(MCD.PLSSVD(2).fit(X, Y).transform(X)),
                                np.abs(SCD.PLSSVD(2).fit(X, Y).transform(X)), atol=1e-9)
+
+
+def test_tsne_mds_on_device():
+    import sklearn.manifold as SMf
+    from sklearn.datasets import load_digits
+
+    import sq_learn_amd.manifold as MMf
+    Xd = load_digits(return_X_y=True)[0][:800]
+    a = SMf.TSNE(method="exact", init="random", learning_rate=200.0, random_state=0).fit(Xd)
+    b = MMf.TSNE(method="exact", init="random", learning_rate=200.0, random_state=0).fit(Xd)
+    assert abs(a.kl_divergence_ - b.kl_divergence_) < 0.1 * a.kl_divergence_
+    assert MMf.trustworthiness(Xd, b.embedding_) > 0.98
