@@ -1,0 +1,5 @@
+"""Reference-layout import path (``sklearn.gaussian_process``)."""
+from ..models.gaussian_process import GaussianProcessClassifier, GaussianProcessRegressor  # noqa
+from ..models.gaussian_process import kernels  # noqa: F401
+
+__all__ = ["GaussianProcessRegressor", "GaussianProcessClassifier", "kernels"]

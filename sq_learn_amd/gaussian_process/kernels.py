@@ -1,0 +1,2 @@
+"""Reference-layout import path (``sklearn.gaussian_process.kernels``)."""
+from ..models.gaussian_process.kernels import *  # noqa: F401,F403
