@@ -85,3 +85,19 @@ def test_tsne_mds_on_device():
     b = MMf.TSNE(method="exact", init="random", learning_rate=200.0, random_state=0).fit(Xd)
     assert abs(a.kl_divergence_ - b.kl_divergence_) < 0.1 * a.kl_divergence_
     assert MMf.trustworthiness(Xd, b.embedding_) > 0.98
+
+
+def test_mlp_trains_on_device():
+    import sklearn.neural_network as SNN
+    from sklearn.datasets import load_digits
+
+    import sq_learn_amd.neural_network as MNN
+    X, y = load_digits(return_X_y=True)
+    X = X[:600] / 16
+    y = y[:600]
+    kw = dict(hidden_layer_sizes=(64, 32), max_iter=20, random_state=0)
+    b = MNN.MLPClassifier(**kw).fit(X, y)
+    assert b._W[0].device.type == "cuda"
+    a = SNN.MLPClassifier(**kw).fit(X, y)
+    # same RNG stream, device GEMM reduction order: tiny drift only
+    np.testing.assert_allclose(a.predict_proba(X), b.predict_proba(X), atol=1e-6)
