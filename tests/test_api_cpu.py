@@ -240,7 +240,8 @@ def _instance(cls):
 
 # estimators that only accept non-negative features
 _NONNEG = ("CategoricalNB", "ComplementNB", "MultinomialNB", "AdditiveChi2Sampler",
-           "SkewedChi2Sampler", "NMF", "LatentDirichletAllocation")
+           "SkewedChi2Sampler", "NMF", "LatentDirichletAllocation", "TfidfTransformer",
+           "BernoulliRBM")
 
 
 _MULTI_OUTPUT = ("MultiOutputClassifier", "MultiOutputRegressor", "ClassifierChain",
@@ -254,6 +255,12 @@ def _X(name):
 
 
 _LABEL_TRANSFORMERS = ("LabelEncoder", "LabelBinarizer", "MultiLabelBinarizer")
+_DOCS = ["the quick brown fox", "a lazy dog sleeps", "the fox and the dog", "quick quick fox"]
+_SPECIAL_INPUT = {
+    "CountVectorizer": _DOCS, "TfidfVectorizer": _DOCS, "HashingVectorizer": _DOCS,
+    "DictVectorizer": [{"a": 1.0, "b": "x"}, {"a": 2.0, "c": 3.0}],
+    "PatchExtractor": np.arange(2 * 20 * 20, dtype=float).reshape(2, 20, 20),
+}
 
 
 def _fit(est):
@@ -266,6 +273,8 @@ def _fit(est):
         return est.fit(X[:, 0], X[:, 1])
     if name == "FeatureHasher":
         return est.fit()
+    if name in _SPECIAL_INPUT:
+        return est.fit(_SPECIAL_INPUT[name])
     if name in ("LSSVC", "QLSSVC"):
         return est.fit(X, np.where(y == 0, -1.0, 1.0))
     if name in _MULTI_OUTPUT:
@@ -310,6 +319,8 @@ def test_estimator_contract(name, cls):
         X = X[:, 0]
     elif name == "FeatureHasher":
         X = [{"a": 1.0, "b": 2.0}, {"c": 3.0}]
+    elif name in _SPECIAL_INPUT:
+        X = _SPECIAL_INPUT[name]
     for meth in ("predict", "transform"):
         if hasattr(est, meth) and name not in ("Pipeline",) or (name == "Pipeline" and meth == "predict"):
             try:
