@@ -4,3 +4,8 @@ from .models.decomposition.incremental import IncrementalPCA  # noqa: F401
 from .models.decomposition._extra import (NMF, FactorAnalysis, FastICA, KernelPCA,  # noqa: F401
                                            LatentDirichletAllocation, fastica,
                                            non_negative_factorization)
+from .models.decomposition._dict_learning import (DictionaryLearning,  # noqa: F401
+                                                  MiniBatchDictionaryLearning,
+                                                  MiniBatchSparsePCA, SparseCoder, SparsePCA,
+                                                  dict_learning, dict_learning_online,
+                                                  sparse_encode)

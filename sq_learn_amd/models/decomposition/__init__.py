@@ -4,3 +4,6 @@ from .pca import PCA, TruncatedSVD
 from ._base import _BasePCA
 
 __all__ = ["QPCA", "qPCA", "PCA", "TruncatedSVD"]
+from ._dict_learning import (DictionaryLearning, MiniBatchDictionaryLearning,  # noqa: E402,F401
+                             MiniBatchSparsePCA, SparseCoder, SparsePCA, dict_learning,
+                             dict_learning_online, sparse_encode)

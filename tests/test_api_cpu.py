@@ -216,6 +216,13 @@ def _instance(cls):
         return Pipeline([("sc", StandardScaler()), ("knn", KNeighborsClassifier(3))])
     elif name in ("GaussianRandomProjection", "SparseRandomProjection", "SelectKBest"):
         kw = {"n_components": 3} if name != "SelectKBest" else {"k": 3}
+    elif name == "SparseCoder":
+        return cls(np.eye(6)[:4], transform_algorithm="threshold", transform_alpha=0.1)
+    elif name in ("DictionaryLearning", "MiniBatchDictionaryLearning", "SparsePCA",
+                  "MiniBatchSparsePCA"):
+        kw = {"n_components": 3, "random_state": 0}
+        kw.update({"max_iter": 5} if name in ("DictionaryLearning", "SparsePCA")
+                  else {"n_iter": 5})
     elif name == "ColumnTransformer":
         return cls([("sc", StandardScaler(), [0, 1, 2])], remainder="passthrough")
     elif name == "FeatureUnion":
