@@ -9,3 +9,4 @@ from .models.cluster._extra import (OPTICS, AffinityPropagation, Birch, MeanShif
                                      cluster_optics_dbscan, cluster_optics_xi,
                                      compute_optics_graph, estimate_bandwidth, get_bin_seeds,
                                      mean_shift, spectral_clustering)
+from .models.cluster._bicluster import SpectralBiclustering, SpectralCoclustering  # noqa: F401,E402

@@ -35,3 +35,4 @@ from .utils.metrics_extra import (SCORERS, auc, average_precision_score,  # noqa
 from .utils.metrics_extra import get_scorer_ext as get_scorer  # noqa: F401,E402
 from .utils.metrics_extra import mean_squared_error_ext as mean_squared_error  # noqa: F401,E402,F811
 from .utils.metrics_extra import r2_score_ext as r2_score  # noqa: F401,E402,F811
+from .models.cluster._bicluster import consensus_score  # noqa: F401,E402

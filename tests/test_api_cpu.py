@@ -216,6 +216,8 @@ def _instance(cls):
         return Pipeline([("sc", StandardScaler()), ("knn", KNeighborsClassifier(3))])
     elif name in ("GaussianRandomProjection", "SparseRandomProjection", "SelectKBest"):
         kw = {"n_components": 3} if name != "SelectKBest" else {"k": 3}
+    elif name in ("SpectralBiclustering", "SpectralCoclustering"):
+        kw = {"n_clusters": 2, "random_state": 0, "n_init": 2}
     elif name == "SparseCoder":
         return cls(np.eye(6)[:4], transform_algorithm="threshold", transform_alpha=0.1)
     elif name in ("DictionaryLearning", "MiniBatchDictionaryLearning", "SparsePCA",
