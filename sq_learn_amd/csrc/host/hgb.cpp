@@ -36,7 +36,28 @@ struct SplitInfo {
   double gl = 0, hl = 0, gr = 0, hr = 0;
   uint32_t nl = 0, nr = 0;
   double vl = 0, vr = 0;
+  bool is_cat = false;
+  uint32_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // categorical: bins that go left
 };
+
+struct CatInfo { unsigned bin; double value; };
+
+// Merge sort with the reference's comparator (a < b ? -1 : 1) and glibc
+// msort's merge rule (take left iff cmp <= 0), so ties order identically.
+void cat_msort(CatInfo* a, CatInfo* tmp, size_t n) {
+  if (n <= 1) return;
+  size_t n1 = n / 2, n2 = n - n1;
+  CatInfo *b1 = a, *b2 = a + n1;
+  cat_msort(b1, tmp, n1);
+  cat_msort(b2, tmp, n2);
+  size_t k = 0;
+  while (n1 > 0 && n2 > 0) {
+    if (b1->value < b2->value) { tmp[k++] = *b1++; --n1; }
+    else { tmp[k++] = *b2++; --n2; }
+  }
+  while (n1 > 0) { tmp[k++] = *b1++; --n1; }
+  for (size_t i = 0; i < k; ++i) a[i] = tmp[i];
+}
 
 struct Node {
   int depth;
@@ -55,6 +76,7 @@ struct Params {
   int64_t n; int d; int n_bins;
   const uint8_t* Xb; const float* grad; const float* hess; bool hess_const;
   const uint32_t* nbnm; const uint8_t* has_missing; const int8_t* mono;
+  const uint8_t* is_cat;
   int max_leaf_nodes, max_depth, min_samples_leaf;
   double min_gain, l2, min_hess, shrinkage;
 };
@@ -175,6 +197,7 @@ struct Grower {
     const bool miss = P.has_missing[f] != 0;
     si.feature = f;
     si.gain = -1.0;
+    if (P.is_cat && P.is_cat[f]) { scan_categorical(nd, f, si); return; }
     // left to right: missing values (last bin) go right
     {
       const unsigned end = P.nbnm[f] - 1 + (miss ? 1 : 0);
@@ -242,6 +265,73 @@ struct Grower {
     }
   }
 
+  // Fisher grouping: categories with enough support sorted by
+  // g / (h + MIN_CAT_SUPPORT), scanned from both ends up to the middle
+  // (reference splitting.pyx _find_best_bin_to_split_category).
+  void scan_categorical(const Node& nd, int f, SplitInfo& si) const {
+    const Bin* h = nd.hist.data() + (size_t)f * P.n_bins;
+    const uint32_t ns = nd.n();
+    const double sg = nd.sum_g, sh = nd.sum_h, lo = nd.lower, hi = nd.upper;
+    const bool miss = P.has_missing[f] != 0;
+    const unsigned nbm = P.nbnm[f], mbin = (unsigned)P.n_bins - 1;
+    const double MIN_CAT_SUPPORT = 10.0, support = (double)ns / sh;
+    std::vector<CatInfo> ci, tmp;
+    ci.reserve(nbm + 1);
+    auto consider = [&](unsigned b) {
+      double hb = P.hess_const ? (double)h[b].c : h[b].h;
+      if (hb * support >= MIN_CAT_SUPPORT) ci.push_back({b, h[b].g / (hb + MIN_CAT_SUPPORT)});
+    };
+    for (unsigned b = 0; b < nbm; ++b) consider(b);
+    if (miss) consider(mbin);
+    const size_t nu = ci.size();
+    if (nu <= 1) return;
+    tmp.resize(nu);
+    cat_msort(ci.data(), tmp.data(), nu);
+    const double loss_cur = sg * nd.value;
+    bool found = false;
+    double best = -1.0, bgl = 0, bhl = 0;
+    uint32_t bnl = 0;
+    size_t bthr = 0;
+    int bdir = 0;
+    for (int dir : {1, -1}) {
+      const size_t middle = dir == 1 ? (nu + 1) / 2 : (nu + 1) / 2 - 1;
+      double gl = 0, hl = 0;
+      uint32_t nl = 0;
+      for (size_t i = 0; i < middle; ++i) {
+        const size_t sidx = dir == 1 ? i : nu - 1 - i;
+        const unsigned b = ci[sidx].bin;
+        nl += h[b].c;
+        const uint32_t nr = ns - nl;
+        hl += P.hess_const ? (double)h[b].c : h[b].h;
+        const double hr = sh - hl;
+        gl += h[b].g;
+        const double gr = sg - gl;
+        if (nl < (uint32_t)P.min_samples_leaf || hl < P.min_hess) continue;
+        if (nr < (uint32_t)P.min_samples_leaf || hr < P.min_hess) break;
+        double gain = split_gain(gl, hl, gr, hr, loss_cur, 0, lo, hi, P.l2);
+        if (gain > best && gain > P.min_gain) {
+          found = true; best = gain; bthr = sidx; bgl = gl; bhl = hl; bnl = nl; bdir = dir;
+        }
+      }
+    }
+    if (!found) return;
+    si.gain = best; si.bin = 0; si.is_cat = true;
+    si.gl = bgl; si.hl = bhl; si.gr = sg - bgl; si.hr = sh - bhl;
+    si.nl = bnl; si.nr = ns - bnl;
+    si.vl = node_value(si.gl, si.hl, lo, hi, P.l2);
+    si.vr = node_value(si.gr, si.hr, lo, hi, P.l2);
+    for (int w = 0; w < 8; ++w) si.bits[w] = 0;
+    if (bdir == 1) {
+      for (size_t k = 0; k <= bthr; ++k) si.bits[ci[k].bin >> 5] |= 1u << (ci[k].bin & 31);
+    } else {
+      for (size_t k = nu - 1; k + 1 > bthr; --k) {
+        si.bits[ci[k].bin >> 5] |= 1u << (ci[k].bin & 31);
+        if (k == 0) break;
+      }
+    }
+    si.missing_left = miss ? ((si.bits[mbin >> 5] >> (mbin & 31)) & 1u) != 0 : false;
+  }
+
   void find_split(Node& nd) {
     std::vector<SplitInfo> infos(P.d);
 #ifdef _OPENMP
@@ -264,6 +354,7 @@ struct Grower {
   }
 
   bool goes_left(const SplitInfo& s, uint8_t b) const {
+    if (s.is_cat) return ((s.bits[b >> 5] >> (b & 31)) & 1u) != 0;
     if (b == (uint8_t)(P.n_bins - 1)) return s.missing_left;
     return b <= (uint8_t)s.bin;
   }
@@ -366,7 +457,8 @@ struct Result {
   // predictor nodes in depth-first preorder (reference _fill_predictor_arrays)
   std::vector<double> value, gain;
   std::vector<int32_t> count, feature, bin, left, right, depth;
-  std::vector<uint8_t> missing_left, is_leaf;
+  std::vector<uint8_t> missing_left, is_leaf, is_cat;
+  std::vector<uint32_t> bits;            // 8 words per node (binned left bitset)
   std::vector<int32_t> leaf_of_sample;   // predictor node id of every training row
 };
 
@@ -407,10 +499,10 @@ void sqh_hgb_map_bins(const double* X, long long n, int d, const double* thr,
 //       min_gain_to_split, l2, min_hessian_to_split, shrinkage, n_bins]
 void* sqh_hgb_grow(const uint8_t* Xb, long long n, int d, const float* grad, const float* hess,
                    int hess_const, const uint32_t* nbnm, const uint8_t* has_missing,
-                   const int8_t* mono, const double* prm) {
+                   const int8_t* mono, const double* prm, const uint8_t* is_cat) {
   Grower G;
   G.P = Params{n, d, (int)prm[7], Xb, grad, hess, hess_const != 0, nbnm, has_missing, mono,
-               (int)prm[0], (int)prm[1], (int)prm[2], prm[3], prm[4], prm[5], prm[6]};
+               is_cat, (int)prm[0], (int)prm[1], (int)prm[2], prm[3], prm[4], prm[5], prm[6]};
   G.grow();
   auto* R = new Result();
   R->leaf_of_sample.assign(n, -1);
@@ -430,6 +522,7 @@ void* sqh_hgb_grow(const uint8_t* Xb, long long n, int d, const float* grad, con
   R->value.resize(m); R->gain.resize(m); R->count.resize(m); R->feature.resize(m);
   R->bin.resize(m); R->left.resize(m); R->right.resize(m); R->depth.resize(m);
   R->missing_left.resize(m); R->is_leaf.resize(m);
+  R->is_cat.assign(m, 0); R->bits.assign(8 * m, 0u);
   for (size_t k = 0; k < m; ++k) {
     const Node& nd = G.nodes[order[k]];
     R->value[k] = nd.value;
@@ -444,6 +537,10 @@ void* sqh_hgb_grow(const uint8_t* Xb, long long n, int d, const float* grad, con
       R->gain[k] = nd.split.gain; R->feature[k] = nd.split.feature; R->bin[k] = nd.split.bin;
       R->missing_left[k] = nd.split.missing_left ? 1 : 0;
       R->left[k] = newid[nd.left]; R->right[k] = newid[nd.right];
+      if (nd.split.is_cat) {
+        R->is_cat[k] = 1;
+        for (int w = 0; w < 8; ++w) R->bits[8 * k + w] = nd.split.bits[w];
+      }
     }
   }
   return R;
@@ -469,7 +566,57 @@ void sqh_hgb_copy(void* h, double* value, double* gain, int* count, int* feature
   if (leaf_of_sample) std::memcpy(leaf_of_sample, R->leaf_of_sample.data(), (size_t)n * 4);
 }
 
+void sqh_hgb_copy_cat(void* h, uint8_t* is_cat, uint32_t* bits) {
+  auto* R = (Result*)h;
+  std::memcpy(is_cat, R->is_cat.data(), R->is_cat.size());
+  std::memcpy(bits, R->bits.data(), R->bits.size() * 4);
+}
+
 void sqh_hgb_free(void* h) { delete (Result*)h; }
+
+// As sqh_hgb_predict, with categorical nodes: raw category c goes left if
+// it is in the node's raw bitset, right if it is a known category, and
+// follows the missing direction otherwise (reference _predictor.pyx).
+void sqh_hgb_predict_cat(const double* X, long long n, int d, const int* feature,
+                         const double* thr, const uint8_t* missing_left, const int* left,
+                         const int* right, const uint8_t* is_leaf, const double* value,
+                         const uint8_t* is_cat, const uint32_t* raw_bits,
+                         const uint32_t* known_bits, const long long* offs, int T, double* out) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (long long i = 0; i < n; ++i) {
+    const double* xi = X + i * d;
+    double acc = 0.0;
+    for (int t = 0; t < T; ++t) {
+      const long long b = offs[t];
+      long long k = 0;
+      while (!is_leaf[b + k]) {
+        const long long q = b + k;
+        const int f = feature[q];
+        const double v = xi[f];
+        bool gl;
+        if (std::isnan(v)) {
+          gl = missing_left[q] != 0;
+        } else if (is_cat[q]) {
+          if (v >= 0 && v < 256) {
+            const unsigned c = (unsigned)v;
+            if ((raw_bits[8 * q + (c >> 5)] >> (c & 31)) & 1u) gl = true;
+            else if ((known_bits[8 * f + (c >> 5)] >> (c & 31)) & 1u) gl = false;
+            else gl = missing_left[q] != 0;
+          } else {
+            gl = missing_left[q] != 0;
+          }
+        } else {
+          gl = v <= thr[q];
+        }
+        k = gl ? left[q] : right[q];
+      }
+      acc += value[b + k];
+    }
+    out[i] = acc;
+  }
+}
 
 // Raw predictions of T stacked predictors on float64 rows (NaN-aware):
 // out[i] = sum_t value_t[leaf].  Node arrays concatenated, offsets per tree.

@@ -45,9 +45,12 @@ def _find_binning_thresholds(col, max_bins):
 class _BinMapper:
     """Quantile bin mapper; the last bin (n_bins - 1) holds missing values."""
 
-    def __init__(self, n_bins=256, subsample=int(2e5), random_state=None):
+    def __init__(self, n_bins=256, subsample=int(2e5), is_categorical=None,
+                 known_categories=None, random_state=None):
         self.n_bins = n_bins
         self.subsample = subsample
+        self.is_categorical = is_categorical
+        self.known_categories = known_categories
         self.random_state = random_state
 
     def fit(self, X):
@@ -68,6 +71,15 @@ class _BinMapper:
                                                range(X.shape[1])))
         self.n_bins_non_missing_ = np.array([t.shape[0] + 1 for t in self.bin_thresholds_],
                                             dtype=np.uint32)
+        if self.is_categorical is not None:
+            # categorical: the "thresholds" are the sorted categories, so a
+            # known category maps to its rank
+            for f in np.flatnonzero(self.is_categorical):
+                cats = np.asarray(self.known_categories[f], dtype=X_DTYPE)
+                self.bin_thresholds_[f] = cats
+                self.n_bins_non_missing_[f] = cats.shape[0]
+        self.is_categorical_ = (np.zeros(X.shape[1], dtype=np.uint8) if self.is_categorical
+                                is None else np.asarray(self.is_categorical, dtype=np.uint8))
         return self
 
     def transform(self, X):
@@ -276,7 +288,7 @@ class TreePredictor:
         return int(self.nodes["depth"].max())
 
 
-def _grow_tree(Xb, g, h, hess_const, nbnm, has_missing, mono, params, shrinkage):
+def _grow_tree(Xb, g, h, hess_const, nbnm, has_missing, mono, params, shrinkage, is_cat):
     lib = _host.lib()
     n, d = Xb.shape
     prm = np.array([params["max_leaf_nodes"], params["max_depth"], params["min_samples_leaf"],
@@ -286,12 +298,16 @@ def _grow_tree(Xb, g, h, hess_const, nbnm, has_missing, mono, params, shrinkage)
     h = np.ascontiguousarray(h, dtype=np.float32).reshape(-1)
     handle = lib.sqh_hgb_grow(Xb.T.ctypes.data, n, d, g.ctypes.data, h.ctypes.data,
                               int(hess_const), nbnm.ctypes.data, has_missing.ctypes.data,
-                              mono.ctypes.data, prm.ctypes.data)
+                              mono.ctypes.data, prm.ctypes.data, is_cat.ctypes.data)
     m = lib.sqh_hgb_size(handle)
     nodes = {name: np.empty(m, dtype=dt) for name, dt in _NODE_FIELDS}
     leaf_of_sample = np.empty(n, dtype=np.int32)
     lib.sqh_hgb_copy(handle, *(nodes[f].ctypes.data for f, _ in _NODE_FIELDS),
                      leaf_of_sample.ctypes.data, n)
+    nodes["is_categorical"] = np.empty(m, dtype=np.uint8)
+    nodes["left_cat_bitset"] = np.empty((m, 8), dtype=np.uint32)
+    lib.sqh_hgb_copy_cat(handle, nodes["is_categorical"].ctypes.data,
+                         nodes["left_cat_bitset"].ctypes.data)
     lib.sqh_hgb_free(handle)
     return nodes, leaf_of_sample
 
@@ -332,11 +348,48 @@ class BaseHistGradientBoosting(BaseEstimator):
         if self.monotonic_cst is not None and self.n_trees_per_iteration_ != 1:
             raise ValueError("monotonic constraints are not supported for multiclass "
                              "classification.")
-        if getattr(self, "categorical_features", None) is not None:
-            cf = np.asarray(self.categorical_features)
-            if cf.size and (cf.dtype.kind == "i" or np.any(cf)):
-                raise NotImplementedError("categorical_features are not supported yet; "
-                                          "one-hot or ordinal-encode them")
+
+    def _check_categories(self, X):
+        """(is_categorical, known_categories) of X (reference
+        ``gradient_boosting.py`` ``_check_categories``)."""
+        cf = getattr(self, "categorical_features", None)
+        if cf is None:
+            return None, None
+        cf = np.asarray(cf)
+        if cf.size == 0:
+            return None, None
+        if cf.dtype.kind not in ("i", "b"):
+            raise ValueError("categorical_features must be an array-like of bools or array-like "
+                             "of ints.")
+        d = X.shape[1]
+        if cf.dtype.kind == "i":
+            if np.max(cf) >= d or np.min(cf) < 0:
+                raise ValueError("categorical_features set as integer indices must be in "
+                                 "[0, n_features - 1]")
+            is_cat = np.zeros(d, dtype=bool)
+            is_cat[cf] = True
+        else:
+            if cf.shape[0] != d:
+                raise ValueError("categorical_features set as a boolean mask must have shape "
+                                 f"(n_features,), got: {cf.shape}")
+            is_cat = cf
+        if not np.any(is_cat):
+            return None, None
+        known = []
+        for f in range(d):
+            if not is_cat[f]:
+                known.append(None)
+                continue
+            cats = np.unique(X[:, f])
+            cats = cats[~np.isnan(cats)]
+            if cats.size > self.max_bins:
+                raise ValueError(f"Categorical feature at index {f} is expected to have a "
+                                 f"cardinality <= {self.max_bins}")
+            if (cats >= self.max_bins).any():
+                raise ValueError(f"Categorical feature at index {f} is expected to be encoded "
+                                 f"with values < {self.max_bins}")
+            known.append(cats)
+        return is_cat, known
 
     def fit(self, X, y, sample_weight=None):
         X = np.asarray(X.detach().cpu().numpy() if hasattr(X, "detach") else X, dtype=X_DTYPE)
@@ -353,7 +406,10 @@ class BaseHistGradientBoosting(BaseEstimator):
         self._validate_parameters()
         n_samples, self._n_features = X.shape
         self.n_features_in_ = self._n_features
-        self.is_categorical_ = None
+        self.is_categorical_, known_categories = self._check_categories(X)
+        if self.is_categorical_ is not None and self.monotonic_cst is not None and np.any(
+                np.asarray(self.monotonic_cst)[self.is_categorical_] != 0):
+            raise ValueError("Categorical features cannot have monotonic constraints.")
         self._loss = self._get_loss(sample_weight) if isinstance(self.loss, str) else self.loss
         self.do_early_stopping_ = (n_samples > 10000 if self.early_stopping == "auto"
                                    else bool(self.early_stopping))
@@ -375,7 +431,9 @@ class BaseHistGradientBoosting(BaseEstimator):
             X_val = y_val = sw_val = None
         n_bins = self.max_bins + 1
         if not (self.warm_start and self._is_fitted()):
-            self._bin_mapper = _BinMapper(n_bins=n_bins, random_state=self._random_seed)
+            self._bin_mapper = _BinMapper(n_bins=n_bins, is_categorical=self.is_categorical_,
+                                          known_categories=known_categories,
+                                          random_state=self._random_seed)
             Xb = self._bin_mapper.fit_transform(X_tr)
         else:
             Xb = self._bin_mapper.transform(X_tr)
@@ -416,18 +474,25 @@ class BaseHistGradientBoosting(BaseEstimator):
                       min_samples_leaf=self.min_samples_leaf,
                       l2_regularization=self.l2_regularization, n_bins=n_bins)
         nbnm = np.ascontiguousarray(self._bin_mapper.n_bins_non_missing_, dtype=np.uint32)
+        is_cat = np.ascontiguousarray(self._bin_mapper.is_categorical_, dtype=np.uint8)
+        self._known_cat_bitsets = np.zeros((self._n_features, 8), dtype=np.uint32)
+        for f in np.flatnonzero(is_cat):
+            for c in self._bin_mapper.bin_thresholds_[f].astype(int):
+                self._known_cat_bitsets[f, c >> 5] |= np.uint32(1 << (c & 31))
         for it in range(begin, self.max_iter):
             self._loss.update_gradients_and_hessians(g, h, y_tr, raw, sw_tr)
             self._predictors.append([])
             for k in range(K):
                 hk = h[0] if self._loss.hessians_are_constant else h[k]
                 nodes, leaf_of = _grow_tree(Xb, g[k], hk, self._loss.hessians_are_constant,
-                                            nbnm, has_missing, mono, params, self.learning_rate)
+                                            nbnm, has_missing, mono, params, self.learning_rate,
+                                            is_cat)
                 if self._loss.need_update_leaves_values:
                     self._loss.update_leaves_values(nodes, leaf_of, y_tr, raw[k], sw_tr,
                                                     self.learning_rate)
                 self._finalize_thresholds(nodes)
                 pred = TreePredictor(nodes)
+                pred.known_cat_bitsets = self._known_cat_bitsets
                 self._predictors[-1].append(pred)
                 raw[k] += nodes["value"][leaf_of]
             stop = False
@@ -451,13 +516,24 @@ class BaseHistGradientBoosting(BaseEstimator):
 
     def _finalize_thresholds(self, nodes):
         thr = np.zeros(len(nodes["value"]))
+        raw = np.zeros((len(nodes["value"]), 8), dtype=np.uint32)
         for i in np.where(nodes["is_leaf"] == 0)[0]:
             f, b = nodes["feature_idx"][i], nodes["bin_threshold"][i]
+            if nodes["is_categorical"][i]:
+                # binned bitset -> raw category values
+                cats = self._bin_mapper.bin_thresholds_[f]
+                bits = nodes["left_cat_bitset"][i]
+                for j, c in enumerate(cats):
+                    if (bits[j >> 5] >> (j & 31)) & 1:
+                        c = int(c)
+                        raw[i, c >> 5] |= np.uint32(1 << (c & 31))
+                continue
             if b == self._bin_mapper.n_bins_non_missing_[f] - 1:
                 thr[i] = np.inf
             else:
                 thr[i] = self._bin_mapper.bin_thresholds_[f][b]
         nodes["num_threshold"] = thr
+        nodes["raw_left_cat_bitset"] = raw
 
     def _is_fitted(self):
         return len(getattr(self, "_predictors", [])) > 0
@@ -527,6 +603,16 @@ def _predict_trees(preds, X):
     arrs = [cat("feature_idx", np.int32), cat("num_threshold", np.float64),
             cat("missing_go_to_left", np.uint8), cat("left", np.int32), cat("right", np.int32),
             cat("is_leaf", np.uint8), cat("value", np.float64)]
+    known = getattr(preds[0], "known_cat_bitsets", None)
+    if known is not None and any(p.nodes.get("is_categorical", np.zeros(1)).any() for p in preds):
+        ic = cat("is_categorical", np.uint8)
+        rb = np.ascontiguousarray(np.concatenate([p.nodes["raw_left_cat_bitset"] for p in preds]),
+                                  dtype=np.uint32)
+        kb = np.ascontiguousarray(known, dtype=np.uint32)
+        _host.lib().sqh_hgb_predict_cat(X.ctypes.data, n, d, *(a.ctypes.data for a in arrs),
+                                        ic.ctypes.data, rb.ctypes.data, kb.ctypes.data,
+                                        offs.ctypes.data, len(preds), out.ctypes.data)
+        return out
     _host.lib().sqh_hgb_predict(X.ctypes.data, n, d, *(a.ctypes.data for a in arrs),
                                 offs.ctypes.data, len(preds), out.ctypes.data)
     return out

@@ -51,7 +51,10 @@ _SIGS = {
     "sqh_tree_free": (None, [_P]),
     "sqh_forest_apply": (None, [_P, _P, _P, _P, _P, _I, _P, _LL, _LL, _P]),
     "sqh_hgb_map_bins": (None, [_P, _LL, _I, _P, _P, _I, _P]),
-    "sqh_hgb_grow": (_P, [_P, _LL, _I, _P, _P, _I, _P, _P, _P, _P]),
+    "sqh_hgb_grow": (_P, [_P, _LL, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "sqh_hgb_copy_cat": (None, [_P, _P, _P]),
+    "sqh_hgb_predict_cat": (None, [_P, _LL, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                   _I, _P]),
     "sqh_hgb_size": (_LL, [_P]),
     "sqh_hgb_copy": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LL]),
     "sqh_hgb_free": (None, [_P]),
