@@ -1,0 +1,4 @@
+"""Reference-layout import path ``sklearn.metrics.cluster``."""
+from ..models.cluster._bicluster import consensus_score  # noqa: F401
+from ..utils.cluster_metrics import *  # noqa: F401,F403
+from ..utils.metrics import adjusted_rand_score  # noqa: F401,E402

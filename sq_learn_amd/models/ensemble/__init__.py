@@ -10,9 +10,10 @@ __all__ = ["RandomForestClassifier", "RandomForestRegressor", "ExtraTreesClassif
            "GradientBoostingRegressor", "HistGradientBoostingClassifier",
            "HistGradientBoostingRegressor"]
 from ._meta import (AdaBoostClassifier, AdaBoostRegressor, BaggingClassifier,  # noqa: E402
+                    BaseEnsemble,
                     BaggingRegressor, IsolationForest, StackingClassifier, StackingRegressor,
                     VotingClassifier, VotingRegressor)
 
 __all__ += ["BaggingClassifier", "BaggingRegressor", "IsolationForest", "AdaBoostClassifier",
             "AdaBoostRegressor", "VotingClassifier", "VotingRegressor", "StackingClassifier",
-            "StackingRegressor"]
+            "StackingRegressor", "BaseEnsemble"]

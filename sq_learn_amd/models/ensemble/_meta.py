@@ -12,6 +12,7 @@ by the native CART of ``csrc/host/tree.cpp``) match the reference's.
 """
 
 import numbers
+from abc import ABCMeta, abstractmethod
 from copy import deepcopy
 
 import numpy as np
@@ -58,6 +59,47 @@ def _accepts_sample_weight(est):
 
 
 # ------------------------------------------------------------------ Bagging
+class BaseEnsemble(MetaEstimatorMixin, BaseEstimator, metaclass=ABCMeta):
+    """Base of homogeneous ensembles (reference ``ensemble/_base.py``):
+    validates ``base_estimator`` and stamps out configured clones."""
+
+    @abstractmethod
+    def __init__(self, base_estimator=None, *, n_estimators=10, estimator_params=tuple()):
+        self.base_estimator = base_estimator
+        self.n_estimators = n_estimators
+        self.estimator_params = estimator_params
+
+    def _validate_estimator(self, default=None):
+        if not isinstance(self.n_estimators, numbers.Integral):
+            raise ValueError("n_estimators must be an integer, got {0}."
+                             .format(type(self.n_estimators)))
+        if self.n_estimators <= 0:
+            raise ValueError("n_estimators must be greater than zero, got {0}."
+                             .format(self.n_estimators))
+        self.base_estimator_ = self.base_estimator if self.base_estimator is not None \
+            else default
+        if self.base_estimator_ is None:
+            raise ValueError("base_estimator cannot be None")
+
+    def _make_estimator(self, append=True, random_state=None):
+        est = clone(self.base_estimator_)
+        est.set_params(**{p: getattr(self, p) for p in self.estimator_params})
+        if random_state is not None:
+            _set_random_states(est, random_state)
+        if append:
+            self.estimators_.append(est)
+        return est
+
+    def __len__(self):
+        return len(self.estimators_)
+
+    def __getitem__(self, index):
+        return self.estimators_[index]
+
+    def __iter__(self):
+        return iter(self.estimators_)
+
+
 class BaseBagging(MetaEstimatorMixin, BaseEstimator):
     def _default_base(self):
         raise NotImplementedError

@@ -944,4 +944,8 @@ __all__ = ["KDTree", "BallTree", "DistanceMetric", "RadiusNeighborsClassifier",
            "RadiusNeighborsRegressor", "KNeighborsTransformer", "RadiusNeighborsTransformer",
            "KernelDensity", "LocalOutlierFactor", "NearestCentroid",
            "NeighborhoodComponentsAnalysis", "kneighbors_graph", "radius_neighbors_graph",
-           "VALID_METRICS"]
+           "VALID_METRICS", "VALID_METRICS_SPARSE"]
+
+VALID_METRICS_SPARSE = {"ball_tree": [], "kd_tree": [],
+                        "brute": sorted({"cityblock", "cosine", "euclidean", "l1", "l2",
+                                         "manhattan", "precomputed"})}

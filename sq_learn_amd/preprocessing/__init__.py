@@ -224,3 +224,54 @@ __all__ += ["PolynomialFeatures", "LabelBinarizer", "LabelEncoder", "MultiLabelB
             "PowerTransformer", "QuantileTransformer", "RobustScaler", "SplineTransformer",
             "add_dummy_feature", "binarize", "maxabs_scale", "power_transform",
             "quantile_transform", "robust_scale"]
+
+
+def scale(X, *, axis=0, with_mean=True, with_std=True, copy=True):
+    """Standardise along an axis (reference ``preprocessing/_data.py``
+    ``scale``: NaN-aware, with the two-pass re-centring of large means)."""
+    import warnings as _w
+    Xa = np.array(to_numpy(X) if hasattr(X, "detach") else X, dtype=np.float64, copy=True)
+    Xr = Xa if axis == 0 else Xa.T
+    if with_mean:
+        mean_ = np.nanmean(Xr, axis=0)
+    if with_std:
+        scale_ = np.nanstd(Xr, axis=0)
+        scale_ = np.where(scale_ < 10 * np.finfo(scale_.dtype).eps, 1.0, scale_)
+    if with_mean:
+        Xr -= mean_
+        m1 = np.nanmean(Xr, axis=0)
+        if not np.allclose(m1, 0):
+            _w.warn("Numerical issues were encountered when centering the data and might not "
+                    "be solved. Dataset may contain too large values. You may need to prescale "
+                    "your features.")
+            Xr -= m1
+    if with_std:
+        Xr /= scale_
+        if with_mean:
+            m2 = np.nanmean(Xr, axis=0)
+            if not np.allclose(m2, 0):
+                _w.warn("Numerical issues were encountered when scaling the data and might not "
+                        "be solved. The standard deviation of the data is probably very close to "
+                        "0. ")
+                Xr -= m2
+    return Xa
+
+
+def minmax_scale(X, feature_range=(0, 1), *, axis=0, copy=True):
+    """Scale every feature (axis=0) or sample (axis=1) to ``feature_range``."""
+    Xa = np.array(to_numpy(X) if hasattr(X, "detach") else X, dtype=np.float64, copy=True)
+    orig_1d = Xa.ndim == 1
+    if orig_1d:
+        Xa = Xa.reshape(-1, 1)
+    Xr = Xa if axis == 0 else Xa.T
+    lo, hi = feature_range
+    if lo >= hi:
+        raise ValueError("Minimum of desired feature range must be smaller than maximum. Got %s."
+                         % str(feature_range))
+    dmin, dmax = np.nanmin(Xr, axis=0), np.nanmax(Xr, axis=0)
+    rng = dmax - dmin
+    rng = np.where(rng < 10 * np.finfo(np.float64).eps, 1.0, rng)
+    s = (hi - lo) / rng
+    Xr *= s
+    Xr += lo - dmin * s
+    return Xa.ravel() if orig_1d else Xa

@@ -44,3 +44,11 @@ def all_estimators(type_filter=None):
            "cluster": ClusterMixin, "transformer": TransformerMixin}
     return [(n, c) for n, c in out if any(issubclass(c, mix[f]) for f in filters)]
 from ._bunch import Bunch  # noqa: E402,F401
+from ._misc import (_safe_indexing, as_float_array, assert_all_finite,  # noqa: E402,F401
+                    check_symmetric, deprecated, indexable, is_scalar_nan, resample, safe_mask,
+                    safe_sqr, shuffle)
+from .class_weight import compute_class_weight, compute_sample_weight  # noqa: E402,F401
+from .murmurhash import murmurhash3_32  # noqa: E402,F401
+from .pairwise import gen_batches, gen_even_slices  # noqa: E402,F401
+from .validation import (check_array, check_consistent_length, check_random_state,  # noqa: E402,F401
+                         check_scalar, check_X_y, column_or_1d)
