@@ -207,6 +207,9 @@ class GaussianMixture(DensityMixin, BaseEstimator):
         self._c = c
         self._pc = _compute_precision_cholesky(c, self.covariance_type)
 
+    def _compute_lower_bound(self, log_resp, log_prob_norm):
+        return float(log_prob_norm)
+
     def _get_params(self):
         return (self._w.clone(), self._m.clone(), self._c.clone() if hasattr(self, "_c") else None,
                 self._pc.clone())
@@ -262,7 +265,7 @@ class GaussianMixture(DensityMixin, BaseEstimator):
                 prev = lower_bound
                 lpn, log_resp = self._e_step(Xt)
                 self._m_step(Xt, log_resp)
-                lower_bound = float(lpn)
+                lower_bound = self._compute_lower_bound(log_resp, lpn)
                 if abs(lower_bound - prev) < self.tol:
                     converged = True
                     break
@@ -346,4 +349,7 @@ class GaussianMixture(DensityMixin, BaseEstimator):
         return st
 
 
-__all__ = ["GaussianMixture"]
+__all__ = ["GaussianMixture", "BayesianGaussianMixture"]
+
+
+from ._bayesian_mixture import BayesianGaussianMixture  # noqa: E402,F401
