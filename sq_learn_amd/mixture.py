@@ -29,30 +29,78 @@ def _dense(X):
     return X
 
 
+def _split_k(n, target=512):
+    """Number of row chunks for a split-K reduction over n rows."""
+    return max(1, n // target)
+
+
+def _atb(A, B):
+    """A^T B for tall (n, p) / (n, q) operands with small p, q.  A library
+    GEMM maps such a product onto a single output tile, i.e. one CU walking
+    all n rows; splitting the rows into chunks turns it into a batched GEMM
+    over many CUs followed by a tiny reduction."""
+    n = A.shape[0]
+    C = _split_k(n)
+    if C == 1 or A.device.type == "cpu":
+        return A.T @ B
+    m = (n // C) * C
+    out = torch.bmm(A[:m].reshape(C, n // C, -1).transpose(1, 2),
+                    B[:m].reshape(C, n // C, -1)).sum(0)
+    if m < n:
+        out += A[m:].T @ B[m:]
+    return out
+
+
+def _weighted_scatter(X, means, resp):
+    """Per-component sum_i r_ik (x_i - m_k)(x_i - m_k)^T, batched over the
+    components and split over the rows (see ``_atb``)."""
+    n, d = X.shape
+    K = means.shape[0]
+    if X.device.type == "cpu":
+        out = torch.empty((K, d, d), dtype=X.dtype)
+        for k in range(K):
+            diff = X - means[k]
+            out[k] = (resp[:, k, None] * diff).T @ diff
+        return out
+    C = _split_k(n)
+    m = (n // C) * C
+    # bound the (K_g, n, d) temporaries to ~1 GiB
+    kg = max(1, min(K, (1 << 30) // max(1, 8 * n * d)))
+    out = torch.empty((K, d, d), dtype=X.dtype, device=X.device)
+    for k0 in range(0, K, kg):
+        k1 = min(K, k0 + kg)
+        D = X[None] - means[k0:k1, None, :]                     # (g, n, d)
+        Dw = D * resp[:, k0:k1].T[:, :, None]
+        g = k1 - k0
+        acc = torch.bmm(Dw[:, :m].reshape(g * C, n // C, d).transpose(1, 2),
+                        D[:, :m].reshape(g * C, n // C, d)).reshape(g, C, d, d).sum(1)
+        if m < n:
+            acc += torch.bmm(Dw[:, m:].transpose(1, 2), D[:, m:])
+        out[k0:k1] = acc
+    return out
+
+
 def _estimate_gaussian_parameters(X, resp, reg_covar, covariance_type):
     nk = resp.sum(0) + 10 * torch.finfo(resp.dtype).eps
-    means = (resp.T @ X) / nk[:, None]
+    means = _atb(resp, X) / nk[:, None]
     d = X.shape[1]
     if covariance_type == "full":
-        cov = torch.empty((len(nk), d, d), dtype=X.dtype, device=X.device)
-        for k in range(len(nk)):
-            diff = X - means[k]
-            cov[k] = (resp[:, k, None] * diff).T @ diff / nk[k]
-            cov[k].diagonal().add_(reg_covar)
+        cov = _weighted_scatter(X, means, resp) / nk[:, None, None]
+        cov.diagonal(dim1=-2, dim2=-1).add_(reg_covar)
     elif covariance_type == "tied":
-        avg_X2 = X.T @ X
+        avg_X2 = _atb(X, X)
         avg_means2 = (nk * means.T) @ means
         cov = (avg_X2 - avg_means2) / nk.sum()
         cov.diagonal().add_(reg_covar)
     elif covariance_type == "diag":
-        avg_X2 = (resp.T @ (X * X)) / nk[:, None]
+        avg_X2 = _atb(resp, X * X) / nk[:, None]
         avg_means2 = means ** 2
-        avg_X_means = means * (resp.T @ X) / nk[:, None]
+        avg_X_means = means * _atb(resp, X) / nk[:, None]
         cov = avg_X2 - 2 * avg_X_means + avg_means2 + reg_covar
     else:
-        avg_X2 = (resp.T @ (X * X)) / nk[:, None]
+        avg_X2 = _atb(resp, X * X) / nk[:, None]
         avg_means2 = means ** 2
-        avg_X_means = means * (resp.T @ X) / nk[:, None]
+        avg_X_means = means * _atb(resp, X) / nk[:, None]
         cov = (avg_X2 - 2 * avg_X_means + avg_means2 + reg_covar).mean(1)
     return nk, means, cov
 

@@ -101,3 +101,21 @@ def test_mlp_trains_on_device():
     a = SNN.MLPClassifier(**kw).fit(X, y)
     # same RNG stream, device GEMM reduction order: tiny drift only
     np.testing.assert_allclose(a.predict_proba(X), b.predict_proba(X), atol=1e-6)
+
+
+def test_mixtures_split_k_on_device():
+    import sklearn.mixture as SMx
+    from sklearn.datasets import make_blobs
+
+    import sq_learn_amd.mixture as MMx
+    X = make_blobs(5000, 6, centers=4, random_state=0)[0]   # n > split-K threshold
+    for ct in ("full", "tied", "diag", "spherical"):
+        kw = dict(n_components=4, covariance_type=ct, init_params="random", random_state=0)
+        a = SMx.GaussianMixture(**kw).fit(X)
+        b = MMx.GaussianMixture(**kw).fit(X)
+        np.testing.assert_allclose(a.means_, b.means_, atol=1e-6)
+        a = SMx.BayesianGaussianMixture(max_iter=200, **kw).fit(X)
+        b = MMx.BayesianGaussianMixture(max_iter=200, **kw).fit(X)
+        assert b._pc.device.type == "cuda"
+        np.testing.assert_allclose(a.weights_, b.weights_, atol=1e-6)
+        np.testing.assert_allclose(a.means_, b.means_, atol=1e-5)
