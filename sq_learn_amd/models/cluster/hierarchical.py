@@ -61,10 +61,116 @@ def _linkage_matrix(cond, n, method, ordered_children=True):
     return Z
 
 
+def _fix_connectivity(X, connectivity, affinity="euclidean"):
+    """Symmetrise the connectivity graph and join disconnected components
+    through their closest pair (reference ``cluster/_agglomerative.py``)."""
+    import warnings
+
+    from scipy import sparse
+    from scipy.sparse.csgraph import connected_components
+
+    from ...utils.pairwise import pairwise_distances
+    n = X.shape[0]
+    if connectivity.shape[0] != n or connectivity.shape[1] != n:
+        raise ValueError("Wrong shape for connectivity matrix: %s when X is %s"
+                         % (connectivity.shape, X.shape))
+    C = sparse.csr_matrix(connectivity)
+    C = (C + C.T).tolil()
+    ncc, labels = connected_components(C)
+    if ncc > 1:
+        warnings.warn("the number of connected components of the connectivity matrix is %d > 1. "
+                      "Completing it to avoid stopping the tree early." % ncc, stacklevel=2)
+        Xn = np.asarray(X.detach().cpu().numpy() if hasattr(X, "detach") else X)
+        for i in range(ncc):
+            ii = np.where(labels == i)[0]
+            for j in range(i):
+                jj = np.where(labels == j)[0]
+                D = np.asarray(pairwise_distances(Xn[ii], Xn[jj], metric=affinity))
+                a, b = np.where(D == np.min(D))
+                C[ii[a[0]], jj[b[0]]] = True
+                C[jj[b[0]], ii[a[0]]] = True
+    return C, ncc
+
+
+def _structured_ward(X, connectivity, n_clusters, return_distance):
+    """Ward agglomeration restricted to a connectivity graph: a heap of
+    candidate merges along graph edges (reference ``ward_tree`` structured
+    branch and ``_hierarchical_fast.pyx`` ``compute_ward_dist`` /
+    ``_get_parents``)."""
+    import heapq
+    Xn = np.asarray(X.detach().cpu().numpy() if hasattr(X, "detach") else X, dtype=np.float64)
+    n, d = Xn.shape
+    C, ncc = _fix_connectivity(Xn, connectivity)
+    rows_i, cols_i, A = [], [], []
+    for ind, row in enumerate(C.rows):
+        A.append(list(row))
+        lower = [i for i in row if i < ind]
+        rows_i.extend([ind] * len(lower))
+        cols_i.extend(lower)
+    if n_clusters is None:
+        n_nodes = 2 * n - 1
+    else:
+        if n_clusters > n:
+            raise ValueError("Cannot provide more clusters than samples. %i n_clusters was asked, "
+                             "and there are %i samples." % (n_clusters, n))
+        n_nodes = 2 * n - n_clusters
+    m1 = np.zeros(n_nodes)
+    m1[:n] = 1
+    m2 = np.zeros((n_nodes, d))
+    m2[:n] = Xn
+
+    def ward_dist(r, c):
+        r = np.asarray(r, dtype=np.intp)
+        c = np.asarray(c, dtype=np.intp)
+        w = m1[r] * m1[c] / (m1[r] + m1[c])
+        diff = m2[r] / m1[r][:, None] - m2[c] / m1[c][:, None]
+        return (diff * diff).sum(1) * w
+
+    heap = list(zip(ward_dist(rows_i, cols_i).tolist(), rows_i, cols_i))
+    heapq.heapify(heap)
+    parent = np.arange(n_nodes, dtype=np.intp)
+    used = np.ones(n_nodes, dtype=bool)
+    children = []
+    dist = np.empty(n_nodes - n) if return_distance else None
+    for k in range(n, n_nodes):
+        while True:
+            inert, i, j = heapq.heappop(heap)
+            if used[i] and used[j]:
+                break
+        parent[i] = parent[j] = k
+        children.append((i, j))
+        used[i] = used[j] = False
+        if return_distance:
+            dist[k - n] = inert
+        m1[k] = m1[i] + m1[j]
+        m2[k] = m2[i] + m2[j]
+        heads, seen = [], np.ones(n_nodes, dtype=bool)
+        seen[k] = False
+        for node0 in A[i] + A[j]:
+            node = node0
+            p = parent[node]
+            while p != node:
+                node = p
+                p = parent[node]
+            if seen[node]:
+                seen[node] = False
+                heads.append(node)
+        for c in heads:
+            A[c].append(k)
+        A.append(heads)
+        if heads:
+            for dd, c in zip(ward_dist([k] * len(heads), heads).tolist(), heads):
+                heapq.heappush(heap, (dd, k, c))
+    children = np.array([c[::-1] for c in children], dtype=np.intp)
+    if return_distance:
+        return children, ncc, n, parent, np.sqrt(2.0 * dist)
+    return children, ncc, n, parent
+
+
 def ward_tree(X, *, connectivity=None, n_clusters=None, return_distance=False, device=None):
     """(children, n_connected_components, n_leaves, parents[, distances])."""
     if connectivity is not None:
-        raise NotImplementedError("connectivity-constrained trees are not implemented")
+        return _structured_ward(X, connectivity, n_clusters, return_distance)
     X = X if isinstance(X, torch.Tensor) else check_array(X)
     n = X.shape[0]
     if n_clusters is not None:
@@ -185,21 +291,45 @@ class AgglomerativeClustering(ClusterMixin, BaseEstimator):
         if self.linkage not in _TREE_BUILDERS:
             raise ValueError("Unknown linkage type %s. Valid options are %s"
                              % (self.linkage, _TREE_BUILDERS.keys()))
-        if self.connectivity is not None:
-            raise NotImplementedError("connectivity-constrained agglomeration is not implemented")
+        connectivity = self.connectivity
+        if connectivity is not None:
+            if callable(connectivity):
+                connectivity = connectivity(X)
+            if self.linkage != "ward":
+                raise NotImplementedError("connectivity-constrained %s linkage is not "
+                                          "implemented (ward is)" % self.linkage)
+        full = self.compute_full_tree
+        if connectivity is None:
+            full = True
+        if full == "auto":
+            full = True if self.distance_threshold is not None else \
+                self.n_clusters < max(100, 0.02 * X.shape[0])
         kwargs = {} if self.linkage == "ward" else {"affinity": self.affinity}
         return_distance = self.distance_threshold is not None or self.compute_distances
-        out = _TREE_BUILDERS[self.linkage](X, connectivity=None, n_clusters=None,
+        out = _TREE_BUILDERS[self.linkage](X, connectivity=connectivity,
+                                           n_clusters=None if full else self.n_clusters,
                                            return_distance=return_distance, device=self.device,
                                            **kwargs)
-        self.children_, self.n_connected_components_, self.n_leaves_, _ = out[:4]
+        self.children_, self.n_connected_components_, self.n_leaves_, parents = out[:4]
         if return_distance:
             self.distances_ = out[-1]
         if self.distance_threshold is not None:
             self.n_clusters_ = int(np.count_nonzero(self.distances_ >= self.distance_threshold)) + 1
         else:
             self.n_clusters_ = self.n_clusters
-        self.labels_ = _hc_cut(self.n_clusters_, self.children_, self.n_leaves_)
+        if full:
+            self.labels_ = _hc_cut(self.n_clusters_, self.children_, self.n_leaves_)
+        else:
+            heads = np.array(parents, copy=True)
+            for node0 in range(len(heads)):
+                node = node0
+                p = heads[node]
+                while p != node:
+                    heads[node0] = p
+                    node = p
+                    p = heads[node]
+            lab = heads[:X.shape[0]]
+            self.labels_ = np.searchsorted(np.unique(lab), lab)
         return self
 
     def fit_predict(self, X, y=None):
