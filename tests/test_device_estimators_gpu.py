@@ -119,3 +119,17 @@ def test_mixtures_split_k_on_device():
         assert b._pc.device.type == "cuda"
         np.testing.assert_allclose(a.weights_, b.weights_, atol=1e-6)
         np.testing.assert_allclose(a.means_, b.means_, atol=1e-5)
+
+
+def test_sparse_encode_batched_cd_on_device():
+    import sklearn.decomposition as SD
+
+    import sq_learn_amd.decomposition as MD
+    rng = np.random.RandomState(0)
+    X = rng.randn(300, 24)
+    D = rng.randn(10, 24)
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    for pos in (False, True):
+        a = SD.sparse_encode(X, D, algorithm="lasso_cd", alpha=0.3, positive=pos)
+        b = MD.sparse_encode(X, D, algorithm="lasso_cd", alpha=0.3, positive=pos)
+        np.testing.assert_allclose(a, b, atol=1e-8)
