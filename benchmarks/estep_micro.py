@@ -19,35 +19,49 @@ ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--delta", type=float, default=0.5)
 ap.add_argument("--what", default="estep", choices=["estep", "reduce", "both"])
+ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16"])
 a = ap.parse_args()
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
 C = torch.randn(a.k, a.d, device=dev, generator=g) * 3
-X = torch.empty(a.n, a.d, dtype=torch.bfloat16, device=dev)
+X = torch.empty(a.n, a.d, dtype=torch.bfloat16 if a.prec == "bf16" else torch.float32, device=dev)
 step = 1 << 20
 for s in range(0, a.n, step):
     e = min(a.n, s + step)
     lab = torch.randint(0, a.k, (e - s,), device=dev, generator=g)
-    X[s:e] = (C[lab] + torch.randn(e - s, a.d, device=dev, generator=g)).to(torch.bfloat16)
+    X[s:e] = (C[lab] + torch.randn(e - s, a.d, device=dev, generator=g)).to(X.dtype)
 kp, dp = K.pad_clusters(a.k), K.pad_features(a.d)
-Cb, cn = K.centers_to_bf16(C, kp, dp)
 xn = L.row_norms_sq(X)
+if a.prec == "bf16":
+    Cb, cn = K.centers_to_bf16(C, kp, dp)
+else:
+    alpha = K.choose_alpha(float(xn.max()), 1.0)
+    Cop = torch.empty(K.operand_f16_shape(kp, dp), dtype=torch.float16, device=dev)
+    K.centers_to_f16_native(C, Cop, a.k, a.d, dp, kp, alpha)
+
+
+def run_estep():
+    if a.prec == "bf16":
+        K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
+    else:
+        K.estep_f32_native(X, Cop, xn, C, a.k, a.delta, alpha, key, 0, buf)
+
 buf = K.EStepBuffers(a.n, dev)
 ws = K.ReduceWorkspace(a.n, a.k, dev).set_scale(float(X.float().abs().max()), a.n)
 sums = torch.zeros(a.k, a.d, dtype=torch.float64, device=dev)
 cnt = torch.zeros(a.k, dtype=torch.float64, device=dev)
 key = RngKey(1, "band_select", 0)
-K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
+run_estep()
 torch.cuda.synchronize()
 for name in (["estep", "reduce"] if a.what == "both" else [a.what]):
     t0 = time.perf_counter()
     for _ in range(a.iters):
         if name == "estep":
-            K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
+            run_estep()
         else:
             sums.zero_(); cnt.zero_()
             K.centroid_reduce_native(X, buf.labels, None, sums, cnt, a.k, ws)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / a.iters * 1e3
     fl = 2.0 * a.n * a.k * dp
-    print(f"{name}: {ms:.3f} ms  ({fl / ms / 1e9:.1f} TFLOP/s equiv)  ovf={int(buf.ovf_count.item())}")
+    print(f"{a.prec} {name}: {ms:.3f} ms  ({fl / ms / 1e9:.1f} TFLOP/s equiv)  ovf={int(buf.ovf_count.item())}")

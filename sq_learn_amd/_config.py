@@ -22,11 +22,13 @@ _global_config = {
     # --- MI355X framework keys ---
     # 'auto' -> cuda (HIP) when a GPU is visible, else cpu
     "device": os.environ.get("SQ_DEVICE", "auto"),
-    # precision of the distance / Gram GEMMs on GPU:
-    #   'bf16'   : bf16 operands, fp32 accumulation (MFMA 32x32x16)
-    #   'bf16x2' : data bf16, centroids split hi+lo bf16 (2 MFMA passes, ~fp32 centroid precision)
-    #   'fp32'   : fp32 operands (library GEMM + band-select kernel)
-    "gemm_precision": os.environ.get("SQ_GEMM_PRECISION", "bf16"),
+    # precision of the q-means / k-means distance GEMMs on GPU:
+    #   'fp32' : fp32-faithful (default) - fused E-step on an fp16 hi/lo split
+    #            (3 MFMA products, fp32 accumulation, csrc/estep_f32.hip),
+    #            overflow rows re-selected in fp64
+    #   'bf16' : bf16 operands, fp32 accumulation (MFMA 32x32x16): ~2x faster,
+    #            band edges only bf16-accurate (2^-9 per operand)
+    "gemm_precision": os.environ.get("SQ_GEMM_PRECISION", "fp32"),
     # default seed of the counter-based (Philox) stochastic layer when an
     # estimator is given random_state=None
     "seed": int(os.environ.get("SQ_SEED", 0x5EED)),
@@ -57,8 +59,8 @@ def set_config(assume_finite=None, working_memory=None, print_changed_only=None,
         if device is not None:
             _global_config["device"] = device
         if gemm_precision is not None:
-            if gemm_precision not in ("bf16", "bf16x2", "fp32"):
-                raise ValueError("gemm_precision must be 'bf16', 'bf16x2' or 'fp32'")
+            if gemm_precision not in ("bf16", "fp32"):
+                raise ValueError("gemm_precision must be 'bf16' or 'fp32'")
             _global_config["gemm_precision"] = gemm_precision
         if seed is not None:
             _global_config["seed"] = int(seed)

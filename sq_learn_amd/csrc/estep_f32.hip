@@ -1,0 +1,539 @@
+// fp32-faithful fused q-means E-step on gfx950 (SURVEY.md §2.6 K1/K2,
+// reference ``sklearn/cluster/_dmeans.py:736-751``: fp64 ``cdist`` squared,
+// then the delta-band {j : D_ij <= min_i + delta}).
+//
+// Arithmetic.  gfx950 has no xf32 MFMA and the exact fp32 MFMA runs at 1/16
+// of the fp16 rate, so the products are formed from an fp16 hi/lo split:
+//   x^ = alpha x = xh + xl,   c^ = -2 alpha c = ch + cl      (fp16 each)
+//   x^.c^ ~= xh.ch + xh.cl + xl.ch                            (3 MFMA passes)
+// alpha is a power of two chosen on the host so that alpha^2 max||x||^2 <=
+// 2^13: every fp16 piece is in range, products of fp16 pieces are exact in
+// fp32 and the accumulation is fp32 (v_mfma_f32_32x32x16_f16).  The split
+// represents each operand to 2^-22 relative (2^-25 absolute for entries far
+// below the row scale) and the dropped xl.cl term is 2^-22 relative, i.e. the
+// result has the error profile of an fp32 GEMM (error ~ 2^-24 sqrt(K) of the
+// partial sums), unlike the bf16 kernel (2^-9 per operand).  The centroid
+// norm alpha^2 ||c||^2 rides in an augmented k-step as a 3-way fp16 split
+// against the constant A fragment [1, 1, 1, 0 ...], so the accumulator holds
+//   D'~ = alpha^2 (||c||^2 - 2 x.c)       (the row-constant ||x||^2 is added
+// only to the reported minimum: the band test needs no cancellation with it)
+// and the band threshold is compared in the same scaled units (delta alpha^2,
+// exact: alpha is a power of two).
+//
+// Selection.  No index packing: every lane keeps the 3 smallest values of its
+// columns (j = lane mod 32 of every tile, 2 per tile) with the indices of the
+// two smallest in separate registers (8 VALU per value, hidden under the 6
+// MFMAs of each k-step).  After the sweep the 32 lanes sharing a row merge
+// their (min, 2nd, argmin) by a transposed reduce-scatter; rows whose 2nd
+// value is inside the band are resolved from the per-lane top-2 lists in
+// kappa order (band.h); a lane whose 3rd value is inside the band could hide
+// a 4th member -> the row goes to the overflow list and is re-done in fp64 by
+// band_rows_f64 (all k distances, sum of (x - c)^2 - cdist's own formula).
+//
+// Layout.  One workgroup = 4 waves (one per SIMD, up to 512 registers) x 32
+// rows; each wave keeps its 32 rows as fp16 hi/lo A fragments in VGPRs for the
+// whole centroid sweep (X is read from HBM once per iteration, as fp32, and
+// split in registers).  Centroid tiles of 64 stream through a 2-deep LDS ring
+// by LDS-DMA (global_load_lds, 16 B per lane); a tile is [hi chunks (d/8 + 2,
+// incl. the norm chunk)][lo chunks (d/8)] of [64 centroids][8 fp16], so every
+// B-fragment read is base + immediate and conflict-free.  Persistent grid; the
+// next block's rows are loaded while the merge / band resolution runs and the
+// epilogue of tile t runs in the MFMA shadow of tile t+1.
+#include "common.h"
+#include "band.h"
+
+namespace sq {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTileN = 64;          // centroids per LDS tile
+
+SQ_DEV float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+SQ_DEV float vmed3(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+template <int KSD>
+__global__ void __launch_bounds__(256, 1) estep_f32_kernel(
+    const float* __restrict__ X, const _Float16* __restrict__ C, const float* __restrict__ xn,
+    int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ ovf_rows,
+    int* __restrict__ ovf_count, double* __restrict__ part, long long n, int k_pad, float alpha,
+    float inv_alpha2, float delta_s, RngKey key, long long row_offset, int ovf_cap) {
+  constexpr int NW = 4;
+  constexpr int DX = KSD * 16;                 // fp32 row length (padded features)
+  constexpr int HI_BYTES = (KSD + 1) * 2048;   // data chunks + norm chunk pair
+  constexpr int TILE_BYTES = HI_BYTES + KSD * 2048;
+  constexpr int PIECES = TILE_BYTES / 1024;
+  constexpr int ROWS = NW * 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * TILE_BYTES; };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int half = lane >> 5;
+  const int n_tiles = k_pad / kTileN;
+  const long long nblk = (n + ROWS - 1) / ROWS;
+  long long blk = blockIdx.x;
+  if (blk >= nblk) return;
+
+  auto stage = [&](int G) {
+    const int t = G % n_tiles;
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_BYTES;
+    unsigned char* dst = buf(G);
+    for (int p = wave; p < PIECES; p += NW) {
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- A operand: 32 rows of this wave, fp32 from HBM, split in registers
+  f16x8 ah[KSD], al[KSD];
+  float4 raw[KSD][2];
+  auto load_raw = [&](long long b) {
+    const long long r = b * ROWS + wave * 32 + r32;
+    const float* xr = X + (size_t)(r < n ? r : n - 1) * DX + half * 8;
+#pragma unroll
+    for (int ks = 0; ks < KSD; ++ks) {
+      raw[ks][0] = *reinterpret_cast<const float4*>(xr + ks * 16);
+      raw[ks][1] = *reinterpret_cast<const float4*>(xr + ks * 16 + 4);
+    }
+  };
+  auto split = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < KSD; ++ks) {
+      const float v[8] = {raw[ks][0].x, raw[ks][0].y, raw[ks][0].z, raw[ks][0].w,
+                          raw[ks][1].x, raw[ks][1].y, raw[ks][1].z, raw[ks][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float s = v[e] * alpha;                  // exact (power of two)
+        const _Float16 h = (_Float16)s;
+        ah[ks][e] = h;
+        al[ks][e] = (_Float16)(s - (float)h);          // s - h exact in fp32
+      }
+    }
+  };
+  f16x8 aug = (f16x8)0;
+  if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
+
+  // per-lane top-3 values and the indices of the two smallest
+  float m1[16], m2[16], m3[16];
+  int i1[16], i2[16];
+
+  const int lane_off = (half * 64 + r32) * 16;
+  auto ldb = [&](const unsigned char* p) -> f16x8 { return *reinterpret_cast<const f16x8*>(p); };
+
+  auto tile_step = [&](const unsigned char* cur, f32x16& n0, f32x16& n1, bool do_mfma,
+                       const f32x16& o0, const f32x16& o1, int t_prev, bool do_epi) {
+    const int j0 = t_prev * kTileN + r32;
+    const int j1 = j0 + 32;
+    auto ins = [&](int i, float v, int j) {
+      // values, not references, in the selects: a select of two array
+      // elements becomes a select of addresses and spills the arrays
+      const float q1 = m1[i], q2 = m2[i];
+      const int a1 = i1[i], a2 = i2[i];
+      const bool lt1 = v < q1, lt2 = v < q2;
+      const int b2 = lt2 ? j : a2;
+      m3[i] = vmed3(q2, v, m3[i]);
+      m2[i] = vmed3(q1, v, q2);
+      m1[i] = vmin(q1, v);
+      i2[i] = lt1 ? a1 : b2;
+      i1[i] = lt1 ? j : a1;
+    };
+    auto epi_row = [&](int i) {
+      ins(i, o0[i], j0);
+      ins(i, o1[i], j1);
+    };
+    if (do_mfma) {
+      f32x16 acc0 = {0}, acc1 = {0};
+      const unsigned char* hb = cur + lane_off;
+      const unsigned char* lb = cur + HI_BYTES + lane_off;
+      f16x8 bh0[2], bh1[2], bl0[2], bl1[2];
+      bh0[0] = ldb(hb);
+      bh1[0] = ldb(hb + 512);
+      bl0[0] = ldb(lb);
+      bl1[0] = ldb(lb + 512);
+#pragma unroll
+      for (int ks = 0; ks < KSD; ++ks) {
+        const int c = ks & 1, nx = c ^ 1;
+        bh0[nx] = ldb(hb + (ks + 1) * 2048);           // ks + 1 == KSD: the norm chunk
+        bh1[nx] = ldb(hb + (ks + 1) * 2048 + 512);
+        if (ks + 1 < KSD) {
+          bl0[nx] = ldb(lb + (ks + 1) * 2048);
+          bl1[nx] = ldb(lb + (ks + 1) * 2048 + 512);
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh0[c], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh1[c], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl0[c], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl1[c], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh0[c], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh1[c], acc1, 0, 0, 0);
+        if (do_epi) {
+#pragma unroll
+          for (int i = (ks * 16) / KSD; i < ((ks + 1) * 16) / KSD; ++i) epi_row(i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aug, bh0[KSD & 1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aug, bh1[KSD & 1], acc1, 0, 0, 0);
+      n0 = acc0;
+      n1 = acc1;
+    } else if (do_epi) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) epi_row(i);
+    }
+  };
+  auto sync_tile = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  // merge two (min, 2nd, argmin) triples; ties of the min keep the smaller index
+  auto merge = [](float& a1, float& a2, int& ai, float b1, float b2, int bi) {
+    const float lo2 = vmin(a2, b2);
+    const bool tb = b1 < a1 || (b1 == a1 && bi < ai);
+    a2 = vmed3(a1, b1, lo2);
+    a1 = vmin(a1, b1);
+    ai = tb ? bi : ai;
+  };
+
+  int G = 0;
+  stage(0);
+  load_raw(blk);
+  sync_tile();
+  split();
+  double my_inertia = 0.0;
+
+  for (; blk < nblk; blk += gridDim.x) {
+    const long long row0 = blk * ROWS + wave * 32;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      m1[i] = m2[i] = m3[i] = __builtin_inff();
+      i1[i] = i2[i] = 0;
+    }
+    f32x16 pA0, pA1, pB0, pB1;
+    stage(G + 1);
+    tile_step(buf(G), pA0, pA1, true, pA0, pA1, 0, false);
+    sync_tile();
+    int t = 0;
+    while (true) {
+      if (t + 1 >= n_tiles) {
+        load_raw(blk + gridDim.x);   // clamped rows: unconditional
+        tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pB0, pB1, true, pA0, pA1, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+      if (t + 1 >= n_tiles) {
+        load_raw(blk + gridDim.x);
+        tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pA0, pA1, true, pB0, pB1, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+    }
+    ++G;
+
+    // ---- transposed reduce-scatter merge of the 32 lanes of each half: a
+    // lane ends with the row-global (min, 2nd, argmin) of row r32 >> 1
+    float R1[16], R2[16];
+    int RI[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { R1[i] = m1[i]; R2[i] = m2[i]; RI[i] = i1[i]; }
+#pragma unroll
+    for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
+      const bool hi = (r32 & o) != 0;
+#pragma unroll
+      for (int j = 0; j < c; ++j) {
+        const float ra = R1[j], rb = R1[c + j], sa = R2[j], sb = R2[c + j];
+        const int ia = RI[j], ib = RI[c + j];
+        const float s1 = hi ? ra : rb, s2 = hi ? sa : sb;
+        const int si = hi ? ia : ib;
+        float k1 = hi ? rb : ra, k2 = hi ? sb : sa;
+        int ki = hi ? ib : ia;
+        merge(k1, k2, ki, __shfl_xor(s1, o, 64), __shfl_xor(s2, o, 64), __shfl_xor(si, o, 64));
+        R1[j] = k1;
+        R2[j] = k2;
+        RI[j] = ki;
+      }
+    }
+    float q1 = R1[0], q2 = R2[0];
+    int qi = RI[0];
+    merge(q1, q2, qi, __shfl_xor(R1[0], 1, 64), __shfl_xor(R2[0], 1, 64), __shfl_xor(RI[0], 1, 64));
+
+    const int irow = r32 >> 1;
+    const int rloc = (irow & 3) + 8 * (irow >> 2) + 4 * half;
+    const long long grow_local = row0 + rloc;
+    const bool owner = ((r32 & 1) == 0) && grow_local < n;
+    const float thr = q1 + delta_s;
+    const bool band2 = q2 <= thr;
+    if (owner) {
+      const float dist = fmaxf(xn[grow_local] + q1 * inv_alpha2, 0.0f);
+      mind[grow_local] = dist;
+      if (!band2) labels[grow_local] = qi;
+      my_inertia += (double)dist;
+    }
+    // rows with >= 2 band members: the rank rule over the per-lane top-2
+    // lists; lane r32 holds the columns j = r32 mod 32, so (lane, index)
+    // order is kappa order.  A lane whose 3rd value is in the band -> overflow.
+    const unsigned long long slow = __ballot(owner && band2);
+    if (slow) {
+      const float urow = band_u(key, row_offset + grow_local);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const unsigned long long sel = slow & ((1ull << (2 * i)) | (1ull << (32 + 2 * i)));
+        if (!sel) continue;
+        const int src = 32 * half + 2 * i;
+        const bool mine = (slow >> src) & 1ull;
+        const float thr_i = __shfl(thr, src, 64);
+        const float u_i = __shfl(urow, src, 64);
+        const int c1 = (mine && m1[i] <= thr_i) ? 1 : 0;
+        const int c2 = (mine && m2[i] <= thr_i) ? 1 : 0;
+        const bool v3 = mine && m3[i] <= thr_i;
+        const int cl = c1 + c2;
+        // inclusive prefix of member counts over the 32 lanes of this half
+        int incl = cl;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const int v = __shfl_up(incl, o, 32);
+          if (r32 >= o) incl += v;
+        }
+        const int total = __shfl(incl, 32 * half + 31, 64);
+        const bool ovf = ((__ballot(v3) >> (32 * half)) & 0xFFFFFFFFull) != 0ull;
+        const int r = band_rank(u_i, total > 0 ? total : 1);
+        // the lane whose [incl - cl, incl) range holds rank r supplies the
+        // member: its (r - (incl - cl))-th in ascending index order
+        const bool hit = cl > 0 && r >= incl - cl && r < incl;
+        const int x1 = i1[i], x2 = i2[i];
+        const int lo_j = min(x1, x2), hi_j = max(x1, x2);
+        const int myj = cl == 1 ? x1 : (r - (incl - cl) == 0 ? lo_j : hi_j);
+        const unsigned long long hb = __ballot(hit) >> (32 * half);
+        const int pl = hb ? __ffsll((long long)hb) - 1 : 0;
+        const int jsel = __shfl(myj, 32 * half + pl, 64);
+        if (mine && r32 == 2 * i) {
+          const long long g = row0 + (i & 3) + 8 * (i >> 2) + 4 * half;
+          if (ovf) {
+            const int slot = atomicAdd(ovf_count, 1);
+            if (slot < ovf_cap) ovf_rows[slot] = g;
+            labels[g] = -1;
+          } else {
+            labels[g] = jsel;
+          }
+        }
+      }
+    }
+    if (blk + gridDim.x < nblk) split();
+  }
+  my_inertia = wave_sum(my_inertia);
+  if (lane == 0) part[(size_t)blockIdx.x * NW + wave] = my_inertia;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// band_rows_f64: exact fp64 re-selection of the rows the fused kernel flagged
+// (a lane held 3+ band candidates).  Driven by the device-side count (no host
+// sync); one 256-thread workgroup per row; D_j = sum_f (x_f - c_f)^2 in fp64
+// (scipy cdist's own formula, then squared) from the fp32 data and the fp32
+// centroids, all k staged in LDS, then the band rule of band.h.
+constexpr int kF64MaxK = 4096;
+__global__ void __launch_bounds__(256) band_rows_f64_kernel(
+    const float* __restrict__ X, const float* __restrict__ C, const long long* __restrict__ rows,
+    const int* __restrict__ count, int* __restrict__ labels, long long cap, int ldx, int d, int k,
+    double delta, RngKey key, long long row_offset) {
+  __shared__ double xs[256];
+  __shared__ double ds[kF64MaxK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long cnt = min((long long)*count, cap);
+  for (long long slot = blockIdx.x; slot < cnt; slot += gridDim.x) {
+    const long long r = rows[slot];
+    __syncthreads();
+    if (tid < d) xs[tid] = (double)X[(size_t)r * ldx + tid];
+    __syncthreads();
+    for (int j = wave; j < k; j += 4) {
+      const float* cr = C + (size_t)j * d;
+      double s = 0.0;
+      for (int f = lane; f < d; f += 64) {
+        const double df = xs[f] - (double)cr[f];
+        s = fma(df, df, s);
+      }
+      s = wave_sum(s);
+      if (lane == 0) ds[j] = s;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      double mn = 1e308;
+      for (int j = lane; j < k; j += 64) mn = fmin(mn, ds[j]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, 64));
+      auto dist = [&](int j) -> double { return ds[j]; };
+      const int win = band_pick_wave(dist, k, mn + delta, band_u(key, row_offset + r), lane);
+      if (lane == 0) labels[r] = win;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp16-split centroid operand from fp32 centroids (initial centres; the
+// per-iteration operand is written by centroid_finalize in kmeans.hip):
+// one workgroup per padded centroid row.
+SQ_DEV void write_f16_operand_row(_Float16* op, int j, int k, const float* c, int d, int d_pad,
+                                  float alpha, int tid, double* red) {
+  const int dch = d_pad / 8;
+  const int cpr = 2 * dch + 2;
+  _Float16* base = op + (size_t)(j >> 6) * cpr * 512 + (size_t)(j & 63) * 8;
+  auto hi_at = [&](int f) -> _Float16& { return base[(size_t)(f >> 3) * 512 + (f & 7)]; };
+  auto lo_at = [&](int f) -> _Float16& { return base[(size_t)(dch + 2 + (f >> 3)) * 512 + (f & 7)]; };
+  double nn = 0.0;
+  for (int f = tid; f < d_pad; f += 256) {
+    _Float16 h = (_Float16)0.0f, l = (_Float16)0.0f;
+    if (j < k && f < d) {
+      const float v = c[f];
+      const double a = (double)v * (double)alpha;
+      nn += a * a;
+      const float s = -2.0f * alpha * v;             // exact scaling
+      h = (_Float16)s;
+      l = (_Float16)(s - (float)h);
+    }
+    hi_at(f) = h;
+    lo_at(f) = l;
+  }
+  for (int f = d_pad + 3 + tid; f < d_pad + 16; f += 256) hi_at(f) = (_Float16)0.0f;
+  nn = wave_sum(nn);
+  if ((tid & 63) == 0) red[tid >> 6] = nn;
+  __syncthreads();
+  if (tid == 0) {
+    if (j >= k) {
+      // padding centroids: a norm above every real scaled distance
+      hi_at(d_pad) = hi_at(d_pad + 1) = hi_at(d_pad + 2) = (_Float16)65504.0f;
+    } else {
+      const float t = (float)(red[0] + red[1] + red[2] + red[3]);
+      const _Float16 hi = (_Float16)t;
+      const float r1 = t - (float)hi;
+      const _Float16 mid = (_Float16)r1;
+      const _Float16 lo = (_Float16)(r1 - (float)mid);
+      hi_at(d_pad) = hi;
+      hi_at(d_pad + 1) = mid;
+      hi_at(d_pad + 2) = lo;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) centers_f16_operand_kernel(const float* __restrict__ Cm,
+                                                                  _Float16* __restrict__ op,
+                                                                  int k, int d, int d_pad,
+                                                                  float alpha) {
+  __shared__ double red[4];
+  const int j = blockIdx.x;
+  write_f16_operand_row(op, j, k, Cm + (size_t)(j < k ? j : 0) * d, d, d_pad, alpha, threadIdx.x,
+                        red);
+}
+
+}  // namespace sq
+
+using namespace sq;
+
+extern "C" int sq_sum_partials(const void* part, int n, void* out, void* stream);
+
+template <int KSD>
+static int launch_estep_f32(const void* X, const void* C, const void* xn, void* labels, void* mind,
+                            void* ovf_rows, void* ovf_count, void* part, int part_cap,
+                            void* inertia, long long n, int k_pad, float alpha, float inv_a2,
+                            float delta_s, RngKey key, long long row_offset, int ovf_cap,
+                            hipStream_t st) {
+  constexpr int NW = 4;
+  const size_t lds = 2 * (size_t)((2 * KSD + 1) * 2048);
+  auto kern = estep_f32_kernel<KSD>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NW * 64, lds);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const long long nblk = (n + NW * 32 - 1) / (NW * 32);
+  unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
+  if ((long long)grid * NW > part_cap) grid = (unsigned)(part_cap / NW);
+  if (grid == 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const float*)X,
+                     (const _Float16*)C, (const float*)xn, (int*)labels, (float*)mind,
+                     (long long*)ovf_rows, (int*)ovf_count, (double*)part, n, k_pad, alpha, inv_a2,
+                     delta_s, key, row_offset, ovf_cap);
+  // per-wave inertia partials summed in a fixed order (bit-reproducible)
+  return sq_sum_partials(part, (int)grid * NW, inertia, st);
+}
+
+extern "C" {
+
+// X: fp32 [n][d_pad] (zero-padded), C: fp16-split operand (see
+// centers_f16_operand_kernel), alpha: power of two, delta in data units.
+int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, void* mind,
+                 void* ovf_rows, void* ovf_count, void* part, int part_cap, void* inertia,
+                 long long n, int d_pad, int k_pad, double alpha, double delta, unsigned k0,
+                 unsigned k1, unsigned s0, unsigned s1, long long row_offset, int ovf_cap,
+                 void* stream) {
+  if (n <= 0) return 0;
+  if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 32768 || part_cap < 4)
+    return (int)hipErrorInvalidValue;
+  const double a2 = alpha * alpha;
+  if (!(alpha > 0.0) || frexp(alpha, nullptr) != 0.5) return (int)hipErrorInvalidValue;  // 2^e
+  RngKey key{k0, k1, s0, s1};
+  hipStream_t st = (hipStream_t)stream;
+  const float fa = (float)alpha, ia2 = (float)(1.0 / a2), ds = (float)(delta * a2);
+  int rc;
+  switch (d_pad) {
+#define CASE(KSD)                                                                                \
+  case KSD * 16:                                                                                 \
+    rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, ovf_count, part, part_cap,      \
+                               inertia, n, k_pad, fa, ia2, ds, key, row_offset, ovf_cap, st);    \
+    break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  return rc;
+}
+
+int sq_band_rows_f64(const void* X, const void* C, const void* rows, const void* count,
+                     void* labels, long long cap, int ldx, int d, int k, double delta, unsigned k0,
+                     unsigned k1, unsigned s0, unsigned s1, long long row_offset, void* stream) {
+  if (cap <= 0) return 0;
+  if (d > 256 || k > kF64MaxK || ldx < d) return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(cap < 2048 ? cap : 2048)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)X, (const float*)C,
+                     (const long long*)rows, (const int*)count, (int*)labels, cap, ldx, d, k,
+                     delta, key, row_offset);
+  return (int)hipGetLastError();
+}
+
+int sq_centers_f16_operand(const void* Cm, void* op, int k, int d, int d_pad, int k_pad,
+                           double alpha, void* stream) {
+  if (k_pad % kTileN != 0 || d_pad % 16 != 0 || d > d_pad) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(centers_f16_operand_kernel, dim3((unsigned)k_pad), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)Cm, (_Float16*)op, k, d, d_pad,
+                     (float)alpha);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -26,6 +26,7 @@
 //              (Utility.py:697-737) - median-of-Q Fejer AE per (row, centroid).
 #include "common.h"
 #include "fejer.h"
+#include "band.h"
 
 namespace sq {
 
@@ -52,64 +53,7 @@ SQ_DEV float med3_raw(float a, float b, float c) {
   return r;
 }
 
-SQ_DEV uint32_t band_key(const RngKey& key, long long grow, uint32_t j) {
-  unsigned long long idx = ((unsigned long long)grow << 16) | (unsigned long long)j;
-  return key.block(idx).x;
-}
-
-// ---------------------------------------------------------------------------
-// delta-band selection rule (shared by every kernel and the torch twin
-// ops/kmeans.py band_select_torch):  members M = {j : D_j <= min + delta},
-// c = |M|, ordered by kappa(j) = (j mod 32, j div 32); the label is the
-// member of rank r = floor(u * c), u = u01(word g of key) - ONE Philox word
-// per row (not per member), so the band resolution costs a few wave ops.
-SQ_DEV float band_u(const RngKey& key, long long grow) {
-  return u01(key.word((unsigned long long)grow));
-}
-SQ_DEV int band_rank(float u, int c) {
-  int r = (int)(u * (float)c);
-  return r < c ? r : c - 1;
-}
-// position of the (r+1)-th set bit of m (r < popcount(m))
-SQ_DEV int nth_set_bit(unsigned long long m, int r) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w > 0; w >>= 1) {
-    const unsigned long long lo = m & ((1ull << w) - 1ull);
-    const int c = __popcll(lo);
-    if (r >= c) { r -= c; m >>= w; pos += w; } else { m = lo; }
-  }
-  return pos;
-}
-// One wave picks the band member of rank r for one row; lanes scan
-// j = lane + 64 t.  dist(j) must be a pure function (called in two passes).
-template <typename DistF>
-SQ_DEV int band_pick_wave(DistF dist, int k, float thr, float u, int lane) {
-  int c = 0;
-  for (int j = lane; j < k; j += 64) c += dist(j) <= thr ? 1 : 0;
-  const int cr = c + __shfl_xor(c, 32, 64);          // count of class rho = lane & 31
-  int incl = cr;
-#pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    const int v = __shfl_up(incl, o, 32);
-    if ((lane & 31) >= o) incl += v;
-  }
-  const int total = __shfl(incl, 31, 64);
-  if (total == 0) return -1;
-  const int r = band_rank(u, total);
-  const unsigned long long hit = __ballot(lane < 32 && incl > r);
-  const int rho = __ffsll((long long)hit) - 1;
-  int rr = r - __shfl(incl - cr, rho, 64);
-  for (int base = 0;; base += 64) {                  // members of class rho in j order
-    const int j = rho + 32 * (base + lane);
-    const bool mem = j < k && dist(j) <= thr;
-    const unsigned long long b = __ballot(mem);
-    const int cnt = __popcll(b);
-    if (rr < cnt) return rho + 32 * (base + nth_set_bit(b, rr));
-    rr -= cnt;
-    if (rho + 32 * base >= k) return -1;             // unreachable for a consistent dist
-  }
-}
+// delta-band rule helpers (band_key, band_u, band_pick_wave, ...): band.h
 
 // Centroid operand layout (written by centroid_finalize / centers_to_bf16):
 // per 64-centroid tile, CPR = (d_pad + 16) / 8 chunks of 16 B, chunk-major:
@@ -1220,30 +1164,49 @@ __global__ void __launch_bounds__(256) pack_stats_kernel(
 }
 
 // one workgroup per (padded) centroid row
+// C_bf16 (bf16 E-step operand) and/or C_f16 (fp16 hi/lo operand of the
+// fp32-faithful E-step, csrc/estep_f32.hip, scale alpha) may be null.
 __global__ void __launch_bounds__(256) centroid_finalize_kernel(
     const double* __restrict__ packed, const float* __restrict__ C_old, float* __restrict__ C_new,
     uint16_t* __restrict__ C_bf16, float* __restrict__ cn, double* __restrict__ shift, int k, int d,
-    int d_pad, float b, float erf_b, RngKey key, int empty_policy) {
+    int d_pad, float b, float erf_b, RngKey key, int empty_policy, _Float16* __restrict__ C_f16,
+    float alpha) {
   const int j = blockIdx.x;
   const int tid = threadIdx.x;
   __shared__ double red[4];
   __shared__ float redf[4];
+  __shared__ double redn[4];
+  // fp16 operand: per 64-centroid tile [hi chunks: d_pad/8 + 2][lo chunks: d_pad/8]
+  const int dch = d_pad / 8;
+  _Float16* Cf = C_f16 ? C_f16 + (size_t)(j >> 6) * (2 * dch + 2) * 512 + (size_t)(j & 63) * 8
+                       : nullptr;
+  auto hi16 = [&](int c) -> _Float16& { return Cf[(size_t)(c >> 3) * 512 + (c & 7)]; };
+  auto lo16 = [&](int c) -> _Float16& { return Cf[(size_t)(dch + 2 + (c >> 3)) * 512 + (c & 7)]; };
   // chunk-major E-step operand (see estep_kernel): -2 c, then [hi, mid, lo]
   // of ||bf16(c)||^2 in the augmented chunk, zeros after
   const int cpr = d_pad / 8 + 2;
   uint16_t* Cb = C_bf16 + (size_t)(j >> 6) * cpr * 512 + (size_t)(j & 63) * 8;
   auto at = [&](int c) -> uint16_t& { return Cb[(size_t)(c >> 3) * 512 + (c & 7)]; };
   if (j >= k) {
-    for (int c = tid; c < d_pad + 16; c += 256) at(c) = 0;
+    if (C_bf16) for (int c = tid; c < d_pad + 16; c += 256) at(c) = 0;
+    if (Cf) {
+      for (int c = tid; c < d_pad + 16; c += 256) hi16(c) = (_Float16)0.0f;
+      for (int c = tid; c < d_pad; c += 256) lo16(c) = (_Float16)0.0f;
+    }
     __syncthreads();
-    if (tid == 0) { at(d_pad) = f32_to_bf16_rne(kBig); cn[j] = kBig; }
+    if (tid == 0) {
+      if (C_bf16) at(d_pad) = f32_to_bf16_rne(kBig);
+      if (Cf) hi16(d_pad) = hi16(d_pad + 1) = hi16(d_pad + 2) = (_Float16)65504.0f;
+      cn[j] = kBig;
+    }
     return;
   }
   const double cntv = packed[(size_t)k * d + j];
-  double sh = 0.0;
+  double sh = 0.0, nn64 = 0.0;
   float nn = 0.0f;
   for (int c = tid; c < d_pad; c += 256) {
     uint16_t hb = 0;
+    _Float16 fh = (_Float16)0.0f, fl = (_Float16)0.0f;
     if (c < d) {
       float old = C_old[(size_t)j * d + c];
       float v;
@@ -1257,25 +1220,45 @@ __global__ void __launch_bounds__(256) centroid_finalize_kernel(
       float hv = bf16_to_f32(h);
       nn += hv * hv;
       hb = f32_to_bf16_rne(-2.0f * hv);   // exact: scaling by -2
+      const double av = (double)v * (double)alpha;
+      nn64 += av * av;
+      const float sv = -2.0f * alpha * v;  // exact: power-of-two scaling
+      fh = (_Float16)sv;
+      fl = (_Float16)(sv - (float)fh);
     }
-    at(c) = hb;
+    if (C_bf16) at(c) = hb;
+    if (Cf) { hi16(c) = fh; lo16(c) = fl; }
   }
-  for (int c = d_pad + 3 + tid; c < d_pad + 16; c += 256) at(c) = 0;
+  if (C_bf16) for (int c = d_pad + 3 + tid; c < d_pad + 16; c += 256) at(c) = 0;
+  if (Cf) for (int c = d_pad + 3 + tid; c < d_pad + 16; c += 256) hi16(c) = (_Float16)0.0f;
   sh = wave_sum(sh);
   nn = wave_sum(nn);
-  if ((tid & 63) == 0) { red[tid >> 6] = sh; redf[tid >> 6] = nn; }
+  nn64 = wave_sum(nn64);
+  if ((tid & 63) == 0) { red[tid >> 6] = sh; redf[tid >> 6] = nn; redn[tid >> 6] = nn64; }
   __syncthreads();
   if (tid == 0) {
     shift[j] = red[0] + red[1] + red[2] + red[3];   // per-centroid part (fixed-order sum)
     float t = redf[0] + redf[1] + redf[2] + redf[3];
     cn[j] = t;
-    uint16_t hi = f32_to_bf16_rne(t);
-    float r1 = t - bf16_to_f32(hi);
-    uint16_t mid = f32_to_bf16_rne(r1);
-    uint16_t lo = f32_to_bf16_rne(r1 - bf16_to_f32(mid));
-    at(d_pad) = hi;
-    at(d_pad + 1) = mid;
-    at(d_pad + 2) = lo;
+    if (C_bf16) {
+      uint16_t hi = f32_to_bf16_rne(t);
+      float r1 = t - bf16_to_f32(hi);
+      uint16_t mid = f32_to_bf16_rne(r1);
+      uint16_t lo = f32_to_bf16_rne(r1 - bf16_to_f32(mid));
+      at(d_pad) = hi;
+      at(d_pad + 1) = mid;
+      at(d_pad + 2) = lo;
+    }
+    if (Cf) {
+      // 3-way fp16 split of alpha^2 ||c||^2 (same as centers_f16_operand)
+      const float tn = (float)(redn[0] + redn[1] + redn[2] + redn[3]);
+      const _Float16 hi = (_Float16)tn;
+      const float r1 = tn - (float)hi;
+      const _Float16 mid = (_Float16)r1;
+      hi16(d_pad) = hi;
+      hi16(d_pad + 1) = mid;
+      hi16(d_pad + 2) = (_Float16)(r1 - (float)mid);
+    }
   }
 }
 
@@ -1637,7 +1620,8 @@ int sq_sum_partials(const void* part, int n, void* out, void* stream) {
 int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* shift_part, void* cn, void* shift, int k, int d, int k_pad,
                          double noise_b, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
-                         int empty_policy, void* scalars, void* ovf_count, void* stream) {
+                         int empty_policy, void* scalars, void* ovf_count, void* C_f16,
+                         double alpha, void* stream) {
   if (!shift_part) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   float b = (float)noise_b;
@@ -1646,7 +1630,7 @@ int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, voi
   hipLaunchKernelGGL(centroid_finalize_kernel, dim3((unsigned)k_pad), dim3(256), 0,
                      (hipStream_t)stream, (const double*)packed, (const float*)C_old,
                      (float*)C_new, (uint16_t*)C_bf16, (float*)cn, (double*)shift_part, k, d,
-                     d_pad, b, eb, key, empty_policy);
+                     d_pad, b, eb, key, empty_policy, (_Float16*)C_f16, (float)alpha);
   if (scalars)
     hipLaunchKernelGGL(iter_scalars_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
                        (const double*)shift_part, k, (double*)shift,

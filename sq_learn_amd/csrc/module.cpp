@@ -62,7 +62,17 @@ __attribute__((weak)) int sq_centroid_reduce(const void*, int, const void*, cons
 __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
                          unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
-                         void* scalars, void* ovf_count, void* stream);
+                         void* scalars, void* ovf_count, void* C_f16, double alpha, void* stream);
+// estep_f32.hip
+__attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, void*, void*, void*,
+                                       void*, void*, int, void*, long long, int, int, double,
+                                       double, unsigned, unsigned, unsigned, unsigned, long long,
+                                       int, void*);
+__attribute__((weak)) int sq_band_rows_f64(const void*, const void*, const void*, const void*,
+                                           void*, long long, int, int, int, double, unsigned,
+                                           unsigned, unsigned, unsigned, long long, void*);
+__attribute__((weak)) int sq_centers_f16_operand(const void*, void*, int, int, int, int, double,
+                                                 void*);
 __attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia,
                                         void* packed, int k, int d, int xexp, int wexp, void*);
 __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void* cn, void* labels, void* mind,
@@ -240,14 +250,44 @@ static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
-  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, st; int k, d, kpad, pol; double nb;
-  unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
-                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &st))
+  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, cf, st; int k, d, kpad, pol; double nb;
+  double alpha; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKKdK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
+                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &cf, &alpha, &st))
     return nullptr;
   CHECK(sq_centroid_finalize)
   return ret(sq_centroid_finalize(P(pk), P(co), P(cnw), P(cb), P(clo), P(cn), P(sh), k, d, kpad, nb,
-                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(st)));
+                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(cf), alpha, P(st)));
+}
+
+static PyObject* py_estep_f32(PyObject*, PyObject* a) {
+  unsigned long long X, C, xn, lab, mind, ovr, ovc, part, inr, st; int pcap, dp, kp, cap;
+  long long n, roff; double alpha, delta; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKKiKLiiddIIIILiK", &X, &C, &xn, &lab, &mind, &ovr, &ovc, &part,
+                        &pcap, &inr, &n, &dp, &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &cap,
+                        &st))
+    return nullptr;
+  CHECK(sq_estep_f32)
+  return ret(sq_estep_f32(P(X), P(C), P(xn), P(lab), P(mind), P(ovr), P(ovc), P(part), pcap, P(inr),
+                          n, dp, kp, alpha, delta, k0, k1, s0, s1, roff, cap, P(st)));
+}
+
+static PyObject* py_band_rows_f64(PyObject*, PyObject* a) {
+  unsigned long long X, C, rows, cnt, lab, st; long long cap, roff; int ldx, d, k; double delta;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKLiiidIIIILK", &X, &C, &rows, &cnt, &lab, &cap, &ldx, &d, &k,
+                        &delta, &k0, &k1, &s0, &s1, &roff, &st))
+    return nullptr;
+  CHECK(sq_band_rows_f64)
+  return ret(sq_band_rows_f64(P(X), P(C), P(rows), P(cnt), P(lab), cap, ldx, d, k, delta, k0, k1,
+                              s0, s1, roff, P(st)));
+}
+
+static PyObject* py_centers_f16_operand(PyObject*, PyObject* a) {
+  unsigned long long Cm, op, st; int k, d, dp, kp; double alpha;
+  if (!PyArg_ParseTuple(a, "KKiiiidK", &Cm, &op, &k, &d, &dp, &kp, &alpha, &st)) return nullptr;
+  CHECK(sq_centers_f16_operand)
+  return ret(sq_centers_f16_operand(P(Cm), P(op), k, d, dp, kp, alpha, P(st)));
 }
 
 static PyObject* py_pack_stats(PyObject*, PyObject* a) {
@@ -333,6 +373,9 @@ static PyMethodDef methods[] = {
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},
+    {"estep_f32", py_estep_f32, METH_VARARGS, "fp32-faithful fused E-step (fp16 hi/lo MFMA)"},
+    {"band_rows_f64", py_band_rows_f64, METH_VARARGS, "fp64 re-selection of overflow rows"},
+    {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},
     {"ipe_estep", py_ipe_estep, METH_VARARGS, "IPE-noised distance argmin"},
     {"gram", py_gram, METH_VARARGS, "G += (X-mean)^T (X-mean)"},

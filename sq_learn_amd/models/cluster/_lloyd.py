@@ -13,14 +13,18 @@ the reference's quantum Lloyd loop (``_dmeans.py:534-671``):
                (intermediate_error) tomography with error delta/2
     loop     best-inertia iterate, Frobenius shift <= tol, final E-step
 
-GPU fast path (d <= 256, gemm_precision 'bf16', no IPE): per iteration
-    estep_bf16 (MFMA distance GEMM + band epilogue + inertia)
-    -> band_select_rows (overflow rows, device-driven)
+GPU fast path (d <= 256, no IPE): per iteration
+    E-step   gemm_precision 'fp32' (default): estep_f32 - fp32-faithful fused
+               MFMA distances from an fp16 hi/lo split (csrc/estep_f32.hip) +
+               band epilogue + inertia -> band_rows_f64 (overflow rows, fp64,
+               device-driven);
+             gemm_precision 'bf16': estep_bf16 (bf16 operands, faster, the
+               band edge is only bf16-accurate) -> band_select_rows
     -> centroid_accumulate (segmented reduce) -> pack_stats (one fp64 bucket)
     -> all_reduce over RCCL (C1: the only collective of the iteration)
     -> centroid_finalize (mean + fused truncated-normal tomography noise +
        shift + bf16 centroids and norms for the next E-step).
-Everything else (CPU tensors, IPE distances, fp32 precision, d > 256) runs
+Everything else (CPU tensors, IPE distances, d > 256, k > 4096) runs
 the generic path: library GEMM distance tiles + selection kernels/torch.
 """
 
@@ -41,7 +45,7 @@ from ...utils import tracing
 class LloydEngine:
     def __init__(self, X, k, *, delta=0.0, true_distance_estimate=False, intermediate_error=False,
                  true_tomography=False, tomography_kw=None, sample_weight=None, seed=0,
-                 comm=None, row_offset=0, gemm_precision="bf16", ipe_Q=13, empty_policy=0,
+                 comm=None, row_offset=0, gemm_precision="fp32", ipe_Q=13, empty_policy=0,
                  Xb=None, xn=None, failure_prob=0.0, failure_attempts=1):
         self.X = X
         self.device = X.device
@@ -67,8 +71,11 @@ class LloydEngine:
         # [estimations made, corrupted rows] over the engine's lifetime (device)
         self.failure_counters = torch.zeros(2, dtype=torch.int64, device=X.device)
         gpu = self.device.type == "cuda"
-        self.fast = (gpu and gemm_precision == "bf16" and not self.ipe and self.d_pad <= 256
-                     and self.k_pad <= 4096)
+        if gemm_precision not in ("bf16", "fp32"):
+            raise ValueError("gemm_precision must be 'bf16' or 'fp32', got %r" % (gemm_precision,))
+        self.precision = gemm_precision
+        self.fast = (gpu and not self.ipe and self.d_pad <= 256 and self.k_pad <= 4096)
+        self.alpha = 1.0
         self.acc_dtype = torch.float64 if not gpu else torch.float32
         if gpu:
             nat.native()  # fail loudly if the HIP layer is unavailable on a GPU box
@@ -80,6 +87,8 @@ class LloydEngine:
     # ------------------------------------------------------------ prep
     def _prepare_fast(self, Xb, xn):
         dev = self.device
+        if self.precision == "fp32":
+            return self._prepare_fast_f32(xn)
         if Xb is None:
             if self.X.dtype == torch.bfloat16 and self.d == self.d_pad and self.X.is_contiguous():
                 Xb = self.X
@@ -94,6 +103,37 @@ class LloydEngine:
             self.Xm = self.X.contiguous()
         else:
             self.Xm = Xb
+        self.C_bf16 = torch.zeros(K.operand_shape(self.k_pad, self.d_pad), dtype=torch.bfloat16,
+                                  device=dev)
+        self.C_op = None
+        self._prepare_reduce()
+
+    def _prepare_fast_f32(self, xn):
+        """fp32-faithful path: fp32 rows (zero-padded to d_pad only when
+        needed) feed both the E-step (split to fp16 hi/lo in registers) and
+        the M-step; alpha from the largest row norm over all ranks."""
+        dev = self.device
+        X = self.X
+        if X.dtype == torch.float32 and self.d == self.d_pad and X.is_contiguous():
+            Xf = X
+        else:
+            Xf = torch.zeros((self.n, self.d_pad), dtype=torch.float32, device=dev)
+            Xf[:, :self.d] = X.to(torch.float32)
+        self.Xf32 = Xf
+        self.xn = (xn.float().contiguous() if xn is not None else L.row_norms_sq(Xf))
+        mx = (self.xn.max() if self.n else torch.zeros((), device=dev)).double().reshape(1)
+        self.comm.all_reduce_(mx, op="max")
+        # a centroid is a mean of rows plus at most delta/2 of tomography error
+        margin = self.delta + self._noise_bound() * math.sqrt(self.k * self.d)
+        self.alpha = K.choose_alpha(float(mx.item()), margin)
+        self.Xm = Xf
+        self.C_bf16 = None
+        self.C_op = torch.zeros(K.operand_f16_shape(self.k_pad, self.d_pad), dtype=torch.float16,
+                                device=dev)
+        self._prepare_reduce()
+
+    def _prepare_reduce(self):
+        dev = self.device
         self.dm = self.Xm.shape[1]
         self.buf = K.EStepBuffers(self.n, dev)
         # deterministic fixed-point reduction: one global quantum for all ranks
@@ -113,7 +153,6 @@ class LloydEngine:
         self.shift_part = torch.zeros(self.k, dtype=torch.float64, device=dev)
         self.C = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
         self.C_new = torch.zeros_like(self.C)
-        self.C_bf16 = torch.zeros(K.operand_shape(self.k_pad, self.d_pad), dtype=torch.bfloat16, device=dev)
         self.cn = torch.full((self.k_pad,), K.BIG, dtype=torch.float32, device=dev)
         self.scalars = torch.zeros(3, dtype=torch.float64, device=dev)
         self.weights = (self.sample_weight.to(torch.float32).contiguous()
@@ -137,6 +176,10 @@ class LloydEngine:
         C = C.to(self.device)
         if self.fast:
             self.C.copy_(C.to(torch.float32))
+            if self.C_op is not None:
+                K.centers_to_f16_native(self.C, self.C_op, self.k, self.d, self.d_pad, self.k_pad,
+                                        self.alpha)
+                return
             Cb, cn = K.centers_to_bf16(self.C, self.k_pad, self.d_pad)
             self.C_bf16.copy_(Cb)
             self.cn.copy_(cn)
@@ -149,10 +192,16 @@ class LloydEngine:
     def checkpoint_tensors(self):
         """Derived device state that must round-trip bit-exactly on resume
         (the E-step operand written by ``centroid_finalize``)."""
-        return {"C_bf16": self.C_bf16, "cn": self.cn} if self.fast else {}
+        if not self.fast:
+            return {}
+        if self.C_op is not None:
+            return {"C_op": self.C_op}
+        return {"C_bf16": self.C_bf16, "cn": self.cn}
 
     def restore_tensors(self, d):
-        if self.fast and "C_bf16" in d:
+        if self.fast and self.C_op is not None and "C_op" in d:
+            self.C_op.copy_(d["C_op"].to(self.device))
+        elif self.fast and self.C_op is None and "C_bf16" in d:
             self.C_bf16.copy_(d["C_bf16"].to(self.device))
             self.cn.copy_(d["cn"].to(self.device))
 
@@ -163,6 +212,12 @@ class LloydEngine:
         if C is not None:
             self.set_centers(C)
         key = self._key("band_select")
+        if self.fast and self.C_op is not None:
+            with tracing.range("estep_f32"):
+                lab, mind = K.estep_f32_native(self.Xf32, self.C_op, self.xn, self.C, self.k,
+                                               self.delta, self.alpha, key, self.row_offset,
+                                               self.buf)
+            return lab, mind, self.buf.inertia
         if self.fast:
             with tracing.range("estep_bf16"):
                 lab, mind = K.estep_native(self.Xb, self.C_bf16, self.cn, self.xn, self.k,
@@ -240,7 +295,8 @@ class LloydEngine:
                                            self.shift, self.k, self.d, self._noise_bound(),
                                            noise_key, self.empty_policy,
                                            shift_part=self.shift_part, scalars=self.scalars,
-                                           buf=self.buf)
+                                           buf=self.buf, C_f16=self.C_op, alpha=self.alpha,
+                                           k_pad=self.k_pad)
                 self.C, self.C_new = self.C_new, self.C
                 if self.intermediate_error and self.true_tomography and self.delta > 0:
                     self._true_tomography_centers()

@@ -297,23 +297,26 @@ def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, 
 
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
-                             empty_policy=0, shift_part=None, scalars=None, buf=None):
+                             empty_policy=0, shift_part=None, scalars=None, buf=None, C_f16=None,
+                             alpha=1.0, k_pad=None):
     """shift[0] = sum_j ||c_j' - c_j||^2 (per-centroid parts summed in a fixed
     order: deterministic); ``shift_part`` is a k-double workspace.
 
     With ``scalars`` (3 doubles) the same launch also writes the iteration's
     [inertia, shift, overflow rows] (inertia from the packed bucket, overflow
     count from ``buf``, an :class:`EStepBuffers`, whose counter it resets)."""
-    k_pad = C_bf16.shape[0] * 64
+    if k_pad is None:
+        k_pad = (C_bf16 if C_bf16 is not None else C_f16).shape[0] * 64
     if shift_part is None:
         shift_part = torch.empty(max(k, 1), dtype=torch.float64, device=packed.device)
     assert shift_part.numel() >= k and shift_part.dtype == torch.float64
     nat.native().centroid_finalize(packed.data_ptr(), C_old.data_ptr(), C_new.data_ptr(),
-                                   C_bf16.data_ptr(), shift_part.data_ptr(), cn.data_ptr(),
+                                   nat.ptr(C_bf16), shift_part.data_ptr(), cn.data_ptr(),
                                    shift.data_ptr(), k, d, k_pad, float(noise_b), key.k0, key.k1,
                                    key.s0, key.s1, int(empty_policy),
                                    0 if scalars is None else scalars.data_ptr(),
                                    0 if buf is None else buf.ovf_count.data_ptr(),
+                                   nat.ptr(C_f16), float(alpha),
                                    nat.stream_handle(packed.device))
     if scalars is not None and buf is not None:
         buf.ovf_clean = True
@@ -379,3 +382,97 @@ def centroid_sums_torch(X, labels, k, weights=None, acc_dtype=torch.float64):
         sums.index_add_(0, lab, X.to(acc_dtype) * weights.to(acc_dtype)[:, None])
         counts.index_add_(0, lab, weights.to(torch.float64))
     return sums, counts
+
+
+# ------------------------------------------------- fp32-faithful E-step
+# (csrc/estep_f32.hip): fp16 hi/lo split operands, 3 MFMA products, fp32
+# accumulation; overflow rows re-selected in fp64.
+
+def operand_f16_shape(k_pad, d_pad):
+    """[tile][hi chunks d_pad/8 + 2 | lo chunks d_pad/8][centroid in tile][8 fp16]."""
+    return (k_pad // 64, 2 * (d_pad // 8) + 2, 64, 8)
+
+
+ALPHA_TARGET_LOG2 = 13   # alpha^2 * (max row norm)^2 <= 2^13 keeps fp16 pieces in range
+
+
+def choose_alpha(max_sq_norm, margin=0.0):
+    """Power-of-two scale of the fp16 split: alpha^2 (R + margin)^2 <= 2^13
+    with R^2 the largest squared row norm (all ranks) and ``margin`` the
+    largest norm any centroid can add on top of a mean (tomography noise)."""
+    r = math.sqrt(max(float(max_sq_norm), 0.0)) + float(margin)
+    if not math.isfinite(r):
+        raise ValueError("non-finite values in the data")
+    if r <= 0.0:
+        return 1.0
+    e = math.floor(ALPHA_TARGET_LOG2 / 2.0 - math.log2(r))
+    return float(2.0 ** max(min(e, 60), -60))
+
+
+def _split3_f16(t):
+    hi = t.to(torch.float16)
+    r = t - hi.float()
+    mid = r.to(torch.float16)
+    lo = (r - mid.float()).to(torch.float16)
+    return hi, mid, lo
+
+
+def centers_to_f16(C, k_pad, d_pad, alpha):
+    """fp16 hi/lo operand of fp32 centroids C [k, d] (torch twin of
+    ``centers_f16_operand_kernel``): hi/lo of -2 alpha c chunk-major, the
+    3-way split of alpha^2 ||c||^2 (fp64 sum) in the augmented chunk, 65504
+    norms on padding centroids."""
+    k, d = C.shape
+    Cf = C.float()
+    s = (-2.0 * alpha) * Cf
+    hi = s.to(torch.float16)
+    lo = (s - hi.float()).to(torch.float16)
+    H = torch.zeros((k_pad, d_pad + 16), dtype=torch.float16, device=C.device)
+    Lo = torch.zeros((k_pad, d_pad), dtype=torch.float16, device=C.device)
+    H[:k, :d] = hi
+    Lo[:k, :d] = lo
+    nn = ((Cf.double() * alpha) ** 2).sum(1).float()
+    a, b, c = _split3_f16(nn)
+    H[:k, d_pad], H[:k, d_pad + 1], H[:k, d_pad + 2] = a, b, c
+    H[k:, d_pad:d_pad + 3] = 65504.0
+    nt = k_pad // 64
+    Hc = H.view(nt, 64, d_pad // 8 + 2, 8).permute(0, 2, 1, 3)
+    Lc = Lo.view(nt, 64, d_pad // 8, 8).permute(0, 2, 1, 3)
+    return torch.cat([Hc, Lc], dim=1).contiguous()
+
+
+def centers_to_f16_native(C, op, k, d, d_pad, k_pad, alpha):
+    C = C.float().contiguous()
+    assert tuple(op.shape) == operand_f16_shape(k_pad, d_pad) and op.dtype == torch.float16
+    nat.native().centers_f16_operand(C.data_ptr(), op.data_ptr(), k, d, d_pad, k_pad, float(alpha),
+                                     nat.stream_handle(C.device))
+    return op
+
+
+def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_offset,
+                     buf: EStepBuffers, stream=None):
+    """fp32-faithful fused E-step (labels, min distances; inertia in
+    ``buf.inertia``) + fp64 re-selection of overflow rows; no host sync."""
+    n, d_pad = Xf.shape
+    k_pad = C_op.shape[0] * 64
+    d = C_master.shape[1]
+    assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in FAST_D
+    assert C_op.dtype == torch.float16 and tuple(C_op.shape) == operand_f16_shape(k_pad, d_pad)
+    assert C_op.is_contiguous() and C_master.dtype == torch.float32 and C_master.is_contiguous()
+    assert C_master.shape[0] >= k and k <= k_pad and d <= d_pad
+    assert xn.dtype == torch.float32 and xn.numel() >= n
+    assert buf.labels.numel() >= n and buf.part_cap >= 4
+    st = stream if stream is not None else nat.stream_handle(Xf.device)
+    m = nat.native()
+    if not buf.ovf_clean:
+        buf.ovf_count.zero_()
+    buf.ovf_clean = False
+    rc = m.estep_f32(Xf.data_ptr(), C_op.data_ptr(), xn.data_ptr(), buf.labels.data_ptr(),
+                     buf.mind.data_ptr(), buf.ovf_rows.data_ptr(), buf.ovf_count.data_ptr(),
+                     buf.inertia_part.data_ptr(), int(buf.part_cap), buf.inertia.data_ptr(), n,
+                     d_pad, k_pad, float(alpha), float(delta), key.k0, key.k1, key.s0, key.s1,
+                     int(row_offset), buf.ovf_cap, st)
+    m.band_rows_f64(Xf.data_ptr(), C_master.data_ptr(), buf.ovf_rows.data_ptr(),
+                    buf.ovf_count.data_ptr(), buf.labels.data_ptr(), buf.ovf_cap, d_pad, d, k,
+                    float(delta), key.k0, key.k1, key.s0, key.s1, int(row_offset), st)
+    return buf.labels, buf.mind

@@ -1,0 +1,164 @@
+"""Reference-precision E-step (csrc/estep_f32.hip) against fp64 distances.
+
+The reference draws the delta-band from fp64 ``cdist(X, C)**2``
+(``sklearn/cluster/_dmeans.py:736-751``).  These tests run the fused GPU
+E-step on UNROUNDED fp32 data at |D'| ~ 1e3 .. 3e4 (d = 256, k = 1024,
+delta = 0.5, mean band size ~3.2 - dense band edges) and require the label of
+every row to be exactly the fp64 rule's label (same Philox uniform, same
+kappa order: ops/kmeans.py ``band_select_torch`` on fp64 distances), except
+at rows where some fp64 distance lies within the documented error bound of
+the band edge:
+
+    |D~_ij - D_ij| <= beta_i = 2^-18 (||x_i||^2 + max_j ||c_j||^2)
+
+(an fp32 GEMM's accumulation error is ~2^-24 sqrt(K) of the partial sums, i.e.
+~2^-20 of that magnitude; beta is 4x that).  The bf16 kernel fails the same
+test (the band is only bf16-accurate) - asserted too, so the test has teeth.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from sq_learn_amd.models.cluster._lloyd import LloydEngine  # noqa: E402
+from sq_learn_amd.ops import kmeans as K  # noqa: E402
+
+
+def _dense_data(n, d, k, off, seed=0, groups=32, s=0.05):
+    rs = np.random.RandomState(seed)
+    G = rs.randn(groups, d)
+    C = G[np.arange(k) % groups] + s * rs.randn(k, d)
+    X = G[rs.randint(groups, size=n)] + 0.5 * rs.randn(n, d)
+    shift = off * rs.randn(d)
+    return (X + shift).astype(np.float32), (C + shift).astype(np.float32)
+
+
+def _fp64_rule(X, C, delta, key, k_pad):
+    Xd = torch.from_numpy(X).double().cuda()
+    Cd = torch.from_numpy(C).double().cuda()
+    D = torch.cdist(Xd, Cd, compute_mode="donot_use_mm_for_euclid_dist") ** 2
+    g = torch.arange(X.shape[0], dtype=torch.int64, device=D.device)
+    lab, mn = K.band_select_torch(D, g, delta, key, k_pad)
+    return D, lab, mn
+
+
+def _run(X, C, delta, precision):
+    Xt = torch.from_numpy(X).cuda()
+    eng = LloydEngine(Xt, C.shape[0], delta=delta, seed=7, gemm_precision=precision)
+    eng.set_centers(torch.from_numpy(C).cuda())
+    key = eng._key("band_select")
+    lab, mind, inertia = eng.estep()
+    torch.cuda.synchronize()
+    return eng, key, lab.long()[: X.shape[0]], mind[: X.shape[0]], inertia
+
+
+def _ambiguous(D, mn, delta, X, C, mult=1.0):
+    xn = torch.from_numpy((X.astype(np.float64) ** 2).sum(1)).cuda()
+    cmax = float((C.astype(np.float64) ** 2).sum(1).max())
+    beta = mult * 2.0 ** -18 * (xn + cmax)
+    edge = mn + delta
+    near_edge = ((D - edge[:, None]).abs() <= 2 * beta[:, None]).any(1)
+    return near_edge, beta
+
+
+@pytest.mark.parametrize("off", [3.0, 12.0])
+def test_fp32_estep_matches_fp64_band_rule(off):
+    n, d, k, delta = 8192, 256, 1024, 0.5
+    X, C = _dense_data(n, d, k, off)
+    eng, key, lab, mind, inertia = _run(X, C, delta, "fp32")
+    D, lab64, mn64 = _fp64_rule(X, C, delta, key, eng.k_pad)
+    amb, beta = _ambiguous(D, mn64, delta, X, C)
+    band = (D <= (mn64 + delta)[:, None]).sum(1).double().mean().item()
+    assert band > 2.0, band            # dense band edges: a real precision test
+    ok = ~amb
+    mism = (lab != lab64) & ok
+    assert int(mism.sum()) == 0, (int(mism.sum()), int(ok.sum()))
+    assert amb.double().mean().item() < 0.10
+    # every label is a member of the fp64 band widened by the bound
+    Dl = D.gather(1, lab[:, None])[:, 0]
+    assert bool((Dl <= mn64 + delta + 2 * beta).all())
+    # min distances and inertia at fp32-faithful accuracy
+    assert bool(((mind.double() - mn64).abs() <= beta + 1e-6 * mn64).all())
+    assert abs(float(inertia) - float(mn64.sum())) <= float(beta.sum())
+
+
+def test_bf16_estep_fails_the_same_test():
+    """The bf16 kernel's band is only bf16-accurate: at |D'| ~ 1.8e3 most
+    rows differ from the fp64 rule (why 'fp32' is the default)."""
+    n, d, k, delta = 8192, 256, 1024, 0.5
+    X, C = _dense_data(n, d, k, 3.0)
+    eng, key, lab, mind, _ = _run(X, C, delta, "bf16")
+    D, lab64, mn64 = _fp64_rule(X, C, delta, key, eng.k_pad)
+    frac = (lab != lab64).double().mean().item()
+    assert frac > 0.2, frac
+
+
+def test_fp32_estep_delta0_is_exact_argmin():
+    n, d, k = 8192, 256, 1024
+    X, C = _dense_data(n, d, k, 3.0, seed=1)
+    eng, key, lab, mind, _ = _run(X, C, 0.0, "fp32")
+    D, lab64, mn64 = _fp64_rule(X, C, 0.0, key, eng.k_pad)
+    amb, _ = _ambiguous(D, mn64, 0.0, X, C)
+    bad = (lab != lab64) & ~amb
+    assert int(bad.sum()) == 0
+    assert amb.double().mean().item() < 0.02
+
+
+@pytest.mark.parametrize("n,d,k", [(3000, 100, 1000), (2049, 16, 70), (5000, 64, 256)])
+def test_fp32_estep_padded_shapes(n, d, k):
+    """d and k not multiples of the tile: zero-padded features, padding
+    centroids (65504 norm) never win."""
+    rs = np.random.RandomState(n)
+    X = (rs.randn(n, d) * 2 + 1).astype(np.float32)
+    C = X[rs.choice(n, k, replace=False)] + 0.01 * rs.randn(k, d).astype(np.float32)
+    eng, key, lab, mind, _ = _run(X, C.astype(np.float32), 0.3, "fp32")
+    D, lab64, mn64 = _fp64_rule(X, C.astype(np.float32), 0.3, key, eng.k_pad)
+    amb, _ = _ambiguous(D, mn64, 0.3, X, C)
+    assert bool((lab >= 0).all()) and bool((lab < k).all())
+    assert int(((lab != lab64) & ~amb).sum()) == 0
+
+
+def test_fp32_estep_overflow_rows_go_through_fp64():
+    """Wide band (delta = 40): most rows have lanes with 3+ members and are
+    re-selected by band_rows_f64 - exact fp64, so labels equal the rule's."""
+    n, d, k = 4096, 256, 1024
+    X, C = _dense_data(n, d, k, 3.0, seed=2)
+    eng, key, lab, _, _ = _run(X, C, 40.0, "fp32")
+    ovf = int(eng.buf.ovf_count.item())
+    assert ovf > 100
+    D, lab64, mn64 = _fp64_rule(X, C, 40.0, key, eng.k_pad)
+    amb, _ = _ambiguous(D, mn64, 40.0, X, C)
+    assert int(((lab != lab64) & ~amb).sum()) == 0
+
+
+def test_f16_operand_twin_and_finalize_agree():
+    """centers_f16_operand (device), centers_to_f16 (torch twin) and the
+    operand centroid_finalize writes after an M-step are bit-identical."""
+    rs = np.random.RandomState(3)
+    n, d, k = 4000, 96, 100
+    X = rs.randn(n, d).astype(np.float32) * 3
+    C = X[:k].copy()
+    Xt = torch.from_numpy(X).cuda()
+    eng = LloydEngine(Xt, k, delta=0.2, seed=1, gemm_precision="fp32")
+    eng.set_centers(torch.from_numpy(C).cuda())
+    twin = K.centers_to_f16(torch.from_numpy(C), eng.k_pad, eng.d_pad, eng.alpha)
+    assert torch.equal(eng.C_op.cpu().view(torch.int16), twin.view(torch.int16))
+    eng.step()
+    torch.cuda.synchronize()
+    twin2 = K.centers_to_f16(eng.C.cpu(), eng.k_pad, eng.d_pad, eng.alpha)
+    assert torch.equal(eng.C_op.cpu().view(torch.int16), twin2.view(torch.int16))
+
+
+def test_qmeans_default_precision_is_fp32_faithful():
+    from sq_learn_amd.models.cluster import QMeans
+    from sq_learn_amd._config import get_config
+    assert get_config()["gemm_precision"] == "fp32"
+    rs = np.random.RandomState(0)
+    X = np.concatenate([rs.randn(2000, 32) + 6 * i for i in range(4)]).astype(np.float32)
+    est = QMeans(n_clusters=4, delta=0.5, true_distance_estimate=False, n_init=1, max_iter=20,
+                 random_state=0, device="cuda:0").fit(X)
+    cpu = QMeans(n_clusters=4, delta=0.5, true_distance_estimate=False, n_init=1, max_iter=20,
+                 random_state=0, device="cpu").fit(X.astype(np.float64))
+    assert np.isclose(est.inertia_, cpu.inertia_, rtol=1e-4)
