@@ -495,7 +495,8 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
   if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 32768 || part_cap < 4)
     return (int)hipErrorInvalidValue;
   const double a2 = alpha * alpha;
-  if (!(alpha > 0.0) || frexp(alpha, nullptr) != 0.5) return (int)hipErrorInvalidValue;  // 2^e
+  int aexp = 0;
+  if (!(alpha > 0.0) || frexp(alpha, &aexp) != 0.5) return (int)hipErrorInvalidValue;  // 2^e
   RngKey key{k0, k1, s0, s1};
   hipStream_t st = (hipStream_t)stream;
   const float fa = (float)alpha, ia2 = (float)(1.0 / a2), ds = (float)(delta * a2);
