@@ -19,7 +19,7 @@ ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--delta", type=float, default=0.5)
 ap.add_argument("--what", default="estep", choices=["estep", "reduce", "both"])
-ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16"])
+ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16", "x64"])
 a = ap.parse_args()
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
@@ -38,11 +38,14 @@ else:
     alpha = K.choose_alpha(float(xn.max()), 1.0)
     Cop = torch.empty(K.operand_f16_shape(kp, dp), dtype=torch.float16, device=dev)
     K.centers_to_f16_native(C, Cop, a.k, a.d, dp, kp, alpha)
+    cmax2 = ((C.double() * alpha) ** 2).sum(1).max().float().reshape(1)
 
 
 def run_estep():
     if a.prec == "bf16":
         K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
+    elif a.prec == "x64":
+        K.estep_x64_native(X, Cop, C, xn, cmax2, a.k, a.delta, alpha, key, 0, buf)
     else:
         K.estep_f32_native(X, Cop, xn, C, a.k, a.delta, alpha, key, 0, buf)
 
@@ -64,4 +67,5 @@ for name in (["estep", "reduce"] if a.what == "both" else [a.what]):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / a.iters * 1e3
     fl = 2.0 * a.n * a.k * dp
-    print(f"{a.prec} {name}: {ms:.3f} ms  ({fl / ms / 1e9:.1f} TFLOP/s equiv)  ovf={int(buf.ovf_count.item())}")
+    print(f"{a.prec} {name}: {ms:.3f} ms  ({fl / ms / 1e9:.1f} TFLOP/s equiv)  "
+          f"counts(ovf,dense)={buf.counts.tolist()}")

@@ -65,7 +65,12 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ C, const float* __restrict__ xn,
     int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ ovf_rows,
     int* __restrict__ ovf_count, double* __restrict__ part, long long n, int k_pad, float alpha,
-    float inv_alpha2, float delta_s, RngKey key, long long row_offset, int ovf_cap) {
+    float inv_alpha2, float delta_s, RngKey key, long long row_offset, int ovf_cap,
+    const long long* __restrict__ rlist, const int* __restrict__ rcount) {
+  // list mode (rlist != null): the rows are rlist[0 .. *rcount) - the dense
+  // rows handed over by the certified filter kernel (estep_x64_kernel)
+  if (rlist) n = min(n, (long long)*rcount);
+  auto map_row = [&](long long r) -> long long { return rlist ? rlist[r] : r; };
   constexpr int NW = 4;
   constexpr int DX = KSD * 16;                 // fp32 row length (padded features)
   constexpr int HI_BYTES = (KSD + 1) * 2048;   // data chunks + norm chunk pair
@@ -101,7 +106,7 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
   float4 raw[KSD][2];
   auto load_raw = [&](long long b) {
     const long long r = b * ROWS + wave * 32 + r32;
-    const float* xr = X + (size_t)(r < n ? r : n - 1) * DX + half * 8;
+    const float* xr = X + (size_t)map_row(r < n ? r : n - 1) * DX + half * 8;
 #pragma unroll
     for (int ks = 0; ks < KSD; ++ks) {
       raw[ks][0] = *reinterpret_cast<const float4*>(xr + ks * 16);
@@ -281,10 +286,11 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     const bool owner = ((r32 & 1) == 0) && grow_local < n;
     const float thr = q1 + delta_s;
     const bool band2 = q2 <= thr;
+    const long long gmap = owner ? map_row(grow_local) : 0;
     if (owner) {
-      const float dist = fmaxf(xn[grow_local] + q1 * inv_alpha2, 0.0f);
-      mind[grow_local] = dist;
-      if (!band2) labels[grow_local] = qi;
+      const float dist = fmaxf(xn[gmap] + q1 * inv_alpha2, 0.0f);
+      mind[gmap] = dist;
+      if (!band2) labels[gmap] = qi;
       my_inertia += (double)dist;
     }
     // rows with >= 2 band members: the rank rule over the per-lane top-2
@@ -292,7 +298,7 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     // order is kappa order.  A lane whose 3rd value is in the band -> overflow.
     const unsigned long long slow = __ballot(owner && band2);
     if (slow) {
-      const float urow = band_u(key, row_offset + grow_local);
+      const float urow = band_u(key, row_offset + gmap);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const unsigned long long sel = slow & ((1ull << (2 * i)) | (1ull << (32 + 2 * i)));
@@ -325,7 +331,7 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         const int pl = hb ? __ffsll((long long)hb) - 1 : 0;
         const int jsel = __shfl(myj, 32 * half + pl, 64);
         if (mine && r32 == 2 * i) {
-          const long long g = row0 + (i & 3) + 8 * (i >> 2) + 4 * half;
+          const long long g = gmap;
           if (ovf) {
             const int slot = atomicAdd(ovf_count, 1);
             if (slot < ovf_cap) ovf_rows[slot] = g;
@@ -384,6 +390,379 @@ __global__ void __launch_bounds__(256) band_rows_f64_kernel(
       if (lane == 0) labels[r] = win;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// estep_x64: certified filter + exact fp64 re-check (the default GPU E-step).
+//
+// One MFMA pass on the fp16 HI pieces only (xh . ch + the norm step) gives
+// D'~ with a RIGOROUS per-row error bound
+//   |D'~_ij - alpha^2 D'_ij| <= E_i = 1.0625 2^-10 |x^_i| C^        (fp16 rounding of both operands)
+//                                   + 2^(qbits-23) M_i               (index packed in the low bits)
+//                                   + 2^-15 M_i                      (fp32 accumulation, <= 2^15 adds)
+//                                   + 2^-21 sqrt(d) (|x^_i| + C^)    (fp16 subnormal pieces)
+// with |x^_i| = alpha |x_i|, C^ = max_j |c^_j| = 2 alpha max_j |c_j| and
+// M_i = C^^2 / 4 + |x^_i| C^ >= every partial sum.  Every centroid that can
+// be the row minimum or a band member then satisfies D'~ <= T_i = min D'~ +
+// delta alpha^2 + 2 E_i (a candidate).  Each lane keeps the 3 smallest packed
+// values of its columns; after the sweep the candidates (at most 2 per lane)
+// go to an LDS list and their distances are recomputed EXACTLY in fp64 from
+// the fp32 rows and centroids (sum_f (x_f - c_f)^2, scipy cdist's formula),
+// so the label is the reference's fp64 delta-band rule, bit for bit:
+//   * 1 candidate   : it is the argmin and the whole band - label known, the
+//                     min distance is left to the M-step (mind = -1 marker:
+//                     the segmented reduce computes |x - c_label|^2 in fp64
+//                     while it streams the row anyway);
+//   * 2..16         : fp64 re-check here (x row re-read from L2, centroid rows
+//                     from L2), min, band, kappa-rank pick, exact mind;
+//   * more, or a lane whose 3rd value is a candidate ("dense" rows, where the
+//     band edge is crowded beyond what one fp16 pass can separate): the row
+//     goes to a device list for the fp32-faithful 3-pass kernel
+//     (estep_f32_kernel in list mode).
+// 8 waves (2 per SIMD) x 32 rows per workgroup share each staged tile (the
+// 1-pass kernel needs <= 256 registers); only the HI region of each operand
+// tile is staged (34 KiB per slot at d = 256).
+constexpr int kMaxCand = 16;
+template <int KSD>
+__global__ void __launch_bounds__(512) estep_x64_kernel(
+    const float* __restrict__ X, const _Float16* __restrict__ C, const float* __restrict__ Cm,
+    const float* __restrict__ xn, const float* __restrict__ cmax2_p, int* __restrict__ labels,
+    float* __restrict__ mind, long long* __restrict__ dense_rows, int* __restrict__ dense_count,
+    long long n, int k_pad, int d, float alpha, float delta_s, double delta, RngKey key,
+    long long row_offset, int dense_cap, int qbits) {
+  constexpr int NW = 8;
+  constexpr int DX = KSD * 16;
+  constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
+  constexpr int TILE_STRIDE = (2 * KSD + 1) * 2048;
+  constexpr int PIECES = HI_BYTES / 1024;
+  constexpr int ROWS = NW * 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * HI_BYTES; };
+  int* cand_all = reinterpret_cast<int*>(smem + 2 * HI_BYTES);       // [NW][32][kMaxCand]
+  int* cnt_all = cand_all + NW * 32 * kMaxCand;                       // [NW][32]
+  double* dist_all = reinterpret_cast<double*>(cnt_all + NW * 32);    // [NW][32][kMaxCand]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int half = lane >> 5;
+  const int n_tiles = k_pad / kTileN;
+  const long long nblk = (n + ROWS - 1) / ROWS;
+  long long blk = blockIdx.x;
+  if (blk >= nblk) return;
+  int* cand = cand_all + wave * 32 * kMaxCand;
+  int* cnt = cnt_all + wave * 32;
+  const uint32_t qmask = (1u << qbits) - 1u;
+  const uint32_t keep = ~qmask;
+  // rigorous bound constants (fp32, rounded up by the 1.0625 / 1+2^-16 factors)
+  const float Ch = 2.0f * sqrtf(*cmax2_p) * (1.0f + 0x1p-16f);
+  const float pack_rel = ldexpf(1.0f, qbits - 23) + 0x1p-15f;
+  const float sub_rel = 0x1p-21f * sqrtf((float)DX);
+
+  auto stage = [&](int G) {
+    const int t = G % n_tiles;
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_STRIDE;
+    unsigned char* dst = buf(G);
+    for (int p = wave; p < PIECES; p += NW) {
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
+    }
+  };
+
+  f16x8 ah[KSD];
+  auto load_split = [&](long long b) {
+    const long long r = b * ROWS + wave * 32 + r32;
+    const float* xr = X + (size_t)(r < n ? r : n - 1) * DX + half * 8;
+    // whole-vector assignment: element inserts into ah[ks] would keep the
+    // previous block's fragments alive (register pressure -> spills)
+#pragma unroll
+    for (int ks = 0; ks < KSD; ++ks) {
+      const float4 r0 = *reinterpret_cast<const float4*>(xr + ks * 16);
+      const float4 r1 = *reinterpret_cast<const float4*>(xr + ks * 16 + 4);
+      ah[ks] = (f16x8){(_Float16)(r0.x * alpha), (_Float16)(r0.y * alpha), (_Float16)(r0.z * alpha),
+                       (_Float16)(r0.w * alpha), (_Float16)(r1.x * alpha), (_Float16)(r1.y * alpha),
+                       (_Float16)(r1.z * alpha), (_Float16)(r1.w * alpha)};
+    }
+  };
+  f16x8 aug = (f16x8)0;
+  if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
+
+  float m1[16], m2[16], m3[16];
+  const int lane_off = (half * 64 + r32) * 16;
+  auto ldb = [&](const unsigned char* p) -> f16x8 { return *reinterpret_cast<const f16x8*>(p); };
+  auto tile_step = [&](const unsigned char* cur, f32x16& n0, f32x16& n1, bool do_mfma,
+                       const f32x16& o0, const f32x16& o1, int t_prev, bool do_epi) {
+    const uint32_t q0 = (uint32_t)(t_prev * 2), q1 = q0 + 1u;
+    auto ins = [&](int i, float v, uint32_t q) {
+      const float p = __uint_as_float((__float_as_uint(v) & keep) | q);
+      const float a1 = m1[i], a2 = m2[i];
+      m3[i] = vmed3(a2, p, m3[i]);
+      m2[i] = vmed3(a1, p, a2);
+      m1[i] = vmin(a1, p);
+    };
+    if (do_mfma) {
+      f32x16 acc0 = {0}, acc1 = {0};
+      const unsigned char* hb = cur + lane_off;
+      f16x8 b0[2], b1[2];
+      b0[0] = ldb(hb);
+      b1[0] = ldb(hb + 512);
+#pragma unroll
+      for (int ks = 0; ks <= KSD; ++ks) {
+        const int c = ks & 1, nx = c ^ 1;
+        if (ks < KSD) {
+          b0[nx] = ldb(hb + (ks + 1) * 2048);
+          b1[nx] = ldb(hb + (ks + 1) * 2048 + 512);
+        }
+        const f16x8 A = ks < KSD ? ah[ks] : aug;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b0[c], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b1[c], acc1, 0, 0, 0);
+        if (do_epi) {
+#pragma unroll
+          for (int i = (ks * 16) / (KSD + 1); i < ((ks + 1) * 16) / (KSD + 1); ++i) {
+            ins(i, o0[i], q0);
+            ins(i, o1[i], q1);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      n0 = acc0;
+      n1 = acc1;
+    } else if (do_epi) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        ins(i, o0[i], q0);
+        ins(i, o1[i], q1);
+      }
+    }
+  };
+  auto sync_tile = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  int G = 0;
+  stage(0);
+  load_split(blk);
+  sync_tile();
+
+  for (; blk < nblk; blk += gridDim.x) {
+    const long long row0 = blk * ROWS + wave * 32;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m1[i] = m2[i] = m3[i] = __builtin_inff();
+    if (lane < 32) cnt[lane] = 0;
+    f32x16 pA0, pA1, pB0, pB1;
+    stage(G + 1);
+    tile_step(buf(G), pA0, pA1, true, pA0, pA1, 0, false);
+    sync_tile();
+    int t = 0;
+    while (true) {
+      if (t + 1 >= n_tiles) {
+        tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pB0, pB1, true, pA0, pA1, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+      if (t + 1 >= n_tiles) {
+        tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
+        break;
+      }
+      stage(G + 2);
+      tile_step(buf(G + 1), pA0, pA1, true, pB0, pB1, t, true);
+      sync_tile();
+      ++t;
+      ++G;
+    }
+    ++G;
+    // the next block's rows: issued now, their latency hides behind the
+    // candidate extraction and the fp64 re-check (ah is dead after the sweep)
+
+    // ---- row minimum (packed) by the transposed reduce-scatter: lane r32
+    // even ends with the min of row irow = r32 >> 1 of its half
+    float R[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) R[i] = m1[i];
+#pragma unroll
+    for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
+      const bool hi = (r32 & o) != 0;
+#pragma unroll
+      for (int j = 0; j < c; ++j) {
+        const float ra = R[j], rb = R[c + j];
+        const float keepv = hi ? rb : ra, sendv = hi ? ra : rb;
+        R[j] = vmin(keepv, __shfl_xor(sendv, o, 64));
+      }
+    }
+    const float rmin = vmin(R[0], __shfl_xor(R[0], 1, 64));
+    const int irow = r32 >> 1;
+    const int rl_own = (irow & 3) + 8 * (irow >> 2) + 4 * half;
+    const long long g_own = row0 + rl_own;
+    const float xsv = alpha * sqrtf(xn[g_own < n ? g_own : n - 1]) * (1.0f + 0x1p-16f);
+    const float prod = xsv * Ch;
+    const float mag = 0.25f * Ch * Ch + prod;
+    const float E = 1.0625f * 0x1p-10f * prod + pack_rel * mag + sub_rel * (xsv + Ch);
+    const float T_own = __uint_as_float(__float_as_uint(rmin) & keep) + delta_s + 2.0f * E;
+
+    // ---- candidates -> LDS list of their row (C/D layout: register i of this
+    // lane is row (i & 3) + 8 (i >> 2) + 4 half, column class r32)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float T = __shfl(T_own, 32 * half + 2 * i, 64);
+      const int rl = (i & 3) + 8 * (i >> 2) + 4 * half;
+      auto jof = [&](float p) -> int {
+        const uint32_t q = __float_as_uint(p) & qmask;
+        return (int)((q >> 1) * kTileN + (q & 1u) * 32u) + r32;
+      };
+      if (m3[i] <= T) atomicAdd(&cnt[rl], kMaxCand + 1);   // lane may hide more: dense
+      if (m1[i] <= T) {
+        const int s = atomicAdd(&cnt[rl], 1);
+        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(m1[i]);
+      }
+      if (m2[i] <= T) {
+        const int s = atomicAdd(&cnt[rl], 1);
+        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(m2[i]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- exact re-check, A layout: lanes r32 and r32 + 32 share row r32
+    // (features half*8 + 16 ks + e), one shuffle joins the two halves
+    const long long g = row0 + r32;
+    const bool valid = g < n;
+    const int c_r = cnt[r32];
+    const bool dense = c_r > kMaxCand;
+    const bool multi = valid && !dense && c_r >= 2;
+    if (valid && half == 0) {
+      if (dense) {
+        const int s = atomicAdd(dense_count, 1);
+        if (s < dense_cap) dense_rows[s] = g;
+        labels[g] = -1;
+      } else if (c_r == 1) {
+        labels[g] = cand[r32 * kMaxCand];
+        mind[g] = -1.0f;   // filled by the M-step's segmented reduce
+      }
+    }
+    const unsigned long long mm = __ballot(multi);
+    if (mm) {
+      int maxc = multi ? c_r : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) maxc = max(maxc, __shfl_xor(maxc, o, 64));
+      const float* xr = X + (size_t)(valid ? g : 0) * DX + half * 8;
+      double* dl = dist_all + (wave * 32 + r32) * kMaxCand;
+      const int* cl = cand + r32 * kMaxCand;
+#pragma unroll 1
+      for (int c = 0; c < maxc; ++c) {   // wave-uniform trip count
+        const int j = (multi && c < c_r) ? cl[c] : 0;
+        const float* cr = Cm + (size_t)j * d;
+        double s = 0.0;
+        if (d == DX) {
+          const float* cc = cr + half * 8;
+#pragma unroll 2
+          for (int ks = 0; ks < KSD; ++ks) {
+            const float4 x0 = *reinterpret_cast<const float4*>(xr + ks * 16);
+            const float4 x1 = *reinterpret_cast<const float4*>(xr + ks * 16 + 4);
+            const float4 c0 = *reinterpret_cast<const float4*>(cc + ks * 16);
+            const float4 c1 = *reinterpret_cast<const float4*>(cc + ks * 16 + 4);
+            const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            const float ca[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const double df = (double)xa[e] - (double)ca[e];
+              s = fma(df, df, s);
+            }
+          }
+        } else {
+#pragma unroll 1
+          for (int ks = 0; ks < KSD; ++ks) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int f = ks * 16 + half * 8 + e;
+              if (f < d) {
+                const double df = (double)xr[ks * 16 + e] - (double)cr[f];
+                s = fma(df, df, s);
+              }
+            }
+          }
+        }
+        s += __shfl_xor(s, 32, 64);
+        if (half == 0) dl[c] = s;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (multi && half == 0) {
+        double dmin = dl[0];
+        for (int c = 1; c < c_r; ++c) dmin = fmin(dmin, dl[c]);
+        const double thr = dmin + delta;
+        int b = 0;
+        for (int c = 0; c < c_r; ++c) b += dl[c] <= thr ? 1 : 0;
+        const int r = band_rank(band_u(key, row_offset + g), b);
+        // the band member of kappa rank r, kappa(j) = (j mod 32, j div 32)
+        int pick = cl[0];
+        for (int c = 0; c < c_r; ++c) {
+          if (!(dl[c] <= thr)) continue;
+          const int jc = cl[c];
+          const int kc = ((jc & 31) << 20) | (jc >> 5);
+          int rank = 0;
+          for (int c2 = 0; c2 < c_r; ++c2) {
+            const int j2 = cl[c2];
+            rank += (dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
+          }
+          if (rank == r) pick = jc;
+        }
+        labels[g] = pick;
+        mind[g] = (float)dmin;
+      }
+    }
+    if (blk + gridDim.x < nblk) load_split(blk + gridDim.x);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// mind of the rows the filter resolved with a single candidate (marker < 0):
+// exact fp64 |x - c_label|^2, one wave per row.  The Lloyd step does this
+// inside the segmented reduce (it streams the rows anyway); this standalone
+// pass serves estep() calls outside a step (final E-step, predict/score).
+__global__ void __launch_bounds__(256) fill_mind_kernel(const float* __restrict__ X, int ldx,
+                                                        const float* __restrict__ Cm, int d,
+                                                        const int* __restrict__ labels,
+                                                        float* __restrict__ mind, long long n) {
+  const int lane = threadIdx.x & 63;
+  for (long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); r < n;
+       r += (long long)gridDim.x * 4) {
+    if (!(mind[r] < 0.0f)) continue;   // wave-uniform
+    const int l = labels[r];
+    if (l < 0) continue;
+    double s = 0.0;
+    for (int f = lane; f < d; f += 64) {
+      const double df = (double)X[(size_t)r * ldx + f] - (double)Cm[(size_t)l * d + f];
+      s = fma(df, df, s);
+    }
+    s = wave_sum(s);
+    if (lane == 0) mind[r] = (float)s;
+  }
+}
+
+// deterministic sum of n floats: every block sums a fixed contiguous chunk in
+// a fixed thread order and tree; the launcher reduces the block partials with
+// the one-block sum_partials kernel (kmeans.hip) - bit-reproducible.
+__global__ void __launch_bounds__(256) sum_f32_blocks_kernel(const float* __restrict__ v,
+                                                             long long n, double* __restrict__ part) {
+  __shared__ double red[256];
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long b = (long long)blockIdx.x * per, e = min(n, b + per);
+  double s = 0.0;
+  for (long long i = b + threadIdx.x; i < e; i += 256) s += (double)v[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -453,7 +832,8 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
                             void* ovf_rows, void* ovf_count, void* part, int part_cap,
                             void* inertia, long long n, int k_pad, float alpha, float inv_a2,
                             float delta_s, RngKey key, long long row_offset, int ovf_cap,
-                            hipStream_t st) {
+                            hipStream_t st, const void* rlist = nullptr,
+                            const void* rcount = nullptr) {
   constexpr int NW = 4;
   const size_t lds = 2 * (size_t)((2 * KSD + 1) * 2048);
   auto kern = estep_f32_kernel<KSD>;
@@ -471,15 +851,52 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const long long nblk = (n + NW * 32 - 1) / (NW * 32);
-  unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
+  // list mode: the row count is on the device - every resident slot launches
+  unsigned grid = (unsigned)(nblk < resident && !rlist ? nblk : resident);
   if ((long long)grid * NW > part_cap) grid = (unsigned)(part_cap / NW);
   if (grid == 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const float*)X,
                      (const _Float16*)C, (const float*)xn, (int*)labels, (float*)mind,
                      (long long*)ovf_rows, (int*)ovf_count, (double*)part, n, k_pad, alpha, inv_a2,
-                     delta_s, key, row_offset, ovf_cap);
+                     delta_s, key, row_offset, ovf_cap, (const long long*)rlist,
+                     (const int*)rcount);
   // per-wave inertia partials summed in a fixed order (bit-reproducible)
+  if (!inertia) return (int)hipGetLastError();
   return sq_sum_partials(part, (int)grid * NW, inertia, st);
+}
+
+template <int KSD>
+static int launch_estep_x64(const void* X, const void* C, const void* Cm, const void* xn,
+                            const void* cmax2, void* labels, void* mind, void* dense_rows,
+                            void* dense_count, long long n, int k, int k_pad, int d, float alpha,
+                            float delta_s, double delta, RngKey key, long long row_offset,
+                            int dense_cap, hipStream_t st) {
+  constexpr int NW = 8;
+  const size_t lds = 2 * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4 +
+                     (size_t)NW * 32 * kMaxCand * 8;
+  auto kern = estep_x64_kernel<KSD>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NW * 64, lds);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  int qbits = 1;
+  while ((1 << qbits) < 2 * (k_pad / kTileN)) ++qbits;
+  const long long nblk = (n + NW * 32 - 1) / (NW * 32);
+  const unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const float*)X,
+                     (const _Float16*)C, (const float*)Cm, (const float*)xn, (const float*)cmax2,
+                     (int*)labels, (float*)mind, (long long*)dense_rows, (int*)dense_count, n,
+                     k_pad, d, alpha, delta_s, delta, key, row_offset, dense_cap, qbits);
+  return (int)hipGetLastError();
 }
 
 extern "C" {
@@ -513,6 +930,67 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
       return (int)hipErrorInvalidValue;
   }
   return rc;
+}
+
+// Certified E-step (the default): filter + fp64 re-check (estep_x64_kernel),
+// dense rows through the 3-pass fp32-faithful kernel in list mode, its
+// overflow rows through band_rows_f64.  counts[0] = 3-pass overflow rows,
+// counts[1] = dense rows; both must be zero on entry.  mind holds -1 for rows
+// whose distance the M-step (or fill_mind) computes; no inertia here.
+int sq_estep_x64(const void* X, const void* C, const void* Cm, const void* xn, const void* cmax2,
+                 void* labels, void* mind, void* dense_rows, void* ovf_rows, void* counts,
+                 void* part, int part_cap, long long n, int d, int d_pad, int k, int k_pad,
+                 double alpha, double delta, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
+                 long long row_offset, void* stream) {
+  if (n <= 0) return 0;
+  if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 4096 || k > k_pad || d > d_pad)
+    return (int)hipErrorInvalidValue;
+  int aexp = 0;
+  if (!(alpha > 0.0) || frexp(alpha, &aexp) != 0.5) return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  hipStream_t st = (hipStream_t)stream;
+  const double a2 = alpha * alpha;
+  const float fa = (float)alpha, ia2 = (float)(1.0 / a2), ds = (float)(delta * a2);
+  int* cnt = (int*)counts;
+  int rc;
+  switch (d_pad) {
+#define CASE(KSD)                                                                                \
+  case KSD * 16:                                                                                 \
+    rc = launch_estep_x64<KSD>(X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1, n, k,     \
+                               k_pad, d, fa, ds, delta, key, row_offset, (int)min(n, 2147483647LL), st); \
+    if (rc) return rc;                                                                           \
+    rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
+                               n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \
+                               st, dense_rows, cnt + 1);                                         \
+    break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(n < 2048 ? n : 2048)), dim3(256), 0,
+                     st, (const float*)X, (const float*)Cm, (const long long*)ovf_rows,
+                     (const int*)cnt, (int*)labels, n, d_pad, d, k, delta, key, row_offset);
+  return (int)hipGetLastError();
+}
+
+int sq_fill_mind(const void* X, int ldx, const void* Cm, int d, const void* labels, void* mind,
+                 long long n, void* stream) {
+  if (n <= 0) return 0;
+  const unsigned grid = (unsigned)((n + 3) / 4 < 8192 ? (n + 3) / 4 : 8192);
+  hipLaunchKernelGGL(fill_mind_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)X, ldx, (const float*)Cm, d, (const int*)labels, (float*)mind, n);
+  return (int)hipGetLastError();
+}
+
+// inertia[0] = sum of mind[0:n) in a fixed order (part: >= 512 doubles)
+int sq_sum_f32(const void* v, long long n, void* part, void* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = 512;
+  hipLaunchKernelGGL(sum_f32_blocks_kernel, dim3(blocks), dim3(256), 0, st, (const float*)v, n,
+                     (double*)part);
+  return sq_sum_partials(part, blocks, out, st);
 }
 
 int sq_band_rows_f64(const void* X, const void* C, const void* rows, const void* count,

@@ -887,12 +887,16 @@ __global__ void __launch_bounds__(256) label_scatter_kernel(const int* __restric
 #ifndef SQ_SEG_U
 #define SQ_SEG_U 4   // rows in flight per wave (perm -> label/row gathers)
 #endif
+// With mind != null (fp32 data, d <= 256: one column pass) the rows whose
+// E-step left mind < 0 (the certified filter's single-candidate rows) get
+// their exact fp64 |x - c_label|^2 here, against the iteration's centroids
+// Cold [k][d], while the row is in registers anyway.
 template <typename T>
 __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
     const T* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
     const float* __restrict__ w, long long n_sorted, int d, int range, float xscale,
     float wscale, double* __restrict__ sums, double* __restrict__ counts,
-    const int* __restrict__ valid_end) {
+    const int* __restrict__ valid_end, float* __restrict__ mind, const float* __restrict__ Cold) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long long p0 = (long long)blockIdx.x * range;
   const long long p1 = min(min(n_sorted, (long long)*valid_end), p0 + range);
@@ -900,6 +904,7 @@ __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
   for (int c0 = lane * 4; c0 < d; c0 += 256) {
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, cnt = 0.0;
     int cur = -1;
+    float4 cold = make_float4(0.f, 0.f, 0.f, 0.f);
     auto flush = [&]() {
       double* dst = sums + (size_t)cur * d + c0;
       if (a0 != 0.0) atomicAdd(dst + 0, a0);
@@ -912,6 +917,7 @@ __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
       int rr[U], ll[U];
       float4 v[U];
       float ww[U];
+      float mk[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         long long q = p + 8LL * u;
@@ -922,6 +928,7 @@ __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
         ll[u] = rr[u] >= 0 ? labels[rr[u]] : -1;
         v[u] = rr[u] >= 0 ? load4<T>(X + (size_t)rr[u] * d + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
         ww[u] = (w && rr[u] >= 0) ? w[rr[u]] : 1.0f;
+        mk[u] = (mind && rr[u] >= 0) ? mind[rr[u]] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -930,6 +937,14 @@ __global__ void __launch_bounds__(512) segment_sum_rows_kernel(
           if (cur >= 0) flush();
           cur = ll[u];
           a0 = a1 = a2 = a3 = cnt = 0.0;
+          if (mind) cold = *reinterpret_cast<const float4*>(Cold + (size_t)cur * d + c0);
+        }
+        if (mk[u] < 0.0f) {   // wave-uniform (one row per wave)
+          const double e0 = (double)v[u].x - (double)cold.x, e1 = (double)v[u].y - (double)cold.y;
+          const double e2 = (double)v[u].z - (double)cold.z, e3 = (double)v[u].w - (double)cold.w;
+          double ds = fma(e0, e0, fma(e1, e1, fma(e2, e2, e3 * e3)));
+          ds = wave_sum(ds);
+          if (lane == 0) mind[rr[u]] = (float)ds;
         }
         const float s = ww[u] * xscale;   // exact when unweighted (power of 2)
         a0 += (double)rintf(v[u].x * s);
@@ -1123,21 +1138,35 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const double* __restr
 // scalars = [inertia (packed tail, after the all-reduce), shift (per-centroid
 // parts summed in the same fixed order as sum_partials_kernel), overflow
 // rows]; the overflow counter is reset for the next E-step.
+// With cmax2 != null it also writes max_j cn[j] (the fp16 operand's largest
+// alpha^2 ||c||^2: the certified E-step's error bound for the next iteration).
 __global__ void __launch_bounds__(256) iter_scalars_kernel(const double* __restrict__ part, int n,
                                                            double* __restrict__ shift,
                                                            const double* __restrict__ inertia,
                                                            int* __restrict__ ovf_count,
-                                                           double* __restrict__ scalars) {
+                                                           double* __restrict__ scalars,
+                                                           const float* __restrict__ cn,
+                                                           float* __restrict__ cmax2) {
   __shared__ double red[256];
+  __shared__ float redm[256];
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  float mx = 0.0f;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    s += part[i];
+    if (cmax2) mx = fmaxf(mx, cn[i]);
+  }
+  redm[threadIdx.x] = mx;
   red[threadIdx.x] = s;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    if ((int)threadIdx.x < o) {
+      red[threadIdx.x] += red[threadIdx.x + o];
+      redm[threadIdx.x] = fmaxf(redm[threadIdx.x], redm[threadIdx.x + o]);
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    if (cmax2) cmax2[0] = redm[0];
     shift[0] = red[0];
     scalars[0] = inertia[0];
     scalars[1] = red[0];
@@ -1239,7 +1268,7 @@ __global__ void __launch_bounds__(256) centroid_finalize_kernel(
   if (tid == 0) {
     shift[j] = red[0] + red[1] + red[2] + red[3];   // per-centroid part (fixed-order sum)
     float t = redf[0] + redf[1] + redf[2] + redf[3];
-    cn[j] = t;
+    cn[j] = C_f16 ? (float)(redn[0] + redn[1] + redn[2] + redn[3]) : t;
     if (C_bf16) {
       uint16_t hi = f32_to_bf16_rne(t);
       float r1 = t - bf16_to_f32(hi);
@@ -1531,7 +1560,9 @@ static int seg_range() {
 
 int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void* weights,
                        void* sums, void* counts, long long n, int d, int k, int xexp, int wexp,
-                       void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
+                       void* ws_hist, void* ws_cursor, void* ws_perm, void* mind,
+                       const void* Cold, void* stream) {
+  if (mind && (xdtype != 0 || d > 256 || d % 4 != 0 || !Cold)) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
   if (d % 4 != 0 || k > 16384 || n > 2147483647LL) return (int)hipErrorInvalidValue;
   if (xexp < -120 || xexp > 120 || wexp < -120 || wexp > 120) return (int)hipErrorInvalidValue;
@@ -1550,7 +1581,7 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
   // kernel bounds itself with the scanned total (cursor[k-1] after scatter)
   const float xs = ldexpf(1.0f, -xexp), wsc = ldexpf(1.0f, -wexp);
   const int V = xdtype == 2 ? 8 : 4;
-  if (d / V >= 32 || d % V != 0) {
+  if (d / V >= 32 || d % V != 0 || mind) {
     // whole-wave rows (large d, or d not a multiple of the 16-B chunk)
     const int range = seg_range();
     unsigned grid = (unsigned)((n + range - 1) / range);
@@ -1558,7 +1589,8 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
       hipLaunchKernelGGL(segment_sum_rows_kernel<float>, dim3(grid), dim3(512), 0, st,
                          (const float*)X, (const int*)ws_perm, (const int*)labels,
                          (const float*)weights, n, d, range, xs, wsc, (double*)sums,
-                         (double*)counts, (const int*)ws_cursor + (k - 1));
+                         (double*)counts, (const int*)ws_cursor + (k - 1), (float*)mind,
+                         (const float*)Cold);
     else if (xdtype == 2 && d % 8 == 0 && seg_half())
       hipLaunchKernelGGL(segment_sum_rows_half_kernel, dim3(grid), dim3(512), 0, st,
                          (const uint16_t*)X, (const int*)ws_perm, (const int*)labels,
@@ -1568,7 +1600,8 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
       hipLaunchKernelGGL(segment_sum_rows_kernel<uint16_t>, dim3(grid), dim3(512), 0, st,
                          (const uint16_t*)X, (const int*)ws_perm, (const int*)labels,
                          (const float*)weights, n, d, range, xs, wsc, (double*)sums,
-                         (double*)counts, (const int*)ws_cursor + (k - 1));
+                         (double*)counts, (const int*)ws_cursor + (k - 1), (float*)nullptr,
+                         (const float*)nullptr);
     else
       return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
@@ -1621,7 +1654,7 @@ int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, voi
                          void* shift_part, void* cn, void* shift, int k, int d, int k_pad,
                          double noise_b, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
                          int empty_policy, void* scalars, void* ovf_count, void* C_f16,
-                         double alpha, void* stream) {
+                         double alpha, void* cmax2, void* stream) {
   if (!shift_part) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   float b = (float)noise_b;
@@ -1635,7 +1668,7 @@ int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, voi
     hipLaunchKernelGGL(iter_scalars_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
                        (const double*)shift_part, k, (double*)shift,
                        (const double*)packed + (long long)k * d + k, (int*)ovf_count,
-                       (double*)scalars);
+                       (double*)scalars, (const float*)cn, (float*)cmax2);
   else
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
                        (const double*)shift_part, k, (double*)shift);

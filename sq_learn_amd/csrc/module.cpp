@@ -58,11 +58,20 @@ __attribute__((weak)) int sq_centroid_accumulate(const void* X, int xdtype, cons
                            void* sums, void* counts, long long n, int d, int k, int chunk,
                            void* stream);
 __attribute__((weak)) int sq_centroid_reduce(const void*, int, const void*, const void*, void*, void*,
-                       long long, int, int, int, int, void*, void*, void*, void*);
+                       long long, int, int, int, int, void*, void*, void*, void*, const void*,
+                       void*);
 __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, void* C_bf16,
                          void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
                          unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
-                         void* scalars, void* ovf_count, void* C_f16, double alpha, void* stream);
+                         void* scalars, void* ovf_count, void* C_f16, double alpha, void* cmax2,
+                         void* stream);
+__attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, const void*,
+                                       const void*, void*, void*, void*, void*, void*, void*, int,
+                                       long long, int, int, int, int, double, double, unsigned,
+                                       unsigned, unsigned, unsigned, long long, void*);
+__attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
+                                       long long, void*);
+__attribute__((weak)) int sq_sum_f32(const void*, long long, void*, void*, void*);
 // estep_f32.hip
 __attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, void*, void*, void*,
                                        void*, void*, int, void*, long long, int, int, double,
@@ -240,24 +249,51 @@ static PyObject* py_centroid_accumulate(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
-  unsigned long long X, lab, w, sums, counts, h, c, pm, st; int xdt, d, k, xe, we; long long n;
-  if (!PyArg_ParseTuple(a, "KiKKKKLiiiiKKKK", &X, &xdt, &lab, &w, &sums, &counts, &n, &d, &k, &xe,
-                        &we, &h, &c, &pm, &st))
+  unsigned long long X, lab, w, sums, counts, h, c, pm, mind, cold, st; int xdt, d, k, xe, we;
+  long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKKLiiiiKKKKKK", &X, &xdt, &lab, &w, &sums, &counts, &n, &d, &k, &xe,
+                        &we, &h, &c, &pm, &mind, &cold, &st))
     return nullptr;
   CHECK(sq_centroid_reduce)
   return ret(sq_centroid_reduce(P(X), xdt, P(lab), P(w), P(sums), P(counts), n, d, k, xe, we, P(h),
-                                P(c), P(pm), P(st)));
+                                P(c), P(pm), P(mind), P(cold), P(st)));
+}
+
+static PyObject* py_estep_x64(PyObject*, PyObject* a) {
+  unsigned long long X, C, Cm, xn, cm2, lab, mind, dr, ovr, cnt, part, st; int pcap, d, dp, k, kp;
+  long long n, roff; double alpha, delta; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKiLiiiiddIIIILK", &X, &C, &Cm, &xn, &cm2, &lab, &mind, &dr,
+                        &ovr, &cnt, &part, &pcap, &n, &d, &dp, &k, &kp, &alpha, &delta, &k0, &k1,
+                        &s0, &s1, &roff, &st))
+    return nullptr;
+  CHECK(sq_estep_x64)
+  return ret(sq_estep_x64(P(X), P(C), P(Cm), P(xn), P(cm2), P(lab), P(mind), P(dr), P(ovr), P(cnt),
+                          P(part), pcap, n, d, dp, k, kp, alpha, delta, k0, k1, s0, s1, roff, P(st)));
+}
+
+static PyObject* py_fill_mind(PyObject*, PyObject* a) {
+  unsigned long long X, Cm, lab, mind, st; int ldx, d; long long n;
+  if (!PyArg_ParseTuple(a, "KiKiKKLK", &X, &ldx, &Cm, &d, &lab, &mind, &n, &st)) return nullptr;
+  CHECK(sq_fill_mind)
+  return ret(sq_fill_mind(P(X), ldx, P(Cm), d, P(lab), P(mind), n, P(st)));
+}
+
+static PyObject* py_sum_f32(PyObject*, PyObject* a) {
+  unsigned long long v, part, out, st; long long n;
+  if (!PyArg_ParseTuple(a, "KLKKK", &v, &n, &part, &out, &st)) return nullptr;
+  CHECK(sq_sum_f32)
+  return ret(sq_sum_f32(P(v), n, P(part), P(out), P(st)));
 }
 
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
-  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, cf, st; int k, d, kpad, pol; double nb;
-  double alpha; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKKdK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
-                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &cf, &alpha, &st))
+  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, cf, cm2, st; int k, d, kpad, pol;
+  double nb, alpha; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKKdKK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
+                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &cf, &alpha, &cm2, &st))
     return nullptr;
   CHECK(sq_centroid_finalize)
   return ret(sq_centroid_finalize(P(pk), P(co), P(cnw), P(cb), P(clo), P(cn), P(sh), k, d, kpad, nb,
-                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(cf), alpha, P(st)));
+                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(cf), alpha, P(cm2), P(st)));
 }
 
 static PyObject* py_estep_f32(PyObject*, PyObject* a) {
@@ -374,6 +410,9 @@ static PyMethodDef methods[] = {
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},
     {"estep_f32", py_estep_f32, METH_VARARGS, "fp32-faithful fused E-step (fp16 hi/lo MFMA)"},
+    {"estep_x64", py_estep_x64, METH_VARARGS, "certified filter E-step + fp64 re-check"},
+    {"fill_mind", py_fill_mind, METH_VARARGS, "exact distance to the label for marked rows"},
+    {"sum_f32", py_sum_f32, METH_VARARGS, "deterministic sum of a float vector"},
     {"band_rows_f64", py_band_rows_f64, METH_VARARGS, "fp64 re-selection of overflow rows"},
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},

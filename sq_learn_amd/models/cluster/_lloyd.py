@@ -130,7 +130,15 @@ class LloydEngine:
         self.C_bf16 = None
         self.C_op = torch.zeros(K.operand_f16_shape(self.k_pad, self.d_pad), dtype=torch.float16,
                                 device=dev)
+        # largest alpha^2 |c|^2 (the certified E-step's error bound; refreshed
+        # by every centroid_finalize)
+        self.cmax2 = torch.zeros(1, dtype=torch.float32, device=dev)
+        # certified filter + fp64 re-check (default); SQ_ESTEP_FILTER=0 runs
+        # the fp32-faithful 3-pass kernel on every row instead (A/B, tests)
+        import os
+        self.certified = os.environ.get("SQ_ESTEP_FILTER", "1") != "0"
         self._prepare_reduce()
+        self.mind_part = torch.zeros(512, dtype=torch.float64, device=dev)
 
     def _prepare_reduce(self):
         dev = self.device
@@ -179,6 +187,8 @@ class LloydEngine:
             if self.C_op is not None:
                 K.centers_to_f16_native(self.C, self.C_op, self.k, self.d, self.d_pad, self.k_pad,
                                         self.alpha)
+                self.cmax2.copy_(((self.C.double() * self.alpha) ** 2).sum(1).max().float()
+                                 .reshape(1) if self.k else torch.zeros(1, device=self.device))
                 return
             Cb, cn = K.centers_to_bf16(self.C, self.k_pad, self.d_pad)
             self.C_bf16.copy_(Cb)
@@ -211,7 +221,20 @@ class LloydEngine:
         returns (labels, mind, local_inertia_tensor)."""
         if C is not None:
             self.set_centers(C)
-        key = self._key("band_select")
+        lab, mind, inertia = self._estep(self._key("band_select"))
+        if self.fast and self.C_op is not None and self.certified:
+            # single-candidate rows: their min distance is |x - c_label|^2
+            K.fill_mind_native(self.Xf32, self.C, lab, mind)
+            K.sum_f32_native(mind, self.n, self.mind_part, self.buf.inertia)
+        return lab, mind, inertia
+
+    def _estep(self, key):
+        if self.fast and self.C_op is not None and self.certified:
+            with tracing.range("estep_x64"):
+                lab, mind = K.estep_x64_native(self.Xf32, self.C_op, self.C, self.xn, self.cmax2,
+                                               self.k, self.delta, self.alpha, key,
+                                               self.row_offset, self.buf)
+            return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):
                 lab, mind = K.estep_f32_native(self.Xf32, self.C_op, self.xn, self.C, self.k,
@@ -283,8 +306,16 @@ class LloydEngine:
         noise_key = self._key("trunc_normal")
         if self.fast:
             with tracing.range("mstep"):
+                exact = self.C_op is not None and self.certified
+                Cold = None
+                if exact:
+                    Cold = self.C if self.dm == self.d else self._padded_centers()
                 K.centroid_reduce_native(self.Xm, labels, self.weights, self.sums,
-                                         self.counts, self.k, self.rws)
+                                         self.counts, self.k, self.rws,
+                                         mind=self.buf.mind if exact else None, C_old=Cold)
+                if exact:
+                    # inertia = sum of the (now complete) min distances, fixed order
+                    K.sum_f32_native(self.buf.mind, self.n, self.mind_part, inertia)
                 sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
                 K.pack_stats_native(sums, self.counts, inertia, self.packed, self.k, self.d,
                                     self.rws, weighted=self.weights is not None)
@@ -296,7 +327,8 @@ class LloydEngine:
                                            noise_key, self.empty_policy,
                                            shift_part=self.shift_part, scalars=self.scalars,
                                            buf=self.buf, C_f16=self.C_op, alpha=self.alpha,
-                                           k_pad=self.k_pad)
+                                           k_pad=self.k_pad,
+                                           cmax2=self.cmax2 if self.C_op is not None else None)
                 self.C, self.C_new = self.C_new, self.C
                 if self.intermediate_error and self.true_tomography and self.delta > 0:
                     self._true_tomography_centers()
@@ -350,6 +382,12 @@ class LloydEngine:
         return torch.stack([tot_inertia, shift, torch.zeros((), dtype=torch.float64,
                                                             device=self.device)])
 
+    def _padded_centers(self):
+        if getattr(self, "_Cpad", None) is None:
+            self._Cpad = torch.zeros((self.k, self.dm), dtype=torch.float32, device=self.device)
+        self._Cpad[:, :self.d].copy_(self.C)
+        return self._Cpad
+
     def _true_tomography_centers(self):
         """Real (shot-based) tomography of the k centre rows with error delta/2,
         replicated on every rank (Philox-keyed: identical everywhere); on the
@@ -363,7 +401,7 @@ class LloydEngine:
     # ---------------------------------------------------------- iteration
     def step(self):
         """One Lloyd iteration; returns (labels, scalars_tensor)."""
-        labels, mind, inertia = self.estep()
+        labels, mind, inertia = self._estep(self._key("band_select"))
         if self.failure_prob > 0:
             # SURVEY.md §5.3: Bernoulli estimation failures (+ resampling)
             failure_inject_(labels, self.k, self.failure_prob, self.failure_attempts,

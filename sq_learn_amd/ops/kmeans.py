@@ -174,8 +174,10 @@ class EStepBuffers:
         self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(n, 1))
         self.ovf_rows = torch.empty(self.ovf_cap, dtype=torch.int64, device=device)
         self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
-        # scalars: [ovf_count(int32)] and inertia (fp64) / shift (fp64)
-        self.ovf_count = torch.zeros(1, dtype=torch.int32, device=device)
+        # [overflow rows, dense rows] (int32); ovf_count is a view of slot 0
+        self.counts = torch.zeros(2, dtype=torch.int32, device=device)
+        self.ovf_count = self.counts[0:1]
+        self.dense_rows = None   # allocated by the certified E-step on first use
         # True while ovf_count is known to be zero (fresh, or reset on the
         # device by the iteration-scalars launch): the E-step skips its memset
         self.ovf_clean = True
@@ -274,7 +276,8 @@ class ReduceWorkspace:
         return self
 
 
-def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorkspace):
+def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorkspace, mind=None,
+                           C_old=None):
     """sums[l] = sum_{i: label_i = l} w_i x_i, counts[l] = sum w_i (GPU; the
     outputs are overwritten - zeroed inside the histogram launch),
     in units of the quanta 2^ws.xexp / 2^ws.wexp (exact integer-valued fp64,
@@ -282,12 +285,16 @@ def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorksp
     n, d = X.shape
     assert labels.dtype == torch.int32 and sums.dtype == torch.float64 and counts.dtype == torch.float64
     assert sums.numel() >= k * d and counts.numel() >= k and labels.numel() >= n
+    if mind is not None:
+        # rows with mind < 0 get |x - C_old[label]|^2 (fp64) from the row pass
+        assert X.dtype == torch.float32 and C_old.dtype == torch.float32
+        assert tuple(C_old.shape) == (k, d) and C_old.is_contiguous() and d <= 256
     nat.native().centroid_reduce(X.data_ptr(), nat.dtype_code(X), labels.data_ptr(),
                                  0 if weights is None else weights.data_ptr(), sums.data_ptr(),
                                  counts.data_ptr(), n, d, k, ws.xexp,
                                  ws.wexp if weights is not None else 0, ws.hist.data_ptr(),
-                                 ws.cursor.data_ptr(), ws.perm.data_ptr(),
-                                 nat.stream_handle(X.device))
+                                 ws.cursor.data_ptr(), ws.perm.data_ptr(), nat.ptr(mind),
+                                 nat.ptr(C_old), nat.stream_handle(X.device))
 
 
 def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, weighted=False):
@@ -298,7 +305,7 @@ def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, 
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
                              empty_policy=0, shift_part=None, scalars=None, buf=None, C_f16=None,
-                             alpha=1.0, k_pad=None):
+                             alpha=1.0, k_pad=None, cmax2=None):
     """shift[0] = sum_j ||c_j' - c_j||^2 (per-centroid parts summed in a fixed
     order: deterministic); ``shift_part`` is a k-double workspace.
 
@@ -316,7 +323,7 @@ def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, nois
                                    key.s0, key.s1, int(empty_policy),
                                    0 if scalars is None else scalars.data_ptr(),
                                    0 if buf is None else buf.ovf_count.data_ptr(),
-                                   nat.ptr(C_f16), float(alpha),
+                                   nat.ptr(C_f16), float(alpha), nat.ptr(cmax2),
                                    nat.stream_handle(packed.device))
     if scalars is not None and buf is not None:
         buf.ovf_clean = True
@@ -476,3 +483,46 @@ def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_o
                     buf.ovf_count.data_ptr(), buf.labels.data_ptr(), buf.ovf_cap, d_pad, d, k,
                     float(delta), key.k0, key.k1, key.s0, key.s1, int(row_offset), st)
     return buf.labels, buf.mind
+
+
+def estep_x64_native(Xf, C_op, C_master, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
+                     buf: EStepBuffers, stream=None):
+    """Certified E-step (``estep_x64_kernel``): one fp16 MFMA pass with a
+    rigorous error bound, fp64 re-check of the candidate centroids, dense rows
+    through the fp32-faithful 3-pass kernel.  Labels are the fp64 delta-band
+    rule's; ``buf.mind`` holds -1 on single-candidate rows (filled by the
+    M-step's row pass or ``fill_mind_native``).  No host sync."""
+    n, d_pad = Xf.shape
+    k_pad = C_op.shape[0] * 64
+    d = C_master.shape[1]
+    assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in FAST_D
+    assert C_op.dtype == torch.float16 and tuple(C_op.shape) == operand_f16_shape(k_pad, d_pad)
+    assert C_master.dtype == torch.float32 and C_master.is_contiguous() and C_master.shape[0] == k
+    assert cmax2.dtype == torch.float32 and xn.dtype == torch.float32 and xn.numel() >= n
+    assert k <= k_pad <= 4096 and d <= d_pad and buf.labels.numel() >= n
+    if buf.dense_rows is None or buf.dense_rows.numel() < n:
+        buf.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
+    st = stream if stream is not None else nat.stream_handle(Xf.device)
+    buf.counts.zero_()
+    buf.ovf_clean = False
+    nat.native().estep_x64(Xf.data_ptr(), C_op.data_ptr(), C_master.data_ptr(), xn.data_ptr(),
+                           cmax2.data_ptr(), buf.labels.data_ptr(), buf.mind.data_ptr(),
+                           buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
+                           buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
+                           n, d, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
+                           key.s0, key.s1, int(row_offset), st)
+    return buf.labels, buf.mind
+
+
+def fill_mind_native(Xf, C_master, labels, mind):
+    """mind[i] = |x_i - c_label(i)|^2 (fp64, stored fp32) where mind[i] < 0."""
+    n, ldx = Xf.shape
+    nat.native().fill_mind(Xf.data_ptr(), ldx, C_master.data_ptr(), C_master.shape[1],
+                           labels.data_ptr(), mind.data_ptr(), n, nat.stream_handle(Xf.device))
+
+
+def sum_f32_native(v, n, part, out):
+    """out[0] = sum(v[:n]) in a fixed order (deterministic); part >= 512 doubles."""
+    assert part.numel() >= 512 and part.dtype == torch.float64
+    nat.native().sum_f32(v.data_ptr(), int(n), part.data_ptr(), out.data_ptr(),
+                         nat.stream_handle(v.device))

@@ -47,6 +47,14 @@ def _fp64_rule(X, C, delta, key, k_pad):
     return D, lab, mn
 
 
+@pytest.fixture(params=["certified", "3pass"])
+def path(request, monkeypatch):
+    """fp32 mode runs the certified filter + fp64 re-check by default;
+    SQ_ESTEP_FILTER=0 runs the 3-pass fp32-faithful kernel on every row."""
+    monkeypatch.setenv("SQ_ESTEP_FILTER", "1" if request.param == "certified" else "0")
+    return request.param
+
+
 def _run(X, C, delta, precision):
     Xt = torch.from_numpy(X).cuda()
     eng = LloydEngine(Xt, C.shape[0], delta=delta, seed=7, gemm_precision=precision)
@@ -67,7 +75,7 @@ def _ambiguous(D, mn, delta, X, C, mult=1.0):
 
 
 @pytest.mark.parametrize("off", [3.0, 12.0])
-def test_fp32_estep_matches_fp64_band_rule(off):
+def test_fp32_estep_matches_fp64_band_rule(off, path):
     n, d, k, delta = 8192, 256, 1024, 0.5
     X, C = _dense_data(n, d, k, off)
     eng, key, lab, mind, inertia = _run(X, C, delta, "fp32")
@@ -103,7 +111,7 @@ def test_bf16_estep_fails_the_same_test():
     assert frac > 0.2, frac
 
 
-def test_fp32_estep_delta0_is_exact_argmin():
+def test_fp32_estep_delta0_is_exact_argmin(path):
     n, d, k = 8192, 256, 1024
     X, C = _dense_data(n, d, k, 3.0, seed=1)
     eng, key, lab, mind, _ = _run(X, C, 0.0, "fp32")
@@ -115,7 +123,7 @@ def test_fp32_estep_delta0_is_exact_argmin():
 
 
 @pytest.mark.parametrize("n,d,k", [(3000, 100, 1000), (2049, 16, 70), (5000, 64, 256)])
-def test_fp32_estep_padded_shapes(n, d, k):
+def test_fp32_estep_padded_shapes(n, d, k, path):
     """d and k not multiples of the tile: zero-padded features, padding
     centroids (65504 norm) never win."""
     rs = np.random.RandomState(n)
@@ -128,14 +136,14 @@ def test_fp32_estep_padded_shapes(n, d, k):
     assert int(((lab != lab64) & ~amb).sum()) == 0
 
 
-def test_fp32_estep_overflow_rows_go_through_fp64():
+def test_fp32_estep_overflow_rows_go_through_fp64(path):
     """Wide band (delta = 40): most rows have lanes with 3+ members and are
     re-selected by band_rows_f64 - exact fp64, so labels equal the rule's."""
     n, d, k = 4096, 256, 1024
     X, C = _dense_data(n, d, k, 3.0, seed=2)
     eng, key, lab, _, _ = _run(X, C, 40.0, "fp32")
     ovf = int(eng.buf.ovf_count.item())
-    assert ovf > 100
+    assert ovf > 100 or (path == "certified" and int(eng.buf.counts[1].item()) > 100)
     D, lab64, mn64 = _fp64_rule(X, C, 40.0, key, eng.k_pad)
     amb, _ = _ambiguous(D, mn64, 40.0, X, C)
     assert int(((lab != lab64) & ~amb).sum()) == 0
@@ -170,3 +178,51 @@ def test_qmeans_default_precision_is_fp32_faithful():
     cpu = QMeans(n_clusters=4, delta=0.5, true_distance_estimate=False, n_init=1, max_iter=20,
                  random_state=0, device="cpu").fit(X.astype(np.float64))
     assert np.isclose(est.inertia_, cpu.inertia_, rtol=1e-4)
+
+
+def _blobs(n, d, k, seed=0, spread=4.0):
+    rs = np.random.RandomState(seed)
+    G = rs.randn(k, d) * spread
+    X = G[rs.randint(k, size=n)] + rs.randn(n, d)
+    C = G + 0.3 * rs.randn(k, d)
+    # a few centroid pairs close together: real multi-candidate rows
+    C[1::7] = C[0::7][: len(C[1::7])] + 0.05 * rs.randn(len(C[1::7]), d)
+    return X.astype(np.float32), C.astype(np.float32)
+
+
+@pytest.mark.parametrize("delta", [0.0, 0.5, 3.0])
+def test_certified_estep_is_fp64_exact(delta, monkeypatch):
+    """Separated data (the bench regime): the filter resolves nearly every
+    row; labels equal the fp64 rule's EXACTLY on every row it resolved, and
+    the min distances (M-step fill / fill_mind) are the fp64 ones."""
+    monkeypatch.setenv("SQ_ESTEP_FILTER", "1")
+    n, d, k = 20000, 256, 512
+    X, C = _blobs(n, d, k)
+    eng, key, lab, mind, inertia = _run(X, C, delta, "fp32")
+    dense = int(eng.buf.counts[1].item())
+    D, lab64, mn64 = _fp64_rule(X, C, delta, key, eng.k_pad)
+    dense_rows = eng.buf.dense_rows[:dense]
+    ok = torch.ones(n, dtype=torch.bool, device=D.device)
+    ok[dense_rows] = False
+    assert dense < n // 20, dense
+    assert int(((lab != lab64) & ok).sum()) == 0
+    rel = ((mind.double() - mn64).abs() / mn64.clamp(min=1e-30))[ok]
+    assert float(rel.max()) < 1e-6
+    assert abs(float(inertia) - float(mn64.sum())) <= 1e-6 * float(mn64.sum())
+
+
+def test_certified_step_fills_mind_in_the_mstep(monkeypatch):
+    """One Lloyd step: the segmented reduce computes the marked rows' exact
+    distances; the iteration inertia is the fp64 sum of min distances."""
+    monkeypatch.setenv("SQ_ESTEP_FILTER", "1")
+    n, d, k = 20000, 256, 512
+    X, C = _blobs(n, d, k, seed=4)
+    Xt = torch.from_numpy(X).cuda()
+    eng = LloydEngine(Xt, k, delta=0.5, seed=7, gemm_precision="fp32")
+    eng.set_centers(torch.from_numpy(C).cuda())
+    key = eng._key("band_select")
+    lab, sc = eng.step()
+    torch.cuda.synchronize()
+    D, lab64, mn64 = _fp64_rule(X, C, 0.5, key, eng.k_pad)
+    assert bool((eng.buf.mind[:n] >= 0).all())
+    assert abs(float(sc[0]) - float(mn64.sum())) <= 1e-6 * float(mn64.sum())
