@@ -1,25 +1,32 @@
 #!/usr/bin/env python
 """Headline benchmark: q-means Lloyd-iteration throughput on 10M x 256,
 k = 1024, row-sharded over N MI355X GPUs (BASELINE.json config 3), plus the
-qPCA wall-clock on the same matrix (config 2/metric part 2) as an extra.
+q-means fit wall-clock and the qPCA wall-clocks (configs 2/5) as extras.
 
 One step = one full q-means iteration of the reference's delta-means path
 (``_dmeans.py:534-671`` with ``delta > 0``, ``true_distance_estimate=False``,
-``intermediate_error=True``, Gaussian tomography): fused MFMA distance +
-delta-band E-step, segmented centroid reduce, one packed RCCL all-reduce,
-centroid finalise with truncated-normal tomography noise, convergence
-scalars read back to the host.  Nothing is skipped inside the timed region.
+``intermediate_error=True``, Gaussian tomography) at REFERENCE PRECISION:
+fp32 data, the certified E-step (csrc/estep_f32.hip: fp16 MFMA filter with a
+rigorous error bound + fp64 re-check of the candidates -> the fp64 delta-band
+labels of ``_dmeans.py:742-751``; crowded rows through the fp32-faithful
+3-pass kernel), the segmented centroid reduce that also yields the exact fp64
+min distances, one packed RCCL all-reduce, centroid finalise with
+truncated-normal tomography noise, convergence scalars read back to the host.
+Nothing is skipped inside the timed region.
 
 Strong scaling: the 10M rows are split across ranks (each rank generates its
 own shard in HBM from the global Philox stream - same dataset for every N).
 
     python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+    (N > 1 without torchrun: re-launched under torch.distributed.run, one
+     process per GPU, before any GPU call)
 """
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,58 +36,122 @@ import torch
 BASELINE_SAMPLES_PER_S = 3.7e3   # reference q-means iteration, 8-core Xeon
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=10_000_000)
-    ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--rows", dest="n", type=int, default=10_000_000)
+    ap.add_argument("--features", dest="d", type=int, default=256)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--delta", type=float, default=0.5)
     ap.add_argument("--blobs", type=int, default=1024)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="fp32: reference precision (default); bf16: fast approximate E-step")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--no-qpca", action="store_true")
+    ap.add_argument("--no-fit", action="store_true")
+    ap.add_argument("--fit-iters", type=int, default=10)
     ap.add_argument("--seed", type=int, default=2024)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def _qpca_extra(extra, name, sa, comm, dev, solver, n_components=16):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn(a):
+    """--gpus N > 1 outside torchrun: run N ranks under torch.distributed.run
+    (one process per GPU) as a child and exit with its code.  No GPU call has
+    been made in this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def _max_over_ranks(comm, dev, v):
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+    comm.all_reduce_(t, op="max")
+    return float(t.item())
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def _qpca_extra(extra, name, sa, comm, dev, solver, n_components=16, true_tomography=False):
     """Wall-clock of a QPCA fit with the quantum extras of ``_qPCA.py:357-465``
-    (CPE singular values, Theorem 11 top-k extraction + Gaussian tomography);
-    one untimed warm fit first.  Never breaks the headline line."""
+    (CPE singular values, Theorem 11 top-k extraction + tomography of the
+    singular vectors); one untimed warm fit first.  Never breaks the line."""
     try:
         from sq_learn_amd.models.decomposition import QPCA
         q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev).fit(sa)
         theta = 0.5 * float(q.singular_values_[n_components - 1])
-        torch.cuda.synchronize()
+        _sync(dev)
         comm.barrier()
         t0 = time.perf_counter()
         q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev)
         q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True,
-              true_tomography=False)
-        torch.cuda.synchronize()
+              true_tomography=true_tomography)
+        _sync(dev)
         comm.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        comm.all_reduce_(el, op="max")
-        extra[name] = float(el.item())
+        extra[name] = _max_over_ranks(comm, dev, time.perf_counter() - t0)
     except Exception as e:  # qPCA must not break the headline line
         extra[name + "_error"] = repr(e)[:200]
 
 
-def main():
-    a = parse()
+def _fit_extra(extra, a, sa, comm, dev, init):
+    """Wall-clock of a whole QMeans.fit (prelude: eta, mu(A), condition
+    number; centring; initialisation; ``fit_iters`` Lloyd iterations with
+    tol = 0; final E-step) on the same matrix (BASELINE: fit wall-clock at a
+    fixed max_iter)."""
+    name = f"fit_wall_s_{init.replace('|', 'par').replace('+', 'pp')}_{a.fit_iters}it"
+    try:
+        from sq_learn_amd.models.cluster import QMeans
+        kw = dict(n_clusters=a.k, delta=a.delta, true_distance_estimate=False,
+                  intermediate_error=True, true_tomography=False, init=init, n_init=1,
+                  max_iter=a.fit_iters, tol=0.0, random_state=a.seed, device=dev,
+                  gemm_precision=a.dtype)
+        _sync(dev)
+        comm.barrier()
+        t0 = time.perf_counter()
+        est = QMeans(**kw).fit(sa)
+        _sync(dev)
+        comm.barrier()
+        extra[name] = _max_over_ranks(comm, dev, time.perf_counter() - t0)
+        extra[name + "_n_iter"] = int(est.n_iter_)
+    except Exception as e:
+        extra[name + "_error"] = repr(e)[:200]
+
+
+def main(argv=None):
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return _spawn(a)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+
     from sq_learn_amd.parallel.comm import init_distributed, shard_bounds, Comm
     from sq_learn_amd.utils.datasets import make_blobs_device
     from sq_learn_amd.models.cluster._lloyd import LloydEngine
     from sq_learn_amd.models._data import Data, gather_rows
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    comm = init_distributed() if world > 1 else Comm(None)
+    gpu = a.device == "cuda"
+    comm = init_distributed(backend=None if gpu else "gloo") if world > 1 else Comm(None)
     rank = comm.rank
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
-    torch.cuda.set_device(dev)
+    if gpu:
+        dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
 
     start, stop = shard_bounds(a.n, rank, comm.world_size)
@@ -93,7 +164,7 @@ def main():
 
     eng = LloydEngine(X, a.k, delta=a.delta, true_distance_estimate=False, intermediate_error=True,
                       true_tomography=False, seed=a.seed, comm=comm, row_offset=start,
-                      gemm_precision="bf16")
+                      gemm_precision=a.dtype)
     eng.set_centers(C0)
 
     def step():
@@ -103,31 +174,42 @@ def main():
     for _ in range(a.warmup):
         step()
     comm.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
         last = step()
-    torch.cuda.synchronize()
+    _sync(dev)
     comm.barrier()
-    t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    comm.all_reduce_(el, op="max")
-    elapsed = float(el.item())
+    elapsed = _max_over_ranks(comm, dev, time.perf_counter() - t0)
     ms_per_step = elapsed / a.steps * 1e3
     value = a.n * a.steps / elapsed
-    ovf = int(last[2]) if last else 0
 
-    extra = {"inertia_last": last[0] if last else None, "overflow_rows_last": ovf,
-             "rows_per_gpu": stop - start, "delta": a.delta, "k": a.k, "d": a.d}
-    if not a.no_qpca:
-        del eng
+    extra = {"inertia_last": last[0] if last else None, "rows_per_gpu": stop - start,
+             "delta": a.delta, "k": a.k, "d": a.d,
+             "precision": ("certified fp64 delta-band labels (fp16 MFMA filter + fp64 re-check)"
+                           if a.dtype == "fp32" else "bf16 operands (approximate band edges)")}
+    if eng.fast and gpu:
+        cnt = eng.buf.counts.tolist()
+        extra["overflow_rows_last"], extra["dense_rows_last"] = int(cnt[0]), int(cnt[1])
+        # per-phase ms of 3 more (untimed) iterations, CUDA events per phase
+        ph = {}
+        for _ in range(3):
+            for kk, v in eng.step_phases().items():
+                ph[kk] = ph.get(kk, 0.0) + v / 3.0
+        extra["phase_ms"] = {kk: round(v, 4) for kk, v in ph.items()}
+
+    del eng
+    if gpu:
         torch.cuda.empty_cache()
-        from sq_learn_amd.parallel.sharding import ShardedArray
+    from sq_learn_amd.parallel.sharding import ShardedArray
+    sa = ShardedArray(X, a.n, start, comm)
+    if not a.no_fit:
+        _fit_extra(extra, a, sa, comm, dev, "random")
+    if not a.no_qpca and gpu:
         # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
-        _qpca_extra(extra, "qpca_10Mx256_full_fit_s", ShardedArray(X, a.n, start, comm), comm,
-                    dev, "full")
-        del X
+        _qpca_extra(extra, "qpca_10Mx256_full_fit_s", sa, comm, dev, "full")
+        del X, sa
         torch.cuda.empty_cache()
         # BASELINE config 2: qPCA 1M x 512 bf16 (low-rank + tail), full and randomized
         from sq_learn_amd.utils.datasets import make_low_rank_device
@@ -152,8 +234,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": value / BASELINE_SAMPLES_PER_S,
             "dtype": a.dtype,
-            "data": "synthetic (on-device make_blobs, Philox-keyed, 1024 blobs)",
-            "config": {"model": f"q-means k={a.k} delta={a.delta} (10M x 256 synthetic)",
+            "data": f"synthetic (on-device make_blobs, Philox-keyed, {a.blobs} blobs)",
+            "config": {"model": f"q-means k={a.k} delta={a.delta} ({a.n} x {a.d} synthetic)",
                        "global_batch": a.n, "seq_len": a.d,
                        "parallelism": f"dp{comm.world_size}"},
             "extra": extra,
@@ -162,6 +244,7 @@ def main():
     if comm.distributed:
         import torch.distributed as dist
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

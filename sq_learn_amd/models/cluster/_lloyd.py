@@ -300,9 +300,11 @@ class LloydEngine:
         # make_gaussian_est on the flattened k x d centre matrix (Utility.py:97)
         return (self.delta / 2.0) / math.sqrt(self.k * self.d)
 
-    def mstep(self, labels, inertia):
+    def mstep(self, labels, inertia, events=None):
         """Centroid update from labels; returns the device scalar tensor
-        [inertia, shift, overflow_count] (one D2H read by the caller)."""
+        [inertia, shift, overflow_count] (one D2H read by the caller).
+        ``events`` (two CUDA events, optional) are recorded after the
+        segmented reduce and after the all-reduce (phase timing)."""
         noise_key = self._key("trunc_normal")
         if self.fast:
             with tracing.range("mstep"):
@@ -319,8 +321,12 @@ class LloydEngine:
                 sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
                 K.pack_stats_native(sums, self.counts, inertia, self.packed, self.k, self.d,
                                     self.rws, weighted=self.weights is not None)
+            if events is not None:
+                events[0].record()
             with tracing.range("allreduce"):
                 self.comm.all_reduce_(self.packed)
+            if events is not None:
+                events[1].record()
             with tracing.range("finalize"):
                 K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
                                            self.shift, self.k, self.d, self._noise_bound(),
@@ -399,6 +405,26 @@ class LloydEngine:
         self.set_centers(est.to(self.C.dtype))
 
     # ---------------------------------------------------------- iteration
+    def step_phases(self):
+        """One Lloyd iteration (GPU fast path) timed per phase with CUDA
+        events: E-step, segmented reduce (+ min distances, inertia, packing),
+        all-reduce, finalize; plus the host wall of the whole step including
+        the scalar read-back.  Returns {phase: ms}."""
+        import time
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        t0 = time.perf_counter()
+        ev[0].record()
+        labels, mind, inertia = self._estep(self._key("band_select"))
+        ev[1].record()
+        sc = self.mstep(labels, inertia, events=(ev[2], ev[3]))
+        ev[4].record()
+        sc.tolist()
+        wall = (time.perf_counter() - t0) * 1e3
+        self.it += 1
+        return {"estep": ev[0].elapsed_time(ev[1]), "reduce": ev[1].elapsed_time(ev[2]),
+                "allreduce": ev[2].elapsed_time(ev[3]), "finalize": ev[3].elapsed_time(ev[4]),
+                "step_wall": wall}
+
     def step(self):
         """One Lloyd iteration; returns (labels, scalars_tensor)."""
         labels, mind, inertia = self._estep(self._key("band_select"))
