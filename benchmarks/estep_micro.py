@@ -39,13 +39,14 @@ else:
     Cop = torch.empty(K.operand_f16_shape(kp, dp), dtype=torch.float16, device=dev)
     K.centers_to_f16_native(C, Cop, a.k, a.d, dp, kp, alpha)
     cmax2 = ((C.double() * alpha) ** 2).sum(1).max().float().reshape(1)
+    Xh = (X * alpha).to(torch.float16)
 
 
 def run_estep():
     if a.prec == "bf16":
         K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
     elif a.prec == "x64":
-        K.estep_x64_native(X, Cop, C, xn, cmax2, a.k, a.delta, alpha, key, 0, buf)
+        K.estep_x64_native(Xh, X, Cop, C, xn, cmax2, a.k, a.delta, alpha, key, 0, buf)
     else:
         K.estep_f32_native(X, Cop, xn, C, a.k, a.delta, alpha, key, 0, buf)
 

@@ -413,34 +413,44 @@ __global__ void __launch_bounds__(256) band_rows_f64_kernel(
 //                     min distance is left to the M-step (mind = -1 marker:
 //                     the segmented reduce computes |x - c_label|^2 in fp64
 //                     while it streams the row anyway);
-//   * 2..16         : fp64 re-check here (x row re-read from L2, centroid rows
-//                     from L2), min, band, kappa-rank pick, exact mind;
+//   * 2..16         : fp64 re-check here, min, band, kappa-rank pick, exact
+//                     mind.  The (row, candidate) pairs of the wave are
+//                     flattened and 8 lanes compute one pair (32 features
+//                     each, every load of the round in flight at once);
 //   * more, or a lane whose 3rd value is a candidate ("dense" rows, where the
 //     band edge is crowded beyond what one fp16 pass can separate): the row
 //     goes to a device list for the fp32-faithful 3-pass kernel
 //     (estep_f32_kernel in list mode).
-// 8 waves (2 per SIMD) x 32 rows per workgroup share each staged tile (the
-// 1-pass kernel needs <= 256 registers); only the HI region of each operand
-// tile is staged (34 KiB per slot at d = 256).
+// The A operand is the fp16 hi copy of the rows (alpha x rounded once at
+// setup, 2 B per value: the same HBM stream as the bf16 kernel) and the next
+// block's fragments are loaded right after the last MFMA of a block, so their
+// latency hides behind the epilogue, the candidate extraction and the
+// re-check.  8 waves (2 per SIMD) x 32 rows per workgroup share each staged
+// tile; only the HI region of each operand tile is staged (34 KiB per slot at
+// d = 256).
 constexpr int kMaxCand = 16;
 template <int KSD>
 __global__ void __launch_bounds__(512) estep_x64_kernel(
-    const float* __restrict__ X, const _Float16* __restrict__ C, const float* __restrict__ Cm,
-    const float* __restrict__ xn, const float* __restrict__ cmax2_p, int* __restrict__ labels,
-    float* __restrict__ mind, long long* __restrict__ dense_rows, int* __restrict__ dense_count,
-    long long n, int k_pad, int d, float alpha, float delta_s, double delta, RngKey key,
-    long long row_offset, int dense_cap, int qbits) {
+    const _Float16* __restrict__ Xh, const float* __restrict__ X, const _Float16* __restrict__ C,
+    const float* __restrict__ Cm, const float* __restrict__ xn, const float* __restrict__ cmax2_p,
+    int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ dense_rows,
+    int* __restrict__ dense_count, long long n, int k_pad, float alpha, float delta_s,
+    double delta, RngKey key, long long row_offset, int dense_cap, int qbits) {
   constexpr int NW = 8;
   constexpr int DX = KSD * 16;
   constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
   constexpr int TILE_STRIDE = (2 * KSD + 1) * 2048;
   constexpr int PIECES = HI_BYTES / 1024;
   constexpr int ROWS = NW * 32;
+  constexpr int LPP = DX >= 64 ? 16 : DX / 4;  // lanes per (row, candidate) pair in the re-check
+  constexpr int FPL = DX / LPP;                // features per lane (a multiple of 4)
+  constexpr int MAXP = 32 * kMaxCand;          // (row, candidate) pairs per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * HI_BYTES; };
   int* cand_all = reinterpret_cast<int*>(smem + 2 * HI_BYTES);       // [NW][32][kMaxCand]
   int* cnt_all = cand_all + NW * 32 * kMaxCand;                       // [NW][32]
   double* dist_all = reinterpret_cast<double*>(cnt_all + NW * 32);    // [NW][32][kMaxCand]
+  int* pair_all = reinterpret_cast<int*>(dist_all + NW * MAXP);       // [NW][MAXP]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -453,6 +463,8 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
   if (blk >= nblk) return;
   int* cand = cand_all + wave * 32 * kMaxCand;
   int* cnt = cnt_all + wave * 32;
+  double* dist = dist_all + wave * MAXP;
+  int* pairs = pair_all + wave * MAXP;
   const uint32_t qmask = (1u << qbits) - 1u;
   const uint32_t keep = ~qmask;
   // rigorous bound constants (fp32, rounded up by the 1.0625 / 1+2^-16 factors)
@@ -472,19 +484,11 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
   };
 
   f16x8 ah[KSD];
-  auto load_split = [&](long long b) {
+  auto load_a = [&](long long b) {
     const long long r = b * ROWS + wave * 32 + r32;
-    const float* xr = X + (size_t)(r < n ? r : n - 1) * DX + half * 8;
-    // whole-vector assignment: element inserts into ah[ks] would keep the
-    // previous block's fragments alive (register pressure -> spills)
+    const _Float16* xr = Xh + (size_t)(r < n ? r : n - 1) * DX + half * 8;
 #pragma unroll
-    for (int ks = 0; ks < KSD; ++ks) {
-      const float4 r0 = *reinterpret_cast<const float4*>(xr + ks * 16);
-      const float4 r1 = *reinterpret_cast<const float4*>(xr + ks * 16 + 4);
-      ah[ks] = (f16x8){(_Float16)(r0.x * alpha), (_Float16)(r0.y * alpha), (_Float16)(r0.z * alpha),
-                       (_Float16)(r0.w * alpha), (_Float16)(r1.x * alpha), (_Float16)(r1.y * alpha),
-                       (_Float16)(r1.z * alpha), (_Float16)(r1.w * alpha)};
-    }
+    for (int ks = 0; ks < KSD; ++ks) ah[ks] = *reinterpret_cast<const f16x8*>(xr + ks * 16);
   };
   f16x8 aug = (f16x8)0;
   if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
@@ -544,7 +548,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 
   int G = 0;
   stage(0);
-  load_split(blk);
+  load_a(blk);
   sync_tile();
 
   for (; blk < nblk; blk += gridDim.x) {
@@ -559,6 +563,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     int t = 0;
     while (true) {
       if (t + 1 >= n_tiles) {
+        load_a(blk + gridDim.x);   // clamped rows: unconditional (no phi on ah)
         tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
         break;
       }
@@ -568,6 +573,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
       ++t;
       ++G;
       if (t + 1 >= n_tiles) {
+        load_a(blk + gridDim.x);
         tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
         break;
       }
@@ -578,8 +584,6 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
       ++G;
     }
     ++G;
-    // the next block's rows: issued now, their latency hides behind the
-    // candidate extraction and the fp64 re-check (ah is dead after the sweep)
 
     // ---- row minimum (packed) by the transposed reduce-scatter: lane r32
     // even ends with the min of row irow = r32 >> 1 of its half
@@ -629,8 +633,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 
-    // ---- exact re-check, A layout: lanes r32 and r32 + 32 share row r32
-    // (features half*8 + 16 ks + e), one shuffle joins the two halves
+    // ---- classify the wave's 32 rows (lane r32 < 32 owns row r32)
     const long long g = row0 + r32;
     const bool valid = g < n;
     const int c_r = cnt[r32];
@@ -646,77 +649,75 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
         mind[g] = -1.0f;   // filled by the M-step's segmented reduce
       }
     }
-    const unsigned long long mm = __ballot(multi);
-    if (mm) {
-      int maxc = multi ? c_r : 0;
+    // flatten the multi rows' (row, candidate) pairs: exclusive scan of the
+    // per-row counts over lanes 0..31
+    const int pc = (multi && half == 0) ? c_r : 0;
+    int incl = pc;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) maxc = max(maxc, __shfl_xor(maxc, o, 64));
-      const float* xr = X + (size_t)(valid ? g : 0) * DX + half * 8;
-      double* dl = dist_all + (wave * 32 + r32) * kMaxCand;
-      const int* cl = cand + r32 * kMaxCand;
-#pragma unroll 1
-      for (int c = 0; c < maxc; ++c) {   // wave-uniform trip count
-        const int j = (multi && c < c_r) ? cl[c] : 0;
-        const float* cr = Cm + (size_t)j * d;
-        double s = 0.0;
-        if (d == DX) {
-          const float* cc = cr + half * 8;
-#pragma unroll 2
-          for (int ks = 0; ks < KSD; ++ks) {
-            const float4 x0 = *reinterpret_cast<const float4*>(xr + ks * 16);
-            const float4 x1 = *reinterpret_cast<const float4*>(xr + ks * 16 + 4);
-            const float4 c0 = *reinterpret_cast<const float4*>(cc + ks * 16);
-            const float4 c1 = *reinterpret_cast<const float4*>(cc + ks * 16 + 4);
-            const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            const float ca[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const double df = (double)xa[e] - (double)ca[e];
-              s = fma(df, df, s);
-            }
-          }
-        } else {
-#pragma unroll 1
-          for (int ks = 0; ks < KSD; ++ks) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int f = ks * 16 + half * 8 + e;
-              if (f < d) {
-                const double df = (double)xr[ks * 16 + e] - (double)cr[f];
-                s = fma(df, df, s);
-              }
-            }
-          }
-        }
-        s += __shfl_xor(s, 32, 64);
-        if (half == 0) dl[c] = s;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (multi && half == 0) {
-        double dmin = dl[0];
-        for (int c = 1; c < c_r; ++c) dmin = fmin(dmin, dl[c]);
-        const double thr = dmin + delta;
-        int b = 0;
-        for (int c = 0; c < c_r; ++c) b += dl[c] <= thr ? 1 : 0;
-        const int r = band_rank(band_u(key, row_offset + g), b);
-        // the band member of kappa rank r, kappa(j) = (j mod 32, j div 32)
-        int pick = cl[0];
-        for (int c = 0; c < c_r; ++c) {
-          if (!(dl[c] <= thr)) continue;
-          const int jc = cl[c];
-          const int kc = ((jc & 31) << 20) | (jc >> 5);
-          int rank = 0;
-          for (int c2 = 0; c2 < c_r; ++c2) {
-            const int j2 = cl[c2];
-            rank += (dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
-          }
-          if (rank == r) pick = jc;
-        }
-        labels[g] = pick;
-        mind[g] = (float)dmin;
-      }
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
     }
-    if (blk + gridDim.x < nblk) load_split(blk + gridDim.x);
+    const int npairs = __shfl(incl, 63, 64);
+    for (int c = 0; c < pc; ++c) pairs[incl - pc + c] = (r32 << 8) | c;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- exact distances: 8 lanes per pair, FPL features per lane, all the
+    // round's loads issued before the first FMA
+    for (int base = 0; base < npairs; base += 64 / LPP) {   // wave-uniform
+      const int pi = base + lane / LPP;
+      const int sub = lane % LPP;
+      const bool live = pi < npairs;
+      const int pr = live ? pairs[pi] : 0;
+      const int rr = pr >> 8, cc = pr & 0xFF;
+      const int j = live ? cand[rr * kMaxCand + cc] : 0;
+      const long long gr = row0 + rr;
+      const float* xr = X + (size_t)(live ? gr : 0) * DX + sub * FPL;
+      const float* cr = Cm + (size_t)j * DX + sub * FPL;
+      float4 xv[FPL / 4], cv[FPL / 4];
+#pragma unroll
+      for (int q = 0; q < FPL / 4; ++q) {
+        xv[q] = *reinterpret_cast<const float4*>(xr + 4 * q);
+        cv[q] = *reinterpret_cast<const float4*>(cr + 4 * q);
+      }
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < FPL / 4; ++q) {
+        const double e0 = (double)xv[q].x - (double)cv[q].x, e1 = (double)xv[q].y - (double)cv[q].y;
+        const double e2 = (double)xv[q].z - (double)cv[q].z, e3 = (double)xv[q].w - (double)cv[q].w;
+        s = fma(e0, e0, fma(e1, e1, fma(e2, e2, fma(e3, e3, s))));
+      }
+#pragma unroll
+      for (int o = 1; o < LPP; o <<= 1) s += __shfl_xor(s, o, 64);
+      if (live && sub == 0) dist[rr * kMaxCand + cc] = s;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (multi && half == 0) {
+      const double* dl = dist + r32 * kMaxCand;
+      const int* cl = cand + r32 * kMaxCand;
+      double dmin = dl[0];
+      for (int c = 1; c < c_r; ++c) dmin = fmin(dmin, dl[c]);
+      const double thr = dmin + delta;
+      int b = 0;
+      for (int c = 0; c < c_r; ++c) b += dl[c] <= thr ? 1 : 0;
+      const int r = band_rank(band_u(key, row_offset + g), b);
+      // the band member of kappa rank r, kappa(j) = (j mod 32, j div 32)
+      int pick = cl[0];
+      for (int c = 0; c < c_r; ++c) {
+        if (!(dl[c] <= thr)) continue;
+        const int jc = cl[c];
+        const int kc = ((jc & 31) << 20) | (jc >> 5);
+        int rank = 0;
+        for (int c2 = 0; c2 < c_r; ++c2) {
+          const int j2 = cl[c2];
+          rank += (dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
+        }
+        if (rank == r) pick = jc;
+      }
+      labels[g] = pick;
+      mind[g] = (float)dmin;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -866,14 +867,14 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
 }
 
 template <int KSD>
-static int launch_estep_x64(const void* X, const void* C, const void* Cm, const void* xn,
-                            const void* cmax2, void* labels, void* mind, void* dense_rows,
-                            void* dense_count, long long n, int k, int k_pad, int d, float alpha,
-                            float delta_s, double delta, RngKey key, long long row_offset,
-                            int dense_cap, hipStream_t st) {
+static int launch_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm,
+                            const void* xn, const void* cmax2, void* labels, void* mind,
+                            void* dense_rows, void* dense_count, long long n, int k_pad,
+                            float alpha, float delta_s, double delta, RngKey key,
+                            long long row_offset, int dense_cap, hipStream_t st) {
   constexpr int NW = 8;
   const size_t lds = 2 * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4 +
-                     (size_t)NW * 32 * kMaxCand * 8;
+                     (size_t)NW * 32 * kMaxCand * (8 + 4);
   auto kern = estep_x64_kernel<KSD>;
   static bool attr = false;
   if (!attr) {
@@ -892,10 +893,11 @@ static int launch_estep_x64(const void* X, const void* C, const void* Cm, const 
   while ((1 << qbits) < 2 * (k_pad / kTileN)) ++qbits;
   const long long nblk = (n + NW * 32 - 1) / (NW * 32);
   const unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const float*)X,
-                     (const _Float16*)C, (const float*)Cm, (const float*)xn, (const float*)cmax2,
-                     (int*)labels, (float*)mind, (long long*)dense_rows, (int*)dense_count, n,
-                     k_pad, d, alpha, delta_s, delta, key, row_offset, dense_cap, qbits);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const _Float16*)Xh,
+                     (const float*)X, (const _Float16*)C, (const float*)Cm, (const float*)xn,
+                     (const float*)cmax2, (int*)labels, (float*)mind, (long long*)dense_rows,
+                     (int*)dense_count, n, k_pad, alpha, delta_s, delta, key, row_offset,
+                     dense_cap, qbits);
   return (int)hipGetLastError();
 }
 
@@ -937,11 +939,13 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 // overflow rows through band_rows_f64.  counts[0] = 3-pass overflow rows,
 // counts[1] = dense rows; both must be zero on entry.  mind holds -1 for rows
 // whose distance the M-step (or fill_mind) computes; no inertia here.
-int sq_estep_x64(const void* X, const void* C, const void* Cm, const void* xn, const void* cmax2,
-                 void* labels, void* mind, void* dense_rows, void* ovf_rows, void* counts,
-                 void* part, int part_cap, long long n, int d, int d_pad, int k, int k_pad,
-                 double alpha, double delta, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
-                 long long row_offset, void* stream) {
+// Xh: fp16(alpha x) [n][d_pad]; X: fp32 [n][d_pad]; Cm: fp32 centroids
+// [k][d_pad] (zero-padded like X); C: the fp16-split operand.
+int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
+                 const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
+                 void* counts, void* part, int part_cap, long long n, int d, int d_pad, int k,
+                 int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
+                 unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
   if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 4096 || k > k_pad || d > d_pad)
     return (int)hipErrorInvalidValue;
@@ -956,8 +960,9 @@ int sq_estep_x64(const void* X, const void* C, const void* Cm, const void* xn, c
   switch (d_pad) {
 #define CASE(KSD)                                                                                \
   case KSD * 16:                                                                                 \
-    rc = launch_estep_x64<KSD>(X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1, n, k,     \
-                               k_pad, d, fa, ds, delta, key, row_offset, (int)min(n, 2147483647LL), st); \
+    rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1, n,    \
+                               k_pad, fa, ds, delta, key, row_offset, (int)min(n, 2147483647LL),  \
+                               st);                                                              \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \
@@ -971,7 +976,7 @@ int sq_estep_x64(const void* X, const void* C, const void* Cm, const void* xn, c
   if (rc) return rc;
   hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(n < 2048 ? n : 2048)), dim3(256), 0,
                      st, (const float*)X, (const float*)Cm, (const long long*)ovf_rows,
-                     (const int*)cnt, (int*)labels, n, d_pad, d, k, delta, key, row_offset);
+                     (const int*)cnt, (int*)labels, n, d_pad, d_pad, k, delta, key, row_offset);
   return (int)hipGetLastError();
 }
 

@@ -137,6 +137,10 @@ class LloydEngine:
         # the fp32-faithful 3-pass kernel on every row instead (A/B, tests)
         import os
         self.certified = os.environ.get("SQ_ESTEP_FILTER", "1") != "0"
+        # the filter's A operand: fp16(alpha x), rounded once (2 B per value,
+        # the bf16 kernel's HBM stream); exact fp32 rows stay for the re-check
+        # and the M-step
+        self.Xh16 = (Xf * self.alpha).to(torch.float16) if self.certified else None
         self._prepare_reduce()
         self.mind_part = torch.zeros(512, dtype=torch.float64, device=dev)
 
@@ -231,8 +235,9 @@ class LloydEngine:
     def _estep(self, key):
         if self.fast and self.C_op is not None and self.certified:
             with tracing.range("estep_x64"):
-                lab, mind = K.estep_x64_native(self.Xf32, self.C_op, self.C, self.xn, self.cmax2,
-                                               self.k, self.delta, self.alpha, key,
+                Cp = self.C if self.d == self.d_pad else self._padded_centers()
+                lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
+                                               self.cmax2, self.k, self.delta, self.alpha, key,
                                                self.row_offset, self.buf)
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
@@ -390,7 +395,7 @@ class LloydEngine:
 
     def _padded_centers(self):
         if getattr(self, "_Cpad", None) is None:
-            self._Cpad = torch.zeros((self.k, self.dm), dtype=torch.float32, device=self.device)
+            self._Cpad = torch.zeros((self.k, self.d_pad), dtype=torch.float32, device=self.device)
         self._Cpad[:, :self.d].copy_(self.C)
         return self._Cpad
 

@@ -485,7 +485,7 @@ def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_o
     return buf.labels, buf.mind
 
 
-def estep_x64_native(Xf, C_op, C_master, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
+def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
                      buf: EStepBuffers, stream=None):
     """Certified E-step (``estep_x64_kernel``): one fp16 MFMA pass with a
     rigorous error bound, fp64 re-check of the candidate centroids, dense rows
@@ -494,22 +494,23 @@ def estep_x64_native(Xf, C_op, C_master, xn, cmax2, k, delta, alpha, key: RngKey
     M-step's row pass or ``fill_mind_native``).  No host sync."""
     n, d_pad = Xf.shape
     k_pad = C_op.shape[0] * 64
-    d = C_master.shape[1]
     assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in FAST_D
+    assert Xh.dtype == torch.float16 and Xh.is_contiguous() and tuple(Xh.shape) == (n, d_pad)
     assert C_op.dtype == torch.float16 and tuple(C_op.shape) == operand_f16_shape(k_pad, d_pad)
-    assert C_master.dtype == torch.float32 and C_master.is_contiguous() and C_master.shape[0] == k
+    assert C_pad.dtype == torch.float32 and C_pad.is_contiguous()
+    assert tuple(C_pad.shape) == (k, d_pad)
     assert cmax2.dtype == torch.float32 and xn.dtype == torch.float32 and xn.numel() >= n
-    assert k <= k_pad <= 4096 and d <= d_pad and buf.labels.numel() >= n
+    assert k <= k_pad <= 4096 and buf.labels.numel() >= n
     if buf.dense_rows is None or buf.dense_rows.numel() < n:
         buf.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
     st = stream if stream is not None else nat.stream_handle(Xf.device)
     buf.counts.zero_()
     buf.ovf_clean = False
-    nat.native().estep_x64(Xf.data_ptr(), C_op.data_ptr(), C_master.data_ptr(), xn.data_ptr(),
-                           cmax2.data_ptr(), buf.labels.data_ptr(), buf.mind.data_ptr(),
-                           buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
+    nat.native().estep_x64(Xh.data_ptr(), Xf.data_ptr(), C_op.data_ptr(), C_pad.data_ptr(),
+                           xn.data_ptr(), cmax2.data_ptr(), buf.labels.data_ptr(),
+                           buf.mind.data_ptr(), buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
-                           n, d, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
+                           n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)
     return buf.labels, buf.mind
 
