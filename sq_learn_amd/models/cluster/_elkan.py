@@ -25,6 +25,7 @@ class ElkanEngine(LloydEngine):
         kw = dict(kw)
         kw["delta"] = 0.0
         kw["gemm_precision"] = "fp32"
+        kw["generic"] = True     # the bounded Elkan E-step replaces the fused one
         super().__init__(X, k, **kw)
         dt = self.Xf.dtype
         self.Xe = self.Xf.contiguous()

@@ -46,7 +46,7 @@ class LloydEngine:
     def __init__(self, X, k, *, delta=0.0, true_distance_estimate=False, intermediate_error=False,
                  true_tomography=False, tomography_kw=None, sample_weight=None, seed=0,
                  comm=None, row_offset=0, gemm_precision="fp32", ipe_Q=13, empty_policy=0,
-                 Xb=None, xn=None, failure_prob=0.0, failure_attempts=1):
+                 Xb=None, xn=None, failure_prob=0.0, failure_attempts=1, generic=False):
         self.X = X
         self.device = X.device
         self.n, self.d = X.shape
@@ -74,7 +74,10 @@ class LloydEngine:
         if gemm_precision not in ("bf16", "fp32"):
             raise ValueError("gemm_precision must be 'bf16' or 'fp32', got %r" % (gemm_precision,))
         self.precision = gemm_precision
-        self.fast = (gpu and not self.ipe and self.d_pad <= 256 and self.k_pad <= 4096)
+        # generic=True: library-GEMM distances + torch/selection kernels only
+        # (engines that replace the E-step, e.g. ElkanEngine)
+        self.fast = (gpu and not generic and not self.ipe and self.d_pad <= 256
+                     and self.k_pad <= 4096)
         self.alpha = 1.0
         self.acc_dtype = torch.float64 if not gpu else torch.float32
         if gpu:
