@@ -20,6 +20,8 @@ definitions; ``SQ_NATIVE_VARIANT=PATH.so`` makes the loader use it.
 """
 
 import argparse
+import contextlib
+import fcntl
 import os
 import subprocess
 import sys
@@ -57,6 +59,21 @@ def needs_build():
     return _newest(srcs) > os.path.getmtime(out)
 
 
+@contextlib.contextmanager
+def _build_lock(name):
+    """Cross-process build lock (``build/<name>.lock``): pytest-xdist workers,
+    gloo test ranks and torchrun ranks all call ``build()`` on first use; only
+    one compiles, the others wait and then see a fresh library."""
+    os.makedirs(os.path.join(HERE, "..", "build"), exist_ok=True)
+    fd = os.open(os.path.join(HERE, "..", "build", name + ".lock"), os.O_CREAT | os.O_RDWR, 0o644)
+    try:
+        fcntl.flock(fd, fcntl.LOCK_EX)
+        yield
+    finally:
+        fcntl.flock(fd, fcntl.LOCK_UN)
+        os.close(fd)
+
+
 def _run(cmd):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
@@ -70,6 +87,14 @@ def build(force=False, jobs=None, debug=False, verbose=False, defines=(), out=No
     out = out or ext_path()
     if not variant and not force and not needs_build():
         return out
+    with _build_lock("sq_native"):
+        # another process may have finished the same build while we waited
+        if not variant and not force and not needs_build():
+            return out
+        return _build_locked(out, variant, jobs, debug, verbose, defines)
+
+
+def _build_locked(out, variant, jobs, debug, verbose, defines):
     bdir = BUILD if not variant else os.path.join(
         BUILD, "variant_" + os.path.splitext(os.path.basename(out))[0])
     os.makedirs(bdir, exist_ok=True)
@@ -95,7 +120,7 @@ def build(force=False, jobs=None, debug=False, verbose=False, defines=(), out=No
     units = hips + ["module.cpp"]
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, units))
-    tmp = out + ".tmp"
+    tmp = f"{out}.{os.getpid()}.tmp"
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
     os.replace(tmp, out)
     return out
@@ -119,18 +144,31 @@ def host_needs_build():
     return not os.path.exists(out) or _newest(_host_sources() + [__file__]) > os.path.getmtime(out)
 
 
-def build_host(force=False, debug=False):
+def build_host(force=False, debug=False, sanitize=None, out=None):
     """Host-native library (``csrc/host/*.cpp`` -> ``_sq_host.so``, loaded
-    with ctypes): C++17 + OpenMP, no HIP dependency."""
-    out = host_path()
-    if not force and not host_needs_build():
+    with ctypes): C++17 + OpenMP, no HIP dependency.
+
+    ``sanitize="address,undefined"`` builds an instrumented copy (default
+    ``build/_sq_host_asan.so``, never the in-tree library) for CPU race /
+    memory checks: load it with ``SQ_HOST_LIB=<path>`` and
+    ``LD_PRELOAD=$(g++ -print-file-name=libasan.so)``
+    (``scripts/host_asan.sh`` runs the host-native tests that way)."""
+    if sanitize and out is None:
+        out = os.path.join(HERE, "..", "build", "_sq_host_asan.so")
+    out = out or host_path()
+    if not force and not sanitize and not host_needs_build():
         return out
-    srcs = [f for f in _host_sources() if f.endswith(".cpp")]
-    opt = ["-O0", "-g"] if debug else ["-O3"]
-    tmp = out + ".tmp"
-    _run([CXX, "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", HOST_SRC] + opt + srcs
-         + ["-o", tmp])
-    os.replace(tmp, out)
+    with _build_lock("sq_host"):
+        if not force and not sanitize and not host_needs_build():
+            return out
+        srcs = [f for f in _host_sources() if f.endswith(".cpp")]
+        opt = ["-O0", "-g"] if debug else ["-O3"]
+        if sanitize:
+            opt = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={sanitize}"]
+        tmp = f"{out}.{os.getpid()}.tmp"
+        _run([CXX, "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", HOST_SRC] + opt + srcs
+             + ["-o", tmp])
+        os.replace(tmp, out)
     return out
 
 
@@ -142,7 +180,12 @@ def main(argv=None):
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--define", action="append", default=[])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--host-sanitize", default=None,
+                    help="build only an instrumented host library, e.g. address,undefined")
     a = ap.parse_args(argv)
+    if a.host_sanitize:
+        print(build_host(force=True, sanitize=a.host_sanitize, out=a.out))
+        return 0
     path = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose,
                  defines=a.define, out=a.out)
     if a.out is None:

@@ -143,6 +143,11 @@ bool parse_line(const char* b, const char* e, Parsed* p, bool multilabel, bool z
 
 }  // namespace
 
+template <class T>
+static void copy_out(T* dst, const std::vector<T>& src) {
+  if (dst && !src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(T));
+}
+
 extern "C" {
 
 void* sqh_svml_parse(const char* buf, long long len, int multilabel, int zero_based,
@@ -182,13 +187,12 @@ void sqh_svml_sizes(void* h, long long* sizes) {
 void sqh_svml_copy(void* h, double* labels, long long* label_off, long long* qids, double* data,
                    long long* indices, long long* indptr) {
   auto* p = static_cast<Parsed*>(h);
-  std::memcpy(labels, p->labels.data(), p->labels.size() * sizeof(double));
-  if (label_off)
-    std::memcpy(label_off, p->label_off.data(), p->label_off.size() * sizeof(long long));
-  std::memcpy(qids, p->qids.data(), p->qids.size() * sizeof(long long));
-  std::memcpy(data, p->data.data(), p->data.size() * sizeof(double));
-  std::memcpy(indices, p->indices.data(), p->indices.size() * sizeof(long long));
-  std::memcpy(indptr, p->indptr.data(), p->indptr.size() * sizeof(long long));
+  copy_out(labels, p->labels);
+  copy_out(label_off, p->label_off);
+  copy_out(qids, p->qids);
+  copy_out(data, p->data);
+  copy_out(indices, p->indices);
+  copy_out(indptr, p->indptr);
 }
 
 void sqh_svml_free(void* h) { delete static_cast<Parsed*>(h); }

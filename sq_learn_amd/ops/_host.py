@@ -8,6 +8,7 @@ the GIL for the duration of each call.
 """
 
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -88,9 +89,13 @@ def lib():
     with _lock:
         if _lib is None:
             from .. import _build
-            if _build.host_needs_build():
-                _build.build_host()
-            h = ctypes.CDLL(_build.host_path())
+            override = os.environ.get("SQ_HOST_LIB")   # e.g. the ASan build
+            if override:
+                h = ctypes.CDLL(override)
+            else:
+                if _build.host_needs_build():
+                    _build.build_host()
+                h = ctypes.CDLL(_build.host_path())
             for name, (res, args) in _SIGS.items():
                 fn = getattr(h, name)
                 fn.restype = res
