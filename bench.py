@@ -88,17 +88,23 @@ def _sync(dev):
 def _qpca_extra(extra, name, sa, comm, dev, solver, n_components=16, true_tomography=False):
     """Wall-clock of a QPCA fit with the quantum extras of ``_qPCA.py:357-465``
     (CPE singular values, Theorem 11 top-k extraction + tomography of the
-    singular vectors); one untimed warm fit first.  Never breaks the line."""
+    right AND the n-long left singular vectors; on the randomized path via
+    ``quantum_truncated=True``, BASELINE config 2); one untimed warm fit
+    first.  Never breaks the line."""
     try:
         from sq_learn_amd.models.decomposition import QPCA
+        qt = solver != "full"
         q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev).fit(sa)
         theta = 0.5 * float(q.singular_values_[n_components - 1])
         _sync(dev)
         comm.barrier()
         t0 = time.perf_counter()
-        q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev)
+        q = QPCA(n_components=n_components, svd_solver=solver, random_state=0, device=dev,
+                 quantum_truncated=qt)
         q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True,
               true_tomography=true_tomography)
+        _sync(dev)
+        assert q.topk == n_components and q.estimate_left_sv is not None
         _sync(dev)
         comm.barrier()
         extra[name] = _max_over_ranks(comm, dev, time.perf_counter() - t0)
@@ -209,6 +215,8 @@ def main(argv=None):
     if not a.no_qpca and gpu:
         # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
         _qpca_extra(extra, "qpca_10Mx256_full_fit_s", sa, comm, dev, "full")
+        _qpca_extra(extra, "qpca_10Mx256_full_truetomo_fit_s", sa, comm, dev, "full",
+                    true_tomography=True)
         del X, sa
         torch.cuda.empty_cache()
         # BASELINE config 2: qPCA 1M x 512 bf16 (low-rank + tail), full and randomized
@@ -220,6 +228,8 @@ def main(argv=None):
         sa2 = ShardedArray(X2, n2, s2, comm)
         _qpca_extra(extra, "qpca_1Mx512_full_fit_s", sa2, comm, dev, "full")
         _qpca_extra(extra, "qpca_1Mx512_randomized_fit_s", sa2, comm, dev, "randomized")
+        _qpca_extra(extra, "qpca_1Mx512_randomized_truetomo_fit_s", sa2, comm, dev, "randomized",
+                    true_tomography=True)
 
     if rank == 0:
         out = {

@@ -24,6 +24,9 @@ __attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long
 __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int, int, const void*,
                                         void*, void*, int, unsigned, unsigned, unsigned, unsigned,
                                         long long, void*);
+__attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, long long,
+                                           long long, const void*, void*, long long, unsigned,
+                                           unsigned, unsigned, unsigned, const void*, int, void*);
 // pairwise_fast.hip
 __attribute__((weak)) int sq_pairwise_reduce(const void*, const void*, void*, int, int, int, int,
                                              double, int, void*);
@@ -181,6 +184,17 @@ static PyObject* py_tomography(PyObject*, PyObject* a) {
   CHECK(sq_tomography)
   return ret(sq_tomography(P(V), r, d, P(sched), T, mode, P(first), P(err), P(out), ninf, k0, k1,
                            s0, s1, roff, P(st)));
+}
+
+static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
+  unsigned long long W, wrow, Ns, cnt, sid, st; long long ldw, m, B, ldc; int level;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KLKLLKKLIIIIKiK", &W, &ldw, &wrow, &m, &B, &Ns, &cnt, &ldc, &k0, &k1,
+                        &s0, &s1, &sid, &level, &st))
+    return nullptr;
+  CHECK(sq_mnom_segments)
+  return ret(sq_mnom_segments(P(W), ldw, P(wrow), m, B, P(Ns), P(cnt), ldc, k0, k1, s0, s1, P(sid),
+                              level, P(st)));
 }
 
 static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {
@@ -408,6 +422,7 @@ static PyMethodDef methods[] = {
     {"elkan_step", py_elkan_step, METH_VARARGS, "Elkan bounded k-means assignment"},
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
+    {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},

@@ -206,6 +206,69 @@ __global__ void __launch_bounds__(256) tomography_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Multinomial over LONG outcome vectors (the left singular vectors of qPCA
+// have n = 1e6..1e7 coordinates, row-sharded over the ranks; SURVEY.md K12,
+// reference Utility.py:313-352 applied at _qPCA.py:1059-1063).
+//
+// The outcome axis is cut into segments of <= kSegP outcomes.  One workgroup
+// draws the counts of one segment given the segment's total count: the
+// segment's weights go to an LDS heap (mass[P + i] = w_i, mass[i] =
+// mass[2i] + mass[2i + 1], pairwise fp64 sums), then the count heap is split
+// top-down, cnt[2i] ~ Binomial(cnt[i], mass[2i] / mass[i]), one tree level
+// per step with a thread per node.  The host recursion (quantum/device.py
+// multinomial_long) draws the segment totals the same way one level up from
+// the segments' masses, so any length is a few launches of O(length) work.
+// Draws are keyed by (sid[b], segment, tree level, node): a pure function of
+// the key, independent of launch geometry and of the checkpoint chunking.
+constexpr int kSegP = 2048;
+
+__global__ void __launch_bounds__(256) mnom_segments_kernel(
+    const double* __restrict__ W, long long ldw, const long long* __restrict__ wrow, long long m,
+    int nseg, const double* __restrict__ Nseg, double* __restrict__ cnt, long long ldc,
+    RngKey key, const long long* __restrict__ sid, int level) {
+  __shared__ double mass[2 * kSegP];
+  __shared__ double cn[2 * kSegP];
+  const long long s = blockIdx.x;          // b * nseg + j
+  const long long b = s / nseg;
+  const int j = (int)(s % nseg);
+  const long long lo = (long long)j * kSegP;
+  const int len = (int)min((long long)kSegP, m - lo);
+  int P = 1;
+  while (P < len) P <<= 1;
+  const double* w = W + (size_t)wrow[b] * ldw + lo;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const double v = i < len ? w[i] : 0.0;
+    mass[P + i] = v > 0.0 ? v : 0.0;
+  }
+  __syncthreads();
+  for (int width = P >> 1; width >= 1; width >>= 1) {
+    for (int i = width + threadIdx.x; i < 2 * width; i += blockDim.x)
+      mass[i] = mass[2 * i] + mass[2 * i + 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cn[1] = Nseg[s];
+  __syncthreads();
+  const unsigned long long seg_ctr =
+      ((((unsigned long long)sid[b] * (unsigned long long)nseg + (unsigned long long)j) << 4) |
+       (unsigned long long)(level & 15)) << 12;
+  for (int width = 1; width < P; width <<= 1) {
+    for (int i = width + threadIdx.x; i < 2 * width; i += blockDim.x) {
+      const double n = cn[i], tot = mass[i], left = mass[2 * i];
+      double nl = 0.0;
+      if (n > 0.0 && tot > 0.0) {
+        const double pl = left / tot;
+        nl = binomial(n, pl < 0.0 ? 0.0 : (pl > 1.0 ? 1.0 : pl), key, seg_ctr | (unsigned long long)i);
+      }
+      cn[2 * i] = nl;
+      cn[2 * i + 1] = n - nl;
+    }
+    __syncthreads();
+  }
+  double* out = cnt + (size_t)b * ldc + lo;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) out[i] = cn[P + i];
+}
+
 }  // namespace sq
 
 using namespace sq;
@@ -229,5 +292,20 @@ extern "C" int sq_tomography(const void* V, int r, int d, const void* sched, int
                      (hipStream_t)stream, (const double*)V, r, d, (const long long*)sched, T,
                      mode, (const int*)first, (double*)err, (double*)out, norm_inf, key,
                      row_offset);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sq_mnom_segments(const void* W, long long ldw, const void* wrow, long long m,
+                                long long B, const void* Nseg, void* cnt, long long ldc,
+                                unsigned k0, unsigned k1, unsigned s0, unsigned s1,
+                                const void* sid, int level, void* stream) {
+  if (B <= 0 || m <= 0) return 0;
+  const long long nseg = (m + kSegP - 1) / kSegP;
+  if (nseg > (1LL << 30) || B * nseg > (1LL << 31) - 1) return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  hipLaunchKernelGGL(mnom_segments_kernel, dim3((unsigned)(B * nseg)), dim3(256), 0,
+                     (hipStream_t)stream, (const double*)W, ldw, (const long long*)wrow, m,
+                     (int)nseg, (const double*)Nseg, (double*)cnt, ldc, key,
+                     (const long long*)sid, level);
   return (int)hipGetLastError();
 }

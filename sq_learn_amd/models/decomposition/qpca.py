@@ -29,7 +29,8 @@ import torch
 
 from ...exceptions import ClassicalPathWarning
 from ...quantum import reference as Q
-from ...quantum.device import gaussian_tomography, tomography_rows_torch
+from ...quantum.device import (gaussian_tomography, tomography_rows_torch, tomography_long,
+                               consistent_phase_estimation_device)
 from ...runtime.device import to_numpy
 from ...runtime.rng import RngKey
 from ...utils.extmath import stable_cumsum, _infer_dimension, fast_logdet
@@ -45,7 +46,7 @@ _QKNOBS = ("quantum_retained_variance", "eps", "theta_major", "theta_minor", "et
            "theta_estimate", "use_computed_qcomponents", "eps_theta", "p", "estimate_all", "delta",
            "true_tomography", "fs_ratio_estimation", "norm", "stop_when_reached_accuracy",
            "incremental_measure", "faster_measure_increment", "check_sv_uniform_distribution",
-           "spectral_norm_est", "condition_number_est", "estimate_least_k")
+           "spectral_norm_est", "condition_number_est", "estimate_least_k", "quantum_truncated")
 
 
 class QPCA(_BasePCA):
@@ -59,7 +60,7 @@ class QPCA(_BasePCA):
                  norm="L2", stop_when_reached_accuracy=False, incremental_measure=False,
                  faster_measure_increment=0, check_sv_uniform_distribution=False,
                  spectral_norm_est=False, condition_number_est=False, estimate_least_k=False,
-                 device=None, preserve_norm_tomography=False):
+                 device=None, preserve_norm_tomography=False, quantum_truncated=False):
         self.n_components = n_components
         self.copy = copy
         self.whiten = whiten
@@ -91,6 +92,7 @@ class QPCA(_BasePCA):
         self.estimate_least_k = estimate_least_k
         self.device = device
         self.preserve_norm_tomography = preserve_norm_tomography
+        self.quantum_truncated = quantum_truncated
 
     # ------------------------------------------------------------ helpers
     def _rng(self, tag):
@@ -161,10 +163,14 @@ class QPCA(_BasePCA):
                 solver = "full"
         self._fit_svd_solver = solver
         self._source_kind = data.source_kind
+        self._device_type = data.device.type
+        self._comm = data.comm
+        self._row_offset = data.row_offset
         if solver == "full":
             return self._fit_full(data, n_components)
         if solver in ("arpack", "randomized"):
-            warnings.warn("Attention! This computational path is purely classic!", ClassicalPathWarning)
+            if not knobs.get("quantum_truncated"):
+                warnings.warn("Attention! This computational path is purely classic!", ClassicalPathWarning)
             return self._fit_truncated(data, n_components, solver)
         raise ValueError(f"Unrecognized svd_solver='{solver}'")
 
@@ -281,6 +287,22 @@ class QPCA(_BasePCA):
             self.noise_variance_ = 0.0
         self.spectral_norm = float(self.singular_values_[0])
         self.scaled_singular_values = self.singular_values_ / self.spectral_norm
+        if self._knobs.get("quantum_truncated"):
+            # framework extension (BASELINE config 2, "randomized_svd +
+            # tomography noise"): the reference's truncated path is purely
+            # classical (_qPCA.py:678-751); with quantum_truncated=True the
+            # quantum model of _fit_full (mu(A), CPE singular values, Theorem
+            # 9/10/11 extractors with tomography of the right AND the n-long
+            # left singular vectors) runs on the randomized factors.
+            self.frob_norm = float(np.sqrt(total_var.sum() * (n_samples - 1)))
+            self.all_components = Vt
+            self.explained_variance_all = self.explained_variance_
+            self.explained_variance_ratio_all = self.explained_variance_ratio_
+            centred = type(data)(self._centred(data, mean), data.n_global, data.row_offset,
+                                 data.comm, data.source_kind)
+            self.norm_muA, self.muA = best_mu_distributed(centred, start=0, end=1.0, step=0.1,
+                                                          fro_sq_global=self.frob_norm ** 2)
+            self._quantum_extras(centred)
         return self
 
     # ------------------------------------------------------- quantum extras
@@ -315,7 +337,15 @@ class QPCA(_BasePCA):
         / scale_denom, CPE(theta_i, eps_pe, gamma), unwrapped with unwrap_eps."""
         sv = np.clip(np.asarray(sv_scaled, dtype=np.float64), -1.0, 1.0)
         theta = 2 * np.arccos(sv) / scale_denom
-        est = Q.consistent_phase_estimation_batch(theta, eps_pe, gamma, random_state=self._rng("cpe"))
+        if getattr(self, "_device_type", "cpu") == "cuda":
+            # pe_batch_kernel draws; every rank draws the same values (same key)
+            self._cpe_calls = getattr(self, "_cpe_calls", 0) + 1
+            t = torch.as_tensor(theta, dtype=torch.float64, device="cuda")
+            est = consistent_phase_estimation_device(t, eps_pe, gamma,
+                                                     self._key("pe", self._cpe_calls)).cpu().numpy()
+        else:
+            est = Q.consistent_phase_estimation_batch(theta, eps_pe, gamma,
+                                                      random_state=self._rng("cpe"))
         return np.cos(est * (unwrap_eps + np.pi) / 2)
 
     def spectral_norm_estimation(self, epsilon, delta):
@@ -401,11 +431,28 @@ class QPCA(_BasePCA):
         return est * self.muA
 
     def _tomography(self, A, delta, true_tomography, norm, stop_when_reached_accuracy,
-                    incremental_measure, faster_measure_increment, tag):
-        """Tomography of the rows of A (numpy or device tensor)."""
+                    incremental_measure, faster_measure_increment, tag, sharded=False):
+        """Tomography of the rows of A (numpy or device tensor).  ``sharded``:
+        A holds this rank's columns of vectors whose coordinates are
+        row-sharded over the ranks (the left singular vectors of row-sharded
+        data)."""
         if delta == 0 or (hasattr(A, "shape") and A.shape[0] == 0):
             return A
         key = self._key("tomography", zlib.crc32(tag.encode()) & 0xFFFF)
+        comm = getattr(self, "_comm", None)
+        if sharded and isinstance(A, torch.Tensor) and comm is not None and comm.distributed:
+            n_glob = int(self.n_samples_)
+            if not true_tomography:
+                # Frobenius budget over the GLOBAL r x n matrix; offset keeps
+                # the ranks' Philox elements disjoint
+                return gaussian_tomography(A, delta, key, offset=int(self._row_offset) * A.shape[0],
+                                           numel=A.shape[0] * n_glob)
+            return tomography_long(A, delta, key, norm=norm,
+                                   stop_when_reached_accuracy=stop_when_reached_accuracy,
+                                   incremental_measure=incremental_measure,
+                                   faster_measure_increment=faster_measure_increment,
+                                   preserve_norm=self.preserve_norm_tomography, comm=comm,
+                                   n_global=n_glob)
         if isinstance(A, torch.Tensor):
             if not true_tomography:
                 return gaussian_tomography(A, delta, key)
@@ -449,7 +496,7 @@ class QPCA(_BasePCA):
         tk = (true_tomography, norm, stop_when_reached_accuracy, incremental_measure,
               faster_measure_increment)
         right_est = self._tomography(self.topk_right_singular_vectors, delta, *tk, tag="right")
-        left_est = self._tomography(left, delta, *tk, tag="left")
+        left_est = self._tomography(left, delta, *tk, tag="left", sharded=True)
         fro2 = self.frob_norm ** 2
         return (right_est, left_est, sv_est, (sv_est ** 2) / (self.n_samples_ - 1),
                 np.array([fs / fro2 for fs in sv_est ** 2]))
@@ -477,7 +524,7 @@ class QPCA(_BasePCA):
         tk = (true_tomography, norm, stop_when_reached_accuracy, incremental_measure,
               faster_measure_increment)
         right_est = self._tomography(self.leastk_right_singular_vectors, delta, *tk, tag="lright")
-        left_est = self._tomography(left, delta, *tk, tag="lleft")
+        left_est = self._tomography(left, delta, *tk, tag="lleft", sharded=True)
         fro2 = self.frob_norm ** 2
         return (right_est, left_est, sv_est, (sv_est ** 2) / (self.n_samples_ - 1),
                 np.array([fs / fro2 for fs in sv_est ** 2]))

@@ -95,6 +95,48 @@ def _worker(rank, world, port, outdir, case):
             np.testing.assert_allclose(q.singular_values_, qr.singular_values_, rtol=1e-8)
             np.testing.assert_allclose(q.estimate_s_values, qr.estimate_s_values, rtol=1e-12)
             assert abs(q.muA - qr.muA) < 1e-9 * qr.muA
+        elif case == "tomography":
+            # long-vector tomography of row-sharded vectors (qPCA left singular
+            # vectors): same law as the single-process draw, stopping rule
+            # evaluated on the GLOBAL error
+            from scipy import stats
+            from sq_learn_amd.parallel.comm import shard_bounds
+            from sq_learn_amd.quantum.device import tomography_long
+            from sq_learn_amd.runtime.rng import RngKey
+            rng = np.random.RandomState(3)
+            n = 1500
+            A = torch.tensor(rng.standard_normal((2, n)))
+            Vn = (A / A.norm(dim=1, keepdim=True)).numpy()
+            s0, s1 = shard_bounds(n, comm.rank, comm.world_size)
+            e_sh, e_one = [], []
+            for rep in range(25):
+                key = RngKey(rep, "tomography", 1)
+                loc = tomography_long(A[:, s0:s1], None, key, N=60000, incremental_measure=False,
+                                      comm=comm, n_global=n)
+                full = torch.cat(comm.all_gather_varlen(loc.T.contiguous())).T.numpy()
+                e_sh += list(np.linalg.norm(full - Vn, axis=1))
+                one = tomography_long(A, None, RngKey(rep, "tomography", 2), N=60000,
+                                      incremental_measure=False).numpy()
+                e_one += list(np.linalg.norm(one - Vn, axis=1))
+            assert stats.ks_2samp(e_sh, e_one).pvalue > 1e-4
+            for rep in range(3):
+                loc = tomography_long(A[:, s0:s1], 0.4, RngKey(rep, "tomography", 3), comm=comm,
+                                      n_global=n)
+                full = torch.cat(comm.all_gather_varlen(loc.T.contiguous())).T.numpy()
+                assert np.all(np.linalg.norm(full - Vn, axis=1) <= 0.4)
+            # qPCA randomized path with the quantum extras on sharded data
+            from sq_learn_amd.models.decomposition import QPCA
+            Z = rng.randn(1200, 10) @ rng.randn(10, 10)
+            sz = shard_rows(Z, comm=comm)
+            q = QPCA(n_components=3, svd_solver="randomized", random_state=0, device="cpu",
+                     quantum_truncated=True).fit(sz, eps=1e-3, theta_major=1e-6, delta=0.3,
+                                                 estimate_all=True, true_tomography=True)
+            left = torch.as_tensor(q.estimate_left_sv)
+            fullL = torch.cat(comm.all_gather_varlen(left.T.contiguous())).T.numpy()
+            Ut = torch.cat(comm.all_gather_varlen(torch.as_tensor(q.left_sv).T.contiguous())).T.numpy()
+            assert fullL.shape == (3, 1200)
+            assert np.all(np.linalg.norm(fullL - Ut, axis=1) <= 0.3)   # N = 36 n ln n / delta^2 shots
+            assert np.all(np.abs(np.linalg.norm(fullL, axis=1) - 1) < 0.2)
         elif case == "resume":
             # sharded fit with failures, crashed mid-fit on every rank, then
             # resumed from the per-rank checkpoint: identical to an
@@ -141,7 +183,7 @@ def _worker(rank, world, port, outdir, case):
 
 
 @pytest.mark.parametrize("case,world", [("qmeans", 2), ("qmeans", 3), ("kmeans", 2), ("pca", 2),
-                                        ("ipe", 2), ("resume", 2)])
+                                        ("ipe", 2), ("resume", 2), ("tomography", 2)])
 def test_sharded_matches_single_process(case, world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, case), nprocs=world, join=True)
