@@ -52,6 +52,8 @@ def parse(argv=None):
     ap.add_argument("--no-qpca", action="store_true")
     ap.add_argument("--no-fit", action="store_true")
     ap.add_argument("--fit-iters", type=int, default=10)
+    ap.add_argument("--ipe-steps", type=int, default=2,
+                    help="timed Lloyd steps of the IPE (true_distance_estimate) extra; 0 = skip")
     ap.add_argument("--seed", type=int, default=2024)
     return ap.parse_args(argv)
 
@@ -110,6 +112,36 @@ def _qpca_extra(extra, name, sa, comm, dev, solver, n_components=16, true_tomogr
         extra[name] = _max_over_ranks(comm, dev, time.perf_counter() - t0)
     except Exception as e:  # qPCA must not break the headline line
         extra[name + "_error"] = repr(e)[:200]
+
+
+def _ipe_extra(extra, a, X, comm, dev, start, C0):
+    """Lloyd throughput with the reference's DEFAULT distance mode,
+    true_distance_estimate=True (``_dmeans.py:753-772``): every (row,
+    centroid) distance is |x|^2 + |c|^2 - 2 IPE(x, c), IPE = median of 13
+    amplitude estimations (csrc/ipe.hip, fused with the fp32 MFMA inner
+    products).  Same data, k and delta as the headline."""
+    try:
+        from sq_learn_amd.models.cluster._lloyd import LloydEngine
+        eng = LloydEngine(X, a.k, delta=a.delta, true_distance_estimate=True,
+                          intermediate_error=True, true_tomography=False, seed=a.seed, comm=comm,
+                          row_offset=start, gemm_precision="fp32")
+        eng.set_centers(C0)
+        eng.step()[1].tolist()
+        _sync(dev)
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.ipe_steps):
+            eng.step()[1].tolist()
+        _sync(dev)
+        comm.barrier()
+        el = _max_over_ranks(comm, dev, time.perf_counter() - t0)
+        extra["ipe_samples_iter_per_s"] = a.n * a.ipe_steps / el
+        extra["ipe_ms_per_step"] = el / a.ipe_steps * 1e3
+        extra["ipe_pairs_per_s"] = a.n * a.k * a.ipe_steps / el
+        del eng
+        torch.cuda.empty_cache()
+    except Exception as e:
+        extra["ipe_error"] = repr(e)[:200]
 
 
 def _fit_extra(extra, a, sa, comm, dev, init):
@@ -208,6 +240,8 @@ def main(argv=None):
     del eng
     if gpu:
         torch.cuda.empty_cache()
+    if a.ipe_steps > 0 and gpu:
+        _ipe_extra(extra, a, X, comm, dev, start, C0)
     from sq_learn_amd.parallel.sharding import ShardedArray
     sa = ShardedArray(X, a.n, start, comm)
     if not a.no_fit:

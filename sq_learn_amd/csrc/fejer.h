@@ -36,63 +36,37 @@ struct WordStream {
   SQ_DEV double u() { return u01d(next()); }
 };
 
-// returns the sampled bin in [0, M)
-SQ_DEV long long fejer_sample(double omega, long long M, WordStream& ws) {
-  const double PI = 3.14159265358979323846;
-  double fl = floor(omega);
-  double phi = omega - fl;
-  double Md = (double)M;
-  long long base = (long long)fl;
-  if (phi == 0.0) {  // the true value sits on a bin: p = 1 there
-    long long j = base % M; if (j < 0) j += M; return j;
+// The per-law setup (phi, sin^2(pi phi), the walk's rotation constants) is
+// computed once; sample() then costs the walk (plus rare tail rejections).
+// fejer_sample() below = FejerLaw(omega, M).sample(ws): identical words and
+// results to the CPU twin (ops/random.py fejer_sample_torch).
+struct FejerLaw {
+  double omega, phi, Md;
+  long long M, base;
+  float s, sa, ca, sb, cb, inv_m2;
+  SQ_DEV FejerLaw(double omega_, long long M_) : omega(omega_), M(M_) {
+    const double PI = 3.14159265358979323846;
+    const double fl = floor(omega);
+    phi = omega - fl;
+    Md = (double)M;
+    base = (long long)fl;
+    s = 0.f; sa = ca = sb = cb = inv_m2 = 0.f;
+    if (phi == 0.0) return;
+    s = (float)sin(PI * phi);
+    s = s * s;
+    if (M <= kFejerSmallM) return;
+    const float alpha = (float)(PI / Md);
+    const float beta = (float)(PI * phi / Md);
+    __sincosf(beta, &sb, &cb);
+    __sincosf(alpha, &sa, &ca);
+    inv_m2 = (float)(1.0 / (Md * Md));
   }
-  float s = (float)sin(PI * phi); s = s * s;
-  if (M <= kFejerSmallM) {
-    // enumerate the whole period: bins j = 0..M-1, inverse CDF
-    double u = ws.u();
-    double acc = 0.0;
-    long long pick = M - 1;
-    double tot = 0.0;
-    for (long long j = 0; j < M; ++j) {
-      double d = (double)j - omega;
-      double sn = sin(PI * d / Md);
-      tot += (sn == 0.0) ? 1.0 : (double)s / (Md * Md * sn * sn);
-    }
-    u *= tot;
-    for (long long j = 0; j < M; ++j) {
-      double d = (double)j - omega;
-      double sn = sin(PI * d / Md);
-      acc += (sn == 0.0) ? 1.0 : (double)s / (Md * Md * sn * sn);
-      if (acc >= u) { pick = j; break; }
-    }
-    return pick;
-  }
-  // ---- walk
-  const float alpha = (float)(PI / Md);
-  const float beta = (float)(PI * phi / Md);
-  float sb, cb; __sincosf(beta, &sb, &cb);
-  float sa, ca; __sincosf(alpha, &sa, &ca);
-  const float inv_m2 = (float)(1.0 / (Md * Md));
-  float u = (float)ws.u();
-  // l = 0 : sin(-beta)
-  float den = sb * sb;
-  float acc = s * inv_m2 / den;
-  long long ell = 0;
-  bool found = acc >= u;
-  float st = 0.f, ct = 1.f;  // sin/cos(t*alpha)
-  for (int t = 1; t <= kFejerWalk && !found; ++t) {
-    float nst = st * ca + ct * sa;
-    float nct = ct * ca - st * sa;
-    st = nst; ct = nct;
-    float sp = st * cb - ct * sb;  // sin(t*alpha - beta)   (l = +t)
-    acc += s * inv_m2 / (sp * sp);
-    if (acc >= u) { ell = t; found = true; break; }
-    float sm = st * cb + ct * sb;  // -sin(-t*alpha - beta) (l = -t)
-    acc += s * inv_m2 / (sm * sm);
-    if (acc >= u) { ell = -t; found = true; break; }
-  }
-  if (!found) {
-    // ---- tails by rejection
+  // pmf of the walk offset l (bin base + l) given sin(l alpha - beta)
+  SQ_DEV float walk_term(float sn) const { return s * inv_m2 / (sn * sn); }
+  // offset of a draw conditioned on |l| > kFejerWalk (rejection, telescoping proposal)
+  SQ_DEV long long tail_ell(WordStream& ws) const {
+    const double PI = 3.14159265358979323846;
+    long long ell = 0;
     double lR = floor(phi + Md / 2.0);
     double lL = lR - Md + 1.0;
     double zR0 = kFejerWalk + 1 - phi, nR = fmax(lR - kFejerWalk, 0.0);
@@ -113,10 +87,67 @@ SQ_DEV long long fejer_sample(double omega, long long M, WordStream& ws) {
         break;
       }
     }
+    return ell;
   }
-  long long j = (base + ell) % M;
-  if (j < 0) j += M;
-  return j;
+  SQ_DEV long long bin_of(long long ell) const {
+    long long j = (base + ell) % M;
+    if (j < 0) j += M;
+    return j;
+  }
+  // returns the sampled bin in [0, M)
+  SQ_DEV long long sample(WordStream& ws) const {
+    const double PI = 3.14159265358979323846;
+    if (phi == 0.0) {  // the true value sits on a bin: p = 1 there
+      long long j = base % M; if (j < 0) j += M; return j;
+    }
+    if (M <= kFejerSmallM) {
+      // enumerate the whole period: bins j = 0..M-1, inverse CDF
+      double u = ws.u();
+      double acc = 0.0;
+      long long pick = M - 1;
+      double tot = 0.0;
+      for (long long j = 0; j < M; ++j) {
+        double d = (double)j - omega;
+        double sn = sin(PI * d / Md);
+        tot += (sn == 0.0) ? 1.0 : (double)s / (Md * Md * sn * sn);
+      }
+      u *= tot;
+      for (long long j = 0; j < M; ++j) {
+        double d = (double)j - omega;
+        double sn = sin(PI * d / Md);
+        acc += (sn == 0.0) ? 1.0 : (double)s / (Md * Md * sn * sn);
+        if (acc >= u) { pick = j; break; }
+      }
+      return pick;
+    }
+    // ---- walk
+    float u = (float)ws.u();
+    // l = 0 : sin(-beta)
+    float den = sb * sb;
+    float acc = s * inv_m2 / den;
+    long long ell = 0;
+    bool found = acc >= u;
+    float st = 0.f, ct = 1.f;  // sin/cos(t*alpha)
+    for (int t = 1; t <= kFejerWalk && !found; ++t) {
+      float nst = st * ca + ct * sa;
+      float nct = ct * ca - st * sa;
+      st = nst; ct = nct;
+      float sp = st * cb - ct * sb;  // sin(t*alpha - beta)   (l = +t)
+      acc += s * inv_m2 / (sp * sp);
+      if (acc >= u) { ell = t; found = true; break; }
+      float sm = st * cb + ct * sb;  // -sin(-t*alpha - beta) (l = -t)
+      acc += s * inv_m2 / (sm * sm);
+      if (acc >= u) { ell = -t; found = true; break; }
+    }
+    if (!found) ell = tail_ell(ws);
+    long long j = (base + ell) % M;
+    if (j < 0) j += M;
+    return j;
+  }
+};
+
+SQ_DEV long long fejer_sample(double omega, long long M, WordStream& ws) {
+  return FejerLaw(omega, M).sample(ws);
 }
 
 // amplitude estimation of a in [0,1] with M bins: returns sin^2(pi j / M)

@@ -1,0 +1,330 @@
+// Fused IPE E-step of q-means: "l2-sampled distance estimation", the
+// reference DEFAULT (``true_distance_estimate=True``, sklearn/cluster/
+// _dmeans.py:753-772 -> QuantumUtility/Utility.py:697-737).
+//
+// For every (row x, centroid c):  ip = x.c (exact fp32 MFMA),
+//   S = |x|^2 + |c|^2,  a = (S - 2 ip) / (2 S),  eps_a = eps max(1,|ip|) / S,
+//   M = ceil(pi / (2 eps_a) (1 + sqrt(1 + 4 eps_a))),  omega = M asin(sqrt a) / pi,
+//   a~ = median of Q amplitude-estimation draws sin^2(pi j / M), j ~ Fejer(omega, M)
+//   D~ = S - 2 S (1 - 2 a~) / 2 = 2 S a~,      label = argmin_j D~ (random ties)
+// and the inner-product matrix G is never materialised.
+//
+// Sampling, per pair (one lane per pair, in the MFMA epilogue):
+//  * odd Q and M <= kIpeWalkM: the median-of-Q is drawn EXACTLY from its own
+//    law with ONE uniform: the AE values sin^2(pi j/M) are ordered by the
+//    circular bin distance t = min(j, M - j), the class masses
+//    p(t) + p(M - t) accumulate into F(t), and the median of Q iid draws has
+//    CDF G(t) = P(Binomial(Q, F(t)) >= (Q+1)/2); inverse-CDF walk over t in
+//    fp64 (angle-addition recurrence, no transcendental per step);
+//  * otherwise Q Fejer draws (fejer.h, exact O(1) sampler) from one Philox
+//    stream per pair, the median taken over the circular distances t_q
+//    (sin^2 is monotone in t) by a register sorting network - no per-thread
+//    double[31] array.
+// Layout: a wave owns 16 rows, their fp32 A fragments (16x16x4 f32 MFMA:
+// lane l holds x[l & 15][4s + (l >> 4)]) staged once in the wave's LDS slot
+// (16 KiB at d = 256; keeps the VGPRs for the sampler, 2 waves per SIMD); centroid tiles of 16 are read as pre-arranged B fragments
+// (ops/kmeans.py: ipe_center_fragments, one coalesced 256-B load per k-step,
+// L2-resident).  Accumulator register i of lane l is pair (row 4(l>>4) + i,
+// centroid l & 15): 4 pairs per lane per tile keep the per-lane state small
+// (the sampling epilogue, not the MFMA, is the cost).  After the sweep the
+// 16 lanes of a row merge their (D~, tie key, j) minima.
+#include "common.h"
+#include "band.h"
+#include "fejer.h"
+
+namespace sq {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kIpeMaxQ = 15;
+constexpr int kIpeWalkM = 128;
+
+// P(Binomial(Q, F) >= h)
+SQ_DEV double binom_upper_tail(double F, int Q, int h) {
+  // sum_{i=h}^{Q} C(Q,i) F^i (1-F)^(Q-i) by the recurrence of the pmf terms
+  const double G = 1.0 - F;
+  if (F <= 0.0) return 0.0;
+  if (F >= 1.0) return 1.0;
+  double term = 1.0;                      // C(Q,0) G^Q, built up below
+  for (int i = 0; i < Q; ++i) term *= G;
+  const double ratio = F / G;
+  double tail = 0.0;
+  for (int i = 0; i <= Q; ++i) {
+    if (i >= h) tail += term;
+    term *= ratio * (double)(Q - i) / (double)(i + 1);
+  }
+  return tail;
+}
+
+// exact draw of the median of Q (odd) iid AE estimates for small M
+SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
+  const double PI = 3.14159265358979323846;
+  const double fl = floor(omega);
+  const double phi = omega - fl;
+  const double Md = (double)M;
+  if (phi == 0.0) {   // all draws land on the true bin
+    long long j = (long long)fl % M;
+    if (j < 0) j += M;
+    const double v = sin(PI * (double)j / Md);
+    return v * v;
+  }
+  const double sp = sin(PI * phi);
+  const double num = sp * sp / (Md * Md);
+  const double alpha = PI / Md, beta = PI * omega / Md;
+  double sa, ca, sb, cb;
+  sincos(alpha, &sa, &ca);
+  sincos(beta, &sb, &cb);
+  const int h = (Q + 1) / 2;
+  const long long tmax = M / 2;
+  double st = 0.0, ct = 1.0;   // sin / cos(t alpha)
+  double F = 0.0;
+  double v = 0.0;
+  for (long long t = 0; t <= tmax; ++t) {
+    const double sm = st * cb - ct * sb;   // sin(t alpha - beta): bin t
+    double mass = num / (sm * sm);
+    if (t != 0 && 2 * t != M) {
+      const double spl = st * cb + ct * sb;   // sin(t alpha + beta): bin M - t
+      mass += num / (spl * spl);
+    }
+    F += mass;
+    v = st * st;
+    if (binom_upper_tail(F, Q, h) >= u) return v;
+    const double nst = st * ca + ct * sa;
+    ct = ct * ca - st * sa;
+    st = nst;
+  }
+  return v;
+}
+
+// median of Q Fejer draws (any Q <= kIpeMaxQ, any M).  The Q draws are one
+// inverse-CDF pass: their uniforms are generated already SORTED (sequential
+// order statistics u_(i+1) = 1 - (1 - u_(i)) V^(1/(Q-i))), so a single
+// central-out walk over l = 0, 1, -1, ..., +-kFejerWalk hands every draw its
+// bin; the draws whose uniform lies beyond the walk's mass are drawn from the
+// tail law (given how many fall there, they are iid from it - the multiset,
+// and so the median, has exactly the law of Q independent draws).  Each
+// draw's circular bin distance is bubbled into a sorted register array.
+SQ_DEV void insert_sorted(double (&c)[kIpeMaxQ], double x) {
+#pragma unroll
+  for (int i = 0; i < kIpeMaxQ; ++i) {
+    const double lo = fmin(c[i], x);
+    x = fmax(c[i], x);
+    c[i] = lo;
+  }
+}
+
+SQ_DEV double ae_median_draws(double omega, long long M, int Q, WordStream& ws) {
+  const double PI = 3.14159265358979323846;
+  const FejerLaw law(omega, M);   // per-pair setup shared by the Q draws
+  double c[kIpeMaxQ];
+#pragma unroll
+  for (int i = 0; i < kIpeMaxQ; ++i) c[i] = 1e300;
+  auto circ = [&](long long j) -> double { return (double)(j < M - j ? j : M - j); };
+  if (law.phi == 0.0 || M <= kFejerSmallM) {
+#pragma nounroll
+    for (int q = 0; q < Q; ++q) insert_sorted(c, circ(law.sample(ws)));
+  } else {
+    int got = 0;
+    float om = 1.0f;   // 1 - u_(got+1)
+    auto next_u = [&]() -> float {
+      const float V = u01(ws.next());
+      om *= __expf(__logf(V) / (float)(Q - got));
+      return 1.0f - om;
+    };
+    float un = next_u();
+    float acc = law.walk_term(law.sb);   // l = 0: sin(-beta)^2
+    while (got < Q && un <= acc) {
+      insert_sorted(c, circ(law.bin_of(0)));
+      ++got;
+      if (got < Q) un = next_u();
+    }
+    float st = 0.f, ct = 1.f;
+    for (int t = 1; t <= kFejerWalk && got < Q; ++t) {
+      const float nst = st * law.ca + ct * law.sa;
+      const float nct = ct * law.ca - st * law.sa;
+      st = nst;
+      ct = nct;
+      acc += law.walk_term(st * law.cb - ct * law.sb);   // l = +t
+      while (got < Q && un <= acc) {
+        insert_sorted(c, circ(law.bin_of(t)));
+        ++got;
+        if (got < Q) un = next_u();
+      }
+      acc += law.walk_term(st * law.cb + ct * law.sb);   // l = -t
+      while (got < Q && un <= acc) {
+        insert_sorted(c, circ(law.bin_of(-t)));
+        ++got;
+        if (got < Q) un = next_u();
+      }
+    }
+#pragma nounroll
+    for (; got < Q; ++got) insert_sorted(c, circ(law.bin_of(law.tail_ell(ws))));
+  }
+  double m1 = 0.0, m0 = 0.0;
+#pragma unroll
+  for (int i = 0; i < kIpeMaxQ; ++i) {
+    if (i == Q / 2) m1 = c[i];
+    if (i == Q / 2 - 1) m0 = c[i];
+  }
+  const double v1 = sin(PI * m1 / (double)M);
+  if (Q & 1) return v1 * v1;
+  const double v0 = sin(PI * m0 / (double)M);
+  return 0.5 * (v0 * v0 + v1 * v1);
+}
+
+SQ_DEV float ipe_distance(float ipf, double nx2, double ny2, double eps, int Q, const RngKey& key,
+                          unsigned long long sid) {
+  const double ip = (double)ipf;
+  const double S = nx2 + ny2;
+  if (!(S > 0.0)) return 0.0f;
+  double a = (S - 2.0 * ip) / (2.0 * S);
+  if (fabs(a) <= 1e-15) a = 0.0;
+  a = fmin(fmax(a, 0.0), 1.0);
+  const double eps_a = eps * fmax(1.0, fabs(ip)) / S;
+  long long M = ae_bins(eps_a);
+  if (M > (1LL << 40)) M = 1LL << 40;
+  if (M < 1) M = 1;
+  const double PI = 3.14159265358979323846;
+  const double omega = (double)M * asin(sqrt(a)) / PI;
+  WordStream ws(key, sid);
+  double at;
+  if ((Q & 1) && M <= kIpeWalkM) {
+    const uint32_t w0 = ws.next(), w1 = ws.next();
+    const double u = ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
+                     (1.0 / 9007199254740992.0);
+    at = ae_median_walk(omega, M, Q, u);
+  } else {
+    at = ae_median_draws(omega, M, Q, ws);
+  }
+  return (float)(2.0 * S * at);
+}
+
+template <int D4>
+__global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
+    const float* __restrict__ X, long long ldx, const float* __restrict__ Cf,
+    const float* __restrict__ xn, const float* __restrict__ cn, int* __restrict__ labels,
+    float* __restrict__ mind, long long n, int d, int k, int n_tiles, double eps, int Q,
+    RngKey key, RngKey tie_key, long long row_offset) {
+  __shared__ float As[4][D4 * 64];   // per wave: its 16 rows as A fragments
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, q4 = lane >> 4;
+  const long long row0 = ((long long)blockIdx.x * 4 + wave) * 16;
+  if (row0 >= n) return;   // wave-uniform; no block-wide barrier below
+  float* as = As[wave];
+  {
+    // A fragments (16x16x4 f32): x[row0 + c16][4s + q4]; rows past n clamped
+    const long long r = row0 + c16 < n ? row0 + c16 : n - 1;
+    const float* xr = X + (size_t)r * ldx + q4;
+#pragma unroll 8
+    for (int s = 0; s < D4; ++s) as[s * 64 + lane] = 4 * s + q4 < d ? xr[4 * s] : 0.0f;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // register i of this lane = pair (row row0 + 4 q4 + i, centroid 16 t + c16)
+  f32x4 nx2, best;
+  uint32_t bkey[4];
+  int bj[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long r = row0 + 4 * q4 + i;
+    nx2[i] = xn[r < n ? r : n - 1];
+    best[i] = __builtin_inff();
+    bkey[i] = 0xFFFFFFFFu;
+    bj[i] = 0;
+  }
+  for (int t = 0; t < n_tiles; ++t) {
+    const float* bf = Cf + (size_t)t * D4 * 64 + lane;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 16
+    for (int s = 0; s < D4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(as[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
+    const int j = t * 16 + c16;
+    if (j < k) {   // padded centroid columns do nothing (no MFMA / sync below)
+      const double ny2 = (double)cn[j];
+      // one inlined copy of the sampler: the 4 pairs rotate through slot 0
+#pragma nounroll
+      for (int i = 0; i < 4; ++i) {
+        const long long r = row0 + 4 * q4 + i;
+        if (r < n) {
+          const long long g = row_offset + r;
+          const float dt = ipe_distance(acc[0], (double)nx2[0], ny2, eps, Q, key,
+                                        (unsigned long long)g * (unsigned long long)k +
+                                            (unsigned long long)j);
+          const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
+          if (dt < best[0] || (dt == best[0] && (tk < bkey[0] || (tk == bkey[0] && j < bj[0])))) {
+            best[0] = dt;
+            bkey[0] = tk;
+            bj[0] = j;
+          }
+        }
+        acc = acc.yzwx;
+        nx2 = nx2.yzwx;
+        best = best.yzwx;
+        const uint32_t k0 = bkey[0];
+        bkey[0] = bkey[1]; bkey[1] = bkey[2]; bkey[2] = bkey[3]; bkey[3] = k0;
+        const int j0 = bj[0];
+        bj[0] = bj[1]; bj[1] = bj[2]; bj[2] = bj[3]; bj[3] = j0;
+      }
+    }
+  }
+  // merge the 16 lanes (centroid classes) holding each row
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float b = best[i];
+    uint32_t kk = bkey[i];
+    int jj = bj[i];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float ob = __shfl_xor(b, o, 64);
+      const uint32_t ok = (uint32_t)__shfl_xor((int)kk, o, 64);
+      const int oj = __shfl_xor(jj, o, 64);
+      if (ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)))) {
+        b = ob;
+        kk = ok;
+        jj = oj;
+      }
+    }
+    const long long r = row0 + 4 * q4 + i;
+    if (c16 == 0 && r < n) {
+      labels[r] = jj;
+      mind[r] = b;
+    }
+  }
+}
+
+}  // namespace sq
+
+using namespace sq;
+
+extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const void* xn,
+                            const void* cn, void* labels, void* mind, long long n, int d, int d_pad,
+                            int k, int k_pad, double eps, int Q, unsigned k0, unsigned k1,
+                            unsigned s0, unsigned s1, unsigned t0, unsigned t1, unsigned ts0,
+                            unsigned ts1, long long row_offset, void* stream) {
+  if (n <= 0) return 0;
+  if (Q < 1 || Q > kIpeMaxQ || k < 1 || k_pad % 16 != 0 || k_pad < k || d < 1 || d > d_pad ||
+      ldx < d)
+    return (int)hipErrorInvalidValue;
+  RngKey key{k0, k1, s0, s1};
+  RngKey tie{t0, t1, ts0, ts1};
+  const long long blocks = (n + 63) / 64;
+  const int nt = k_pad / 16;
+#define CASE(DP)                                                                              \
+  case DP:                                                                                    \
+    hipLaunchKernelGGL(ipe_fused_kernel<DP / 4>, dim3((unsigned)blocks), dim3(256), 0,         \
+                       (hipStream_t)stream, (const float*)X, ldx, (const float*)Cf,           \
+                       (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, \
+                       nt, eps, Q, key, tie, row_offset);                                     \
+    break;
+  switch (d_pad) {
+    CASE(32)
+    CASE(64)
+    CASE(128)
+    CASE(256)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef CASE
+  return (int)hipGetLastError();
+}

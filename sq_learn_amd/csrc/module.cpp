@@ -27,6 +27,11 @@ __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int,
 __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, long long,
                                            long long, const void*, void*, long long, unsigned,
                                            unsigned, unsigned, unsigned, const void*, int, void*);
+// ipe.hip
+__attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, const void*, const void*,
+                                       void*, void*, long long, int, int, int, int, double, int,
+                                       unsigned, unsigned, unsigned, unsigned, unsigned, unsigned,
+                                       unsigned, unsigned, long long, void*);
 // pairwise_fast.hip
 __attribute__((weak)) int sq_pairwise_reduce(const void*, const void*, void*, int, int, int, int,
                                              double, int, void*);
@@ -195,6 +200,18 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
   CHECK(sq_mnom_segments)
   return ret(sq_mnom_segments(P(W), ldw, P(wrow), m, B, P(Ns), P(cnt), ldc, k0, k1, s0, s1, P(sid),
                               level, P(st)));
+}
+
+static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
+  unsigned long long X, Cf, xn, cn, lab, mind, st; long long ldx, n, roff; int d, dp, k, kp, Q;
+  double eps; unsigned k0, k1, s0, s1, t0, t1, ts0, ts1;
+  if (!PyArg_ParseTuple(a, "KLKKKKKLiiiidiIIIIIIIILK", &X, &ldx, &Cf, &xn, &cn, &lab, &mind, &n,
+                        &d, &dp, &k, &kp, &eps, &Q, &k0, &k1, &s0, &s1, &t0, &t1, &ts0, &ts1,
+                        &roff, &st))
+    return nullptr;
+  CHECK(sq_ipe_fused)
+  return ret(sq_ipe_fused(P(X), ldx, P(Cf), P(xn), P(cn), P(lab), P(mind), n, d, dp, k, kp, eps, Q,
+                          k0, k1, s0, s1, t0, t1, ts0, ts1, roff, P(st)));
 }
 
 static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {
@@ -423,6 +440,7 @@ static PyMethodDef methods[] = {
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
+    {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},

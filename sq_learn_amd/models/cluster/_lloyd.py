@@ -284,6 +284,24 @@ class LloydEngine:
     def _estep_ipe(self, key):
         eps = self.delta / 2.0
         ipe_key = self._key("ipe")
+        if self.device.type == "cuda" and self.d <= 256 and self.Xf.dtype == torch.float32 \
+                and self.Xf.stride(1) == 1 and self.ipe_Q <= 15:
+            # fused kernel: fp32 MFMA inner products + per-pair median-of-Q AE
+            n = self.n
+            labels32 = torch.empty(n, dtype=torch.int32, device=self.device)
+            mind = torch.empty(n, dtype=torch.float32, device=self.device)
+            dp = 32
+            while dp < self.d:
+                dp *= 2
+            kp = -(-self.k // 16) * 16
+            C32 = self.C.float()
+            cn = (C32 * C32).sum(1).contiguous()
+            with tracing.range("ipe_fused"):
+                K.ipe_fused_native(self.Xf, K.ipe_center_fragments(C32, kp, dp),
+                                   self.xn.float().contiguous(), cn, self.k, kp, dp, eps,
+                                   self.ipe_Q, ipe_key, self._key("band_select"), self.row_offset,
+                                   labels32, mind)
+            return labels32, mind, mind.double().sum().reshape(1)
         if self.device.type == "cuda":
             n = self.n
             labels32 = torch.empty(n, dtype=torch.int32, device=self.device)

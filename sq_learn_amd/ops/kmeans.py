@@ -232,6 +232,33 @@ def ipe_estep_native(G, xn, cn, eps, Q, key: RngKey, row_offset, labels, mind):
                            key.s0, key.s1, int(row_offset), nat.stream_handle(G.device))
 
 
+def ipe_center_fragments(C, k_pad, d_pad):
+    """Centroids as 16x16x4 f32 MFMA B fragments (csrc/ipe.hip): tile t,
+    k-step s, lane l -> C[16 t + (l & 15)][4 s + (l >> 4)], zero padded."""
+    k, d = C.shape
+    Cp = torch.zeros((k_pad, d_pad), dtype=torch.float32, device=C.device)
+    Cp[:k, :d] = C.float()
+    return Cp.view(k_pad // 16, 16, d_pad // 4, 4).permute(0, 2, 3, 1).contiguous()
+
+
+def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie_key: RngKey,
+                     row_offset, labels, mind):
+    """Fused IPE E-step (csrc/ipe.hip): exact fp32 MFMA inner products, the
+    median-of-Q amplitude-estimation distance per pair in the epilogue,
+    per-row argmin with random ties; G is never materialised."""
+    n, d = X.shape
+    assert X.dtype == torch.float32 and X.stride(1) == 1
+    assert xn.dtype == torch.float32 and cn.dtype == torch.float32 and xn.numel() >= n
+    assert Cfrag.numel() == k_pad * d_pad and labels.dtype == torch.int32
+    rc = nat.native().ipe_fused(X.data_ptr(), X.stride(0), Cfrag.data_ptr(), xn.data_ptr(),
+                                cn.data_ptr(), labels.data_ptr(), mind.data_ptr(), n, d, d_pad, k,
+                                k_pad, float(eps), int(Q), key.k0, key.k1, key.s0, key.s1,
+                                tie_key.k0, tie_key.k1, tie_key.s0, tie_key.s1, int(row_offset),
+                                nat.stream_handle(X.device))
+    if rc:
+        raise RuntimeError(f"ipe_fused failed (hip error {rc})")
+
+
 def centroid_accumulate_native(X, labels, weights, sums, counts, k, chunk=None):
     n, d = X.shape
     if chunk is None:

@@ -1,0 +1,162 @@
+"""Fused IPE E-step (csrc/ipe.hip) - the reference's default distance mode
+(``_dmeans.py:753-772`` -> ``Utility.py:697-737``).
+
+Law tests: with one centroid the kernel's per-row output IS the estimated
+distance D~ = 2 S a~ of that pair, so n identical rows give n iid draws of
+the median-of-Q amplitude-estimation law.  It is compared (chi^2) with the
+EXACT law computed from the Fejer pmf (fejer_pmf, the reference's p_aj) and
+with the CPU twin (ops/kmeans.py ipe_estep_torch), on pairs whose M falls
+in the exact median-law walk (M <= 128) and in the draw path (large M, even Q).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+from scipy import stats
+
+from sq_learn_amd.ops import kmeans as K
+from sq_learn_amd.quantum.fejer import fejer_pmf, ae_bins
+from sq_learn_amd.runtime.rng import RngKey
+
+pytestmark = pytest.mark.gpu
+
+
+def _exact_law(ip, nx2, ny2, eps, Q):
+    """{D~ value: probability} of the median of Q AE draws."""
+    S = nx2 + ny2
+    a = min(max((S - 2 * ip) / (2 * S), 0.0), 1.0)
+    eps_a = eps * max(1.0, abs(ip)) / S
+    M = int(ae_bins(a, eps_a))
+    omega = M * math.asin(math.sqrt(a)) / math.pi
+    p = fejer_pmf(omega, M)
+    p = p / p.sum()
+    t = np.minimum(np.arange(M), M - np.arange(M))
+    mass = np.bincount(t, weights=p)              # value classes t = 0..M/2
+    F = np.cumsum(mass)
+    h = (Q + 1) // 2
+    G = stats.binom.sf(h - 1, Q, np.clip(F, 0, 1)) if Q % 2 else None
+    vals = 2 * S * np.sin(np.pi * np.arange(len(mass)) / M) ** 2
+    if Q % 2:
+        pm = np.diff(np.concatenate([[0.0], G]))
+        return M, vals, pm
+    return M, vals, None
+
+
+def _run_kernel(x, c, n, eps, Q, cuda, seed=0):
+    d = x.size
+    X = torch.tensor(np.tile(x, (n, 1)), dtype=torch.float32, device=cuda)
+    C = torch.tensor(c[None], dtype=torch.float32, device=cuda)
+    dp = 32
+    while dp < d:
+        dp *= 2
+    xn = (X.double() ** 2).sum(1).float()
+    cn = (C.double() ** 2).sum(1).float()
+    lab = torch.empty(n, dtype=torch.int32, device=cuda)
+    mind = torch.empty(n, dtype=torch.float32, device=cuda)
+    K.ipe_fused_native(X, K.ipe_center_fragments(C, 16, dp), xn, cn, 1, 16, dp, eps, Q,
+                       RngKey(seed, "ipe", 0), RngKey(seed, "band_select", 0), 0, lab, mind)
+    torch.cuda.synchronize()
+    assert int(lab.max()) == 0
+    return mind.double().cpu().numpy(), float(xn[0]), float(cn[0]), float((X[0].double() @ C[0].double()))
+
+
+def _gof(samples, vals, pm):
+    idx = np.argmin(np.abs(samples[:, None] - vals[None, :]), axis=1)
+    assert np.allclose(samples, vals[idx], rtol=2e-6, atol=1e-5)
+    obs = np.bincount(idx, minlength=len(vals)).astype(float)
+    exp = pm * len(samples)
+    big = exp >= 5
+    o = np.append(obs[big], obs[~big].sum())
+    e = np.append(exp[big], exp[~big].sum())
+    if e[-1] == 0:
+        o, e = o[:-1], e[:-1]
+    chi2 = ((o - e) ** 2 / e).sum()
+    return stats.chi2.sf(chi2, max(len(e) - 1, 1))
+
+
+@pytest.mark.parametrize("case", ["walk", "walk_q1", "draws"])
+def test_ipe_fused_law_exact(cuda, case):
+    rng = np.random.default_rng(1)
+    d = 200
+    x = rng.standard_normal(d)
+    if case.startswith("walk"):
+        c = x + 0.8 * rng.standard_normal(d)      # |ip| ~ S/2 -> M ~ 30
+        eps = 0.25
+    else:
+        c = rng.standard_normal(d)                  # nearly orthogonal -> small eps_a, large M
+        eps = 0.25
+    Q = 1 if case == "walk_q1" else 13
+    n = 60000
+    s, nx2, ny2, ip = _run_kernel(x, c, n, eps, Q, cuda)
+    M, vals, pm = _exact_law(ip, nx2, ny2, eps, Q)
+    if case.startswith("walk"):
+        assert M <= 128
+    else:
+        assert M > 128
+    if Q == 1:
+        # single draw: value class law = class masses
+        S = nx2 + ny2
+        a = min(max((S - 2 * ip) / (2 * S), 0.0), 1.0)
+        omega = M * math.asin(math.sqrt(a)) / math.pi
+        p = fejer_pmf(omega, M)
+        t = np.minimum(np.arange(M), M - np.arange(M))
+        pm = np.bincount(t, weights=p / p.sum())
+    assert _gof(s, vals, pm) > 1e-4
+
+
+def test_ipe_fused_even_q_matches_cpu_twin(cuda):
+    rng = np.random.default_rng(2)
+    d = 64
+    x = rng.standard_normal(d)
+    c = x + 0.5 * rng.standard_normal(d)
+    n = 20000
+    g, *_ = _run_kernel(x, c, n, 0.3, 4, cuda)
+    X = torch.tensor(np.tile(x, (3000, 1)), dtype=torch.float32)
+    C = torch.tensor(c[None], dtype=torch.float32)
+    _, mind = K.ipe_estep_torch(X, C, 0.3, RngKey(5, "ipe", 0), 0, 16, Q=4)
+    a = np.round(g, 3)
+    b = np.round(mind.numpy(), 3)
+    vals, inv = np.unique(np.concatenate([a, b]), return_inverse=True)
+    ca = np.bincount(inv[: len(a)], minlength=len(vals))
+    cb = np.bincount(inv[len(a):], minlength=len(vals))
+    keep = (ca + cb) >= 10
+    table = np.stack([np.append(ca[keep], ca[~keep].sum()), np.append(cb[keep], cb[~keep].sum())])
+    table = table[:, table.sum(0) > 0]
+    assert stats.chi2_contingency(table)[1] > 1e-4
+
+
+def test_ipe_fused_argmin_and_inertia(cuda):
+    """Many centroids: the label is the argmin of the per-pair estimates;
+    with a small eps the estimates are close to the true distances."""
+    rng = np.random.default_rng(3)
+    n, d, k = 4096, 48, 70
+    centers = rng.standard_normal((k, d)) * 4
+    X = centers[rng.integers(0, k, n)] + 0.3 * rng.standard_normal((n, d))
+    Xt = torch.tensor(X, dtype=torch.float32, device=cuda)
+    Ct = torch.tensor(centers, dtype=torch.float32, device=cuda)
+    xn = (Xt.double() ** 2).sum(1).float()
+    cn = (Ct.double() ** 2).sum(1).float()
+    lab = torch.empty(n, dtype=torch.int32, device=cuda)
+    mind = torch.empty(n, dtype=torch.float32, device=cuda)
+    K.ipe_fused_native(Xt, K.ipe_center_fragments(Ct, 80, 64), xn, cn, k, 80, 64, 0.05, 13,
+                       RngKey(7, "ipe", 0), RngKey(7, "band_select", 0), 0, lab, mind)
+    D = ((X[:, None, :] - centers[None]) ** 2).sum(-1)
+    true = D.argmin(1)
+    assert np.mean(lab.cpu().numpy() == true) > 0.99
+    m = mind.cpu().numpy()
+    assert np.median(np.abs(m - D.min(1)) / D.min(1).clip(1)) < 0.5
+
+
+def test_qmeans_ipe_end_to_end_gpu(cuda):
+    from sq_learn_amd.models.cluster import QMeans
+    from sq_learn_amd.utils.datasets import make_blobs
+    from sklearn.metrics import adjusted_rand_score
+    X, y = make_blobs(6000, 32, centers=6, cluster_std=1.0, random_state=0)
+    kw = dict(n_clusters=6, delta=0.5, true_distance_estimate=True, random_state=0, n_init=1,
+              max_iter=10, init="k-means++")
+    g = QMeans(device=cuda, **kw).fit(X)
+    c = QMeans(device="cpu", **kw).fit(X)
+    assert adjusted_rand_score(y, g.labels_) > 0.95
+    assert adjusted_rand_score(y, c.labels_) > 0.95
+    assert abs(g.inertia_ - c.inertia_) < 0.1 * c.inertia_
