@@ -164,6 +164,9 @@ def _fit_extra(extra, a, sa, comm, dev, init):
         comm.barrier()
         extra[name] = _max_over_ranks(comm, dev, time.perf_counter() - t0)
         extra[name + "_n_iter"] = int(est.n_iter_)
+        extra[name + "_inertia"] = float(est.inertia_)
+        for ph, v in getattr(est, "fit_phase_s_", {}).items():
+            extra[name + "_" + ph] = round(v, 4)
     except Exception as e:
         extra[name + "_error"] = repr(e)[:200]
 
@@ -245,7 +248,8 @@ def main(argv=None):
     from sq_learn_amd.parallel.sharding import ShardedArray
     sa = ShardedArray(X, a.n, start, comm)
     if not a.no_fit:
-        _fit_extra(extra, a, sa, comm, dev, "random")
+        for init in ("random", "k-means||", "k-means++"):
+            _fit_extra(extra, a, sa, comm, dev, init)
     if not a.no_qpca and gpu:
         # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
         _qpca_extra(extra, "qpca_10Mx256_full_fit_s", sa, comm, dev, "full")

@@ -27,6 +27,9 @@ __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int,
 __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, long long,
                                            long long, const void*, void*, long long, unsigned,
                                            unsigned, unsigned, unsigned, const void*, int, void*);
+// gram64.hip
+__attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, long long, int, void*,
+                                    int, void*);
 // ipe.hip
 __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, const void*, const void*,
                                        void*, void*, long long, int, int, int, int, double, int,
@@ -200,6 +203,14 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
   CHECK(sq_mnom_segments)
   return ret(sq_mnom_segments(P(W), ldw, P(wrow), m, B, P(Ns), P(cnt), ldc, k0, k1, s0, s1, P(sid),
                               level, P(st)));
+}
+
+static PyObject* py_gram64(PyObject*, PyObject* a) {
+  unsigned long long X, mu, part, st; int f64, d, grid; long long ldx, n;
+  if (!PyArg_ParseTuple(a, "KiLKLiKiK", &X, &f64, &ldx, &mu, &n, &d, &part, &grid, &st))
+    return nullptr;
+  CHECK(sq_gram64)
+  return ret(sq_gram64(P(X), f64, ldx, P(mu), n, d, P(part), grid, P(st)));
 }
 
 static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
@@ -440,6 +451,7 @@ static PyMethodDef methods[] = {
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
+    {"gram64", py_gram64, METH_VARARGS, "fp64 MFMA Gram partials"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},

@@ -26,7 +26,7 @@ from ...utils.validation import check_is_fitted, check_random_state, seed_from_r
 from ...runtime.device import to_numpy
 from ..._config import get_config
 from .._data import as_data, global_mean_var, Data
-from ._init import kmeans_plusplus as _kpp, random_init
+from ._init import kmeans_plusplus as _kpp, kmeans_parallel as _kpar, random_init
 from ._lloyd import LloydEngine
 from ._elkan import ElkanEngine
 from ...ops import kmeans as K
@@ -112,6 +112,9 @@ class KMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             eng.restart, eng.it = r, 0
             if isinstance(self.init, str) and self.init == "k-means++":
                 C0, _ = _kpp(dc, self.n_clusters, rs, x_squared_norms=eng.xn)
+            elif isinstance(self.init, str) and self.init == "k-means||":
+                C0, _ = _kpar(dc, self.n_clusters, rs, x_squared_norms=eng.xn,
+                              seed=int(rs.randint(2 ** 31 - 1)))
             elif isinstance(self.init, str) and self.init == "random":
                 C0, _ = random_init(dc, self.n_clusters, rs)
             elif callable(self.init):

@@ -39,7 +39,7 @@ from ...runtime.device import to_numpy
 from ..._config import get_config
 from .._data import as_data, check_n_features, global_mean_var, prelude_stats
 from ...utils.checkpoint import Checkpointer, rs_state_from_tensors, rs_state_to_tensors
-from ._init import kmeans_plusplus, random_init
+from ._init import kmeans_plusplus, kmeans_parallel, random_init
 from ._lloyd import LloydEngine
 from ...ops import kmeans as K
 from ...quantum.fejer import median_repetitions
@@ -117,8 +117,8 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         if self.algorithm not in ("auto", "full", "elkan", "lloyd"):
             raise ValueError(f"Algorithm must be 'auto', 'full' or 'elkan', got {self.algorithm} instead.")
         if not (hasattr(self.init, "__array__") or callable(self.init)
-                or (isinstance(self.init, str) and self.init in ("k-means++", "random"))):
-            raise ValueError("init should be either 'k-means++', 'random', a ndarray or a callable, "
+                or (isinstance(self.init, str) and self.init in ("k-means++", "k-means||", "random"))):
+            raise ValueError("init should be either 'k-means++', 'k-means||', 'random', a ndarray or a callable, "
                              f"got '{self.init}' instead.")
         self._n_init = self.n_init
         if hasattr(self.init, "__array__") and self._n_init != 1:
@@ -144,6 +144,9 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
     def _init_centroids(self, data, init, rs, xn, mean):
         if isinstance(init, str) and init == "k-means++":
             C, _ = kmeans_plusplus(data, self.n_clusters, rs, x_squared_norms=xn)
+        elif isinstance(init, str) and init == "k-means||":
+            C, _ = kmeans_parallel(data, self.n_clusters, rs, x_squared_norms=xn,
+                                   seed=int(rs.randint(2 ** 31 - 1)))
         elif isinstance(init, str) and init == "random":
             C, _ = random_init(data, self.n_clusters, rs)
         elif hasattr(init, "__array__") or isinstance(init, torch.Tensor):
@@ -172,9 +175,21 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             if self.intermediate_error:
                 raise ValueError("intermediate_error value cannot be True if delta is zero.")
         comm = data.comm
+        import time as _time
+        phases = {}
+        mark = [_time.perf_counter()]
+
+        def phase(name):
+            # wall-clock per fit phase (device-synchronised at the boundary)
+            if data.device.type == "cuda":
+                torch.cuda.synchronize(data.device)
+            now = _time.perf_counter()
+            phases[name] = phases.get(name, 0.0) + now - mark[0]
+            mark[0] = now
         if self.compute_prelude:
             eta, mu_label, mu, cond = prelude_stats(data, 0.0, 0.1, 0.05)
             self.eta, self.muA, self.muA_norm, self.condition_number = eta, mu, mu_label, cond
+        phase("prelude_s")
         rs = check_random_state(self.random_state)
         seed = seed_from_random_state(self.random_state)
         mean, var = global_mean_var(data)
@@ -229,6 +244,7 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                 engine.failure_counters.copy_(st["failure_counters"].to(engine.device))
             self.resumed_from_ = (start_restart, int(st["it"]))
         self._ckpt_ctx = dict(ckpt=ckpt, fingerprint=fingerprint, rs=rs)
+        phase("setup_s")
         for restart in range(start_restart, self._n_init):
             engine.restart = restart
             engine.it = 0
@@ -242,8 +258,10 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             else:
                 C0 = self._init_centroids(data_c, self.init, rs, xn, mean)
                 inner = None
+            phase("init_s")
             self._ckpt_ctx["outer_best"] = best
             labels, inertia, centers, n_iter = self._run_lloyd(engine, C0, resume=inner)
+            phase("lloyd_s")
             if best is None or inertia < best[1]:
                 best = (labels, inertia, centers, n_iter)
         ckpt.clear()
@@ -260,6 +278,8 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         self.labels_ = to_numpy(labels).astype(np.int32)
         self.inertia_ = float(inertia)
         self.n_iter_ = int(n_iter)
+        phase("finish_s")
+        self.fit_phase_s_ = phases
         self._mean = to_numpy(mean)
         self._engine_comm = comm
         distinct = self._count_distinct(labels, comm)

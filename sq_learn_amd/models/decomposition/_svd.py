@@ -8,6 +8,11 @@
   all-reduce, ``eigh`` in fp64 -> S, V; left singular vectors
   U = (X-mu) V S^-1 are materialised only for the retained columns, on the
   shard that owns the rows.
+* ``cholqr2`` (default for tall matrices): sharded CholeskyQR2 in fp64
+  (two passes over X, two d x d all-reduces), then the SVD of the d x d R:
+  singular values and right vectors to ~eps64 * cond relative, like the
+  reference's fp64 LAPACK (the ``gram`` eigenvalues lose eps * cond^2);
+  falls back to ``gram`` when cond(X) >~ 1e8 or X is rank deficient.
 * ``randomized``: :func:`utils.extmath.randomized_svd_distributed` (fused
   power-iteration kernel, CholeskyQR2, K14, C6/C7).
 """
@@ -35,8 +40,15 @@ def _small(data):
 def full_svd(data, mean, k_left, method="auto"):
     """Thin SVD of (X - mean); U computed for the first ``k_left`` columns."""
     if method == "auto":
-        method = "exact" if (_small(data) or data.n_global < data.d) else "gram"
+        method = "exact" if (_small(data) or data.n_global < data.d) else "cholqr2"
     X = data.X
+    if method == "cholqr2":
+        R = L.cholqr2_r(X, data.comm, mean)
+        if R is None:
+            method = "gram"
+        else:
+            _, S, Vt = torch.linalg.svd(R)
+            return _finish(data, mean, S, Vt, k_left, "cholqr2")
     if method == "exact":
         full = X if data.comm.world_size == 1 else torch.cat(data.comm.all_gather_varlen(X), 0)
         Xc = full.to(torch.float64) - mean.to(torch.float64).to(full.device)
@@ -55,6 +67,13 @@ def full_svd(data, mean, k_left, method="auto"):
     V = V.flip(1)
     S = torch.sqrt(ev)
     Vt = V.T.contiguous()
+    return _finish(data, mean, S, Vt, k_left, "gram")
+
+
+def _finish(data, mean, S, Vt, k_left, method):
+    """Left vectors U = (X - mean) V S^-1 for the retained columns on the
+    row shard, deterministic signs."""
+    X = data.X
     r = min(data.n_global, data.d)
     S, Vt = S[:r], Vt[:r]
     k = min(k_left, int((S > S[0] * 1e-12).sum()) if S.numel() else 0) if r else 0
@@ -78,7 +97,7 @@ def full_svd(data, mean, k_left, method="auto"):
         sg = torch.sign(rest[torch.arange(rest.shape[0], device=rest.device), idx])
         sg = torch.where(sg == 0, torch.ones_like(sg), sg)
         Vt_dev = torch.cat([Vt_dev[:k], rest * sg[:, None]], 0)
-    return SVDResult(S.cpu().numpy(), Vt_dev.to(torch.float64).cpu().numpy(), Uk, "gram")
+    return SVDResult(S.cpu().numpy(), Vt_dev.to(torch.float64).cpu().numpy(), Uk, method)
 
 
 def truncated_svd(data, mean, n_components, n_iter="auto", seed=0, n_oversamples=10):

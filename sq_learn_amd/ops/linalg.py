@@ -52,6 +52,83 @@ def gram_local(X, mean):
     return Xc.T @ Xc
 
 
+def gram64_native(X, mean=None):
+    """G = (X - mean)^T (X - mean) in fp64 on the matrix cores
+    (csrc/gram64.hip, v_mfma_f64_16x16x4_f64): per-workgroup partial upper
+    blocks summed in a fixed order (deterministic); X fp32 or fp64, d <= 256."""
+    n, d = X.shape
+    assert X.dtype in (torch.float32, torch.float64) and X.stride(1) == 1 and d <= 256
+    nb = (d + 15) // 16
+    nblk = nb * (nb + 1) // 2
+    grid = int(max(1, min(256, (n + 255) // 256)))
+    part = torch.empty((grid, nblk, 16, 16), dtype=torch.float64, device=X.device)
+    mu = None if mean is None else mean.to(torch.float64).to(X.device).contiguous()
+    rc = nat.native().gram64(X.data_ptr(), int(X.dtype == torch.float64), X.stride(0),
+                             0 if mu is None else mu.data_ptr(), n, d, part.data_ptr(), grid,
+                             nat.stream_handle(X.device))
+    if rc:
+        raise RuntimeError(f"gram64 failed (hip error {rc})")
+    blocks = part.sum(0)
+    Gp = torch.zeros((nb * 16, nb * 16), dtype=torch.float64, device=X.device)
+    iu = torch.triu_indices(nb, nb).tolist()
+    for t, (bi, bj) in enumerate(zip(*iu)):
+        Gp[16 * bi:16 * bi + 16, 16 * bj:16 * bj + 16] = blocks[t]
+        if bi != bj:
+            Gp[16 * bj:16 * bj + 16, 16 * bi:16 * bi + 16] = blocks[t].T
+    return Gp[:d, :d].contiguous()
+
+
+def gram64_local(X, mean=None, W=None, chunk_rows=1 << 19):
+    """Local partial of G = ((X - mean) W)^T ((X - mean) W) accumulated in
+    fp64.  GPU: the fp64-MFMA kernel (:func:`gram64_native`) on X (pass 1)
+    or on row chunks of (X - mean) W formed by library DGEMM (pass 2); CPU:
+    torch fp64.  The building block of the fp64-faithful sharded
+    CholeskyQR2 (:func:`cholqr2_r`)."""
+    n, d = X.shape
+    dw = d if W is None else W.shape[1]
+    native = (nat.use_native(X) and X.dtype in (torch.float32, torch.float64) and d <= 256
+              and dw <= 256 and X.stride(1) == 1)
+    if native and W is None:
+        return gram64_native(X, mean)
+    G = torch.zeros((dw, dw), dtype=torch.float64, device=X.device)
+    m = None if mean is None else mean.to(torch.float64).to(X.device)
+    Wd = None if W is None else W.to(torch.float64).to(X.device)
+    for s in range(0, n, chunk_rows):
+        Xc = X[s:s + chunk_rows].to(torch.float64)
+        if m is not None:
+            Xc = Xc - m
+        if Wd is not None:
+            Xc = Xc @ Wd
+        if native:
+            G += gram64_native(Xc.contiguous())
+        else:
+            G.addmm_(Xc.T, Xc)
+    return G
+
+
+def cholqr2_r(X, comm, mean=None):
+    """R factor of the thin QR of the row-sharded matrix X - mean by
+    CholeskyQR2 in fp64 (two passes over X, one d x d all-reduce each):
+    R1 = chol(X^T X), R2 = chol((X R1^-1)^T (X R1^-1)), R = R2 R1.  The
+    singular values of R are those of X to ~eps64 * cond(X) relative (the
+    Gram eigenvalues alone: eps * cond^2).  Returns None when the first
+    Cholesky fails (cond(X) >~ 1e8 or rank deficient): callers fall back to
+    the Gram eigenvalues."""
+    G1 = comm.all_reduce_(gram64_local(X, mean))
+    G1 = 0.5 * (G1 + G1.T)
+    R1, info = torch.linalg.cholesky_ex(G1, upper=True)
+    if int(info) != 0:
+        return None
+    eye = torch.eye(G1.shape[0], dtype=torch.float64, device=G1.device)
+    W1 = torch.linalg.solve_triangular(R1, eye, upper=True)
+    G2 = comm.all_reduce_(gram64_local(X, mean, W1))
+    G2 = 0.5 * (G2 + G2.T)
+    R2, info = torch.linalg.cholesky_ex(G2, upper=True)
+    if int(info) != 0:
+        return None
+    return R2 @ R1
+
+
 def power_iter_local(X, Q, mean):
     """Local partial of Z = (X - mean)^T ((X - mean) Q)  (one pass over X)."""
     n, d = X.shape

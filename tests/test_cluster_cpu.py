@@ -223,3 +223,43 @@ def test_elkan_single_cluster_warns():
     X = np.random.RandomState(0).randn(50, 3)
     with pytest.warns(RuntimeWarning, match="single cluster"):
         KMeans(1, algorithm="elkan", n_init=1).fit(X)
+
+
+def _kpp_oracle(X, k, rs, t=None):
+    """The reference's greedy k-means++ (``cluster/_kmeans.py:153-247``),
+    verbatim semantics in numpy fp64."""
+    n = X.shape[0]
+    t = t or 2 + int(np.log(k))
+    xn = (X * X).sum(1)
+    idx = [rs.randint(n)]
+    closest = np.maximum(xn + xn[idx[0]] - 2 * X @ X[idx[0]], 0)
+    pot = closest.sum()
+    for _ in range(1, k):
+        vals = rs.random_sample(t) * pot
+        cand = np.clip(np.searchsorted(np.cumsum(closest), vals), None, n - 1)
+        D = np.maximum(xn[None, :] + xn[cand][:, None] - 2 * X[cand] @ X.T, 0)
+        D = np.minimum(closest, D)
+        p = D.sum(1)
+        b = int(np.argmin(p))
+        pot, closest = p[b], D[b]
+        idx.append(cand[b])
+    return np.array(idx)
+
+
+@pytest.mark.parametrize("k", [3, 17])
+def test_kmeans_plusplus_matches_reference_algorithm(k):
+    rng = np.random.RandomState(0)
+    X = rng.standard_normal((600, 7))
+    _, idx = kmeans_plusplus(X, k, random_state=5)
+    np.testing.assert_array_equal(idx, _kpp_oracle(X, k, np.random.RandomState(5)))
+
+
+def test_kmeans_parallel_init(blobs):
+    X, y = blobs
+    q = QMeans(n_clusters=4, init="k-means||", n_init=1, delta=0.0, intermediate_error=False,
+               random_state=0, device="cpu").fit(X)
+    assert adjusted_rand_score(q.labels_, y) > 0.95
+    k = KMeans(n_clusters=4, init="k-means||", n_init=1, random_state=0, device="cpu").fit(X)
+    assert adjusted_rand_score(k.labels_, y) > 0.95
+    k2 = KMeans(n_clusters=4, init="k-means||", n_init=1, random_state=0, device="cpu").fit(X)
+    np.testing.assert_allclose(k.cluster_centers_, k2.cluster_centers_)
