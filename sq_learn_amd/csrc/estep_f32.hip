@@ -429,28 +429,37 @@ __global__ void __launch_bounds__(256) band_rows_f64_kernel(
 // tile; only the HI region of each operand tile is staged (34 KiB per slot at
 // d = 256).
 constexpr int kMaxCand = 16;
+#ifndef SQ_X64_NW
+#define SQ_X64_NW 8
+#endif
+constexpr int kX64Waves = SQ_X64_NW;   // waves per workgroup (2 per SIMD at 8)
+#ifndef SQ_X64_RING
+#define SQ_X64_RING 3
+#endif
+#ifndef SQ_X64_PIN
+#define SQ_X64_PIN 1
+#endif
+constexpr int kX64Ring = SQ_X64_RING;  // centroid-tile LDS slots (3: 2 tiles in flight)
 template <int KSD>
 __global__ void __launch_bounds__(512) estep_x64_kernel(
     const _Float16* __restrict__ Xh, const float* __restrict__ X, const _Float16* __restrict__ C,
     const float* __restrict__ Cm, const float* __restrict__ xn, const float* __restrict__ cmax2_p,
     int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ dense_rows,
-    int* __restrict__ dense_count, long long n, int k_pad, float alpha, float delta_s,
-    double delta, RngKey key, long long row_offset, int dense_cap, int qbits) {
-  constexpr int NW = 8;
+    int* __restrict__ dense_count, long long* __restrict__ mrows, int* __restrict__ mcand,
+    int* __restrict__ multi_count, long long n, int k_pad, float alpha, float delta_s,
+    RngKey key, long long row_offset, int dense_cap, int qbits) {
+  constexpr int NW = kX64Waves;
   constexpr int DX = KSD * 16;
   constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
   constexpr int TILE_STRIDE = (2 * KSD + 1) * 2048;
   constexpr int PIECES = HI_BYTES / 1024;
   constexpr int ROWS = NW * 32;
-  constexpr int LPP = DX >= 64 ? 16 : DX / 4;  // lanes per (row, candidate) pair in the re-check
-  constexpr int FPL = DX / LPP;                // features per lane (a multiple of 4)
-  constexpr int MAXP = 32 * kMaxCand;          // (row, candidate) pairs per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  auto buf = [&](int g) -> unsigned char* { return smem + (g & 1) * HI_BYTES; };
-  int* cand_all = reinterpret_cast<int*>(smem + 2 * HI_BYTES);       // [NW][32][kMaxCand]
+  constexpr int RING = kX64Ring;                // LDS tile slots
+  constexpr int PPW = (PIECES + NW - 1) / NW;   // glds per wave per stage (uniform: counted vmcnt)
+  auto buf = [&](int g) -> unsigned char* { return smem + (g % RING) * HI_BYTES; };
+  int* cand_all = reinterpret_cast<int*>(smem + RING * HI_BYTES);    // [NW][32][kMaxCand]
   int* cnt_all = cand_all + NW * 32 * kMaxCand;                       // [NW][32]
-  double* dist_all = reinterpret_cast<double*>(cnt_all + NW * 32);    // [NW][32][kMaxCand]
-  int* pair_all = reinterpret_cast<int*>(dist_all + NW * MAXP);       // [NW][MAXP]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -463,8 +472,6 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
   if (blk >= nblk) return;
   int* cand = cand_all + wave * 32 * kMaxCand;
   int* cnt = cnt_all + wave * 32;
-  double* dist = dist_all + wave * MAXP;
-  int* pairs = pair_all + wave * MAXP;
   const uint32_t qmask = (1u << qbits) - 1u;
   const uint32_t keep = ~qmask;
   // rigorous bound constants (fp32, rounded up by the 1.0625 / 1+2^-16 factors)
@@ -476,7 +483,11 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     const int t = G % n_tiles;
     const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_STRIDE;
     unsigned char* dst = buf(G);
-    for (int p = wave; p < PIECES; p += NW) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      // every wave issues PPW loads (the surplus repeat the last piece: same
+      // bytes to the same LDS slot) so one counted vmcnt fits all waves
+      const int p = wave + NW * i < PIECES ? wave + NW * i : PIECES - 1;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
           (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
@@ -529,7 +540,9 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
             ins(i, o1[i], q1);
           }
         }
+#if SQ_X64_PIN
         __builtin_amdgcn_sched_barrier(0);
+#endif
       }
       n0 = acc0;
       n1 = acc1;
@@ -541,15 +554,26 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
       }
     }
   };
+  // RING == 2: the tile staged in this step must land before the barrier
+  // (vmcnt(0)).  RING == 3: staging runs two tiles ahead and the barrier
+  // only retires the tile staged one step earlier - vmcnt(PPW) leaves this
+  // step's glds in flight across the raw s_barrier (no __syncthreads: its
+  // fence would drain them).
   auto sync_tile = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (RING == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    }
+    __builtin_amdgcn_s_barrier();
   };
 
   int G = 0;
   stage(0);
+  if constexpr (RING == 3) stage(1);
   load_a(blk);
-  sync_tile();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   for (; blk < nblk; blk += gridDim.x) {
     const long long row0 = blk * ROWS + wave * 32;
@@ -557,7 +581,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     for (int i = 0; i < 16; ++i) m1[i] = m2[i] = m3[i] = __builtin_inff();
     if (lane < 32) cnt[lane] = 0;
     f32x16 pA0, pA1, pB0, pB1;
-    stage(G + 1);
+    stage(G + RING - 1);
     tile_step(buf(G), pA0, pA1, true, pA0, pA1, 0, false);
     sync_tile();
     int t = 0;
@@ -567,7 +591,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
         tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
         break;
       }
-      stage(G + 2);
+      stage(G + RING);
       tile_step(buf(G + 1), pB0, pB1, true, pA0, pA1, t, true);
       sync_tile();
       ++t;
@@ -577,7 +601,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
         tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
         break;
       }
-      stage(G + 2);
+      stage(G + RING);
       tile_step(buf(G + 1), pA0, pA1, true, pB0, pB1, t, true);
       sync_tile();
       ++t;
@@ -649,77 +673,121 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
         mind[g] = -1.0f;   // filled by the M-step's segmented reduce
       }
     }
-    // flatten the multi rows' (row, candidate) pairs: exclusive scan of the
-    // per-row counts over lanes 0..31
-    const int pc = (multi && half == 0) ? c_r : 0;
-    int incl = pc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += v;
+    // multi-candidate rows -> global list; their fp64 re-check runs in
+    // recheck_rows_kernel (latency-bound global loads kept out of this
+    // MFMA-bound sweep); a full list routes rows to the dense path
+    const bool mrow = multi && half == 0;
+    const unsigned long long mm = __ballot(mrow);
+    const int nm = __popcll(mm);
+    int mbase = 0;
+    if (lane == 0 && nm) mbase = atomicAdd(multi_count, nm);
+    mbase = __shfl(mbase, 0, 64);
+    if (mrow) {
+      const long long slot = (long long)mbase + __popcll(mm & ((1ull << lane) - 1ull));
+      if (slot < n) {
+        mrows[slot] = g;
+        int* mc = mcand + slot * (kMaxCand + 1);
+        mc[0] = c_r;
+        for (int c = 0; c < c_r; ++c) mc[1 + c] = cand[r32 * kMaxCand + c];
+      } else {
+        const int s2 = atomicAdd(dense_count, 1);
+        if (s2 < dense_cap) dense_rows[s2] = g;
+        labels[g] = -1;
+      }
     }
-    const int npairs = __shfl(incl, 63, 64);
-    for (int c = 0; c < pc; ++c) pairs[incl - pc + c] = (r32 << 8) | c;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    // ---- exact distances: 8 lanes per pair, FPL features per lane, all the
-    // round's loads issued before the first FMA
-    for (int base = 0; base < npairs; base += 64 / LPP) {   // wave-uniform
-      const int pi = base + lane / LPP;
-      const int sub = lane % LPP;
-      const bool live = pi < npairs;
-      const int pr = live ? pairs[pi] : 0;
-      const int rr = pr >> 8, cc = pr & 0xFF;
-      const int j = live ? cand[rr * kMaxCand + cc] : 0;
-      const long long gr = row0 + rr;
-      const float* xr = X + (size_t)(live ? gr : 0) * DX + sub * FPL;
-      const float* cr = Cm + (size_t)j * DX + sub * FPL;
-      float4 xv[FPL / 4], cv[FPL / 4];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// fp64 re-check of the multi-candidate rows listed by estep_x64_kernel: the
+// candidates' distances sum_f (x_f - c_f)^2 in fp64 (scipy cdist's formula,
+// the reference's ``_dmeans.py:736-737``), then the delta-band rule exactly
+// as band.h: min, members {d <= min + delta}, the member of kappa rank
+// r = band_rank(u, |band|), kappa(j) = (j mod 32, j div 32).  A wave takes 4
+// list rows (16 lanes each, 16 features per lane at d = 256) and keeps its
+// row in registers across that row's candidates; short kernel, many waves
+// per CU, so the row / centroid gathers overlap.
+template <int DX>
+__global__ void __launch_bounds__(256) recheck_rows_kernel(
+    const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
+    const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
+    float* __restrict__ mind, long long cap, double delta, RngKey key, long long row_offset) {
+  constexpr int LPR = 16;                  // lanes per row
+  constexpr int FPL = DX / LPR;            // features per lane (DX >= 64) or fewer
+  constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const long long cnt = min((long long)*multi_count, cap);
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long base = gw * 4; base < cnt; base += nw * 4) {
+    const long long e = base + (lane >> 4);
+    const bool live = e < cnt;
+    const long long g = live ? mrows[e] : 0;
+    const int* mc = mcand + (live ? e : 0) * (kMaxCand + 1);
+    const int c_r = live ? mc[0] : 0;
+    float4 xv[F4];
+    const float* xr = X + (size_t)g * DX + sub * 4 * F4;
 #pragma unroll
-      for (int q = 0; q < FPL / 4; ++q) {
-        xv[q] = *reinterpret_cast<const float4*>(xr + 4 * q);
-        cv[q] = *reinterpret_cast<const float4*>(cr + 4 * q);
-      }
+    for (int q = 0; q < F4; ++q)
+      xv[q] = (sub * 4 * F4 + 4 * q < DX) ? *reinterpret_cast<const float4*>(xr + 4 * q)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    double dl[kMaxCand];
+    int cl[kMaxCand];
+    int cmax = c_r;
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
+    for (int c = 0; c < cmax; ++c) {            // wave-uniform trip count
+      const int j = c < c_r ? mc[1 + c] : 0;
+      const float* cr = Cm + (size_t)j * DX + sub * 4 * F4;
       double s = 0.0;
 #pragma unroll
-      for (int q = 0; q < FPL / 4; ++q) {
-        const double e0 = (double)xv[q].x - (double)cv[q].x, e1 = (double)xv[q].y - (double)cv[q].y;
-        const double e2 = (double)xv[q].z - (double)cv[q].z, e3 = (double)xv[q].w - (double)cv[q].w;
-        s = fma(e0, e0, fma(e1, e1, fma(e2, e2, fma(e3, e3, s))));
+      for (int q = 0; q < F4; ++q) {
+        if (sub * 4 * F4 + 4 * q < DX) {
+          const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * q);
+          const double e0 = (double)xv[q].x - (double)cv.x, e1 = (double)xv[q].y - (double)cv.y;
+          const double e2 = (double)xv[q].z - (double)cv.z, e3 = (double)xv[q].w - (double)cv.w;
+          s = fma(e0, e0, fma(e1, e1, fma(e2, e2, fma(e3, e3, s))));
+        }
       }
 #pragma unroll
-      for (int o = 1; o < LPP; o <<= 1) s += __shfl_xor(s, o, 64);
-      if (live && sub == 0) dist[rr * kMaxCand + cc] = s;
+      for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o, 64);
+#pragma unroll
+      for (int t = 0; t < kMaxCand; ++t)
+        if (t == c) { dl[t] = s; cl[t] = j; }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    if (multi && half == 0) {
-      const double* dl = dist + r32 * kMaxCand;
-      const int* cl = cand + r32 * kMaxCand;
+    if (live && sub == 0) {
       double dmin = dl[0];
-      for (int c = 1; c < c_r; ++c) dmin = fmin(dmin, dl[c]);
+#pragma unroll
+      for (int c = 1; c < kMaxCand; ++c)
+        if (c < c_r) dmin = fmin(dmin, dl[c]);
       const double thr = dmin + delta;
       int b = 0;
-      for (int c = 0; c < c_r; ++c) b += dl[c] <= thr ? 1 : 0;
+#pragma unroll
+      for (int c = 0; c < kMaxCand; ++c) b += (c < c_r && dl[c] <= thr) ? 1 : 0;
       const int r = band_rank(band_u(key, row_offset + g), b);
-      // the band member of kappa rank r, kappa(j) = (j mod 32, j div 32)
       int pick = cl[0];
-      for (int c = 0; c < c_r; ++c) {
-        if (!(dl[c] <= thr)) continue;
-        const int jc = cl[c];
-        const int kc = ((jc & 31) << 20) | (jc >> 5);
-        int rank = 0;
-        for (int c2 = 0; c2 < c_r; ++c2) {
-          const int j2 = cl[c2];
-          rank += (dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
+#pragma unroll
+      for (int c = 0; c < kMaxCand; ++c) {
+        if (c < c_r && dl[c] <= thr) {
+          const int jc = cl[c];
+          const int kc = ((jc & 31) << 20) | (jc >> 5);
+          int rank = 0;
+#pragma unroll
+          for (int c2 = 0; c2 < kMaxCand; ++c2) {
+            const int j2 = cl[c2];
+            rank += (c2 < c_r && dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
+          }
+          if (rank == r) pick = jc;
         }
-        if (rank == r) pick = jc;
       }
       labels[g] = pick;
       mind[g] = (float)dmin;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -869,12 +937,12 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
 template <int KSD>
 static int launch_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm,
                             const void* xn, const void* cmax2, void* labels, void* mind,
-                            void* dense_rows, void* dense_count, long long n, int k_pad,
-                            float alpha, float delta_s, double delta, RngKey key,
-                            long long row_offset, int dense_cap, hipStream_t st) {
-  constexpr int NW = 8;
-  const size_t lds = 2 * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4 +
-                     (size_t)NW * 32 * kMaxCand * (8 + 4);
+                            void* dense_rows, void* dense_count, void* mrows, void* mcand,
+                            void* multi_count, long long n, int k_pad, float alpha,
+                            float delta_s, double delta, RngKey key, long long row_offset,
+                            int dense_cap, hipStream_t st) {
+  constexpr int NW = kX64Waves;
+  const size_t lds = kX64Ring * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4;
   auto kern = estep_x64_kernel<KSD>;
   static bool attr = false;
   if (!attr) {
@@ -896,8 +964,17 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const _Float16*)Xh,
                      (const float*)X, (const _Float16*)C, (const float*)Cm, (const float*)xn,
                      (const float*)cmax2, (int*)labels, (float*)mind, (long long*)dense_rows,
-                     (int*)dense_count, n, k_pad, alpha, delta_s, delta, key, row_offset,
-                     dense_cap, qbits);
+                     (int*)dense_count, (long long*)mrows, (int*)mcand, (int*)multi_count, n,
+                     k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  // the re-check: one pass over the multi list (count read on the device)
+  const long long rblocks = (n / 16 + 63) / 64;
+  const unsigned rgrid = (unsigned)(rblocks < 4096 ? (rblocks > 0 ? rblocks : 1) : 4096);
+  hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
+                     (const float*)X, (const float*)Cm, (const long long*)mrows,
+                     (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
+                     delta, key, row_offset);
   return (int)hipGetLastError();
 }
 
@@ -936,14 +1013,17 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 
 // Certified E-step (the default): filter + fp64 re-check (estep_x64_kernel),
 // dense rows through the 3-pass fp32-faithful kernel in list mode, its
-// overflow rows through band_rows_f64.  counts[0] = 3-pass overflow rows,
-// counts[1] = dense rows; both must be zero on entry.  mind holds -1 for rows
+// overflow rows through band_rows_f64, the multi-candidate rows through
+// recheck_rows_kernel.  counts[0] = 3-pass overflow rows, counts[1] = dense
+// rows, counts[2] = multi rows; all zero on entry.  mrows [n] (int64) and
+// mcand [n][kMaxCand + 1] (int32) hold the multi list.  mind holds -1 for rows
 // whose distance the M-step (or fill_mind) computes; no inertia here.
 // Xh: fp16(alpha x) [n][d_pad]; X: fp32 [n][d_pad]; Cm: fp32 centroids
 // [k][d_pad] (zero-padded like X); C: the fp16-split operand.
 int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
                  const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
-                 void* counts, void* part, int part_cap, long long n, int d, int d_pad, int k,
+                 void* mrows, void* mcand, void* counts, void* part, int part_cap, long long n,
+                 int d, int d_pad, int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
@@ -960,9 +1040,9 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   switch (d_pad) {
 #define CASE(KSD)                                                                                \
   case KSD * 16:                                                                                 \
-    rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1, n,    \
-                               k_pad, fa, ds, delta, key, row_offset, (int)min(n, 2147483647LL),  \
-                               st);                                                              \
+    rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
+                               mrows, mcand, cnt + 2, n, k_pad, fa, ds, delta, key, row_offset,  \
+                               (int)min(n, 2147483647LL), st);                                   \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \

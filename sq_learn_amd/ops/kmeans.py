@@ -174,10 +174,13 @@ class EStepBuffers:
         self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(n, 1))
         self.ovf_rows = torch.empty(self.ovf_cap, dtype=torch.int64, device=device)
         self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
-        # [overflow rows, dense rows] (int32); ovf_count is a view of slot 0
-        self.counts = torch.zeros(2, dtype=torch.int32, device=device)
+        # [overflow rows, dense rows, multi-candidate rows] (int32); ovf_count
+        # is a view of slot 0
+        self.counts = torch.zeros(3, dtype=torch.int32, device=device)
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
+        self.multi_rows = None   # certified E-step: rows sent to the fp64 re-check kernel
+        self.multi_cand = None   # ... and their candidate lists [n][1 + 16]
         # True while ovf_count is known to be zero (fresh, or reset on the
         # device by the iteration-scalars launch): the E-step skips its memset
         self.ovf_clean = True
@@ -530,12 +533,16 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     assert k <= k_pad <= 4096 and buf.labels.numel() >= n
     if buf.dense_rows is None or buf.dense_rows.numel() < n:
         buf.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
+    if buf.multi_rows is None or buf.multi_rows.numel() < n:
+        buf.multi_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
+        buf.multi_cand = torch.empty((max(n, 1), 17), dtype=torch.int32, device=Xf.device)
     st = stream if stream is not None else nat.stream_handle(Xf.device)
     buf.counts.zero_()
     buf.ovf_clean = False
     nat.native().estep_x64(Xh.data_ptr(), Xf.data_ptr(), C_op.data_ptr(), C_pad.data_ptr(),
                            xn.data_ptr(), cmax2.data_ptr(), buf.labels.data_ptr(),
                            buf.mind.data_ptr(), buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
+                           buf.multi_rows.data_ptr(), buf.multi_cand.data_ptr(),
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)
