@@ -359,7 +359,7 @@ constexpr int kF64MaxK = 4096;
 __global__ void __launch_bounds__(256) band_rows_f64_kernel(
     const float* __restrict__ X, const float* __restrict__ C, const long long* __restrict__ rows,
     const int* __restrict__ count, int* __restrict__ labels, long long cap, int ldx, int d, int k,
-    double delta, RngKey key, long long row_offset) {
+    double delta, RngKey key, long long row_offset, float* __restrict__ corr) {
   __shared__ double xs[256];
   __shared__ double ds[kF64MaxK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -387,7 +387,10 @@ __global__ void __launch_bounds__(256) band_rows_f64_kernel(
       for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, 64));
       auto dist = [&](int j) -> double { return ds[j]; };
       const int win = band_pick_wave(dist, k, mn + delta, band_u(key, row_offset + r), lane);
-      if (lane == 0) labels[r] = win;
+      if (lane == 0) {
+        labels[r] = win;
+        if (corr) corr[r] = (float)(mn - ds[win]);   // min - distance to the label
+      }
     }
   }
 }
@@ -714,7 +717,8 @@ template <int DX>
 __global__ void __launch_bounds__(256) recheck_rows_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
-    float* __restrict__ mind, long long cap, double delta, RngKey key, long long row_offset) {
+    float* __restrict__ mind, long long cap, double delta, RngKey key, long long row_offset,
+    float* __restrict__ corr) {
   constexpr int LPR = 16;                  // lanes per row
   constexpr int FPL = DX / LPR;            // features per lane (DX >= 64) or fewer
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
@@ -770,6 +774,7 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
       for (int c = 0; c < kMaxCand; ++c) b += (c < c_r && dl[c] <= thr) ? 1 : 0;
       const int r = band_rank(band_u(key, row_offset + g), b);
       int pick = cl[0];
+      double dpick = dl[0];
 #pragma unroll
       for (int c = 0; c < kMaxCand; ++c) {
         if (c < c_r && dl[c] <= thr) {
@@ -781,12 +786,37 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
             const int j2 = cl[c2];
             rank += (c2 < c_r && dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
           }
-          if (rank == r) pick = jc;
+          if (rank == r) { pick = jc; dpick = dl[c]; }
         }
       }
       labels[g] = pick;
       mind[g] = (float)dmin;
+      if (corr) corr[g] = (float)(dmin - dpick);
     }
+  }
+}
+
+// Rows resolved by the 3-pass kernel (dense list): corr = mind - exact fp64
+// |x - c_label|^2 (the per-cluster inertia of the incremental M-step counts
+// every row at its label's distance; corr brings it back to the min).
+__global__ void __launch_bounds__(256) dense_corr_kernel(
+    const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ rows,
+    const int* __restrict__ count, const int* __restrict__ labels, const float* __restrict__ mind,
+    float* __restrict__ corr, long long cap, int d) {
+  const int lane = threadIdx.x & 63;
+  const long long cnt = min((long long)*count, cap);
+  for (long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); e < cnt;
+       e += (long long)gridDim.x * 4) {
+    const long long r = rows[e];
+    const int l = labels[r];
+    if (l < 0) continue;
+    double s = 0.0;
+    for (int f = lane; f < d; f += 64) {
+      const double df = (double)X[(size_t)r * d + f] - (double)Cm[(size_t)l * d + f];
+      s = fma(df, df, s);
+    }
+    s = wave_sum(s);
+    if (lane == 0) corr[r] = (float)((double)mind[r] - s);
   }
 }
 
@@ -938,7 +968,7 @@ template <int KSD>
 static int launch_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm,
                             const void* xn, const void* cmax2, void* labels, void* mind,
                             void* dense_rows, void* dense_count, void* mrows, void* mcand,
-                            void* multi_count, long long n, int k_pad, float alpha,
+                            void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st) {
   constexpr int NW = kX64Waves;
@@ -974,7 +1004,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,
                      (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
-                     delta, key, row_offset);
+                     delta, key, row_offset, (float*)corr);
   return (int)hipGetLastError();
 }
 
@@ -1022,8 +1052,8 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 // [k][d_pad] (zero-padded like X); C: the fp16-split operand.
 int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
                  const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
-                 void* mrows, void* mcand, void* counts, void* part, int part_cap, long long n,
-                 int d, int d_pad, int k,
+                 void* mrows, void* mcand, void* corr, void* counts, void* part, int part_cap,
+                 long long n, int d, int d_pad, int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
@@ -1036,12 +1066,14 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   const double a2 = alpha * alpha;
   const float fa = (float)alpha, ia2 = (float)(1.0 / a2), ds = (float)(delta * a2);
   int* cnt = (int*)counts;
+  if (corr) hipMemsetAsync(corr, 0, (size_t)n * sizeof(float), st);
   int rc;
   switch (d_pad) {
 #define CASE(KSD)                                                                                \
   case KSD * 16:                                                                                 \
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
-                               mrows, mcand, cnt + 2, n, k_pad, fa, ds, delta, key, row_offset,  \
+                               mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
+                               row_offset,                                                       \
                                (int)min(n, 2147483647LL), st);                                   \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
@@ -1054,9 +1086,14 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
       return (int)hipErrorInvalidValue;
   }
   if (rc) return rc;
+  if (corr)
+    hipLaunchKernelGGL(dense_corr_kernel, dim3(256), dim3(256), 0, st, (const float*)X,
+                       (const float*)Cm, (const long long*)dense_rows, (const int*)(cnt + 1),
+                       (const int*)labels, (const float*)mind, (float*)corr, n, d_pad);
   hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(n < 2048 ? n : 2048)), dim3(256), 0,
                      st, (const float*)X, (const float*)Cm, (const long long*)ovf_rows,
-                     (const int*)cnt, (int*)labels, n, d_pad, d_pad, k, delta, key, row_offset);
+                     (const int*)cnt, (int*)labels, n, d_pad, d_pad, k, delta, key, row_offset,
+                     (float*)corr);
   return (int)hipGetLastError();
 }
 
@@ -1087,7 +1124,7 @@ int sq_band_rows_f64(const void* X, const void* C, const void* rows, const void*
   hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(cap < 2048 ? cap : 2048)), dim3(256), 0,
                      (hipStream_t)stream, (const float*)X, (const float*)C,
                      (const long long*)rows, (const int*)count, (int*)labels, cap, ldx, d, k,
-                     delta, key, row_offset);
+                     delta, key, row_offset, (float*)nullptr);
   return (int)hipGetLastError();
 }
 

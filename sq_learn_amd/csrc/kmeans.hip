@@ -871,6 +871,160 @@ __global__ void __launch_bounds__(256) label_scatter_kernel(const int* __restric
   }
 }
 
+#ifndef SQ_SEG_U
+#define SQ_SEG_U 4   // rows in flight per wave (perm -> label/row gathers)
+#endif
+// ---------------------------------------------------------------------------
+// Incremental M-step (the rows are the same every Lloyd iteration, only the
+// labels move): the fixed-point cluster statistics
+//   S_c = sum q(x_i),  n_c = |{i}|,  Q_c = sum q2(|x_i|^2)     (i: label c)
+// are exact integers in fp64 (see the quantisation note above), so
+//   S(t+1) = S(t) + sum_{i moved into c} q(x_i) - sum_{i moved out} q(x_i)
+// is bit-identical to summing the new members from scratch, in any order.
+// Only the moved rows are read: a signed entry list (row << 1 | out) is
+// counting-sorted by the label it updates (new label for "in", previous for
+// "out") and summed with the same run-length flushes as segment_sum_rows.
+// prev < 0 marks "no previous label" (first iteration / after a reset:
+// every row enters).  Q feeds the per-cluster inertia (cluster_inertia).
+__global__ void __launch_bounds__(256) delta_hist_kernel(const int* __restrict__ labels,
+                                                         const int* __restrict__ prev,
+                                                         long long n, int k,
+                                                         int* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) int dh[];
+  for (int j = threadIdx.x; j < k; j += 256) dh[j] = 0;
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * kHistChunk;
+  const long long r1 = min(n, r0 + kHistChunk);
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    const int l = labels[r], p = prev[r];
+    if (l == p) continue;
+    if (l >= 0 && l < k) atomicAdd(&dh[l], 1);
+    if (p >= 0 && p < k) atomicAdd(&dh[p], 1);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256)
+    if (dh[j]) atomicAdd(&hist[j], dh[j]);
+}
+
+__global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restrict__ labels,
+                                                            const int* __restrict__ prev,
+                                                            long long n, int k,
+                                                            int* __restrict__ cursor,
+                                                            int* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) int ds2[];
+  int* lh = ds2;
+  int* base = ds2 + k;
+  for (int j = threadIdx.x; j < k; j += 256) lh[j] = 0;
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * kHistChunk;
+  const long long r1 = min(n, r0 + kHistChunk);
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    const int l = labels[r], p = prev[r];
+    if (l == p) continue;
+    if (l >= 0 && l < k) atomicAdd(&lh[l], 1);
+    if (p >= 0 && p < k) atomicAdd(&lh[p], 1);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256) {
+    const int c = lh[j];
+    base[j] = c ? atomicAdd(&cursor[j], c) : 0;
+    lh[j] = 0;
+  }
+  __syncthreads();
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    const int l = labels[r], p = prev[r];
+    if (l == p) continue;
+    if (l >= 0 && l < k) perm[base[l] + atomicAdd(&lh[l], 1)] = (int)(r << 1);
+    if (p >= 0 && p < k) perm[base[p] + atomicAdd(&lh[p], 1)] = (int)((r << 1) | 1);
+  }
+}
+
+// one wave per entry (d <= 256: 4 fp32 values per lane), SQ_SEG_U entries in
+// flight per wave; the entry count is the scanned total (cursor[k-1]).
+__global__ void __launch_bounds__(512) delta_segment_kernel(
+    const float* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
+    const int* __restrict__ prev, int d, int range, float xscale, double qscale,
+    double* __restrict__ sums, double* __restrict__ counts, double* __restrict__ qsum,
+    const int* __restrict__ valid_end) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long p0 = (long long)blockIdx.x * range;
+  const long long p1 = min((long long)*valid_end, p0 + range);
+  constexpr int U = SQ_SEG_U;
+  const int c0 = lane * 4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, aq = 0.0, cnt = 0.0;
+  int cur = -1;
+  auto flush = [&]() {
+    double* dst = sums + (size_t)cur * d + c0;
+    if (c0 < d) {
+      if (a0 != 0.0) atomicAdd(dst + 0, a0);
+      if (a1 != 0.0 && c0 + 1 < d) atomicAdd(dst + 1, a1);
+      if (a2 != 0.0 && c0 + 2 < d) atomicAdd(dst + 2, a2);
+      if (a3 != 0.0 && c0 + 3 < d) atomicAdd(dst + 3, a3);
+    }
+    const double q = wave_sum(aq);   // integer-valued: exact in any order
+    if (lane == 0) {
+      if (cnt != 0.0) atomicAdd(&counts[cur], cnt);
+      if (q != 0.0) atomicAdd(&qsum[cur], q);
+    }
+  };
+  for (long long p = p0 + wave; p < p1; p += 8 * U) {
+    int code[U], ll[U];
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long q = p + 8LL * u;
+      code[u] = q < p1 ? perm[q] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = code[u] >= 0 ? (code[u] >> 1) : 0;
+      ll[u] = code[u] < 0 ? -1 : ((code[u] & 1) ? prev[r] : labels[r]);
+      v[u] = (code[u] >= 0 && c0 < d) ? *reinterpret_cast<const float4*>(X + (size_t)r * d + c0)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ll[u] < 0) continue;      // wave-uniform (one entry per wave)
+      if (ll[u] != cur) {
+        if (cur >= 0) flush();
+        cur = ll[u];
+        a0 = a1 = a2 = a3 = aq = cnt = 0.0;
+      }
+      const double sg = (code[u] & 1) ? -1.0 : 1.0;
+      a0 += sg * (double)rintf(v[u].x * xscale);
+      a1 += sg * (double)rintf(v[u].y * xscale);
+      a2 += sg * (double)rintf(v[u].z * xscale);
+      a3 += sg * (double)rintf(v[u].w * xscale);
+      const double x0 = v[u].x, x1 = v[u].y, x2 = v[u].z, x3 = v[u].w;   // squares exact in fp64
+      aq += sg * (rint(x0 * x0 * qscale) + rint(x1 * x1 * qscale) + rint(x2 * x2 * qscale) +
+                  rint(x3 * x3 * qscale));
+      cnt += sg;
+    }
+  }
+  if (cur >= 0) flush();
+}
+
+// inertia part of cluster c at the E-step's centroids C (fp32 [k][d]):
+//   sum_{i: label c} |x_i - c|^2 = Q_c - 2 c.S_c + n_c |c|^2
+// from the fixed-point statistics (fp64; one wave per cluster).
+__global__ void __launch_bounds__(256) cluster_inertia_kernel(
+    const double* __restrict__ sums, const double* __restrict__ counts,
+    const double* __restrict__ qsum, const float* __restrict__ C, int k, int d, double xunit,
+    double qunit, double* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= k) return;
+  double cs = 0.0, cc = 0.0;
+  for (int f = lane; f < d; f += 64) {
+    const double cf = (double)C[(size_t)c * d + f];
+    cs = fma(cf, sums[(size_t)c * d + f], cs);
+    cc = fma(cf, cf, cc);
+  }
+  cs = wave_sum(cs);
+  cc = wave_sum(cc);
+  if (lane == 0) part[c] = qsum[c] * qunit - 2.0 * cs * xunit + counts[c] * cc;
+}
+
 // Deterministic segmented sums: every contribution is quantised to an
 // integer multiple of 2^qexp (x * 2^-qexp rounded in fp32: exact scaling by a
 // power of two, then v_rndne) and accumulated in fp64.  The host picks qexp
@@ -1631,6 +1785,45 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
     return (int)hipErrorInvalidValue;
   }
 #undef SEG_CASE
+  return (int)hipGetLastError();
+}
+
+// Incremental fixed-point cluster statistics (see delta_segment_kernel):
+// sums / counts / qsum are UPDATED (not overwritten) by the rows whose label
+// differs from prev; qexp is the quantum of the squared norms.
+int sq_centroid_delta(const void* X, const void* labels, const void* prev, void* sums,
+                      void* counts, void* qsum, long long n, int d, int k, int xexp, int qexp,
+                      void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
+  if (n <= 0) return 0;
+  if (d % 4 != 0 || d > 256 || k > 16384 || 2 * n > 2147483647LL) return (int)hipErrorInvalidValue;
+  if (xexp < -120 || xexp > 120 || qexp < -200 || qexp > 200) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
+  hipLaunchKernelGGL(delta_hist_kernel, dim3(chunks), dim3(256), (size_t)k * 4, st,
+                     (const int*)labels, (const int*)prev, n, k, (int*)ws_hist);
+  hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)ws_hist, k,
+                     (int*)ws_cursor);
+  hipLaunchKernelGGL(delta_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
+                     (const int*)labels, (const int*)prev, n, k, (int*)ws_cursor, (int*)ws_perm);
+  // entries <= 2n; the kernel bounds itself with the scanned total
+  const int range = seg_range();
+  const unsigned grid = (unsigned)((2 * n + range - 1) / range);
+  hipLaunchKernelGGL(delta_segment_kernel, dim3(grid), dim3(512), 0, st, (const float*)X,
+                     (const int*)ws_perm, (const int*)labels, (const int*)prev, d, range,
+                     ldexpf(1.0f, -xexp), ldexp(1.0, -qexp), (double*)sums, (double*)counts,
+                     (double*)qsum, (const int*)ws_cursor + (k - 1));
+  return (int)hipGetLastError();
+}
+
+// part[c] = Q_c - 2 c.S_c + n_c |c|^2 (fp64) for the centroids C the labels
+// were assigned with; sums / qsum in their fixed-point units 2^xexp / 2^qexp.
+int sq_cluster_inertia(const void* sums, const void* counts, const void* qsum, const void* C,
+                       int k, int d, int xexp, int qexp, void* part, void* stream) {
+  if (k <= 0) return 0;
+  hipLaunchKernelGGL(cluster_inertia_kernel, dim3((unsigned)((k + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const double*)sums, (const double*)counts,
+                     (const double*)qsum, (const float*)C, k, d, ldexp(1.0, xexp),
+                     ldexp(1.0, qexp), (double*)part);
   return (int)hipGetLastError();
 }
 

@@ -35,6 +35,11 @@ __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, cons
                                        void*, void*, long long, int, int, int, int, double, int,
                                        unsigned, unsigned, unsigned, unsigned, unsigned, unsigned,
                                        unsigned, unsigned, long long, void*);
+__attribute__((weak)) int sq_centroid_delta(const void*, const void*, const void*, void*, void*,
+                                            void*, long long, int, int, int, int, void*, void*,
+                                            void*, void*);
+__attribute__((weak)) int sq_cluster_inertia(const void*, const void*, const void*, const void*,
+                                             int, int, int, int, void*, void*);
 // pairwise_fast.hip
 __attribute__((weak)) int sq_pairwise_reduce(const void*, const void*, void*, int, int, int, int,
                                              double, int, void*);
@@ -78,7 +83,7 @@ __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C
                          void* stream);
 __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, const void*,
                                        const void*, const void*, void*, void*, void*, void*, void*,
-                                       void*, void*, void*, int,
+                                       void*, void*, void*, void*, int,
                                        long long, int, int, int, int, double, double, unsigned,
                                        unsigned, unsigned, unsigned, long long, void*);
 __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
@@ -205,6 +210,24 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
                               level, P(st)));
 }
 
+static PyObject* py_centroid_delta(PyObject*, PyObject* a) {
+  unsigned long long X, lab, prev, sums, cnts, q, h, c, pm, st; long long n; int d, k, xe, qe;
+  if (!PyArg_ParseTuple(a, "KKKKKKLiiiiKKKK", &X, &lab, &prev, &sums, &cnts, &q, &n, &d, &k, &xe,
+                        &qe, &h, &c, &pm, &st))
+    return nullptr;
+  CHECK(sq_centroid_delta)
+  return ret(sq_centroid_delta(P(X), P(lab), P(prev), P(sums), P(cnts), P(q), n, d, k, xe, qe,
+                               P(h), P(c), P(pm), P(st)));
+}
+
+static PyObject* py_cluster_inertia(PyObject*, PyObject* a) {
+  unsigned long long sums, cnts, q, C, part, st; int k, d, xe, qe;
+  if (!PyArg_ParseTuple(a, "KKKKiiiiKK", &sums, &cnts, &q, &C, &k, &d, &xe, &qe, &part, &st))
+    return nullptr;
+  CHECK(sq_cluster_inertia)
+  return ret(sq_cluster_inertia(P(sums), P(cnts), P(q), P(C), k, d, xe, qe, P(part), P(st)));
+}
+
 static PyObject* py_gram64(PyObject*, PyObject* a) {
   unsigned long long X, mu, part, st; int f64, d, grid; long long ldx, n;
   if (!PyArg_ParseTuple(a, "KiLKLiKiK", &X, &f64, &ldx, &mu, &n, &d, &part, &grid, &st))
@@ -303,16 +326,16 @@ static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_estep_x64(PyObject*, PyObject* a) {
-  unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, cnt, part, st;
+  unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, corr, cnt, part, st;
   int pcap, d, dp, k, kp; long long n, roff; double alpha, delta; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2, &lab,
-                        &mind, &dr, &ovr, &mr, &mc, &cnt, &part, &pcap, &n, &d, &dp, &k, &kp,
-                        &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st))
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2, &lab,
+                        &mind, &dr, &ovr, &mr, &mc, &corr, &cnt, &part, &pcap, &n, &d, &dp, &k,
+                        &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st))
     return nullptr;
   CHECK(sq_estep_x64)
   return ret(sq_estep_x64(P(Xh), P(X), P(C), P(Cm), P(xn), P(cm2), P(lab), P(mind), P(dr), P(ovr),
-                          P(mr), P(mc), P(cnt), P(part), pcap, n, d, dp, k, kp, alpha, delta, k0,
-                          k1, s0, s1, roff, P(st)));
+                          P(mr), P(mc), P(corr), P(cnt), P(part), pcap, n, d, dp, k, kp, alpha,
+                          delta, k0, k1, s0, s1, roff, P(st)));
 }
 
 static PyObject* py_fill_mind(PyObject*, PyObject* a) {
@@ -452,6 +475,8 @@ static PyMethodDef methods[] = {
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
     {"gram64", py_gram64, METH_VARARGS, "fp64 MFMA Gram partials"},
+    {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
+    {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},

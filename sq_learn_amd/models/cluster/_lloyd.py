@@ -29,6 +29,7 @@ the generic path: library GEMM distance tiles + selection kernels/torch.
 """
 
 import math
+import os
 
 import torch
 
@@ -146,6 +147,22 @@ class LloydEngine:
         self.Xh16 = (Xf * self.alpha).to(torch.float16) if self.certified else None
         self._prepare_reduce()
         self.mind_part = torch.zeros(512, dtype=torch.float64, device=dev)
+        # incremental M-step (certified path, unweighted, no failure
+        # injection): only the rows whose label moved are re-read; the
+        # inertia comes from the per-cluster statistics + the E-step's
+        # min-vs-label corrections.  SQ_MSTEP_INCREMENTAL=0 disables it.
+        self.incremental = (self.certified and self.sample_weight is None
+                            and self.failure_prob == 0.0
+                            and os.environ.get("SQ_MSTEP_INCREMENTAL", "1") != "0")
+        if self.incremental:
+            self.prev_labels = torch.full((self.n,), -1, dtype=torch.int32, device=dev)
+            self.qsum = torch.zeros(self.k, dtype=torch.float64, device=dev)
+            self.perm2 = torch.empty(max(2 * self.n, 1), dtype=torch.int32, device=dev)
+            self.inertia_part = torch.zeros(self.k, dtype=torch.float64, device=dev)
+            self.buf.corr = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
+            nr = int(self._nrows_global)
+            self.qexp = K.fixed_point_exp(self._max_abs ** 2 * self.dm, nr)
+        self.inc_valid = False
 
     def _prepare_reduce(self):
         dev = self.device
@@ -159,6 +176,7 @@ class LloydEngine:
         self.comm.all_reduce_(mx, op="max")
         self.comm.all_reduce_(nrows)
         mxl = mx.tolist()
+        self._max_abs, self._nrows_global = mxl[0], nrows.item()
         self.rws = K.ReduceWorkspace(self.n, self.k, dev).set_scale(
             mxl[0], int(nrows.item()), mxl[1] if self.sample_weight is not None else None)
         self.sums = torch.zeros((self.k, self.dm), dtype=torch.float64, device=dev)
@@ -189,6 +207,7 @@ class LloydEngine:
     # ---------------------------------------------------------- state
     def set_centers(self, C):
         C = C.to(self.device)
+        self.inc_valid = False   # the incremental M-step restarts from scratch
         if self.fast:
             self.C.copy_(C.to(torch.float32))
             if self.C_op is not None:
@@ -216,6 +235,7 @@ class LloydEngine:
         return {"C_bf16": self.C_bf16, "cn": self.cn}
 
     def restore_tensors(self, d):
+        self.inc_valid = False
         if self.fast and self.C_op is not None and "C_op" in d:
             self.C_op.copy_(d["C_op"].to(self.device))
         elif self.fast and self.C_op is None and "C_bf16" in d:
@@ -332,6 +352,8 @@ class LloydEngine:
         ``events`` (two CUDA events, optional) are recorded after the
         segmented reduce and after the all-reduce (phase timing)."""
         noise_key = self._key("trunc_normal")
+        if self.fast and getattr(self, "incremental", False) and self.buf.corr is not None:
+            return self._mstep_incremental(labels, inertia, noise_key, events)
         if self.fast:
             with tracing.range("mstep"):
                 exact = self.C_op is not None and self.certified
@@ -413,6 +435,50 @@ class LloydEngine:
         shift = ((self.C.double() - old.double()) ** 2).sum()
         return torch.stack([tot_inertia, shift, torch.zeros((), dtype=torch.float64,
                                                             device=self.device)])
+
+    def _mstep_incremental(self, labels, inertia, noise_key, events):
+        """Incremental fixed-point M-step (``centroid_delta_native``): the
+        cluster sums / counts / squared-norm sums are updated by the rows
+        whose label moved; the iteration's inertia is
+        sum_c (Q_c - 2 c.S_c + n_c |c|^2) at the E-step's centroids plus the
+        E-step's per-row (min - label distance) corrections - the reference's
+        sum of minimum distances (``_dmeans.py:774-777``)."""
+        with tracing.range("mstep_incremental"):
+            if not self.inc_valid:
+                self.sums.zero_()
+                self.counts.zero_()
+                self.qsum.zero_()
+                self.prev_labels.fill_(-1)
+            K.centroid_delta_native(self.Xm, labels, self.prev_labels, self.sums, self.counts,
+                                    self.qsum, self.k, self.rws, self.perm2, self.qexp)
+            self.prev_labels.copy_(labels[:self.n])
+            self.inc_valid = True
+            Cold = self.C if self.dm == self.d else self._padded_centers()
+            K.cluster_inertia_native(self.sums, self.counts, self.qsum, Cold, self.k, self.dm,
+                                     self.rws, self.qexp, self.inertia_part)
+            K.sum_f32_native(self.buf.corr, self.n, self.mind_part, inertia)
+            inertia.add_(self.inertia_part.sum())
+            sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
+            K.pack_stats_native(sums, self.counts, inertia, self.packed, self.k, self.d,
+                                self.rws, weighted=False)
+        if events is not None:
+            events[0].record()
+        with tracing.range("allreduce"):
+            self.comm.all_reduce_(self.packed)
+        if events is not None:
+            events[1].record()
+        with tracing.range("finalize"):
+            K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
+                                       self.shift, self.k, self.d, self._noise_bound(),
+                                       noise_key, self.empty_policy,
+                                       shift_part=self.shift_part, scalars=self.scalars,
+                                       buf=self.buf, C_f16=self.C_op, alpha=self.alpha,
+                                       k_pad=self.k_pad, cmax2=self.cmax2)
+            self.C, self.C_new = self.C_new, self.C
+            if self.intermediate_error and self.true_tomography and self.delta > 0:
+                self._true_tomography_centers()
+                self.scalars[1:2].copy_(((self.C.double() - self.C_new.double()) ** 2).sum())
+        return self.scalars
 
     def _padded_centers(self):
         if getattr(self, "_Cpad", None) is None:

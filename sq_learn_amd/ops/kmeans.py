@@ -181,6 +181,10 @@ class EStepBuffers:
         self.dense_rows = None   # allocated by the certified E-step on first use
         self.multi_rows = None   # certified E-step: rows sent to the fp64 re-check kernel
         self.multi_cand = None   # ... and their candidate lists [n][1 + 16]
+        # per-row (min distance - distance to the label) of the rows whose
+        # label is not their argmin (fp64 re-check / dense / overflow rows):
+        # the incremental M-step's inertia correction; None = not produced
+        self.corr = None
         # True while ovf_count is known to be zero (fresh, or reset on the
         # device by the iteration-scalars launch): the E-step skips its memset
         self.ovf_clean = True
@@ -325,6 +329,34 @@ def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorksp
                                  ws.wexp if weights is not None else 0, ws.hist.data_ptr(),
                                  ws.cursor.data_ptr(), ws.perm.data_ptr(), nat.ptr(mind),
                                  nat.ptr(C_old), nat.stream_handle(X.device))
+
+
+def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWorkspace, perm2,
+                          qexp):
+    """Incremental fixed-point cluster statistics (csrc/kmeans.hip
+    delta_segment_kernel): sums / counts / qsum are UPDATED by the rows whose
+    label differs from ``prev`` (prev = -1: the row enters).  Bit-identical
+    to recomputing them from scratch (exact integer arithmetic in fp64)."""
+    n, d = X.shape
+    assert X.dtype == torch.float32 and X.is_contiguous() and d % 4 == 0 and d <= 256
+    assert labels.dtype == torch.int32 and prev.dtype == torch.int32 and perm2.numel() >= 2 * n
+    assert sums.dtype == torch.float64 and sums.numel() >= k * d and qsum.numel() >= k
+    rc = nat.native().centroid_delta(X.data_ptr(), labels.data_ptr(), prev.data_ptr(),
+                                     sums.data_ptr(), counts.data_ptr(), qsum.data_ptr(), n, d, k,
+                                     ws.xexp, int(qexp), ws.hist.data_ptr(), ws.cursor.data_ptr(),
+                                     perm2.data_ptr(), nat.stream_handle(X.device))
+    if rc:
+        raise RuntimeError(f"centroid_delta failed (hip error {rc})")
+
+
+def cluster_inertia_native(sums, counts, qsum, C, k, d, ws: ReduceWorkspace, qexp, part):
+    """part[c] = Q_c - 2 c.S_c + n_c |c|^2 at the centroids C (fp32 [k][d])."""
+    assert C.dtype == torch.float32 and C.is_contiguous() and tuple(C.shape) == (k, d)
+    rc = nat.native().cluster_inertia(sums.data_ptr(), counts.data_ptr(), qsum.data_ptr(),
+                                      C.data_ptr(), k, d, ws.xexp, int(qexp), part.data_ptr(),
+                                      nat.stream_handle(C.device))
+    if rc:
+        raise RuntimeError(f"cluster_inertia failed (hip error {rc})")
 
 
 def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, weighted=False):
@@ -543,6 +575,7 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
                            xn.data_ptr(), cmax2.data_ptr(), buf.labels.data_ptr(),
                            buf.mind.data_ptr(), buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
                            buf.multi_rows.data_ptr(), buf.multi_cand.data_ptr(),
+                           0 if buf.corr is None else buf.corr.data_ptr(),
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)

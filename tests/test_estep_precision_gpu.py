@@ -215,10 +215,15 @@ def test_certified_estep_is_fp64_exact(delta, monkeypatch):
     assert abs(float(inertia) - float(mn64.sum())) <= 1e-6 * float(mn64.sum())
 
 
-def test_certified_step_fills_mind_in_the_mstep(monkeypatch):
-    """One Lloyd step: the segmented reduce computes the marked rows' exact
-    distances; the iteration inertia is the fp64 sum of min distances."""
+@pytest.mark.parametrize("incremental", ["0", "1"])
+def test_certified_step_fills_mind_in_the_mstep(monkeypatch, incremental):
+    """One Lloyd step.  Full reduce: the segmented reduce computes the marked
+    rows' exact distances.  Incremental M-step: the marked rows keep the -1
+    marker and the inertia comes from the per-cluster statistics plus the
+    E-step's corrections.  Either way the iteration inertia is the fp64 sum
+    of min distances."""
     monkeypatch.setenv("SQ_ESTEP_FILTER", "1")
+    monkeypatch.setenv("SQ_MSTEP_INCREMENTAL", incremental)
     n, d, k = 20000, 256, 512
     X, C = _blobs(n, d, k, seed=4)
     Xt = torch.from_numpy(X).cuda()
@@ -228,5 +233,8 @@ def test_certified_step_fills_mind_in_the_mstep(monkeypatch):
     lab, sc = eng.step()
     torch.cuda.synchronize()
     D, lab64, mn64 = _fp64_rule(X, C, 0.5, key, eng.k_pad)
-    assert bool((eng.buf.mind[:n] >= 0).all())
-    assert abs(float(sc[0]) - float(mn64.sum())) <= 1e-6 * float(mn64.sum())
+    assert eng.incremental == (incremental == "1")
+    if incremental == "0":
+        assert bool((eng.buf.mind[:n] >= 0).all())
+    tol = 1e-9 if incremental == "1" else 1e-6   # full path: sum of fp32-stored distances
+    assert abs(float(sc[0]) - float(mn64.sum())) <= tol * float(mn64.sum())
