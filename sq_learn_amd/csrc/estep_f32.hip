@@ -450,7 +450,8 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ dense_rows,
     int* __restrict__ dense_count, long long* __restrict__ mrows, int* __restrict__ mcand,
     int* __restrict__ multi_count, long long n, int k_pad, float alpha, float delta_s,
-    RngKey key, long long row_offset, int dense_cap, int qbits) {
+    RngKey key, long long row_offset, int dense_cap, int qbits, const long long* __restrict__ rlist,
+    const int* __restrict__ rcount, float* __restrict__ ub, float* __restrict__ lb) {
   constexpr int NW = kX64Waves;
   constexpr int DX = KSD * 16;
   constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
@@ -470,7 +471,14 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
   const int r32 = lane & 31;
   const int half = lane >> 5;
   const int n_tiles = k_pad / kTileN;
-  const long long nblk = (n + ROWS - 1) / ROWS;
+  // list mode (rlist != null): the rows to process are rlist[0 .. *rcount)
+  // (the rows the Hamerly bounds could not prune); positions map to rows
+  const long long ne = rlist ? min((long long)*rcount, n) : n;
+  auto row_at = [&](long long pos) -> long long {
+    const long long q = pos < ne ? pos : ne - 1;
+    return rlist ? rlist[q] : q;
+  };
+  const long long nblk = (ne + ROWS - 1) / ROWS;
   long long blk = blockIdx.x;
   if (blk >= nblk) return;
   int* cand = cand_all + wave * 32 * kMaxCand;
@@ -499,8 +507,8 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 
   f16x8 ah[KSD];
   auto load_a = [&](long long b) {
-    const long long r = b * ROWS + wave * 32 + r32;
-    const _Float16* xr = Xh + (size_t)(r < n ? r : n - 1) * DX + half * 8;
+    const long long r = row_at(b * ROWS + wave * 32 + r32);
+    const _Float16* xr = Xh + (size_t)r * DX + half * 8;
 #pragma unroll
     for (int ks = 0; ks < KSD; ++ks) ah[ks] = *reinterpret_cast<const f16x8*>(xr + ks * 16);
   };
@@ -614,28 +622,47 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 
     // ---- row minimum (packed) by the transposed reduce-scatter: lane r32
     // even ends with the min of row irow = r32 >> 1 of its half
-    float R[16];
+    float R[16], R2[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) R[i] = m1[i];
+    for (int i = 0; i < 16; ++i) { R[i] = m1[i]; R2[i] = m2[i]; }
+    // (min, 2nd) pairs merge as (min(a1, b1), min(max(a1, b1), min(a2, b2)))
 #pragma unroll
     for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
       const bool hi = (r32 & o) != 0;
 #pragma unroll
       for (int j = 0; j < c; ++j) {
-        const float ra = R[j], rb = R[c + j];
+        const float ra = R[j], rb = R[c + j], ra2 = R2[j], rb2 = R2[c + j];
         const float keepv = hi ? rb : ra, sendv = hi ? ra : rb;
-        R[j] = vmin(keepv, __shfl_xor(sendv, o, 64));
+        const float keep2 = hi ? rb2 : ra2, send2 = hi ? ra2 : rb2;
+        const float o1 = __shfl_xor(sendv, o, 64), o2 = __shfl_xor(send2, o, 64);
+        R[j] = vmin(keepv, o1);
+        R2[j] = vmin(fmaxf(keepv, o1), vmin(keep2, o2));
       }
     }
-    const float rmin = vmin(R[0], __shfl_xor(R[0], 1, 64));
+    const float q1 = __shfl_xor(R[0], 1, 64), q2 = __shfl_xor(R2[0], 1, 64);
+    const float rmin = vmin(R[0], q1);
+    const float rsec = vmin(fmaxf(R[0], q1), vmin(R2[0], q2));
     const int irow = r32 >> 1;
     const int rl_own = (irow & 3) + 8 * (irow >> 2) + 4 * half;
-    const long long g_own = row0 + rl_own;
-    const float xsv = alpha * sqrtf(xn[g_own < n ? g_own : n - 1]) * (1.0f + 0x1p-16f);
+    const long long g_own = row_at(row0 + rl_own);
+    const float xn_own = xn[g_own];
+    const float xsv = alpha * sqrtf(xn_own) * (1.0f + 0x1p-16f);
     const float prod = xsv * Ch;
     const float mag = 0.25f * Ch * Ch + prod;
     const float E = 1.0625f * 0x1p-10f * prod + pack_rel * mag + sub_rel * (xsv + Ch);
     const float T_own = __uint_as_float(__float_as_uint(rmin) & keep) + delta_s + 2.0f * E;
+    // Hamerly bounds of this row (distances, not squared): ub >= |x - c_min|,
+    // lb <= distance to every other centroid (the 2nd smallest filter value
+    // minus the bound), from D = |x|^2 + D'/alpha^2 with an fp32 margin
+    float ub_own = 0.f, lb_own = 0.f;
+    if (ub) {
+      const float ia2 = 1.0f / (alpha * alpha);
+      const float d1 = (__uint_as_float(__float_as_uint(rmin) & keep) + E) * ia2;
+      const float d2 = (__uint_as_float(__float_as_uint(rsec) & keep) - E) * ia2;
+      const float marg = 0x1p-20f * (xn_own + fabsf(d1) + fabsf(d2));
+      ub_own = sqrtf(fmaxf(xn_own + d1 + marg, 0.f)) * (1.0f + 0x1p-20f);
+      lb_own = sqrtf(fmaxf(xn_own + d2 - marg, 0.f)) * (1.0f - 0x1p-20f);
+    }
 
     // ---- candidates -> LDS list of their row (C/D layout: register i of this
     // lane is row (i & 3) + 8 (i >> 2) + 4 half, column class r32)
@@ -661,8 +688,17 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     __builtin_amdgcn_wave_barrier();
 
     // ---- classify the wave's 32 rows (lane r32 < 32 owns row r32)
-    const long long g = row0 + r32;
-    const bool valid = g < n;
+    const bool valid = row0 + r32 < ne;
+    const long long g = row_at(row0 + r32);
+    // bounds of row r32 live on lane 2 * rl_inv(r32) of its half
+    if (ub) {
+      const int src = ((r32 & 3) + 4 * ((r32 >> 3) & 3)) * 2 + 32 * ((r32 >> 2) & 1);
+      const float u = __shfl(ub_own, src, 64), l = __shfl(lb_own, src, 64);
+      if (valid && half == 0) {
+        ub[g] = u;
+        lb[g] = cnt[r32] == 1 ? l : 0.0f;   // several candidates: always re-evaluate
+      }
+    }
     const int c_r = cnt[r32];
     const bool dense = c_r > kMaxCand;
     const bool multi = valid && !dense && c_r >= 2;
@@ -702,6 +738,56 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     __builtin_amdgcn_wave_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Hamerly pruning of the certified E-step (exact: the pruned rows provably
+// keep a one-member delta-band, i.e. label = argmin, under the new
+// centroids).  After a centroid update with per-centroid shifts s_j =
+// |c_j' - c_j| (fp64): ub_i += s_{label_i}, lb_i -= max_j s_j; the row is
+// pruned when lb_i > 0 and lb_i^2 - ub_i^2 > delta (every other centroid is
+// more than delta beyond the label's squared distance), otherwise it goes to
+// the list the x64 kernel processes.  No host sync: the count stays on the
+// device.
+__global__ void __launch_bounds__(256) bounds_filter_kernel(
+    const int* __restrict__ labels, float* __restrict__ ub, float* __restrict__ lb,
+    const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
+    long long* __restrict__ rlist, int* __restrict__ rcount) {
+  const int lane = threadIdx.x & 63;
+  const double sm = *smax;
+  for (long long base = (long long)blockIdx.x * 256; base < n; base += (long long)gridDim.x * 256) {
+    const long long i = base + threadIdx.x;
+    bool act = false;
+    if (i < n) {
+      const int l = labels[i];
+      const double u = (double)ub[i] + (l >= 0 ? shift[l] : 1e300);
+      const double w = (double)lb[i] - sm;
+      act = !(l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30);
+      if (!act) {
+        ub[i] = (float)u * (1.0f + 0x1p-22f);
+        lb[i] = (float)w * (1.0f - 0x1p-22f);
+      }
+    }
+    const unsigned long long m = __ballot(act);
+    int b0 = 0;
+    if (lane == 0 && m) b0 = atomicAdd(rcount, __popcll(m));
+    b0 = __shfl(b0, 0, 64);
+    if (act) rlist[b0 + __popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+}
+
+extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const void* shift,
+                                const void* smax, long long n, double delta, void* rlist,
+                                void* rcount, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  hipMemsetAsync(rcount, 0, sizeof(int), st);
+  const long long blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)),
+                     dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
+                     (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
+                     (int*)rcount);
+  return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -970,7 +1056,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             void* dense_rows, void* dense_count, void* mrows, void* mcand,
                             void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
-                            int dense_cap, hipStream_t st) {
+                            int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
+                            void* ub, void* lb) {
   constexpr int NW = kX64Waves;
   const size_t lds = kX64Ring * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4;
   auto kern = estep_x64_kernel<KSD>;
@@ -990,12 +1077,14 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   int qbits = 1;
   while ((1 << qbits) < 2 * (k_pad / kTileN)) ++qbits;
   const long long nblk = (n + NW * 32 - 1) / (NW * 32);
-  const unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
+  // list mode: the row count is on the device - every resident slot launches
+  const unsigned grid = (unsigned)(nblk < resident && !rlist ? nblk : resident);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const _Float16*)Xh,
                      (const float*)X, (const _Float16*)C, (const float*)Cm, (const float*)xn,
                      (const float*)cmax2, (int*)labels, (float*)mind, (long long*)dense_rows,
                      (int*)dense_count, (long long*)mrows, (int*)mcand, (int*)multi_count, n,
-                     k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits);
+                     k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits,
+                     (const long long*)rlist, (const int*)rcount, (float*)ub, (float*)lb);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   // the re-check: one pass over the multi list (count read on the device)
@@ -1052,8 +1141,9 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 // [k][d_pad] (zero-padded like X); C: the fp16-split operand.
 int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
                  const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
-                 void* mrows, void* mcand, void* corr, void* counts, void* part, int part_cap,
-                 long long n, int d, int d_pad, int k,
+                 void* mrows, void* mcand, void* corr, void* rlist, void* rcount, void* ub,
+                 void* lb, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
+                 int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
@@ -1073,8 +1163,7 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   case KSD * 16:                                                                                 \
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
-                               row_offset,                                                       \
-                               (int)min(n, 2147483647LL), st);                                   \
+                               row_offset, (int)min(n, 2147483647LL), st, rlist, rcount, ub, lb); \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \

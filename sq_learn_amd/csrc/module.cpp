@@ -27,6 +27,8 @@ __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int,
 __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, long long,
                                            long long, const void*, void*, long long, unsigned,
                                            unsigned, unsigned, unsigned, const void*, int, void*);
+__attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
+                                           long long, double, void*, void*, void*);
 // gram64.hip
 __attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, long long, int, void*,
                                     int, void*);
@@ -83,7 +85,7 @@ __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C
                          void* stream);
 __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, const void*,
                                        const void*, const void*, void*, void*, void*, void*, void*,
-                                       void*, void*, void*, void*, int,
+                                       void*, void*, void*, void*, void*, void*, void*, void*, int,
                                        long long, int, int, int, int, double, double, unsigned,
                                        unsigned, unsigned, unsigned, long long, void*);
 __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
@@ -210,6 +212,14 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
                               level, P(st)));
 }
 
+static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
+  unsigned long long lab, ub, lb, sh, sm, rl, rc, st; long long n; double delta;
+  if (!PyArg_ParseTuple(a, "KKKKKLdKKK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc, &st))
+    return nullptr;
+  CHECK(sq_bounds_filter)
+  return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(st)));
+}
+
 static PyObject* py_centroid_delta(PyObject*, PyObject* a) {
   unsigned long long X, lab, prev, sums, cnts, q, h, c, pm, st; long long n; int d, k, xe, qe;
   if (!PyArg_ParseTuple(a, "KKKKKKLiiiiKKKK", &X, &lab, &prev, &sums, &cnts, &q, &n, &d, &k, &xe,
@@ -326,16 +336,17 @@ static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_estep_x64(PyObject*, PyObject* a) {
-  unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, corr, cnt, part, st;
+  unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, corr, rl, rc, ub, lb, cnt,
+      part, st;
   int pcap, d, dp, k, kp; long long n, roff; double alpha, delta; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2, &lab,
-                        &mind, &dr, &ovr, &mr, &mc, &corr, &cnt, &part, &pcap, &n, &d, &dp, &k,
-                        &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st))
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2, &lab,
+                        &mind, &dr, &ovr, &mr, &mc, &corr, &rl, &rc, &ub, &lb, &cnt, &part, &pcap,
+                        &n, &d, &dp, &k, &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st))
     return nullptr;
   CHECK(sq_estep_x64)
   return ret(sq_estep_x64(P(Xh), P(X), P(C), P(Cm), P(xn), P(cm2), P(lab), P(mind), P(dr), P(ovr),
-                          P(mr), P(mc), P(corr), P(cnt), P(part), pcap, n, d, dp, k, kp, alpha,
-                          delta, k0, k1, s0, s1, roff, P(st)));
+                          P(mr), P(mc), P(corr), P(rl), P(rc), P(ub), P(lb), P(cnt), P(part), pcap,
+                          n, d, dp, k, kp, alpha, delta, k0, k1, s0, s1, roff, P(st)));
 }
 
 static PyObject* py_fill_mind(PyObject*, PyObject* a) {
@@ -475,6 +486,7 @@ static PyMethodDef methods[] = {
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
     {"gram64", py_gram64, METH_VARARGS, "fp64 MFMA Gram partials"},
+    {"bounds_filter", py_bounds_filter, METH_VARARGS, "Hamerly pruning -> active row list"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},

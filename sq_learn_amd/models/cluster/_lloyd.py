@@ -163,6 +163,18 @@ class LloydEngine:
             nr = int(self._nrows_global)
             self.qexp = K.fixed_point_exp(self._max_abs ** 2 * self.dm, nr)
         self.inc_valid = False
+        # Hamerly pruning of the certified E-step (exact: pruned rows keep a
+        # one-member band); SQ_ESTEP_BOUNDS=0 disables it
+        self.bounds = (self.certified and self.failure_prob == 0.0
+                       and os.environ.get("SQ_ESTEP_BOUNDS", "1") != "0")
+        if self.bounds:
+            self.ub = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
+            self.lb = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
+            self.rlist = torch.empty(max(self.n, 1), dtype=torch.int64, device=dev)
+            self.rcount = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.shift_s = torch.zeros(self.k, dtype=torch.float64, device=dev)
+            self.smax = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.bounds_valid = False
 
     def _prepare_reduce(self):
         dev = self.device
@@ -208,6 +220,7 @@ class LloydEngine:
     def set_centers(self, C):
         C = C.to(self.device)
         self.inc_valid = False   # the incremental M-step restarts from scratch
+        self.bounds_valid = False
         if self.fast:
             self.C.copy_(C.to(torch.float32))
             if self.C_op is not None:
@@ -236,6 +249,7 @@ class LloydEngine:
 
     def restore_tensors(self, d):
         self.inc_valid = False
+        self.bounds_valid = False
         if self.fast and self.C_op is not None and "C_op" in d:
             self.C_op.copy_(d["C_op"].to(self.device))
         elif self.fast and self.C_op is None and "C_bf16" in d:
@@ -248,20 +262,28 @@ class LloydEngine:
         returns (labels, mind, local_inertia_tensor)."""
         if C is not None:
             self.set_centers(C)
-        lab, mind, inertia = self._estep(self._key("band_select"))
+        lab, mind, inertia = self._estep(self._key("band_select"), full=True)
         if self.fast and self.C_op is not None and self.certified:
             # single-candidate rows: their min distance is |x - c_label|^2
             K.fill_mind_native(self.Xf32, self.C, lab, mind)
             K.sum_f32_native(mind, self.n, self.mind_part, self.buf.inertia)
         return lab, mind, inertia
 
-    def _estep(self, key):
+    def _estep(self, key, full=False):
         if self.fast and self.C_op is not None and self.certified:
             with tracing.range("estep_x64"):
                 Cp = self.C if self.d == self.d_pad else self._padded_centers()
+                rows = None
+                if self.bounds and self.bounds_valid and not full:
+                    K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
+                                           self.shift_s, self.smax, self.delta, self.rlist,
+                                           self.rcount)
+                    rows = (self.rlist, self.rcount)
                 lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
                                                self.cmax2, self.k, self.delta, self.alpha, key,
-                                               self.row_offset, self.buf)
+                                               self.row_offset, self.buf,
+                                               bounds=(self.ub, self.lb) if self.bounds else None,
+                                               rows=rows)
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):
@@ -478,6 +500,16 @@ class LloydEngine:
             if self.intermediate_error and self.true_tomography and self.delta > 0:
                 self._true_tomography_centers()
                 self.scalars[1:2].copy_(((self.C.double() - self.C_new.double()) ** 2).sum())
+                if self.bounds:
+                    self.shift_part[:self.k].copy_(
+                        ((self.C.double() - self.C_new.double()) ** 2).sum(1))
+            if self.bounds:
+                # per-centroid shifts of this update (fp64, rounded up) for the
+                # next E-step's Hamerly bound update
+                torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
+                self.shift_s.mul_(1.0 + 1e-12)
+                torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
+                self.bounds_valid = True
         return self.scalars
 
     def _padded_centers(self):
@@ -494,7 +526,11 @@ class LloydEngine:
         key = self._key("tomography")
         C = self.C.double()
         est = tomography_rows_torch(C, self.delta / 2.0, key, **self.tomography_kw)
+        # a centroid update, not a restart: the incremental statistics stay
+        # valid (label based) and the bounds move by the recomputed shifts
+        flags = (self.inc_valid, self.bounds_valid)
         self.set_centers(est.to(self.C.dtype))
+        self.inc_valid, self.bounds_valid = flags
 
     # ---------------------------------------------------------- iteration
     def step_phases(self):

@@ -331,6 +331,21 @@ def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorksp
                                  nat.ptr(C_old), nat.stream_handle(X.device))
 
 
+def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount):
+    """Hamerly pruning (csrc/estep_f32.hip bounds_filter_kernel): bounds
+    moved by the centroid shifts; rows that can no longer be proven to keep a
+    one-member band go to ``rlist`` (count in ``rcount``, on the device)."""
+    n = labels.numel()
+    assert ub.dtype == torch.float32 and lb.dtype == torch.float32 and rlist.numel() >= n
+    assert shift.dtype == torch.float64 and smax.dtype == torch.float64
+    rc = nat.native().bounds_filter(labels.data_ptr(), ub.data_ptr(), lb.data_ptr(),
+                                    shift.data_ptr(), smax.data_ptr(), n, float(delta),
+                                    rlist.data_ptr(), rcount.data_ptr(),
+                                    nat.stream_handle(labels.device))
+    if rc:
+        raise RuntimeError(f"bounds_filter failed (hip error {rc})")
+
+
 def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWorkspace, perm2,
                           qexp):
     """Incremental fixed-point cluster statistics (csrc/kmeans.hip
@@ -548,7 +563,10 @@ def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_o
 
 
 def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
-                     buf: EStepBuffers, stream=None):
+                     buf: EStepBuffers, stream=None, bounds=None, rows=None):
+    """``bounds`` = (ub, lb) fp32 [n]: the kernel writes each processed
+    row's Hamerly bounds; ``rows`` = (rlist int64 [n], rcount int32 [1]):
+    process only the listed rows (list mode, count on the device)."""
     """Certified E-step (``estep_x64_kernel``): one fp16 MFMA pass with a
     rigorous error bound, fp64 re-check of the candidate centroids, dense rows
     through the fp32-faithful 3-pass kernel.  Labels are the fp64 delta-band
@@ -576,6 +594,10 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
                            buf.mind.data_ptr(), buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
                            buf.multi_rows.data_ptr(), buf.multi_cand.data_ptr(),
                            0 if buf.corr is None else buf.corr.data_ptr(),
+                           0 if rows is None else rows[0].data_ptr(),
+                           0 if rows is None else rows[1].data_ptr(),
+                           0 if bounds is None else bounds[0].data_ptr(),
+                           0 if bounds is None else bounds[1].data_ptr(),
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)

@@ -52,3 +52,43 @@ def test_incremental_mstep_bit_identical(cuda, delta, d):
     la, sa = inc.step()
     lb, sb = ful.step()
     assert torch.equal(inc.C, ful.C)
+
+
+def _engine_b(X, k, delta, bounds, tomo=False):
+    old = os.environ.get("SQ_ESTEP_BOUNDS")
+    os.environ["SQ_ESTEP_BOUNDS"] = "1" if bounds else "0"
+    try:
+        return LloydEngine(X, k, delta=delta, intermediate_error=delta > 0, true_tomography=tomo,
+                           seed=5, gemm_precision="fp32")
+    finally:
+        if old is None:
+            del os.environ["SQ_ESTEP_BOUNDS"]
+        else:
+            os.environ["SQ_ESTEP_BOUNDS"] = old
+
+
+@pytest.mark.parametrize("delta,tomo", [(0.0, False), (0.5, False), (2.0, True)])
+def test_hamerly_pruning_is_exact(cuda, delta, tomo):
+    """Pruned rows provably keep a one-member band: labels, centroids and
+    inertia BIT-identical to the unpruned certified E-step, and most rows
+    are pruned once the centroids settle."""
+    X, _ = make_blobs(80000, 64, centers=30, cluster_std=1.0, random_state=2)
+    Xt = torch.tensor(X, dtype=torch.float32, device=cuda)
+    k = 32
+    C0 = Xt[torch.as_tensor(np.random.RandomState(3).choice(80000, k, replace=False), device=cuda)]
+    a = _engine_b(Xt, k, delta, True, tomo)
+    b = _engine_b(Xt, k, delta, False, tomo)
+    assert a.bounds and not b.bounds
+    a.set_centers(C0)
+    b.set_centers(C0)
+    active = []
+    for it in range(10):
+        la, sa = a.step()
+        lb, sb = b.step()
+        assert torch.equal(la, lb), f"labels differ at iteration {it}"
+        assert torch.equal(a.C, b.C)
+        assert sa.tolist()[0] == sb.tolist()[0]
+        if it > 0:
+            active.append(int(a.rcount.item()))
+    if not tomo:   # (shot tomography moves every centroid far each step)
+        assert min(active) < 0.5 * 80000, active
