@@ -16,6 +16,7 @@ Behavioural parity with the reference's ``sklearn/base.py``:
 """
 
 import copy
+import functools
 import inspect
 import warnings
 from collections import defaultdict
@@ -61,8 +62,54 @@ def _same_param(a, b):
         return False
 
 
+def _validate_fit_X(est, X):
+    """The reference's ``check_array`` contract at ``fit`` for dense numeric
+    host arrays (``utils/validation.py:477-760``): at least one sample and one
+    feature, no NaN unless the estimator's ``allow_nan`` tag says so, never
+    infinity.  Device tensors / sharded arrays are validated by the device
+    layer (``models/_data.py``), other input kinds by the estimators."""
+    if not isinstance(X, np.ndarray) or X.ndim != 2 or X.dtype.kind not in "fiub":
+        return
+    tags = est._get_tags()
+    if "2darray" not in tags.get("X_types", ["2darray"]):
+        return
+    name = type(est).__name__
+    if X.shape[0] == 0:
+        raise ValueError(f"Found array with 0 sample(s) (shape={X.shape}) while a minimum of 1 "
+                         f"is required by {name}.")
+    if X.shape[1] == 0:
+        raise ValueError(f"Found array with 0 feature(s) (shape={X.shape}) while a minimum of 1 "
+                         f"is required by {name}.")
+    if X.dtype.kind == "f" and not np.isfinite(X).all():
+        if np.isinf(X).any():
+            raise ValueError(f"Input X contains infinity or a value too large for {X.dtype!r}.")
+        if not tags.get("allow_nan", False):
+            raise ValueError(f"Input X contains NaN. {name} does not accept missing values "
+                             "encoded as NaN natively.")
+
+
+def _validating_fit(fit):
+    @functools.wraps(fit)
+    def fit_validated(self, *args, **kwargs):
+        if args:
+            _validate_fit_X(self, args[0])
+        elif "X" in kwargs:
+            _validate_fit_X(self, kwargs["X"])
+        return fit(self, *args, **kwargs)
+    fit_validated._sq_validated = True
+    return fit_validated
+
+
 class BaseEstimator:
     """Base class for all estimators of the framework."""
+
+    def __init_subclass__(cls, **kwargs):
+        # every estimator's fit validates its dense host input like the
+        # reference's check_array (one wrapper per class that defines fit)
+        super().__init_subclass__(**kwargs)
+        fit = cls.__dict__.get("fit")
+        if fit is not None and callable(fit) and not getattr(fit, "_sq_validated", False):
+            cls.fit = _validating_fit(fit)
 
     @classmethod
     def _get_param_names(cls):

@@ -210,12 +210,20 @@ class _PLS(TransformerMixin, RegressorMixin, MultiOutputMixin, BaseEstimator):
 
 
 class PLSRegression(_PLS):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def __init__(self, n_components=2, *, scale=True, max_iter=500, tol=1e-06, copy=True):
         super().__init__(n_components=n_components, scale=scale, deflation_mode="regression",
                          mode="A", algorithm="nipals", max_iter=max_iter, tol=tol, copy=copy)
 
 
 class PLSCanonical(_PLS):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def __init__(self, n_components=2, *, scale=True, algorithm="nipals", max_iter=500, tol=1e-06,
                  copy=True):
         super().__init__(n_components=n_components, scale=scale, deflation_mode="canonical",
@@ -223,6 +231,10 @@ class PLSCanonical(_PLS):
 
 
 class CCA(_PLS):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def __init__(self, n_components=2, *, scale=True, max_iter=500, tol=1e-06, copy=True):
         super().__init__(n_components=n_components, scale=scale, deflation_mode="canonical",
                          mode="B", algorithm="nipals", max_iter=max_iter, tol=tol, copy=copy)
@@ -230,6 +242,10 @@ class CCA(_PLS):
 
 class PLSSVD(TransformerMixin, BaseEstimator):
     """SVD of the cross-covariance X^T Y (on the device)."""
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
 
     def __init__(self, n_components=2, *, scale=True, copy=True):
         self.n_components = n_components

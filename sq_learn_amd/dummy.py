@@ -14,6 +14,10 @@ def _rows(X):
 
 
 class DummyClassifier(ClassifierMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True, "poor_score": True}
+
     def __init__(self, *, strategy="prior", random_state=None, constant=None):
         self.strategy = strategy
         self.random_state = random_state
@@ -112,6 +116,10 @@ class DummyClassifier(ClassifierMixin, BaseEstimator):
 
 
 class DummyRegressor(RegressorMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True, "poor_score": True}
+
     def __init__(self, *, strategy="mean", constant=None, quantile=None):
         self.strategy = strategy
         self.constant = constant

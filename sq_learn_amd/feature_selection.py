@@ -336,6 +336,10 @@ class GenericUnivariateSelect(_BaseFilter):
 
 
 class VarianceThreshold(SelectorMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, threshold=0.0):
         self.threshold = threshold
 

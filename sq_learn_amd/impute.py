@@ -30,6 +30,10 @@ def _arr(X, force_float=True):
 
 
 class MissingIndicator(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, missing_values=np.nan, features="missing-only", sparse="auto",
                  error_on_new=True):
         self.missing_values = missing_values
@@ -63,6 +67,10 @@ class MissingIndicator(TransformerMixin, BaseEstimator):
 
 
 class SimpleImputer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, missing_values=np.nan, strategy="mean", fill_value=None, verbose=0,
                  copy=True, add_indicator=False):
         self.missing_values = missing_values
@@ -157,6 +165,10 @@ def nan_euclidean_distances(X, Y=None, *, squared=False, missing_values=np.nan, 
 
 
 class KNNImputer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, missing_values=np.nan, n_neighbors=5, weights="uniform",
                  metric="nan_euclidean", copy=True, add_indicator=False):
         self.missing_values = missing_values
@@ -217,6 +229,10 @@ class KNNImputer(TransformerMixin, BaseEstimator):
 
 
 class IterativeImputer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, estimator=None, *, missing_values=np.nan, sample_posterior=False,
                  max_iter=10, tol=1e-3, n_nearest_features=None, initial_strategy="mean",
                  imputation_order="ascending", skip_complete=False, min_value=-np.inf,

@@ -66,6 +66,10 @@ class RBFSampler(TransformerMixin, BaseEstimator):
 
 
 class SkewedChi2Sampler(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"requires_positive_X": True}
+
     def __init__(self, *, skewedness=1.0, n_components=100, random_state=None):
         self.skewedness = skewedness
         self.n_components = n_components
@@ -91,6 +95,10 @@ class SkewedChi2Sampler(TransformerMixin, BaseEstimator):
 
 
 class AdditiveChi2Sampler(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"requires_positive_X": True, "stateless": True}
+
     def __init__(self, *, sample_steps=2, sample_interval=None):
         self.sample_steps = sample_steps
         self.sample_interval = sample_interval

@@ -47,7 +47,8 @@ class LloydEngine:
     def __init__(self, X, k, *, delta=0.0, true_distance_estimate=False, intermediate_error=False,
                  true_tomography=False, tomography_kw=None, sample_weight=None, seed=0,
                  comm=None, row_offset=0, gemm_precision="fp32", ipe_Q=13, empty_policy=0,
-                 Xb=None, xn=None, failure_prob=0.0, failure_attempts=1, generic=False):
+                 Xb=None, xn=None, failure_prob=0.0, failure_attempts=1, generic=False,
+                 relocate_empty=False):
         self.X = X
         self.device = X.device
         self.n, self.d = X.shape
@@ -67,6 +68,8 @@ class LloydEngine:
         self.d_pad = K.pad_features(self.d)
         self.restart = 0
         self.it = 0
+        self.relocate_empty = bool(relocate_empty)
+        self.n_relocated = 0
         self.failure_prob = float(failure_prob or 0.0)
         self.failure_attempts = max(1, int(failure_attempts))
         # [estimations made, corrupted rows] over the engine's lifetime (device)
@@ -553,6 +556,57 @@ class LloydEngine:
                 "allreduce": ev[2].elapsed_time(ev[3]), "finalize": ev[3].elapsed_time(ev[4]),
                 "step_wall": wall}
 
+    def _relocate(self, labels):
+        """Empty-cluster relocation of the classical Lloyd step (reference
+        ``cluster/_k_means_fast.pyx:162-200``): each cluster left without rows
+        by the E-step takes one of the rows farthest from their own centre
+        (the row moves: old cluster loses it, the empty one gets it - the
+        reference's sums / weights update, expressed as a relabel).  Row
+        sharded: per-shard top-e distances, one all-gather,
+        the same global pick on every rank, the owner relabels its row."""
+        k = self.k
+        lab = labels[:self.n].long()
+        w = self.sample_weight
+        cnt = torch.zeros(k, dtype=torch.float64, device=self.device)
+        valid = lab >= 0
+        cnt.index_add_(0, lab.clamp(min=0), (w.double() if w is not None else
+                                              torch.ones(self.n, dtype=torch.float64,
+                                                         device=self.device)) * valid)
+        self.comm.all_reduce_(cnt)
+        empty = torch.nonzero(cnt == 0)[:, 0]
+        e = int(empty.numel())
+        if e == 0:
+            return labels
+        C = self.C.double()
+        d = torch.empty(self.n, dtype=torch.float64, device=self.device)
+        X = self.X
+        step = 1 << 19
+        for s0 in range(0, self.n, step):
+            xs = X[s0:s0 + step].double()
+            d[s0:s0 + step] = ((xs - C[lab[s0:s0 + step].clamp(min=0)]) ** 2).sum(1)
+        d = torch.where(valid, d, torch.full_like(d, -1.0))
+        m = min(e, self.n)
+        vals, idx = torch.topk(d, m) if m > 0 else (d[:0], lab[:0])
+        rows = idx + self.row_offset
+        if m < e:   # pad so every rank sends e entries
+            vals = torch.cat([vals, torch.full((e - m,), -2.0, dtype=vals.dtype, device=vals.device)])
+            rows = torch.cat([rows, torch.full((e - m,), -1, dtype=rows.dtype, device=rows.device)])
+        allv = torch.cat(self.comm.all_gather(vals))
+        allr = torch.cat(self.comm.all_gather(rows))
+        # descending distance, ascending row on ties: the same order everywhere
+        order = sorted(range(allv.numel()), key=lambda i: (-float(allv[i]), int(allr[i])))[:e]
+        for j, i in enumerate(order):
+            g = int(allr[i])
+            if g < 0:
+                continue
+            loc = g - self.row_offset
+            if 0 <= loc < self.n:
+                labels[loc] = int(empty[j])
+                if getattr(self, "bounds", False):
+                    self.lb[loc] = 0.0   # label moved: re-evaluate next E-step
+        self.n_relocated += e
+        return labels
+
     def step(self):
         """One Lloyd iteration; returns (labels, scalars_tensor)."""
         labels, mind, inertia = self._estep(self._key("band_select"))
@@ -560,6 +614,8 @@ class LloydEngine:
             # Bernoulli estimation failures (+ resampling)
             failure_inject_(labels, self.k, self.failure_prob, self.failure_attempts,
                             self._key("failure"), self.row_offset, self.failure_counters)
+        if self.relocate_empty:
+            labels = self._relocate(labels)
         sc = self.mstep(labels, inertia)
         self.it += 1
         return labels, sc

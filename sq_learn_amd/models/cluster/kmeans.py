@@ -11,8 +11,9 @@ distances); 'auto' / 'full' / 'lloyd' run the fused MFMA Lloyd engine,
 which on MI355X beats bounds at d >= 64.  The reference's
 'auto' picks Elkan for dense data: the labels agree (both are the exact
 argmin), only the cost differs.
-Empty clusters keep their previous centre (the reference relocates the
-farthest points).
+Empty clusters are relocated to the rows farthest from their centres, like
+the reference (``_k_means_fast.pyx:162-200``; per-shard top-e + one
+all-gather when row-sharded).
 """
 
 import warnings
@@ -106,7 +107,7 @@ class KMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         else:
             eng = LloydEngine(Xc, self.n_clusters, delta=0.0, sample_weight=sw, seed=seed,
                               comm=data.comm, row_offset=data.row_offset,
-                              gemm_precision=self._precision())
+                              gemm_precision=self._precision(), relocate_empty=True)
         best = None
         for r in range(n_init):
             eng.restart, eng.it = r, 0

@@ -126,8 +126,8 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                           f"{self.__class__.__name__} instead of n_init={self._n_init}.",
                           RuntimeWarning, stacklevel=3)
             self._n_init = 1
-        if self.empty_cluster not in ("keep", "zero"):
-            raise ValueError("empty_cluster must be 'keep' or 'zero'")
+        if self.empty_cluster not in ("keep", "zero", "relocate"):
+            raise ValueError("empty_cluster must be 'keep', 'zero' or 'relocate'")
         if not 0.0 <= float(self.failure_prob) < 1.0:
             raise ValueError(f"failure_prob must be in [0, 1), got {self.failure_prob}")
         if self.failure_policy not in ("ignore", "resample"):
@@ -216,7 +216,8 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                              true_tomography=self.true_tomography, tomography_kw=tomo_kw,
                              sample_weight=sw, seed=seed, comm=comm, row_offset=data.row_offset,
                              gemm_precision=self._precision(), ipe_Q=Q,
-                             empty_policy=0 if self.empty_cluster == "keep" else 1,
+                             empty_policy=1 if self.empty_cluster == "zero" else 0,
+                             relocate_empty=self.empty_cluster == "relocate",
                              failure_prob=float(self.failure_prob),
                              failure_attempts=(int(self.failure_max_attempts)
                                                if self.failure_policy == "resample" else 1))

@@ -716,6 +716,10 @@ class NMF(TransformerMixin, BaseEstimator):
     """Non-negative matrix factorisation X ~ W H (coordinate descent or
     multiplicative updates; Frobenius / KL / IS / beta losses)."""
 
+    def _more_tags(self):
+        return {"requires_positive_X": True}
+
+
     def __init__(self, n_components=None, *, init="warn", solver="cd", beta_loss="frobenius",
                  tol=1e-4, max_iter=200, random_state=None, alpha=0.0, l1_ratio=0.0, verbose=0,
                  shuffle=False, regularization="both"):
@@ -839,6 +843,10 @@ def _as_csr(X):
 
 class LatentDirichletAllocation(TransformerMixin, BaseEstimator):
     """Latent Dirichlet allocation with batch or online variational Bayes."""
+
+    def _more_tags(self):
+        return {"requires_positive_X": True}
+
 
     def __init__(self, n_components=10, *, doc_topic_prior=None, topic_word_prior=None,
                  learning_method="batch", learning_decay=0.7, learning_offset=10.0, max_iter=10,

@@ -567,7 +567,8 @@ class GradientBoostingClassifier(ClassifierMixin, BaseGradientBoosting):
         self.n_iter_no_change = n_iter_no_change
         self.tol = tol
         self.ccp_alpha = ccp_alpha
-        self.alpha = 0.9
+
+    alpha = 0.9   # (regression-loss quantile; fixed for the classifier, not a parameter)
 
     def _validate_y(self, y, sample_weight):
         self.classes_, y = np.unique(y, return_inverse=True)

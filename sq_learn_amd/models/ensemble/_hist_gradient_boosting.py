@@ -619,6 +619,10 @@ def _predict_trees(preds, X):
 
 
 class HistGradientBoostingRegressor(RegressorMixin, BaseHistGradientBoosting):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     _VALID_LOSSES = ("squared_error", "least_squares", "absolute_error",
                      "least_absolute_deviation", "poisson")
 
@@ -667,6 +671,10 @@ class HistGradientBoostingRegressor(RegressorMixin, BaseHistGradientBoosting):
 
 
 class HistGradientBoostingClassifier(ClassifierMixin, BaseHistGradientBoosting):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     _VALID_LOSSES = ("binary_crossentropy", "categorical_crossentropy", "log_loss", "auto")
 
     def __init__(self, loss="auto", *, learning_rate=0.1, max_iter=100, max_leaf_nodes=31,

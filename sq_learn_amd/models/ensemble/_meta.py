@@ -329,6 +329,12 @@ def _average_path_length(n):
 
 
 class IsolationForest(OutlierMixin, BaseBagging):
+    # fixed bagging settings of the shared BaseBagging machinery (class
+    # attributes: not constructor parameters)
+    base_estimator = None
+    bootstrap_features = False
+    oob_score = False
+
     """Isolation forest: random-split trees; anomaly score from the mean
     isolation depth."""
 
@@ -344,9 +350,6 @@ class IsolationForest(OutlierMixin, BaseBagging):
         self.random_state = random_state
         self.verbose = verbose
         self.warm_start = warm_start
-        self.base_estimator = None
-        self.bootstrap_features = False
-        self.oob_score = False
 
     def get_params(self, deep=True):
         p = super().get_params(deep)
@@ -866,12 +869,14 @@ class StackingClassifier(ClassifierMixin, _BaseStacking):
 
 
 class StackingRegressor(RegressorMixin, _BaseStacking):
+    stack_method = "predict"   # fixed for regressors (not a parameter)
+
     def __init__(self, estimators, final_estimator=None, *, cv=None, n_jobs=None,
                  passthrough=False, verbose=0):
         self.estimators = estimators
         self.final_estimator = final_estimator
         self.cv = cv
-        self.stack_method = "predict"
+
         self.n_jobs = n_jobs
         self.passthrough = passthrough
         self.verbose = verbose

@@ -76,6 +76,10 @@ def _fit_hyper(est, kernel, lml):
 
 
 class GaussianProcessRegressor(MultiOutputMixin, RegressorMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"requires_fit": False}
+
     def __init__(self, kernel=None, *, alpha=1e-10, optimizer="fmin_l_bfgs_b",
                  n_restarts_optimizer=0, normalize_y=False, copy_X_train=True,
                  random_state=None):

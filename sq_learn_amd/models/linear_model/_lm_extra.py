@@ -268,6 +268,10 @@ class Lars(MultiOutputMixin, RegressorMixin, LinearModel):
 
 
 class LassoLars(Lars):
+
+    def _more_tags(self):
+        return {"poor_score": True}
+
     method = "lasso"
 
     def __init__(self, alpha=1.0, *, fit_intercept=True, verbose=False, normalize="deprecated",
@@ -523,6 +527,10 @@ def orthogonal_mp(X, y, *, n_nonzero_coefs=None, tol=None, precompute=False, cop
 
 
 class OrthogonalMatchingPursuit(MultiOutputMixin, RegressorMixin, LinearModel):
+
+    def _more_tags(self):
+        return {"poor_score": True}
+
     def __init__(self, *, n_nonzero_coefs=None, tol=None, fit_intercept=True,
                  normalize="deprecated", precompute="auto"):
         self.n_nonzero_coefs = n_nonzero_coefs
@@ -920,6 +928,10 @@ class TweedieRegressor(RegressorMixin, BaseEstimator):
     """Generalised linear model with a Tweedie distribution (power p) and
     identity / log link, fitted by L-BFGS on 0.5 * mean deviance + L2."""
 
+    def _more_tags(self):
+        return {"requires_positive_y": True}
+
+
     def __init__(self, *, power=0.0, alpha=1.0, fit_intercept=True, link="auto", max_iter=100,
                  tol=1e-4, warm_start=False, verbose=0):
         self.power = power
@@ -1021,6 +1033,10 @@ class TweedieRegressor(RegressorMixin, BaseEstimator):
 
 
 class PoissonRegressor(TweedieRegressor):
+
+    def _more_tags(self):
+        return {"requires_positive_y": True}
+
     def __init__(self, *, alpha=1.0, fit_intercept=True, max_iter=100, tol=1e-4,
                  warm_start=False, verbose=0):
         super().__init__(power=1.0, alpha=alpha, fit_intercept=fit_intercept, link="log",
@@ -1032,6 +1048,10 @@ class PoissonRegressor(TweedieRegressor):
 
 
 class GammaRegressor(TweedieRegressor):
+
+    def _more_tags(self):
+        return {"requires_positive_y": True}
+
     def __init__(self, *, alpha=1.0, fit_intercept=True, max_iter=100, tol=1e-4,
                  warm_start=False, verbose=0):
         super().__init__(power=2.0, alpha=alpha, fit_intercept=fit_intercept, link="log",
@@ -1045,6 +1065,10 @@ class GammaRegressor(TweedieRegressor):
 # ================================================================= Quantile
 class QuantileRegressor(RegressorMixin, LinearModel):
     """L1-penalised quantile regression as a linear program (HiGHS)."""
+
+    def _more_tags(self):
+        return {"poor_score": True}
+
 
     def __init__(self, *, quantile=0.5, alpha=1.0, fit_intercept=True, solver="highs",
                  solver_options=None):
@@ -1151,6 +1175,10 @@ def _mt_cd(W, l1, l2, X, Y, max_iter, tol, rs, random):
 class MultiTaskElasticNet(RegressorMixin, LinearModel):
     """Elastic net with a shared (L2,1) sparsity pattern across targets."""
 
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
+
     def __init__(self, alpha=1.0, *, l1_ratio=0.5, fit_intercept=True, normalize=False,
                  copy_X=True, max_iter=1000, tol=1e-4, warm_start=False, random_state=None,
                  selection="cyclic"):
@@ -1189,6 +1217,10 @@ class MultiTaskElasticNet(RegressorMixin, LinearModel):
 
 
 class MultiTaskLasso(MultiTaskElasticNet):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def __init__(self, alpha=1.0, *, fit_intercept=True, normalize=False, copy_X=True,
                  max_iter=1000, tol=1e-4, warm_start=False, random_state=None,
                  selection="cyclic"):
@@ -1249,6 +1281,10 @@ class _MultiTaskCV(RegressorMixin, LinearModel):
 
 
 class MultiTaskElasticNetCV(_MultiTaskCV):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def __init__(self, *, l1_ratio=0.5, eps=1e-3, n_alphas=100, alphas=None, fit_intercept=True,
                  normalize=False, max_iter=1000, tol=1e-4, cv=None, copy_X=True, verbose=0,
                  n_jobs=None, random_state=None, selection="cyclic"):
@@ -1272,6 +1308,10 @@ class MultiTaskElasticNetCV(_MultiTaskCV):
 
 
 class MultiTaskLassoCV(_MultiTaskCV):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def __init__(self, *, eps=1e-3, n_alphas=100, alphas=None, fit_intercept=True,
                  normalize=False, max_iter=1000, tol=1e-4, copy_X=True, cv=None, verbose=False,
                  n_jobs=None, random_state=None, selection="cyclic"):

@@ -84,6 +84,10 @@ class _KernelMixin:
 class LSSVC(_KernelMixin, ClassifierMixin, BaseEstimator):
     """Classical least-squares SVM classifier (labels in {-1, +1})."""
 
+    def _more_tags(self):
+        return {"binary_only": True}
+
+
     def __init__(self, kernel="linear", penalty=0.1, degree=3, gamma="scale", coef0=0.0,
                  verbose=False, algorithm="classic", device=None, cg_tol=1e-10, cg_maxiter=1000):
         self.kernel = kernel
@@ -135,6 +139,7 @@ class LSSVC(_KernelMixin, ClassifierMixin, BaseEstimator):
         self.b, self.alpha = self.b_, self.alpha_
         if self.kernel == "linear":
             self.coef_ = self.alpha_ @ X
+        self.classes_ = np.array([-1.0, 1.0])
         self.is_fitted_ = True
         return self
 
@@ -176,6 +181,10 @@ def conjugate_gradient(A, B, tol=1e-10, maxiter=1000):
 
 class QLSSVC(_KernelMixin, ClassifierMixin, BaseEstimator):
     """Quantum least-squares SVM (``_qSVM.py:10-404``)."""
+
+    def _more_tags(self):
+        return {"binary_only": True}
+
 
     def __init__(self, kernel="linear", penalty=0.1, degree=3, gamma="scale", coef0=0.0,
                  verbose=False, algorithm="classic", low_rank=False, var=0.9,
@@ -250,6 +259,7 @@ class QLSSVC(_KernelMixin, ClassifierMixin, BaseEstimator):
         self.Nu = self.b_ ** 2 + float(np.sum(self.alpha_ ** 2 * np.sum(X ** 2, 1)))
         if self.kernel == "linear":
             self.coef_ = self.alpha_ @ X
+        self.classes_ = np.array([-1.0, 1.0])
         self.is_fitted_ = True
         self._calls = 0
         return self

@@ -150,7 +150,7 @@ class BaseDecisionTree(BaseEstimator):
                 self.classes_.append(cls)
                 self.n_classes_.append(cls.shape[0])
             y = enc
-            if self.class_weight is not None:
+            if getattr(self, "class_weight", None) is not None:   # classifiers only
                 expanded_class_weight = compute_sample_weight(self.class_weight, y_original)
             self.n_classes_ = np.array(self.n_classes_, dtype=np.intp)
         return np.ascontiguousarray(y, dtype=np.float64), expanded_class_weight
@@ -302,7 +302,6 @@ class DecisionTreeRegressor(RegressorMixin, BaseDecisionTree):
         self.max_leaf_nodes = max_leaf_nodes
         self.min_impurity_decrease = min_impurity_decrease
         self.ccp_alpha = ccp_alpha
-        self.class_weight = None
 
 
 class ExtraTreeClassifier(DecisionTreeClassifier):

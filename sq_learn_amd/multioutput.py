@@ -77,9 +77,17 @@ class _MultiOutputEstimator(MetaEstimatorMixin, MultiOutputMixin, BaseEstimator)
 class MultiOutputRegressor(RegressorMixin, _MultiOutputEstimator):
     """One regressor per target."""
 
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
+
 
 class MultiOutputClassifier(ClassifierMixin, _MultiOutputEstimator):
     """One classifier per target."""
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
 
     @available_if(_has_est("predict_proba"))
     def predict_proba(self, X):
@@ -161,6 +169,10 @@ class _BaseChain(BaseEstimator):
 
 
 class ClassifierChain(MetaEstimatorMixin, ClassifierMixin, _BaseChain):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def fit(self, X, Y):
         super().fit(X, Y)
         self.classes_ = [e.classes_ for e in self.estimators_]
@@ -184,6 +196,10 @@ class ClassifierChain(MetaEstimatorMixin, ClassifierMixin, _BaseChain):
 
 
 class RegressorChain(MetaEstimatorMixin, RegressorMixin, _BaseChain):
+
+    def _more_tags(self):
+        return {"multioutput_only": True}
+
     def fit(self, X, Y, **fit_params):
         return super().fit(X, Y, **fit_params)
 

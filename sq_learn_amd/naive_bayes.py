@@ -219,6 +219,10 @@ class _BaseDiscreteNB(_BaseNB):
 
 
 class MultinomialNB(_BaseDiscreteNB):
+
+    def _more_tags(self):
+        return {"requires_positive_X": True}
+
     def __init__(self, *, alpha=1.0, fit_prior=True, class_prior=None):
         self.alpha = alpha
         self.fit_prior = fit_prior
@@ -240,6 +244,10 @@ class MultinomialNB(_BaseDiscreteNB):
 
 
 class ComplementNB(_BaseDiscreteNB):
+
+    def _more_tags(self):
+        return {"requires_positive_X": True}
+
     def __init__(self, *, alpha=1.0, fit_prior=True, class_prior=None, norm=False):
         self.alpha = alpha
         self.fit_prior = fit_prior
@@ -270,6 +278,10 @@ class ComplementNB(_BaseDiscreteNB):
 
 
 class BernoulliNB(_BaseDiscreteNB):
+
+    def _more_tags(self):
+        return {"poor_score": True}
+
     def __init__(self, *, alpha=1.0, binarize=0.0, fit_prior=True, class_prior=None):
         self.alpha = alpha
         self.binarize = binarize
@@ -306,6 +318,10 @@ class BernoulliNB(_BaseDiscreteNB):
 
 
 class CategoricalNB(_BaseDiscreteNB):
+
+    def _more_tags(self):
+        return {"requires_positive_X": True}
+
     def __init__(self, *, alpha=1.0, fit_prior=True, class_prior=None, min_categories=None):
         self.alpha = alpha
         self.fit_prior = fit_prior

@@ -194,6 +194,10 @@ def normalize(X, norm="l2", *, axis=1, copy=True, return_norm=False):
 
 
 class Normalizer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"stateless": True}
+
     def __init__(self, norm="l2", *, copy=True):
         self.norm = norm
         self.copy = copy

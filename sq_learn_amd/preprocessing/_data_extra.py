@@ -38,6 +38,10 @@ def _handle_zeros_in_scale(scale):
 
 
 class MaxAbsScaler(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, copy=True):
         self.copy = copy
 
@@ -73,6 +77,10 @@ class MaxAbsScaler(TransformerMixin, BaseEstimator):
 
 
 class RobustScaler(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, with_centering=True, with_scaling=True, quantile_range=(25.0, 75.0),
                  copy=True, unit_variance=False):
         self.with_centering = with_centering
@@ -123,6 +131,10 @@ def binarize(X, *, threshold=0.0, copy=True):
 
 
 class Binarizer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"stateless": True}
+
     def __init__(self, *, threshold=0.0, copy=True):
         self.threshold = threshold
         self.copy = copy
@@ -163,6 +175,10 @@ def add_dummy_feature(X, value=1.0):
 
 
 class QuantileTransformer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, n_quantiles=1000, output_distribution="uniform",
                  ignore_implicit_zeros=False, subsample=int(1e5), random_state=None, copy=True):
         self.n_quantiles = n_quantiles
@@ -254,6 +270,10 @@ def quantile_transform(X, *, axis=0, n_quantiles=1000, output_distribution="unif
 
 
 class PowerTransformer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, method="yeo-johnson", *, standardize=True, copy=True):
         self.method = method
         self.standardize = standardize
@@ -377,6 +397,10 @@ def robust_scale(X, *, axis=0, with_centering=True, with_scaling=True,
 
 
 class FunctionTransformer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"stateless": True, "allow_nan": True}
+
     def __init__(self, func=None, inverse_func=None, *, validate=False, accept_sparse=False,
                  check_inverse=True, kw_args=None, inv_kw_args=None):
         self.func = func

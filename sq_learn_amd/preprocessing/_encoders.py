@@ -75,6 +75,10 @@ class _BaseEncoder(TransformerMixin, BaseEstimator):
 
 
 class OneHotEncoder(_BaseEncoder):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, categories="auto", drop=None, sparse=True, dtype=np.float64,
                  handle_unknown="error"):
         self.categories = categories
@@ -182,6 +186,10 @@ class OneHotEncoder(_BaseEncoder):
 
 
 class OrdinalEncoder(_BaseEncoder):
+
+    def _more_tags(self):
+        return {"allow_nan": True}
+
     def __init__(self, *, categories="auto", dtype=np.float64, handle_unknown="error",
                  unknown_value=None):
         self.categories = categories
@@ -224,6 +232,10 @@ class OrdinalEncoder(_BaseEncoder):
 
 
 class LabelEncoder(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"X_types": ["1dlabels"]}
+
     def fit(self, y):
         self.classes_ = _unique_sorted(np.asarray(y).ravel())
         return self
@@ -288,6 +300,10 @@ def label_binarize(y, *, classes, neg_label=0, pos_label=1, sparse_output=False)
 
 
 class LabelBinarizer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"X_types": ["1dlabels"]}
+
     def __init__(self, *, neg_label=0, pos_label=1, sparse_output=False):
         self.neg_label = neg_label
         self.pos_label = pos_label
@@ -322,6 +338,10 @@ class LabelBinarizer(TransformerMixin, BaseEstimator):
 
 
 class MultiLabelBinarizer(TransformerMixin, BaseEstimator):
+
+    def _more_tags(self):
+        return {"X_types": ["2dlabels"]}
+
     def __init__(self, *, classes=None, sparse_output=False):
         self.classes = classes
         self.sparse_output = sparse_output

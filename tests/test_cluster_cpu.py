@@ -263,3 +263,19 @@ def test_kmeans_parallel_init(blobs):
     assert adjusted_rand_score(k.labels_, y) > 0.95
     k2 = KMeans(n_clusters=4, init="k-means||", n_init=1, random_state=0, device="cpu").fit(X)
     np.testing.assert_allclose(k.cluster_centers_, k2.cluster_centers_)
+
+
+def test_kmeans_relocates_empty_clusters_like_sklearn():
+    """An init centre that attracts no row is moved to the farthest row
+    (reference ``_k_means_fast.pyx:162-200``) - same result as scikit-learn."""
+    sk = pytest.importorskip("sklearn.cluster")
+    rng = np.random.RandomState(0)
+    X = np.vstack([rng.randn(200, 2), rng.randn(200, 2) + [8, 8], [[30.0, -30.0]]])
+    init = np.array([[0.0, 0.0], [8.0, 8.0], [500.0, 500.0]])
+    ours = KMeans(n_clusters=3, init=init, n_init=1, device="cpu").fit(X)
+    ref = sk.KMeans(n_clusters=3, init=init, n_init=1, algorithm="lloyd").fit(X)
+    np.testing.assert_allclose(ours.cluster_centers_, ref.cluster_centers_, atol=1e-9)
+    np.testing.assert_array_equal(ours.labels_, ref.labels_)
+    assert ours.inertia_ == pytest.approx(ref.inertia_, rel=1e-9)
+    # the relocated centre is the outlier
+    assert np.any(np.all(np.isclose(ours.cluster_centers_, [30.0, -30.0]), axis=1))

@@ -95,6 +95,17 @@ def _worker(rank, world, port, outdir, case):
             np.testing.assert_allclose(q.singular_values_, qr.singular_values_, rtol=1e-8)
             np.testing.assert_allclose(q.estimate_s_values, qr.estimate_s_values, rtol=1e-12)
             assert abs(q.muA - qr.muA) < 1e-9 * qr.muA
+        elif case == "relocate":
+            # empty-cluster relocation across shards: per-shard top-e + all-gather
+            from sq_learn_amd.models.cluster import KMeans
+            rng = np.random.RandomState(0)
+            Xr = np.vstack([rng.randn(300, 2), rng.randn(300, 2) + [8, 8], [[30.0, -30.0]],
+                            [[-25.0, 20.0]]])
+            init = np.array([[0.0, 0.0], [8.0, 8.0], [500.0, 500.0], [-500.0, 500.0]])
+            ref = KMeans(n_clusters=4, init=init, n_init=1, device="cpu").fit(Xr)
+            got = KMeans(n_clusters=4, init=init, n_init=1, device="cpu").fit(
+                shard_rows(Xr, comm=comm))
+            np.testing.assert_allclose(got.cluster_centers_, ref.cluster_centers_, atol=1e-9)
         elif case == "tomography":
             # long-vector tomography of row-sharded vectors (qPCA left singular
             # vectors): same law as the single-process draw, stopping rule
@@ -183,7 +194,8 @@ def _worker(rank, world, port, outdir, case):
 
 
 @pytest.mark.parametrize("case,world", [("qmeans", 2), ("qmeans", 3), ("kmeans", 2), ("pca", 2),
-                                        ("ipe", 2), ("resume", 2), ("tomography", 2)])
+                                        ("ipe", 2), ("resume", 2), ("tomography", 2),
+                                        ("relocate", 3)])
 def test_sharded_matches_single_process(case, world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, case), nprocs=world, join=True)
