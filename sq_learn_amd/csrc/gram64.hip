@@ -4,7 +4,7 @@
 // ``_dmeans.py:1244-1245``, ``_qPCA.py:581``).  The building block of the
 // sharded CholeskyQR2 in ops/linalg.py (pass 1 on X, pass 2 on X R1^-1).
 //
-// X is fp32 (products of fp32 values are exact in fp64) or fp64; d <= 256
+// X is fp32 / bf16 (products of their values are exact in fp64) or fp64; d <= 256
 // (padded to a multiple of 16: NB column blocks, NB (NB + 1) / 2 upper
 // 16 x 16 blocks of G).  A workgroup of 8 waves streams its contiguous row
 // range in k-steps of 4 rows; the 16-column fragment of block b for the
@@ -20,6 +20,10 @@
 namespace sq {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+SQ_DEV double to_f64(float v) { return (double)v; }
+SQ_DEV double to_f64(double v) { return v; }
+SQ_DEV double to_f64(uint16_t v) { return (double)bf16_to_f32(v); }   // bf16 bits
 
 // Block assignment: wave w < ceil(NB/2) owns upper-block rows w and NB-1-w
 // (NB - w + w + 1 = NB + 1 blocks; the middle row of odd NB once): slot t <
@@ -65,7 +69,7 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
     const T* xr = X + (size_t)(ok ? r : r_begin) * ldx;
     auto ld = [&](int b, double m) -> double {
       const int col = 16 * b + c16;
-      return (ok && col < d) ? (double)xr[col] - m : 0.0;
+      return (ok && col < d) ? to_f64(xr[col]) - m : 0.0;
     };
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) fb[buf][t] = t < nslot ? ld(colblk(t), mcol[t]) : 0.0;
@@ -123,10 +127,14 @@ static int launch_gram64(const T* X, long long ldx, const double* mu, long long 
   return (int)hipGetLastError();
 }
 
+// dtype: 0 fp32, 1 fp64, 2 bf16
 extern "C" int sq_gram64(const void* X, int is_f64, long long ldx, const void* mu, long long n,
                          int d, void* part, int grid, void* stream) {
   if (n <= 0) return 0;
   if (d < 1 || d > 256 || grid < 1 || ldx < d) return (int)hipErrorInvalidValue;
+  if (is_f64 == 2)
+    return launch_gram64((const uint16_t*)X, ldx, (const double*)mu, n, d, (double*)part, grid,
+                         (hipStream_t)stream);
   if (is_f64)
     return launch_gram64((const double*)X, ldx, (const double*)mu, n, d, (double*)part, grid,
                          (hipStream_t)stream);

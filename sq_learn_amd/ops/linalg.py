@@ -57,13 +57,14 @@ def gram64_native(X, mean=None):
     (csrc/gram64.hip, v_mfma_f64_16x16x4_f64): per-workgroup partial upper
     blocks summed in a fixed order (deterministic); X fp32 or fp64, d <= 256."""
     n, d = X.shape
-    assert X.dtype in (torch.float32, torch.float64) and X.stride(1) == 1 and d <= 256
+    assert X.dtype in (torch.float32, torch.float64, torch.bfloat16) and X.stride(1) == 1 and d <= 256
+    code = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2}[X.dtype]
     nb = (d + 15) // 16
     nblk = nb * (nb + 1) // 2
     grid = int(max(1, min(256, (n + 255) // 256)))
     part = torch.empty((grid, nblk, 16, 16), dtype=torch.float64, device=X.device)
     mu = None if mean is None else mean.to(torch.float64).to(X.device).contiguous()
-    rc = nat.native().gram64(X.data_ptr(), int(X.dtype == torch.float64), X.stride(0),
+    rc = nat.native().gram64(X.data_ptr(), code, X.stride(0),
                              0 if mu is None else mu.data_ptr(), n, d, part.data_ptr(), grid,
                              nat.stream_handle(X.device))
     if rc:
@@ -86,8 +87,8 @@ def gram64_local(X, mean=None, W=None, chunk_rows=1 << 19):
     CholeskyQR2 (:func:`cholqr2_r`)."""
     n, d = X.shape
     dw = d if W is None else W.shape[1]
-    native = (nat.use_native(X) and X.dtype in (torch.float32, torch.float64) and d <= 256
-              and dw <= 256 and X.stride(1) == 1)
+    native = (nat.use_native(X) and X.dtype in (torch.float32, torch.float64, torch.bfloat16)
+              and d <= 256 and dw <= 256 and X.stride(1) == 1)
     if native and W is None:
         return gram64_native(X, mean)
     G = torch.zeros((dw, dw), dtype=torch.float64, device=X.device)

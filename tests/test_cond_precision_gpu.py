@@ -37,3 +37,12 @@ def test_gram64_kernel_exact(cuda, d):
     np.testing.assert_allclose(G, Xc.T @ Xc, rtol=1e-12, atol=1e-9)
     G64 = gram64_native(torch.tensor(Xc, device=cuda)).cpu().numpy()
     np.testing.assert_allclose(G64, Xc.T @ Xc, rtol=1e-12, atol=1e-9)
+
+
+def test_gram64_kernel_bf16(cuda):
+    from sq_learn_amd.ops.linalg import gram64_native
+    rng = np.random.RandomState(1)
+    X = torch.tensor(rng.standard_normal((30001, 128)), dtype=torch.bfloat16, device=cuda)
+    Xd = X.double().cpu().numpy()
+    G = gram64_native(X).cpu().numpy()
+    np.testing.assert_allclose(G, Xd.T @ Xd, rtol=1e-12, atol=1e-9)
