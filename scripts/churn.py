@@ -25,6 +25,8 @@ for it in range(15):
     lab = lab.clone()
     cnt = eng.buf.counts.tolist()
     ch = int((lab != prev).sum()) if prev is not None else n
-    print(f"it {it}: changed {ch} ({ch / n:.3%}), multi {cnt[2]} ({cnt[2] / n:.2%}), dense {cnt[1]}, "
-          f"ovf {cnt[0]}, inertia {sc.tolist()[0]:.6e}", flush=True)
+    act = int(eng.rcount.item()) if getattr(eng, "bounds", False) and it > 0 else n
+    print(f"it {it}: changed {ch} ({ch / n:.3%}), active (not pruned) {act} ({act / n:.2%}), "
+          f"multi {cnt[2]} ({cnt[2] / n:.2%}), dense {cnt[1]}, ovf {cnt[0]}, "
+          f"inertia {sc.tolist()[0]:.6e}", flush=True)
     prev = lab

@@ -62,21 +62,29 @@ def _weighted_scatter(X, means, resp):
             diff = X - means[k]
             out[k] = (resp[:, k, None] * diff).T @ diff
         return out
-    C = _split_k(n)
-    m = (n // C) * C
-    # bound the (K_g, n, d) temporaries to ~1 GiB
-    kg = max(1, min(K, (1 << 30) // max(1, 8 * n * d)))
-    out = torch.empty((K, d, d), dtype=X.dtype, device=X.device)
-    for k0 in range(0, K, kg):
-        k1 = min(K, k0 + kg)
-        D = X[None] - means[k0:k1, None, :]                     # (g, n, d)
-        Dw = D * resp[:, k0:k1].T[:, :, None]
-        g = k1 - k0
-        acc = torch.bmm(Dw[:, :m].reshape(g * C, n // C, d).transpose(1, 2),
-                        D[:, :m].reshape(g * C, n // C, d)).reshape(g, C, d, d).sum(1)
-        if m < n:
-            acc += torch.bmm(Dw[:, m:].transpose(1, 2), D[:, m:])
-        out[k0:k1] = acc
+    # bound the temporaries to ~1 GiB: per (component group, row chunk) the
+    # loop holds three (g, rows, d) tensors - D, Dw and the split-K reshape
+    budget = 1 << 30
+    per_row = 3 * X.element_size() * d
+    rows = max(1, min(n, budget // max(1, per_row)))
+    kg = max(1, min(K, budget // max(1, per_row * rows)))
+    out = torch.zeros((K, d, d), dtype=X.dtype, device=X.device)
+    for r0 in range(0, n, rows):
+        Xr = X[r0:r0 + rows]
+        rr = resp[r0:r0 + rows]
+        nr = Xr.shape[0]
+        C = _split_k(nr)
+        m = (nr // C) * C
+        for k0 in range(0, K, kg):
+            k1 = min(K, k0 + kg)
+            D = Xr[None] - means[k0:k1, None, :]                     # (g, rows, d)
+            Dw = D * rr[:, k0:k1].T[:, :, None]
+            g = k1 - k0
+            acc = torch.bmm(Dw[:, :m].reshape(g * C, nr // C, d).transpose(1, 2),
+                            D[:, :m].reshape(g * C, nr // C, d)).reshape(g, C, d, d).sum(1)
+            if m < nr:
+                acc += torch.bmm(Dw[:, m:].transpose(1, 2), D[:, m:])
+            out[k0:k1] += acc
     return out
 
 

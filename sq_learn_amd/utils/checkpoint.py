@@ -68,8 +68,15 @@ class Checkpointer:
         if not self.enabled:
             return
         self.comm.barrier()
+        # a generation tag ties the rank files to the state file: a crash
+        # between the two writes leaves new rank files beside an old state,
+        # which load() then rejects instead of mixing iterations
+        self._generation = getattr(self, "_generation", 0) + 1
+        gen = (int(state.get("restart", 0)) << 32) | (int(state.get("it", 0)) & 0xFFFFFFFF)
+        tag = float(gen) * 1024.0 + float(self._generation % 1024)
         cpu_local = {k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
                      for k, v in local.items()}
+        cpu_local["_generation"] = torch.tensor([tag], dtype=torch.float64)
         # rank files first, then the state file that makes the set valid
         self._atomic_save(cpu_local, self._rank_path())
         self.comm.barrier()
@@ -77,6 +84,7 @@ class Checkpointer:
             cpu_state = {k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
                          for k, v in state.items()}
             cpu_state["world_size"] = self.comm.world_size
+            cpu_state["_generation"] = torch.tensor([tag], dtype=torch.float64)
             self._atomic_save(cpu_state, self._state_path())
         self.comm.barrier()
 
@@ -93,6 +101,16 @@ class Checkpointer:
         if int(state.get("world_size", 1)) != self.comm.world_size:
             return None
         local = torch.load(self._rank_path(), weights_only=True)
+        # every rank's file must belong to the state's generation (all ranks)
+        sg = state.get("_generation")
+        lg = local.get("_generation")
+        same = torch.tensor([1.0 if (sg is None and lg is None) or
+                             (sg is not None and lg is not None and torch.equal(sg, lg)) else 0.0])
+        self.comm.all_reduce_(same, op="min")
+        if float(same.item()) < 1.0:
+            return None
+        state.pop("_generation", None)
+        local.pop("_generation", None)
         return state, local
 
     def clear(self):

@@ -110,3 +110,26 @@ def test_checkpoint_mismatch_starts_over(tmp_path):
     with pytest.warns(UserWarning, match="does not match"):
         m = QMeans(checkpoint_dir=ckdir, **{**kw, "n_clusters": 4}).fit(X)
     assert not hasattr(m, "resumed_from_")
+
+
+def test_checkpoint_rejects_mixed_generations(tmp_path):
+    """A crash between the rank-file and state-file writes leaves new rank
+    files beside the previous state: load() must refuse the mix."""
+    import torch
+    from sq_learn_amd.utils.checkpoint import Checkpointer
+    from sq_learn_amd.parallel.comm import Comm
+    ck = Checkpointer(str(tmp_path), Comm(None), tag="t", every=1)
+    ck.save({"restart": 0, "it": 3, "C": torch.zeros(2)}, {"lab": torch.zeros(3)})
+    assert ck.load() is not None
+    # simulate: rank file of the next generation written, state file not
+    orig = ck._atomic_save
+    calls = []
+
+    def only_rank(obj, path):
+        calls.append(path)
+        if path == ck._rank_path():
+            orig(obj, path)
+    ck._atomic_save = only_rank
+    ck.save({"restart": 0, "it": 6, "C": torch.ones(2)}, {"lab": torch.ones(3)})
+    ck._atomic_save = orig
+    assert ck.load() is None
