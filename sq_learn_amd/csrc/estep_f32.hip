@@ -749,30 +749,57 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 // more than delta beyond the label's squared distance), otherwise it goes to
 // the list the x64 kernel processes.  No host sync: the count stays on the
 // device.
+constexpr int kBoundsChunk = 16384;   // rows per workgroup: one list atomic per chunk
 __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const int* __restrict__ labels, float* __restrict__ ub, float* __restrict__ lb,
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
     long long* __restrict__ rlist, int* __restrict__ rcount) {
-  const int lane = threadIdx.x & 63;
+  constexpr int PER = kBoundsChunk / 256;   // rows per thread (bit mask)
+  __shared__ int wsum[4];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const double sm = *smax;
-  for (long long base = (long long)blockIdx.x * 256; base < n; base += (long long)gridDim.x * 256) {
-    const long long i = base + threadIdx.x;
-    bool act = false;
-    if (i < n) {
-      const int l = labels[i];
-      const double u = (double)ub[i] + (l >= 0 ? shift[l] : 1e300);
-      const double w = (double)lb[i] - sm;
-      act = !(l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30);
-      if (!act) {
-        ub[i] = (float)u * (1.0f + 0x1p-22f);
-        lb[i] = (float)w * (1.0f - 0x1p-22f);
-      }
+  const long long c0 = (long long)blockIdx.x * kBoundsChunk;
+  unsigned long long act = 0;   // bit p: row c0 + p * 256 + tid is active
+#pragma unroll 4
+  for (int p = 0; p < PER; ++p) {
+    const long long i = c0 + (long long)p * 256 + tid;
+    if (i >= n) break;
+    const int l = labels[i];
+    const double u = (double)ub[i] + (l >= 0 ? shift[l] : 1e300);
+    const double w = (double)lb[i] - sm;
+    const bool a = !(l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30);
+    if (a) {
+      act |= 1ull << p;
+    } else {
+      ub[i] = (float)u * (1.0f + 0x1p-22f);
+      lb[i] = (float)w * (1.0f - 0x1p-22f);
     }
-    const unsigned long long m = __ballot(act);
-    int b0 = 0;
-    if (lane == 0 && m) b0 = atomicAdd(rcount, __popcll(m));
-    b0 = __shfl(b0, 0, 64);
-    if (act) rlist[b0 + __popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+  // block-wide exclusive scan of the per-thread counts, ONE list atomic per chunk
+  const int mine = __popcll(act);
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < 4; ++w2) {
+    before += w2 < wv ? wsum[w2] : 0;
+    total += wsum[w2];
+  }
+  if (tid == 0) base_s = total ? atomicAdd(rcount, total) : 0;
+  __syncthreads();
+  int pos = base_s + before + incl - mine;
+  for (int p = 0; p < PER && act; ++p) {
+    if (act & (1ull << p)) {
+      rlist[pos++] = c0 + (long long)p * 256 + tid;
+      act &= ~(1ull << p);
+    }
   }
 }
 
@@ -782,9 +809,8 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(rcount, 0, sizeof(int), st);
-  const long long blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)),
-                     dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
+  const long long blocks = (n + kBoundsChunk - 1) / kBoundsChunk;
+  hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
                      (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
                      (int*)rcount);
   return (int)hipGetLastError();
