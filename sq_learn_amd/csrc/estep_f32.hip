@@ -451,7 +451,8 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     int* __restrict__ dense_count, long long* __restrict__ mrows, int* __restrict__ mcand,
     int* __restrict__ multi_count, long long n, int k_pad, float alpha, float delta_s,
     RngKey key, long long row_offset, int dense_cap, int qbits, const long long* __restrict__ rlist,
-    const int* __restrict__ rcount, float* __restrict__ ub, float* __restrict__ lb) {
+    const int* __restrict__ rcount, float* __restrict__ ub, float* __restrict__ lb,
+    int* __restrict__ mslot) {
   constexpr int NW = kX64Waves;
   constexpr int DX = KSD * 16;
   constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
@@ -622,26 +623,22 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 
     // ---- row minimum (packed) by the transposed reduce-scatter: lane r32
     // even ends with the min of row irow = r32 >> 1 of its half
-    float R[16], R2[16];
+    auto row_min = [&](float (&R)[16]) -> float {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { R[i] = m1[i]; R2[i] = m2[i]; }
-    // (min, 2nd) pairs merge as (min(a1, b1), min(max(a1, b1), min(a2, b2)))
+      for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
+        const bool hi = (r32 & o) != 0;
 #pragma unroll
-    for (int o = 16, c = 8; o >= 2; o >>= 1, c >>= 1) {
-      const bool hi = (r32 & o) != 0;
-#pragma unroll
-      for (int j = 0; j < c; ++j) {
-        const float ra = R[j], rb = R[c + j], ra2 = R2[j], rb2 = R2[c + j];
-        const float keepv = hi ? rb : ra, sendv = hi ? ra : rb;
-        const float keep2 = hi ? rb2 : ra2, send2 = hi ? ra2 : rb2;
-        const float o1 = __shfl_xor(sendv, o, 64), o2 = __shfl_xor(send2, o, 64);
-        R[j] = vmin(keepv, o1);
-        R2[j] = vmin(fmaxf(keepv, o1), vmin(keep2, o2));
+        for (int j = 0; j < c; ++j) {
+          const float keepv = hi ? R[c + j] : R[j], sendv = hi ? R[j] : R[c + j];
+          R[j] = vmin(keepv, __shfl_xor(sendv, o, 64));
+        }
       }
-    }
-    const float q1 = __shfl_xor(R[0], 1, 64), q2 = __shfl_xor(R2[0], 1, 64);
-    const float rmin = vmin(R[0], q1);
-    const float rsec = vmin(fmaxf(R[0], q1), vmin(R2[0], q2));
+      return vmin(R[0], __shfl_xor(R[0], 1, 64));
+    };
+    float R[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) R[i] = m1[i];
+    const float rmin = row_min(R);
     const int irow = r32 >> 1;
     const int rl_own = (irow & 3) + 8 * (irow >> 2) + 4 * half;
     const long long g_own = row_at(row0 + rl_own);
@@ -651,24 +648,14 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     const float mag = 0.25f * Ch * Ch + prod;
     const float E = 1.0625f * 0x1p-10f * prod + pack_rel * mag + sub_rel * (xsv + Ch);
     const float T_own = __uint_as_float(__float_as_uint(rmin) & keep) + delta_s + 2.0f * E;
-    // Hamerly bounds of this row (distances, not squared): ub >= |x - c_min|,
-    // lb <= distance to every other centroid (the 2nd smallest filter value
-    // minus the bound), from D = |x|^2 + D'/alpha^2 with an fp32 margin
-    float ub_own = 0.f, lb_own = 0.f;
-    if (ub) {
-      const float ia2 = 1.0f / (alpha * alpha);
-      const float d1 = (__uint_as_float(__float_as_uint(rmin) & keep) + E) * ia2;
-      const float d2 = (__uint_as_float(__float_as_uint(rsec) & keep) - E) * ia2;
-      const float marg = 0x1p-20f * (xn_own + fabsf(d1) + fabsf(d2));
-      ub_own = sqrtf(fmaxf(xn_own + d1 + marg, 0.f)) * (1.0f + 0x1p-20f);
-      lb_own = sqrtf(fmaxf(xn_own + d2 - marg, 0.f)) * (1.0f - 0x1p-20f);
-    }
 
     // ---- candidates -> LDS list of their row (C/D layout: register i of this
     // lane is row (i & 3) + 8 (i >> 2) + 4 half, column class r32)
+    float nc[16];   // per register: this lane's smallest NON-candidate value
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float T = __shfl(T_own, 32 * half + 2 * i, 64);
+      nc[i] = m1[i] > T ? m1[i] : (m2[i] > T ? m2[i] : m3[i]);
       const int rl = (i & 3) + 8 * (i >> 2) + 4 * half;
       auto jof = [&](float p) -> int {
         const uint32_t q = __float_as_uint(p) & qmask;
@@ -684,6 +671,22 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
         if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(m2[i]);
       }
     }
+    // Hamerly bounds of this row (distances, not squared): ub >= |x - c_min|,
+    // lb <= distance to every NON-candidate centroid (the smallest filter
+    // value above T minus the bound; for a one-candidate row the 2nd
+    // smallest), from D = |x|^2 + D'/alpha^2 with an fp32 margin.  A
+    // multi-candidate row whose non-candidates stay beyond the band under
+    // the next centroid shifts keeps its candidate set (bounds_filter).
+    float ub_own = 0.f, lb_own = 0.f;
+    if (ub) {
+      const float ncmin = row_min(nc);
+      const float ia2 = 1.0f / (alpha * alpha);
+      const float d1 = (__uint_as_float(__float_as_uint(rmin) & keep) + E) * ia2;
+      const float d2 = (__uint_as_float(__float_as_uint(ncmin) & keep) - E) * ia2;
+      const float marg = 0x1p-20f * (xn_own + fabsf(d1) + fabsf(d2));
+      ub_own = sqrtf(fmaxf(xn_own + d1 + marg, 0.f)) * (1.0f + 0x1p-20f);
+      lb_own = sqrtf(fmaxf(xn_own + d2 - marg, 0.f)) * (1.0f - 0x1p-20f);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 
@@ -695,13 +698,14 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
       const int src = ((r32 & 3) + 4 * ((r32 >> 3) & 3)) * 2 + 32 * ((r32 >> 2) & 1);
       const float u = __shfl(ub_own, src, 64), l = __shfl(lb_own, src, 64);
       if (valid && half == 0) {
-        ub[g] = u;
-        lb[g] = cnt[r32] == 1 ? l : 0.0f;   // several candidates: always re-evaluate
+        ub[g] = u;   // multi rows: replaced by the re-check (label distance)
+        lb[g] = cnt[r32] <= kMaxCand ? l : 0.0f;   // dense: always re-evaluate
       }
     }
     const int c_r = cnt[r32];
     const bool dense = c_r > kMaxCand;
     const bool multi = valid && !dense && c_r >= 2;
+    if (mslot && valid && half == 0 && !multi) mslot[g] = -1;
     if (valid && half == 0) {
       if (dense) {
         const int s = atomicAdd(dense_count, 1);
@@ -723,6 +727,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     mbase = __shfl(mbase, 0, 64);
     if (mrow) {
       const long long slot = (long long)mbase + __popcll(mm & ((1ull << lane) - 1ull));
+      if (mslot) mslot[g] = slot < n ? (int)slot : -1;
       if (slot < n) {
         mrows[slot] = g;
         int* mc = mcand + slot * (kMaxCand + 1);
@@ -741,26 +746,33 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Hamerly pruning of the certified E-step (exact: the pruned rows provably
-// keep a one-member delta-band, i.e. label = argmin, under the new
-// centroids).  After a centroid update with per-centroid shifts s_j =
-// |c_j' - c_j| (fp64): ub_i += s_{label_i}, lb_i -= max_j s_j; the row is
-// pruned when lb_i > 0 and lb_i^2 - ub_i^2 > delta (every other centroid is
-// more than delta beyond the label's squared distance), otherwise it goes to
-// the list the x64 kernel processes.  No host sync: the count stays on the
-// device.
-constexpr int kBoundsChunk = 16384;   // rows per workgroup: one list atomic per chunk
+// Hamerly pruning of the certified E-step (exact).  After a centroid update
+// with per-centroid shifts s_j = |c_j' - c_j| (fp64): ub_i += s_{label_i},
+// lb_i -= max_j s_j.  ub bounds the distance to the label, lb the distance to
+// every centroid outside the row's candidate set S (S = {label} for a
+// one-candidate row).  When lb_i > 0 and lb_i^2 - ub_i^2 > delta, every
+// centroid outside S is more than delta beyond the label's squared distance
+// under the new centroids, so the argmin and the whole delta-band lie in S:
+//   * |S| = 1 (mslot < 0): the label stands, the row is skipped;
+//   * |S| >= 2: the row skips the filter sweep and goes straight to the fp64
+//     re-check over S (its candidate list is copied from the previous
+//     iteration's multi list, slot mslot, into this iteration's list).
+// The rest go to rlist for the x64 kernel.  No host sync: both counts stay
+// on the device (one atomic per 16K-row chunk and list).
+constexpr int kBoundsChunk = 16384;
 __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const int* __restrict__ labels, float* __restrict__ ub, float* __restrict__ lb,
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
-    long long* __restrict__ rlist, int* __restrict__ rcount) {
-  constexpr int PER = kBoundsChunk / 256;   // rows per thread (bit mask)
+    long long* __restrict__ rlist, int* __restrict__ rcount, int* __restrict__ mslot,
+    const int* __restrict__ mcand_prev, long long* __restrict__ mrows, int* __restrict__ mcand,
+    int* __restrict__ multi_count) {
+  constexpr int PER = kBoundsChunk / 256;   // rows per thread (bit masks)
   __shared__ int wsum[4];
-  __shared__ int base_s;
+  __shared__ int base_a, base_m;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const double sm = *smax;
   const long long c0 = (long long)blockIdx.x * kBoundsChunk;
-  unsigned long long act = 0;   // bit p: row c0 + p * 256 + tid is active
+  unsigned long long act = 0, rec = 0;   // bit p: row c0 + p * 256 + tid
 #pragma unroll 4
   for (int p = 0; p < PER; ++p) {
     const long long i = c0 + (long long)p * 256 + tid;
@@ -774,10 +786,12 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     } else {
       ub[i] = (float)u * (1.0f + 0x1p-22f);
       lb[i] = (float)w * (1.0f - 0x1p-22f);
+      if (mslot[i] >= 0) rec |= 1ull << p;
     }
   }
-  // block-wide exclusive scan of the per-thread counts, ONE list atomic per chunk
-  const int mine = __popcll(act);
+  // block-wide exclusive scan of both per-thread counts (packed 16 | 16 bits:
+  // a chunk holds 2^14 rows), ONE atomic per list and chunk
+  const int mine = __popcll(act) | (__popcll(rec) << 16);
   int incl = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -792,27 +806,47 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     before += w2 < wv ? wsum[w2] : 0;
     total += wsum[w2];
   }
-  if (tid == 0) base_s = total ? atomicAdd(rcount, total) : 0;
+  if (tid == 0) {
+    base_a = (total & 0xffff) ? atomicAdd(rcount, total & 0xffff) : 0;
+    base_m = (total >> 16) ? atomicAdd(multi_count, total >> 16) : 0;
+  }
   __syncthreads();
-  int pos = base_s + before + incl - mine;
+  const int ex = before + incl - mine;
+  int pos = base_a + (ex & 0xffff);
   for (int p = 0; p < PER && act; ++p) {
     if (act & (1ull << p)) {
       rlist[pos++] = c0 + (long long)p * 256 + tid;
       act &= ~(1ull << p);
     }
   }
+  int mpos = base_m + (ex >> 16);
+  for (int p = 0; p < PER && rec; ++p) {
+    if (rec & (1ull << p)) {
+      const long long i = c0 + (long long)p * 256 + tid;
+      const int* src = mcand_prev + (size_t)mslot[i] * (kMaxCand + 1);
+      int* dst = mcand + (size_t)mpos * (kMaxCand + 1);
+      const int c_r = src[0];
+      for (int c = 0; c <= c_r; ++c) dst[c] = src[c];
+      mrows[mpos] = i;
+      mslot[i] = mpos++;
+      rec &= ~(1ull << p);
+    }
+  }
 }
 
 extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const void* shift,
                                 const void* smax, long long n, double delta, void* rlist,
-                                void* rcount, void* stream) {
+                                void* rcount, void* mslot, const void* mcand_prev, void* mrows,
+                                void* mcand, void* multi_count, void* stream) {
   if (n <= 0) return 0;
+  if (!mslot || !mcand_prev || !mrows || !mcand || !multi_count) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(rcount, 0, sizeof(int), st);
   const long long blocks = (n + kBoundsChunk - 1) / kBoundsChunk;
-  hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
-                     (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
-                     (int*)rcount);
+  hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (const int*)labels, (float*)ub, (float*)lb, (const double*)shift,
+                     (const double*)smax, n, delta, (long long*)rlist, (int*)rcount, (int*)mslot,
+                     (const int*)mcand_prev, (long long*)mrows, (int*)mcand, (int*)multi_count);
   return (int)hipGetLastError();
 }
 
@@ -830,7 +864,7 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
     float* __restrict__ mind, long long cap, double delta, RngKey key, long long row_offset,
-    float* __restrict__ corr) {
+    float* __restrict__ corr, float* __restrict__ ub) {
   constexpr int LPR = 16;                  // lanes per row
   constexpr int FPL = DX / LPR;            // features per lane (DX >= 64) or fewer
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
@@ -904,6 +938,9 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
       labels[g] = pick;
       mind[g] = (float)dmin;
       if (corr) corr[g] = (float)(dmin - dpick);
+      // Hamerly upper bound of a multi row: the distance to its LABEL (the
+      // filter moves it by the label's shift)
+      if (ub) ub[g] = (float)sqrt(dpick) * (1.0f + 0x1p-20f);
     }
   }
 }
@@ -1083,7 +1120,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
-                            void* ub, void* lb) {
+                            void* ub, void* lb, void* mslot) {
   constexpr int NW = kX64Waves;
   const size_t lds = kX64Ring * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4;
   auto kern = estep_x64_kernel<KSD>;
@@ -1110,7 +1147,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                      (const float*)cmax2, (int*)labels, (float*)mind, (long long*)dense_rows,
                      (int*)dense_count, (long long*)mrows, (int*)mcand, (int*)multi_count, n,
                      k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits,
-                     (const long long*)rlist, (const int*)rcount, (float*)ub, (float*)lb);
+                     (const long long*)rlist, (const int*)rcount, (float*)ub, (float*)lb,
+                     (int*)mslot);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   // the re-check: one pass over the multi list (count read on the device)
@@ -1119,7 +1157,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,
                      (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
-                     delta, key, row_offset, (float*)corr);
+                     delta, key, row_offset, (float*)corr, (float*)ub);
   return (int)hipGetLastError();
 }
 
@@ -1168,13 +1206,15 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
                  const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
                  void* mrows, void* mcand, void* corr, void* rlist, void* rcount, void* ub,
-                 void* lb, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
+                 void* lb, void* mslot, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
                  int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
   if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 4096 || k > k_pad || d > d_pad)
     return (int)hipErrorInvalidValue;
+  if ((ub != nullptr) != (lb != nullptr) || (ub != nullptr) != (mslot != nullptr))
+    return (int)hipErrorInvalidValue;   // bounds need the multi-row slot map
   int aexp = 0;
   if (!(alpha > 0.0) || frexp(alpha, &aexp) != 0.5) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
@@ -1189,7 +1229,8 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   case KSD * 16:                                                                                 \
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
-                               row_offset, (int)min(n, 2147483647LL), st, rlist, rcount, ub, lb); \
+                               row_offset, (int)min(n, 2147483647LL), st, rlist, rcount, ub, lb,  \
+                               mslot);                                                           \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \

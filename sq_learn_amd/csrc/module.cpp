@@ -28,7 +28,8 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
                                            long long, const void*, void*, long long, unsigned,
                                            unsigned, unsigned, unsigned, const void*, int, void*);
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
-                                           long long, double, void*, void*, void*);
+                                           long long, double, void*, void*, void*, const void*,
+                                           void*, void*, void*, void*);
 // gram64.hip
 __attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, long long, int, void*,
                                     int, void*);
@@ -85,8 +86,8 @@ __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C
                          void* stream);
 __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, const void*,
                                        const void*, const void*, void*, void*, void*, void*, void*,
-                                       void*, void*, void*, void*, void*, void*, void*, void*, int,
-                                       long long, int, int, int, int, double, double, unsigned,
+                                       void*, void*, void*, void*, void*, void*, void*, void*,
+                                       void*, int, long long, int, int, int, int, double, double, unsigned,
                                        unsigned, unsigned, unsigned, long long, void*);
 __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
                                        long long, void*);
@@ -213,11 +214,14 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
-  unsigned long long lab, ub, lb, sh, sm, rl, rc, st; long long n; double delta;
-  if (!PyArg_ParseTuple(a, "KKKKKLdKKK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc, &st))
+  unsigned long long lab, ub, lb, sh, sm, rl, rc, ms, mcp, mr, mc, mcnt, st; long long n;
+  double delta;
+  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc, &ms,
+                        &mcp, &mr, &mc, &mcnt, &st))
     return nullptr;
   CHECK(sq_bounds_filter)
-  return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(st)));
+  return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(ms),
+                              P(mcp), P(mr), P(mc), P(mcnt), P(st)));
 }
 
 static PyObject* py_centroid_delta(PyObject*, PyObject* a) {
@@ -336,16 +340,17 @@ static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_estep_x64(PyObject*, PyObject* a) {
-  unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, corr, rl, rc, ub, lb, cnt,
-      part, st;
+  unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, corr, rl, rc, ub, lb, ms,
+      cnt, part, st;
   int pcap, d, dp, k, kp; long long n, roff; double alpha, delta; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2, &lab,
-                        &mind, &dr, &ovr, &mr, &mc, &corr, &rl, &rc, &ub, &lb, &cnt, &part, &pcap,
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2, &lab,
+                        &mind, &dr, &ovr, &mr, &mc, &corr, &rl, &rc, &ub, &lb, &ms, &cnt, &part, &pcap,
                         &n, &d, &dp, &k, &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st))
     return nullptr;
   CHECK(sq_estep_x64)
   return ret(sq_estep_x64(P(Xh), P(X), P(C), P(Cm), P(xn), P(cm2), P(lab), P(mind), P(dr), P(ovr),
-                          P(mr), P(mc), P(corr), P(rl), P(rc), P(ub), P(lb), P(cnt), P(part), pcap,
+                          P(mr), P(mc), P(corr), P(rl), P(rc), P(ub), P(lb), P(ms), P(cnt),
+                          P(part), pcap,
                           n, d, dp, k, kp, alpha, delta, k0, k1, s0, s1, roff, P(st)));
 }
 

@@ -278,15 +278,17 @@ class LloydEngine:
                 Cp = self.C if self.d == self.d_pad else self._padded_centers()
                 rows = None
                 if self.bounds and self.bounds_valid and not full:
+                    K.ensure_multi_buffers(self.buf, self.n, self.device, True)
+                    self.buf.counts.zero_()
                     K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
                                            self.shift_s, self.smax, self.delta, self.rlist,
-                                           self.rcount)
+                                           self.rcount, self.buf)
                     rows = (self.rlist, self.rcount)
                 lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
                                                self.cmax2, self.k, self.delta, self.alpha, key,
                                                self.row_offset, self.buf,
                                                bounds=(self.ub, self.lb) if self.bounds else None,
-                                               rows=rows)
+                                               rows=rows, zero_counts=rows is None)
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):

@@ -181,6 +181,11 @@ class EStepBuffers:
         self.dense_rows = None   # allocated by the certified E-step on first use
         self.multi_rows = None   # certified E-step: rows sent to the fp64 re-check kernel
         self.multi_cand = None   # ... and their candidate lists [n][1 + 16]
+        # Hamerly pruning: the previous iteration's candidate lists (the
+        # filter copies a pruned multi row's list from there) and each row's
+        # slot in the current list (-1: not a multi row)
+        self.multi_cand_prev = None
+        self.mslot = None
         # per-row (min distance - distance to the label) of the rows whose
         # label is not their argmin (fp64 re-check / dense / overflow rows):
         # the incremental M-step's inertia correction; None = not produced
@@ -331,19 +336,39 @@ def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorksp
                                  nat.ptr(C_old), nat.stream_handle(X.device))
 
 
-def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount):
+def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf: EStepBuffers):
     """Hamerly pruning (csrc/estep_f32.hip bounds_filter_kernel): bounds
-    moved by the centroid shifts; rows that can no longer be proven to keep a
-    one-member band go to ``rlist`` (count in ``rcount``, on the device)."""
+    moved by the centroid shifts; rows that can no longer be proven to keep
+    their candidate set go to ``rlist`` (count in ``rcount``, on the device);
+    pruned multi-candidate rows are appended to ``buf``'s multi list (their
+    candidates copied from the previous iteration's) for the fp64 re-check.
+    ``buf.counts`` must be zeroed before (the multi count accumulates)."""
     n = labels.numel()
     assert ub.dtype == torch.float32 and lb.dtype == torch.float32 and rlist.numel() >= n
     assert shift.dtype == torch.float64 and smax.dtype == torch.float64
+    assert buf.mslot is not None and buf.mslot.numel() >= n and buf.multi_cand_prev is not None
     rc = nat.native().bounds_filter(labels.data_ptr(), ub.data_ptr(), lb.data_ptr(),
                                     shift.data_ptr(), smax.data_ptr(), n, float(delta),
-                                    rlist.data_ptr(), rcount.data_ptr(),
+                                    rlist.data_ptr(), rcount.data_ptr(), buf.mslot.data_ptr(),
+                                    buf.multi_cand_prev.data_ptr(), buf.multi_rows.data_ptr(),
+                                    buf.multi_cand.data_ptr(), buf.counts[2:3].data_ptr(),
                                     nat.stream_handle(labels.device))
     if rc:
         raise RuntimeError(f"bounds_filter failed (hip error {rc})")
+
+
+def ensure_multi_buffers(buf: EStepBuffers, n, device, bounds=False):
+    """Allocate the certified E-step's row lists (and, with ``bounds``, the
+    double-buffered candidate lists + slot map of the Hamerly pruning)."""
+    if buf.dense_rows is None or buf.dense_rows.numel() < n:
+        buf.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=device)
+    if buf.multi_rows is None or buf.multi_rows.numel() < n:
+        buf.multi_rows = torch.empty(max(n, 1), dtype=torch.int64, device=device)
+        buf.multi_cand = torch.empty((max(n, 1), 17), dtype=torch.int32, device=device)
+        buf.multi_cand_prev = None
+    if bounds and (buf.multi_cand_prev is None or buf.mslot is None or buf.mslot.numel() < n):
+        buf.multi_cand_prev = torch.empty_like(buf.multi_cand)
+        buf.mslot = torch.full((max(n, 1),), -1, dtype=torch.int32, device=device)
 
 
 def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWorkspace, perm2,
@@ -563,15 +588,19 @@ def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_o
 
 
 def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
-                     buf: EStepBuffers, stream=None, bounds=None, rows=None):
-    """``bounds`` = (ub, lb) fp32 [n]: the kernel writes each processed
-    row's Hamerly bounds; ``rows`` = (rlist int64 [n], rcount int32 [1]):
-    process only the listed rows (list mode, count on the device)."""
+                     buf: EStepBuffers, stream=None, bounds=None, rows=None, zero_counts=True):
     """Certified E-step (``estep_x64_kernel``): one fp16 MFMA pass with a
     rigorous error bound, fp64 re-check of the candidate centroids, dense rows
     through the fp32-faithful 3-pass kernel.  Labels are the fp64 delta-band
     rule's; ``buf.mind`` holds -1 on single-candidate rows (filled by the
-    M-step's row pass or ``fill_mind_native``).  No host sync."""
+    M-step's row pass or ``fill_mind_native``).  No host sync.
+
+    ``bounds`` = (ub, lb) fp32 [n]: the kernel writes each processed row's
+    Hamerly bounds and multi-list slot (``buf.mslot``), and the candidate
+    lists are swapped with ``buf.multi_cand_prev`` afterwards; ``rows`` =
+    (rlist int64 [n], rcount int32 [1]): process only the listed rows (list
+    mode, count on the device; the filter already started this iteration's
+    multi list, so ``zero_counts`` is False)."""
     n, d_pad = Xf.shape
     k_pad = C_op.shape[0] * 64
     assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in FAST_D
@@ -581,13 +610,10 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     assert tuple(C_pad.shape) == (k, d_pad)
     assert cmax2.dtype == torch.float32 and xn.dtype == torch.float32 and xn.numel() >= n
     assert k <= k_pad <= 4096 and buf.labels.numel() >= n
-    if buf.dense_rows is None or buf.dense_rows.numel() < n:
-        buf.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
-    if buf.multi_rows is None or buf.multi_rows.numel() < n:
-        buf.multi_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
-        buf.multi_cand = torch.empty((max(n, 1), 17), dtype=torch.int32, device=Xf.device)
+    ensure_multi_buffers(buf, n, Xf.device, bounds is not None)
     st = stream if stream is not None else nat.stream_handle(Xf.device)
-    buf.counts.zero_()
+    if zero_counts:
+        buf.counts.zero_()
     buf.ovf_clean = False
     nat.native().estep_x64(Xh.data_ptr(), Xf.data_ptr(), C_op.data_ptr(), C_pad.data_ptr(),
                            xn.data_ptr(), cmax2.data_ptr(), buf.labels.data_ptr(),
@@ -598,9 +624,12 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
                            0 if rows is None else rows[1].data_ptr(),
                            0 if bounds is None else bounds[0].data_ptr(),
                            0 if bounds is None else bounds[1].data_ptr(),
+                           0 if bounds is None else buf.mslot.data_ptr(),
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)
+    if bounds is not None:   # this iteration's lists are the next one's "previous"
+        buf.multi_cand, buf.multi_cand_prev = buf.multi_cand_prev, buf.multi_cand
     return buf.labels, buf.mind
 
 
