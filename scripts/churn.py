@@ -29,4 +29,33 @@ for it in range(15):
     print(f"it {it}: changed {ch} ({ch / n:.3%}), active (not pruned) {act} ({act / n:.2%}), "
           f"multi {cnt[2]} ({cnt[2] / n:.2%}), dense {cnt[1]}, ovf {cnt[0]}, "
           f"inertia {sc.tolist()[0]:.6e}", flush=True)
+    if getattr(eng, "bounds", False):
+        q = torch.quantile(eng.shift_s.float(), torch.tensor([0.5, 0.9, 0.99], device=dev)).tolist()
+        print(f"   shifts: median {q[0]:.3g} p90 {q[1]:.3g} p99 {q[2]:.3g} max {eng.smax.item():.3g}")
     prev = lab
+# exact candidate gaps of the last iteration's multi rows (candidate lists
+# are stored per row)
+if getattr(eng, "bounds", False):
+    b = eng.buf
+    m = int(b.counts[2].item())
+    rows = b.multi_rows[:m]
+    sel = torch.arange(0, m, max(1, m // 20000), device=dev)
+    rows = rows[sel]
+    cand = b.multi_cand[rows]
+    C = eng.C.double()
+    x = X[rows].double()
+    cr = cand[:, 0].long()
+    D = torch.full((sel.numel(), 16), float("inf"), dtype=torch.float64, device=dev)
+    for c in range(16):
+        ok = cr > c
+        j = cand[:, 1 + c].long().clamp(0, 1023)
+        d = ((x - C[j]) ** 2).sum(1)
+        D[:, c] = torch.where(ok, d, D[:, c])
+    Ds = D.sort(1).values
+    gap = Ds[:, 1] - Ds[:, 0]
+    band1 = gap > 0.5
+    qs = torch.tensor([0.1, 0.5, 0.9], device=dev, dtype=torch.float64)
+    print(f"multi rows sampled {sel.numel()}: band>=2 {(~band1).float().mean().item():.3f}; "
+          f"c_r mean {cr.float().mean().item():.2f}; gap quantiles {torch.quantile(gap, qs).tolist()}; "
+          f"dmin median {Ds[:, 0].median().item():.4g}")
+    print("E-range of filter: alpha", eng.alpha)

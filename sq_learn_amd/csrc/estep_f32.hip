@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     int* __restrict__ multi_count, long long n, int k_pad, float alpha, float delta_s,
     RngKey key, long long row_offset, int dense_cap, int qbits, const long long* __restrict__ rlist,
     const int* __restrict__ rcount, float* __restrict__ ub, float* __restrict__ lb,
-    int* __restrict__ mslot) {
+    int* __restrict__ mflag) {
   constexpr int NW = kX64Waves;
   constexpr int DX = KSD * 16;
   constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
@@ -705,7 +705,7 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     const int c_r = cnt[r32];
     const bool dense = c_r > kMaxCand;
     const bool multi = valid && !dense && c_r >= 2;
-    if (mslot && valid && half == 0 && !multi) mslot[g] = -1;
+    if (mflag && valid && half == 0 && !multi) mflag[g] = 0;
     if (valid && half == 0) {
       if (dense) {
         const int s = atomicAdd(dense_count, 1);
@@ -727,10 +727,10 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
     mbase = __shfl(mbase, 0, 64);
     if (mrow) {
       const long long slot = (long long)mbase + __popcll(mm & ((1ull << lane) - 1ull));
-      if (mslot) mslot[g] = slot < n ? (int)slot : -1;
+      if (mflag) mflag[g] = slot < n ? 1 : 0;
       if (slot < n) {
         mrows[slot] = g;
-        int* mc = mcand + slot * (kMaxCand + 1);
+        int* mc = mcand + g * (kMaxCand + 1);   // per row: kept across iterations
         mc[0] = c_r;
         for (int c = 0; c < c_r; ++c) mc[1 + c] = cand[r32 * kMaxCand + c];
       } else {
@@ -753,23 +753,38 @@ __global__ void __launch_bounds__(512) estep_x64_kernel(
 // one-candidate row).  When lb_i > 0 and lb_i^2 - ub_i^2 > delta, every
 // centroid outside S is more than delta beyond the label's squared distance
 // under the new centroids, so the argmin and the whole delta-band lie in S:
-//   * |S| = 1 (mslot < 0): the label stands, the row is skipped;
+//   * |S| = 1 (mflag = 0): the label stands, the row is skipped;
 //   * |S| >= 2: the row skips the filter sweep and goes straight to the fp64
 //     re-check over S (its candidate list is copied from the previous
-//     iteration's multi list, slot mslot, into this iteration's list).
+//     iteration's multi list; its candidates stay in the per-row mcand).
 // The rest go to rlist for the x64 kernel.  No host sync: both counts stay
-// on the device (one atomic per 16K-row chunk and list).
-constexpr int kBoundsChunk = 16384;
+// on the device (one atomic per 4K-row chunk and list).
+// A few centroids move far more than the rest (the contested ones: median
+// shift ~0.006 vs max ~1 on the bench), so max_j s_j would collapse every
+// row's lb: the nf fastest centroids F are taken out of the max (sm = the
+// largest shift outside F) and bounded one by one: max(lb - s_f, cc[l][f] -
+// ub) with Elkan's cc[l][f] = |c_l' - c_f'| (rounded down; +inf for f = l)
+// from fast_centroids - never weaker than lb - max_j s_j.
+constexpr int kBoundsChunk = 4096;   // rows per workgroup
 __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const int* __restrict__ labels, float* __restrict__ ub, float* __restrict__ lb,
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
-    long long* __restrict__ rlist, int* __restrict__ rcount, int* __restrict__ mslot,
-    const int* __restrict__ mcand_prev, long long* __restrict__ mrows, int* __restrict__ mcand,
-    int* __restrict__ multi_count) {
+    long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
+    long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
+    const int* __restrict__ fidx, int nf, int k) {
   constexpr int PER = kBoundsChunk / 256;   // rows per thread (bit masks)
   __shared__ int wsum[4];
   __shared__ int base_a, base_m;
+  __shared__ double sf_s[65];               // shifts of the fast centroids, [nf] = max
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < nf) sf_s[tid] = shift[fidx[tid]];
+  __syncthreads();
+  if (tid == 0) {
+    double m = 0.0;
+    for (int f = 0; f < nf; ++f) m = fmax(m, sf_s[f]);
+    sf_s[nf] = m;
+  }
+  __syncthreads();
   const double sm = *smax;
   const long long c0 = (long long)blockIdx.x * kBoundsChunk;
   unsigned long long act = 0, rec = 0;   // bit p: row c0 + p * 256 + tid
@@ -779,14 +794,39 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     if (i >= n) break;
     const int l = labels[i];
     const double u = (double)ub[i] + (l >= 0 ? shift[l] : 1e300);
-    const double w = (double)lb[i] - sm;
+    double w = (double)lb[i] - sm;
+    // the nf fastest centroids (excluded from sm): the better of Elkan's
+    // bound through the label, |x - c_f'| >= |c_l' - c_f'| - |x - c_l'| >=
+    // cc[l][f] - u, and the moved lower bound lb - s_f
+    if (l >= 0 && nf > 0 && w > 0.0) {   // (w <= 0: active anyway)
+      const double lb0 = (double)lb[i];
+      // cheap form first: every fast centroid is at least cmin[l] from the
+      // label and moved at most s_F = max_f s_f
+      const double wc = fmin(w, fmax((double)cc[(size_t)k * nf + l] - u, lb0 - sf_s[nf]));
+      if (wc > 0.0 && wc * wc - u * u > delta * (1.0 + 1e-9) + 1e-30) {
+        w = wc;
+      } else {   // per fast centroid (tighter)
+        const float* cl = cc + (size_t)l * nf;
+        if ((nf & 3) == 0) {
+          for (int f = 0; f < nf; f += 4) {
+            const float4 c4 = *reinterpret_cast<const float4*>(cl + f);
+            w = fmin(w, fmax((double)c4.x - u, lb0 - sf_s[f]));
+            w = fmin(w, fmax((double)c4.y - u, lb0 - sf_s[f + 1]));
+            w = fmin(w, fmax((double)c4.z - u, lb0 - sf_s[f + 2]));
+            w = fmin(w, fmax((double)c4.w - u, lb0 - sf_s[f + 3]));
+          }
+        } else {
+          for (int f = 0; f < nf; ++f) w = fmin(w, fmax((double)cl[f] - u, lb0 - sf_s[f]));
+        }
+      }
+    }
     const bool a = !(l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30);
     if (a) {
       act |= 1ull << p;
     } else {
       ub[i] = (float)u * (1.0f + 0x1p-22f);
       lb[i] = (float)w * (1.0f - 0x1p-22f);
-      if (mslot[i] >= 0) rec |= 1ull << p;
+      if (mflag[i]) rec |= 1ull << p;
     }
   }
   // block-wide exclusive scan of both per-thread counts (packed 16 | 16 bits:
@@ -822,13 +862,7 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
   int mpos = base_m + (ex >> 16);
   for (int p = 0; p < PER && rec; ++p) {
     if (rec & (1ull << p)) {
-      const long long i = c0 + (long long)p * 256 + tid;
-      const int* src = mcand_prev + (size_t)mslot[i] * (kMaxCand + 1);
-      int* dst = mcand + (size_t)mpos * (kMaxCand + 1);
-      const int c_r = src[0];
-      for (int c = 0; c <= c_r; ++c) dst[c] = src[c];
-      mrows[mpos] = i;
-      mslot[i] = mpos++;
+      mrows[mpos++] = c0 + (long long)p * 256 + tid;
       rec &= ~(1ull << p);
     }
   }
@@ -836,17 +870,84 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
 
 extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const void* shift,
                                 const void* smax, long long n, double delta, void* rlist,
-                                void* rcount, void* mslot, const void* mcand_prev, void* mrows,
-                                void* mcand, void* multi_count, void* stream) {
+                                void* rcount, const void* mflag, void* mrows, void* multi_count,
+                                const void* cc, const void* fidx, int nf, int k, void* stream) {
   if (n <= 0) return 0;
-  if (!mslot || !mcand_prev || !mrows || !mcand || !multi_count) return (int)hipErrorInvalidValue;
+  if (!mflag || !mrows || !multi_count) return (int)hipErrorInvalidValue;
+  if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(rcount, 0, sizeof(int), st);
   const long long blocks = (n + kBoundsChunk - 1) / kBoundsChunk;
   hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
                      (const int*)labels, (float*)ub, (float*)lb, (const double*)shift,
-                     (const double*)smax, n, delta, (long long*)rlist, (int*)rcount, (int*)mslot,
-                     (const int*)mcand_prev, (long long*)mrows, (int*)mcand, (int*)multi_count);
+                     (const double*)smax, n, delta, (long long*)rlist, (int*)rcount, (const int*)mflag,
+                     (long long*)mrows, (int*)multi_count,
+                     (const float*)cc, (const int*)fidx, nf, k);
+  return (int)hipGetLastError();
+}
+
+// The nf fastest centroids of an update: F = top-nf of the shifts by rank
+// (rank of c = #{j : s_j > s_c, or s_j = s_c and j < c}: unique, ties to the
+// lower index), one thread per centroid against all k shifts in LDS;
+// idx[rank] = c for rank < nf, smax_rest = the shift of rank nf.
+__global__ void __launch_bounds__(256) fast_select_kernel(const double* __restrict__ shift, int k,
+                                                          int nf, int* __restrict__ idx,
+                                                          double* __restrict__ smax_rest) {
+  extern __shared__ double sh_s[];
+  for (int j = threadIdx.x; j < k; j += 256) sh_s[j] = shift[j];
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= k) return;
+  const double v = sh_s[c];
+  int rank = 0;
+  for (int j = 0; j < k; ++j) {
+    const double u = sh_s[j];
+    rank += (u > v || (u == v && j < c)) ? 1 : 0;
+  }
+  if (rank < nf) idx[rank] = c;
+  if (rank == nf) *smax_rest = v > 0.0 ? v : 0.0;
+}
+
+// cc[j][f] = |c_j - c_idx[f]| (fp64 from the fp32 centroids, rounded down to
+// fp32), +inf for j = idx[f]; cc[k nf + j] = min_f cc[j][f].  One workgroup
+// per centroid j, wave w takes f = w, w + 4, ...
+__global__ void __launch_bounds__(256) fast_cc_kernel(const float* __restrict__ C, int k, int d,
+                                                      const int* __restrict__ idx, int nf,
+                                                      float* __restrict__ cc) {
+  __shared__ float wmin[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x;
+  float m = __builtin_inff();
+  for (int f = w; f < nf; f += 4) {
+    const int jf = idx[f];
+    double s = 0.0;
+    for (int c = lane; c < d; c += 64) {
+      const double e = (double)C[(size_t)j * d + c] - (double)C[(size_t)jf * d + c];
+      s = fma(e, e, s);
+    }
+    s = wave_sum(s);
+    const float v = j == jf ? __builtin_inff() : (float)sqrt(s) * (1.0f - 0x1p-20f) - 1e-30f;
+    if (lane == 0) cc[(size_t)j * nf + f] = v;
+    m = fminf(m, v);
+  }
+  if (lane == 0) wmin[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    cc[(size_t)k * nf + j] = fminf(fminf(wmin[0], wmin[1]), fminf(wmin[2], wmin[3]));
+}
+
+extern "C" int sq_fast_centroids(const void* shift, const void* C, int k, int d, int nf,
+                                 void* idx, void* smax_rest, void* cc, void* stream) {
+  if (k <= 0) return 0;
+  if (nf < 0 || nf > 64 || nf >= k) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (k > 8192) return (int)hipErrorInvalidValue;   // shifts staged in LDS
+  hipLaunchKernelGGL(fast_select_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256),
+                     (size_t)k * sizeof(double), st, (const double*)shift, k, nf, (int*)idx,
+                     (double*)smax_rest);
+  if (nf > 0)
+    hipLaunchKernelGGL(fast_cc_kernel, dim3((unsigned)k), dim3(256), 0, st, (const float*)C, k, d,
+                       (const int*)idx, nf, (float*)cc);
   return (int)hipGetLastError();
 }
 
@@ -877,7 +978,7 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
     const long long e = base + (lane >> 4);
     const bool live = e < cnt;
     const long long g = live ? mrows[e] : 0;
-    const int* mc = mcand + (live ? e : 0) * (kMaxCand + 1);
+    const int* mc = mcand + g * (kMaxCand + 1);
     const int c_r = live ? mc[0] : 0;
     float4 xv[F4];
     const float* xr = X + (size_t)g * DX + sub * 4 * F4;
@@ -1120,7 +1221,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
-                            void* ub, void* lb, void* mslot) {
+                            void* ub, void* lb, void* mflag) {
   constexpr int NW = kX64Waves;
   const size_t lds = kX64Ring * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4;
   auto kern = estep_x64_kernel<KSD>;
@@ -1148,7 +1249,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                      (int*)dense_count, (long long*)mrows, (int*)mcand, (int*)multi_count, n,
                      k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits,
                      (const long long*)rlist, (const int*)rcount, (float*)ub, (float*)lb,
-                     (int*)mslot);
+                     (int*)mflag);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   // the re-check: one pass over the multi list (count read on the device)
@@ -1198,22 +1299,22 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 // dense rows through the 3-pass fp32-faithful kernel in list mode, its
 // overflow rows through band_rows_f64, the multi-candidate rows through
 // recheck_rows_kernel.  counts[0] = 3-pass overflow rows, counts[1] = dense
-// rows, counts[2] = multi rows; all zero on entry.  mrows [n] (int64) and
-// mcand [n][kMaxCand + 1] (int32) hold the multi list.  mind holds -1 for rows
+// rows, counts[2] = multi rows; all zero on entry.  mrows [n] (int64) is the
+// multi list, mcand [n][kMaxCand + 1] (int32) the candidate lists BY ROW.  mind holds -1 for rows
 // whose distance the M-step (or fill_mind) computes; no inertia here.
 // Xh: fp16(alpha x) [n][d_pad]; X: fp32 [n][d_pad]; Cm: fp32 centroids
 // [k][d_pad] (zero-padded like X); C: the fp16-split operand.
 int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
                  const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
                  void* mrows, void* mcand, void* corr, void* rlist, void* rcount, void* ub,
-                 void* lb, void* mslot, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
+                 void* lb, void* mflag, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
                  int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
   if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 4096 || k > k_pad || d > d_pad)
     return (int)hipErrorInvalidValue;
-  if ((ub != nullptr) != (lb != nullptr) || (ub != nullptr) != (mslot != nullptr))
+  if ((ub != nullptr) != (lb != nullptr) || (ub != nullptr) != (mflag != nullptr))
     return (int)hipErrorInvalidValue;   // bounds need the multi-row slot map
   int aexp = 0;
   if (!(alpha > 0.0) || frexp(alpha, &aexp) != 0.5) return (int)hipErrorInvalidValue;
@@ -1230,7 +1331,7 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
                                row_offset, (int)min(n, 2147483647LL), st, rlist, rcount, ub, lb,  \
-                               mslot);                                                           \
+                               mflag);                                                           \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \

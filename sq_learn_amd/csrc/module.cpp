@@ -28,8 +28,10 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
                                            long long, const void*, void*, long long, unsigned,
                                            unsigned, unsigned, unsigned, const void*, int, void*);
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
-                                           long long, double, void*, void*, void*, const void*,
-                                           void*, void*, void*, void*);
+                                           long long, double, void*, void*, const void*, void*,
+                                           void*, const void*, const void*, int, int, void*);
+__attribute__((weak)) int sq_fast_centroids(const void*, const void*, int, int, int, void*, void*,
+                                            void*, void*);
 // gram64.hip
 __attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, long long, int, void*,
                                     int, void*);
@@ -214,14 +216,21 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
-  unsigned long long lab, ub, lb, sh, sm, rl, rc, ms, mcp, mr, mc, mcnt, st; long long n;
-  double delta;
-  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc, &ms,
-                        &mcp, &mr, &mc, &mcnt, &st))
+  unsigned long long lab, ub, lb, sh, sm, rl, rc, mf, mr, mcnt, cc, fi, st; long long n;
+  double delta; int nf, k;
+  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKiiK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc,
+                        &mf, &mr, &mcnt, &cc, &fi, &nf, &k, &st))
     return nullptr;
   CHECK(sq_bounds_filter)
-  return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(ms),
-                              P(mcp), P(mr), P(mc), P(mcnt), P(st)));
+  return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(mf),
+                              P(mr), P(mcnt), P(cc), P(fi), nf, k, P(st)));
+}
+
+static PyObject* py_fast_centroids(PyObject*, PyObject* a) {
+  unsigned long long sh, C, idx, smr, cc, st; int k, d, nf;
+  if (!PyArg_ParseTuple(a, "KKiiiKKKK", &sh, &C, &k, &d, &nf, &idx, &smr, &cc, &st)) return nullptr;
+  CHECK(sq_fast_centroids)
+  return ret(sq_fast_centroids(P(sh), P(C), k, d, nf, P(idx), P(smr), P(cc), P(st)));
 }
 
 static PyObject* py_centroid_delta(PyObject*, PyObject* a) {
@@ -492,6 +501,7 @@ static PyMethodDef methods[] = {
     {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
     {"gram64", py_gram64, METH_VARARGS, "fp64 MFMA Gram partials"},
     {"bounds_filter", py_bounds_filter, METH_VARARGS, "Hamerly pruning -> active row list"},
+    {"fast_centroids", py_fast_centroids, METH_VARARGS, "fastest centroids + Elkan distances"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},

@@ -177,6 +177,12 @@ class LloydEngine:
             self.rcount = torch.zeros(1, dtype=torch.int32, device=dev)
             self.shift_s = torch.zeros(self.k, dtype=torch.float64, device=dev)
             self.smax = torch.zeros(1, dtype=torch.float64, device=dev)
+            # the fastest centroids are bounded through the label (Elkan)
+            # instead of widening every row's lower bound by their shift
+            self.n_fast = min(int(os.environ.get("SQ_ESTEP_FAST", "16")), self.k - 1)
+            self.fast_idx = torch.zeros(max(self.n_fast, 1), dtype=torch.int32, device=dev)
+            self.fast_cc = torch.zeros(max(self.k * (self.n_fast + 1), 1), dtype=torch.float32,
+                                       device=dev)
         self.bounds_valid = False
 
     def _prepare_reduce(self):
@@ -282,7 +288,8 @@ class LloydEngine:
                     self.buf.counts.zero_()
                     K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
                                            self.shift_s, self.smax, self.delta, self.rlist,
-                                           self.rcount, self.buf)
+                                           self.rcount, self.buf, cc=self.fast_cc,
+                                           nf=self.n_fast, fidx=self.fast_idx)
                     rows = (self.rlist, self.rcount)
                 lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
                                                self.cmax2, self.k, self.delta, self.alpha, key,
@@ -513,7 +520,11 @@ class LloydEngine:
                 # next E-step's Hamerly bound update
                 torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
                 self.shift_s.mul_(1.0 + 1e-12)
-                torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
+                if self.n_fast > 0 and self.device.type == "cuda":
+                    K.fast_centroids_native(self.shift_s, self.C, self.n_fast, self.fast_idx,
+                                            self.smax, self.fast_cc)
+                else:
+                    torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
                 self.bounds_valid = True
         return self.scalars
 

@@ -180,12 +180,10 @@ class EStepBuffers:
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
         self.multi_rows = None   # certified E-step: rows sent to the fp64 re-check kernel
-        self.multi_cand = None   # ... and their candidate lists [n][1 + 16]
-        # Hamerly pruning: the previous iteration's candidate lists (the
-        # filter copies a pruned multi row's list from there) and each row's
-        # slot in the current list (-1: not a multi row)
-        self.multi_cand_prev = None
-        self.mslot = None
+        self.multi_cand = None   # ... and their candidate lists [n][1 + 16], by ROW
+        # Hamerly pruning: 1 for the rows whose candidate list (kept per row in
+        # multi_cand) is current, 0 otherwise
+        self.mflag = None
         # per-row (min distance - distance to the label) of the rows whose
         # label is not their argmin (fp64 re-check / dense / overflow rows):
         # the incremental M-step's inertia correction; None = not produced
@@ -336,39 +334,57 @@ def centroid_reduce_native(X, labels, weights, sums, counts, k, ws: ReduceWorksp
                                  nat.ptr(C_old), nat.stream_handle(X.device))
 
 
-def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf: EStepBuffers):
+def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf: EStepBuffers,
+                         cc=None, nf=0, fidx=None):
     """Hamerly pruning (csrc/estep_f32.hip bounds_filter_kernel): bounds
     moved by the centroid shifts; rows that can no longer be proven to keep
     their candidate set go to ``rlist`` (count in ``rcount``, on the device);
     pruned multi-candidate rows are appended to ``buf``'s multi list (their
-    candidates copied from the previous iteration's) for the fp64 re-check.
-    ``buf.counts`` must be zeroed before (the multi count accumulates)."""
+    per-row candidate lists stay valid) for the fp64 re-check.
+    ``buf.counts`` must be zeroed before (the multi count accumulates).
+    ``cc`` [k nf + k] fp32 / ``nf``: the fastest centroids' Elkan distances
+    (:func:`fast_centroids_native`; ``smax`` then excludes them)."""
     n = labels.numel()
     assert ub.dtype == torch.float32 and lb.dtype == torch.float32 and rlist.numel() >= n
     assert shift.dtype == torch.float64 and smax.dtype == torch.float64
-    assert buf.mslot is not None and buf.mslot.numel() >= n and buf.multi_cand_prev is not None
+    assert buf.mflag is not None and buf.mflag.numel() >= n
     rc = nat.native().bounds_filter(labels.data_ptr(), ub.data_ptr(), lb.data_ptr(),
                                     shift.data_ptr(), smax.data_ptr(), n, float(delta),
-                                    rlist.data_ptr(), rcount.data_ptr(), buf.mslot.data_ptr(),
-                                    buf.multi_cand_prev.data_ptr(), buf.multi_rows.data_ptr(),
-                                    buf.multi_cand.data_ptr(), buf.counts[2:3].data_ptr(),
+                                    rlist.data_ptr(), rcount.data_ptr(), buf.mflag.data_ptr(),
+                                    buf.multi_rows.data_ptr(), buf.counts[2:3].data_ptr(),
+                                    0 if cc is None else cc.data_ptr(),
+                                    0 if cc is None else fidx.data_ptr(),
+                                    int(nf if cc is not None else 0), int(shift.numel()),
                                     nat.stream_handle(labels.device))
     if rc:
         raise RuntimeError(f"bounds_filter failed (hip error {rc})")
 
 
+def fast_centroids_native(shift, C, nf, idx, smax_rest, cc):
+    """The nf fastest centroids of an update (top-nf shifts) -> ``idx``,
+    ``smax_rest`` = the largest shift outside them, ``cc[j][f]`` = |c_j -
+    c_idx[f]| rounded down (+inf on j = idx[f]), ``cc[k nf + j]`` = min_f
+    cc[j][f]; csrc/estep_f32.hip."""
+    k, d = C.shape
+    assert C.dtype == torch.float32 and C.is_contiguous() and shift.dtype == torch.float64
+    assert 0 <= nf < k and idx.numel() >= nf and cc.numel() >= k * (nf + 1)
+    rc = nat.native().fast_centroids(shift.data_ptr(), C.data_ptr(), k, d, int(nf), idx.data_ptr(),
+                                     smax_rest.data_ptr(), cc.data_ptr(),
+                                     nat.stream_handle(C.device))
+    if rc:
+        raise RuntimeError(f"fast_centroids failed (hip error {rc})")
+
+
 def ensure_multi_buffers(buf: EStepBuffers, n, device, bounds=False):
     """Allocate the certified E-step's row lists (and, with ``bounds``, the
-    double-buffered candidate lists + slot map of the Hamerly pruning)."""
+    per-row multi flag of the Hamerly pruning)."""
     if buf.dense_rows is None or buf.dense_rows.numel() < n:
         buf.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=device)
     if buf.multi_rows is None or buf.multi_rows.numel() < n:
         buf.multi_rows = torch.empty(max(n, 1), dtype=torch.int64, device=device)
         buf.multi_cand = torch.empty((max(n, 1), 17), dtype=torch.int32, device=device)
-        buf.multi_cand_prev = None
-    if bounds and (buf.multi_cand_prev is None or buf.mslot is None or buf.mslot.numel() < n):
-        buf.multi_cand_prev = torch.empty_like(buf.multi_cand)
-        buf.mslot = torch.full((max(n, 1),), -1, dtype=torch.int32, device=device)
+    if bounds and (buf.mflag is None or buf.mflag.numel() < n):
+        buf.mflag = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
 
 
 def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWorkspace, perm2,
@@ -596,8 +612,7 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     M-step's row pass or ``fill_mind_native``).  No host sync.
 
     ``bounds`` = (ub, lb) fp32 [n]: the kernel writes each processed row's
-    Hamerly bounds and multi-list slot (``buf.mslot``), and the candidate
-    lists are swapped with ``buf.multi_cand_prev`` afterwards; ``rows`` =
+    Hamerly bounds and multi flag (``buf.mflag``); ``rows`` =
     (rlist int64 [n], rcount int32 [1]): process only the listed rows (list
     mode, count on the device; the filter already started this iteration's
     multi list, so ``zero_counts`` is False)."""
@@ -624,12 +639,10 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
                            0 if rows is None else rows[1].data_ptr(),
                            0 if bounds is None else bounds[0].data_ptr(),
                            0 if bounds is None else bounds[1].data_ptr(),
-                           0 if bounds is None else buf.mslot.data_ptr(),
+                           0 if bounds is None else buf.mflag.data_ptr(),
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)
-    if bounds is not None:   # this iteration's lists are the next one's "previous"
-        buf.multi_cand, buf.multi_cand_prev = buf.multi_cand_prev, buf.multi_cand
     return buf.labels, buf.mind
 
 
