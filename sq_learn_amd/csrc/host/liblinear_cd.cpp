@@ -6,7 +6,10 @@
 // seeded by the caller and the Lemire bounded integer of
 // ``svm/src/newrand/newrand.h`` - so iterates, n_iter and the returned w are
 // the reference's.  Rows are dense (row-major, bias column appended by the
-// caller when fitting an intercept).
+// caller when fitting an intercept).  Also the Crammer-Singer multi-class
+// dual (``Solver_MCSVM_CS``, linear.cpp:493-787): per-instance sub-problems
+// over the class scores with per-class shrinking.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <random>
@@ -201,6 +204,146 @@ int sqh_linear_svr_dual(const double* X, long long l, long long d, const double*
       continue;
     }
     Gmax_old = Gmax_new;
+  }
+  return iter;
+}
+
+}  // extern "C"
+
+// Crammer-Singer multi-class SVM dual (reference linear.cpp:493-787):
+//   min_a 0.5 sum_m |w_m|^2 + sum_{i, m != y_i} a_i^m,  w_m = sum_i a_i^m x_i,
+//   sum_m a_i^m = 0,  a_i^m <= C_i [m = y_i]  (C_i = W_i C_{y_i}),
+// solved one instance at a time (all its class scores at once, the closed-
+// form sub-problem below) in a random order, with the reference's per-class
+// and per-instance shrinking and its stopping rule.  y: class ids 0..K-1
+// (rows grouped by class).  w: [d][K] feature-major, like liblinear's model.
+namespace {
+
+struct McsCs {
+  int K;
+  std::vector<double> D;
+  explicit McsCs(int k) : K(k), D(k) {}
+  // new scores of one instance: the threshold beta of the sorted shifted
+  // gradients, then a^m = min(bound_m, (beta - B_m) / A)
+  void sub_problem(double A, int yi, double Cy, int na, const double* B, double* out) {
+    for (int m = 0; m < na; ++m) D[m] = B[m];
+    if (yi < na) D[yi] += A * Cy;
+    std::sort(D.begin(), D.begin() + na, [](double a, double b) { return a > b; });
+    double beta = D[0] - A * Cy;
+    int r = 1;
+    while (r < na && beta < r * D[r]) beta += D[r++];
+    beta /= r;
+    for (int m = 0; m < na; ++m) {
+      const double v = (beta - B[m]) / A;
+      out[m] = m == yi ? std::min(Cy, v) : std::min(0.0, v);
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int sqh_linear_mcsvm_cs(const double* X, long long l, long long d, const int* y, int K,
+                        const double* Cvec, double eps, int max_iter, void* stream, double* w) {
+  Rng& rng = *(Rng*)stream;
+  McsCs sp(K);
+  std::vector<double> alpha((size_t)l * K, 0.0), QD(l), G(K), B(K), anew(K), dval(K);
+  std::vector<int> aidx((size_t)l * K), index(l), yidx(l), na_i(l, K), dind(K);
+  for (int64_t k = 0; k < d * K; ++k) w[k] = 0;
+  for (int64_t i = 0; i < l; ++i) {
+    for (int m = 0; m < K; ++m) aidx[(size_t)i * K + m] = m;
+    QD[i] = dot(X + i * d, X + i * d, d);
+    yidx[i] = y[i];
+    index[i] = (int)i;
+  }
+  // a score sits at its bound with a gradient below every free one: shrink
+  auto shrunk = [&](int64_t i, int m, double a, double minG) {
+    const double bound = m == yidx[i] ? Cvec[i] : 0.0;
+    return a == bound && G[m] < minG;
+  };
+  int64_t active = l;
+  double eps_shrink = std::max(10.0 * eps, 1.0);
+  bool from_all = true;
+  int iter = 0;
+  while (iter < max_iter) {
+    double stopping = -kInf;
+    for (int64_t i = 0; i < active; ++i) {
+      int64_t j = i + rng.bounded((uint32_t)(active - i));
+      std::swap(index[i], index[j]);
+    }
+    for (int64_t s = 0; s < active; ++s) {
+      const int64_t i = index[s];
+      const double A = QD[i];
+      if (!(A > 0)) continue;
+      double* ai = &alpha[(size_t)i * K];
+      int* ix = &aidx[(size_t)i * K];
+      const double* xi = X + i * d;
+      int na = na_i[i];
+      for (int m = 0; m < na; ++m) G[m] = 1.0;
+      if (yidx[i] < na) G[yidx[i]] = 0.0;
+      for (int64_t f = 0; f < d; ++f) {
+        const double v = xi[f];
+        const double* wf = w + f * K;
+        for (int m = 0; m < na; ++m) G[m] += wf[ix[m]] * v;
+      }
+      double minG = kInf, maxG = -kInf;
+      for (int m = 0; m < na; ++m) {
+        if (ai[ix[m]] < 0 && G[m] < minG) minG = G[m];
+        if (G[m] > maxG) maxG = G[m];
+      }
+      if (yidx[i] < na && ai[y[i]] < Cvec[i] && G[yidx[i]] < minG) minG = G[yidx[i]];
+      for (int m = 0; m < na_i[i]; ++m) {
+        if (!shrunk(i, m, ai[ix[m]], minG)) continue;
+        --na_i[i];
+        while (na_i[i] > m) {
+          const int t = na_i[i];
+          if (!shrunk(i, t, ai[ix[t]], minG)) {
+            std::swap(ix[m], ix[t]);
+            std::swap(G[m], G[t]);
+            if (yidx[i] == t) yidx[i] = m;
+            else if (yidx[i] == m) yidx[i] = t;
+            break;
+          }
+          --na_i[i];
+        }
+      }
+      na = na_i[i];
+      if (na <= 1) {
+        --active;
+        std::swap(index[s], index[active]);
+        --s;
+        continue;
+      }
+      if (maxG - minG <= 1e-12) continue;
+      stopping = std::max(stopping, maxG - minG);
+      for (int m = 0; m < na; ++m) B[m] = G[m] - A * ai[ix[m]];
+      sp.sub_problem(A, yidx[i], Cvec[i], na, B.data(), anew.data());
+      int nz = 0;
+      for (int m = 0; m < na; ++m) {
+        const double dl = anew[m] - ai[ix[m]];
+        ai[ix[m]] = anew[m];
+        if (std::fabs(dl) >= 1e-12) {
+          dind[nz] = ix[m];
+          dval[nz++] = dl;
+        }
+      }
+      for (int64_t f = 0; f < d; ++f) {
+        const double v = xi[f];
+        double* wf = w + f * K;
+        for (int m = 0; m < nz; ++m) wf[dind[m]] += dval[m] * v;
+      }
+    }
+    ++iter;
+    if (stopping < eps_shrink) {
+      if (stopping < eps && from_all) break;
+      active = l;
+      for (int64_t i = 0; i < l; ++i) na_i[i] = K;
+      eps_shrink = std::max(eps_shrink / 2, eps);
+      from_all = true;
+    } else {
+      from_all = false;
+    }
   }
   return iter;
 }

@@ -96,8 +96,22 @@ def _svc_primal_l1(X, y, C, tol, max_iter):
     return w, it
 
 
+def _svc_crammer_singer(X, y, Cvec, K, tol, stream, max_iter=100000):
+    """Crammer-Singer multi-class dual (host native, ``sqh_linear_mcsvm_cs``):
+    returns (coef rows [K, d], iterations)."""
+    X = np.ascontiguousarray(X)
+    yi = np.ascontiguousarray(y, dtype=np.int32)
+    C = np.ascontiguousarray(Cvec, dtype=np.float64)
+    w = np.zeros(X.shape[1] * K)
+    it = _host.lib().sqh_linear_mcsvm_cs(X.ctypes.data, X.shape[0], X.shape[1], yi.ctypes.data,
+                                         int(K), C.ctypes.data, float(tol), int(max_iter),
+                                         stream.h, w.ctypes.data)
+    return w.reshape(X.shape[1], K).T.copy(), it
+
+
 class LinearSVC(ClassifierMixin, BaseEstimator):
-    """Linear support vector classification (one-vs-rest, liblinear)."""
+    """Linear support vector classification (one-vs-rest or Crammer-Singer,
+    liblinear)."""
 
     def __init__(self, penalty="l2", loss="squared_hinge", *, dual=True, tol=1e-4, C=1.0,
                  multi_class="ovr", fit_intercept=True, intercept_scaling=1, class_weight=None,
@@ -144,9 +158,6 @@ class LinearSVC(ClassifierMixin, BaseEstimator):
         seed = rnd.randint(np.iinfo("i").max)
         Xa = _augment(X, self.fit_intercept, self.intercept_scaling)
         solver = self._solver()
-        if solver == "cs":
-            raise NotImplementedError("multi_class='crammer_singer' is not implemented; use "
-                                      "multi_class='ovr'")
         # liblinear groups samples by (sorted) class, original order within a class
         perm = np.argsort(y_ind, kind="stable")
         Xp, yp, swp = Xa[perm], y_ind[perm], sw[perm]
@@ -155,7 +166,12 @@ class LinearSVC(ClassifierMixin, BaseEstimator):
         models = []
         n_iter = 0
         stream = _MTStream(seed)
-        if K == 2:
+        tasks = []
+        if solver == "cs":
+            # one joint problem over all classes; the reference runs it with
+            # the solver's own iteration cap (linear.cpp:496, :2530)
+            raw, n_iter = _svc_crammer_singer(Xp, yp, swp * weighted_C[yp], K, self.tol, stream)
+        elif K == 2:
             tasks = [(np.where(yp == 1, 1.0, -1.0), weighted_C[1], weighted_C[0])]
         else:
             tasks = [(np.where(yp == k, 1.0, -1.0), weighted_C[k], self.C) for k in range(K)]
@@ -170,13 +186,19 @@ class LinearSVC(ClassifierMixin, BaseEstimator):
                 w, it = _svc_primal_l1(Xp, ysub, Cvec, self.tol, self.max_iter)
             models.append(w)
             n_iter = max(n_iter, it)
-        raw = np.asarray(models)
+        if solver != "cs":
+            raw = np.asarray(models)
         if self.fit_intercept:
             self.coef_ = raw[:, :-1]
             self.intercept_ = self.intercept_scaling * raw[:, -1]
         else:
             self.coef_ = raw
             self.intercept_ = np.zeros(raw.shape[0])
+        if solver == "cs" and K == 2:
+            # binary Crammer-Singer: the score difference (reference
+            # svm/_classes.py:242-246)
+            self.coef_ = (self.coef_[1] - self.coef_[0]).reshape(1, -1)
+            self.intercept_ = np.array([self.intercept_[1] - self.intercept_[0]])
         self.n_iter_ = n_iter
         if n_iter >= self.max_iter:
             warnings.warn("Liblinear failed to converge, increase the number of iterations.",

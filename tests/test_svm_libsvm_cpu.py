@@ -79,3 +79,24 @@ def test_linear_svc_primal_and_svr():
             b = sks.LinearSVR(random_state=0, dual=True, **kw).fit(Xr, yr)
             np.testing.assert_allclose(a.coef_, b.coef_, atol=1e-10)
             assert a.n_iter_ == b.n_iter_
+
+
+@pytest.mark.parametrize("data", [(X2, y2), (X3, y3)])
+@pytest.mark.parametrize("kw", [dict(), dict(C=0.1, class_weight="balanced"),
+                                dict(fit_intercept=False, tol=1e-3)])
+def test_linear_svc_crammer_singer_is_bit_compatible(data, kw):
+    """Crammer-Singer dual (linear.cpp:493-787, host-native
+    sqh_linear_mcsvm_cs): same random order and shrinking -> same w.  The
+    installed scikit-learn's n_iter_ for this solver is not comparable
+    (reported from an uninitialised buffer), so only coefficients are
+    pinned; binary problems keep the score difference (_classes.py:242)."""
+    X, y = data
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        a = LinearSVC(multi_class="crammer_singer", random_state=0, **kw).fit(X, y)
+        b = sks.LinearSVC(multi_class="crammer_singer", random_state=0, **kw).fit(X, y)
+    assert a.coef_.shape == b.coef_.shape
+    np.testing.assert_allclose(a.coef_, b.coef_, atol=1e-10)
+    np.testing.assert_allclose(a.intercept_, b.intercept_, atol=1e-10)
+    np.testing.assert_array_equal(a.predict(X), b.predict(X))
+    assert a.n_iter_ >= 1
