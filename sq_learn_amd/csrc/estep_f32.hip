@@ -958,8 +958,9 @@ extern "C" int sq_fast_centroids(const void* shift, const void* C, int k, int d,
 // as band.h: min, members {d <= min + delta}, the member of kappa rank
 // r = band_rank(u, |band|), kappa(j) = (j mod 32, j div 32).  A wave takes 4
 // list rows (16 lanes each, 16 features per lane at d = 256) and keeps its
-// row in registers across that row's candidates; short kernel, many waves
-// per CU, so the row / centroid gathers overlap.
+// row in registers across that row's candidates (two at a time); lane t of a
+// row's group then holds candidate t, so min, band and kappa ranks are
+// group-wide shuffles rather than per-lane O(16^2) loops.
 template <int DX>
 __global__ void __launch_bounds__(256) recheck_rows_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
@@ -971,71 +972,76 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
   const int lane = threadIdx.x & 63;
   const int sub = lane & (LPR - 1);
+  const int gbase = lane & ~(LPR - 1);
+  const unsigned long long gmask = 0xffffull << gbase;
   const long long cnt = min((long long)*multi_count, cap);
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  auto cdist = [&](const float4 (&xv)[F4], int j) -> double {
+    const float* cr = Cm + (size_t)j * DX + sub * 4 * F4;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < F4; ++q) {
+      if (sub * 4 * F4 + 4 * q < DX) {
+        const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * q);
+        const double e0 = (double)xv[q].x - (double)cv.x, e1 = (double)xv[q].y - (double)cv.y;
+        const double e2 = (double)xv[q].z - (double)cv.z, e3 = (double)xv[q].w - (double)cv.w;
+        s = fma(e0, e0, fma(e1, e1, fma(e2, e2, fma(e3, e3, s))));
+      }
+    }
+    return s;
+  };
   for (long long base = gw * 4; base < cnt; base += nw * 4) {
     const long long e = base + (lane >> 4);
     const bool live = e < cnt;
     const long long g = live ? mrows[e] : 0;
     const int* mc = mcand + g * (kMaxCand + 1);
     const int c_r = live ? mc[0] : 0;
+    // lane sub of the row's group holds candidate sub (index, distance)
+    const bool mine = sub < c_r;
+    const int myj = mine ? mc[1 + sub] : 0;
     float4 xv[F4];
     const float* xr = X + (size_t)g * DX + sub * 4 * F4;
 #pragma unroll
     for (int q = 0; q < F4; ++q)
       xv[q] = (sub * 4 * F4 + 4 * q < DX) ? *reinterpret_cast<const float4*>(xr + 4 * q)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-    double dl[kMaxCand];
-    int cl[kMaxCand];
     int cmax = c_r;
 #pragma unroll
     for (int o = 16; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
-    for (int c = 0; c < cmax; ++c) {            // wave-uniform trip count
-      const int j = c < c_r ? mc[1 + c] : 0;
-      const float* cr = Cm + (size_t)j * DX + sub * 4 * F4;
-      double s = 0.0;
+    double dme = __builtin_inf();
+    // candidates in pairs: both centroid fragments in flight at once
+    for (int c = 0; c < cmax; c += 2) {            // wave-uniform trip count
+      const int j0 = __shfl(myj, gbase + c, 64);
+      const int j1 = __shfl(myj, gbase + min(c + 1, LPR - 1), 64);
+      double s0 = cdist(xv, c < c_r ? j0 : 0);
+      double s1 = cdist(xv, c + 1 < c_r ? j1 : 0);
 #pragma unroll
-      for (int q = 0; q < F4; ++q) {
-        if (sub * 4 * F4 + 4 * q < DX) {
-          const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * q);
-          const double e0 = (double)xv[q].x - (double)cv.x, e1 = (double)xv[q].y - (double)cv.y;
-          const double e2 = (double)xv[q].z - (double)cv.z, e3 = (double)xv[q].w - (double)cv.w;
-          s = fma(e0, e0, fma(e1, e1, fma(e2, e2, fma(e3, e3, s))));
-        }
+      for (int o = 1; o < LPR; o <<= 1) {
+        s0 += __shfl_xor(s0, o, 64);
+        s1 += __shfl_xor(s1, o, 64);
       }
-#pragma unroll
-      for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o, 64);
-#pragma unroll
-      for (int t = 0; t < kMaxCand; ++t)
-        if (t == c) { dl[t] = s; cl[t] = j; }
+      if (sub == c) dme = s0;
+      if (sub == c + 1) dme = s1;
     }
+    // delta-band over the group's lanes (band.h's rule): min, members
+    // {d <= min + delta}, the member of kappa rank r = band_rank(u, |band|)
+    double dmin = mine ? dme : __builtin_inf();
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) dmin = fmin(dmin, __shfl_xor(dmin, o, 64));
+    const bool inb = mine && dme <= dmin + delta;
+    const unsigned long long bm = __ballot(inb) & gmask;
+    const int b = __popcll(bm);
+    const int kme = inb ? (((myj & 31) << 20) | (myj >> 5)) : 0x7fffffff;
+    int rank = 0;
+#pragma unroll
+    for (int t = 0; t < LPR; ++t) rank += __shfl(kme, gbase + t, 64) < kme ? 1 : 0;
+    const int r = b > 0 ? band_rank(band_u(key, row_offset + g), b) : 0;
+    const unsigned long long pm = __ballot(inb && rank == r) & gmask;
+    const int plane = pm ? __ffsll((long long)pm) - 1 : gbase;
+    const int pick = __shfl(myj, plane, 64);
+    const double dpick = __shfl(dme, plane, 64);
     if (live && sub == 0) {
-      double dmin = dl[0];
-#pragma unroll
-      for (int c = 1; c < kMaxCand; ++c)
-        if (c < c_r) dmin = fmin(dmin, dl[c]);
-      const double thr = dmin + delta;
-      int b = 0;
-#pragma unroll
-      for (int c = 0; c < kMaxCand; ++c) b += (c < c_r && dl[c] <= thr) ? 1 : 0;
-      const int r = band_rank(band_u(key, row_offset + g), b);
-      int pick = cl[0];
-      double dpick = dl[0];
-#pragma unroll
-      for (int c = 0; c < kMaxCand; ++c) {
-        if (c < c_r && dl[c] <= thr) {
-          const int jc = cl[c];
-          const int kc = ((jc & 31) << 20) | (jc >> 5);
-          int rank = 0;
-#pragma unroll
-          for (int c2 = 0; c2 < kMaxCand; ++c2) {
-            const int j2 = cl[c2];
-            rank += (c2 < c_r && dl[c2] <= thr && (((j2 & 31) << 20) | (j2 >> 5)) < kc) ? 1 : 0;
-          }
-          if (rank == r) { pick = jc; dpick = dl[c]; }
-        }
-      }
       labels[g] = pick;
       mind[g] = (float)dmin;
       if (corr) corr[g] = (float)(dmin - dpick);

@@ -5,12 +5,13 @@ Loss and gradient are evaluated on the resolved device in fp64 (two GEMMs
 per evaluation: X W^T forward, residual^T X backward, a fused
 log-sum-exp); the quasi-Newton driver is scipy's L-BFGS-B on the host with
 the reference's options (gtol = tol, maxiter = max_iter), so the iterates
-follow the reference's lbfgs solver.  'newton-cg', 'sag', 'saga' and
-'liblinear' with an l2 / none penalty solve the same strictly convex problem
-with this driver; l1 / elastic-net penalties use an accelerated proximal
-gradient (FISTA with backtracking) on the device, minimising
-sum_i w_i loss_i + (1 - r) / (2C) ||W||^2 + r / C ||W||_1 (the saga
-objective up to the 1/n scaling)."""
+follow the reference's lbfgs solver.  'sag' / 'saga' run the reference's
+stochastic average gradient epochs (host-native, :mod:`._sag`; l1 and
+elastic-net through SAGA's proximal step).  'newton-cg' and 'liblinear'
+with an l2 / none penalty solve the same strictly convex problem with the
+L-BFGS driver; liblinear's l1 penalty uses an accelerated proximal gradient
+(FISTA with backtracking) on the device, minimising
+sum_i w_i loss_i + (1 - r) / (2C) ||W||^2 + r / C ||W||_1."""
 
 import numbers
 import warnings
@@ -217,7 +218,9 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
                 return _fista(obj, w0, l1, self.tol, self.max_iter)
             return _lbfgs(obj, w0, self.tol, self.max_iter)
 
-        if multi == "multinomial":
+        if self.solver in ("sag", "saga"):
+            W = self._fit_sag(X, y, sw, alpha, l1, multi, warm)
+        elif multi == "multinomial":
             Y = (y[:, None] == self.classes_[None, :]).astype(np.float64)
             w0 = np.zeros((n_classes, nf1))
             if warm is not None:
@@ -254,6 +257,45 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
             self.intercept_ = np.zeros(W.shape[0])
         self._multi = multi
         return self
+
+    def _fit_sag(self, X, y, sw, alpha, beta, multi, warm):
+        """The reference's stochastic average gradient path (``_logistic.py:
+        784-805``, :mod:`._sag`): one 'log' problem per class on {-1, +1}
+        targets (OvR) or one 'multinomial' problem on label-encoded targets;
+        returns the coefficient rows [n_rows, n_features (+1)]."""
+        from ._sag import sag_solver
+        n_classes = len(self.classes_)
+        nf1 = X.shape[1] + int(self.fit_intercept)
+        max_sq = float(np.einsum("ij,ij->i", X, X).max())
+        saga = self.solver == "saga"
+        if multi == "multinomial":
+            w0 = np.zeros((n_classes, nf1))
+            if warm is not None:
+                w0[-warm.shape[0]:, :warm.shape[1]] = warm
+                if self.fit_intercept:
+                    w0[-warm.shape[0]:, -1] = self.intercept_
+            target = np.searchsorted(self.classes_, y).astype(np.float64)
+            coef, it, _ = sag_solver(X, target, sw, "multinomial", alpha, beta, self.max_iter,
+                                     self.tol, self.verbose, self.random_state, False, max_sq,
+                                     {"coef": w0.T}, is_saga=saga)
+            self.n_iter_ = np.array([it], dtype=np.int32)
+            return coef[1][None, :] if n_classes == 2 else coef
+        pos = self.classes_[1:] if n_classes == 2 else self.classes_
+        rows, its = [], []
+        for k, c in enumerate(pos):
+            w0 = np.zeros(nf1)
+            if warm is not None:
+                w0[:warm.shape[1]] = warm[k]
+                if self.fit_intercept:
+                    w0[-1] = self.intercept_[k]
+            t = np.where(y == c, 1.0, -1.0)
+            coef, it, _ = sag_solver(X, t, sw, "log", alpha, beta, self.max_iter, self.tol,
+                                     self.verbose, self.random_state, False, max_sq,
+                                     {"coef": w0[:, None]}, is_saga=saga)
+            rows.append(coef)
+            its.append(it)
+        self.n_iter_ = np.asarray(its, dtype=np.int32)
+        return np.vstack(rows)
 
     def predict_proba(self, X):
         ovr = (self.multi_class == "ovr" or

@@ -6,7 +6,9 @@ form otherwise, and ``solver='svd'`` / ``RidgeCV`` from one thin SVD of
 the centred design (every alpha re-uses it; leave-one-out errors come from
 the closed-form hat-matrix diagonal with an unpenalised intercept).
 ``solver`` values of the reference ('auto', 'cholesky', 'svd', 'lsqr',
-'sparse_cg', 'sag', 'saga') are accepted; iterative ones solve the same
+'sparse_cg', 'sag', 'saga') are accepted: 'sag' / 'saga' run the reference's
+stochastic average gradient epochs (:mod:`._sag`, sample weights passed to
+the solver, ``n_iter_`` per target); the other iterative ones solve the same
 strongly convex problem exactly (normal equations)."""
 
 import numpy as np
@@ -48,6 +50,28 @@ def _solve(X, y, alpha, solver, device):
     return torch.stack(coefs)
 
 
+def _solve_sag(X, y, alpha, sw, solver, max_iter, tol, random_state, fit_intercept=False):
+    """Per-target SAG / SAGA on the squared loss (reference ``_ridge.py:
+    477-501``): (coef [n_targets, d], n_iter [n_targets], intercept)."""
+    from ._sag import sag_solver
+    Y = y[:, None] if y.ndim == 1 else y
+    n, d = X.shape
+    alphas = np.broadcast_to(np.asarray(alpha, dtype=np.float64).ravel(), (Y.shape[1],))
+    max_sq = float(np.einsum("ij,ij->i", X, X).max()) if n else 0.0
+    coef = np.empty((Y.shape[1], d))
+    n_iter = np.empty(Y.shape[1], dtype=np.int32)
+    intercept = np.zeros(Y.shape[1])
+    for t in range(Y.shape[1]):
+        init = {"coef": np.zeros((d + int(fit_intercept), 1))}
+        c, it, _ = sag_solver(X, Y[:, t], sw, "squared", alphas[t], 0.0, max_iter, tol, 0,
+                              random_state, False, max_sq, init, is_saga=solver == "saga")
+        coef[t] = c[:d]
+        if fit_intercept:
+            intercept[t] = c[d]
+        n_iter[t] = it
+    return coef, n_iter, intercept
+
+
 def ridge_regression(X, y, alpha, *, sample_weight=None, solver="auto", max_iter=None, tol=1e-3,
                      verbose=0, random_state=None, return_n_iter=False, return_intercept=False,
                      check_input=True, device=None):
@@ -55,6 +79,21 @@ def ridge_regression(X, y, alpha, *, sample_weight=None, solver="auto", max_iter
     X = _as_dense64(X)
     y = np.asarray(y, dtype=np.float64)
     intercept = 0.0
+    if solver in ("sag", "saga"):
+        if return_intercept and solver != "sag":
+            raise ValueError("In Ridge, only 'sag' solver can directly fit the intercept. Please "
+                             "change solver to 'sag' or set return_intercept=False.")
+        sw = _check_sample_weight(sample_weight, X.shape[0])
+        coef, n_iter, icpt = _solve_sag(X, y, alpha, sw, solver, max_iter, tol, random_state,
+                                        fit_intercept=return_intercept)
+        if y.ndim == 1:
+            coef, icpt = coef.ravel(), icpt[0]
+        out = (coef,)
+        if return_n_iter:
+            out += (n_iter,)
+        if return_intercept:
+            out += (icpt,)
+        return out[0] if len(out) == 1 else out
     if return_intercept:
         X, y, X_offset, y_offset, _ = _preprocess_data(X, y, True, sample_weight=sample_weight)
     sw = _check_sample_weight(sample_weight, X.shape[0])
@@ -98,6 +137,14 @@ class _BaseRidge(LinearModel):
         sw = _check_sample_weight(sample_weight, X.shape[0], X.dtype)
         X, y, X_offset, y_offset, X_scale = _preprocess_data(
             X, y, self.fit_intercept, self.normalize, copy=self.copy_X, sample_weight=sw)
+        if self.solver in ("sag", "saga"):
+            # the solver takes the weights itself (reference _ridge.py:430-434)
+            coef, n_iter, _ = _solve_sag(X, y, self.alpha, sw, self.solver, self.max_iter,
+                                         self.tol, self.random_state)
+            self.coef_ = coef.ravel() if y.ndim == 1 else coef
+            self.n_iter_ = n_iter
+            self._set_intercept(X_offset, y_offset, X_scale)
+            return self
         if sw is not None:
             X, y = _rescale_data(X, y, sw)
         coef = _solve(X, y, self.alpha, "svd" if self.solver == "svd" else "cholesky",

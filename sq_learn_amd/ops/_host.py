@@ -63,6 +63,7 @@ _SIGS = {
     "sqh_linear_svc_dual": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _I, _P, _P, _P]),
     "sqh_linear_svr_dual": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _D, _I, _P, _P]),
     "sqh_linear_mcsvm_cs": (_I, [_P, _LL, _LL, _P, _I, _P, _D, _I, _P, _P]),
+    "sqh_sag": (_I, [_P, _P, _P, _LL, _LL, _I, _I, _D, _D, _D, _I, _D, _I, _D, _I, _U, _P, _P]),
     "sqh_mt_new": (_P, [_U]),
     "sqh_sgd_plain": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _U, _P]),
     "sqh_mt_free": (None, [_P]),
