@@ -20,6 +20,7 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--delta", type=float, default=0.5)
 ap.add_argument("--what", default="estep", choices=["estep", "reduce", "both"])
 ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16", "x64"])
+ap.add_argument("--bounds", action="store_true", help="x64: write the Hamerly bounds too")
 a = ap.parse_args()
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
@@ -46,11 +47,14 @@ def run_estep():
     if a.prec == "bf16":
         K.estep_native(X, Cb, cn, xn, a.k, a.delta, key, 0, buf)
     elif a.prec == "x64":
-        K.estep_x64_native(Xh, X, Cop, C, xn, cmax2, a.k, a.delta, alpha, key, 0, buf)
+        K.estep_x64_native(Xh, X, Cop, C, xn, cmax2, a.k, a.delta, alpha, key, 0, buf,
+                           bounds=bnd)
     else:
         K.estep_f32_native(X, Cop, xn, C, a.k, a.delta, alpha, key, 0, buf)
 
 buf = K.EStepBuffers(a.n, dev)
+bnd = ((torch.zeros(a.n, device=dev), torch.zeros(2 * a.n, device=dev))
+       if a.bounds and a.prec == "x64" else None)
 ws = K.ReduceWorkspace(a.n, a.k, dev).set_scale(float(X.float().abs().max()), a.n)
 sums = torch.zeros(a.k, a.d, dtype=torch.float64, device=dev)
 cnt = torch.zeros(a.k, dtype=torch.float64, device=dev)

@@ -9,7 +9,7 @@ for rep in 1 2; do
     case $v in
       cur) ;;
       env:*) export "${v#env:}" ;;
-      *) export SQ_NATIVE_VARIANT=build/variants/_C_$v.so ;;
+      *) export SQ_NATIVE_VARIANT=sq_learn_amd/_variants/_C_$v.so ;;
     esac
     echo -n "$v: "; timeout -k 10 120 python benchmarks/estep_micro.py --what $what --iters 20 $AB_ARGS 2>&1 | grep $what || exit 1
   done

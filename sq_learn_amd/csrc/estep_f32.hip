@@ -444,7 +444,7 @@ constexpr int kX64Waves = SQ_X64_NW;   // waves per workgroup (2 per SIMD at 8)
 #endif
 constexpr int kX64Ring = SQ_X64_RING;  // centroid-tile LDS slots (3: 2 tiles in flight)
 template <int KSD>
-__global__ void __launch_bounds__(512) estep_x64_kernel(
+__global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     const _Float16* __restrict__ Xh, const float* __restrict__ X, const _Float16* __restrict__ C,
     const float* __restrict__ Cm, const float* __restrict__ xn, const float* __restrict__ cmax2_p,
     int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ dense_rows,
@@ -966,7 +966,7 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
     float* __restrict__ mind, long long cap, double delta, RngKey key, long long row_offset,
-    float* __restrict__ corr, float* __restrict__ ub) {
+    float* __restrict__ corr, float* __restrict__ ub, const unsigned char* __restrict__ xflag) {
   constexpr int LPR = 16;                  // lanes per row
   constexpr int FPL = DX / LPR;            // features per lane (DX >= 64) or fewer
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
@@ -978,12 +978,12 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
   auto cdist = [&](const float4 (&xv)[F4], int j) -> double {
-    const float* cr = Cm + (size_t)j * DX + sub * 4 * F4;
+    const float* cr = Cm + (size_t)j * DX;
     double s = 0.0;
 #pragma unroll
     for (int q = 0; q < F4; ++q) {
-      if (sub * 4 * F4 + 4 * q < DX) {
-        const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * q);
+      if (4 * (q * LPR + sub) < DX) {   // group-contiguous float4s: coalesced
+        const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * (q * LPR + sub));
         const double e0 = (double)xv[q].x - (double)cv.x, e1 = (double)xv[q].y - (double)cv.y;
         const double e2 = (double)xv[q].z - (double)cv.z, e3 = (double)xv[q].w - (double)cv.w;
         s = fma(e0, e0, fma(e1, e1, fma(e2, e2, fma(e3, e3, s))));
@@ -991,9 +991,7 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
     }
     return s;
   };
-  for (long long base = gw * 4; base < cnt; base += nw * 4) {
-    const long long e = base + (lane >> 4);
-    const bool live = e < cnt;
+  auto process = [&](long long e, bool live) {
     const long long g = live ? mrows[e] : 0;
     const int* mc = mcand + g * (kMaxCand + 1);
     const int c_r = live ? mc[0] : 0;
@@ -1001,11 +999,12 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
     const bool mine = sub < c_r;
     const int myj = mine ? mc[1 + sub] : 0;
     float4 xv[F4];
-    const float* xr = X + (size_t)g * DX + sub * 4 * F4;
+    const float* xr = X + (size_t)g * DX;
 #pragma unroll
     for (int q = 0; q < F4; ++q)
-      xv[q] = (sub * 4 * F4 + 4 * q < DX) ? *reinterpret_cast<const float4*>(xr + 4 * q)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      xv[q] = (4 * (q * LPR + sub) < DX)
+                  ? *reinterpret_cast<const float4*>(xr + 4 * (q * LPR + sub))
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
     int cmax = c_r;
 #pragma unroll
     for (int o = 16; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
@@ -1049,6 +1048,139 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
       // filter moves it by the label's shift)
       if (ub) ub[g] = (float)sqrt(dpick) * (1.0f + 0x1p-20f);
     }
+  };
+  if (!xflag) {   // contiguous slice per wave (page locality, see the screen)
+    const long long per = ((cnt + nw - 1) / nw + 3) / 4 * 4;
+    const long long e_end = min(cnt, (gw + 1) * per);
+    for (long long base = gw * per; base < e_end; base += 4) {
+      const long long e = base + (lane >> 4);
+      process(e, e < e_end);
+    }
+    return;
+  }
+  // flagged entries only (the fp32 screen's leftovers): a wave scans 64
+  // list entries, its 4 row groups take the flagged ones 4 at a time
+  const int q = lane >> 4;
+  for (long long base = gw * 64; base < cnt; base += nw * 64) {
+    const long long el = base + lane;
+    unsigned long long m = __ballot(el < cnt && xflag[el] != 0);
+    while (m) {   // wave-uniform
+      unsigned long long mm = m;
+      for (int t = 0; t < q; ++t) mm &= mm - 1ull;
+      const bool live = mm != 0ull;
+      process(live ? base + (__ffsll((long long)mm) - 1) : 0, live);
+      for (int t = 0; t < 4; ++t) m &= m - 1ull;
+    }
+  }
+}
+
+// fp32 screen of the multi-candidate rows (Lloyd steps with the incremental
+// M-step, where only labels, the label-vs-min corrections and the Hamerly
+// upper bounds are consumed): the candidates' distances in fp32 (the same
+// sum of squared differences; 20 roundings -> |D32 - D| <= 2^-18 D32), then
+// each candidate's band membership is CERTAIN when
+//   in : D32_c + B_c <= min_j (D32_j - B_j) + delta,
+//   out: D32_c - B_c >  min_j (D32_j + B_j) + delta.
+// A row whose band is certainly {argmin} is done here (label = argmin,
+// corr = 0 - the memset value, mind = D32, ub from D32 + B); every other row
+// (a wider band: its kappa pick and correction need the exact values, or an
+// uncertain member) is flagged for recheck_rows_kernel (fp64).
+// fp32 sub/fma instead of fp64 cvt/sub/fma: the re-check is VALU bound.
+#ifndef SQ_SCREEN_LPR
+#define SQ_SCREEN_LPR 16
+#endif
+template <int DX, int LPR>
+__global__ void __launch_bounds__(256) recheck_fast_kernel(
+    const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
+    const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
+    float* __restrict__ mind, long long cap, double delta, float* __restrict__ ub,
+    unsigned char* __restrict__ xflag) {
+  constexpr int RPW = 64 / LPR;   // rows per wave step
+  constexpr int FPL = DX / LPR;
+  constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const int gbase = lane & ~(LPR - 1);
+  const long long cnt = min((long long)*multi_count, cap);
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  auto cdist32 = [&](const float4 (&xv)[F4], int j) -> float {
+    const float* cr = Cm + (size_t)j * DX;
+    float s = 0.0f;
+#pragma unroll
+    for (int q = 0; q < F4; ++q) {
+      if (4 * (q * LPR + sub) < DX) {   // group-contiguous float4s: coalesced
+        const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * (q * LPR + sub));
+        const float e0 = xv[q].x - cv.x, e1 = xv[q].y - cv.y;
+        const float e2 = xv[q].z - cv.z, e3 = xv[q].w - cv.w;
+        s = fmaf(e0, e0, fmaf(e1, e1, fmaf(e2, e2, fmaf(e3, e3, s))));
+      }
+    }
+    return s;
+  };
+  // each wave walks a CONTIGUOUS slice of the list (rows in ascending
+  // order within a 4K-row chunk): few pages of X live per CU at a time
+  const long long per = ((cnt + nw - 1) / nw + RPW - 1) / RPW * RPW;
+  const long long e_end = min(cnt, (gw + 1) * per);
+  for (long long base = gw * per; base < e_end; base += RPW) {
+    const long long e = base + lane / LPR;
+    const bool live = e < e_end;
+    const long long g = live ? mrows[e] : 0;
+    const int* mc = mcand + g * (kMaxCand + 1);
+    const int c_r = live ? mc[0] : 0;
+    const bool fits = c_r <= LPR;   // one candidate per lane of the group
+    const bool mine = sub < c_r;
+    const int myj = mine ? mc[1 + sub] : 0;
+    float4 xv[F4];
+    const float* xr = X + (size_t)g * DX;
+#pragma unroll
+    for (int q = 0; q < F4; ++q)
+      xv[q] = (4 * (q * LPR + sub) < DX)
+                  ? *reinterpret_cast<const float4*>(xr + 4 * (q * LPR + sub))
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    int cmax = c_r;
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
+    cmax = min(cmax, LPR);
+    float dme = __builtin_inff();
+    for (int c = 0; c < cmax; c += 2) {
+      const int j0 = __shfl(myj, gbase + c, 64);
+      const int j1 = __shfl(myj, gbase + min(c + 1, LPR - 1), 64);
+      float s0 = cdist32(xv, c < c_r ? j0 : 0);
+      float s1 = cdist32(xv, c + 1 < c_r ? j1 : 0);
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) {
+        s0 += __shfl_xor(s0, o, 64);
+        s1 += __shfl_xor(s1, o, 64);
+      }
+      if (sub == c) dme = s0;
+      if (sub == c + 1) dme = s1;
+    }
+    const double B = (double)dme * 0x1p-18 + 1e-30;
+    const double lo = mine ? (double)dme - B : 1e300, hi = mine ? (double)dme + B : 1e300;
+    double minlo = lo, minhi = hi;
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {
+      minlo = fmin(minlo, __shfl_xor(minlo, o, 64));
+      minhi = fmin(minhi, __shfl_xor(minhi, o, 64));
+    }
+    const bool cin = mine && hi <= minlo + delta;
+    const bool cout = mine && lo > minhi + delta;
+    const unsigned long long gmask = ((1ull << LPR) - 1ull) << gbase;
+    const unsigned long long inm = __ballot(cin) & gmask;
+    const bool unsure = !fits || (__ballot(mine && !cin && !cout) & gmask) != 0;
+    const bool done = live && !unsure && __popcll(inm) == 1;
+    const int plane = inm ? __ffsll((long long)inm) - 1 : gbase;
+    const int pick = __shfl(myj, plane, 64);
+    const float dpick = __shfl(dme, plane, 64);
+    const double hpick = __shfl(hi, plane, 64);
+    if (done && sub == 0) {
+      labels[g] = pick;
+      mind[g] = dpick;
+      if (ub) ub[g] = (float)sqrt(hpick) * (1.0f + 0x1p-20f);
+    }
+    // the rest -> flagged for the fp64 pass (a per-entry byte: no atomics)
+    if (live && sub == 0) xflag[e] = done ? 0 : 1;
   }
 }
 
@@ -1227,7 +1359,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
-                            void* ub, void* lb, void* mflag) {
+                            void* ub, void* lb, void* mflag, void* xflag) {
   constexpr int NW = kX64Waves;
   const size_t lds = kX64Ring * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4;
   auto kern = estep_x64_kernel<KSD>;
@@ -1258,13 +1390,20 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                      (int*)mflag);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  // the re-check: one pass over the multi list (count read on the device)
+  // the re-check: one pass over the multi list (count read on the device);
+  // with xrows the fp32 screen first, the fp64 pass over what it left
   const long long rblocks = (n / 16 + 63) / 64;
   const unsigned rgrid = (unsigned)(rblocks < 4096 ? (rblocks > 0 ? rblocks : 1) : 4096);
+  if (xflag)
+    hipLaunchKernelGGL((recheck_fast_kernel<KSD * 16, SQ_SCREEN_LPR>), dim3(rgrid), dim3(256), 0, st,
+                       (const float*)X, (const float*)Cm, (const long long*)mrows,
+                       (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
+                       delta, (float*)ub, (unsigned char*)xflag);
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,
                      (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
-                     delta, key, row_offset, (float*)corr, (float*)ub);
+                     delta, key, row_offset, (float*)corr, (float*)ub,
+                     (const unsigned char*)xflag);
   return (int)hipGetLastError();
 }
 
@@ -1305,7 +1444,9 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 // dense rows through the 3-pass fp32-faithful kernel in list mode, its
 // overflow rows through band_rows_f64, the multi-candidate rows through
 // recheck_rows_kernel.  counts[0] = 3-pass overflow rows, counts[1] = dense
-// rows, counts[2] = multi rows; all zero on entry.  mrows [n] (int64) is the
+// rows, counts[2] = multi rows; all zero on entry.  xflag [n] (uint8, per
+// multi-list entry): with it the fp32 screen runs first and the fp64
+// re-check takes only the entries it flags (null: every multi row).  mrows [n] (int64) is the
 // multi list, mcand [n][kMaxCand + 1] (int32) the candidate lists BY ROW.  mind holds -1 for rows
 // whose distance the M-step (or fill_mind) computes; no inertia here.
 // Xh: fp16(alpha x) [n][d_pad]; X: fp32 [n][d_pad]; Cm: fp32 centroids
@@ -1313,7 +1454,7 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, const void* xn,
                  const void* cmax2, void* labels, void* mind, void* dense_rows, void* ovf_rows,
                  void* mrows, void* mcand, void* corr, void* rlist, void* rcount, void* ub,
-                 void* lb, void* mflag, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
+                 void* lb, void* mflag, void* xflag, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
                  int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
@@ -1337,7 +1478,7 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
                                row_offset, (int)min(n, 2147483647LL), st, rlist, rcount, ub, lb,  \
-                               mflag);                                                           \
+                               mflag, xflag);                                                    \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \

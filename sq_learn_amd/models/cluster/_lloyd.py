@@ -295,7 +295,8 @@ class LloydEngine:
                                                self.cmax2, self.k, self.delta, self.alpha, key,
                                                self.row_offset, self.buf,
                                                bounds=(self.ub, self.lb) if self.bounds else None,
-                                               rows=rows, zero_counts=rows is None)
+                                               rows=rows, zero_counts=rows is None,
+                                               screen=self.incremental and not full)
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):

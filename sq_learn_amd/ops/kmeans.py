@@ -177,6 +177,7 @@ class EStepBuffers:
         # [overflow rows, dense rows, multi-candidate rows] (int32); ovf_count
         # is a view of slot 0
         self.counts = torch.zeros(3, dtype=torch.int32, device=device)
+        self.exact_flag = None   # the fp32 screen's hand-off flags (per multi entry)
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
         self.multi_rows = None   # certified E-step: rows sent to the fp64 re-check kernel
@@ -604,7 +605,8 @@ def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_o
 
 
 def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
-                     buf: EStepBuffers, stream=None, bounds=None, rows=None, zero_counts=True):
+                     buf: EStepBuffers, stream=None, bounds=None, rows=None, zero_counts=True,
+                     screen=False):
     """Certified E-step (``estep_x64_kernel``): one fp16 MFMA pass with a
     rigorous error bound, fp64 re-check of the candidate centroids, dense rows
     through the fp32-faithful 3-pass kernel.  Labels are the fp64 delta-band
@@ -615,7 +617,10 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     Hamerly bounds and multi flag (``buf.mflag``); ``rows`` =
     (rlist int64 [n], rcount int32 [1]): process only the listed rows (list
     mode, count on the device; the filter already started this iteration's
-    multi list, so ``zero_counts`` is False)."""
+    multi list, so ``zero_counts`` is False).  ``screen``: multi rows go
+    through the fp32 screen first (``recheck_fast_kernel``; their ``mind``
+    is then fp32 - for steps whose inertia comes from the incremental
+    statistics), the fp64 re-check takes the rest."""
     n, d_pad = Xf.shape
     k_pad = C_op.shape[0] * 64
     assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in FAST_D
@@ -626,6 +631,8 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     assert cmax2.dtype == torch.float32 and xn.dtype == torch.float32 and xn.numel() >= n
     assert k <= k_pad <= 4096 and buf.labels.numel() >= n
     ensure_multi_buffers(buf, n, Xf.device, bounds is not None)
+    if screen and (buf.exact_flag is None or buf.exact_flag.numel() < n):
+        buf.exact_flag = torch.empty(max(n, 1), dtype=torch.uint8, device=Xf.device)
     st = stream if stream is not None else nat.stream_handle(Xf.device)
     if zero_counts:
         buf.counts.zero_()
@@ -640,6 +647,7 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
                            0 if bounds is None else bounds[0].data_ptr(),
                            0 if bounds is None else bounds[1].data_ptr(),
                            0 if bounds is None else buf.mflag.data_ptr(),
+                           buf.exact_flag.data_ptr() if screen else 0,
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
                            key.s0, key.s1, int(row_offset), st)
