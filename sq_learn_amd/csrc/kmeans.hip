@@ -895,11 +895,20 @@ __global__ void __launch_bounds__(256) delta_hist_kernel(const int* __restrict__
   __syncthreads();
   const long long r0 = (long long)blockIdx.x * kHistChunk;
   const long long r1 = min(n, r0 + kHistChunk);
-  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
-    const int l = labels[r], p = prev[r];
-    if (l == p) continue;
+  auto one = [&](int l, int p) {
+    if (l == p) return;
     if (l >= 0 && l < k) atomicAdd(&dh[l], 1);
     if (p >= 0 && p < k) atomicAdd(&dh[p], 1);
+  };
+  // 4 rows per load (chunk starts are multiples of 4: int4-aligned)
+  for (long long r = r0 + 4 * threadIdx.x; r < r1; r += 1024) {
+    if (r + 4 <= r1) {
+      const int4 l4 = *reinterpret_cast<const int4*>(labels + r);
+      const int4 p4 = *reinterpret_cast<const int4*>(prev + r);
+      one(l4.x, p4.x); one(l4.y, p4.y); one(l4.z, p4.z); one(l4.w, p4.w);
+    } else {
+      for (long long q = r; q < r1; ++q) one(labels[q], prev[q]);
+    }
   }
   __syncthreads();
   for (int j = threadIdx.x; j < k; j += 256)
@@ -918,11 +927,24 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
   __syncthreads();
   const long long r0 = (long long)blockIdx.x * kHistChunk;
   const long long r1 = min(n, r0 + kHistChunk);
-  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
-    const int l = labels[r], p = prev[r];
-    if (l == p) continue;
+  auto count = [&](int l, int p) {
+    if (l == p) return;
     if (l >= 0 && l < k) atomicAdd(&lh[l], 1);
     if (p >= 0 && p < k) atomicAdd(&lh[p], 1);
+  };
+  auto place = [&](long long r, int l, int p) {
+    if (l == p) return;
+    if (l >= 0 && l < k) perm[base[l] + atomicAdd(&lh[l], 1)] = (int)(r << 1);
+    if (p >= 0 && p < k) perm[base[p] + atomicAdd(&lh[p], 1)] = (int)((r << 1) | 1);
+  };
+  for (long long r = r0 + 4 * threadIdx.x; r < r1; r += 1024) {
+    if (r + 4 <= r1) {
+      const int4 l4 = *reinterpret_cast<const int4*>(labels + r);
+      const int4 p4 = *reinterpret_cast<const int4*>(prev + r);
+      count(l4.x, p4.x); count(l4.y, p4.y); count(l4.z, p4.z); count(l4.w, p4.w);
+    } else {
+      for (long long q = r; q < r1; ++q) count(labels[q], prev[q]);
+    }
   }
   __syncthreads();
   for (int j = threadIdx.x; j < k; j += 256) {
@@ -931,11 +953,15 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
     lh[j] = 0;
   }
   __syncthreads();
-  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
-    const int l = labels[r], p = prev[r];
-    if (l == p) continue;
-    if (l >= 0 && l < k) perm[base[l] + atomicAdd(&lh[l], 1)] = (int)(r << 1);
-    if (p >= 0 && p < k) perm[base[p] + atomicAdd(&lh[p], 1)] = (int)((r << 1) | 1);
+  for (long long r = r0 + 4 * threadIdx.x; r < r1; r += 1024) {
+    if (r + 4 <= r1) {
+      const int4 l4 = *reinterpret_cast<const int4*>(labels + r);
+      const int4 p4 = *reinterpret_cast<const int4*>(prev + r);
+      place(r, l4.x, p4.x); place(r + 1, l4.y, p4.y);
+      place(r + 2, l4.z, p4.z); place(r + 3, l4.w, p4.w);
+    } else {
+      for (long long q = r; q < r1; ++q) place(q, labels[q], prev[q]);
+    }
   }
 }
 
@@ -947,8 +973,12 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
     double* __restrict__ sums, double* __restrict__ counts, double* __restrict__ qsum,
     const int* __restrict__ valid_end) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long p0 = (long long)blockIdx.x * range;
-  const long long p1 = min((long long)*valid_end, p0 + range);
+  // range <= 0: the entry count (on the device) is split evenly over the
+  // grid - a few moved rows still keep every block busy
+  const long long total = *valid_end;
+  const long long rng = range > 0 ? range : max(8LL, (total + gridDim.x - 1) / gridDim.x);
+  const long long p0 = (long long)blockIdx.x * rng;
+  const long long p1 = min(total, p0 + rng);
   constexpr int U = SQ_SEG_U;
   const int c0 = lane * 4;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, aq = 0.0, cnt = 0.0;
@@ -1805,11 +1835,11 @@ int sq_centroid_delta(const void* X, const void* labels, const void* prev, void*
                      (int*)ws_cursor);
   hipLaunchKernelGGL(delta_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
                      (const int*)labels, (const int*)prev, n, k, (int*)ws_cursor, (int*)ws_perm);
-  // entries <= 2n; the kernel bounds itself with the scanned total
-  const int range = seg_range();
-  const unsigned grid = (unsigned)((2 * n + range - 1) / range);
+  // entries <= 2n, usually far fewer: a fixed grid shares the scanned total
+  const long long cap_blocks = (2 * n + 63) / 64;
+  const unsigned grid = (unsigned)(cap_blocks < 2048 ? cap_blocks : 2048);
   hipLaunchKernelGGL(delta_segment_kernel, dim3(grid), dim3(512), 0, st, (const float*)X,
-                     (const int*)ws_perm, (const int*)labels, (const int*)prev, d, range,
+                     (const int*)ws_perm, (const int*)labels, (const int*)prev, d, 0,
                      ldexpf(1.0f, -xexp), ldexp(1.0, -qexp), (double*)sums, (double*)counts,
                      (double*)qsum, (const int*)ws_cursor + (k - 1));
   return (int)hipGetLastError();

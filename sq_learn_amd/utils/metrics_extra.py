@@ -17,28 +17,7 @@ def _arr(a, dtype=None):
     return a.astype(dtype) if dtype is not None else a
 
 
-def type_of_target(y):
-    y = np.asarray(to_numpy(y)) if not isinstance(y, list) else np.asarray(y, dtype=object)
-    if y.ndim > 2 or (y.dtype == object and len(y) and not isinstance(y.flat[0], str)):
-        return "unknown"
-    if y.ndim == 2 and y.shape[1] == 0:
-        return "unknown"
-    if y.ndim == 2 and y.shape[1] > 1:
-        suffix = "-multioutput"
-    else:
-        suffix = ""
-    if y.ndim == 2 and y.shape[1] > 1 and np.isin(np.unique(y), [0, 1]).all() and \
-            y.dtype.kind in "biuf":
-        return "multilabel-indicator"
-    if y.dtype.kind == "f" and np.any(y != y.astype(int)):
-        return "continuous" + suffix
-    if len(np.unique(y)) > 2 or (y.ndim >= 2 and len(y[0]) > 1):
-        return "multiclass" + suffix
-    return "binary"
-
-
-def unique_labels(*ys):
-    return np.unique(np.concatenate([np.asarray(to_numpy(y)).ravel() for y in ys]))
+from .multiclass import type_of_target, unique_labels  # noqa: E402  (one definition)
 
 
 def _check_targets(y_true, y_pred):
