@@ -6,8 +6,11 @@ form, no norm expansion, so merge heights match a float64 pdist), reduced
 to the condensed upper triangle, and handed to the host-native linkage core
 ``sqh_linkage`` (``csrc/host/hier_host.cpp``: nearest-neighbour chain with
 Lance-Williams updates, Prim's MST for single linkage, stable height sort,
-union-find relabelling).  Trees are unstructured (no ``connectivity``
-graph): a connectivity-constrained build raises ``NotImplementedError``.
+union-find relabelling).  Connectivity-constrained trees (reference
+``_agglomerative.py:501-603``) merge only along graph edges: ward through a
+heap of edge inertias, complete / average through per-node neighbour maps
+merged by max / size-weighted mean, single through the minimum spanning
+tree of the graph and union-find labelling.
 """
 
 from heapq import heappush, heappushpop
@@ -186,10 +189,150 @@ def ward_tree(X, *, connectivity=None, n_clusters=None, return_distance=False, d
     return children, 1, n, None
 
 
+class _Edge:
+    """Heap entry ordered by weight only (ties keep heap order, like the
+    reference's WeightedEdge)."""
+    __slots__ = ("w", "a", "b")
+
+    def __init__(self, w, a, b):
+        self.w, self.a, self.b = w, a, b
+
+    def __lt__(self, other):
+        return self.w < other.w
+
+
+def _label_mst(edges, n):
+    """Union-find labelling of weight-sorted MST edges into a linkage
+    matrix (reference ``_single_linkage_label``)."""
+    parent = np.full(2 * n - 1, -1, dtype=np.intp)
+    size = np.zeros(2 * n - 1, dtype=np.intp)
+    size[:n] = 1
+    nxt = n
+    out = np.zeros((len(edges), 4))
+
+    def find(v):
+        root = v
+        while parent[root] != -1:
+            root = parent[root]
+        while v != root and parent[v] != root:
+            parent[v], v = root, parent[v]
+        return root
+
+    for t, (a, b, w) in enumerate(edges):
+        ra, rb = find(int(a)), find(int(b))
+        out[t] = (ra, rb, w, size[ra] + size[rb])
+        parent[ra] = parent[rb] = nxt
+        size[nxt] = size[ra] + size[rb]
+        nxt += 1
+    return out
+
+
+def _structured_linkage(X, connectivity, n_clusters, linkage, affinity, return_distance):
+    """complete / average / single linkage restricted to a connectivity
+    graph (reference ``linkage_tree`` structured branch)."""
+    import heapq
+
+    from scipy.sparse.csgraph import minimum_spanning_tree
+
+    from ...utils.pairwise import paired_distances
+    Xn = np.asarray(X.detach().cpu().numpy() if hasattr(X, "detach") else X)
+    if Xn.ndim == 1:
+        Xn = Xn.reshape(-1, 1)
+    n = Xn.shape[0]
+    C, ncc = _fix_connectivity(Xn, connectivity, affinity=affinity)
+    C = C.tocoo()
+    keep = C.row != C.col
+    rows, cols = C.row[keep], C.col[keep]
+    if affinity == "precomputed":
+        dist = np.asarray(Xn[rows, cols], dtype=np.float64)
+    else:
+        dist = np.asarray(paired_distances(Xn[rows], Xn[cols], metric=affinity),
+                          dtype=np.float64)
+    if n_clusters is None:
+        n_nodes = 2 * n - 1
+    else:
+        if n_clusters > n:
+            raise ValueError("Cannot provide more clusters than samples. %i n_clusters was asked, "
+                             "and there are %i samples." % (n_clusters, n))
+        n_nodes = 2 * n - n_clusters
+    from scipy import sparse
+    G = sparse.coo_matrix((dist, (rows, cols)), shape=(n, n))
+    if linkage == "single":
+        # zero-length edges survive the MST as machine epsilon, then go back to 0
+        G = G.astype(np.float64)
+        eps = np.finfo(np.float64).eps
+        G.data[G.data == 0] = eps
+        mst = minimum_spanning_tree(G.tocsr()).tocoo()
+        mst.data[mst.data == eps] = 0
+        E = np.vstack([mst.row, mst.col, mst.data]).T
+        E = E[np.argsort(E[:, 2], kind="mergesort")]
+        Z = _label_mst(E, n)
+        children = Z[:, :2].astype(np.intp)
+        parent = np.arange(n_nodes, dtype=np.intp)
+        for i, (left, right) in enumerate(children, n):
+            if n_clusters is not None and i >= n_nodes:
+                break
+            if left < n_nodes:
+                parent[left] = i
+            if right < n_nodes:
+                parent[right] = i
+        if return_distance:
+            return children, ncc, n, parent, Z[:, 2]
+        return children, ncc, n, parent
+    # per-node neighbour maps (key order = the reference's std::map order)
+    L = G.tolil()
+    A = [dict(zip(r, d)) for r, d in zip(L.rows, L.data)] + [None] * (n_nodes - n)
+    heap = [_Edge(d, i, r) for i, (r_, d_) in enumerate(zip(L.rows, L.data))
+            for r, d in zip(r_, d_) if r < i]
+    heapq.heapify(heap)
+    parent = np.arange(n_nodes, dtype=np.intp)
+    used = np.ones(n_nodes, dtype=np.intp)
+    children = []
+    distances = np.empty(n_nodes - n) if return_distance else None
+    for k in range(n, n_nodes):
+        while True:
+            e = heapq.heappop(heap)
+            if used[e.a] and used[e.b]:
+                break
+        i, j = e.a, e.b
+        if return_distance:
+            distances[k - n] = e.w
+        parent[i] = parent[j] = k
+        children.append((i, j))
+        n_i, n_j = used[i], used[j]
+        used[k] = n_i + n_j
+        used[i] = used[j] = 0
+        merged = {c: v for c, v in A[i].items() if used[c]}
+        for c, v in A[j].items():
+            if not used[c]:
+                continue
+            if c in merged:
+                merged[c] = (max(merged[c], v) if linkage == "complete"
+                             else (n_i * merged[c] + n_j * v) / (n_i + n_j))
+            else:
+                merged[c] = v
+        merged = dict(sorted(merged.items()))
+        for c, v in merged.items():
+            A[c][k] = v
+            heapq.heappush(heap, _Edge(v, k, c))
+        A[k] = merged
+        A[i] = A[j] = None
+    children = np.array(children, dtype=np.intp)[:, ::-1]
+    if return_distance:
+        return children, ncc, n, parent, distances
+    return children, ncc, n, parent
+
+
 def linkage_tree(X, connectivity=None, n_clusters=None, linkage="complete",
                  affinity="euclidean", return_distance=False, device=None):
+    if linkage not in ("average", "complete", "single"):
+        raise ValueError("Unknown linkage option, linkage should be one of %s, but %s was given"
+                         % (("average", "complete", "single"), linkage))
     if connectivity is not None:
-        raise NotImplementedError("connectivity-constrained trees are not implemented")
+        if affinity == "cosine" and np.any(~np.any(np.asarray(X), axis=1)):
+            raise ValueError("Cosine affinity cannot be used when X contains zero vectors")
+        return _structured_linkage(X, connectivity, n_clusters, linkage, affinity,
+                                   return_distance)
     if linkage not in ("average", "complete", "single"):
         raise ValueError("Unknown linkage option, linkage should be one of %s, but %s was given"
                          % (("average", "complete", "single"), linkage))
@@ -295,9 +438,6 @@ class AgglomerativeClustering(ClusterMixin, BaseEstimator):
         if connectivity is not None:
             if callable(connectivity):
                 connectivity = connectivity(X)
-            if self.linkage != "ward":
-                raise NotImplementedError("connectivity-constrained %s linkage is not "
-                                          "implemented (ward is)" % self.linkage)
         full = self.compute_full_tree
         if connectivity is None:
             full = True
