@@ -21,3 +21,10 @@ print(f"GPU busy {busy / steps:.1f} us/step, span {span / steps:.1f} us/step "
       f"(idle {100 * (1 - busy / span):.1f}%)")
 for k, v in sorted(tot.items(), key=lambda t: -t[1])[:top]:
     print(f"{k:60s} {v / steps:8.1f} us/step {100 * v / busy:5.1f}%")
+
+series = {}
+for n, s, e in rows[lo:hi]:
+    k = n.split("(")[0][:60]
+    series.setdefault(k, []).append(int((e - s) / 1000))
+for k, v in sorted(tot.items(), key=lambda t: -t[1])[:6]:
+    print(f"{k[:40]:40s} per call: {series[k]}")

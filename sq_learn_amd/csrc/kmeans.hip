@@ -976,10 +976,24 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
   // range <= 0: the entry count (on the device) is split evenly over the
   // grid - a few moved rows still keep every block busy
   const long long total = *valid_end;
-  const long long rng = range > 0 ? range : max(8LL, (total + gridDim.x - 1) / gridDim.x);
-  const long long p0 = (long long)blockIdx.x * rng;
-  const long long p1 = min(total, p0 + rng);
   constexpr int U = SQ_SEG_U;
+  // range > 0: a block takes `range` entries, its 8 waves interleaved;
+  // range <= 0: each wave takes a CONTIGUOUS run of >= 64 entries (runs of
+  // one label stay in one wave: few flushes, few fp64 atomics)
+  long long p0, p1, pstep, ustep;
+  if (range > 0) {
+    p0 = (long long)blockIdx.x * range + wave;
+    p1 = min(total, (long long)blockIdx.x * range + range);
+    pstep = 8LL * U;
+    ustep = 8;
+  } else {
+    const long long waves = (long long)gridDim.x * 8;
+    const long long rw = max(64LL, (total + waves - 1) / waves);
+    p0 = ((long long)blockIdx.x * 8 + wave) * rw;
+    p1 = min(total, p0 + rw);
+    pstep = U;
+    ustep = 1;
+  }
   const int c0 = lane * 4;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, aq = 0.0, cnt = 0.0;
   int cur = -1;
@@ -997,12 +1011,12 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
       if (q != 0.0) atomicAdd(&qsum[cur], q);
     }
   };
-  for (long long p = p0 + wave; p < p1; p += 8 * U) {
+  for (long long p = p0; p < p1; p += pstep) {
     int code[U], ll[U];
     float4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long q = p + 8LL * u;
+      const long long q = p + ustep * u;
       code[u] = q < p1 ? perm[q] : -1;
     }
 #pragma unroll
