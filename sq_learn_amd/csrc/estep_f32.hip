@@ -428,14 +428,15 @@ __global__ void __launch_bounds__(256) band_rows_f64_kernel(
 // setup, 2 B per value: the same HBM stream as the bf16 kernel) and the next
 // block's fragments are loaded right after the last MFMA of a block, so their
 // latency hides behind the epilogue, the candidate extraction and the
-// re-check.  8 waves (2 per SIMD) x 32 rows per workgroup share each staged
+// re-check.  4 waves (1 per SIMD: 512 registers, no spills) x 32 rows per
+// workgroup share each staged
 // tile; only the HI region of each operand tile is staged (34 KiB per slot at
 // d = 256).
 constexpr int kMaxCand = 16;
 #ifndef SQ_X64_NW
-#define SQ_X64_NW 8
+#define SQ_X64_NW 4
 #endif
-constexpr int kX64Waves = SQ_X64_NW;   // waves per workgroup (2 per SIMD at 8)
+constexpr int kX64Waves = SQ_X64_NW;   // waves per workgroup (8: 2 per SIMD, spills)
 #ifndef SQ_X64_RING
 #define SQ_X64_RING 3
 #endif
