@@ -766,14 +766,17 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
 // largest shift outside F) and bounded one by one: max(lb - s_f, cc[l][f] -
 // ub) with Elkan's cc[l][f] = |c_l' - c_f'| (rounded down; +inf for f = l)
 // from fast_centroids - never weaker than lb - max_j s_j.
-constexpr int kBoundsChunk = 4096;   // rows per workgroup
+// Rows per workgroup = 256 PER: 4096 on large shards (one list atomic per
+// chunk), 1024 below ~4M rows so a small shard (8-GPU strong scaling: 1.25M
+// rows per rank) still spreads over >= 1024 workgroups instead of 305.
+template <int PER>
 __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const int* __restrict__ labels, float* __restrict__ ub, float* __restrict__ lb,
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
     long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
     long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
     const int* __restrict__ fidx, int nf, int k) {
-  constexpr int PER = kBoundsChunk / 256;   // rows per thread (bit masks)
+  constexpr int kBoundsChunk = PER * 256;   // PER rows per thread (bit masks)
   __shared__ int wsum[4];
   __shared__ int base_a, base_m;
   __shared__ double sf_s[65];               // shifts of the fast centroids, [nf] = max
@@ -878,35 +881,50 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(rcount, 0, sizeof(int), st);
-  const long long blocks = (n + kBoundsChunk - 1) / kBoundsChunk;
-  hipLaunchKernelGGL(bounds_filter_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     (const int*)labels, (float*)ub, (float*)lb, (const double*)shift,
-                     (const double*)smax, n, delta, (long long*)rlist, (int*)rcount, (const int*)mflag,
-                     (long long*)mrows, (int*)multi_count,
+  const bool big = n >= 4096LL * 1024;
+  const long long chunk = big ? 4096 : 1024;
+  const long long blocks = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(big ? bounds_filter_kernel<16> : bounds_filter_kernel<4>, dim3((unsigned)blocks),
+                     dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
+                     (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
+                     (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
                      (const float*)cc, (const int*)fidx, nf, k);
   return (int)hipGetLastError();
 }
 
 // The nf fastest centroids of an update: F = top-nf of the shifts by rank
 // (rank of c = #{j : s_j > s_c, or s_j = s_c and j < c}: unique, ties to the
-// lower index), one thread per centroid against all k shifts in LDS;
+// lower index).  One WAVE per centroid c: each lane counts its k / 64 strided
+// shifts (coalesced, L2-resident), one wave sum - k / 4 workgroups instead of
+// one thread walking all k shifts (29.6 -> ~4 us at k = 1024).
+// With shift_sq != null the shifts are first made from the squared
+// per-centroid shifts of the finalize, s = sqrt(s^2) (1 + 1e-12) rounded up
+// (the Hamerly update's margin), and written to shift (the fused form of the
+// former sqrt / scale launches); every lane recomputes the same values.
 // idx[rank] = c for rank < nf, smax_rest = the shift of rank nf.
-__global__ void __launch_bounds__(256) fast_select_kernel(const double* __restrict__ shift, int k,
-                                                          int nf, int* __restrict__ idx,
+__global__ void __launch_bounds__(256) fast_select_kernel(double* __restrict__ shift,
+                                                          const double* __restrict__ shift_sq,
+                                                          int k, int nf, int* __restrict__ idx,
                                                           double* __restrict__ smax_rest) {
-  extern __shared__ double sh_s[];
-  for (int j = threadIdx.x; j < k; j += 256) sh_s[j] = shift[j];
-  __syncthreads();
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= k) return;
-  const double v = sh_s[c];
+  auto sv = [&](int j) -> double {
+    return shift_sq ? sqrt(shift_sq[j]) * (1.0 + 1e-12) : shift[j];
+  };
+  const double v = sv(c);
   int rank = 0;
-  for (int j = 0; j < k; ++j) {
-    const double u = sh_s[j];
+  for (int j = lane; j < k; j += 64) {
+    const double u = sv(j);
     rank += (u > v || (u == v && j < c)) ? 1 : 0;
   }
-  if (rank < nf) idx[rank] = c;
-  if (rank == nf) *smax_rest = v > 0.0 ? v : 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) rank += __shfl_xor(rank, o, 64);
+  if (lane == 0) {
+    if (shift_sq) shift[c] = v;
+    if (rank < nf) idx[rank] = c;
+    if (rank == nf) *smax_rest = v > 0.0 ? v : 0.0;
+  }
 }
 
 // cc[j][f] = |c_j - c_idx[f]| (fp64 from the fp32 centroids, rounded down to
@@ -937,14 +955,13 @@ __global__ void __launch_bounds__(256) fast_cc_kernel(const float* __restrict__ 
     cc[(size_t)k * nf + j] = fminf(fminf(wmin[0], wmin[1]), fminf(wmin[2], wmin[3]));
 }
 
-extern "C" int sq_fast_centroids(const void* shift, const void* C, int k, int d, int nf,
-                                 void* idx, void* smax_rest, void* cc, void* stream) {
+extern "C" int sq_fast_centroids(void* shift, const void* shift_sq, const void* C, int k, int d,
+                                 int nf, void* idx, void* smax_rest, void* cc, void* stream) {
   if (k <= 0) return 0;
   if (nf < 0 || nf > 64 || nf >= k) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  if (k > 8192) return (int)hipErrorInvalidValue;   // shifts staged in LDS
-  hipLaunchKernelGGL(fast_select_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256),
-                     (size_t)k * sizeof(double), st, (const double*)shift, k, nf, (int*)idx,
+  hipLaunchKernelGGL(fast_select_kernel, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, st,
+                     (double*)shift, (const double*)shift_sq, k, nf, (int*)idx,
                      (double*)smax_rest);
   if (nf > 0)
     hipLaunchKernelGGL(fast_cc_kernel, dim3((unsigned)k), dim3(256), 0, st, (const float*)C, k, d,
@@ -1512,12 +1529,16 @@ int sq_fill_mind(const void* X, int ldx, const void* Cm, int d, const void* labe
 }
 
 // inertia[0] = sum of mind[0:n) in a fixed order (part: >= 512 doubles)
-int sq_sum_f32(const void* v, long long n, void* part, void* out, void* stream) {
+// out = sum(v[:n]) + sum(part[512 : 512 + extra]) in a fixed order (the
+// extra partials - e.g. the per-cluster inertia parts - are written there by
+// an earlier launch: one final reduce for both)
+int sq_sum_f32(const void* v, long long n, void* part, int extra, void* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int blocks = 512;
+  if (extra < 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(sum_f32_blocks_kernel, dim3(blocks), dim3(256), 0, st, (const float*)v, n,
                      (double*)part);
-  return sq_sum_partials(part, blocks, out, st);
+  return sq_sum_partials(part, blocks + extra, out, st);
 }
 
 int sq_band_rows_f64(const void* X, const void* C, const void* rows, const void* count,

@@ -965,8 +965,22 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
   }
 }
 
-// one wave per entry (d <= 256: 4 fp32 values per lane), SQ_SEG_U entries in
+// one wave per entry (d <= 256: 4 fp32 values per lane), SQ_DSEG_U entries in
 // flight per wave; the entry count is the scanned total (cursor[k-1]).
+// Each wave takes a run of max(SQ_DSEG_RUN, total / SQ_DSEG_WAVES) entries:
+// long runs keep the fp64 flush atomics few (many moved rows), short ones
+// keep the serial gather chain (perm -> label / row) of a few-moved-rows step
+// short (measured: 64-entry minimum 78 us/step on a 1.25M-row shard, 16 ->
+// 52 us; a fixed 16 costs 27 us at 10M rows through the extra flushes).
+#ifndef SQ_DSEG_U
+#define SQ_DSEG_U 8
+#endif
+#ifndef SQ_DSEG_RUN
+#define SQ_DSEG_RUN 16
+#endif
+#ifndef SQ_DSEG_WAVES
+#define SQ_DSEG_WAVES 2048
+#endif
 __global__ void __launch_bounds__(512) delta_segment_kernel(
     const float* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
     const int* __restrict__ prev, int d, int range, float xscale, double qscale,
@@ -976,7 +990,7 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
   // range <= 0: the entry count (on the device) is split evenly over the
   // grid - a few moved rows still keep every block busy
   const long long total = *valid_end;
-  constexpr int U = SQ_SEG_U;
+  constexpr int U = SQ_DSEG_U;
   // range > 0: a block takes `range` entries, its 8 waves interleaved;
   // range <= 0: each wave takes a CONTIGUOUS run of >= 64 entries (runs of
   // one label stay in one wave: few flushes, few fp64 atomics)
@@ -987,8 +1001,8 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
     pstep = 8LL * U;
     ustep = 8;
   } else {
-    const long long waves = (long long)gridDim.x * 8;
-    const long long rw = max(64LL, (total + waves - 1) / waves);
+    const long long waves = min((long long)gridDim.x * 8, (long long)SQ_DSEG_WAVES);
+    const long long rw = max((long long)SQ_DSEG_RUN, (total + waves - 1) / waves);
     p0 = ((long long)blockIdx.x * 8 + wave) * rw;
     p1 = min(total, p0 + rw);
     pstep = U;

@@ -30,8 +30,8 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
                                            long long, double, void*, void*, const void*, void*,
                                            void*, const void*, const void*, int, int, void*);
-__attribute__((weak)) int sq_fast_centroids(const void*, const void*, int, int, int, void*, void*,
-                                            void*, void*);
+__attribute__((weak)) int sq_fast_centroids(void*, const void*, const void*, int, int, int, void*,
+                                            void*, void*, void*);
 // gram64.hip
 __attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, long long, int, void*,
                                     int, void*);
@@ -94,7 +94,7 @@ __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, co
                                        unsigned, unsigned, unsigned, long long, void*);
 __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
                                        long long, void*);
-__attribute__((weak)) int sq_sum_f32(const void*, long long, void*, void*, void*);
+__attribute__((weak)) int sq_sum_f32(const void*, long long, void*, int, void*, void*);
 // estep_f32.hip
 __attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, void*, void*, void*,
                                        void*, void*, int, void*, long long, int, int, double,
@@ -228,10 +228,11 @@ static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_fast_centroids(PyObject*, PyObject* a) {
-  unsigned long long sh, C, idx, smr, cc, st; int k, d, nf;
-  if (!PyArg_ParseTuple(a, "KKiiiKKKK", &sh, &C, &k, &d, &nf, &idx, &smr, &cc, &st)) return nullptr;
+  unsigned long long sh, sq, C, idx, smr, cc, st; int k, d, nf;
+  if (!PyArg_ParseTuple(a, "KKKiiiKKKK", &sh, &sq, &C, &k, &d, &nf, &idx, &smr, &cc, &st))
+    return nullptr;
   CHECK(sq_fast_centroids)
-  return ret(sq_fast_centroids(P(sh), P(C), k, d, nf, P(idx), P(smr), P(cc), P(st)));
+  return ret(sq_fast_centroids(P(sh), P(sq), P(C), k, d, nf, P(idx), P(smr), P(cc), P(st)));
 }
 
 static PyObject* py_centroid_delta(PyObject*, PyObject* a) {
@@ -373,10 +374,10 @@ static PyObject* py_fill_mind(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_sum_f32(PyObject*, PyObject* a) {
-  unsigned long long v, part, out, st; long long n;
-  if (!PyArg_ParseTuple(a, "KLKKK", &v, &n, &part, &out, &st)) return nullptr;
+  unsigned long long v, part, out, st; long long n; int extra;
+  if (!PyArg_ParseTuple(a, "KLKiKK", &v, &n, &part, &extra, &out, &st)) return nullptr;
   CHECK(sq_sum_f32)
-  return ret(sq_sum_f32(P(v), n, P(part), P(out), P(st)));
+  return ret(sq_sum_f32(P(v), n, P(part), extra, P(out), P(st)));
 }
 
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {

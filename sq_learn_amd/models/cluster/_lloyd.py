@@ -149,7 +149,9 @@ class LloydEngine:
         # and the M-step
         self.Xh16 = (Xf * self.alpha).to(torch.float16) if self.certified else None
         self._prepare_reduce()
-        self.mind_part = torch.zeros(512, dtype=torch.float64, device=dev)
+        # 512 block partials of the min-distance sums + (incremental M-step)
+        # the k per-cluster inertia parts, reduced together in one launch
+        self.mind_part = torch.zeros(512 + self.k, dtype=torch.float64, device=dev)
         # incremental M-step (certified path, unweighted, no failure
         # injection): only the rows whose label moved are re-read; the
         # inertia comes from the per-cluster statistics + the E-step's
@@ -161,7 +163,6 @@ class LloydEngine:
             self.prev_labels = torch.full((self.n,), -1, dtype=torch.int32, device=dev)
             self.qsum = torch.zeros(self.k, dtype=torch.float64, device=dev)
             self.perm2 = torch.empty(max(2 * self.n, 1), dtype=torch.int32, device=dev)
-            self.inertia_part = torch.zeros(self.k, dtype=torch.float64, device=dev)
             self.buf.corr = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
             nr = int(self._nrows_global)
             self.qexp = K.fixed_point_exp(self._max_abs ** 2 * self.dm, nr)
@@ -490,9 +491,8 @@ class LloydEngine:
             self.inc_valid = True
             Cold = self.C if self.dm == self.d else self._padded_centers()
             K.cluster_inertia_native(self.sums, self.counts, self.qsum, Cold, self.k, self.dm,
-                                     self.rws, self.qexp, self.inertia_part)
-            K.sum_f32_native(self.buf.corr, self.n, self.mind_part, inertia)
-            inertia.add_(self.inertia_part.sum())
+                                     self.rws, self.qexp, self.mind_part[512:512 + self.k])
+            K.sum_f32_native(self.buf.corr, self.n, self.mind_part, inertia, extra=self.k)
             sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
             K.pack_stats_native(sums, self.counts, inertia, self.packed, self.k, self.d,
                                 self.rws, weighted=False)
@@ -519,12 +519,14 @@ class LloydEngine:
             if self.bounds:
                 # per-centroid shifts of this update (fp64, rounded up) for the
                 # next E-step's Hamerly bound update
-                torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
-                self.shift_s.mul_(1.0 + 1e-12)
                 if self.n_fast > 0 and self.device.type == "cuda":
+                    # sqrt + margin fused into the top-shift select
                     K.fast_centroids_native(self.shift_s, self.C, self.n_fast, self.fast_idx,
-                                            self.smax, self.fast_cc)
+                                            self.smax, self.fast_cc,
+                                            shift_sq=self.shift_part[:self.k])
                 else:
+                    torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
+                    self.shift_s.mul_(1.0 + 1e-12)
                     torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
                 self.bounds_valid = True
         return self.scalars

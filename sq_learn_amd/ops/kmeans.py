@@ -361,17 +361,23 @@ def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf:
         raise RuntimeError(f"bounds_filter failed (hip error {rc})")
 
 
-def fast_centroids_native(shift, C, nf, idx, smax_rest, cc):
+def fast_centroids_native(shift, C, nf, idx, smax_rest, cc, shift_sq=None):
     """The nf fastest centroids of an update (top-nf shifts) -> ``idx``,
     ``smax_rest`` = the largest shift outside them, ``cc[j][f]`` = |c_j -
     c_idx[f]| rounded down (+inf on j = idx[f]), ``cc[k nf + j]`` = min_f
-    cc[j][f]; csrc/estep_f32.hip."""
+    cc[j][f]; csrc/estep_f32.hip.  With ``shift_sq`` (the squared
+    per-centroid shifts) ``shift`` is first written as sqrt(shift_sq) (1 +
+    1e-12) in the same launch."""
     k, d = C.shape
     assert C.dtype == torch.float32 and C.is_contiguous() and shift.dtype == torch.float64
     assert 0 <= nf < k and idx.numel() >= nf and cc.numel() >= k * (nf + 1)
-    rc = nat.native().fast_centroids(shift.data_ptr(), C.data_ptr(), k, d, int(nf), idx.data_ptr(),
-                                     smax_rest.data_ptr(), cc.data_ptr(),
-                                     nat.stream_handle(C.device))
+    assert shift.numel() >= k and shift.is_contiguous()
+    if shift_sq is not None:
+        assert shift_sq.dtype == torch.float64 and shift_sq.is_contiguous() and shift_sq.numel() >= k
+    rc = nat.native().fast_centroids(shift.data_ptr(),
+                                     0 if shift_sq is None else shift_sq.data_ptr(), C.data_ptr(),
+                                     k, d, int(nf), idx.data_ptr(), smax_rest.data_ptr(),
+                                     cc.data_ptr(), nat.stream_handle(C.device))
     if rc:
         raise RuntimeError(f"fast_centroids failed (hip error {rc})")
 
@@ -661,8 +667,12 @@ def fill_mind_native(Xf, C_master, labels, mind):
                            labels.data_ptr(), mind.data_ptr(), n, nat.stream_handle(Xf.device))
 
 
-def sum_f32_native(v, n, part, out):
-    """out[0] = sum(v[:n]) in a fixed order (deterministic); part >= 512 doubles."""
-    assert part.numel() >= 512 and part.dtype == torch.float64
-    nat.native().sum_f32(v.data_ptr(), int(n), part.data_ptr(), out.data_ptr(),
-                         nat.stream_handle(v.device))
+def sum_f32_native(v, n, part, out, extra=0):
+    """out[0] = sum(v[:n]) + sum(part[512:512 + extra]) in a fixed order
+    (deterministic); part >= 512 + extra doubles (the extra partials were
+    written there by an earlier launch)."""
+    assert part.numel() >= 512 + extra and part.dtype == torch.float64 and extra >= 0
+    rc = nat.native().sum_f32(v.data_ptr(), int(n), part.data_ptr(), int(extra), out.data_ptr(),
+                              nat.stream_handle(v.device))
+    if rc:
+        raise RuntimeError(f"sum_f32 failed (hip error {rc})")
