@@ -5,8 +5,15 @@ Mirrors the reference's ``sklearn/_config.py:6-150`` (``get_config`` /
 MI355X build needs: the compute device, the GEMM precision
 policy for the fused distance kernels and the default counter-RNG seed.
 
-The config is process-global (one process per GPU), exactly like the
-reference; worker threads inherit it because there are none on the hot path.
+Like newer scikit-learn the config is THREAD-LOCAL: each thread starts from
+the process defaults and ``set_config`` / ``config_context`` change only the
+calling thread's view.  Task-parallel workers (``sq_learn_amd.parallel.tasks``:
+cross-validation folds, search candidates, one-vs-rest members, fanned out
+over threads and GPUs) therefore get the dispatching thread's config
+explicitly - ``utils.fixes.delayed`` captures it at dispatch and restores
+it in the worker (reference ``utils/fixes.py:205-222``) - and each worker can
+be pinned to its own GPU through the ``device`` key without touching the
+other threads.
 """
 
 import os
@@ -36,36 +43,48 @@ _global_config = {
     "log_iterations": bool(int(os.environ.get("SQ_LOG_ITERATIONS", "0"))),
 }
 _lock = threading.Lock()
+_threadlocal = threading.local()
+
+
+def _config():
+    """This thread's mutable config (created from the process defaults)."""
+    cfg = getattr(_threadlocal, "config", None)
+    if cfg is None:
+        with _lock:
+            cfg = _threadlocal.config = dict(_global_config)
+    return cfg
 
 
 def get_config():
-    """Return a copy of the current global configuration."""
-    return dict(_global_config)
+    """Return a copy of the current (thread's) configuration."""
+    return dict(_config())
 
 
 def set_config(assume_finite=None, working_memory=None, print_changed_only=None,
                display=None, device=None, gemm_precision=None, seed=None,
                log_iterations=None):
-    """Set global configuration (reference: ``sklearn/_config.py:30``)."""
-    with _lock:
-        if assume_finite is not None:
-            _global_config["assume_finite"] = assume_finite
-        if working_memory is not None:
-            _global_config["working_memory"] = working_memory
-        if print_changed_only is not None:
-            _global_config["print_changed_only"] = print_changed_only
-        if display is not None:
-            _global_config["display"] = display
-        if device is not None:
-            _global_config["device"] = device
-        if gemm_precision is not None:
-            if gemm_precision not in ("bf16", "fp32"):
-                raise ValueError("gemm_precision must be 'bf16' or 'fp32'")
-            _global_config["gemm_precision"] = gemm_precision
-        if seed is not None:
-            _global_config["seed"] = int(seed)
-        if log_iterations is not None:
-            _global_config["log_iterations"] = bool(log_iterations)
+    """Set the configuration of the calling thread (reference:
+    ``sklearn/_config.py:30``); threads started afterwards by the task layer
+    receive it through ``utils.fixes.delayed``."""
+    cfg = _config()
+    if assume_finite is not None:
+        cfg["assume_finite"] = assume_finite
+    if working_memory is not None:
+        cfg["working_memory"] = working_memory
+    if print_changed_only is not None:
+        cfg["print_changed_only"] = print_changed_only
+    if display is not None:
+        cfg["display"] = display
+    if device is not None:
+        cfg["device"] = device
+    if gemm_precision is not None:
+        if gemm_precision not in ("bf16", "fp32"):
+            raise ValueError("gemm_precision must be 'bf16' or 'fp32'")
+        cfg["gemm_precision"] = gemm_precision
+    if seed is not None:
+        cfg["seed"] = int(seed)
+    if log_iterations is not None:
+        cfg["log_iterations"] = bool(log_iterations)
 
 
 @contextmanager

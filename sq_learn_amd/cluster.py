@@ -10,3 +10,6 @@ from .models.cluster._extra import (OPTICS, AffinityPropagation, Birch, MeanShif
                                      compute_optics_graph, estimate_bandwidth, get_bin_seeds,
                                      mean_shift, spectral_clustering)
 from .models.cluster._bicluster import SpectralBiclustering, SpectralCoclustering  # noqa: F401,E402
+
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_bicluster", target="sq_learn_amd.models.cluster._bicluster")

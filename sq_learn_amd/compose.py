@@ -346,3 +346,5 @@ class TransformedTargetRegressor(RegressorMixin, BaseEstimator):
 __all__ = ["ColumnTransformer", "make_column_transformer", "make_column_selector",
            "TransformedTargetRegressor"]
 
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_column_transformer", "_target")

@@ -294,3 +294,6 @@ class PLSSVD(TransformerMixin, BaseEstimator):
 
 
 __all__ = ["PLSRegression", "PLSCanonical", "CCA", "PLSSVD"]
+
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_pls")

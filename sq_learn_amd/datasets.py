@@ -4,3 +4,6 @@ from .utils.datasets import (make_blobs, make_blobs_device, make_classification,
 from .utils.svmlight import dump_svmlight_file, load_svmlight_file, load_svmlight_files  # noqa: F401
 from .utils.datasets_extra import *  # noqa: F401,F403,E402
 from .utils.datasets_extra import __all__ as _extra_all  # noqa: E402,F401
+
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_openml")

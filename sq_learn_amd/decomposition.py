@@ -9,3 +9,6 @@ from .models.decomposition._dict_learning import (DictionaryLearning,  # noqa: F
                                                   MiniBatchSparsePCA, SparseCoder, SparsePCA,
                                                   dict_learning, dict_learning_online,
                                                   sparse_encode)
+
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_fastica", "_truncated_svd")

@@ -147,4 +147,10 @@ def partial_dependence(estimator, X, features, *, response_method="auto",
     return Bunch(average=avg, individual=indiv, values=values, grid_values=values)
 
 
-__all__ = ["permutation_importance", "partial_dependence"]
+from ._inspection_plot import PartialDependenceDisplay, plot_partial_dependence  # noqa: E402
+
+__all__ = ["permutation_importance", "partial_dependence", "PartialDependenceDisplay",
+           "plot_partial_dependence"]
+
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_partial_dependence")

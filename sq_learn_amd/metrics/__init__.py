@@ -38,3 +38,6 @@ from ..utils.metrics_extra import r2_score_ext as r2_score  # noqa: F401,E402,F8
 from ..models.cluster._bicluster import consensus_score  # noqa: F401,E402
 from .pairwise import nan_euclidean_distances  # noqa: F401,E402
 from . import cluster, pairwise  # noqa: F401,E402
+from ._plot import (ConfusionMatrixDisplay, DetCurveDisplay, PrecisionRecallDisplay,  # noqa: F401,E402
+                    RocCurveDisplay, plot_confusion_matrix, plot_det_curve,
+                    plot_precision_recall_curve, plot_roc_curve)

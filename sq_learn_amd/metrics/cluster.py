@@ -2,3 +2,6 @@
 from ..models.cluster._bicluster import consensus_score  # noqa: F401
 from ..utils.cluster_metrics import *  # noqa: F401,F403
 from ..utils.metrics import adjusted_rand_score  # noqa: F401,E402
+
+from ..utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_bicluster")

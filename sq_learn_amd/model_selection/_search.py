@@ -14,6 +14,8 @@ the reference's joblib pool would only contend for the device.
 
 import time
 import warnings
+from ..parallel.tasks import Parallel
+from ..utils.fixes import delayed
 from collections import defaultdict
 from collections.abc import Iterable as Iterable_
 from collections.abc import Mapping, Sequence
@@ -184,15 +186,15 @@ class BaseSearchCV(BaseEstimator):
                   n_resources=None):
         cv = cv or check_cv(self.cv, y, classifier=is_classifier(self.estimator))
         splits = list(cv.split(X, y, groups))
-        out = []
-        for params in candidates:
-            fold = []
-            for train, test in splits:
-                est = clone(self.estimator).set_params(**params)
-                fold.append(_fit_and_score(est, X, y, train, test, scorers, fit_params,
-                                           self.return_train_score, self.error_score))
-            out.append(fold)
-        return out, len(splits)
+        # every (candidate, fold) fit is one task (reference _search.py:795)
+        flat = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_and_score)(clone(self.estimator).set_params(**params), X, y, train,
+                                    test, scorers, fit_params, self.return_train_score,
+                                    self.error_score)
+            for params in candidates for train, test in splits)
+        ns = len(splits)
+        out = [flat[i * ns:(i + 1) * ns] for i in range(len(candidates))]
+        return out, ns
 
     def _format_results(self, candidates, results, n_splits, scorers):
         res = {}
@@ -496,8 +498,11 @@ def permutation_test_score(estimator, X, y, *, groups=None, cv=None, n_permutati
         return yy[idx]
 
     y = np.asarray(y)
-    score = cv_score(y)
-    perm = np.array([cv_score(shuffle(y)) for _ in range(n_permutations)])
+    # the permutations are drawn in order (same stream as sequential), then
+    # the n_permutations + 1 cross-validations run as parallel tasks
+    ys = [y] + [shuffle(y) for _ in range(n_permutations)]
+    scores = Parallel(n_jobs=n_jobs)(delayed(cv_score)(yy) for yy in ys)
+    score, perm = scores[0], np.array(scores[1:])
     pvalue = (np.sum(perm >= score) + 1.0) / (n_permutations + 1)
     return score, perm, pvalue
 
@@ -542,12 +547,14 @@ def learning_curve(estimator, X, y, *, groups=None, train_sizes=np.linspace(0.1,
     test_scores = np.zeros_like(train_scores)
     fit_times = np.zeros_like(train_scores)
     score_times = np.zeros_like(train_scores)
-    for j, (tr, te) in enumerate(splits):
-        for i, m in enumerate(sizes):
-            r = _fit_and_score(clone(estimator), X, y, tr[:m], te, {"s": scorer},
-                               fit_params or {}, True, error_score)
-            train_scores[i, j], test_scores[i, j] = r["train"]["s"], r["test"]["s"]
-            fit_times[i, j], score_times[i, j] = r["fit_time"], r["score_time"]
+    jobs = [(i, j) for j in range(len(splits)) for i in range(len(sizes))]
+    res = Parallel(n_jobs=n_jobs)(
+        delayed(_fit_and_score)(clone(estimator), X, y, splits[j][0][:sizes[i]], splits[j][1],
+                                {"s": scorer}, fit_params or {}, True, error_score)
+        for i, j in jobs)
+    for (i, j), r in zip(jobs, res):
+        train_scores[i, j], test_scores[i, j] = r["train"]["s"], r["test"]["s"]
+        fit_times[i, j], score_times[i, j] = r["fit_time"], r["score_time"]
     if return_times:
         return sizes, train_scores, test_scores, fit_times, score_times
     return sizes, train_scores, test_scores
@@ -562,15 +569,34 @@ def validation_curve(estimator, X, y, *, param_name, param_range, groups=None, c
     scorer = get_scorer(scoring)
     tr_s = np.zeros((len(param_range), len(splits)))
     te_s = np.zeros_like(tr_s)
-    for i, v in enumerate(param_range):
-        for j, (tr, te) in enumerate(splits):
-            est = clone(estimator).set_params(**{param_name: v})
-            r = _fit_and_score(est, X, y, tr, te, {"s": scorer}, fit_params or {}, True,
-                               error_score)
-            tr_s[i, j], te_s[i, j] = r["train"]["s"], r["test"]["s"]
+    jobs = [(i, j) for i in range(len(param_range)) for j in range(len(splits))]
+    res = Parallel(n_jobs=n_jobs)(
+        delayed(_fit_and_score)(clone(estimator).set_params(**{param_name: param_range[i]}), X,
+                                y, splits[j][0], splits[j][1], {"s": scorer}, fit_params or {},
+                                True, error_score)
+        for i, j in jobs)
+    for (i, j), r in zip(jobs, res):
+        tr_s[i, j], te_s[i, j] = r["train"]["s"], r["test"]["s"]
     return tr_s, te_s
+
+
+def fit_grid_point(X, y, estimator, parameters, train, test, scorer, verbose,
+                   error_score=np.nan, **fit_params):
+    """Fit one parameter setting on one split and score it (reference
+    ``_search.py:330``, deprecated there): returns (score, parameters,
+    n_test_samples); ``scorer`` may be a callable or a dict of them (the
+    score is then a dict)."""
+    import warnings as _w
+    _w.warn("fit_grid_point is deprecated in 0.23 and will be removed in 1.0 (renaming of "
+            "0.25).", FutureWarning)
+    multi = isinstance(scorer, dict)
+    scorers = scorer if multi else {"score": scorer}
+    est = clone(estimator).set_params(**parameters)
+    r = _fit_and_score(est, X, y, train, test, scorers, fit_params, False, error_score)
+    score = r["test"] if multi else r["test"]["score"]
+    return score, parameters, len(test)
 
 
 __all__ = ["ParameterGrid", "ParameterSampler", "GridSearchCV", "RandomizedSearchCV",
            "HalvingGridSearchCV", "HalvingRandomSearchCV", "permutation_test_score",
-           "learning_curve", "validation_curve"]
+           "learning_curve", "validation_curve", "fit_grid_point"]

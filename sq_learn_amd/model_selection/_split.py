@@ -293,3 +293,18 @@ class _CVIterableWrapper(BaseCrossValidator):
     def split(self, X=None, y=None, groups=None):
         for train, test in self.cv:
             yield train, test
+
+
+# The group / leave-out / repeated / predefined splitters live in
+# _split_extra.py (which imports this module); the reference exposes them
+# from model_selection/_split.py, so they resolve here lazily (PEP 562).
+_EXTRA_SPLITTERS = ("GroupKFold", "LeaveOneGroupOut", "LeaveOneOut", "LeavePGroupsOut",
+                    "LeavePOut", "RepeatedStratifiedKFold", "RepeatedKFold", "GroupShuffleSplit",
+                    "StratifiedGroupKFold", "PredefinedSplit", "TimeSeriesSplit")
+
+
+def __getattr__(name):
+    if name in _EXTRA_SPLITTERS:
+        from . import _split_extra
+        return getattr(_split_extra, name)
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")

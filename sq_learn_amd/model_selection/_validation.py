@@ -14,6 +14,8 @@ import warnings
 
 import numpy as np
 
+from ..parallel.tasks import Parallel
+from ..utils.fixes import delayed
 from ..base import clone, is_classifier
 from ..exceptions import FitFailedWarning
 from ..utils import metrics as M
@@ -103,10 +105,12 @@ def cross_validate(estimator, X, y=None, *, groups=None, scoring=None, cv=None, 
         scorers = {k: get_scorer(v) for k, v in scoring.items()}
     else:
         scorers = {s: get_scorer(s) for s in scoring}
-    results = []
-    for train, test in cv.split(X, y, groups):
-        results.append(_fit_and_score(clone(estimator), X, y, train, test, scorers,
-                                      fit_params or {}, return_train_score, error_score))
+    # one task per fold: threads, one GPU per fold when several are visible
+    # (parallel/tasks.py; the reference's joblib fan-out, _validation.py:267)
+    results = Parallel(n_jobs=n_jobs)(
+        delayed(_fit_and_score)(clone(estimator), X, y, train, test, scorers, fit_params or {},
+                                return_train_score, error_score)
+        for train, test in cv.split(X, y, groups))
     out = {"fit_time": np.array([r["fit_time"] for r in results]),
            "score_time": np.array([r["score_time"] for r in results])}
     if return_estimator:
@@ -122,7 +126,7 @@ def cross_validate(estimator, X, y=None, *, groups=None, scoring=None, cv=None, 
 
 def cross_val_score(estimator, X, y=None, *, groups=None, scoring=None, cv=None, n_jobs=None,
                     verbose=0, fit_params=None, pre_dispatch="2*n_jobs", error_score=np.nan):
-    r = cross_validate(estimator, X, y, groups=groups, scoring=scoring, cv=cv,
+    r = cross_validate(estimator, X, y, groups=groups, scoring=scoring, cv=cv, n_jobs=n_jobs,
                        fit_params=fit_params, error_score=error_score)
     return r["test_score"]
 
@@ -131,14 +135,28 @@ def cross_val_predict(estimator, X, y=None, *, groups=None, cv=None, n_jobs=None
                       fit_params=None, method="predict"):
     cv = check_cv(cv, y, classifier=is_classifier(estimator))
     n = len(X) if not hasattr(X, "shape") else X.shape[0]
-    preds = None
-    for train, test in cv.split(X, y, groups):
-        est = clone(estimator)
+    def fold(est, train, test):
         ytr = _safe_index(y, train)
-        est.fit(_safe_index(X, train), ytr, **(fit_params or {})) if ytr is not None else \
+        if ytr is not None:
+            est.fit(_safe_index(X, train), ytr, **(fit_params or {}))
+        else:
             est.fit(_safe_index(X, train), **(fit_params or {}))
-        p = np.asarray(getattr(est, method)(_safe_index(X, test)))
+        return test, np.asarray(getattr(est, method)(_safe_index(X, test)))
+
+    parts = Parallel(n_jobs=n_jobs)(delayed(fold)(clone(estimator), train, test)
+                                    for train, test in cv.split(X, y, groups))
+    preds = None
+    for test, p in parts:
         if preds is None:
             preds = np.empty((n,) + p.shape[1:], dtype=p.dtype)
         preds[test] = p
     return preds
+
+
+def __getattr__(name):
+    # the curves and the permutation test are defined with the searches
+    # (_search.py); the reference exposes them from _validation.py
+    if name in ("learning_curve", "validation_curve", "permutation_test_score"):
+        from . import _search
+        return getattr(_search, name)
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")

@@ -9,10 +9,11 @@ from ._stochastic_gradient import (PassiveAggressiveClassifier, PassiveAggressiv
 from ._lm_extra import *  # noqa: F401,F403
 from ._lm_extra import __all__ as _extra_all
 from ._ridge import Ridge, RidgeClassifier, RidgeClassifierCV, RidgeCV, ridge_regression
+from ._sgd_losses import Hinge, Huber, Log, ModifiedHuber, SquaredLoss
 
 __all__ = ["LinearRegression", "ElasticNet", "ElasticNetCV", "Lasso", "LassoCV", "enet_path",
            "lasso_path", "Ridge", "RidgeClassifier", "RidgeClassifierCV", "RidgeCV",
            "ridge_regression", "LogisticRegression", "ARDRegression", "BayesianRidge", "SGDClassifier", "SGDRegressor",
            "SGDOneClassSVM", "Perceptron", "PassiveAggressiveClassifier",
-           "PassiveAggressiveRegressor"]
+           "PassiveAggressiveRegressor", "Hinge", "Huber", "Log", "ModifiedHuber", "SquaredLoss"]
 __all__ = __all__ + list(_extra_all)

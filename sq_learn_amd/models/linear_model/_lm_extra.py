@@ -1062,6 +1062,43 @@ class GammaRegressor(TweedieRegressor):
                                                "warm_start", "verbose")}
 
 
+class GeneralizedLinearRegressor(TweedieRegressor):
+    """Generalised linear model of a named exponential-dispersion family
+    (reference ``linear_model/_glm/glm.py:GeneralizedLinearRegressor``,
+    the base of the Poisson / Gamma / Tweedie regressors): 'normal',
+    'poisson', 'gamma' and 'inverse-gaussian' are the Tweedie powers 0, 1,
+    2, 3; same L-BFGS solver as TweedieRegressor."""
+
+    _FAMILY_POWER = {"normal": 0.0, "poisson": 1.0, "gamma": 2.0, "inverse-gaussian": 3.0}
+
+    def __init__(self, *, alpha=1.0, fit_intercept=True, family="normal", link="auto",
+                 solver="lbfgs", max_iter=100, tol=1e-4, warm_start=False, verbose=0):
+        self.family = family
+        self.solver = solver
+        super().__init__(power=0.0, alpha=alpha, fit_intercept=fit_intercept, link=link,
+                         max_iter=max_iter, tol=tol, warm_start=warm_start, verbose=verbose)
+
+    # the family is a constructor parameter here (not TweedieRegressor's
+    # read-only property)
+    family = None
+
+    def get_params(self, deep=True):
+        return {k: getattr(self, k) for k in ("alpha", "fit_intercept", "family", "link",
+                                               "solver", "max_iter", "tol", "warm_start",
+                                               "verbose")}
+
+    def fit(self, X, y, sample_weight=None):
+        if self.family not in self._FAMILY_POWER:
+            raise ValueError("The family must be an instance of class ExponentialDispersionModel "
+                             "or an element of ['normal', 'poisson', 'gamma', "
+                             "'inverse-gaussian']; got (family={0})".format(self.family))
+        if self.solver != "lbfgs":
+            raise ValueError("GeneralizedLinearRegressor supports only solvers 'lbfgs'; got "
+                             "{0}".format(self.solver))
+        self.power = self._FAMILY_POWER[self.family]
+        return super().fit(X, y, sample_weight=sample_weight)
+
+
 # ================================================================= Quantile
 class QuantileRegressor(RegressorMixin, LinearModel):
     """L1-penalised quantile regression as a linear program (HiGHS)."""

@@ -31,6 +31,7 @@ from ...ops import _host
 from ...utils.class_weight import compute_class_weight
 from ...utils.validation import check_array, check_is_fitted, check_random_state
 from ._base import LinearClassifierMixin, SparseCoefMixin
+from ._sgd_losses import make_loss
 
 MAX_INT = np.iinfo(np.int32).max
 DEFAULT_EPSILON = 0.1
@@ -300,7 +301,7 @@ class BaseSGDClassifier(LinearClassifierMixin, BaseSGD):
         elif d != self.coef_.shape[-1]:
             raise ValueError("Number of features %d does not match previous data %d."
                              % (d, self.coef_.shape[-1]))
-        self.loss_function_ = loss
+        self.loss_function_ = make_loss(loss, self._loss_param(loss))
         self._fit_loss = loss
         if not hasattr(self, "t_"):
             self.t_ = 1.0
@@ -833,7 +834,7 @@ class SGDOneClassSVM(OutlierMixin, BaseSGD):
         if self.average and getattr(self, "_average_coef", None) is None:
             self._average_coef = np.zeros(d, dtype=np.float64)
             self._average_intercept = np.zeros(1, dtype=np.float64)
-        self.loss_function_ = loss
+        self.loss_function_ = make_loss(loss, self._loss_param(loss))
         if not hasattr(self, "t_"):
             self.t_ = 1.0
         self._fit_one_class(X, alpha, C, sample_weight, learning_rate, max_iter)

@@ -10,6 +10,7 @@ follow the reference so that a fitted tree is the reference's tree; growth
 itself is the host-native builder (``csrc/host/tree.cpp``).
 """
 
+from abc import ABCMeta, abstractmethod
 import numbers
 import warnings
 from math import ceil
@@ -67,8 +68,14 @@ def resolve_max_features(max_features, n_features, is_clf):
     return max(1, int(max_features * n_features)) if max_features > 0.0 else 0
 
 
-class BaseDecisionTree(BaseEstimator):
-    """Shared fit / predict machinery of the tree estimators."""
+class BaseDecisionTree(BaseEstimator, metaclass=ABCMeta):
+    """Shared fit / predict machinery of the tree estimators (abstract, as
+    the reference's ``tree/_classes.py:BaseDecisionTree``: the concrete
+    classes define the constructor)."""
+
+    @abstractmethod
+    def __init__(self):
+        pass
 
     def get_depth(self):
         check_is_fitted(self)

@@ -214,18 +214,18 @@ class Normalizer(TransformerMixin, BaseEstimator):
 __all__ = ["StandardScaler", "MinMaxScaler", "Normalizer", "normalize"]
 
 
-from ._polynomial import PolynomialFeatures  # noqa: E402,F401
+from ._polynomial import PolynomialFeatures, SplineTransformer  # noqa: E402,F401
 from ._encoders import (LabelBinarizer, LabelEncoder, MultiLabelBinarizer,  # noqa: E402,F401
                         OneHotEncoder, OrdinalEncoder, label_binarize)
 from ._data_extra import (Binarizer, FunctionTransformer, KBinsDiscretizer,  # noqa: E402,F401
                           KernelCenterer, MaxAbsScaler, PowerTransformer, QuantileTransformer,
-                          RobustScaler, SplineTransformer, add_dummy_feature, binarize,
+                          RobustScaler, add_dummy_feature, binarize,
                           maxabs_scale, power_transform, quantile_transform, robust_scale)
 
-__all__ += ["PolynomialFeatures", "LabelBinarizer", "LabelEncoder", "MultiLabelBinarizer",
+__all__ += ["PolynomialFeatures", "SplineTransformer", "LabelBinarizer", "LabelEncoder", "MultiLabelBinarizer",
             "OneHotEncoder", "OrdinalEncoder", "label_binarize", "Binarizer",
             "FunctionTransformer", "KBinsDiscretizer", "KernelCenterer", "MaxAbsScaler",
-            "PowerTransformer", "QuantileTransformer", "RobustScaler", "SplineTransformer",
+            "PowerTransformer", "QuantileTransformer", "RobustScaler",
             "add_dummy_feature", "binarize", "maxabs_scale", "power_transform",
             "quantile_transform", "robust_scale"]
 
@@ -279,3 +279,6 @@ def minmax_scale(X, feature_range=(0, 1), *, axis=0, copy=True):
     Xr *= s
     Xr += lo - dmin * s
     return Xa.ravel() if orig_1d else Xa
+
+from ..utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_data", "_label")

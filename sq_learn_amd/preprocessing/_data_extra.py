@@ -2,7 +2,7 @@
 ``preprocessing/_data.py`` (MaxAbsScaler, RobustScaler, Binarizer,
 KernelCenterer, QuantileTransformer, PowerTransformer, add_dummy_feature
 and the functional forms), ``_discretization.py`` (KBinsDiscretizer),
-``_function_transformer.py`` and ``_polynomial.py`` (SplineTransformer).
+``_function_transformer.py`` (SplineTransformer is in ``_polynomial.py``).
 Dense numpy (fp64) implementations; statistics follow the reference."""
 
 import warnings
@@ -518,86 +518,3 @@ class KBinsDiscretizer(TransformerMixin, BaseEstimator):
             centers = (e[1:] + e[:-1]) * 0.5
             out[:, j] = centers[Xt[:, j].astype(int)]
         return out
-
-
-class SplineTransformer(TransformerMixin, BaseEstimator):
-    def __init__(self, n_knots=5, degree=3, *, knots="uniform", extrapolation="constant",
-                 include_bias=True, order="C"):
-        self.n_knots = n_knots
-        self.degree = degree
-        self.knots = knots
-        self.extrapolation = extrapolation
-        self.include_bias = include_bias
-        self.order = order
-
-    def fit(self, X, y=None, sample_weight=None):
-        X = _dense(X)
-        self.n_features_in_ = X.shape[1]
-        if isinstance(self.knots, str):
-            if self.knots == "uniform":
-                lo, hi = X.min(0), X.max(0)
-                base = np.linspace(lo, hi, self.n_knots)
-            else:
-                base = np.percentile(X, np.linspace(0, 100, self.n_knots), axis=0)
-        else:
-            base = np.asarray(self.knots, dtype=np.float64)
-        k = self.degree
-        dist_min = base[1] - base[0]
-        dist_max = base[-1] - base[-2]
-        if self.extrapolation == "periodic":
-            period = base[-1] - base[0]
-            knots = np.r_[base[-(k + 1):-1] - period, base, base[1:(k + 1)] + period]
-        else:
-            knots = np.r_[np.linspace(base[0] - k * dist_min, base[0] - dist_min, num=k),
-                          base, np.linspace(base[-1] + dist_max, base[-1] + k * dist_max, num=k)]
-        n_splines = knots.shape[0] - k - 1
-        if self.extrapolation == "periodic":
-            n_splines -= k
-        self.bsplines_ = []
-        for j in range(X.shape[1]):
-            coef = np.eye(knots.shape[0] - k - 1)
-            self.bsplines_.append(BSpline.construct_fast(knots[:, j], coef, k,
-                                                         extrapolate=self.extrapolation in
-                                                         ("periodic", "continue")))
-        self.n_features_out_ = n_splines * X.shape[1] - (0 if self.include_bias
-                                                         else X.shape[1])
-        self._n_splines = n_splines
-        self._base = base
-        return self
-
-    def transform(self, X):
-        check_is_fitted(self)
-        X = _dense(X)
-        _nf(self, X)
-        k = self.degree
-        ns = self._n_splines
-        blocks = []
-        for j, spl in enumerate(self.bsplines_):
-            x = X[:, j]
-            if self.extrapolation == "periodic":
-                t = spl.t
-                x = t[k] + (x - t[k]) % (t[-k - 1] - t[k])
-                B = spl(x)
-                B = B[:, :ns] + np.pad(B[:, ns:], ((0, 0), (0, ns - B[:, ns:].shape[1])))
-            else:
-                lo, hi = self._base[0, j], self._base[-1, j]
-                inside = (x >= lo) & (x <= hi)
-                B = np.zeros((x.shape[0], spl.c.shape[0]))
-                B[inside] = spl(x[inside])
-                if self.extrapolation == "continue":
-                    B[~inside] = spl(x[~inside])
-                elif self.extrapolation == "constant":
-                    f_lo, f_hi = spl(lo), spl(hi)
-                    B[x < lo] = f_lo
-                    B[x > hi] = f_hi
-                elif self.extrapolation == "linear":
-                    f_lo, f_hi = spl(lo), spl(hi)
-                    d_lo, d_hi = spl(lo, nu=1), spl(hi, nu=1)
-                    B[x < lo] = f_lo + (x[x < lo, None] - lo) * d_lo
-                    B[x > hi] = f_hi + (x[x > hi, None] - hi) * d_hi
-                elif self.extrapolation == "error" and (~inside).any():
-                    raise ValueError("X contains values beyond the limits of the knots.")
-            if not self.include_bias:
-                B = B[:, :-1]
-            blocks.append(B)
-        return np.hstack(blocks)

@@ -299,3 +299,6 @@ class SelfTrainingClassifier(MetaEstimatorMixin, ClassifierMixin, BaseEstimator)
 
 
 __all__ = ["LabelPropagation", "LabelSpreading", "SelfTrainingClassifier"]
+
+from .utils._aliases import alias_submodules  # noqa: E402
+alias_submodules(__name__, "_self_training")

@@ -513,6 +513,34 @@ def load_files(container_path, *, description=None, categories=None, load_conten
     return Bunch(**out)
 
 
+def load_sample_images():
+    """The two bundled sample photographs (``china.jpg``, ``flower.jpg``,
+    427 x 640 x 3 uint8; CC-BY, see ``_data/images/README.txt``) as a Bunch
+    with ``images``, ``filenames`` and ``DESCR`` (reference
+    ``datasets/_base.py:1096``); decoded with Pillow."""
+    from PIL import Image
+    folder = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_data",
+                          "images")
+    files = sorted(os.path.join(folder, f) for f in os.listdir(folder) if f.endswith(".jpg"))
+    images = []
+    for f in files:
+        with Image.open(f) as im:
+            images.append(np.asarray(im.convert("RGB"), dtype=np.uint8))
+    return Bunch(images=images, filenames=files,
+                 DESCR="Two sample photographs (china.jpg, flower.jpg) for image processing "
+                       "examples; Creative Commons BY 2.0 (README.txt next to the files).")
+
+
+def load_sample_image(image_name):
+    """One sample image by file name ('china.jpg' or 'flower.jpg') as a
+    (height, width, 3) uint8 array (reference ``datasets/_base.py:1147``)."""
+    data = load_sample_images()
+    for name, img in zip(data.filenames, data.images):
+        if name.endswith(image_name):
+            return img
+    raise AttributeError("Cannot find sample image: %s" % image_name)
+
+
 def _fetch_unavailable(name):
     def f(*args, **kwargs):
         raise IOError("%s downloads its data from the internet, which is not available in this "

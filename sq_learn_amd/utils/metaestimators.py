@@ -109,3 +109,31 @@ def _delegate_has(attr, *names):
                 return hasattr(inner, attr)
         return False
     return check
+
+
+def if_delegate_has_method(delegate):
+    """Method decorator of meta-estimators (reference
+    ``utils/metaestimators.py:158``): the decorated method exists only when
+    the sub-estimator stored under ``delegate`` (an attribute name, or a
+    tuple of them tried in order - e.g. the fitted ``estimator_`` before the
+    unfitted ``estimator``) has a method of the same name; otherwise
+    accessing it raises AttributeError, so ``hasattr`` reflects the
+    delegate's capabilities."""
+    if isinstance(delegate, list):
+        delegate = tuple(delegate)
+    names = delegate if isinstance(delegate, tuple) else (delegate,)
+
+    def wrap(fn):
+        attr = fn.__name__
+
+        def check(self):
+            for n in names:
+                obj = getattr(self, n, None)
+                if obj is not None:
+                    return hasattr(obj, attr)
+            # none of the delegates is set: raise like the reference (the
+            # last name's AttributeError)
+            getattr(self, names[-1])
+            return False
+        return _AvailableIf(fn, check, attr)
+    return wrap

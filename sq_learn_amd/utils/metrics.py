@@ -30,16 +30,59 @@ def r2_score(y_true, y_pred, *, sample_weight=None):
     return float(1 - num / den)
 
 
-def confusion_matrix(y_true, y_pred, *, labels=None):
+def confusion_matrix(y_true, y_pred, *, labels=None, sample_weight=None, normalize=None):
+    """C[i, j] = (weighted) count of samples of true class labels[i]
+    predicted as labels[j] (reference ``metrics/_classification.py:222``);
+    ``normalize`` in {'true', 'pred', 'all'} divides by the row sums, the
+    column sums or the total (0/0 -> 0).  One scatter-add, no Python loop."""
     y_true = np.asarray(to_numpy(y_true)).reshape(-1)
     y_pred = np.asarray(to_numpy(y_pred)).reshape(-1)
+    if y_true.shape[0] != y_pred.shape[0]:
+        raise ValueError("Found input variables with inconsistent numbers of samples: "
+                         f"[{y_true.shape[0]}, {y_pred.shape[0]}]")
+    if normalize not in ("true", "pred", "all", None):
+        raise ValueError("normalize must be one of {'true', 'pred', 'all', None}")
     if labels is None:
         labels = np.unique(np.concatenate([y_true, y_pred]))
-    idx = {l: i for i, l in enumerate(labels)}
-    cm = np.zeros((len(labels), len(labels)), dtype=np.int64)
-    for t, p in zip(y_true, y_pred):
-        if t in idx and p in idx:
-            cm[idx[t], idx[p]] += 1
+    else:
+        labels = np.asarray(labels)
+        if labels.size == 0:
+            raise ValueError("'labels' should contains at least one label.")
+        if y_true.size == 0:
+            return np.zeros((labels.size, labels.size), dtype=int)
+        if not np.isin(y_true, labels).any():
+            raise ValueError("At least one label specified must be in y_true")
+    n = labels.size
+    if sample_weight is None:
+        sw = np.ones(y_true.shape[0], dtype=np.int64)
+    else:
+        sw = np.asarray(sample_weight).reshape(-1)
+        if sw.shape[0] != y_true.shape[0]:
+            raise ValueError("Found input variables with inconsistent numbers of samples.")
+    dtype = np.int64 if sw.dtype.kind in "iub" else np.float64
+    # map labels to indices (labels need not be sorted); unknown -> dropped
+    order = np.argsort(labels, kind="stable")
+    sl = labels[order]
+
+    def index(y):
+        pos = np.clip(np.searchsorted(sl, y), 0, n - 1)
+        ok = sl[pos] == y
+        return order[pos], ok
+
+    ti, tok = index(y_true)
+    pi, pok = index(y_pred)
+    keep = tok & pok
+    cm = np.zeros((n, n), dtype=dtype)
+    np.add.at(cm, (ti[keep], pi[keep]), sw[keep].astype(dtype))
+    if normalize is not None:
+        with np.errstate(all="ignore"):
+            if normalize == "true":
+                cm = cm / cm.sum(axis=1, keepdims=True)
+            elif normalize == "pred":
+                cm = cm / cm.sum(axis=0, keepdims=True)
+            else:
+                cm = cm / cm.sum()
+        cm = np.nan_to_num(cm)
     return cm
 
 

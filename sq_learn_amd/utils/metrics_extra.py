@@ -462,14 +462,20 @@ def roc_auc_score(y_true, y_score, *, average="macro", sample_weight=None, max_f
 
 
 def det_curve(y_true, y_score, pos_label=None, sample_weight=None):
+    """False positive / false negative rates per threshold (reference
+    ``metrics/_ranking.py:235``): from the last threshold with no false
+    positive beyond the first one, to the first one with no false negative,
+    in order of decreasing false positive rate."""
+    if len(np.unique(np.asarray(y_true))) != 2:
+        raise ValueError("Only one class present in y_true. Detection error tradeoff curve is "
+                         "not defined in that case.")
     fps, tps, thr = _binary_clf_curve(y_true, y_score, pos_label, sample_weight)
     fns = tps[-1] - tps
     p, n = tps[-1], fps[-1]
-    first = fps.searchsorted(fps[-1], side="right")
-    last = fps.searchsorted(fps[0])
-    sl = slice(first, last, -1) if first > last else slice(-1, last - 1, -1)
-    sl = slice(min(first, len(fps) - 1), None, -1)
-    return fps[sl] / n, fns[sl] / p, thr[sl]
+    first = fps.searchsorted(fps[0], side="right") - 1
+    last = tps.searchsorted(tps[-1]) + 1
+    sl = slice(max(first, 0), last)
+    return fps[sl][::-1] / n, fns[sl][::-1] / p, thr[sl][::-1]
 
 
 def top_k_accuracy_score(y_true, y_score, *, k=2, normalize=True, sample_weight=None,
