@@ -5,13 +5,14 @@
 
 MI355X mapping:
 * t-SNE: the perplexity binary search runs for all rows at once on the
-  device; the gradient is the exact O(n^2) Student-t force computed with
-  dense device matmuls every iteration (n x n tiles stay in HBM).  With
-  ``method='barnes_hut'`` the affinities are the reference's sparse
-  k-NN P (3*perplexity neighbours) but the repulsion is still evaluated
-  exactly on the device instead of by a Barnes-Hut quad-tree - more
-  accurate than the reference's approximation; ``angle`` is accepted and
-  unused.
+  device.  ``method='exact'``: the O(n^2) Student-t gradient from dense
+  device matmuls every iteration (n x n tiles in HBM, as the reference's
+  dense P).  ``method='barnes_hut'`` (reference ``_barnes_hut_tsne.pyx``):
+  the sparse k-NN P (3*perplexity neighbours) stays CSR and the gradient
+  comes from the host-native Barnes-Hut kernel (``csrc/host/tsne_bh.cpp``:
+  quad/oct-tree rebuilt per iteration, ``angle`` opening criterion,
+  OpenMP over points, deterministic reductions) - O(n log n) time and O(n)
+  memory per iteration.
 * SMACOF iterations are n x n device matmuls; Isomap's geodesics use the
   framework's shortest-path kernels and device eigensolvers.
 """
@@ -97,14 +98,38 @@ def _joint_probabilities(D2, perplexity):
 
 
 def _joint_probabilities_nn(dist, ind, n, perplexity):
-    dev = _dev()
+    """Symmetric sparse joint probabilities from the k-NN conditional ones
+    (reference ``_t_sne.py:_joint_probabilities_nn``): CSR, kept sparse."""
     cond = _binary_search_perplexity(dist.astype(np.float32).astype(np.float64), perplexity,
                                      True).cpu().numpy()
     P = sp.csr_matrix((cond.ravel(), ind.ravel(), np.arange(0, ind.size + 1, ind.shape[1])),
                       shape=(n, n))
     P = P + P.T
     P = P / max(P.sum(), MACHINE_EPSILON)
-    return torch.as_tensor(P.toarray(), device=dev)
+    if not np.all(np.abs(P.data) <= 1.0):
+        raise ValueError("All probabilities should be less or then equal to one")
+    P = P.tocsr()
+    P.sort_indices()
+    return P
+
+
+def _kl_grad_bh(Y, P, dof, angle, compute_error=True):
+    """KL divergence and gradient with the Barnes-Hut repulsion (host
+    kernel ``sqh_tsne_bh_grad``); Y: (n, dim) fp64 numpy, P: CSR."""
+    from ...ops import _host
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    n, dim = Y.shape
+    if dim > 3:
+        raise ValueError("'n_components' should be inferior to 4 for the barnes_hut algorithm "
+                         "as it relies on quad-tree or oct-tree.")
+    indptr = np.ascontiguousarray(P.indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(P.indices, dtype=np.int32)
+    data = np.ascontiguousarray(P.data, dtype=np.float64)
+    grad = np.empty_like(Y)
+    kl = _host.lib().sqh_tsne_bh_grad(Y.ctypes.data, n, dim, indptr.ctypes.data,
+                                      indices.ctypes.data, data.ctypes.data, float(angle),
+                                      float(dof), int(bool(compute_error)), grad.ctypes.data)
+    return (float(kl) if compute_error else None), grad
 
 
 def _kl_grad(Y, P, dof, compute_error=True):
@@ -125,17 +150,28 @@ def _kl_grad(Y, P, dof, compute_error=True):
 
 
 def _gradient_descent(Y, P, dof, it, n_iter, n_iter_check, n_iter_without_progress, momentum,
-                      learning_rate, min_gain, min_grad_norm):
-    update = torch.zeros_like(Y)
-    gains = torch.ones_like(Y)
+                      learning_rate, min_gain, min_grad_norm, angle=None):
+    """Gradient descent with momentum and per-coordinate gains (reference
+    ``_t_sne.py:_gradient_descent``).  ``angle=None``: exact gradient on the
+    device tensors; otherwise Barnes-Hut on host arrays (Y numpy, P CSR)."""
+    bh = angle is not None
+    xp = np if bh else torch
+    update = xp.zeros_like(Y)
+    gains = xp.ones_like(Y)
     error = best = np.finfo(float).max
     best_iter = i = it
     for i in range(it, n_iter):
         check = (i + 1) % n_iter_check == 0
-        kl, g = _kl_grad(Y, P, dof, check)
-        gn = float(torch.linalg.norm(g))
-        inc = (update * g) < 0.0
-        gains = torch.where(inc, gains + 0.2, gains * 0.8).clamp(min=min_gain)
+        if bh:
+            kl, g = _kl_grad_bh(Y, P, dof, angle, check)
+            gn = float(np.linalg.norm(g))
+            inc = (update * g) < 0.0
+            gains = np.maximum(np.where(inc, gains + 0.2, gains * 0.8), min_gain)
+        else:
+            kl, g = _kl_grad(Y, P, dof, check)
+            gn = float(torch.linalg.norm(g))
+            inc = (update * g) < 0.0
+            gains = torch.where(inc, gains + 0.2, gains * 0.8).clamp(min=min_gain)
         g = g * gains
         update = momentum * update - learning_rate * g
         Y = Y + update
@@ -227,9 +263,16 @@ class TSNE(BaseEstimator):
         else:
             raise ValueError("'init' must be 'pca', 'random', or a numpy array")
         dof = max(self.n_components - 1, 1)
-        Y = torch.as_tensor(np.asarray(Y0, dtype=np.float64), device=dev)
         kw = dict(n_iter_check=50, min_gain=0.01, min_grad_norm=self.min_grad_norm,
                   learning_rate=lr)
+        if self.method == "barnes_hut":
+            if self.n_components > 3:
+                raise ValueError("'n_components' should be inferior to 4 for the barnes_hut "
+                                 "algorithm as it relies on quad-tree or oct-tree.")
+            Y = np.array(Y0, dtype=np.float64)
+            kw["angle"] = float(self.angle)
+        else:
+            Y = torch.as_tensor(np.asarray(Y0, dtype=np.float64), device=dev)
         Y, kl, it = _gradient_descent(Y, P * self.early_exaggeration, dof, 0, 250,
                                       n_iter_without_progress=250, momentum=0.5, **kw)
         if it < 250 or self.n_iter - 250 > 0:
@@ -239,7 +282,7 @@ class TSNE(BaseEstimator):
         self.kl_divergence_ = kl
         self.n_iter_ = it
         self.n_features_in_ = X.shape[1]
-        return Y.cpu().numpy()
+        return Y if isinstance(Y, np.ndarray) else Y.cpu().numpy()
 
     def fit_transform(self, X, y=None):
         self.embedding_ = self._fit(X)

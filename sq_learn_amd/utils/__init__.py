@@ -51,4 +51,5 @@ from .class_weight import compute_class_weight, compute_sample_weight  # noqa: E
 from .murmurhash import murmurhash3_32  # noqa: E402,F401
 from .pairwise import gen_batches, gen_even_slices  # noqa: E402,F401
 from .validation import (check_array, check_consistent_length, check_random_state,  # noqa: E402,F401
-                         check_scalar, check_X_y, column_or_1d)
+                         check_scalar, check_X_y, column_or_1d, check_memory,
+                         check_non_negative, has_fit_parameter)

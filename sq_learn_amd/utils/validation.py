@@ -292,3 +292,61 @@ def check_scalar(x, name, target_type, *, min_val=None, max_val=None):
         raise ValueError(f"`{name}`= {x}, must be >= {min_val}.")
     if max_val is not None and x > max_val:
         raise ValueError(f"`{name}`= {x}, must be <= {max_val}.")
+
+
+def check_memory(memory):
+    """``memory`` as an object with a joblib.Memory-style ``cache`` method
+    (reference ``utils/validation.py:316``): None or a str path -> a
+    joblib.Memory (identity-caching stub when joblib is absent); objects
+    with ``cache`` pass through."""
+    if memory is None or isinstance(memory, str):
+        try:
+            import joblib
+            return joblib.Memory(location=memory, verbose=0)
+        except ImportError:  # pragma: no cover
+            if memory is not None:
+                raise ValueError("a cache directory needs joblib")
+
+            class _NoCache:
+                location = None
+
+                def cache(self, func=None, **kw):
+                    return func if func is not None else (lambda f: f)
+            return _NoCache()
+    if not hasattr(memory, "cache"):
+        raise ValueError("'memory' should be None, a string or have the same interface as "
+                         "joblib.Memory. Got memory='{}' instead.".format(memory))
+    return memory
+
+
+def has_fit_parameter(estimator, parameter):
+    """Whether ``estimator.fit`` accepts an argument named ``parameter``
+    (reference ``utils/validation.py:1003``)."""
+    import inspect
+    return parameter in inspect.signature(estimator.fit).parameters
+
+
+def check_non_negative(X, whom):
+    """Raise ValueError when ``X`` (dense, sparse or tensor) has a negative
+    entry (reference ``utils/validation.py:1153``)."""
+    import scipy.sparse as sp
+    if sp.issparse(X):
+        data = X.data if X.format in ("csr", "csc", "coo", "bsr") else X.tocsr().data
+        xmin = data.min() if data.size else 0
+        if X.nnz < X.shape[0] * X.shape[1]:
+            xmin = min(xmin, 0)
+    elif isinstance(X, torch.Tensor):
+        xmin = float(X.min()) if X.numel() else 0
+    else:
+        X = np.asarray(X)
+        xmin = X.min() if X.size else 0
+    if xmin < 0:
+        raise ValueError("Negative values in data passed to %s" % whom)
+
+
+def __getattr__(name):
+    # helpers implemented in utils/_misc.py, exposed here like the reference
+    if name in ("indexable", "as_float_array", "assert_all_finite", "check_symmetric"):
+        from . import _misc
+        return getattr(_misc, name)
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
