@@ -9,9 +9,15 @@ Work split (MI355X-first): the Gram / kernel matrix - the only O(n^2 d)
 part - is one fp64 GEMM + epilogue on the resolved device (MFMA on the
 MI355X), the SMO iterations run host-native over it
 (``csrc/host/svm_smo.cpp``), and prediction kernels against the support
-vectors are again device GEMMs.  The dense kernel bounds the training set to
-what an n x n fp64 matrix allows (about 40k rows per 13 GB).
+vectors are again device GEMMs.  Problems whose n x n kernel would exceed
+``SQ_SVM_DENSE_BYTES`` (default 2 GiB: n ~ 16k) or whose input is sparse
+switch to kernel rows computed on demand by the host library (dense or CSR
+rows, never densified) behind an LRU cache of ``cache_size`` MB - the
+reference's libsvm ``Cache`` - so the training-set size is bounded by
+time, not by an n x n matrix.  ``shrinking`` follows libsvm's heuristic.
 """
+
+import os
 
 import numbers
 import warnings
@@ -53,19 +59,74 @@ def kernel_matrix(X, Y, kernel, gamma, degree, coef0, device=None):
     return K.cpu().numpy()
 
 
-def _solve(K, idx, y, p, C, alpha0, eps, max_iter, nu):
+_KTYPE = {"linear": 0, "poly": 1, "rbf": 2, "sigmoid": 3}
+
+
+class _RowKernel:
+    """Kernel of the (reordered) training rows evaluated on demand by the
+    host SMO (``sqh_svm_solve_rows``): dense fp64 rows or CSR."""
+
+    def __init__(self, X, kernel, gamma, degree, coef0, cache_mb):
+        if sp.issparse(X):
+            X = sp.csr_matrix(X, dtype=np.float64)
+            X.sort_indices()
+            self.Xd = None
+            self.indptr = np.ascontiguousarray(X.indptr, dtype=np.int64)
+            self.indices = np.ascontiguousarray(X.indices, dtype=np.int32)
+            self.data = np.ascontiguousarray(X.data, dtype=np.float64)
+        else:
+            self.Xd = np.ascontiguousarray(X, dtype=np.float64)
+            self.indptr = self.indices = self.data = None
+        self.n, self.d = X.shape
+        self.ktype = _KTYPE[kernel]
+        self.gamma, self.degree, self.coef0 = float(gamma), int(degree), float(coef0)
+        self.cache_bytes = int(max(float(cache_mb), 1.0) * 2 ** 20)
+
+    def _ptrs(self):
+        z = 0
+        return (self.Xd.ctypes.data if self.Xd is not None else z,
+                self.indptr.ctypes.data if self.indptr is not None else z,
+                self.indices.ctypes.data if self.indices is not None else z,
+                self.data.ctypes.data if self.data is not None else z)
+
+    def block(self, rows, cols):
+        """K[rows][:, cols] (host, OpenMP)."""
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        out = np.empty((len(rows), len(cols)))
+        _host.lib().sqh_svm_kernel_rows(*self._ptrs(), self.n, self.d, self.ktype, self.gamma,
+                                        self.coef0, self.degree, rows.ctypes.data, len(rows),
+                                        cols.ctypes.data, len(cols), out.ctypes.data)
+        return out
+
+
+def _solve(K, idx, y, p, C, alpha0, eps, max_iter, nu, shrinking=True):
+    """One SMO sub-problem; ``K`` is the dense kernel (numpy) or a
+    :class:`_RowKernel`.  Returns (alpha, rho, r, status)."""
     lib = _host.lib()
-    K = np.ascontiguousarray(K, dtype=np.float64)
     idx = np.ascontiguousarray(idx, dtype=np.int32)
     y = np.ascontiguousarray(y, dtype=np.int8)
     p = np.ascontiguousarray(p, dtype=np.float64)
     C = np.ascontiguousarray(C, dtype=np.float64)
     alpha = np.ascontiguousarray(alpha0, dtype=np.float64).copy()
-    out = np.zeros(4)
-    lib.sqh_svm_solve(K.ctypes.data, K.shape[0], idx.ctypes.data, y.ctypes.data, p.ctypes.data,
-                      C.ctypes.data, len(idx), float(eps), int(max_iter), 1 if nu else 0,
-                      alpha.ctypes.data, out.ctypes.data)
+    out = np.zeros(7)
+    if isinstance(K, _RowKernel):
+        lib.sqh_svm_solve_rows(*K._ptrs(), K.n, K.d, K.ktype, K.gamma, K.coef0, K.degree,
+                               K.cache_bytes, idx.ctypes.data, y.ctypes.data, p.ctypes.data,
+                               C.ctypes.data, len(idx), float(eps), int(max_iter),
+                               1 if nu else 0, int(bool(shrinking)), alpha.ctypes.data,
+                               out.ctypes.data)
+    else:
+        K = np.ascontiguousarray(K, dtype=np.float64)
+        lib.sqh_svm_solve(K.ctypes.data, K.shape[0], idx.ctypes.data, y.ctypes.data,
+                          p.ctypes.data, C.ctypes.data, len(idx), float(eps), int(max_iter),
+                          1 if nu else 0, int(bool(shrinking)), alpha.ctypes.data,
+                          out.ctypes.data)
     return alpha, out[0], out[1], int(out[3])
+
+
+def _dense_limit_bytes():
+    return int(os.environ.get("SQ_SVM_DENSE_BYTES", 2 << 30))
 
 
 def _ovr_decision_function(predictions, confidences, n_classes):
@@ -170,7 +231,10 @@ class BaseLibSVM(BaseEstimator):
             return 0.0
         if isinstance(self.gamma, str):
             if self.gamma == "scale":
-                v = X.var()
+                if sp.issparse(X):
+                    v = X.multiply(X).mean() - X.mean() ** 2
+                else:
+                    v = X.var()
                 return 1.0 / (X.shape[1] * v) if v != 0 else 1.0
             if self.gamma == "auto":
                 return 1.0 / X.shape[1]
@@ -178,16 +242,32 @@ class BaseLibSVM(BaseEstimator):
                              "Got '{}' instead.".format(self.gamma))
         return float(self.gamma)
 
-    def _prep_X(self, X):
+    def _prep_X(self, X, keep_sparse=False):
         if hasattr(X, "detach"):
             X = X.detach().cpu().numpy()
         if sp.issparse(X):
+            if keep_sparse:
+                X = sp.csr_matrix(X, dtype=np.float64)
+                X.sort_indices()
+                return X
             X = X.toarray()
         return np.ascontiguousarray(X, dtype=np.float64)
 
+    def _kernel_source(self, Xs):
+        """Kernel of the training rows ``Xs`` for the SMO: the dense matrix
+        (one device GEMM) when it fits ``SQ_SVM_DENSE_BYTES``, else a
+        :class:`_RowKernel` (rows on demand + LRU cache of ``cache_size``
+        MB); sparse input always takes the row path (never densified)."""
+        n = Xs.shape[0]
+        if self.kernel in _KTYPE and (sp.issparse(Xs) or 8 * n * n > _dense_limit_bytes()):
+            return _RowKernel(Xs, self.kernel, self._gamma, self.degree, self.coef0,
+                              getattr(self, "cache_size", 200))
+        Xd = Xs.toarray() if sp.issparse(Xs) else Xs
+        return self._kernel(Xd, Xd)
+
     def fit(self, X, y, sample_weight=None):
         rnd = check_random_state(self.random_state)
-        X = self._prep_X(X)
+        X = self._prep_X(X, keep_sparse=self.kernel in _KTYPE)
         if X.ndim != 2:
             raise ValueError("Expected 2D array")
         n = X.shape[0]
@@ -227,7 +307,7 @@ class BaseLibSVM(BaseEstimator):
     def _fit_single(self, X, y, sw, keep):
         rows = np.where(keep)[0]
         Xk = X if self.kernel == "precomputed" else X[rows]
-        K = self._kernel(Xk, Xk) if self.kernel != "precomputed" else X[np.ix_(rows, rows)]
+        K = self._kernel_source(Xk) if self.kernel != "precomputed" else X[np.ix_(rows, rows)]
         l = len(rows)
         w = sw[rows]
         ar = np.arange(l, dtype=np.int32)
@@ -241,7 +321,8 @@ class BaseLibSVM(BaseEstimator):
                 nu_l -= alpha[i]
                 i += 1
             a, rho, _, st = _solve(K, ar, np.ones(l), np.zeros(l), C, alpha, self.tol,
-                                   self._max_iter(l), nu=False)
+                                   self._max_iter(l), nu=False,
+                                   shrinking=getattr(self, "shrinking", True))
             coef = a
         elif self._impl == "epsilon_svr":
             C = np.r_[w * self.C, w * self.C]
@@ -249,7 +330,8 @@ class BaseLibSVM(BaseEstimator):
             yy = np.r_[np.ones(l), -np.ones(l)]
             p = np.r_[self.epsilon - y[rows], self.epsilon + y[rows]]
             a, rho, _, st = _solve(K, idx, yy, p, C, np.zeros(2 * l), self.tol,
-                                   self._max_iter(2 * l), nu=False)
+                                   self._max_iter(2 * l), nu=False,
+                                   shrinking=getattr(self, "shrinking", True))
             coef = a[:l] - a[l:]
         else:  # nu_svr
             C = np.r_[w * self.C, w * self.C]
@@ -262,7 +344,8 @@ class BaseLibSVM(BaseEstimator):
             yy = np.r_[np.ones(l), -np.ones(l)]
             p = np.r_[-y[rows], y[rows]]
             a, rho, _, st = _solve(K, idx, yy, p, C, alpha2, self.tol, self._max_iter(2 * l),
-                                   nu=True)
+                                   nu=True,
+                                   shrinking=getattr(self, "shrinking", True))
             coef = a[:l] - a[l:]
         sv = np.where(coef != 0)[0]
         self.support_ = rows[sv].astype(np.int32)
@@ -283,7 +366,8 @@ class BaseLibSVM(BaseEstimator):
             if X.shape[1] != self.shape_fit_[1]:
                 raise ValueError("X.shape[1] = %d should be equal to %d, the number of features "
                                  "at training time" % (X.shape[1], self.shape_fit_[1]))
-            Kx = self._kernel(X, self.support_vectors_)
+            sv = self.support_vectors_
+            Kx = self._kernel(X, sv.toarray() if sp.issparse(sv) else sv)
         return Kx
 
     @property
@@ -301,7 +385,10 @@ class BaseLibSVM(BaseEstimator):
         return coef
 
     def _get_coef(self):
-        return self._dual_coef_ @ self.support_vectors_
+        sv = self.support_vectors_
+        if sp.issparse(sv):
+            return np.asarray((sv.T @ self._dual_coef_.T).T)
+        return self._dual_coef_ @ sv
 
 
 class BaseSVC(ClassifierMixin, BaseLibSVM):
@@ -329,7 +416,7 @@ class BaseSVC(ClassifierMixin, BaseLibSVM):
         order = np.concatenate(groups)
         Kx = order if K_full is not None else None
         K = (K_full[np.ix_(order, order)] if K_full is not None
-             else self._kernel(X[order], X[order]))
+             else self._kernel_source(X[order]))
         start = np.r_[0, np.cumsum(counts)]
         nonzero = np.zeros(len(order), dtype=bool)
         pair_coef, rhos, status = {}, [], 0
@@ -347,7 +434,8 @@ class BaseSVC(ClassifierMixin, BaseLibSVM):
                     C = np.r_[self.C * self.class_weight_[i] * w[:len(si)],
                               self.C * self.class_weight_[j] * w[len(si):]]
                     a, rho, _, st = _solve(K, idx, yy, -np.ones(l), C, np.zeros(l), self.tol,
-                                           self._max_iter(l), nu=False)
+                                           self._max_iter(l), nu=False,
+                                           shrinking=getattr(self, "shrinking", True))
                     coef = a * yy
                 else:
                     C = w.copy()
@@ -362,7 +450,8 @@ class BaseSVC(ClassifierMixin, BaseLibSVM):
                             alpha[t] = min(C[t], sn_)
                             sn_ -= alpha[t]
                     a, rho, r, st = _solve(K, idx, yy, np.zeros(l), C, alpha, self.tol,
-                                           self._max_iter(l), nu=True)
+                                           self._max_iter(l), nu=True,
+                                           shrinking=getattr(self, "shrinking", True))
                     coef = a * yy / r
                     rho = rho / r
                 status = max(status, st)
@@ -418,7 +507,8 @@ class BaseSVC(ClassifierMixin, BaseLibSVM):
             if self._impl == "c_svc":
                 a, rho, _, _ = _solve(K, sub, ytr, -np.ones(len(train)), C * w[train],
                                       np.zeros(len(train)), self.tol, self._max_iter(len(train)),
-                                      nu=False)
+                                      nu=False,
+                                      shrinking=getattr(self, "shrinking", True))
                 coef = a * ytr
             else:
                 C = w[train].copy()
@@ -433,10 +523,15 @@ class BaseSVC(ClassifierMixin, BaseLibSVM):
                         alpha[t] = min(C[t], s2)
                         s2 -= alpha[t]
                 a, rho, r, _ = _solve(K, sub, ytr, np.zeros(len(train)), C, alpha, self.tol,
-                                      self._max_iter(len(train)), nu=True)
+                                      self._max_iter(len(train)), nu=True,
+                                      shrinking=getattr(self, "shrinking", True))
                 coef = a * ytr / r
                 rho = rho / r
-            dec[test] = K[np.ix_(idx[test], sub)] @ coef - rho
+            if isinstance(K, _RowKernel):
+                nz = coef != 0
+                dec[test] = K.block(idx[test], sub[nz]) @ coef[nz] - rho
+            else:
+                dec[test] = K[np.ix_(idx[test], sub)] @ coef - rho
         return _sigmoid_train(dec, yy)
 
     def _ovo_decision(self, X):

@@ -60,7 +60,11 @@ _SIGS = {
     "sqh_hgb_size": (_LL, [_P]),
     "sqh_hgb_copy": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LL]),
     "sqh_hgb_free": (None, [_P]),
-    "sqh_svm_solve": (None, [_P, _LL, _P, _P, _P, _P, _LL, _D, _LL, _I, _P, _P]),
+    "sqh_svm_solve": (None, [_P, _LL, _P, _P, _P, _P, _LL, _D, _LL, _I, _I, _P, _P]),
+    "sqh_svm_solve_rows": (None, [_P, _P, _P, _P, _LL, _LL, _I, _D, _D, _I, _LL, _P, _P, _P, _P,
+                                  _LL, _D, _LL, _I, _I, _P, _P]),
+    "sqh_svm_kernel_rows": (None, [_P, _P, _P, _P, _LL, _LL, _I, _D, _D, _I, _P, _LL, _P, _LL,
+                                   _P]),
     "sqh_linear_svc_dual": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _I, _P, _P, _P]),
     "sqh_linear_svr_dual": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _D, _I, _P, _P]),
     "sqh_linear_mcsvm_cs": (_I, [_P, _LL, _LL, _P, _I, _P, _D, _I, _P, _P]),

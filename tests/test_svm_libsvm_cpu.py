@@ -100,3 +100,64 @@ def test_linear_svc_crammer_singer_is_bit_compatible(data, kw):
     np.testing.assert_allclose(a.intercept_, b.intercept_, atol=1e-10)
     np.testing.assert_array_equal(a.predict(X), b.predict(X))
     assert a.n_iter_ >= 1
+
+
+# ---- kernel-row cache, shrinking and sparse input (csrc/host/svm_smo.cpp)
+@pytest.mark.parametrize("Est,kw", [("SVC", {"kernel": "rbf", "C": 3.0}),
+                                    ("SVC", {"kernel": "poly", "degree": 2}),
+                                    ("NuSVC", {"kernel": "rbf", "nu": 0.05}),
+                                    ("SVR", {"kernel": "rbf", "C": 2.0}),
+                                    ("NuSVR", {"kernel": "linear"}),
+                                    ("OneClassSVM", {"kernel": "rbf", "nu": 0.2})])
+def test_row_kernel_path_matches_dense(monkeypatch, Est, kw):
+    """Kernel rows on demand (tiny LRU cache, forcing evictions) give the
+    dense-kernel solution; sparse input trains without densifying and
+    predicts the same; shrinking off / on agree within the tolerance."""
+    import scipy.sparse as sps
+    import sq_learn_amd.svm as S
+    rs = np.random.RandomState(0)
+    X = rs.randn(160, 6)
+    X[rs.rand(*X.shape) < 0.5] = 0.0
+    if Est in ("SVC", "NuSVC"):
+        y = (X[:, 0] + X[:, 1] ** 2 > 0.3).astype(int) + (X[:, 2] > 0.8)
+    else:
+        y = X[:, 0] - 0.5 * X[:, 1] + 0.1 * rs.randn(160)
+    cls = getattr(S, Est)
+    fit = (lambda e, A: e.fit(A)) if Est == "OneClassSVM" else (lambda e, A: e.fit(A, y))
+    kw = dict(kw, tol=1e-9)   # converge far below the kernel-rounding differences
+    dense = fit(cls(**kw), X)
+    monkeypatch.setenv("SQ_SVM_DENSE_BYTES", "0")
+    rows = fit(cls(cache_size=0.05, **kw), X)
+    # (kernel values differ from the GEMM-formed ones in the last bits, so
+    # a coefficient at ~1e-12 may survive: compare the decision functions)
+    assert len(np.setxor1d(rows.support_, dense.support_)) <= 2
+    f = (lambda e: e.predict(X)) if Est in ("SVR", "NuSVR") else (lambda e: e.decision_function(X))
+    np.testing.assert_allclose(f(rows), f(dense), rtol=1e-6, atol=1e-6)
+    Xs = sps.csr_matrix(X)
+    sparse = fit(cls(**kw), Xs)
+    assert sps.issparse(sparse.support_vectors_)
+    np.testing.assert_allclose(sparse.decision_function(X) if Est != "SVR" and Est != "NuSVR"
+                               else sparse.predict(X),
+                               dense.decision_function(X) if Est != "SVR" and Est != "NuSVR"
+                               else dense.predict(X), rtol=1e-7, atol=1e-8)
+    noshr = fit(cls(shrinking=False, **kw), X)
+    np.testing.assert_allclose(noshr.predict(X) if Est != "OneClassSVM" else noshr.decision_function(X),
+                               dense.predict(X) if Est != "OneClassSVM" else dense.decision_function(X),
+                               rtol=1e-2, atol=5e-2)
+
+
+def test_row_kernel_probability_and_sklearn(monkeypatch):
+    """SVC(probability=True) on the row path (Platt folds from kernel
+    blocks) and agreement with scikit-learn's libsvm (shrinking on)."""
+    import sq_learn_amd.svm as S
+    skl = pytest.importorskip("sklearn.svm")
+    rs = np.random.RandomState(1)
+    X = rs.randn(200, 4)
+    y = (X[:, 0] * X[:, 1] > 0).astype(int)
+    monkeypatch.setenv("SQ_SVM_DENSE_BYTES", "0")
+    a = S.SVC(kernel="rbf", C=2.0, probability=True, random_state=0).fit(X, y)
+    b = skl.SVC(kernel="rbf", C=2.0).fit(X, y)
+    np.testing.assert_allclose(a.decision_function(X), b.decision_function(X), rtol=1e-3,
+                               atol=1e-3)
+    P = a.predict_proba(X)
+    assert P.shape == (200, 2) and np.allclose(P.sum(1), 1.0)
