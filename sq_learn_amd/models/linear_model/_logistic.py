@@ -7,9 +7,12 @@ log-sum-exp); the quasi-Newton driver is scipy's L-BFGS-B on the host with
 the reference's options (gtol = tol, maxiter = max_iter), so the iterates
 follow the reference's lbfgs solver.  'sag' / 'saga' run the reference's
 stochastic average gradient epochs (host-native, :mod:`._sag`; l1 and
-elastic-net through SAGA's proximal step).  'newton-cg' and 'liblinear'
-with an l2 / none penalty solve the same strictly convex problem with the
-L-BFGS driver; liblinear's l1 penalty uses an accelerated proximal gradient
+elastic-net through SAGA's proximal step).  'liblinear' with the l2
+penalty is liblinear's trust-region Newton method (host-native TRON,
+``csrc/host/tron.cpp``; penalised bias column of intercept_scaling) -
+coefficients and n_iter_ as the reference's; 'newton-cg' solves the same
+strictly convex problem with the L-BFGS driver; liblinear's l1 penalty
+uses an accelerated proximal gradient
 (FISTA with backtracking) on the device, minimising
 sum_i w_i loss_i + (1 - r) / (2C) ||W||^2 + r / C ||W||_1."""
 
@@ -208,6 +211,7 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
         sw = _check_sample_weight(sample_weight, X.shape[0])
         sw = np.ones(X.shape[0]) if sw is None else sw.copy()
         cw = _class_weights(self.class_weight, self.classes_, y)
+        sw_raw = sw
         sw = sw * cw[np.searchsorted(self.classes_, y)]
         dev = resolve_device(self.device)
         nf1 = X.shape[1] + int(self.fit_intercept)
@@ -243,20 +247,47 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
                     w0[:warm.shape[1]] = warm[k]
                     if self.fit_intercept:
                         w0[-1] = self.intercept_[k]
-                obj = _Objective(X, t, sw, alpha, self.fit_intercept, False, dev)
-                w, it = solve(obj, w0)
+                if self.solver == "liblinear" and l1 == 0 and np.isfinite(C):
+                    # L2R_LR (liblinear type 0): TRON on the augmented rows,
+                    # the bias column scaled by intercept_scaling and
+                    # penalised like the weights (reference _base.py
+                    # _fit_liblinear, linear.cpp:2320)
+                    # liblinear's one-vs-rest weighs only the positive
+                    # class (weighted_C[k]); the rest keep C (linear.cpp
+                    # train(), nr_class > 2); binary: both classes weighted
+                    Cv = sw * C if n_classes == 2 else \
+                        sw_raw * C * np.where(y == c, cw[k], 1.0)
+                    w, it = self._liblinear_l2(X, t, Cv, w0)
+                else:
+                    obj = _Objective(X, t, sw, alpha, self.fit_intercept, False, dev)
+                    w, it = solve(obj, w0)
                 rows.append(w)
                 its.append(it)
             W = np.vstack(rows)
             self.n_iter_ = np.asarray(its, dtype=np.int32)
         if self.fit_intercept:
             self.intercept_ = W[:, -1].copy()
+            if self.solver == "liblinear" and l1 == 0 and np.isfinite(C):
+                self.intercept_ *= self.intercept_scaling
             self.coef_ = W[:, :-1].copy()
         else:
             self.coef_ = W
             self.intercept_ = np.zeros(W.shape[0])
         self._multi = multi
         return self
+
+    def _liblinear_l2(self, X, t, Cvec, w0):
+        from ..svm._liblinear import primal_tol, tron
+        Xa = np.hstack([X, np.full((X.shape[0], 1), float(self.intercept_scaling))]) \
+            if self.fit_intercept else X
+        if self.fit_intercept and w0 is not None and np.any(w0):
+            w0 = w0.copy()
+            w0[-1] /= self.intercept_scaling
+        w, it = tron(0, Xa, t, Cvec, primal_tol(self.tol, t), self.max_iter, w0=w0)
+        if it >= self.max_iter:
+            warnings.warn("Liblinear failed to converge, increase the number of iterations.",
+                          ConvergenceWarning)
+        return w, it
 
     def _fit_sag(self, X, y, sw, alpha, beta, multi, warm):
         """The reference's stochastic average gradient path (``_logistic.py:

@@ -15,7 +15,6 @@ kept.
 import warnings
 
 import numpy as np
-import scipy.optimize as so
 import scipy.sparse as sp
 
 from ...base import BaseEstimator, ClassifierMixin, RegressorMixin
@@ -65,15 +64,30 @@ def _svc_dual(X, y, C, l1loss, tol, max_iter, stream):
     return w, it
 
 
+def tron(kind, X, y, C, eps, max_iter, p=0.0, w0=None):
+    """liblinear's trust-region Newton method on the primal (host native,
+    ``csrc/host/tron.cpp``): kind 0 L2R_LR, 1 L2R_L2LOSS_SVC, 2
+    L2R_L2LOSS_SVR.  Returns (w, iterations)."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    C = np.ascontiguousarray(np.broadcast_to(C, (X.shape[0],)), dtype=np.float64)
+    w = np.zeros(X.shape[1]) if w0 is None else np.array(w0, dtype=np.float64)
+    it = _host.lib().sqh_tron(X.ctypes.data, X.shape[0], X.shape[1], y.ctypes.data, C.ctypes.data,
+                              int(kind), float(p), float(eps), int(max_iter), w.ctypes.data)
+    return w, int(it)
+
+
+def primal_tol(tol, y):
+    """liblinear's primal stopping tolerance for the classification types:
+    eps * max(min(#pos, #neg), 1) / l (reference ``linear.cpp:2315``)."""
+    pos = int(np.sum(y > 0))
+    return tol * max(min(pos, len(y) - pos), 1) / len(y)
+
+
 def _svc_primal_l2(X, y, C, tol, max_iter):
-    """min 0.5 |w|^2 + sum C_i max(0, 1 - y_i w.x_i)^2 (liblinear type 2)."""
-    def f(w):
-        m = 1 - y * (X @ w)
-        a = np.maximum(m, 0)
-        return 0.5 * w @ w + np.sum(C * a * a), w - 2 * X.T @ (C * a * y)
-    res = so.minimize(f, np.zeros(X.shape[1]), jac=True, method="L-BFGS-B",
-                      options={"maxiter": max_iter, "gtol": tol * 1e-2})
-    return res.x, res.nit
+    """min 0.5 |w|^2 + sum C_i max(0, 1 - y_i w.x_i)^2 (liblinear type 2) by
+    TRON."""
+    return tron(1, X, y, C, primal_tol(tol, y), max_iter)
 
 
 def _svc_primal_l1(X, y, C, tol, max_iter):
@@ -269,16 +283,8 @@ class LinearSVR(RegressorMixin, BaseEstimator):
                 int(self.loss == "epsilon_insensitive"), float(self.epsilon), float(self.tol),
                 int(self.max_iter), stream.h, w.ctypes.data)
         else:
-            eps = self.epsilon
-
-            def f(w):
-                r = Xa @ w - y
-                a = np.maximum(np.abs(r) - eps, 0) * np.sign(r)
-                return 0.5 * w @ w + np.sum(Cvec * a * a), w + 2 * Xa.T @ (Cvec * a)
-
-            res = so.minimize(f, np.zeros(Xa.shape[1]), jac=True, method="L-BFGS-B",
-                              options={"maxiter": self.max_iter, "gtol": self.tol * 1e-2})
-            w, it = res.x, res.nit
+            # L2R_L2LOSS_SVR primal: TRON with eps = tol (reference linear.cpp:2397)
+            w, it = tron(2, Xa, y, Cvec, self.tol, self.max_iter, p=self.epsilon)
         if self.fit_intercept:
             self.coef_ = w[:-1]
             self.intercept_ = np.array([self.intercept_scaling * w[-1]])

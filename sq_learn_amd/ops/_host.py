@@ -44,6 +44,7 @@ _SIGS = {
     "sqh_cholesky_delete": (None, [_P, _LL, _LL, _LL]),
     "sqh_csr_poly": (_LL, [_P, _P, _P, _LL, _LL, _I, _I, _P, _P, _P]),
     "sqh_linkage": (_I, [_P, _LL, _I, _I, _P]),
+    "sqh_tron": (_I, [_P, _LL, _LL, _P, _P, _I, _D, _D, _I, _P]),
     "sqh_tsne_bh_grad": (_D, [_P, _LL, _I, _P, _P, _P, _D, _D, _I, _P]),
     "sqh_enet_cd_dense": (None, [_P, _D, _D, _P, _P, _LL, _LL, _I, _D, _U, _I, _I, _P]),
     "sqh_enet_cd_gram": (None, [_P, _D, _D, _P, _P, _D, _LL, _I, _D, _U, _I, _I, _P]),
