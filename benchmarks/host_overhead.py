@@ -19,14 +19,15 @@ def main():
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     X, _ = make_blobs_device(a.n, a.d, centers=1024, cluster_std=1.0, seed=1, device=dev,
-                             dtype=torch.bfloat16)
+                             dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float32)
     C0 = X[torch.from_numpy(np.random.RandomState(0).choice(a.n, a.k, replace=False)).to(dev)]
-    eng = LloydEngine(X, a.k, delta=0.5, intermediate_error=True, seed=1, gemm_precision="bf16")
+    eng = LloydEngine(X, a.k, delta=0.5, intermediate_error=True, seed=1, gemm_precision=a.dtype)
     eng.set_centers(C0.float())
-    for _ in range(3):
+    for _ in range(8):
         eng.step()[1].tolist()
     torch.cuda.synchronize()
     enq, tot = [], []
