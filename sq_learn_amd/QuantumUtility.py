@@ -6,3 +6,7 @@ quantum-simulation routines (host oracle + batched device samplers).
 """
 from . import quantum as Utility  # noqa: F401
 from .quantum import *  # noqa: F401,F403
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

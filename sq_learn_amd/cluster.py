@@ -13,3 +13,7 @@ from .models.cluster._bicluster import SpectralBiclustering, SpectralCoclusterin
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_bicluster", target="sq_learn_amd.models.cluster._bicluster")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

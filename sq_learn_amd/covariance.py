@@ -484,3 +484,7 @@ __all__ = ["EmpiricalCovariance", "ShrunkCovariance", "LedoitWolf", "OAS", "MinC
            "EllipticEnvelope", "GraphicalLasso", "GraphicalLassoCV", "empirical_covariance",
            "shrunk_covariance", "ledoit_wolf", "ledoit_wolf_shrinkage", "oas", "log_likelihood",
            "graphical_lasso", "fast_mcd"]
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -7,3 +7,7 @@ from .utils.datasets_extra import __all__ as _extra_all  # noqa: E402,F401
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_openml")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

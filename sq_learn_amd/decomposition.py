@@ -12,3 +12,7 @@ from .models.decomposition._dict_learning import (DictionaryLearning,  # noqa: F
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_fastica", "_truncated_svd")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

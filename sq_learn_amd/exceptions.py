@@ -54,3 +54,20 @@ class NumericalGuardError(FloatingPointError):
 
 class UndefinedMetricWarning(UserWarning):
     """A metric is ill-defined (e.g. no positive predictions for precision)."""
+
+
+class ChangedBehaviorWarning(UserWarning):
+    """A class or function changed behaviour since an earlier release."""
+
+
+class NonBLASDotWarning(EfficiencyWarning):
+    """A dot product could not use BLAS (kept for API parity: every product
+    here goes to a library GEMM or a hand-written MFMA kernel)."""
+
+
+class SkipTestWarning(UserWarning):
+    """A test was skipped (estimator_checks)."""
+
+
+class PositiveSpectrumWarning(UserWarning):
+    """Tiny negative eigenvalues of a PSD matrix were set to zero."""

@@ -613,3 +613,7 @@ __all__ = ["f_classif", "f_regression", "r_regression", "chi2", "f_oneway",
            "mutual_info_regression", "mutual_info_classif", "SelectKBest", "SelectPercentile",
            "SelectFpr", "SelectFdr", "SelectFwe", "GenericUnivariateSelect", "VarianceThreshold",
            "SelectFromModel", "RFE", "RFECV", "SequentialFeatureSelector", "SelectorMixin"]
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -3,3 +3,7 @@ from ..models.gaussian_process import GaussianProcessClassifier, GaussianProcess
 from ..models.gaussian_process import kernels  # noqa: F401
 
 __all__ = ["GaussianProcessRegressor", "GaussianProcessClassifier", "kernels"]
+
+from ..utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -346,3 +346,7 @@ class IterativeImputer(TransformerMixin, BaseEstimator):
 
 __all__ = ["SimpleImputer", "MissingIndicator", "KNNImputer", "IterativeImputer",
            "nan_euclidean_distances"]
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

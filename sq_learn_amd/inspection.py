@@ -154,3 +154,7 @@ __all__ = ["permutation_importance", "partial_dependence", "PartialDependenceDis
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_partial_dependence")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

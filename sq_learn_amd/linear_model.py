@@ -5,3 +5,7 @@ from .models.linear_model._lm_extra import GeneralizedLinearRegressor  # noqa: F
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_glm")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -41,3 +41,7 @@ from . import cluster, pairwise  # noqa: F401,E402
 from ._plot import (ConfusionMatrixDisplay, DetCurveDisplay, PrecisionRecallDisplay,  # noqa: F401,E402
                     RocCurveDisplay, plot_confusion_matrix, plot_det_curve,
                     plot_precision_recall_curve, plot_roc_curve)
+
+from ..utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

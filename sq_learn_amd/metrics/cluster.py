@@ -5,3 +5,4 @@ from ..utils.metrics import adjusted_rand_score  # noqa: F401,E402
 
 from ..utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_bicluster")
+from ..utils._ref_api import check_number_of_labels  # noqa: E402,F401

@@ -31,3 +31,5 @@ def nan_euclidean_distances(X, Y=None, *, squared=False, missing_values=np.nan, 
     D /= cnt
     D *= X.shape[1]
     return D if squared else np.sqrt(D, out=D)
+from ..utils._ref_api import (check_paired_arrays, check_pairwise_arrays,  # noqa: E402,F401
+                              distance_metrics, kernel_metrics)

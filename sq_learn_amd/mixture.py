@@ -409,3 +409,7 @@ __all__ = ["GaussianMixture", "BayesianGaussianMixture"]
 
 
 from ._bayesian_mixture import BayesianGaussianMixture  # noqa: E402,F401
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -1088,6 +1088,13 @@ class GeneralizedLinearRegressor(TweedieRegressor):
                                                "verbose")}
 
     def fit(self, X, y, sample_weight=None):
+        from ..._loss.glm_distribution import TweedieDistribution
+        if isinstance(self.family, TweedieDistribution):
+            if self.solver != "lbfgs":
+                raise ValueError("GeneralizedLinearRegressor supports only solvers 'lbfgs'; "
+                                 "got {0}".format(self.solver))
+            self.power = self.family.power
+            return super().fit(X, y, sample_weight=sample_weight)
         if self.family not in self._FAMILY_POWER:
             raise ValueError("The family must be an instance of class ExponentialDispersionModel "
                              "or an element of ['normal', 'poisson', 'gamma', "

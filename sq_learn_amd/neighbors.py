@@ -4,3 +4,7 @@ from .models.neighbors import __all__  # noqa: F401
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_lof")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -282,3 +282,7 @@ def minmax_scale(X, feature_range=(0, 1), *, axis=0, copy=True):
 
 from ..utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_data", "_label")
+
+from ..utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

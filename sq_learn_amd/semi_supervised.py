@@ -302,3 +302,7 @@ __all__ = ["LabelPropagation", "LabelSpreading", "SelfTrainingClassifier"]
 
 from .utils._aliases import alias_submodules  # noqa: E402
 alias_submodules(__name__, "_self_training")
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

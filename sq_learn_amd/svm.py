@@ -23,3 +23,7 @@ def l1_min_c(X, y, *, loss="squared_hinge", fit_intercept=True, intercept_scalin
         raise ValueError("Ill-posed l1_min_c calculation: l1 will always select zero "
                          "coefficients for this data")
     return 0.5 / den if loss == "squared_hinge" else 2.0 / den
+
+from .utils._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

@@ -2,6 +2,14 @@
 model selection, tracing, checkpointing."""
 
 
+def _ref_internal_names():
+    """Base classes / internals exposed only for reference-layout imports
+    (utils._aliases.REF_NAMES): abstract in the reference, so not listed by
+    all_estimators."""
+    from ._aliases import REF_NAMES
+    return {n for d in REF_NAMES.values() for n in d} | {"BaseRandomProjection"}
+
+
 def all_estimators(type_filter=None):
     """(name, class) of every public estimator of the framework (reference
     ``utils/__init__.py:1098``: crawls the package for ``BaseEstimator``
@@ -27,7 +35,7 @@ def all_estimators(type_filter=None):
         for cname, cls in inspect.getmembers(m, inspect.isclass):
             if (issubclass(cls, BaseEstimator) and cls is not BaseEstimator
                     and not cname.startswith("_") and cls.__module__.startswith("sq_learn_amd")
-                    and not inspect.isabstract(cls)):
+                    and not inspect.isabstract(cls) and cname not in _ref_internal_names()):
                 found[cls] = cname
     items = sorted(((n, c) for c, n in found.items()), key=lambda t: (t[0], t[1].__module__))
     # aliases (qMeans_ = QMeans) collapse to one entry per class
@@ -53,3 +61,7 @@ from .pairwise import gen_batches, gen_even_slices  # noqa: E402,F401
 from .validation import (check_array, check_consistent_length, check_random_state,  # noqa: E402,F401
                          check_scalar, check_X_y, column_or_1d, check_memory,
                          check_non_negative, has_fit_parameter)
+
+from ._aliases import alias_reference_layout  # noqa: E402
+
+alias_reference_layout(__name__)

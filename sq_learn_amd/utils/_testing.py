@@ -319,3 +319,47 @@ class MinimalTransformer:
 __all__ = ["assert_raises", "assert_raises_regexp", "assert_array_equal", "assert_almost_equal",
            "assert_array_almost_equal", "assert_array_less", "assert_approx_equal",
            "assert_allclose", "assert_run_python_script", "SkipTest"]
+
+
+def assert_warns_div0(func, *args, **kw):
+    """func(*args) must emit a RuntimeWarning about division by zero /
+    invalid values (or none at all, where the platform does not warn)."""
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        result = func(*args, **kw)
+    msgs = [str(w.message) for w in rec if issubclass(w.category, RuntimeWarning)]
+    if rec and not any(("divide" in m) or ("invalid value" in m) for m in msgs):
+        raise AssertionError(f"expected a division-by-zero warning, got {msgs}")
+    return result
+
+
+def check_docstring_parameters(func, doc=None, ignore=None):
+    """Names of the signature parameters of ``func`` that its numpydoc
+    ``Parameters`` section does not document (and vice versa), as a list of
+    error strings (empty = consistent)."""
+    import inspect
+    ignore = set(ignore or ())
+    try:
+        sig = inspect.signature(func)
+    except (TypeError, ValueError):
+        return []
+    params = [p for p in sig.parameters if p not in ("self", "cls", "args", "kwargs")
+              and p not in ignore]
+    text = doc if doc is not None else (inspect.getdoc(func) or "")
+    m = re.search(r"Parameters\n-+\n(.*?)(\n\n[A-Z][a-z]+\n-+\n|\Z)", text, re.S)
+    documented = []
+    if m:
+        for line in m.group(1).split("\n"):
+            mm = re.match(r"^(\w+)\s*(:|$)", line)
+            if mm:
+                documented.append(mm.group(1))
+    documented = [d for d in documented if d not in ignore]
+    errors = []
+    if m and params != documented:
+        missing = [p for p in params if p not in documented]
+        extra = [d for d in documented if d not in params]
+        if missing:
+            errors.append(f"{getattr(func, '__qualname__', func)}: undocumented {missing}")
+        if extra:
+            errors.append(f"{getattr(func, '__qualname__', func)}: documented but absent {extra}")
+    return errors

@@ -247,3 +247,86 @@ def _infer_dimension(spectrum, n_samples):
     for rank in range(1, spectrum.shape[0]):
         ll[rank] = _assess_dimension(spectrum, rank, n_samples)
     return int(ll.argmax())
+
+
+def density(w, **kwargs):
+    """Fraction of non-zero entries of a vector / (sparse) matrix."""
+    import scipy.sparse as _sp
+    if hasattr(w, "toarray") and _sp.issparse(w):
+        return float(w.nnz) / (w.shape[0] * w.shape[1])
+    w = np.asarray(w)
+    return 0.0 if w.size == 0 else float((w != 0).sum()) / w.size
+
+
+def weighted_mode(a, w, *, axis=0):
+    """Most frequent value along ``axis`` with weights ``w`` (ties: the
+    smallest value).  Returns (mode, score) with the reduced axis kept as
+    size 1, like scipy.stats.mode."""
+    if axis is None:
+        a, w, axis = np.ravel(a), np.ravel(w), 0
+    else:
+        a, w = np.asarray(a), np.asarray(w)
+    if a.shape != w.shape:
+        w = np.full(a.shape, w, dtype=w.dtype)
+    scores = np.unique(np.ravel(a))
+    shape = list(a.shape)
+    shape[axis] = 1
+    oldmost = np.zeros(shape)
+    oldcounts = np.zeros(shape)
+    for score in scores:
+        template = np.zeros(a.shape)
+        ind = a == score
+        template[ind] = w[ind]
+        counts = np.expand_dims(np.sum(template, axis), axis)
+        mostfrequent = np.where(counts > oldcounts, score, oldmost)
+        oldcounts = np.maximum(counts, oldcounts)
+        oldmost = mostfrequent
+    return mostfrequent, oldcounts
+
+
+def cartesian(arrays, out=None):
+    """All combinations of the input 1-D arrays as rows (first array varies
+    slowest)."""
+    arrays = [np.asarray(x) for x in arrays]
+    dtype = np.result_type(*arrays)
+    grids = np.meshgrid(*arrays, indexing="ij")
+    res = np.stack([g.reshape(-1) for g in grids], axis=1).astype(dtype, copy=False)
+    if out is not None:
+        out[...] = res
+        return out
+    return res
+
+
+def log_logistic(X, out=None):
+    """log(1 / (1 + exp(-x))) computed stably elementwise (2-D input, as the
+    reference)."""
+    X = np.asarray(X, dtype=np.float64)
+    is_1d = X.ndim == 1
+    X = np.atleast_2d(X)
+    res = -np.logaddexp(0.0, -X)
+    if out is not None:
+        out[...] = res.reshape(out.shape)
+        return out
+    return res[0] if is_1d else res
+
+
+def softmax(X, copy=True):
+    """Row-wise softmax (in place unless ``copy``)."""
+    X = np.array(X, dtype=np.float64, copy=True) if copy else X
+    X -= X.max(axis=1)[:, None]
+    np.exp(X, X)
+    X /= X.sum(axis=1)[:, None]
+    return X
+
+
+def make_nonnegative(X, min_value=0):
+    """X shifted so that its minimum is at least ``min_value``."""
+    X = np.asarray(X)
+    min_ = X.min()
+    if min_ < min_value:
+        import scipy.sparse as _sp
+        if _sp.issparse(X):
+            raise ValueError("Cannot make the data matrix nonnegative because it is sparse."
+                             " Adding a value to every entry would make it dense.")
+        X = X + (min_value - min_)
+    return X

@@ -38,3 +38,9 @@ def delayed(function):
 
 
 __all__ = ["delayed"]
+
+
+# numpy / scipy names the reference re-exports from its fixes module
+from numpy import linspace  # noqa: E402,F401
+from numpy.ma import MaskedArray  # noqa: E402,F401
+from scipy.stats import loguniform  # noqa: E402,F401
