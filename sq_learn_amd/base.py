@@ -62,12 +62,41 @@ def _same_param(a, b):
         return False
 
 
+def _validate_fit_y_sw(est, X, y, sample_weight):
+    """Target / sample-weight half of the fit contract (reference
+    ``check_X_y`` / ``_check_sample_weight`` / ``check_classification_targets``)
+    for host arrays: a float y must be finite; a classifier refuses a
+    continuous target; sample_weight is a scalar or a 1-D array with one
+    entry per row."""
+    n = X.shape[0] if isinstance(X, np.ndarray) and X.ndim >= 1 else None
+    if y is not None and not isinstance(y, torch.Tensor) and hasattr(y, "__len__") \
+            and not hasattr(y, "toarray"):
+        ya = np.asarray(y)
+        if ya.dtype.kind == "f" and ya.size and not np.isfinite(ya).all():
+            raise ValueError("Input y contains NaN or infinity.")
+        if ya.dtype.kind == "c":
+            raise ValueError("Complex data not supported")
+        if getattr(est, "_estimator_type", None) == "classifier" and ya.dtype.kind == "f" \
+                and ya.ndim == 1 and ya.size and np.any(ya != np.round(ya)):
+            from .utils.multiclass import check_classification_targets
+            check_classification_targets(ya)
+    if sample_weight is not None and n is not None and not np.isscalar(sample_weight) \
+            and not isinstance(sample_weight, torch.Tensor):
+        sw = np.asarray(sample_weight)
+        if sw.ndim != 1:
+            raise ValueError("Sample weights must be 1D array or scalar")
+        if sw.shape[0] != n:
+            raise ValueError(f"sample_weight.shape == {sw.shape}, expected {(n,)}!")
+
+
 def _validate_fit_X(est, X):
     """The reference's ``check_array`` contract at ``fit`` for dense numeric
     host arrays (``utils/validation.py:477-760``): at least one sample and one
     feature, no NaN unless the estimator's ``allow_nan`` tag says so, never
     infinity.  Device tensors / sharded arrays are validated by the device
     layer (``models/_data.py``), other input kinds by the estimators."""
+    if isinstance(X, np.ndarray) and X.dtype.kind == "c":
+        raise ValueError("Complex data not supported")
     if not isinstance(X, np.ndarray) or X.ndim != 2 or X.dtype.kind not in "fiub":
         return
     tags = est._get_tags()
@@ -89,12 +118,22 @@ def _validate_fit_X(est, X):
 
 
 def _validating_fit(fit):
+    try:
+        names = [p for p in inspect.signature(fit).parameters][1:]
+    except (TypeError, ValueError):  # pragma: no cover
+        names = []
+    i_y = names.index("y") if "y" in names else None
+    i_sw = names.index("sample_weight") if "sample_weight" in names else None
+
     @functools.wraps(fit)
     def fit_validated(self, *args, **kwargs):
-        if args:
-            _validate_fit_X(self, args[0])
-        elif "X" in kwargs:
-            _validate_fit_X(self, kwargs["X"])
+        X = args[0] if args else kwargs.get("X")
+        if X is not None:
+            _validate_fit_X(self, X)
+            y = args[i_y] if i_y is not None and len(args) > i_y else kwargs.get("y")
+            sw = (args[i_sw] if i_sw is not None and len(args) > i_sw
+                  else kwargs.get("sample_weight"))
+            _validate_fit_y_sw(self, X, y, sw)
         return fit(self, *args, **kwargs)
     fit_validated._sq_validated = True
     return fit_validated

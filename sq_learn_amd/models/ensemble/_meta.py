@@ -387,6 +387,9 @@ class IsolationForest(OutlierMixin, BaseBagging):
     def score_samples(self, X):
         check_is_fitted(self, "estimators_")
         X = _dense(X)
+        if X.ndim != 2:
+            raise ValueError(f"Expected 2D array, got {X.ndim}D array instead. Reshape your data "
+                             "either using array.reshape(-1, 1) or array.reshape(1, -1).")
         if X.shape[1] != self.n_features_in_:
             raise ValueError("X has %d features, but IsolationForest is expecting %d features "
                              "as input." % (X.shape[1], self.n_features_in_))
@@ -405,8 +408,9 @@ class IsolationForest(OutlierMixin, BaseBagging):
         return self.score_samples(X) - self.offset_
 
     def predict(self, X):
-        out = np.ones(np.asarray(X).shape[0], dtype=int)
-        out[self.decision_function(X) < 0] = -1
+        dec = self.decision_function(X)
+        out = np.ones(dec.shape[0], dtype=int)
+        out[dec < 0] = -1
         return out
 
 
