@@ -95,6 +95,10 @@ __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, co
 __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
                                        long long, void*);
 __attribute__((weak)) int sq_sum_f32(const void*, long long, void*, int, void*, void*);
+// kmpp.hip
+__attribute__((weak)) int sq_kmpp_grid(long long);
+__attribute__((weak)) int sq_kmpp_trials(const void*, long long, int, long long, int, const void*,
+                                         const void*, const void*, void*, void*, void*);
 // estep_f32.hip
 __attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, void*, void*, void*,
                                        void*, void*, int, void*, long long, int, int, double,
@@ -373,6 +377,22 @@ static PyObject* py_fill_mind(PyObject*, PyObject* a) {
   return ret(sq_fill_mind(P(X), ldx, P(Cm), d, P(lab), P(mind), n, P(st)));
 }
 
+static PyObject* py_kmpp_grid(PyObject*, PyObject* a) {
+  long long n;
+  if (!PyArg_ParseTuple(a, "L", &n)) return nullptr;
+  CHECK(sq_kmpp_grid)
+  return PyLong_FromLong(sq_kmpp_grid(n));
+}
+
+static PyObject* py_kmpp_trials(PyObject*, PyObject* a) {
+  unsigned long long X, cand, closest, w, D, part, st; long long ldx, n; int d, t;
+  if (!PyArg_ParseTuple(a, "KLiLiKKKKKK", &X, &ldx, &d, &n, &t, &cand, &closest, &w, &D, &part,
+                        &st))
+    return nullptr;
+  CHECK(sq_kmpp_trials)
+  return ret(sq_kmpp_trials(P(X), ldx, d, n, t, P(cand), P(closest), P(w), P(D), P(part), P(st)));
+}
+
 static PyObject* py_sum_f32(PyObject*, PyObject* a) {
   unsigned long long v, part, out, st; long long n; int extra;
   if (!PyArg_ParseTuple(a, "KLKiKK", &v, &n, &part, &extra, &out, &st)) return nullptr;
@@ -515,6 +535,8 @@ static PyMethodDef methods[] = {
     {"estep_x64", py_estep_x64, METH_VARARGS, "certified filter E-step + fp64 re-check"},
     {"fill_mind", py_fill_mind, METH_VARARGS, "exact distance to the label for marked rows"},
     {"sum_f32", py_sum_f32, METH_VARARGS, "deterministic sum of a float vector"},
+    {"kmpp_grid", py_kmpp_grid, METH_VARARGS, "k-means++ trial pass grid size"},
+    {"kmpp_trials", py_kmpp_trials, METH_VARARGS, "k-means++ trial distances + potentials"},
     {"band_rows_f64", py_band_rows_f64, METH_VARARGS, "fp64 re-selection of overflow rows"},
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},

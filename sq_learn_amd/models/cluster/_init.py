@@ -14,8 +14,11 @@ closest-distance column are device tensors; the data-dependent parts are
 three small collectives per centre on a multi-rank run (all-gather of the
 shard totals of the potential, owner-contributes all-reduce of the t
 candidate rows, all-reduce of the t trial potentials).  The per-centre
-work is one pass over the shard: ``X C^T`` for the t candidates (library
-GEMM, exact fp32) fused with the min / block-sum epilogue in torch.
+work is one pass over the shard: on the GPU the fused trial kernel
+(``csrc/kmpp.hip``: direct-form fp32 distances to the t candidates, the
+t potentials as fixed-order fp64 block partials, distances written
+transposed so the winner's column is contiguous); elsewhere ``X C^T``
+(library GEMM) with the min / sum epilogue in torch.
 
 ``kmeans_parallel`` is k-means|| (Bahmani et al. 2012), an option the
 reference does not have: O(log phi) oversampling rounds of ~l = 2k rows
@@ -33,6 +36,7 @@ import torch
 
 from .._data import Data, gather_rows
 from ...ops import linalg as L
+from ...ops import kmeans as K
 from ...runtime.rng import RngKey
 
 
@@ -110,11 +114,29 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     pot_rows = closest if w is None else closest * w
     total = pot_rows.sum()
     current_pot = comm.all_reduce_(total.clone().reshape(1))[0]
+    # fused HIP trial pass (csrc/kmpp.hip): one HBM pass over the shard per
+    # centre, no [n, t] temporaries; the torch path below is the CPU / odd-
+    # shape fallback
+    native = (dev.type == "cuda" and Xf.dtype == torch.float32 and Xf.dim() == 2
+              and Xf.stride(1) == 1 and Xf.stride(0) == data.d and data.d % 4 == 0
+              and Xf.data_ptr() % 16 == 0 and 1 <= t <= 16)
+    D = part = None
     for c in range(1, k):
         vals = draws[c - 1] * current_pot
         cs = torch.cumsum(pot_rows, 0)
         cand_ids = _search_device(data, cs, total, vals)
         cands = _gather_rows_device(data, cand_ids).to(Xf.dtype)
+        if native:
+            D, pots = K.kmpp_trials_native(Xf, cands.contiguous(), closest, w, D, part)
+            comm.all_reduce_(pots)
+            best = torch.argmin(pots)
+            current_pot = pots[best]
+            closest = torch.minimum(closest, D.index_select(0, best.reshape(1))[0].double())
+            pot_rows = closest if w is None else closest * w
+            total = pot_rows.sum()
+            centers[c] = cands.index_select(0, best.reshape(1))[0]
+            ids[c] = cand_ids.index_select(0, best.reshape(1))[0]
+            continue
         newd = torch.minimum(closest[:, None], _sq_dist(Xf, cands, xn).double())   # [n_loc, t]
         pots = (newd if w is None else newd * w[:, None]).sum(0)
         comm.all_reduce_(pots)

@@ -676,3 +676,33 @@ def sum_f32_native(v, n, part, out, extra=0):
                               nat.stream_handle(v.device))
     if rc:
         raise RuntimeError(f"sum_f32 failed (hip error {rc})")
+
+
+# ------------------------------------------------- k-means++ trial pass
+def kmpp_trials_native(Xf, cand, closest, w=None, D=None, part=None):
+    """One greedy k-means++ step's trial pass (csrc/kmpp.hip): returns
+    (D fp32 [t, n] squared distances of every row to every candidate,
+    pots fp64 [t] = sum_i w_i min(closest_i, D[j, i]) over this shard,
+    summed over the kernel's block partials in a fixed order).  ``D`` /
+    ``part`` may be passed in to reuse buffers."""
+    n, ldx = Xf.shape
+    t, d = cand.shape
+    if n == 0:
+        return (torch.empty((t, 0), dtype=torch.float32, device=Xf.device),
+                torch.zeros(t, dtype=torch.float64, device=Xf.device))
+    assert Xf.dtype == torch.float32 and Xf.stride(1) == 1 and Xf.stride(0) == ldx
+    assert cand.dtype == torch.float32 and cand.is_contiguous() and d == ldx and d % 4 == 0
+    assert Xf.data_ptr() % 16 == 0 and 1 <= t <= 16
+    assert closest.dtype == torch.float64 and closest.numel() == n and closest.is_contiguous()
+    assert w is None or (w.dtype == torch.float64 and w.numel() == n and w.is_contiguous())
+    m = nat.native()
+    grid = m.kmpp_grid(int(n))
+    if D is None or D.shape != (t, n):
+        D = torch.empty((t, n), dtype=torch.float32, device=Xf.device)
+    if part is None or part.numel() < grid * t:
+        part = torch.empty(grid * t, dtype=torch.float64, device=Xf.device)
+    m.kmpp_trials(Xf.data_ptr(), int(ldx), int(d), int(n), int(t), cand.data_ptr(),
+                  closest.data_ptr(), 0 if w is None else w.data_ptr(), D.data_ptr(),
+                  part.data_ptr(), nat.stream_handle(Xf.device))
+    pots = part[:grid * t].view(grid, t).sum(0)
+    return D, pots
