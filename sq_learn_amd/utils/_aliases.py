@@ -72,7 +72,7 @@ REF_LAYOUT = {
     "sq_learn_amd.semi_supervised": ["_label_propagation"],
     "sq_learn_amd.svm": ["_base", "_bounds", "_classes", "_qSVM"],
     "sq_learn_amd.tree": ["_export", "_reingold_tilford"],
-    "sq_learn_amd.utils": ["_encode", "_estimator_html_repr", "_mocking", "_pprint"],
+    "sq_learn_amd.utils": ["_encode", "_estimator_html_repr", "_pprint"],
 }
 
 

@@ -138,3 +138,25 @@ def test_dmeans_labels_estimation_band():
     mins = D.min(1)
     assert all(D[i, l] <= mins[i] + 0.5 for i, l in enumerate(lab))
     assert np.isclose(inertia, mins.sum())
+
+
+def test_mocking_doubles():
+    from sq_learn_amd.utils._mocking import (CheckingClassifier, MockDataFrame,
+                                             NoSampleWeightWrapper)
+    from sq_learn_amd.model_selection import cross_val_score
+    from sq_learn_amd.linear_model import LogisticRegression
+    X = np.arange(40.0).reshape(20, 2)
+    y = np.arange(20) % 2
+    df = MockDataFrame(X)
+    assert len(df) == 20 and isinstance(df.iloc[:5], MockDataFrame)
+    assert np.asarray(df.iloc[:5]).shape == (5, 2)
+    clf = CheckingClassifier(check_X=lambda A: A.shape[1] == 2, foo_param=2).fit(X, y)
+    assert (clf.predict(X) == 0).all() and clf.score() == 1.0
+    with pytest.raises(AssertionError):
+        CheckingClassifier(check_X=lambda A: False).fit(X, y)
+    with pytest.raises(AssertionError):
+        CheckingClassifier(expected_fit_params=["spam"]).fit(X, y)
+    s = cross_val_score(CheckingClassifier(foo_param=2), X, y, cv=2)
+    assert np.all(s == 1.0)
+    w = NoSampleWeightWrapper(LogisticRegression()).fit(X, y)
+    assert w.predict(X).shape == (20,)
