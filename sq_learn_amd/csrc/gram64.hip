@@ -10,8 +10,9 @@
 // range in k-steps of 4 rows; the 16-column fragment of block b for the
 // k-step - lane l: X[r0 + (l >> 4)][16 b + (l & 15)] - is BOTH the A operand
 // (A[i][k] = X[r0+k][16 bi + i]) of block row bi and the B operand of block
-// column bj; a wave's fragments for the next k-step are loaded (L1/L2: the
-// 8 waves read the same rows) while its NB + 1 block MFMAs run.
+// column bj; a wave loads its fragments of a k-step (L1/L2: the 8 waves
+// read the same rows) and runs its NB + 1 block MFMAs on them; the second
+// wave of each SIMD covers the load latency of the first.
 // Each workgroup writes its partial upper blocks; the host side sums the
 // partials in a fixed order (deterministic).  f64 C/D layout: lane l,
 // register r -> (row (l >> 4) + 4 r, col l & 15).
@@ -62,8 +63,11 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
   f64x4 acc[SLOTS];
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) acc[t] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  double fb[2][SLOTS], fa1[2], fa2[2];
-  auto load = [&](long long r0, int buf) {
+  // one fragment buffer per k-step (a runtime-indexed [2][SLOTS] double
+  // buffer lived in scratch: 320 B / lane of private traffic per k-step);
+  // the other wave of the SIMD covers this wave's load latency
+  double fb[SLOTS], fa1, fa2;
+  for (long long r0 = r_begin; r0 < r_end; r0 += 4) {
     const long long r = r0 + q4;
     const bool ok = r < r_end;
     const T* xr = X + (size_t)(ok ? r : r_begin) * ldx;
@@ -72,22 +76,16 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
       return (ok && col < d) ? to_f64(xr[col]) - m : 0.0;
     };
 #pragma unroll
-    for (int t = 0; t < SLOTS; ++t) fb[buf][t] = t < nslot ? ld(colblk(t), mcol[t]) : 0.0;
-    fa1[buf] = ld(i1, ma1);
-    fa2[buf] = ld(i2, ma2);
-  };
-  if (r_begin < r_end) load(r_begin, 0);
-  int cur = 0;
-  for (long long r0 = r_begin; r0 < r_end; r0 += 4) {
-    if (r0 + 4 < r_end) load(r0 + 4, cur ^ 1);
+    for (int t = 0; t < SLOTS; ++t) fb[t] = t < nslot ? ld(colblk(t), mcol[t]) : 0.0;
+    fa1 = ld(i1, ma1);
+    fa2 = ld(i2, ma2);
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) {
       if (t < nslot) {   // wave-uniform
-        const double a = t < n1 ? fa1[cur] : fa2[cur];
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[cur][t], acc[t], 0, 0, 0);
+        const double a = t < n1 ? fa1 : fa2;
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[t], acc[t], 0, 0, 0);
       }
     }
-    cur ^= 1;
   }
   // partial upper blocks of this workgroup: block (bi, bj) at linear id
   // bi * NB - bi (bi - 1) / 2 + (bj - bi)

@@ -69,14 +69,14 @@ def gram64_native(X, mean=None):
                              nat.stream_handle(X.device))
     if rc:
         raise RuntimeError(f"gram64 failed (hip error {rc})")
-    blocks = part.sum(0)
-    Gp = torch.zeros((nb * 16, nb * 16), dtype=torch.float64, device=X.device)
-    iu = torch.triu_indices(nb, nb).tolist()
-    for t, (bi, bj) in enumerate(zip(*iu)):
-        Gp[16 * bi:16 * bi + 16, 16 * bj:16 * bj + 16] = blocks[t]
-        if bi != bj:
-            Gp[16 * bj:16 * bj + 16, 16 * bi:16 * bi + 16] = blocks[t].T
-    return Gp[:d, :d].contiguous()
+    blocks = part.sum(0)                                   # [nblk, 16, 16], fixed order
+    # scatter the upper blocks and their transposes in two indexed copies
+    # (was one tiny copy per block: ~270 launches per call)
+    iu = torch.triu_indices(nb, nb, device=X.device)
+    G4 = torch.zeros((nb, nb, 16, 16), dtype=torch.float64, device=X.device)
+    G4[iu[1], iu[0]] = blocks.transpose(1, 2)
+    G4[iu[0], iu[1]] = blocks                              # diagonal blocks: the upper copy
+    return G4.permute(0, 2, 1, 3).reshape(nb * 16, nb * 16)[:d, :d].contiguous()
 
 
 def gram64_local(X, mean=None, W=None, chunk_rows=1 << 19):
