@@ -104,7 +104,7 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     rs = random_state
     center_id = int(rs.randint(n))
     draws = torch.as_tensor(rs.random_sample((max(k - 1, 0), t)), dtype=torch.float64, device=dev)
-    w = None if sample_weight is None else sample_weight.to(torch.float64).to(dev)
+    w = None if sample_weight is None else sample_weight.to(torch.float64).to(dev).contiguous()
     ids = torch.empty(k, dtype=torch.int64, device=dev)
     ids[0] = center_id
     c0 = gather_rows(data, [center_id]).to(Xf.dtype)
