@@ -260,28 +260,20 @@ def density(w, **kwargs):
 
 def weighted_mode(a, w, *, axis=0):
     """Most frequent value along ``axis`` with weights ``w`` (ties: the
-    smallest value).  Returns (mode, score) with the reduced axis kept as
-    size 1, like scipy.stats.mode."""
+    smallest value; no positive weight at all: 0).  Returns (mode, score)
+    with the reduced axis kept as size 1, like scipy.stats.mode."""
     if axis is None:
         a, w, axis = np.ravel(a), np.ravel(w), 0
     else:
         a, w = np.asarray(a), np.asarray(w)
     if a.shape != w.shape:
-        w = np.full(a.shape, w, dtype=w.dtype)
-    scores = np.unique(np.ravel(a))
-    shape = list(a.shape)
-    shape[axis] = 1
-    oldmost = np.zeros(shape)
-    oldcounts = np.zeros(shape)
-    for score in scores:
-        template = np.zeros(a.shape)
-        ind = a == score
-        template[ind] = w[ind]
-        counts = np.expand_dims(np.sum(template, axis), axis)
-        mostfrequent = np.where(counts > oldcounts, score, oldmost)
-        oldcounts = np.maximum(counts, oldcounts)
-        oldmost = mostfrequent
-    return mostfrequent, oldcounts
+        w = np.broadcast_to(w, a.shape)
+    values = np.unique(a)                                   # ascending
+    totals = np.stack([np.where(a == v, w, 0).sum(axis=axis) for v in values])
+    first_max = np.argmax(totals, axis=0)                   # first = smallest value
+    best = np.take_along_axis(totals, first_max[None], 0)[0]
+    mode = np.where(best > 0, values[first_max], 0).astype(float)
+    return np.expand_dims(mode, axis), np.expand_dims(np.maximum(best, 0).astype(float), axis)
 
 
 def cartesian(arrays, out=None):
