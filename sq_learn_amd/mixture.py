@@ -167,7 +167,13 @@ def _estimate_log_gaussian_prob(X, means, pc, covariance_type):
     return -0.5 * (d * np.log(2 * np.pi) + log_prob) + log_det
 
 
-class GaussianMixture(DensityMixin, BaseEstimator):
+class BaseMixture(DensityMixin, BaseEstimator):
+    """Base of the mixture models (reference ``mixture/_base.py``): EM
+    estimators exposing fit / predict / predict_proba / score_samples /
+    sample."""
+
+
+class GaussianMixture(BaseMixture):
     def __init__(self, n_components=1, *, covariance_type="full", tol=1e-3, reg_covar=1e-6,
                  max_iter=100, n_init=1, init_params="kmeans", weights_init=None,
                  means_init=None, precisions_init=None, random_state=None, warm_start=False,

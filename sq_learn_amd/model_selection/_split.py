@@ -129,7 +129,16 @@ class StratifiedKFold(_BaseKFold):
         return super().split(X, y, groups)
 
 
-class ShuffleSplit(BaseCrossValidator):
+class BaseShuffleSplit(BaseCrossValidator):
+    """Base of the random-permutation splitters (reference
+    ``model_selection/_split.py`` BaseShuffleSplit): ``n_splits`` independent
+    train / test draws."""
+
+    def get_n_splits(self, X=None, y=None, groups=None):
+        return self.n_splits
+
+
+class ShuffleSplit(BaseShuffleSplit):
     def __init__(self, n_splits=10, *, test_size=None, train_size=None, random_state=None):
         self.n_splits = n_splits
         self.test_size = test_size

@@ -7,7 +7,7 @@ def _ref_internal_names():
     (utils._aliases.REF_NAMES): abstract in the reference, so not listed by
     all_estimators."""
     from ._aliases import REF_NAMES
-    return {n for d in REF_NAMES.values() for n in d} | {"BaseRandomProjection"}
+    return {n for d in REF_NAMES.values() for n in d} | {"BaseRandomProjection", "BaseMixture"}
 
 
 def all_estimators(type_filter=None):

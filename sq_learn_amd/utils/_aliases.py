@@ -136,11 +136,14 @@ REF_NAMES = {
         "barycenter_kneighbors_graph":
             "sq_learn_amd.models.manifold._embed:barycenter_kneighbors_graph",
         "null_space": "sq_learn_amd.models.manifold._embed:null_space"},
+    "sq_learn_amd.tree": {"Sentinel": _R + "Sentinel"},
+    "sq_learn_amd.mixture": {},
     "sq_learn_amd.svm": {"BaseLibSVM": "sq_learn_amd.models.svm._libsvm:BaseLibSVM",
                          "BaseSVC": "sq_learn_amd.models.svm._libsvm:BaseSVC"},
     "sq_learn_amd.utils": {n: _R + n for n in (
         "axis0_safe_slice", "tosequence", "indices_to_mask", "check_matplotlib_support",
-        "check_pandas_support", "KeyValTuple", "KeyValTupleParam", "estimator_html_repr")},
+        "check_pandas_support", "KeyValTuple", "KeyValTupleParam", "estimator_html_repr",
+        "MissingValues")},
 }
 REF_NAMES["sq_learn_amd.utils"]["get_chunk_n_rows"] = "sq_learn_amd.utils.pairwise:get_chunk_n_rows"
 _GB = "sq_learn_amd.models.ensemble._gb:"
@@ -171,6 +174,7 @@ REF_NAMES["sq_learn_amd.linear_model"] = {
     "BaseSGDClassifier": _LM + "_stochastic_gradient:BaseSGDClassifier",
     "BaseSGDRegressor": _LM + "_stochastic_gradient:BaseSGDRegressor",
     "get_auto_step_size": _LM + "_sag:get_auto_step_size",
+    "LinearModelCV": _LM + "_coordinate_descent:_LinearModelCV",
     "sag_solver": _LM + "_sag:sag_solver"}
 REF_NAMES["sq_learn_amd.gaussian_process"] = {
     "KernelOperator": "sq_learn_amd.models.gaussian_process.kernels:KernelOperator"}

@@ -345,6 +345,33 @@ def strip_newsgroup_footer(text):
     return text
 
 
+class MissingValues(tuple):
+    """(nan, none): which missing-value markers a set of categories holds
+    (reference ``utils/_encode.py``)."""
+
+    def __new__(cls, nan=False, none=False):
+        return super().__new__(cls, (bool(nan), bool(none)))
+
+    nan = property(lambda self: self[0])
+    none = property(lambda self: self[1])
+
+    def to_list(self):
+        out = []
+        if self.none:
+            out.append(None)
+        if self.nan:
+            out.append(np.nan)
+        return out
+
+
+class Sentinel:
+    """Default ``out_file`` marker of export_graphviz (reference
+    ``tree/_export.py``): prints as the literal default file name."""
+
+    def __repr__(self):
+        return '"tree.dot"'
+
+
 # --------------------------------------------------------------- repr helpers
 class KeyValTuple(tuple):
     """A (key, value) pair the estimator pretty-printer renders as k: v."""
