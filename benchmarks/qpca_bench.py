@@ -1,0 +1,37 @@
+"""qPCA full fit with the quantum extras on the headline matrix (10M x 256
+fp32, 1 GPU): wall-clock of the second (warm) fit.
+python benchmarks/qpca_bench.py [--n N --solver full|randomized]"""
+import argparse
+import time
+
+import torch
+
+from sq_learn_amd.models.decomposition import QPCA
+from sq_learn_amd.parallel.comm import Comm
+from sq_learn_amd.parallel.sharding import ShardedArray
+from sq_learn_amd.utils.datasets import make_blobs_device
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--solver", default="full")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    X, _ = make_blobs_device(a.n, 256, centers=1024, cluster_std=1.0, seed=1, device=dev,
+                             dtype=torch.float32)
+    sa = ShardedArray(X, a.n, 0, Comm(None))
+    q = QPCA(n_components=16, svd_solver=a.solver, random_state=0, device=dev).fit(sa)
+    theta = 0.5 * float(q.singular_values_[15])
+    for rep in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        q = QPCA(n_components=16, svd_solver=a.solver, random_state=0, device=dev,
+                 quantum_truncated=a.solver != "full")
+        q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True)
+        torch.cuda.synchronize()
+        print(rep, f"qPCA {a.solver} fit {time.perf_counter() - t0:.3f} s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

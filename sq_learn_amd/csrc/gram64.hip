@@ -32,7 +32,7 @@ SQ_DEV double to_f64(uint16_t v) { return (double)bf16_to_f32(v); }   // bf16 bi
 // The A operand of a slot is one of two row fragments (a wave-uniform
 // select), its B operand the fragment of the slot's column block, loaded
 // straight from memory (runtime column, no register-array indexing).
-template <typename T, int NB>
+template <typename T, int NB, bool HAS_MU>
 __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, long long ldx,
                                                      const double* __restrict__ mu, long long n,
                                                      int d, double* __restrict__ part) {
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
   {
     auto mv = [&](int b) -> double {
       const int col = 16 * b + c16;
-      return (mu != nullptr && col < d) ? mu[col] : 0.0;
+      return (HAS_MU && col < d) ? mu[col] : 0.0;
     };
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) mcol[t] = t < nslot ? mv(colblk(t)) : 0.0;
@@ -63,27 +63,77 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
   f64x4 acc[SLOTS];
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) acc[t] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  // one fragment buffer per k-step (a runtime-indexed [2][SLOTS] double
-  // buffer lived in scratch: 320 B / lane of private traffic per k-step);
-  // the other wave of the SIMD covers this wave's load latency
-  double fb[SLOTS], fa1, fa2;
-  for (long long r0 = r_begin; r0 < r_end; r0 += 4) {
-    const long long r = r0 + q4;
-    const bool ok = r < r_end;
-    const T* xr = X + (size_t)(ok ? r : r_begin) * ldx;
-    auto ld = [&](int b, double m) -> double {
-      const int col = 16 * b + c16;
-      return (ok && col < d) ? to_f64(xr[col]) - m : 0.0;
-    };
+  if constexpr (sizeof(T) <= 4 && !HAS_MU) {
+    // fp32 / bf16 input, no centring: the raw values of TWO k-steps are loaded together
+    // (8 rows in flight per wave; 2 x 19 raw registers - the fp64 copies of
+    // both would not fit 2 waves / SIMD) and widened / centred right before
+    // their MFMAs
+    float rA[SLOTS], rB[SLOTS], a1A, a2A, a1B, a2B;
+    for (long long r0 = r_begin; r0 < r_end; r0 += 8) {
+      const long long ra = r0 + q4, rb = r0 + 4 + q4;
+      const bool okA = ra < r_end, okB = rb < r_end;
+      const T* xa = X + (size_t)(okA ? ra : r_begin) * ldx;
+      const T* xb = X + (size_t)(okB ? rb : r_begin) * ldx;
 #pragma unroll
-    for (int t = 0; t < SLOTS; ++t) fb[t] = t < nslot ? ld(colblk(t), mcol[t]) : 0.0;
-    fa1 = ld(i1, ma1);
-    fa2 = ld(i2, ma2);
+      for (int t = 0; t < SLOTS; ++t) {
+        const int col = 16 * colblk(t) + c16;
+        const bool live = t < nslot && col < d;
+        rA[t] = live && okA ? (float)to_f64(xa[col]) : 0.0f;
+        rB[t] = live && okB ? (float)to_f64(xb[col]) : 0.0f;
+      }
+      const int c1 = 16 * i1 + c16, c2 = 16 * i2 + c16;
+      a1A = c1 < d && okA ? (float)to_f64(xa[c1]) : 0.0f;
+      a2A = c2 < d && okA ? (float)to_f64(xa[c2]) : 0.0f;
+      a1B = c1 < d && okB ? (float)to_f64(xb[c1]) : 0.0f;
+      a2B = c2 < d && okB ? (float)to_f64(xb[c2]) : 0.0f;
+      {
+        const double fa1 = okA && c1 < d ? (double)a1A - ma1 : 0.0;
+        const double fa2 = okA && c2 < d ? (double)a2A - ma2 : 0.0;
 #pragma unroll
-    for (int t = 0; t < SLOTS; ++t) {
-      if (t < nslot) {   // wave-uniform
-        const double a = t < n1 ? fa1 : fa2;
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[t], acc[t], 0, 0, 0);
+        for (int t = 0; t < SLOTS; ++t) {
+          if (t < nslot) {
+            const double a = t < n1 ? fa1 : fa2;
+            const double b = okA && 16 * colblk(t) + c16 < d ? (double)rA[t] - mcol[t] : 0.0;
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+          }
+        }
+      }
+      {
+        const double fa1 = okB && c1 < d ? (double)a1B - ma1 : 0.0;
+        const double fa2 = okB && c2 < d ? (double)a2B - ma2 : 0.0;
+#pragma unroll
+        for (int t = 0; t < SLOTS; ++t) {
+          if (t < nslot) {
+            const double a = t < n1 ? fa1 : fa2;
+            const double b = okB && 16 * colblk(t) + c16 < d ? (double)rB[t] - mcol[t] : 0.0;
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+          }
+        }
+      }
+    }
+  } else {
+    // one fragment buffer per k-step (a runtime-indexed [2][SLOTS] double
+    // buffer lived in scratch: 320 B / lane of private traffic per k-step);
+    // the other wave of the SIMD covers this wave's load latency
+    double fb[SLOTS], fa1, fa2;
+    for (long long r0 = r_begin; r0 < r_end; r0 += 4) {
+      const long long r = r0 + q4;
+      const bool ok = r < r_end;
+      const T* xr = X + (size_t)(ok ? r : r_begin) * ldx;
+      auto ld = [&](int b, double m) -> double {
+        const int col = 16 * b + c16;
+        return (ok && col < d) ? to_f64(xr[col]) - m : 0.0;
+      };
+  #pragma unroll
+      for (int t = 0; t < SLOTS; ++t) fb[t] = t < nslot ? ld(colblk(t), mcol[t]) : 0.0;
+      fa1 = ld(i1, ma1);
+      fa2 = ld(i2, ma2);
+  #pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        if (t < nslot) {   // wave-uniform
+          const double a = t < n1 ? fa1 : fa2;
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[t], acc[t], 0, 0, 0);
+        }
       }
     }
   }
@@ -113,8 +163,12 @@ static int launch_gram64(const T* X, long long ldx, const double* mu, long long 
   switch (nb) {
 #define CASE(NB)                                                                        \
   case NB:                                                                              \
-    hipLaunchKernelGGL((gram64_kernel<T, NB>), dim3(grid), dim3(512), 0, st, X, ldx, mu, n, \
-                       d, part);                                                        \
+    if (mu)                                                                             \
+      hipLaunchKernelGGL((gram64_kernel<T, NB, true>), dim3(grid), dim3(512), 0, st, X, ldx, \
+                         mu, n, d, part);                                               \
+    else                                                                                \
+      hipLaunchKernelGGL((gram64_kernel<T, NB, false>), dim3(grid), dim3(512), 0, st, X,     \
+                         ldx, mu, n, d, part);                                          \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
     CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
