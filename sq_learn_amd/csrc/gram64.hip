@@ -41,6 +41,13 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
+  // the mean in LDS (read per MFMA operand by the two-k-step path: 2 x 17
+  // fp64 registers saved), filled before any wave leaves
+  __shared__ double smu[16 * NB];
+  if (HAS_MU) {
+    for (int c = threadIdx.x; c < 16 * NB; c += blockDim.x) smu[c] = c < d ? mu[c] : 0.0;
+    __syncthreads();
+  }
   if (w >= (NB + 1) / 2) return;   // wave-uniform; no block barrier below
   const int i1 = w, i2 = NB - 1 - w;
   const int n1 = NB - w;                         // slots of row i1
@@ -63,8 +70,8 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
   f64x4 acc[SLOTS];
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) acc[t] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  if constexpr (sizeof(T) <= 4 && !HAS_MU) {
-    // fp32 / bf16 input, no centring: the raw values of TWO k-steps are loaded together
+  if constexpr (sizeof(T) <= 4) {
+    // fp32 / bf16 input: the raw values of TWO k-steps are loaded together
     // (8 rows in flight per wave; 2 x 19 raw registers - the fp64 copies of
     // both would not fit 2 waves / SIMD) and widened / centred right before
     // their MFMAs
@@ -87,25 +94,27 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
       a1B = c1 < d && okB ? (float)to_f64(xb[c1]) : 0.0f;
       a2B = c2 < d && okB ? (float)to_f64(xb[c2]) : 0.0f;
       {
-        const double fa1 = okA && c1 < d ? (double)a1A - ma1 : 0.0;
-        const double fa2 = okA && c2 < d ? (double)a2A - ma2 : 0.0;
+        const double fa1 = okA && c1 < d ? (double)a1A - (HAS_MU ? smu[c1] : 0.0) : 0.0;
+        const double fa2 = okA && c2 < d ? (double)a2A - (HAS_MU ? smu[c2] : 0.0) : 0.0;
 #pragma unroll
         for (int t = 0; t < SLOTS; ++t) {
           if (t < nslot) {
             const double a = t < n1 ? fa1 : fa2;
-            const double b = okA && 16 * colblk(t) + c16 < d ? (double)rA[t] - mcol[t] : 0.0;
+            const int cb = 16 * colblk(t) + c16;
+            const double b = okA && cb < d ? (double)rA[t] - (HAS_MU ? smu[cb] : 0.0) : 0.0;
             acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
           }
         }
       }
       {
-        const double fa1 = okB && c1 < d ? (double)a1B - ma1 : 0.0;
-        const double fa2 = okB && c2 < d ? (double)a2B - ma2 : 0.0;
+        const double fa1 = okB && c1 < d ? (double)a1B - (HAS_MU ? smu[c1] : 0.0) : 0.0;
+        const double fa2 = okB && c2 < d ? (double)a2B - (HAS_MU ? smu[c2] : 0.0) : 0.0;
 #pragma unroll
         for (int t = 0; t < SLOTS; ++t) {
           if (t < nslot) {
             const double a = t < n1 ? fa1 : fa2;
-            const double b = okB && 16 * colblk(t) + c16 < d ? (double)rB[t] - mcol[t] : 0.0;
+            const int cb = 16 * colblk(t) + c16;
+            const double b = okB && cb < d ? (double)rB[t] - (HAS_MU ? smu[cb] : 0.0) : 0.0;
             acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
           }
         }
