@@ -104,22 +104,32 @@ SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
 // tail law (given how many fall there, they are iid from it - the multiset,
 // and so the median, has exactly the law of Q independent draws).  Each
 // draw's circular bin distance is bubbled into a sorted register array.
-SQ_DEV void insert_sorted(double (&c)[kIpeMaxQ], double x) {
+// The bin distances are integers: with M < 2^31 (every pair of realistic
+// data - the caller decides per wave) they are kept as uint32 (one register,
+// full-rate v_min_u32 / v_max_u32 compare-exchanges) instead of fp64.
+SQ_DEV uint32_t ce_lo(uint32_t a, uint32_t b) { return min(a, b); }
+SQ_DEV uint32_t ce_hi(uint32_t a, uint32_t b) { return max(a, b); }
+SQ_DEV double ce_lo(double a, double b) { return fmin(a, b); }
+SQ_DEV double ce_hi(double a, double b) { return fmax(a, b); }
+
+template <typename K>
+SQ_DEV void insert_sorted(K (&c)[kIpeMaxQ], K x) {
 #pragma unroll
   for (int i = 0; i < kIpeMaxQ; ++i) {
-    const double lo = fmin(c[i], x);
-    x = fmax(c[i], x);
+    const K lo = ce_lo(c[i], x);
+    x = ce_hi(c[i], x);
     c[i] = lo;
   }
 }
 
+template <typename K>
 SQ_DEV double ae_median_draws(double omega, long long M, int Q, WordStream& ws) {
   const double PI = 3.14159265358979323846;
   const FejerLaw law(omega, M);   // per-pair setup shared by the Q draws
-  double c[kIpeMaxQ];
+  K c[kIpeMaxQ];
 #pragma unroll
-  for (int i = 0; i < kIpeMaxQ; ++i) c[i] = 1e300;
-  auto circ = [&](long long j) -> double { return (double)(j < M - j ? j : M - j); };
+  for (int i = 0; i < kIpeMaxQ; ++i) c[i] = sizeof(K) == 4 ? (K)0xFFFFFFFFu : (K)1e300;
+  auto circ = [&](long long j) -> K { return (K)(j < M - j ? j : M - j); };
   if (law.phi == 0.0 || M <= kFejerSmallM) {
 #pragma nounroll
     for (int q = 0; q < Q; ++q) insert_sorted(c, circ(law.sample(ws)));
@@ -163,8 +173,8 @@ SQ_DEV double ae_median_draws(double omega, long long M, int Q, WordStream& ws) 
   double m1 = 0.0, m0 = 0.0;
 #pragma unroll
   for (int i = 0; i < kIpeMaxQ; ++i) {
-    if (i == Q / 2) m1 = c[i];
-    if (i == Q / 2 - 1) m0 = c[i];
+    if (i == Q / 2) m1 = (double)c[i];
+    if (i == Q / 2 - 1) m0 = (double)c[i];
   }
   const double v1 = sin(PI * m1 / (double)M);
   if (Q & 1) return v1 * v1;
@@ -194,7 +204,11 @@ SQ_DEV float ipe_distance(float ipf, double nx2, double ny2, double eps, int Q, 
                      (1.0 / 9007199254740992.0);
     at = ae_median_walk(omega, M, Q, u);
   } else {
-    at = ae_median_draws(omega, M, Q, ws);
+    // wave-uniform choice of the key type (same draws, same law either way)
+    if (__ballot(M >= (1LL << 31)) == 0ull)
+      at = ae_median_draws<uint32_t>(omega, M, Q, ws);
+    else
+      at = ae_median_draws<double>(omega, M, Q, ws);
   }
   return (float)(2.0 * S * at);
 }
