@@ -17,6 +17,7 @@
 // partials in a fixed order (deterministic).  f64 C/D layout: lane l,
 // register r -> (row (l >> 4) + 4 r, col l & 15).
 #include "common.h"
+#include <type_traits>
 
 namespace sq {
 
@@ -56,92 +57,55 @@ __global__ void __launch_bounds__(512) gram64_kernel(const T* __restrict__ X, lo
   const long long r_begin = (long long)blockIdx.x * per;
   const long long r_end = r_begin + per < n ? r_begin + per : n;
   auto colblk = [&](int t) { return t < n1 ? w + t : t - 1; };
-  double mcol[SLOTS], ma1, ma2;
-  {
-    auto mv = [&](int b) -> double {
-      const int col = 16 * b + c16;
-      return (HAS_MU && col < d) ? mu[col] : 0.0;
-    };
-#pragma unroll
-    for (int t = 0; t < SLOTS; ++t) mcol[t] = t < nslot ? mv(colblk(t)) : 0.0;
-    ma1 = mv(i1);
-    ma2 = mv(i2);
-  }
   f64x4 acc[SLOTS];
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) acc[t] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  if constexpr (sizeof(T) <= 4) {
-    // fp32 / bf16 input: the raw values of TWO k-steps are loaded together
-    // (8 rows in flight per wave; 2 x 19 raw registers - the fp64 copies of
-    // both would not fit 2 waves / SIMD) and widened / centred right before
-    // their MFMAs
-    float rA[SLOTS], rB[SLOTS], a1A, a2A, a1B, a2B;
-    for (long long r0 = r_begin; r0 < r_end; r0 += 8) {
-      const long long ra = r0 + q4, rb = r0 + 4 + q4;
-      const bool okA = ra < r_end, okB = rb < r_end;
-      const T* xa = X + (size_t)(okA ? ra : r_begin) * ldx;
-      const T* xb = X + (size_t)(okB ? rb : r_begin) * ldx;
+  // the raw values of TWO k-steps are loaded together (8 rows in flight per
+  // wave; fp32 / bf16 input: 2 x 19 raw fp32 registers - the fp64 copies of
+  // both would not fit 2 waves / SIMD) and widened / centred right before
+  // their MFMAs; no runtime-indexed register arrays (those live in scratch)
+  using R = typename std::conditional<sizeof(T) == 8, double, float>::type;
+  R rA[SLOTS], rB[SLOTS], a1A, a2A, a1B, a2B;
+  for (long long r0 = r_begin; r0 < r_end; r0 += 8) {
+    const long long ra = r0 + q4, rb = r0 + 4 + q4;
+    const bool okA = ra < r_end, okB = rb < r_end;
+    const T* xa = X + (size_t)(okA ? ra : r_begin) * ldx;
+    const T* xb = X + (size_t)(okB ? rb : r_begin) * ldx;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      const int col = 16 * colblk(t) + c16;
+      const bool live = t < nslot && col < d;
+      rA[t] = live && okA ? (R)to_f64(xa[col]) : (R)0;
+      rB[t] = live && okB ? (R)to_f64(xb[col]) : (R)0;
+    }
+    const int c1 = 16 * i1 + c16, c2 = 16 * i2 + c16;
+    a1A = c1 < d && okA ? (R)to_f64(xa[c1]) : (R)0;
+    a2A = c2 < d && okA ? (R)to_f64(xa[c2]) : (R)0;
+    a1B = c1 < d && okB ? (R)to_f64(xb[c1]) : (R)0;
+    a2B = c2 < d && okB ? (R)to_f64(xb[c2]) : (R)0;
+    {
+      const double fa1 = okA && c1 < d ? (double)a1A - (HAS_MU ? smu[c1] : 0.0) : 0.0;
+      const double fa2 = okA && c2 < d ? (double)a2A - (HAS_MU ? smu[c2] : 0.0) : 0.0;
 #pragma unroll
       for (int t = 0; t < SLOTS; ++t) {
-        const int col = 16 * colblk(t) + c16;
-        const bool live = t < nslot && col < d;
-        rA[t] = live && okA ? (float)to_f64(xa[col]) : 0.0f;
-        rB[t] = live && okB ? (float)to_f64(xb[col]) : 0.0f;
-      }
-      const int c1 = 16 * i1 + c16, c2 = 16 * i2 + c16;
-      a1A = c1 < d && okA ? (float)to_f64(xa[c1]) : 0.0f;
-      a2A = c2 < d && okA ? (float)to_f64(xa[c2]) : 0.0f;
-      a1B = c1 < d && okB ? (float)to_f64(xb[c1]) : 0.0f;
-      a2B = c2 < d && okB ? (float)to_f64(xb[c2]) : 0.0f;
-      {
-        const double fa1 = okA && c1 < d ? (double)a1A - (HAS_MU ? smu[c1] : 0.0) : 0.0;
-        const double fa2 = okA && c2 < d ? (double)a2A - (HAS_MU ? smu[c2] : 0.0) : 0.0;
-#pragma unroll
-        for (int t = 0; t < SLOTS; ++t) {
-          if (t < nslot) {
-            const double a = t < n1 ? fa1 : fa2;
-            const int cb = 16 * colblk(t) + c16;
-            const double b = okA && cb < d ? (double)rA[t] - (HAS_MU ? smu[cb] : 0.0) : 0.0;
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-          }
-        }
-      }
-      {
-        const double fa1 = okB && c1 < d ? (double)a1B - (HAS_MU ? smu[c1] : 0.0) : 0.0;
-        const double fa2 = okB && c2 < d ? (double)a2B - (HAS_MU ? smu[c2] : 0.0) : 0.0;
-#pragma unroll
-        for (int t = 0; t < SLOTS; ++t) {
-          if (t < nslot) {
-            const double a = t < n1 ? fa1 : fa2;
-            const int cb = 16 * colblk(t) + c16;
-            const double b = okB && cb < d ? (double)rB[t] - (HAS_MU ? smu[cb] : 0.0) : 0.0;
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-          }
+        if (t < nslot) {
+          const double a = t < n1 ? fa1 : fa2;
+          const int cb = 16 * colblk(t) + c16;
+          const double b = okA && cb < d ? (double)rA[t] - (HAS_MU ? smu[cb] : 0.0) : 0.0;
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
         }
       }
     }
-  } else {
-    // one fragment buffer per k-step (a runtime-indexed [2][SLOTS] double
-    // buffer lived in scratch: 320 B / lane of private traffic per k-step);
-    // the other wave of the SIMD covers this wave's load latency
-    double fb[SLOTS], fa1, fa2;
-    for (long long r0 = r_begin; r0 < r_end; r0 += 4) {
-      const long long r = r0 + q4;
-      const bool ok = r < r_end;
-      const T* xr = X + (size_t)(ok ? r : r_begin) * ldx;
-      auto ld = [&](int b, double m) -> double {
-        const int col = 16 * b + c16;
-        return (ok && col < d) ? to_f64(xr[col]) - m : 0.0;
-      };
-  #pragma unroll
-      for (int t = 0; t < SLOTS; ++t) fb[t] = t < nslot ? ld(colblk(t), mcol[t]) : 0.0;
-      fa1 = ld(i1, ma1);
-      fa2 = ld(i2, ma2);
-  #pragma unroll
+    {
+      const double fa1 = okB && c1 < d ? (double)a1B - (HAS_MU ? smu[c1] : 0.0) : 0.0;
+      const double fa2 = okB && c2 < d ? (double)a2B - (HAS_MU ? smu[c2] : 0.0) : 0.0;
+#pragma unroll
       for (int t = 0; t < SLOTS; ++t) {
-        if (t < nslot) {   // wave-uniform
+        if (t < nslot) {
           const double a = t < n1 ? fa1 : fa2;
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb[t], acc[t], 0, 0, 0);
+          const int cb = 16 * colblk(t) + c16;
+          const double b = okB && cb < d ? (double)rB[t] - (HAS_MU ? smu[cb] : 0.0) : 0.0;
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
         }
       }
     }
