@@ -11,9 +11,9 @@ centre), generated for all centres up front and shared by every rank.
 Every centre is enqueued on the device with NO host synchronisation: the
 current potential, the candidate ids, the argmin over trials and the
 closest-distance column are device tensors; the data-dependent parts are
-three small collectives per centre on a multi-rank run (all-gather of the
-shard totals of the potential, owner-contributes all-reduce of the t
-candidate rows, all-reduce of the t trial potentials).  The per-centre
+two small collectives per centre on a multi-rank run (owner-contributes
+all-reduce of the t packed candidate rows + ids, all-gather of the per-rank
+t trial potentials, which also carries the next prefix of shard totals).  The per-centre
 work is one pass over the shard: on the GPU the fused trial kernel
 (``csrc/kmpp.hip``: direct-form fp32 distances to the t candidates, the
 t potentials as fixed-order fp64 block partials, distances written
@@ -49,38 +49,43 @@ def _sq_dist(X, C, xn=None):
     return (xn[:, None] + cn[None, :] - 2.0 * (Xf @ Cf.T)).clamp_(min=0.0)
 
 
-def _gather_rows_device(data: Data, ids):
-    """Rows of the global indices ``ids`` (device int64 tensor) on every
-    rank: the owner contributes, one all-reduce, no host sync."""
-    X = data.X
-    lo = data.row_offset
-    loc = (ids - lo).clamp(0, max(data.n_local - 1, 0))
-    mine = (ids >= lo) & (ids < lo + data.n_local)
-    rows = X[loc].to(torch.float64 if X.device.type == "cpu" else torch.float32)
-    rows = torch.where(mine[:, None], rows, torch.zeros_like(rows))
-    data.comm.all_reduce_(rows)
-    return rows
-
-
-def _search_device(data: Data, cs, total_local, vals):
-    """Global row of each value of ``vals`` (device, replicated) in the
-    cumulative potential: shard totals all-gathered, each trial resolved by
-    the rank whose prefix range holds it (searchsorted in its local fp64
-    cumulative sum ``cs``), ids combined by a sum all-reduce."""
+def _pick_candidates(data: Data, cs, prefix, sizes, vals, xdtype):
+    """Candidate rows of the values ``vals`` (device, replicated) in the
+    global cumulative potential, in ONE collective: the rank whose prefix
+    range (prefix[r], prefix[r + 1]] holds a value (first non-empty such rank:
+    left-side search, the reference's ``np.searchsorted``) resolves it in its
+    local fp64 cumulative sum ``cs`` and contributes the row and its global
+    id; one all-reduce of the packed [t, d + 1] block combines them.  An empty
+    shard never owns a value (and never indexes its rows)."""
     comm = data.comm
+    X = data.X
+    t = vals.shape[0]
+    d = data.d
+    wd = torch.float64
     if comm.world_size > 1:
-        tot = torch.cat(comm.all_gather(total_local.reshape(1)))
-        prefix = torch.cat([torch.zeros(1, dtype=tot.dtype, device=tot.device), torch.cumsum(tot, 0)])
-        owner = torch.searchsorted(prefix[1:].contiguous(), vals).clamp(max=comm.world_size - 1)
+        ends = prefix[1:]
+        ok = (ends[None, :] >= vals[:, None]) & (sizes[None, :] > 0)          # [t, W]
+        nz = torch.nonzero(sizes > 0)
+        last = nz[-1, 0] if nz.numel() else torch.zeros((), dtype=torch.int64, device=vals.device)
+        owner = torch.where(ok.any(1), ok.to(torch.int32).argmax(1).to(torch.int64), last)
         local_vals = vals - prefix[comm.rank]
     else:
-        owner = torch.zeros_like(vals, dtype=torch.int64)
+        owner = torch.zeros(t, dtype=torch.int64, device=vals.device)
         local_vals = vals
-    pos = torch.searchsorted(cs, local_vals.contiguous()).clamp(max=max(cs.numel() - 1, 0))
-    ids = torch.where(owner == comm.rank, pos + data.row_offset, torch.zeros_like(pos))
-    if comm.world_size > 1:
-        comm.all_reduce_(ids)
-    return ids.clamp(max=data.n_global - 1)
+    if comm.world_size == 1:
+        pos = torch.searchsorted(cs, local_vals.contiguous()).clamp(0, max(data.n_local - 1, 0))
+        return X[pos].to(xdtype), (pos + data.row_offset).clamp(0, data.n_global - 1)
+    packed = torch.zeros((t, d + 1), dtype=wd, device=X.device)
+    if data.n_local > 0:
+        pos = torch.searchsorted(cs, local_vals.contiguous()).clamp(max=data.n_local - 1)
+        mine = (owner == comm.rank)
+        packed[:, :d] = torch.where(mine[:, None], X[pos].to(wd), torch.zeros((), dtype=wd,
+                                                                             device=X.device))
+        packed[:, d] = torch.where(mine, (pos + data.row_offset).to(wd),
+                                   torch.zeros((), dtype=wd, device=X.device))
+    comm.all_reduce_(packed)   # ids < 2^53: exact in fp64
+    ids = packed[:, d].round().to(torch.int64).clamp(0, data.n_global - 1)
+    return packed[:, :d].to(xdtype), ids
 
 
 def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
@@ -88,7 +93,15 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     """Returns (centers [k, d] tensor on the data device, global indices).
 
     ``sample_weight`` (framework extension, used by k-means||): the potential
-    of a row is w * d^2."""
+    of a row is w * d^2.
+
+    Collectives on a multi-rank run: TWO per centre, both tiny and with no
+    host synchronisation - the all-reduce of the packed candidate rows + ids
+    (``_pick_candidates``) and the all-gather of the per-rank trial
+    potentials [W, t].  The gather gives both the global trial potentials
+    (summed in rank order, identical on every rank) and, at the winning
+    trial, every shard's new potential total - the prefix the next centre's
+    search needs (the former separate all-gather of the shard totals)."""
     X = data.X
     comm = data.comm
     n = data.n_global
@@ -110,10 +123,17 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     c0 = gather_rows(data, [center_id]).to(Xf.dtype)
     centers = torch.empty((k, data.d), dtype=Xf.dtype, device=dev)
     centers[0] = c0[0]
-    closest = _sq_dist(Xf, c0, xn)[:, 0].double()
+    if data.n_local:
+        closest = _sq_dist(Xf, c0, xn)[:, 0].double()
+    else:
+        closest = torch.zeros(0, dtype=torch.float64, device=dev)
     pot_rows = closest if w is None else closest * w
-    total = pot_rows.sum()
-    current_pot = comm.all_reduce_(total.clone().reshape(1))[0]
+    W = comm.world_size
+    # shard potential totals and sizes (one all-gather for the first centre)
+    ts = torch.stack([pot_rows.sum(), torch.tensor(float(data.n_local), dtype=torch.float64,
+                                                   device=dev)])
+    g = torch.stack(comm.all_gather(ts))                                  # [W, 2]
+    totals, sizes = g[:, 0].contiguous(), g[:, 1].contiguous()
     # fused HIP trial pass (csrc/kmpp.hip): one HBM pass over the shard per
     # centre, no [n, t] temporaries; the torch path below is the CPU / odd-
     # shape fallback
@@ -121,30 +141,29 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
               and Xf.stride(1) == 1 and Xf.stride(0) == data.d and data.d % 4 == 0
               and Xf.data_ptr() % 16 == 0 and 1 <= t <= 16)
     D = part = None
+    zero = torch.zeros(1, dtype=torch.float64, device=dev)
     for c in range(1, k):
+        prefix = torch.cat([zero, torch.cumsum(totals, 0)])
+        current_pot = prefix[-1]
         vals = draws[c - 1] * current_pot
         cs = torch.cumsum(pot_rows, 0)
-        cand_ids = _search_device(data, cs, total, vals)
-        cands = _gather_rows_device(data, cand_ids).to(Xf.dtype)
+        cands, cand_ids = _pick_candidates(data, cs, prefix, sizes, vals, Xf.dtype)
         if native:
-            D, pots = K.kmpp_trials_native(Xf, cands.contiguous(), closest, w, D, part)
-            comm.all_reduce_(pots)
-            best = torch.argmin(pots)
-            current_pot = pots[best]
-            closest = torch.minimum(closest, D.index_select(0, best.reshape(1))[0].double())
-            pot_rows = closest if w is None else closest * w
-            total = pot_rows.sum()
-            centers[c] = cands.index_select(0, best.reshape(1))[0]
-            ids[c] = cand_ids.index_select(0, best.reshape(1))[0]
-            continue
-        newd = torch.minimum(closest[:, None], _sq_dist(Xf, cands, xn).double())   # [n_loc, t]
-        pots = (newd if w is None else newd * w[:, None]).sum(0)
-        comm.all_reduce_(pots)
+            D, pots_loc = K.kmpp_trials_native(Xf, cands.contiguous(), closest, w, D, part)
+        else:
+            newd = torch.minimum(closest[:, None], _sq_dist(Xf, cands, xn).double())   # [n_loc, t]
+            pots_loc = (newd if w is None else newd * w[:, None]).sum(0)
+        allp = torch.stack(comm.all_gather(pots_loc.reshape(t)))          # [W, t]
+        pots = allp[0].clone()
+        for r in range(1, W):                                             # rank order: replicated
+            pots += allp[r]
         best = torch.argmin(pots)
-        current_pot = pots[best]
-        closest = newd.index_select(1, best.reshape(1))[:, 0].contiguous()
+        totals = allp.index_select(1, best.reshape(1))[:, 0].contiguous()
+        if native:
+            closest = torch.minimum(closest, D.index_select(0, best.reshape(1))[0].double())
+        else:
+            closest = newd.index_select(1, best.reshape(1))[:, 0].contiguous()
         pot_rows = closest if w is None else closest * w
-        total = pot_rows.sum()
         centers[c] = cands.index_select(0, best.reshape(1))[0]
         ids[c] = cand_ids.index_select(0, best.reshape(1))[0]
     return centers, ids.cpu().numpy()

@@ -411,6 +411,7 @@ class LloydEngine:
                 self.comm.all_reduce_(self.packed)
             if events is not None:
                 events[1].record()
+            self._last_counts = self.packed[self.k * self.d:self.k * self.d + self.k]
             with tracing.range("finalize"):
                 K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
                                            self.shift, self.k, self.d, self._noise_bound(),
@@ -456,6 +457,8 @@ class LloydEngine:
         kd = self.k * self.d
         sums = packed[:kd].reshape(self.k, self.d)
         counts = packed[kd:kd + self.k]
+        self._last_counts = counts
+        self._C_prev = self.C
         tot_inertia = packed[-1]
         old = self.C
         new = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1e-300)[:, None],
@@ -502,6 +505,7 @@ class LloydEngine:
             self.comm.all_reduce_(self.packed)
         if events is not None:
             events[1].record()
+        self._last_counts = self.packed[self.k * self.d:self.k * self.d + self.k]
         with tracing.range("finalize"):
             K.centroid_finalize_native(self.packed, self.C, self.C_new, self.C_bf16, self.cn,
                                        self.shift, self.k, self.d, self._noise_bound(),
@@ -572,29 +576,34 @@ class LloydEngine:
                 "allreduce": ev[2].elapsed_time(ev[3]), "finalize": ev[3].elapsed_time(ev[4]),
                 "step_wall": wall}
 
-    def _relocate(self, labels):
+    def _undo_update(self):
+        """Back to the centres the last M-step started from (the relocation
+        re-runs that M-step; the finalize recomputes every derived operand)."""
+        if self.fast:
+            self.C, self.C_new = self.C_new, self.C
+        else:
+            self.C = self._C_prev
+
+    def _relocate(self, labels, counts):
         """Empty-cluster relocation of the classical Lloyd step (reference
-        ``cluster/_k_means_fast.pyx:162-200``): each cluster left without rows
-        by the E-step takes one of the rows farthest from their own centre
+        ``cluster/_k_means_fast.pyx:162-200``): each cluster the M-step left
+        without weight takes one of the rows farthest from their own centre
         (the row moves: old cluster loses it, the empty one gets it - the
-        reference's sums / weights update, expressed as a relabel).  Row
-        sharded: per-shard top-e distances, one all-gather,
-        the same global pick on every rank, the owner relabels its row."""
-        k = self.k
-        lab = labels[:self.n].long()
-        w = self.sample_weight
-        cnt = torch.zeros(k, dtype=torch.float64, device=self.device)
-        valid = lab >= 0
-        cnt.index_add_(0, lab.clamp(min=0), (w.double() if w is not None else
-                                              torch.ones(self.n, dtype=torch.float64,
-                                                         device=self.device)) * valid)
-        self.comm.all_reduce_(cnt)
-        empty = torch.nonzero(cnt == 0)[:, 0]
+        reference's sums / weights update, expressed as a relabel before the
+        M-step is re-run).  Row sharded: per-shard top-e distances, one
+        all-gather, the same device-side global order on every
+        rank (descending distance, ascending global row), the owner relabels
+        its rows.  Only runs when the M-step's global counts (already
+        all-reduced) show an empty cluster."""
+        dev = self.device
+        empty = torch.nonzero(counts == 0)[:, 0]
         e = int(empty.numel())
         if e == 0:
             return labels
+        lab = labels[:self.n].long()
+        valid = lab >= 0
         C = self.C.double()
-        d = torch.empty(self.n, dtype=torch.float64, device=self.device)
+        d = torch.empty(self.n, dtype=torch.float64, device=dev)
         X = self.X
         step = 1 << 19
         for s0 in range(0, self.n, step):
@@ -605,33 +614,56 @@ class LloydEngine:
         vals, idx = torch.topk(d, m) if m > 0 else (d[:0], lab[:0])
         rows = idx + self.row_offset
         if m < e:   # pad so every rank sends e entries
-            vals = torch.cat([vals, torch.full((e - m,), -2.0, dtype=vals.dtype, device=vals.device)])
-            rows = torch.cat([rows, torch.full((e - m,), -1, dtype=rows.dtype, device=rows.device)])
+            vals = torch.cat([vals, torch.full((e - m,), -2.0, dtype=vals.dtype, device=dev)])
+            rows = torch.cat([rows, torch.full((e - m,), -1, dtype=rows.dtype, device=dev)])
         allv = torch.cat(self.comm.all_gather(vals))
         allr = torch.cat(self.comm.all_gather(rows))
-        # descending distance, ascending row on ties: the same order everywhere
-        order = sorted(range(allv.numel()), key=lambda i: (-float(allv[i]), int(allr[i])))[:e]
-        for j, i in enumerate(order):
-            g = int(allr[i])
-            if g < 0:
-                continue
-            loc = g - self.row_offset
-            if 0 <= loc < self.n:
-                labels[loc] = int(empty[j])
-                if getattr(self, "bounds", False):
-                    self.lb[loc] = 0.0   # label moved: re-evaluate next E-step
+        # global order on the device: ascending row, then (stable) descending
+        # distance - identical on every rank
+        o1 = torch.argsort(allr, stable=True)
+        o2 = torch.argsort(-allv[o1], stable=True)
+        order = o1[o2][:e]
+        g = allr[order]
+        loc = g - self.row_offset
+        mine = (g >= 0) & (loc >= 0) & (loc < self.n)
+        li = loc[mine]
+        newlab = empty[mine]
+        if li.numel():
+            if getattr(self, "incremental", False) and self.buf.corr is not None:
+                # the per-cluster inertia counts a row at its label's (old)
+                # centre: bring a relocated row back to its min distance
+                xr = X[li].double()
+                dnew = ((xr - C[newlab]) ** 2).sum(1)
+                self.buf.corr[li] = (d[li] - dnew).to(self.buf.corr.dtype)
+            labels[li] = newlab.to(labels.dtype)
+            if getattr(self, "bounds", False):
+                self.lb[li] = 0.0   # label moved: re-evaluate next E-step
         self.n_relocated += e
         return labels
 
     def step(self):
-        """One Lloyd iteration; returns (labels, scalars_tensor)."""
+        """One Lloyd iteration; returns (labels, scalars_tensor).
+
+        With empty-cluster relocation the scalars come back as a host tensor:
+        the iteration's single device->host read carries the number of
+        empty clusters of the M-step's (global) counts as well, and only when
+        it is non-zero is the M-step re-run after the relocation."""
         labels, mind, inertia = self._estep(self._key("band_select"))
         if self.failure_prob > 0:
             # SURVEY.md §5.3: Bernoulli estimation failures (+ resampling)
             failure_inject_(labels, self.k, self.failure_prob, self.failure_attempts,
                             self._key("failure"), self.row_offset, self.failure_counters)
-        if self.relocate_empty:
-            labels = self._relocate(labels)
         sc = self.mstep(labels, inertia)
+        if self.relocate_empty:
+            counts = self._last_counts
+            ne = (counts == 0).sum().to(torch.float64).reshape(1)
+            vals = torch.cat([sc.reshape(-1)[:3].to(torch.float64), ne]).cpu()
+            if vals[3] > 0:
+                self._undo_update()
+                labels = self._relocate(labels, counts.clone())
+                sc = self.mstep(labels, inertia)
+                vals = torch.cat([sc.reshape(-1)[:3].to(torch.float64),
+                                  torch.zeros(1, dtype=torch.float64, device=sc.device)]).cpu()
+            sc = vals
         self.it += 1
         return labels, sc

@@ -443,10 +443,11 @@ class QPCA(_BasePCA):
         if sharded and isinstance(A, torch.Tensor) and comm is not None and comm.distributed:
             n_glob = int(self.n_samples_)
             if not true_tomography:
-                # Frobenius budget over the GLOBAL r x n matrix; offset keeps
-                # the ranks' Philox elements disjoint
-                return gaussian_tomography(A, delta, key, offset=int(self._row_offset) * A.shape[0],
-                                           numel=A.shape[0] * n_glob)
+                # Frobenius budget over the GLOBAL r x n matrix; element (i, j)
+                # draws Philox element i * n_global + row_offset + j - the
+                # unsharded draw (shard invariant)
+                return gaussian_tomography(A, delta, key, offset=int(self._row_offset),
+                                           numel=A.shape[0] * n_glob, row_stride=n_glob)
             return tomography_long(A, delta, key, norm=norm,
                                    stop_when_reached_accuracy=stop_when_reached_accuracy,
                                    incremental_measure=incremental_measure,

@@ -193,6 +193,8 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
         if not isinstance(self.max_iter, numbers.Number) or self.max_iter < 0:
             raise ValueError("Maximum number of iteration must be positive; got (max_iter=%r)"
                              % self.max_iter)
+        import scipy.sparse as _sp
+        self._sparse_fit = _sp.issparse(X)
         X = _as_dense64(X).astype(np.float64)
         y = np.asarray(y)
         if y.ndim != 1:
@@ -308,7 +310,8 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
             target = np.searchsorted(self.classes_, y).astype(np.float64)
             coef, it, _ = sag_solver(X, target, sw, "multinomial", alpha, beta, self.max_iter,
                                      self.tol, self.verbose, self.random_state, False, max_sq,
-                                     {"coef": w0.T}, is_saga=saga)
+                                     {"coef": w0.T}, is_saga=saga,
+                                     sparse_input=getattr(self, "_sparse_fit", False))
             self.n_iter_ = np.array([it], dtype=np.int32)
             return coef[1][None, :] if n_classes == 2 else coef
         pos = self.classes_[1:] if n_classes == 2 else self.classes_
@@ -322,7 +325,8 @@ class LogisticRegression(LinearClassifierMixin, SparseCoefMixin, BaseEstimator):
             t = np.where(y == c, 1.0, -1.0)
             coef, it, _ = sag_solver(X, t, sw, "log", alpha, beta, self.max_iter, self.tol,
                                      self.verbose, self.random_state, False, max_sq,
-                                     {"coef": w0[:, None]}, is_saga=saga)
+                                     {"coef": w0[:, None]}, is_saga=saga,
+                                     sparse_input=getattr(self, "_sparse_fit", False))
             rows.append(coef)
             its.append(it)
         self.n_iter_ = np.asarray(its, dtype=np.int32)

@@ -41,12 +41,20 @@ def get_auto_step_size(max_squared_sum, alpha_scaled, loss, fit_intercept, n_sam
 
 def sag_solver(X, y, sample_weight=None, loss="log", alpha=1.0, beta=0.0, max_iter=1000,
                tol=0.001, verbose=0, random_state=None, check_input=True, max_squared_sum=None,
-               warm_start_mem=None, is_saga=False):
-    """Returns (coef_, n_iter_, warm_start_mem) like the reference."""
+               warm_start_mem=None, is_saga=False, sparse_input=None):
+    """Returns (coef_, n_iter_, warm_start_mem) like the reference.
+    ``sparse_input`` (callers that densified a sparse X themselves): apply
+    the sparse dataset's intercept decay; default: ``sp.issparse(X)``."""
     if warm_start_mem is None:
         warm_start_mem = {}
     if max_iter is None:
         max_iter = 1000
+    # sparse input: the reference's make_dataset damps the intercept updates
+    # (SPARSE_INTERCEPT_DECAY, linear_model/_base.py:206); the solver runs on
+    # the dense rows with that decay
+    if sparse_input is None:
+        sparse_input = sp.issparse(X)
+    intercept_decay = 0.01 if sparse_input else 1.0
     if sp.issparse(X):
         X = X.toarray()
     X = np.ascontiguousarray(X, dtype=np.float64)
@@ -79,7 +87,7 @@ def sag_solver(X, y, sample_weight=None, loss="log", alpha=1.0, beta=0.0, max_it
                          % (loss, sorted(_LOSSES)))
     it = _host.lib().sqh_sag(X.ctypes.data, y.ctypes.data, sw.ctypes.data, n, d, K,
                              _LOSSES[loss], alpha_scaled, beta_scaled, step, int(max_iter),
-                             float(tol), int(fit_intercept), 1.0, int(bool(is_saga)),
+                             float(tol), int(fit_intercept), intercept_decay, int(bool(is_saga)),
                              seed & 0xFFFFFFFF, W.ctypes.data, b.ctypes.data)
     if it < 0:
         raise ValueError("Floating-point under-/overflow occurred at epoch #%d. Scaling input "

@@ -59,6 +59,8 @@ def gram64_native(X, mean=None):
     n, d = X.shape
     assert X.dtype in (torch.float32, torch.float64, torch.bfloat16) and X.stride(1) == 1 and d <= 256
     code = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2}[X.dtype]
+    if n == 0:   # an empty shard contributes an exact zero (the kernel writes nothing)
+        return torch.zeros((d, d), dtype=torch.float64, device=X.device)
     nb = (d + 15) // 16
     nblk = nb * (nb + 1) // 2
     grid = int(max(1, min(256, (n + 255) // 256)))

@@ -29,16 +29,24 @@ from ..runtime.rng import RngKey
 from .reference import check_measure
 
 
-def gaussian_tomography(A, noise, key: RngKey, offset=0, numel=None):
+def gaussian_tomography(A, noise, key: RngKey, offset=0, numel=None, row_stride=None):
     """A + TN(+-noise/sqrt(numel)) per component (Frobenius budget; ``numel``
-    defaults to A.numel(), pass the global count for a shard of a matrix)."""
+    defaults to A.numel(), pass the global count for a shard of a matrix).
+    Element (i, j) draws Philox element ``offset + i * row_stride + j``
+    (``row_stride`` defaults to the row length): a column shard of an
+    r x n_global matrix passes row_stride = n_global and offset = its first
+    column, so every element draws the value it draws unsharded."""
     from ..ops.random import trunc_normal_add_
     if noise == 0:
         return A
     out = A.clone() if A.dtype in (torch.float32, torch.float64) else A.float()
     out = out.contiguous()
     b = float(noise) / math.sqrt(out.numel() if numel is None else numel)
-    trunc_normal_add_(out.view(-1), b, key, offset=offset)
+    if row_stride is None or out.dim() != 2 or row_stride == out.shape[1]:
+        trunc_normal_add_(out.view(-1), b, key, offset=offset)
+    else:
+        for i in range(out.shape[0]):
+            trunc_normal_add_(out[i], b, key, offset=offset + i * int(row_stride))
     return out
 
 

@@ -95,6 +95,16 @@ def _worker(rank, world, port, outdir, case):
             np.testing.assert_allclose(q.singular_values_, qr.singular_values_, rtol=1e-8)
             np.testing.assert_allclose(q.estimate_s_values, qr.estimate_s_values, rtol=1e-12)
             assert abs(q.muA - qr.muA) < 1e-9 * qr.muA
+            # Gaussian tomography of the row-sharded left vectors draws the
+            # Philox element (vector, GLOBAL row): the unsharded tensor fit's
+            # noise, element for element
+            qt = QPCA(n_components=3, svd_solver="full", random_state=0, device="cpu").fit(
+                torch.as_tensor(Z), eps=0.01, theta_major=1e-3, delta=0.1, estimate_all=True,
+                true_tomography=False)
+            left = torch.as_tensor(np.asarray(q.estimate_left_sv))
+            fullL = torch.cat(comm.all_gather_varlen(left.T.contiguous())).T.numpy()
+            np.testing.assert_allclose(np.abs(fullL), np.abs(np.asarray(qt.estimate_left_sv)),
+                                       atol=1e-10)
         elif case == "relocate":
             # empty-cluster relocation across shards: per-shard top-e + all-gather
             from sq_learn_amd.models.cluster import KMeans

@@ -73,3 +73,21 @@ def test_sag_solver_api():
     assert n_iter == 2 and coef.shape == (3,) and mem["coef"].shape == (3, 1)
     with pytest.raises(ValueError, match="overflow"):
         sag_solver(X, y * 1e308, loss="squared", alpha=1.0, max_iter=5, random_state=0)
+
+
+@pytest.mark.parametrize("solver", ["sag", "saga"])
+def test_sparse_fit_intercept_matches_reference(solver):
+    # sparse input: the reference damps intercept updates by
+    # SPARSE_INTERCEPT_DECAY = 0.01 (make_dataset, linear_model/_base.py:206)
+    import scipy.sparse as sparse
+    X, y = make_classification(300, 6, n_informative=4, random_state=1)
+    X = StandardScaler().fit_transform(X)
+    X[np.abs(X) < 0.5] = 0.0
+    Xs = sparse.csr_matrix(X)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        a = sklm.LogisticRegression(solver=solver, tol=1e-8, max_iter=5000, random_state=0).fit(Xs, y)
+        b = LogisticRegression(solver=solver, tol=1e-8, max_iter=5000, random_state=0).fit(Xs, y)
+    np.testing.assert_allclose(b.coef_, a.coef_, atol=1e-8)
+    np.testing.assert_allclose(b.intercept_, a.intercept_, atol=1e-8)
+    np.testing.assert_array_equal(b.n_iter_, a.n_iter_)
