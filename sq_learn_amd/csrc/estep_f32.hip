@@ -27,8 +27,9 @@
 // their (min, 2nd, argmin) by a transposed reduce-scatter; rows whose 2nd
 // value is inside the band are resolved from the per-lane top-2 lists in
 // kappa order (band.h); a lane whose 3rd value is inside the band could hide
-// a 4th member -> the row goes to the overflow list and is re-done in fp64 by
-// band_rows_f64 (all k distances, sum of (x - c)^2 - cdist's own formula).
+// a 4th member -> the row goes to the overflow list and is re-done exactly in
+// fp64 by the rows kernel (csrc/rows_f64.hip: fp64-MFMA candidates, then
+// sum of (x - c)^2 - cdist's own formula).
 //
 // Layout.  One workgroup = 4 waves (one per SIMD, up to 512 registers) x 32
 // rows; each wave keeps its 32 rows as fp16 hi/lo A fragments in VGPRs for the
@@ -41,6 +42,7 @@
 // epilogue of tile t runs in the MFMA shadow of tile t+1.
 #include "common.h"
 #include "band.h"
+#include <utility>
 
 namespace sq {
 
@@ -350,52 +352,6 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// band_rows_f64: exact fp64 re-selection of the rows the fused kernel flagged
-// (a lane held 3+ band candidates).  Driven by the device-side count (no host
-// sync); one 256-thread workgroup per row; D_j = sum_f (x_f - c_f)^2 in fp64
-// (scipy cdist's own formula, then squared) from the fp32 data and the fp32
-// centroids, all k staged in LDS, then the band rule of band.h.
-constexpr int kF64MaxK = 4096;
-__global__ void __launch_bounds__(256) band_rows_f64_kernel(
-    const float* __restrict__ X, const float* __restrict__ C, const long long* __restrict__ rows,
-    const int* __restrict__ count, int* __restrict__ labels, long long cap, int ldx, int d, int k,
-    double delta, RngKey key, long long row_offset, float* __restrict__ corr) {
-  __shared__ double xs[256];
-  __shared__ double ds[kF64MaxK];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long cnt = min((long long)*count, cap);
-  for (long long slot = blockIdx.x; slot < cnt; slot += gridDim.x) {
-    const long long r = rows[slot];
-    __syncthreads();
-    if (tid < d) xs[tid] = (double)X[(size_t)r * ldx + tid];
-    __syncthreads();
-    for (int j = wave; j < k; j += 4) {
-      const float* cr = C + (size_t)j * d;
-      double s = 0.0;
-      for (int f = lane; f < d; f += 64) {
-        const double df = xs[f] - (double)cr[f];
-        s = fma(df, df, s);
-      }
-      s = wave_sum(s);
-      if (lane == 0) ds[j] = s;
-    }
-    __syncthreads();
-    if (tid < 64) {
-      double mn = 1e308;
-      for (int j = lane; j < k; j += 64) mn = fmin(mn, ds[j]);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o, 64));
-      auto dist = [&](int j) -> double { return ds[j]; };
-      const int win = band_pick_wave(dist, k, mn + delta, band_u(key, row_offset + r), lane);
-      if (lane == 0) {
-        labels[r] = win;
-        if (corr) corr[r] = (float)(mn - ds[win]);   // min - distance to the label
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // estep_x64: certified filter + exact fp64 re-check (the default GPU E-step).
 //
 // One MFMA pass on the fp16 HI pieces only (xh . ch + the norm step) gives
@@ -444,6 +400,31 @@ constexpr int kX64Waves = SQ_X64_NW;   // waves per workgroup (8: 2 per SIMD, sp
 #define SQ_X64_PIN 1
 #endif
 constexpr int kX64Ring = SQ_X64_RING;  // centroid-tile LDS slots (3: 2 tiles in flight)
+
+// Tile geometry of the certified filter: a 64-centroid tile is KT = KSD + 1
+// k-steps (d_pad / 16 data steps + the norm step) of 2 KiB each.  Up to
+// d_pad = 256 a whole tile is one LDS ring slot; above, the tile is staged in
+// NS sub-tiles of at most 24 k-steps (48 KiB) so the 3-slot ring stays within
+// the 160 KiB LDS at every d_pad <= 1024, and the accumulation of a tile spans
+// NS slots (one counted-vmcnt barrier each).  The A operand (the wave's 32
+// rows, d_pad / 4 fp16x2 registers) stays resident for the whole sweep.
+template <int KSD>
+struct X64Geom {
+  static constexpr int KT = KSD + 1;
+  static constexpr int NS = (KT + 23) / 24;
+  static constexpr int SK = (KT + NS - 1) / NS;    // k-steps per slot
+  static constexpr int SLOT = SK * 2048;           // bytes per LDS slot
+};
+
+template <typename F, int... I>
+SQ_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+SQ_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <int KSD>
 __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     const _Float16* __restrict__ Xh, const float* __restrict__ X, const _Float16* __restrict__ C,
@@ -456,15 +437,16 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     int* __restrict__ mflag) {
   constexpr int NW = kX64Waves;
   constexpr int DX = KSD * 16;
-  constexpr int HI_BYTES = (KSD + 1) * 2048;   // staged per tile
+  using GEO = X64Geom<KSD>;
+  constexpr int KT = GEO::KT, NS = GEO::NS, SK = GEO::SK, SLOT = GEO::SLOT;
   constexpr int TILE_STRIDE = (2 * KSD + 1) * 2048;
-  constexpr int PIECES = HI_BYTES / 1024;
+  constexpr int PIECES = SLOT / 1024;           // 1 KiB LDS-DMA pieces per slot
   constexpr int ROWS = NW * 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int RING = kX64Ring;                // LDS tile slots
+  constexpr int RING = kX64Ring;                // LDS slots
   constexpr int PPW = (PIECES + NW - 1) / NW;   // glds per wave per stage (uniform: counted vmcnt)
-  auto buf = [&](int g) -> unsigned char* { return smem + (g % RING) * HI_BYTES; };
-  int* cand_all = reinterpret_cast<int*>(smem + RING * HI_BYTES);    // [NW][32][kMaxCand]
+  auto buf = [&](int g) -> unsigned char* { return smem + (g % RING) * SLOT; };
+  int* cand_all = reinterpret_cast<int*>(smem + RING * SLOT);        // [NW][32][kMaxCand]
   int* cnt_all = cand_all + NW * 32 * kMaxCand;                       // [NW][32]
 
   const int tid = threadIdx.x;
@@ -492,15 +474,21 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   const float pack_rel = ldexpf(1.0f, qbits - 23) + 0x1p-15f;
   const float sub_rel = 0x1p-21f * sqrtf((float)DX);
 
-  auto stage = [&](int G) {
-    const int t = G % n_tiles;
-    const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_STRIDE;
-    unsigned char* dst = buf(G);
+  // unit U = sub-tile U % NS of tile (U / NS) % n_tiles (the sequence runs on
+  // across row blocks: the next block's first tiles are staged during the
+  // current block's last ones)
+  auto stage = [&](int U) {
+    const int t = (NS == 1 ? U : U / NS) % n_tiles;
+    const int sub = NS == 1 ? 0 : U % NS;
+    const int npc = 2 * min(SK, KT - sub * SK);   // valid pieces of this sub-tile
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(C) + (size_t)t * TILE_STRIDE +
+                                (size_t)sub * SLOT;
+    unsigned char* dst = buf(U);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       // every wave issues PPW loads (the surplus repeat the last piece: same
       // bytes to the same LDS slot) so one counted vmcnt fits all waves
-      const int p = wave + NW * i < PIECES ? wave + NW * i : PIECES - 1;
+      const int p = wave + NW * i < npc ? wave + NW * i : npc - 1;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
           (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
@@ -520,51 +508,53 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   float m1[16], m2[16], m3[16];
   const int lane_off = (half * 64 + r32) * 16;
   auto ldb = [&](const unsigned char* p) -> f16x8 { return *reinterpret_cast<const f16x8*>(p); };
-  auto tile_step = [&](const unsigned char* cur, f32x16& n0, f32x16& n1, bool do_mfma,
-                       const f32x16& o0, const f32x16& o1, int t_prev, bool do_epi) {
+  auto ins = [&](int i, float v, uint32_t q) {
+    const float p = __uint_as_float((__float_as_uint(v) & keep) | q);
+    const float a1 = m1[i], a2 = m2[i];
+    m3[i] = vmed3(a2, p, m3[i]);
+    m2[i] = vmed3(a1, p, a2);
+    m1[i] = vmin(a1, p);
+  };
+  // k-steps [S SK, min((S+1) SK, KT)) of the current tile from the slot at
+  // cur, with the epilogue rows of the previous tile (o0 / o1, tile t_prev)
+  // spread over the tile's KT k-steps
+  auto sub_step = [&](auto S_, const unsigned char* cur, f32x16& acc0, f32x16& acc1,
+                      const f32x16& o0, const f32x16& o1, int t_prev, bool do_epi) {
+    constexpr int S = decltype(S_)::value;
+    constexpr int K0 = S * SK, K1 = (S + 1) * SK < KT ? (S + 1) * SK : KT;
     const uint32_t q0 = (uint32_t)(t_prev * 2), q1 = q0 + 1u;
-    auto ins = [&](int i, float v, uint32_t q) {
-      const float p = __uint_as_float((__float_as_uint(v) & keep) | q);
-      const float a1 = m1[i], a2 = m2[i];
-      m3[i] = vmed3(a2, p, m3[i]);
-      m2[i] = vmed3(a1, p, a2);
-      m1[i] = vmin(a1, p);
-    };
-    if (do_mfma) {
-      f32x16 acc0 = {0}, acc1 = {0};
-      const unsigned char* hb = cur + lane_off;
-      f16x8 b0[2], b1[2];
-      b0[0] = ldb(hb);
-      b1[0] = ldb(hb + 512);
+    const unsigned char* hb = cur + lane_off;
+    f16x8 b0[2], b1[2];
+    b0[0] = ldb(hb);
+    b1[0] = ldb(hb + 512);
 #pragma unroll
-      for (int ks = 0; ks <= KSD; ++ks) {
-        const int c = ks & 1, nx = c ^ 1;
-        if (ks < KSD) {
-          b0[nx] = ldb(hb + (ks + 1) * 2048);
-          b1[nx] = ldb(hb + (ks + 1) * 2048 + 512);
-        }
-        const f16x8 A = ks < KSD ? ah[ks] : aug;
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b0[c], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b1[c], acc1, 0, 0, 0);
-        if (do_epi) {
+    for (int ks = K0; ks < K1; ++ks) {
+      const int c = (ks - K0) & 1, nx = c ^ 1;
+      if (ks + 1 < K1) {
+        b0[nx] = ldb(hb + (ks + 1 - K0) * 2048);
+        b1[nx] = ldb(hb + (ks + 1 - K0) * 2048 + 512);
+      }
+      const f16x8 A = ks < KSD ? ah[ks] : aug;
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b0[c], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b1[c], acc1, 0, 0, 0);
+      if (do_epi) {
 #pragma unroll
-          for (int i = (ks * 16) / (KSD + 1); i < ((ks + 1) * 16) / (KSD + 1); ++i) {
-            ins(i, o0[i], q0);
-            ins(i, o1[i], q1);
-          }
+        for (int i = (ks * 16) / KT; i < ((ks + 1) * 16) / KT; ++i) {
+          ins(i, o0[i], q0);
+          ins(i, o1[i], q1);
         }
+      }
 #if SQ_X64_PIN
-        __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
 #endif
-      }
-      n0 = acc0;
-      n1 = acc1;
-    } else if (do_epi) {
+    }
+  };
+  auto epi_all = [&](const f32x16& o0, const f32x16& o1, int t_prev) {
+    const uint32_t q0 = (uint32_t)(t_prev * 2), q1 = q0 + 1u;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        ins(i, o0[i], q0);
-        ins(i, o1[i], q1);
-      }
+    for (int i = 0; i < 16; ++i) {
+      ins(i, o0[i], q0);
+      ins(i, o1[i], q1);
     }
   };
   // RING == 2: the tile staged in this step must land before the barrier
@@ -581,7 +571,22 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     __builtin_amdgcn_s_barrier();
   };
 
-  int G = 0;
+  // one tile = NS sub-steps, each: stage the unit RING - 1 ahead, MFMAs on
+  // the current unit, retire the next one (counted vmcnt + raw barrier)
+  int U = 0;
+  auto tile = [&](f32x16& n0, f32x16& n1, const f32x16& o0, const f32x16& o1, int t_prev,
+                  bool do_epi) {
+    f32x16 acc0 = {0}, acc1 = {0};
+    static_for<NS>([&](auto S_) {
+      stage(U + RING - 1);
+      sub_step(S_, buf(U), acc0, acc1, o0, o1, t_prev, do_epi);
+      sync_tile();
+      ++U;
+    });
+    n0 = acc0;
+    n1 = acc1;
+  };
+
   stage(0);
   if constexpr (RING == 3) stage(1);
   load_a(blk);
@@ -594,33 +599,24 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     for (int i = 0; i < 16; ++i) m1[i] = m2[i] = m3[i] = __builtin_inff();
     if (lane < 32) cnt[lane] = 0;
     f32x16 pA0, pA1, pB0, pB1;
-    stage(G + RING - 1);
-    tile_step(buf(G), pA0, pA1, true, pA0, pA1, 0, false);
-    sync_tile();
+    tile(pA0, pA1, pA0, pA1, 0, false);
     int t = 0;
     while (true) {
       if (t + 1 >= n_tiles) {
         load_a(blk + gridDim.x);   // clamped rows: unconditional (no phi on ah)
-        tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
+        epi_all(pA0, pA1, t);
         break;
       }
-      stage(G + RING);
-      tile_step(buf(G + 1), pB0, pB1, true, pA0, pA1, t, true);
-      sync_tile();
+      tile(pB0, pB1, pA0, pA1, t, true);
       ++t;
-      ++G;
       if (t + 1 >= n_tiles) {
         load_a(blk + gridDim.x);
-        tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
+        epi_all(pB0, pB1, t);
         break;
       }
-      stage(G + RING);
-      tile_step(buf(G + 1), pA0, pA1, true, pB0, pB1, t, true);
-      sync_tile();
+      tile(pA0, pA1, pB0, pB1, t, true);
       ++t;
-      ++G;
     }
-    ++G;
 
     // ---- row minimum (packed) by the transposed reduce-scatter: lane r32
     // even ends with the min of row irow = r32 >> 1 of its half
@@ -1331,6 +1327,11 @@ __global__ void __launch_bounds__(256) centers_f16_operand_kernel(const float* _
 using namespace sq;
 
 extern "C" int sq_sum_partials(const void* part, int n, void* out, void* stream);
+extern "C" int sq_rows_f64(const void* X, long long ldx, const void* C, long long ldc, int d, int k,
+                           const void* rows, const void* count, long long n_direct, long long cap,
+                           void* labels, void* mind, void* corr, void* ub, double delta,
+                           unsigned k0, unsigned k1, unsigned s0, unsigned s1,
+                           long long row_offset, int grid, void* stream);
 
 template <int KSD>
 static int launch_estep_f32(const void* X, const void* C, const void* xn, void* labels, void* mind,
@@ -1379,7 +1380,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
                             void* ub, void* lb, void* mflag, void* xflag) {
   constexpr int NW = kX64Waves;
-  const size_t lds = kX64Ring * (size_t)((KSD + 1) * 2048) + (size_t)NW * 32 * (kMaxCand + 1) * 4;
+  const size_t lds = kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * 32 * (kMaxCand + 1) * 4;
   auto kern = estep_x64_kernel<KSD>;
   static bool attr = false;
   if (!attr) {
@@ -1460,7 +1461,8 @@ int sq_estep_f32(const void* X, const void* C, const void* xn, void* labels, voi
 
 // Certified E-step (the default): filter + fp64 re-check (estep_x64_kernel),
 // dense rows through the 3-pass fp32-faithful kernel in list mode, its
-// overflow rows through band_rows_f64, the multi-candidate rows through
+// overflow rows through the exact fp64 rows kernel (rows_f64.hip; at d_pad >
+// 256 the dense rows go there directly), the multi-candidate rows through
 // recheck_rows_kernel.  counts[0] = 3-pass overflow rows, counts[1] = dense
 // rows, counts[2] = multi rows; all zero on entry.  xflag [n] (uint8, per
 // multi-list entry): with it the fp32 screen runs first and the fp64
@@ -1477,7 +1479,7 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
                  unsigned s1, long long row_offset, void* stream) {
   if (n <= 0) return 0;
-  if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 4096 || k > k_pad || d > d_pad)
+  if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 32768 || k > k_pad || d > d_pad)
     return (int)hipErrorInvalidValue;
   if ((ub != nullptr) != (lb != nullptr) || (ub != nullptr) != (mflag != nullptr))
     return (int)hipErrorInvalidValue;   // bounds need the multi-row slot map
@@ -1489,33 +1491,47 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   const float fa = (float)alpha, ia2 = (float)(1.0 / a2), ds = (float)(delta * a2);
   int* cnt = (int*)counts;
   if (corr) hipMemsetAsync(corr, 0, (size_t)n * sizeof(float), st);
+  const int cap = (int)min(n, 2147483647LL);
+  const unsigned fgrid = (unsigned)min((n + 15) / 16, 512LL);   // exact fp64 rows kernel
   int rc;
   switch (d_pad) {
+    // d_pad <= 256: dense rows through the fp32-faithful 3-pass kernel (list
+    // mode), its overflow rows through the exact fp64 rows kernel
 #define CASE(KSD)                                                                                \
   case KSD * 16:                                                                                 \
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
-                               row_offset, (int)min(n, 2147483647LL), st, rlist, rcount, ub, lb,  \
-                               mflag, xflag);                                                    \
+                               row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag);        \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
-                               n, k_pad, fa, ia2, ds, key, row_offset, (int)min(n, 2147483647LL), \
-                               st, dense_rows, cnt + 1);                                         \
+                               n, k_pad, fa, ia2, ds, key, row_offset, cap, st, dense_rows,       \
+                               cnt + 1);                                                         \
+    if (rc) return rc;                                                                           \
+    if (corr)                                                                                    \
+      hipLaunchKernelGGL(dense_corr_kernel, dim3(256), dim3(256), 0, st, (const float*)X,        \
+                         (const float*)Cm, (const long long*)dense_rows, (const int*)(cnt + 1),   \
+                         (const int*)labels, (const float*)mind, (float*)corr, n, d_pad);        \
+    rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, ovf_rows, cnt, 0, n, labels, mind, corr,      \
+                     ub, delta, k0, k1, s0, s1, row_offset, (int)fgrid, stream);                 \
     break;
     CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+    // d_pad > 256: the dense rows straight to the exact fp64 rows kernel
+#define CASE(KSD)                                                                                \
+  case KSD * 16:                                                                                 \
+    rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
+                               mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
+                               row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag);        \
+    if (rc) return rc;                                                                           \
+    rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, dense_rows, cnt + 1, 0, n, labels, mind,      \
+                     corr, ub, delta, k0, k1, s0, s1, row_offset, (int)fgrid, stream);           \
+    break;
+    CASE(24) CASE(32) CASE(40) CASE(48) CASE(56) CASE(64)
 #undef CASE
     default:
       return (int)hipErrorInvalidValue;
   }
   if (rc) return rc;
-  if (corr)
-    hipLaunchKernelGGL(dense_corr_kernel, dim3(256), dim3(256), 0, st, (const float*)X,
-                       (const float*)Cm, (const long long*)dense_rows, (const int*)(cnt + 1),
-                       (const int*)labels, (const float*)mind, (float*)corr, n, d_pad);
-  hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(n < 2048 ? n : 2048)), dim3(256), 0,
-                     st, (const float*)X, (const float*)Cm, (const long long*)ovf_rows,
-                     (const int*)cnt, (int*)labels, n, d_pad, d_pad, k, delta, key, row_offset,
-                     (float*)corr);
   return (int)hipGetLastError();
 }
 
@@ -1539,19 +1555,6 @@ int sq_sum_f32(const void* v, long long n, void* part, int extra, void* out, voi
   hipLaunchKernelGGL(sum_f32_blocks_kernel, dim3(blocks), dim3(256), 0, st, (const float*)v, n,
                      (double*)part);
   return sq_sum_partials(part, blocks + extra, out, st);
-}
-
-int sq_band_rows_f64(const void* X, const void* C, const void* rows, const void* count,
-                     void* labels, long long cap, int ldx, int d, int k, double delta, unsigned k0,
-                     unsigned k1, unsigned s0, unsigned s1, long long row_offset, void* stream) {
-  if (cap <= 0) return 0;
-  if (d > 256 || k > kF64MaxK || ldx < d) return (int)hipErrorInvalidValue;
-  RngKey key{k0, k1, s0, s1};
-  hipLaunchKernelGGL(band_rows_f64_kernel, dim3((unsigned)(cap < 2048 ? cap : 2048)), dim3(256), 0,
-                     (hipStream_t)stream, (const float*)X, (const float*)C,
-                     (const long long*)rows, (const int*)count, (int*)labels, cap, ldx, d, k,
-                     delta, key, row_offset, (float*)nullptr);
-  return (int)hipGetLastError();
 }
 
 int sq_centers_f16_operand(const void* Cm, void* op, int k, int d, int d_pad, int k_pad,

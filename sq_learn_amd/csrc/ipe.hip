@@ -13,21 +13,23 @@
 //  * odd Q and M <= kIpeWalkM: the median-of-Q is drawn EXACTLY from its own
 //    law with ONE uniform: the AE values sin^2(pi j/M) are ordered by the
 //    circular bin distance t = min(j, M - j), the class masses
-//    p(t) + p(M - t) accumulate into F(t), and the median of Q iid draws has
-//    CDF G(t) = P(Binomial(Q, F(t)) >= (Q+1)/2); inverse-CDF walk over t in
-//    fp64 (angle-addition recurrence, no transcendental per step);
+//    p(t) + p(M - t) accumulate into F(t); the median of Q iid draws is
+//    F^-1(U_(h)) with U_(h) ~ Beta(h, h), drawn once per pair by inverting
+//    G(x) = P(Binomial(Q, x) >= h), then one inverse-CDF walk over t in fp64
+//    (angle-addition recurrence, no transcendental or binomial per step);
 //  * otherwise Q Fejer draws (fejer.h, exact O(1) sampler) from one Philox
 //    stream per pair, the median taken over the circular distances t_q
 //    (sin^2 is monotone in t) by a register sorting network - no per-thread
 //    double[31] array.
-// Layout: a wave owns 16 rows, their fp32 A fragments (16x16x4 f32 MFMA:
-// lane l holds x[l & 15][4s + (l >> 4)]) staged once in the wave's LDS slot
-// (16 KiB at d = 256; keeps the VGPRs for the sampler, 2 waves per SIMD); centroid tiles of 16 are read as pre-arranged B fragments
+// Layout: a workgroup owns 16 rows, their fp32 A fragments (16x16x4 f32
+// MFMA: lane l holds x[l & 15][4s + (l >> 4)]) staged once in LDS and shared
+// by its 4 waves, which split the centroid tiles (d_pad * 64 B of LDS: 64 KiB
+// at d_pad = 1024); centroid tiles of 16 are read as pre-arranged B fragments
 // (ops/kmeans.py: ipe_center_fragments, one coalesced 256-B load per k-step,
 // L2-resident).  Accumulator register i of lane l is pair (row 4(l>>4) + i,
 // centroid l & 15): 4 pairs per lane per tile keep the per-lane state small
 // (the sampling epilogue, not the MFMA, is the cost).  After the sweep the
-// 16 lanes of a row merge their (D~, tie key, j) minima.
+// 16 lanes of a row merge their (D~, tie key, j) minima, then the 4 waves.
 #include "common.h"
 #include "band.h"
 #include "fejer.h"
@@ -56,7 +58,40 @@ SQ_DEV double binom_upper_tail(double F, int Q, int h) {
   return tail;
 }
 
-// exact draw of the median of Q (odd) iid AE estimates for small M
+// The median of Q (odd) iid draws T_1..T_Q with CDF F is F^-1(U_(h)), h =
+// (Q + 1) / 2, U_(h) the h-th order statistic of Q uniforms ~ Beta(h, h):
+// P(U_(h) <= x) = G(x) = P(Binomial(Q, x) >= h).  One uniform u gives
+// x* = G^-1(u) (safeguarded Newton in fp64 from the normal approximation;
+// G' = Q C(Q-1, h-1) x^(h-1) (1-x)^(Q-h)), after which the draw is ONE
+// inverse-CDF walk of F to x* - no binomial tail per step, no per-draw
+// sorting (Utility.py:534-572's median over Q repetitions, exact law).
+SQ_DEV double median_order_stat(double u, int Q) {
+  const int h = (Q + 1) / 2;
+  if (Q == 1) return u;
+  double cq = (double)Q;                  // Q C(Q-1, h-1)
+  for (int i = 1; i < h; ++i) cq = cq * (double)(Q - i) / (double)i;
+  double lo = 0.0, hi = 1.0;
+  // start: the normal approximation (fp32 erfinv: only the Newton start)
+  double x = 0.5 + 0.7071067811865476 / sqrt((double)Q + 2.0) * (double)erfinvf((float)(2.0 * u - 1.0));
+  x = fmin(fmax(x, 1e-9), 1.0 - 1e-9);
+  for (int it = 0; it < 40; ++it) {
+    const double g = binom_upper_tail(x, Q, h) - u;
+    if (g > 0.0) hi = x; else lo = x;
+    double dens = cq;
+    for (int i = 0; i < h - 1; ++i) dens *= x * (1.0 - x);   // Q = 2h - 1: x^(h-1) (1-x)^(h-1)
+    double xn = dens > 0.0 ? x - g / dens : 0.5 * (lo + hi);
+    if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+    const bool done = fabs(xn - x) <= 1e-15 * fmax(fmin(x, 1.0 - x), 1e-300) || hi - lo <= 1e-16;
+    x = xn;
+    if (done) break;
+  }
+  return x;
+}
+
+// exact draw of the median of Q (odd) iid AE estimates for small M: the
+// value classes t = min(j, M - j) in increasing sin^2 order, their masses
+// p(t) + p(M - t) accumulated until F(t) >= x* (fp64 angle-addition
+// recurrence, no transcendental per step)
 SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
   const double PI = 3.14159265358979323846;
   const double fl = floor(omega);
@@ -68,13 +103,13 @@ SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
     const double v = sin(PI * (double)j / Md);
     return v * v;
   }
+  const double xs = median_order_stat(u, Q);
   const double sp = sin(PI * phi);
   const double num = sp * sp / (Md * Md);
   const double alpha = PI / Md, beta = PI * omega / Md;
   double sa, ca, sb, cb;
   sincos(alpha, &sa, &ca);
   sincos(beta, &sb, &cb);
-  const int h = (Q + 1) / 2;
   const long long tmax = M / 2;
   double st = 0.0, ct = 1.0;   // sin / cos(t alpha)
   double F = 0.0;
@@ -88,7 +123,7 @@ SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
     }
     F += mass;
     v = st * st;
-    if (binom_upper_tail(F, Q, h) >= u) return v;
+    if (F >= xs) return v;
     const double nst = st * ca + ct * sa;
     ct = ct * ca - st * sa;
     st = nst;
@@ -219,22 +254,23 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     const float* __restrict__ xn, const float* __restrict__ cn, int* __restrict__ labels,
     float* __restrict__ mind, long long n, int d, int k, int n_tiles, double eps, int Q,
     RngKey key, RngKey tie_key, long long row_offset) {
-  __shared__ float As[4][D4 * 64];   // per wave: its 16 rows as A fragments
+  extern __shared__ __attribute__((aligned(16))) float As[];   // [D4][64] A fragments
+  __shared__ float mb[4][16];
+  __shared__ uint32_t mk[4][16];
+  __shared__ int mj[4][16];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
-  const long long row0 = ((long long)blockIdx.x * 4 + wave) * 16;
-  if (row0 >= n) return;   // wave-uniform; no block-wide barrier below
-  float* as = As[wave];
-  {
-    // A fragments (16x16x4 f32): x[row0 + c16][4s + q4]; rows past n clamped
-    const long long r = row0 + c16 < n ? row0 + c16 : n - 1;
-    const float* xr = X + (size_t)r * ldx + q4;
-#pragma unroll 8
-    for (int s = 0; s < D4; ++s) as[s * 64 + lane] = 4 * s + q4 < d ? xr[4 * s] : 0.0f;
+  const long long row0 = (long long)blockIdx.x * 16;
+  // A fragments (16x16x4 f32) of the workgroup's 16 rows, shared by the 4
+  // waves: As[s][l] = x[row0 + (l & 15)][4 s + (l >> 4)]; rows past n clamped
+  for (int e = threadIdx.x; e < D4 * 64; e += 256) {
+    const int s = e >> 6, l = e & 63;
+    const long long r = row0 + (l & 15) < n ? row0 + (l & 15) : n - 1;
+    const int f = 4 * s + (l >> 4);
+    As[e] = f < d ? X[(size_t)r * ldx + f] : 0.0f;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __syncthreads();
   // register i of this lane = pair (row row0 + 4 q4 + i, centroid 16 t + c16)
   f32x4 nx2, best;
   uint32_t bkey[4];
@@ -247,12 +283,12 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     bkey[i] = 0xFFFFFFFFu;
     bj[i] = 0;
   }
-  for (int t = 0; t < n_tiles; ++t) {
+  for (int t = wave; t < n_tiles; t += 4) {   // the waves split the centroid tiles
     const float* bf = Cf + (size_t)t * D4 * 64 + lane;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 16
     for (int s = 0; s < D4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(as[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
     const int j = t * 16 + c16;
     if (j < k) {   // padded centroid columns do nothing (no MFMA / sync below)
       const double ny2 = (double)cn[j];
@@ -282,7 +318,11 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       }
     }
   }
-  // merge the 16 lanes (centroid classes) holding each row
+  // merge the 16 lanes (centroid classes) holding each row, then the 4 waves
+  // (the order (D~, tie key, j) is total: any merge order gives the same pick)
+  auto better = [](float ob, uint32_t ok, int oj, float b, uint32_t kk, int jj) {
+    return ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)));
+  };
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float b = best[i];
@@ -293,14 +333,32 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       const float ob = __shfl_xor(b, o, 64);
       const uint32_t ok = (uint32_t)__shfl_xor((int)kk, o, 64);
       const int oj = __shfl_xor(jj, o, 64);
-      if (ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)))) {
+      if (better(ob, ok, oj, b, kk, jj)) {
         b = ob;
         kk = ok;
         jj = oj;
       }
     }
-    const long long r = row0 + 4 * q4 + i;
-    if (c16 == 0 && r < n) {
+    if (c16 == 0) {
+      mb[wave][4 * q4 + i] = b;
+      mk[wave][4 * q4 + i] = kk;
+      mj[wave][4 * q4 + i] = jj;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int rr = threadIdx.x;
+    float b = mb[0][rr];
+    uint32_t kk = mk[0][rr];
+    int jj = mj[0][rr];
+    for (int w = 1; w < 4; ++w)
+      if (better(mb[w][rr], mk[w][rr], mj[w][rr], b, kk, jj)) {
+        b = mb[w][rr];
+        kk = mk[w][rr];
+        jj = mj[w][rr];
+      }
+    const long long r = row0 + rr;
+    if (r < n) {
       labels[r] = jj;
       mind[r] = b;
     }
@@ -322,20 +380,22 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
     return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   RngKey tie{t0, t1, ts0, ts1};
-  const long long blocks = (n + 63) / 64;
+  const long long blocks = (n + 15) / 16;
   const int nt = k_pad / 16;
 #define CASE(DP)                                                                              \
   case DP:                                                                                    \
-    hipLaunchKernelGGL(ipe_fused_kernel<DP / 4>, dim3((unsigned)blocks), dim3(256), 0,         \
-                       (hipStream_t)stream, (const float*)X, ldx, (const float*)Cf,           \
-                       (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, \
-                       nt, eps, Q, key, tie, row_offset);                                     \
+    hipLaunchKernelGGL(ipe_fused_kernel<DP / 4>, dim3((unsigned)blocks), dim3(256),            \
+                       (size_t)DP * 64, (hipStream_t)stream, (const float*)X, ldx,            \
+                       (const float*)Cf, (const float*)xn, (const float*)cn, (int*)labels,    \
+                       (float*)mind, n, d, k, nt, eps, Q, key, tie, row_offset);              \
     break;
   switch (d_pad) {
     CASE(32)
     CASE(64)
     CASE(128)
     CASE(256)
+    CASE(512)
+    CASE(1024)
     default:
       return (int)hipErrorInvalidValue;
   }

@@ -965,7 +965,7 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
   }
 }
 
-// one wave per entry (d <= 256: 4 fp32 values per lane), SQ_DSEG_U entries in
+// one wave per entry (4 fp32 values per lane per 256-column chunk), U entries in
 // flight per wave; the entry count is the scanned total (cursor[k-1]).
 // Each wave takes a run of max(SQ_DSEG_RUN, total / SQ_DSEG_WAVES) entries:
 // long runs keep the fp64 flush atomics few (many moved rows), short ones
@@ -981,6 +981,9 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
 #ifndef SQ_DSEG_WAVES
 #define SQ_DSEG_WAVES 2048
 #endif
+// M = ceil(d / 256) column chunks of 256 features per lane pass (d <= 1024):
+// lane covers features 4 lane + 256 m, m < M, of every entry it streams.
+template <int M>
 __global__ void __launch_bounds__(512) delta_segment_kernel(
     const float* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
     const int* __restrict__ prev, int d, int range, float xscale, double qscale,
@@ -990,7 +993,7 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
   // range <= 0: the entry count (on the device) is split evenly over the
   // grid - a few moved rows still keep every block busy
   const long long total = *valid_end;
-  constexpr int U = SQ_DSEG_U;
+  constexpr int U = M == 1 ? SQ_DSEG_U : (M == 2 ? 4 : 2);
   // range > 0: a block takes `range` entries, its 8 waves interleaved;
   // range <= 0: each wave takes a CONTIGUOUS run of >= 64 entries (runs of
   // one label stay in one wave: few flushes, few fp64 atomics)
@@ -1008,16 +1011,21 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
     pstep = U;
     ustep = 1;
   }
-  const int c0 = lane * 4;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, aq = 0.0, cnt = 0.0;
+  double a[M][4], aq = 0.0, cnt = 0.0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) a[m][0] = a[m][1] = a[m][2] = a[m][3] = 0.0;
   int cur = -1;
   auto flush = [&]() {
-    double* dst = sums + (size_t)cur * d + c0;
-    if (c0 < d) {
-      if (a0 != 0.0) atomicAdd(dst + 0, a0);
-      if (a1 != 0.0 && c0 + 1 < d) atomicAdd(dst + 1, a1);
-      if (a2 != 0.0 && c0 + 2 < d) atomicAdd(dst + 2, a2);
-      if (a3 != 0.0 && c0 + 3 < d) atomicAdd(dst + 3, a3);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int c0 = lane * 4 + 256 * m;
+      double* dst = sums + (size_t)cur * d + c0;
+      if (c0 < d) {
+        if (a[m][0] != 0.0) atomicAdd(dst + 0, a[m][0]);
+        if (a[m][1] != 0.0 && c0 + 1 < d) atomicAdd(dst + 1, a[m][1]);
+        if (a[m][2] != 0.0 && c0 + 2 < d) atomicAdd(dst + 2, a[m][2]);
+        if (a[m][3] != 0.0 && c0 + 3 < d) atomicAdd(dst + 3, a[m][3]);
+      }
     }
     const double q = wave_sum(aq);   // integer-valued: exact in any order
     if (lane == 0) {
@@ -1027,7 +1035,7 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
   };
   for (long long p = p0; p < p1; p += pstep) {
     int code[U], ll[U];
-    float4 v[U];
+    float4 v[U][M];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long q = p + ustep * u;
@@ -1037,8 +1045,12 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
     for (int u = 0; u < U; ++u) {
       const int r = code[u] >= 0 ? (code[u] >> 1) : 0;
       ll[u] = code[u] < 0 ? -1 : ((code[u] & 1) ? prev[r] : labels[r]);
-      v[u] = (code[u] >= 0 && c0 < d) ? *reinterpret_cast<const float4*>(X + (size_t)r * d + c0)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int c0 = lane * 4 + 256 * m;
+        v[u][m] = (code[u] >= 0 && c0 < d) ? *reinterpret_cast<const float4*>(X + (size_t)r * d + c0)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1046,16 +1058,22 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
       if (ll[u] != cur) {
         if (cur >= 0) flush();
         cur = ll[u];
-        a0 = a1 = a2 = a3 = aq = cnt = 0.0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) a[m][0] = a[m][1] = a[m][2] = a[m][3] = 0.0;
+        aq = cnt = 0.0;
       }
       const double sg = (code[u] & 1) ? -1.0 : 1.0;
-      a0 += sg * (double)rintf(v[u].x * xscale);
-      a1 += sg * (double)rintf(v[u].y * xscale);
-      a2 += sg * (double)rintf(v[u].z * xscale);
-      a3 += sg * (double)rintf(v[u].w * xscale);
-      const double x0 = v[u].x, x1 = v[u].y, x2 = v[u].z, x3 = v[u].w;   // squares exact in fp64
-      aq += sg * (rint(x0 * x0 * qscale) + rint(x1 * x1 * qscale) + rint(x2 * x2 * qscale) +
-                  rint(x3 * x3 * qscale));
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const float4 x = v[u][m];
+        a[m][0] += sg * (double)rintf(x.x * xscale);
+        a[m][1] += sg * (double)rintf(x.y * xscale);
+        a[m][2] += sg * (double)rintf(x.z * xscale);
+        a[m][3] += sg * (double)rintf(x.w * xscale);
+        const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;   // squares exact in fp64
+        aq += sg * (rint(x0 * x0 * qscale) + rint(x1 * x1 * qscale) + rint(x2 * x2 * qscale) +
+                    rint(x3 * x3 * qscale));
+      }
       cnt += sg;
     }
   }
@@ -1853,7 +1871,7 @@ int sq_centroid_delta(const void* X, const void* labels, const void* prev, void*
                       void* counts, void* qsum, long long n, int d, int k, int xexp, int qexp,
                       void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
   if (n <= 0) return 0;
-  if (d % 4 != 0 || d > 256 || k > 16384 || 2 * n > 2147483647LL) return (int)hipErrorInvalidValue;
+  if (d % 4 != 0 || d > 1024 || k > 16384 || 2 * n > 2147483647LL) return (int)hipErrorInvalidValue;
   if (xexp < -120 || xexp > 120 || qexp < -200 || qexp > 200) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
@@ -1866,7 +1884,10 @@ int sq_centroid_delta(const void* X, const void* labels, const void* prev, void*
   // entries <= 2n, usually far fewer: a fixed grid shares the scanned total
   const long long cap_blocks = (2 * n + 63) / 64;
   const unsigned grid = (unsigned)(cap_blocks < 2048 ? cap_blocks : 2048);
-  hipLaunchKernelGGL(delta_segment_kernel, dim3(grid), dim3(512), 0, st, (const float*)X,
+  auto seg = d <= 256 ? delta_segment_kernel<1>
+             : d <= 512 ? delta_segment_kernel<2>
+             : d <= 768 ? delta_segment_kernel<3> : delta_segment_kernel<4>;
+  hipLaunchKernelGGL(seg, dim3(grid), dim3(512), 0, st, (const float*)X,
                      (const int*)ws_perm, (const int*)labels, (const int*)prev, d, 0,
                      ldexpf(1.0f, -xexp), ldexp(1.0, -qexp), (double*)sums, (double*)counts,
                      (double*)qsum, (const int*)ws_cursor + (k - 1));

@@ -104,9 +104,10 @@ __attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, vo
                                        void*, void*, int, void*, long long, int, int, double,
                                        double, unsigned, unsigned, unsigned, unsigned, long long,
                                        int, void*);
-__attribute__((weak)) int sq_band_rows_f64(const void*, const void*, const void*, const void*,
-                                           void*, long long, int, int, int, double, unsigned,
-                                           unsigned, unsigned, unsigned, long long, void*);
+__attribute__((weak)) int sq_rows_f64(const void*, long long, const void*, long long, int, int,
+                                      const void*, const void*, long long, long long, void*, void*,
+                                      void*, void*, double, unsigned, unsigned, unsigned, unsigned,
+                                      long long, int, void*);
 __attribute__((weak)) int sq_centers_f16_operand(const void*, void*, int, int, int, int, double,
                                                  void*);
 __attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia,
@@ -423,15 +424,16 @@ static PyObject* py_estep_f32(PyObject*, PyObject* a) {
                           n, dp, kp, alpha, delta, k0, k1, s0, s1, roff, cap, P(st)));
 }
 
-static PyObject* py_band_rows_f64(PyObject*, PyObject* a) {
-  unsigned long long X, C, rows, cnt, lab, st; long long cap, roff; int ldx, d, k; double delta;
-  unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKLiiidIIIILK", &X, &C, &rows, &cnt, &lab, &cap, &ldx, &d, &k,
-                        &delta, &k0, &k1, &s0, &s1, &roff, &st))
+static PyObject* py_rows_f64(PyObject*, PyObject* a) {
+  unsigned long long X, C, rows, cnt, lab, mind, corr, ub, st; long long ldx, ldc, nd, cap, roff;
+  int d, k, grid; double delta; unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KLKLiiKKLLKKKKdIIIILiK", &X, &ldx, &C, &ldc, &d, &k, &rows, &cnt, &nd,
+                        &cap, &lab, &mind, &corr, &ub, &delta, &k0, &k1, &s0, &s1, &roff, &grid,
+                        &st))
     return nullptr;
-  CHECK(sq_band_rows_f64)
-  return ret(sq_band_rows_f64(P(X), P(C), P(rows), P(cnt), P(lab), cap, ldx, d, k, delta, k0, k1,
-                              s0, s1, roff, P(st)));
+  CHECK(sq_rows_f64)
+  return ret(sq_rows_f64(P(X), ldx, P(C), ldc, d, k, P(rows), P(cnt), nd, cap, P(lab), P(mind),
+                         P(corr), P(ub), delta, k0, k1, s0, s1, roff, grid, P(st)));
 }
 
 static PyObject* py_centers_f16_operand(PyObject*, PyObject* a) {
@@ -537,7 +539,7 @@ static PyMethodDef methods[] = {
     {"sum_f32", py_sum_f32, METH_VARARGS, "deterministic sum of a float vector"},
     {"kmpp_grid", py_kmpp_grid, METH_VARARGS, "k-means++ trial pass grid size"},
     {"kmpp_trials", py_kmpp_trials, METH_VARARGS, "k-means++ trial distances + potentials"},
-    {"band_rows_f64", py_band_rows_f64, METH_VARARGS, "fp64 re-selection of overflow rows"},
+    {"rows_f64", py_rows_f64, METH_VARARGS, "exact fp64 E-step over a row list (fp64 MFMA)"},
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},
     {"ipe_estep", py_ipe_estep, METH_VARARGS, "IPE-noised distance argmin"},

@@ -13,19 +13,23 @@ the reference's quantum Lloyd loop (``_dmeans.py:534-671``):
                (intermediate_error) tomography with error delta/2
     loop     best-inertia iterate, Frobenius shift <= tol, final E-step
 
-GPU fast path (d <= 256, no IPE): per iteration
-    E-step   gemm_precision 'fp32' (default): estep_f32 - fp32-faithful fused
-               MFMA distances from an fp16 hi/lo split (csrc/estep_f32.hip) +
-               band epilogue + inertia -> band_rows_f64 (overflow rows, fp64,
-               device-driven);
-             gemm_precision 'bf16': estep_bf16 (bf16 operands, faster, the
-               band edge is only bf16-accurate) -> band_select_rows
+GPU fast path (d_pad <= 1024, k_pad <= 16384, no IPE): per iteration
+    E-step   gemm_precision 'fp32' (default): the certified filter
+               (csrc/estep_f32.hip estep_x64: one fp16 MFMA pass with a
+               rigorous error bound, Hamerly pruning, fp32 screen + fp64
+               re-check of multi-candidate rows; dense rows through the
+               fp32-faithful 3-pass kernel (d_pad <= 256) or the exact fp64
+               rows kernel (csrc/rows_f64.hip), which also takes the 3-pass
+               overflow rows) - the fp64 delta-band labels, device-driven;
+             gemm_precision 'bf16' (d_pad <= 256): estep_bf16 (bf16
+               operands, faster, the band edge is only bf16-accurate)
     -> centroid_accumulate (segmented reduce) -> pack_stats (one fp64 bucket)
     -> all_reduce over RCCL (C1: the only collective of the iteration)
     -> centroid_finalize (mean + fused truncated-normal tomography noise +
        shift + bf16 centroids and norms for the next E-step).
-Everything else (CPU tensors, IPE distances, d > 256, k > 4096) runs
-the generic path: library GEMM distance tiles + selection kernels/torch.
+CPU tensors run the torch twins; GPU shapes outside the filter run the exact
+fp64 rows kernel on every row (csrc/rows_f64.hip); IPE distances run the
+fused IPE kernel (csrc/ipe.hip).
 """
 
 import math
@@ -77,11 +81,16 @@ class LloydEngine:
         gpu = self.device.type == "cuda"
         if gemm_precision not in ("bf16", "fp32"):
             raise ValueError("gemm_precision must be 'bf16' or 'fp32', got %r" % (gemm_precision,))
+        # the bf16 kernel is an option up to d_pad = 256; wider rows take the
+        # certified path (a precision upgrade, never an uncertified fallback)
+        if gemm_precision == "bf16" and self.d_pad > 256:
+            gemm_precision = "fp32"
         self.precision = gemm_precision
-        # generic=True: library-GEMM distances + torch/selection kernels only
-        # (engines that replace the E-step, e.g. ElkanEngine)
-        self.fast = (gpu and not generic and not self.ipe and self.d_pad <= 256
-                     and self.k_pad <= 4096)
+        # generic=True: engines that replace the E-step (e.g. ElkanEngine);
+        # GPU shapes outside the certified filter (d_pad > 1024, k_pad >
+        # 16384) run the exact fp64 rows kernel on every row (_estep_generic)
+        self.fast = (gpu and not generic and not self.ipe and self.d_pad in K.X64_D
+                     and self.k_pad <= K.X64_MAX_K)
         self.alpha = 1.0
         self.acc_dtype = torch.float64 if not gpu else torch.float32
         if gpu:
@@ -319,20 +328,19 @@ class LloydEngine:
         return max(1024, wm // (4 * max(self.k, 1)))
 
     def _estep_generic(self, key):
-        Cw = self.C.to(self.Xf.dtype)
-        cn = (Cw * Cw).sum(1)
         n = self.n
         if self.device.type == "cuda":
+            # exact fp64 E-step on every row (csrc/rows_f64.hip: fp64-MFMA
+            # candidates + direct-form re-check): the reference's fp64 band
+            # rule at any shape, no uncertified library-GEMM fallback
             labels32 = torch.empty(n, dtype=torch.int32, device=self.device)
             mind = torch.empty(n, dtype=torch.float32, device=self.device)
-            step = self._chunk_rows()
-            for s in range(0, n, step):
-                e = min(n, s + step)
-                D = cn[None, :] - 2.0 * (self.Xf[s:e].float() @ Cw.float().T)
-                K.band_select_native(D, self.xn[s:e].float().contiguous(), self.delta, key,
-                                     self.row_offset + s, labels32[s:e], mind[s:e], k=self.k)
-            inertia = mind.double().sum().reshape(1)
-            return labels32, mind, inertia
+            Xg = self.Xf if (self.Xf.dtype == torch.float32 and self.Xf.stride(1) == 1) \
+                else self.Xf.float().contiguous()
+            K.rows_f64_native(Xg, self.C.float().contiguous(), labels32, mind, self.delta, key,
+                              self.row_offset)
+            return labels32, mind, mind.double().sum().reshape(1)
+        Cw = self.C.to(self.Xf.dtype)
         lab, mind = K.estep_torch(self.Xf, Cw, self.delta, key, self.row_offset, self.k_pad,
                                   chunk_rows=self._chunk_rows(), xn=self.xn)
         return lab, mind, mind.double().sum().reshape(1)
@@ -340,7 +348,7 @@ class LloydEngine:
     def _estep_ipe(self, key):
         eps = self.delta / 2.0
         ipe_key = self._key("ipe")
-        if self.device.type == "cuda" and self.d <= 256 and self.Xf.dtype == torch.float32 \
+        if self.device.type == "cuda" and self.d <= 1024 and self.Xf.dtype == torch.float32 \
                 and self.Xf.stride(1) == 1 and self.ipe_Q <= 15:
             # fused kernel: fp32 MFMA inner products + per-pair median-of-Q AE
             n = self.n
@@ -396,9 +404,16 @@ class LloydEngine:
                 Cold = None
                 if exact:
                     Cold = self.C if self.dm == self.d else self._padded_centers()
+                # the row pass fills the single-candidate rows' min distances
+                # when a row is one column pass (d <= 256); wider rows: a
+                # separate wave-per-row pass
+                in_pass = exact and self.dm <= 256
                 K.centroid_reduce_native(self.Xm, labels, self.weights, self.sums,
                                          self.counts, self.k, self.rws,
-                                         mind=self.buf.mind if exact else None, C_old=Cold)
+                                         mind=self.buf.mind if in_pass else None,
+                                         C_old=Cold if in_pass else None)
+                if exact and not in_pass:
+                    K.fill_mind_native(self.Xf32, self.C, labels, self.buf.mind)
                 if exact:
                     # inertia = sum of the (now complete) min distances, fixed order
                     K.sum_f32_native(self.buf.mind, self.n, self.mind_part, inertia)

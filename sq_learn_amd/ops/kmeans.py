@@ -15,12 +15,16 @@ from . import _native as nat
 from .random import amplitude_estimation_batch
 
 FAST_D = (16, 32, 64, 128, 256)
+# d_pad of the certified filter (csrc/estep_f32.hip estep_x64_kernel): the
+# power-of-two ladder to 256, then steps of 128 to 1024 (sub-staged tiles)
+X64_D = FAST_D + (384, 512, 640, 768, 896, 1024)
+X64_MAX_K = 16384   # k_pad of the filter (the segmented reduce's LDS histogram)
 BIG = 3.0e38
 
 
 def pad_features(d):
     """Padded feature count used by the MFMA kernels (zero columns)."""
-    for f in FAST_D:
+    for f in X64_D:
         if d <= f:
             return f
     return ((d + 15) // 16) * 16
@@ -401,7 +405,7 @@ def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWork
     label differs from ``prev`` (prev = -1: the row enters).  Bit-identical
     to recomputing them from scratch (exact integer arithmetic in fp64)."""
     n, d = X.shape
-    assert X.dtype == torch.float32 and X.is_contiguous() and d % 4 == 0 and d <= 256
+    assert X.dtype == torch.float32 and X.is_contiguous() and d % 4 == 0 and d <= 1024
     assert labels.dtype == torch.int32 and prev.dtype == torch.int32 and perm2.numel() >= 2 * n
     assert sums.dtype == torch.float64 and sums.numel() >= k * d and qsum.numel() >= k
     rc = nat.native().centroid_delta(X.data_ptr(), labels.data_ptr(), prev.data_ptr(),
@@ -604,10 +608,45 @@ def estep_f32_native(Xf, C_op, xn, C_master, k, delta, alpha, key: RngKey, row_o
                      buf.inertia_part.data_ptr(), int(buf.part_cap), buf.inertia.data_ptr(), n,
                      d_pad, k_pad, float(alpha), float(delta), key.k0, key.k1, key.s0, key.s1,
                      int(row_offset), buf.ovf_cap, st)
-    m.band_rows_f64(Xf.data_ptr(), C_master.data_ptr(), buf.ovf_rows.data_ptr(),
-                    buf.ovf_count.data_ptr(), buf.labels.data_ptr(), buf.ovf_cap, d_pad, d, k,
-                    float(delta), key.k0, key.k1, key.s0, key.s1, int(row_offset), st)
+    rows_f64_native(Xf, C_master, buf.labels, buf.mind, delta, key, row_offset,
+                    rows=(buf.ovf_rows, buf.ovf_count, buf.ovf_cap), stream=st)
     return buf.labels, buf.mind
+
+
+def rows_f64_native(X, C, labels, mind, delta, key: RngKey, row_offset, rows=None, corr=None,
+                    ub=None, d=None, grid=None, stream=None):
+    """Exact fp64 E-step over a row list (csrc/rows_f64.hip: fp64-MFMA
+    candidates with a rigorous bound, direct-form sum_f (x_f - c_f)^2 re-check,
+    the delta-band rule of band.h).  ``rows`` = (list int64, count int32 [1]
+    on the device, cap) or None for every row of X.  X fp32 [n][ldx], C fp32
+    [k][ldc] (the first ``d`` columns of each are used).  Writes labels,
+    mind (the min distance) and, when given, corr = mind - d(label) and
+    ub = |x - c_label|.  No host sync."""
+    n, ldx = X.shape
+    k, ldc = C.shape
+    d = int(min(ldx, ldc) if d is None else d)
+    assert X.dtype == torch.float32 and X.stride(1) == 1 and X.stride(0) == ldx
+    assert C.dtype == torch.float32 and C.is_contiguous() and d <= min(ldx, ldc)
+    assert labels.dtype == torch.int32 and mind.dtype == torch.float32
+    if rows is None:
+        if n == 0:
+            return labels, mind
+        cnt_ptr, nd, cap, rptr = 0, n, n, 0
+        groups = (n + 15) // 16
+    else:
+        rlist, count, cap = rows
+        rptr, cnt_ptr, nd = rlist.data_ptr(), count.data_ptr(), 0
+        groups = (int(cap) + 15) // 16
+    if grid is None:
+        grid = max(1, min(groups, 1024 if rows is None else 512))
+    st = stream if stream is not None else nat.stream_handle(X.device)
+    rc = nat.native().rows_f64(X.data_ptr(), int(ldx), C.data_ptr(), int(ldc), d, int(k), rptr,
+                               cnt_ptr, int(nd), int(cap), labels.data_ptr(), mind.data_ptr(),
+                               nat.ptr(corr), nat.ptr(ub), float(delta), key.k0, key.k1, key.s0,
+                               key.s1, int(row_offset), int(grid), st)
+    if rc:
+        raise RuntimeError(f"rows_f64 failed (hip error {rc})")
+    return labels, mind
 
 
 def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
@@ -629,13 +668,13 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     statistics), the fp64 re-check takes the rest."""
     n, d_pad = Xf.shape
     k_pad = C_op.shape[0] * 64
-    assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in FAST_D
+    assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in X64_D
     assert Xh.dtype == torch.float16 and Xh.is_contiguous() and tuple(Xh.shape) == (n, d_pad)
     assert C_op.dtype == torch.float16 and tuple(C_op.shape) == operand_f16_shape(k_pad, d_pad)
     assert C_pad.dtype == torch.float32 and C_pad.is_contiguous()
     assert tuple(C_pad.shape) == (k, d_pad)
     assert cmax2.dtype == torch.float32 and xn.dtype == torch.float32 and xn.numel() >= n
-    assert k <= k_pad <= 4096 and buf.labels.numel() >= n
+    assert k <= k_pad <= X64_MAX_K and buf.labels.numel() >= n
     ensure_multi_buffers(buf, n, Xf.device, bounds is not None)
     if screen and (buf.exact_flag is None or buf.exact_flag.numel() < n):
         buf.exact_flag = torch.empty(max(n, 1), dtype=torch.uint8, device=Xf.device)

@@ -27,12 +27,12 @@ def _engine(X, k, delta, incremental):
             os.environ["SQ_MSTEP_INCREMENTAL"] = old
 
 
-@pytest.mark.parametrize("delta,d", [(0.0, 64), (0.5, 256), (3.0, 100)])
+@pytest.mark.parametrize("delta,d", [(0.0, 64), (0.5, 256), (3.0, 100), (0.5, 512), (0.5, 784)])
 def test_incremental_mstep_bit_identical(cuda, delta, d):
-    X, _ = make_blobs(60000, d, centers=40, cluster_std=1.5, random_state=0)
+    X, _ = make_blobs(60000 if d <= 256 else 20000, d, centers=40, cluster_std=1.5, random_state=0)
     Xt = torch.tensor(X, dtype=torch.float32, device=cuda)
     k = 48
-    C0 = Xt[torch.as_tensor(np.random.RandomState(1).choice(60000, k, replace=False), device=cuda)]
+    C0 = Xt[torch.as_tensor(np.random.RandomState(1).choice(Xt.shape[0], k, replace=False), device=cuda)]
     inc = _engine(Xt, k, delta, True)
     ful = _engine(Xt, k, delta, False)
     assert inc.incremental and not ful.incremental
