@@ -56,6 +56,13 @@ SQ_DEV float vmin(float a, float b) {
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// (bits(a) & m) | q in ONE VALU op (v_and_or_b32; the compiler emits an and
+// plus an or3 that it pairs across values)
+SQ_DEV float and_or(float a, uint32_t m, uint32_t q) {
+  float r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(q));   // one SGPR per VOP3 on gfx9
+  return r;
+}
 SQ_DEV float vmed3(float a, float b, float c) {
   float r;
   asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -509,7 +516,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   const int lane_off = (half * 64 + r32) * 16;
   auto ldb = [&](const unsigned char* p) -> f16x8 { return *reinterpret_cast<const f16x8*>(p); };
   auto ins = [&](int i, float v, uint32_t q) {
-    const float p = __uint_as_float((__float_as_uint(v) & keep) | q);
+    const float p = and_or(v, keep, q);   // (v & keep) | q: the tile index in the low bits
     const float a1 = m1[i], a2 = m2[i];
     m3[i] = vmed3(a2, p, m3[i]);
     m2[i] = vmed3(a1, p, a2);
@@ -626,7 +633,10 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
         const bool hi = (r32 & o) != 0;
 #pragma unroll
         for (int j = 0; j < c; ++j) {
-          const float keepv = hi ? R[c + j] : R[j], sendv = hi ? R[j] : R[c + j];
+          // values first, then the selects: a select of two array elements
+          // becomes a select of addresses (runtime-indexed register array)
+          const float lo_v = R[j], hi_v = R[c + j];
+          const float keepv = hi ? hi_v : lo_v, sendv = hi ? lo_v : hi_v;
           R[j] = vmin(keepv, __shfl_xor(sendv, o, 64));
         }
       }

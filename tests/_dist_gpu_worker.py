@@ -62,6 +62,9 @@ def main(out_path):
         t = torch.as_tensor(np.asarray(lab).astype(np.int64))
         return torch.cat(comm.all_gather_varlen(t)).numpy()
 
+    def tonp(a):
+        return a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+
     def rel(a, b):
         a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
         return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
@@ -140,14 +143,14 @@ def main(out_path):
         # returns them as numpy and takes the host RNG, like the reference)
         ref = QPCA(**kw).fit(torch.as_tensor(Zq).to(dev), **fk)
         got = QPCA(**kw).fit(shard(Zq), **fk)
-        left = np.asarray(got.estimate_left_sv)
+        left = tonp(got.estimate_left_sv)
         fullL = torch.cat(comm.all_gather_varlen(torch.as_tensor(left.T).contiguous())).T.numpy()
         Ug = torch.cat(comm.all_gather_varlen(
-            torch.as_tensor(np.asarray(got.left_sv).T).contiguous())).T.numpy()
-        refL = np.asarray(ref.estimate_left_sv)
+            torch.as_tensor(tonp(got.left_sv).T).contiguous())).T.numpy()
+        refL = tonp(ref.estimate_left_sv)
         res[f"qpca_{solver}_{'true' if tt else 'gauss'}"] = dict(
-            sv_rel=rel(got.singular_values_, ref.singular_values_),
-            comp_absdiff=float(np.max(np.abs(np.abs(got.components_) - np.abs(ref.components_)))),
+            sv_rel=rel(tonp(got.singular_values_), tonp(ref.singular_values_)),
+            comp_absdiff=float(np.max(np.abs(np.abs(tonp(got.components_)) - np.abs(tonp(ref.components_))))),
             left_err=[float(v) for v in np.linalg.norm(fullL - Ug, axis=1)],
             left_shape=list(fullL.shape),
             # Gaussian tomography draws Philox element (i, global column):

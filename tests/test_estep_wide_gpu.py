@@ -105,7 +105,7 @@ def test_generic_gpu_engine_is_exact(n, d, k):
     uncertified library-GEMM fallback."""
     rs = np.random.RandomState(k)
     X = (rs.randn(n, d) * 1.5).astype(np.float32)
-    C = (X[rs.choice(n, min(k, n), replace=True)] + 0.05 * rs.randn(k, d)).astype(np.float32)
+    C = (X[rs.choice(n, k, replace=True)] + 0.05 * rs.randn(k, d)).astype(np.float32)
     Xt = torch.from_numpy(X).cuda()
     eng = LloydEngine(Xt, k, delta=0.3, seed=5, gemm_precision="fp32",
                       generic=(d == 7))

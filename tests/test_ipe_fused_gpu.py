@@ -50,6 +50,7 @@ def _run_kernel(x, c, n, eps, Q, cuda, seed=0):
     dp = 32
     while dp < d:
         dp *= 2
+    assert dp <= 1024
     xn = (X.double() ** 2).sum(1).float()
     cn = (C.double() ** 2).sum(1).float()
     lab = torch.empty(n, dtype=torch.int32, device=cuda)
@@ -160,3 +161,32 @@ def test_qmeans_ipe_end_to_end_gpu(cuda):
     assert adjusted_rand_score(y, g.labels_) > 0.95
     assert adjusted_rand_score(y, c.labels_) > 0.95
     assert abs(g.inertia_ - c.inertia_) < 0.1 * c.inertia_
+
+
+@pytest.mark.parametrize("d", [384, 784])
+def test_ipe_fused_law_exact_wide(cuda, d):
+    """d_pad 512 / 1024: the workgroup-shared A tile; same exact median law."""
+    rng = np.random.default_rng(d)
+    x = rng.standard_normal(d)
+    c = x + 0.8 * rng.standard_normal(d)
+    s, nx2, ny2, ip = _run_kernel(x, c, 40000, 0.25, 13, cuda, seed=3)
+    M, vals, pm = _exact_law(ip, nx2, ny2, 0.25, 13)
+    assert M <= 128
+    assert _gof(s, vals, pm) > 1e-4
+
+
+def test_ipe_fused_argmin_wide(cuda):
+    rng = np.random.default_rng(4)
+    n, d, k = 2048, 600, 40
+    centers = rng.standard_normal((k, d)) * 4
+    X = centers[rng.integers(0, k, n)] + 0.3 * rng.standard_normal((n, d))
+    Xt = torch.tensor(X, dtype=torch.float32, device=cuda)
+    Ct = torch.tensor(centers, dtype=torch.float32, device=cuda)
+    xn = (Xt.double() ** 2).sum(1).float()
+    cn = (Ct.double() ** 2).sum(1).float()
+    lab = torch.empty(n, dtype=torch.int32, device=cuda)
+    mind = torch.empty(n, dtype=torch.float32, device=cuda)
+    K.ipe_fused_native(Xt, K.ipe_center_fragments(Ct, 48, 1024), xn, cn, k, 48, 1024, 0.05, 13,
+                       RngKey(7, "ipe", 0), RngKey(7, "band_select", 0), 0, lab, mind)
+    D = ((X[:, None, :] - centers[None]) ** 2).sum(-1)
+    assert np.mean(lab.cpu().numpy() == D.argmin(1)) > 0.99
