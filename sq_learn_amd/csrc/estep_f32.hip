@@ -423,6 +423,17 @@ struct X64Geom {
   static constexpr int SLOT = SK * 2048;           // bytes per LDS slot
 };
 
+// Row sets of 32 per wave: 2 (64 rows share each staged B fragment - half
+// the L2 -> LDS staging per row, which bounds the d <= 256 sweep) while the
+// A fragments fit the registers; 1 above d_pad = 256.
+#ifndef SQ_X64_RS
+#define SQ_X64_RS 2
+#endif
+template <int KSD>
+struct X64RowSets {
+  static constexpr int value = KSD <= 16 ? SQ_X64_RS : 1;
+};
+
 template <typename F, int... I>
 SQ_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
@@ -432,7 +443,7 @@ SQ_DEV void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int KSD>
+template <int KSD, int RS>
 __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     const _Float16* __restrict__ Xh, const float* __restrict__ X, const _Float16* __restrict__ C,
     const float* __restrict__ Cm, const float* __restrict__ xn, const float* __restrict__ cmax2_p,
@@ -448,13 +459,13 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   constexpr int KT = GEO::KT, NS = GEO::NS, SK = GEO::SK, SLOT = GEO::SLOT;
   constexpr int TILE_STRIDE = (2 * KSD + 1) * 2048;
   constexpr int PIECES = SLOT / 1024;           // 1 KiB LDS-DMA pieces per slot
-  constexpr int ROWS = NW * 32;
+  constexpr int ROWS = NW * 32 * RS;              // RS sets of 32 rows per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int RING = kX64Ring;                // LDS slots
   constexpr int PPW = (PIECES + NW - 1) / NW;   // glds per wave per stage (uniform: counted vmcnt)
   auto buf = [&](int g) -> unsigned char* { return smem + (g % RING) * SLOT; };
-  int* cand_all = reinterpret_cast<int*>(smem + RING * SLOT);        // [NW][32][kMaxCand]
-  int* cnt_all = cand_all + NW * 32 * kMaxCand;                       // [NW][32]
+  int* cand_all = reinterpret_cast<int*>(smem + RING * SLOT);        // [NW][RS][32][kMaxCand]
+  int* cnt_all = cand_all + NW * RS * 32 * kMaxCand;                  // [NW][RS][32]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -472,8 +483,6 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   const long long nblk = (ne + ROWS - 1) / ROWS;
   long long blk = blockIdx.x;
   if (blk >= nblk) return;
-  int* cand = cand_all + wave * 32 * kMaxCand;
-  int* cnt = cnt_all + wave * 32;
   const uint32_t qmask = (1u << qbits) - 1u;
   const uint32_t keep = ~qmask;
   // rigorous bound constants (fp32, rounded up by the 1.0625 / 1+2^-16 factors)
@@ -502,31 +511,37 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     }
   };
 
-  f16x8 ah[KSD];
+  // the wave's RS sets of 32 rows share every B fragment (register blocking:
+  // the staged centroid tiles are read once per 32 RS rows)
+  f16x8 ah[RS][KSD];
   auto load_a = [&](long long b) {
-    const long long r = row_at(b * ROWS + wave * 32 + r32);
-    const _Float16* xr = Xh + (size_t)r * DX + half * 8;
 #pragma unroll
-    for (int ks = 0; ks < KSD; ++ks) ah[ks] = *reinterpret_cast<const f16x8*>(xr + ks * 16);
+    for (int st = 0; st < RS; ++st) {
+      const long long r = row_at(b * ROWS + (wave * RS + st) * 32 + r32);
+      const _Float16* xr = Xh + (size_t)r * DX + half * 8;
+#pragma unroll
+      for (int ks = 0; ks < KSD; ++ks) ah[st][ks] = *reinterpret_cast<const f16x8*>(xr + ks * 16);
+    }
   };
   f16x8 aug = (f16x8)0;
   if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
 
-  float m1[16], m2[16], m3[16];
+  float m1[RS][16], m2[RS][16], m3[RS][16];
   const int lane_off = (half * 64 + r32) * 16;
   auto ldb = [&](const unsigned char* p) -> f16x8 { return *reinterpret_cast<const f16x8*>(p); };
-  auto ins = [&](int i, float v, uint32_t q) {
+  auto ins = [&](int st, int i, float v, uint32_t q) {
     const float p = and_or(v, keep, q);   // (v & keep) | q: the tile index in the low bits
-    const float a1 = m1[i], a2 = m2[i];
-    m3[i] = vmed3(a2, p, m3[i]);
-    m2[i] = vmed3(a1, p, a2);
-    m1[i] = vmin(a1, p);
+    const float a1 = m1[st][i], a2 = m2[st][i];
+    m3[st][i] = vmed3(a2, p, m3[st][i]);
+    m2[st][i] = vmed3(a1, p, a2);
+    m1[st][i] = vmin(a1, p);
   };
+  typedef f32x16 Acc[RS][2];
   // k-steps [S SK, min((S+1) SK, KT)) of the current tile from the slot at
   // cur, with the epilogue rows of the previous tile (o0 / o1, tile t_prev)
   // spread over the tile's KT k-steps
-  auto sub_step = [&](auto S_, const unsigned char* cur, f32x16& acc0, f32x16& acc1,
-                      const f32x16& o0, const f32x16& o1, int t_prev, bool do_epi) {
+  auto sub_step = [&](auto S_, const unsigned char* cur, Acc& acc, const Acc& o, int t_prev,
+                      bool do_epi) {
     constexpr int S = decltype(S_)::value;
     constexpr int K0 = S * SK, K1 = (S + 1) * SK < KT ? (S + 1) * SK : KT;
     const uint32_t q0 = (uint32_t)(t_prev * 2), q1 = q0 + 1u;
@@ -541,14 +556,18 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
         b0[nx] = ldb(hb + (ks + 1 - K0) * 2048);
         b1[nx] = ldb(hb + (ks + 1 - K0) * 2048 + 512);
       }
-      const f16x8 A = ks < KSD ? ah[ks] : aug;
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b0[c], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b1[c], acc1, 0, 0, 0);
-      if (do_epi) {
 #pragma unroll
-        for (int i = (ks * 16) / KT; i < ((ks + 1) * 16) / KT; ++i) {
-          ins(i, o0[i], q0);
-          ins(i, o1[i], q1);
+      for (int st = 0; st < RS; ++st) {
+        const f16x8 A = ks < KSD ? ah[st][ks] : aug;
+        acc[st][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b0[c], acc[st][0], 0, 0, 0);
+        acc[st][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, b1[c], acc[st][1], 0, 0, 0);
+      }
+      if (do_epi) {
+        // the previous tile's RS x 16 rows, spread evenly over the KT k-steps
+#pragma unroll
+        for (int e = (ks * 16 * RS) / KT; e < ((ks + 1) * 16 * RS) / KT; ++e) {
+          ins(e / 16, e % 16, o[e / 16][0][e % 16], q0);
+          ins(e / 16, e % 16, o[e / 16][1][e % 16], q1);
         }
       }
 #if SQ_X64_PIN
@@ -556,13 +575,15 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
 #endif
     }
   };
-  auto epi_all = [&](const f32x16& o0, const f32x16& o1, int t_prev) {
+  auto epi_all = [&](const Acc& o, int t_prev) {
     const uint32_t q0 = (uint32_t)(t_prev * 2), q1 = q0 + 1u;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      ins(i, o0[i], q0);
-      ins(i, o1[i], q1);
-    }
+    for (int st = 0; st < RS; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        ins(st, i, o[st][0][i], q0);
+        ins(st, i, o[st][1][i], q1);
+      }
   };
   // RING == 2: the tile staged in this step must land before the barrier
   // (vmcnt(0)).  RING == 3: staging runs two tiles ahead and the barrier
@@ -581,17 +602,17 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   // one tile = NS sub-steps, each: stage the unit RING - 1 ahead, MFMAs on
   // the current unit, retire the next one (counted vmcnt + raw barrier)
   int U = 0;
-  auto tile = [&](f32x16& n0, f32x16& n1, const f32x16& o0, const f32x16& o1, int t_prev,
-                  bool do_epi) {
-    f32x16 acc0 = {0}, acc1 = {0};
+  auto tile = [&](Acc& acc, const Acc& o, int t_prev, bool do_epi) {
+    // accumulates straight into the destination set (its previous contents
+    // were the epilogue input of the tile before: consumed)
+#pragma unroll
+    for (int st = 0; st < RS; ++st) acc[st][0] = acc[st][1] = (f32x16){0};
     static_for<NS>([&](auto S_) {
       stage(U + RING - 1);
-      sub_step(S_, buf(U), acc0, acc1, o0, o1, t_prev, do_epi);
+      sub_step(S_, buf(U), acc, o, t_prev, do_epi);
       sync_tile();
       ++U;
     });
-    n0 = acc0;
-    n1 = acc1;
   };
 
   stage(0);
@@ -601,28 +622,103 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   __builtin_amdgcn_s_barrier();
 
   for (; blk < nblk; blk += gridDim.x) {
-    const long long row0 = blk * ROWS + wave * 32;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) m1[i] = m2[i] = m3[i] = __builtin_inff();
-    if (lane < 32) cnt[lane] = 0;
-    f32x16 pA0, pA1, pB0, pB1;
-    tile(pA0, pA1, pA0, pA1, 0, false);
-    int t = 0;
-    while (true) {
-      if (t + 1 >= n_tiles) {
-        load_a(blk + gridDim.x);   // clamped rows: unconditional (no phi on ah)
-        epi_all(pA0, pA1, t);
-        break;
+    for (int st = 0; st < RS; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m1[st][i] = m2[st][i] = m3[st][i] = __builtin_inff();
+    if (lane < 32)
+#pragma unroll
+      for (int st = 0; st < RS; ++st) cnt_all[(wave * RS + st) * 32 + lane] = 0;
+    if constexpr (RS == 1) {
+      Acc pA, pB;
+      tile(pA, pA, 0, false);
+      int t = 0;
+      while (true) {
+        if (t + 1 >= n_tiles) {
+          load_a(blk + gridDim.x);   // clamped rows: unconditional (no phi on ah)
+          epi_all(pA, t);
+          break;
+        }
+        tile(pB, pA, t, true);
+        ++t;
+        if (t + 1 >= n_tiles) {
+          load_a(blk + gridDim.x);
+          epi_all(pB, t);
+          break;
+        }
+        tile(pA, pB, t, true);
+        ++t;
       }
-      tile(pB0, pB1, pA0, pA1, t, true);
-      ++t;
-      if (t + 1 >= n_tiles) {
-        load_a(blk + gridDim.x);
-        epi_all(pB0, pB1, t);
-        break;
+    } else {
+      // RS row sets: each staged tile is swept one column half at a time
+      // (both row sets per B fragment); the half just finished is inserted
+      // during the next half's MFMAs - two RS x 16-register accumulator sets
+      // live instead of four
+      f32x16 cA[RS], cB[RS];
+      auto pass = [&](const unsigned char* cur, int h, f32x16 (&acc)[RS], const f32x16 (&o)[RS],
+                      uint32_t qo, bool do_epi) {
+#pragma unroll
+        for (int st = 0; st < RS; ++st) acc[st] = (f32x16){0};
+        const unsigned char* hb = cur + lane_off + h * 512;
+        f16x8 b[2];
+        b[0] = ldb(hb);
+#pragma unroll
+        for (int ks = 0; ks < KT; ++ks) {
+          const int c = ks & 1, nx = c ^ 1;
+          if (ks + 1 < KT) b[nx] = ldb(hb + (ks + 1) * 2048);
+#pragma unroll
+          for (int st = 0; st < RS; ++st)
+            acc[st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ks < KSD ? ah[st][ks] : aug, b[c],
+                                                             acc[st], 0, 0, 0);
+          if (do_epi) {
+#pragma unroll
+            for (int e = (ks * 16 * RS) / KT; e < ((ks + 1) * 16 * RS) / KT; ++e)
+              ins(e / 16, e % 16, o[e / 16][e % 16], qo);
+          }
+#if SQ_X64_PIN
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+      };
+      auto drain = [&](const f32x16 (&o)[RS], uint32_t qo) {
+#pragma unroll
+        for (int st = 0; st < RS; ++st)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) ins(st, i, o[st][i], qo);
+      };
+      static_assert(NS == 1, "row sets need whole tiles per LDS slot");
+      for (int t = 0; t < n_tiles; ++t) {
+        stage(U + RING - 1);
+        // half 0 of tile t (with the previous tile's half 1), then half 1
+        // (with this tile's half 0); packed index q = 2 t + half
+        pass(buf(U), 0, cA, cB, (uint32_t)(2 * t - 1), t > 0);
+        pass(buf(U), 1, cB, cA, (uint32_t)(2 * t), true);
+        sync_tile();
+        ++U;
       }
-      tile(pA0, pA1, pB0, pB1, t, true);
-      ++t;
+      load_a(blk + gridDim.x);   // clamped rows: unconditional
+      drain(cB, (uint32_t)(2 * n_tiles - 1));
+    }
+
+    // ---- per row set: row minimum, candidates, bounds, classification (a
+    // runtime loop: one copy of the code; the set's top-3 lists are selected
+    // by value into ms1..ms3 - compile-time register indices only)
+#pragma nounroll
+    for (int st = 0; st < RS; ++st) {
+    const long long row0 = blk * ROWS + (wave * RS + st) * 32;
+    int* cand = cand_all + (wave * RS + st) * 32 * kMaxCand;
+    int* cnt = cnt_all + (wave * RS + st) * 32;
+    float ms1[16], ms2[16], ms3[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ms1[i] = m1[0][i]; ms2[i] = m2[0][i]; ms3[i] = m3[0][i];
+#pragma unroll
+      for (int o = 1; o < RS; ++o) {
+        const float a1 = m1[o][i], a2 = m2[o][i], a3 = m3[o][i];
+        ms1[i] = st == o ? a1 : ms1[i];
+        ms2[i] = st == o ? a2 : ms2[i];
+        ms3[i] = st == o ? a3 : ms3[i];
+      }
     }
 
     // ---- row minimum (packed) by the transposed reduce-scatter: lane r32
@@ -644,7 +740,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     };
     float R[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) R[i] = m1[i];
+    for (int i = 0; i < 16; ++i) R[i] = ms1[i];
     const float rmin = row_min(R);
     const int irow = r32 >> 1;
     const int rl_own = (irow & 3) + 8 * (irow >> 2) + 4 * half;
@@ -662,20 +758,20 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float T = __shfl(T_own, 32 * half + 2 * i, 64);
-      nc[i] = m1[i] > T ? m1[i] : (m2[i] > T ? m2[i] : m3[i]);
+      nc[i] = ms1[i] > T ? ms1[i] : (ms2[i] > T ? ms2[i] : ms3[i]);
       const int rl = (i & 3) + 8 * (i >> 2) + 4 * half;
       auto jof = [&](float p) -> int {
         const uint32_t q = __float_as_uint(p) & qmask;
         return (int)((q >> 1) * kTileN + (q & 1u) * 32u) + r32;
       };
-      if (m3[i] <= T) atomicAdd(&cnt[rl], kMaxCand + 1);   // lane may hide more: dense
-      if (m1[i] <= T) {
+      if (ms3[i] <= T) atomicAdd(&cnt[rl], kMaxCand + 1);   // lane may hide more: dense
+      if (ms1[i] <= T) {
         const int s = atomicAdd(&cnt[rl], 1);
-        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(m1[i]);
+        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(ms1[i]);
       }
-      if (m2[i] <= T) {
+      if (ms2[i] <= T) {
         const int s = atomicAdd(&cnt[rl], 1);
-        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(m2[i]);
+        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(ms2[i]);
       }
     }
     // Hamerly bounds of this row (distances, not squared): ub >= |x - c_min|,
@@ -748,6 +844,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    }   // row sets
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -1390,8 +1487,10 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
                             void* ub, void* lb, void* mflag, void* xflag) {
   constexpr int NW = kX64Waves;
-  const size_t lds = kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * 32 * (kMaxCand + 1) * 4;
-  auto kern = estep_x64_kernel<KSD>;
+  constexpr int RS = X64RowSets<KSD>::value;
+  const size_t lds =
+      kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * RS * 32 * (kMaxCand + 1) * 4;
+  auto kern = estep_x64_kernel<KSD, RS>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1407,7 +1506,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   }
   int qbits = 1;
   while ((1 << qbits) < 2 * (k_pad / kTileN)) ++qbits;
-  const long long nblk = (n + NW * 32 - 1) / (NW * 32);
+  const long long nblk = (n + NW * 32 * RS - 1) / (NW * 32 * RS);
   // list mode: the row count is on the device - every resident slot launches
   const unsigned grid = (unsigned)(nblk < resident && !rlist ? nblk : resident);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const _Float16*)Xh,

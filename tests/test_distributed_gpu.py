@@ -14,7 +14,8 @@ The analogue of the reference's thread-count invariance test
 * classical KMeans with empty-cluster relocation (per-shard top-e +
   all-gather): bit-identical labels and centroids;
 * CholeskyQR2 sigma_min on the fp64-MFMA Gram, centred and not, and the
-  qPCA spectrum (full and randomized): fp64 sums over shards, <= 1e-10 rel;
+  full qPCA spectrum: fp64 sums over shards, <= 1e-10 rel; the randomized
+  spectrum: fp32 range-finder sums over shards, <= 1e-5 rel;
 * tomography of the row-sharded left singular vectors: Gaussian noise
   keyed by (vector, GLOBAL column) - the single-process draw; true
   tomography (rank-split multinomial) within its delta guarantee.
@@ -84,11 +85,13 @@ def test_sharded_gpu_fast_path_matches_single_process(world):
     for key in ("qpca_full_gauss", "qpca_full_true", "qpca_randomized_gauss",
                 "qpca_randomized_true"):
         q = res[key]
-        assert q["sv_rel"] <= 1e-9, (key, q)
-        assert q["comp_absdiff"] <= 1e-6, (key, q)
+        # full: fp64 Gram + CholQR2; randomized: the fp32 range finder's
+        # shard sums (fp32 rounding of the power-iteration products)
+        assert q["sv_rel"] <= (1e-9 if "full" in key else 1e-5), (key, q)
+        assert q["comp_absdiff"] <= (1e-6 if "full" in key else 1e-4), (key, q)
         assert q["left_shape"] == [4, 6007], (key, q)
         assert max(q["left_err"]) <= 0.3 + 1e-9, (key, q)     # the delta guarantee
         assert q["muA_rel"] <= 1e-10, (key, q)
         if key.endswith("gauss"):
             # same Philox elements as the unsharded draw
-            assert q["left_vs_ref"] <= 1e-5, (key, q)
+            assert q["left_vs_ref"] <= (1e-5 if "full" in key else 1e-4), (key, q)
