@@ -55,6 +55,7 @@ def parse(argv=None):
     ap.add_argument("--ipe-steps", type=int, default=2,
                     help="timed Lloyd steps of the IPE (true_distance_estimate) extra; 0 = skip")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--no-hard", action="store_true", help="skip the overlapping-blobs extra")
     return ap.parse_args(argv)
 
 
@@ -142,6 +143,74 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
         torch.cuda.empty_cache()
     except Exception as e:
         extra["ipe_error"] = repr(e)[:200]
+
+
+def _hard_extra(extra, a, comm, dev):
+    """A hard regime for the certified E-step: 1024 strongly overlapping
+    blobs (centres in [-0.1, 0.1]^d, unit spread) so that many rows have
+    several centroids within delta of their minimum.  Reports the steady-state
+    and unpruned ms per step, the first iteration, the dense / multi-candidate
+    row fractions of the last step and the mean delta-band size (fp64, on a
+    4096-row sample).  Rows: a.n / 5 (2M at the default)."""
+    try:
+        from sq_learn_amd.parallel.comm import shard_bounds
+        from sq_learn_amd.utils.datasets import make_blobs_device
+        from sq_learn_amd.models.cluster._lloyd import LloydEngine
+        from sq_learn_amd.models._data import Data, gather_rows
+        n = max(a.n // 5, 4096)
+        s0, s1 = shard_bounds(n, comm.rank, comm.world_size)
+        X, _ = make_blobs_device(n, a.d, centers=a.blobs, cluster_std=1.0, center_box=(-0.1, 0.1),
+                                 seed=a.seed + 1, device=dev, dtype=torch.float32,
+                                 row_range=(s0, s1))
+        data = Data(X, n, s0, comm, "sharded")
+        rs = np.random.RandomState(a.seed + 1)
+        C0 = gather_rows(data, rs.choice(n, a.k, replace=False))
+        eng = LloydEngine(X, a.k, delta=a.delta, true_distance_estimate=False,
+                          intermediate_error=True, true_tomography=False, seed=a.seed, comm=comm,
+                          row_offset=s0, gemm_precision="fp32")
+        eng.set_centers(C0)
+
+        def timed(steps):
+            _sync(dev)
+            comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                eng.step()[1].tolist()
+            _sync(dev)
+            comm.barrier()
+            return _max_over_ranks(comm, dev, (time.perf_counter() - t0) / steps * 1e3)
+
+        extra["hard_first_iter_ms"] = timed(1)
+        for _ in range(4):
+            eng.step()[1].tolist()
+        extra["hard_ms_per_step"] = timed(5)
+        cnt = eng.buf.counts.tolist()
+        tot = torch.tensor([float(cnt[1]), float(cnt[2])], dtype=torch.float64, device=dev)
+        comm.all_reduce_(tot)
+        extra["hard_dense_row_frac"] = float(tot[0]) / n
+        extra["hard_multi_row_frac"] = float(tot[1]) / n
+        if getattr(eng, "bounds", False):
+            eng.bounds = False
+            eng.step()[1].tolist()
+            extra["hard_unpruned_ms_per_step"] = timed(3)
+            cnt = eng.buf.counts.tolist()
+            tot = torch.tensor([float(cnt[1]), float(cnt[2])], dtype=torch.float64, device=dev)
+            comm.all_reduce_(tot)
+            extra["hard_unpruned_dense_row_frac"] = float(tot[0]) / n
+            extra["hard_unpruned_multi_row_frac"] = float(tot[1]) / n
+            eng.bounds = True
+        if comm.rank == 0:
+            m = min(4096, s1 - s0)
+            Xs = X[:m].double()
+            C = eng.centers().double()
+            D = ((Xs * Xs).sum(1)[:, None] + (C * C).sum(1)[None, :] - 2.0 * Xs @ C.T)
+            band = (D <= D.min(1, keepdim=True).values + a.delta).sum(1).double()
+            extra["hard_mean_band_size"] = float(band.mean())
+        extra["hard_rows"] = n
+        del eng, X
+        torch.cuda.empty_cache()
+    except Exception as e:
+        extra["hard_error"] = repr(e)[:200]
 
 
 def _fit_extra(extra, a, sa, comm, dev, init):
@@ -239,12 +308,39 @@ def main(argv=None):
             for kk, v in eng.step_phases().items():
                 ph[kk] = ph.get(kk, 0.0) + v / 3.0
         extra["phase_ms"] = {kk: round(v, 4) for kk, v in ph.items()}
+        # the regimes behind the steady-state number: the same iteration with
+        # the Hamerly pruning off (every row through the filter sweep) and the
+        # first iteration after (re)setting the centres (no valid bounds, the
+        # full incremental M-step start)
+        if getattr(eng, "bounds", False):
+            eng.bounds = False
+            step()
+            _sync(dev)
+            comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                step()
+            _sync(dev)
+            comm.barrier()
+            extra["unpruned_ms_per_step"] = _max_over_ranks(
+                comm, dev, (time.perf_counter() - t0) / 3 * 1e3)
+            eng.bounds = True
+        eng.set_centers(C0)
+        _sync(dev)
+        comm.barrier()
+        t0 = time.perf_counter()
+        step()
+        _sync(dev)
+        comm.barrier()
+        extra["first_iter_ms"] = _max_over_ranks(comm, dev, (time.perf_counter() - t0) * 1e3)
 
     del eng
     if gpu:
         torch.cuda.empty_cache()
     if a.ipe_steps > 0 and gpu:
         _ipe_extra(extra, a, X, comm, dev, start, C0)
+    if gpu and not a.no_hard:
+        _hard_extra(extra, a, comm, dev)
     from sq_learn_amd.parallel.sharding import ShardedArray
     sa = ShardedArray(X, a.n, start, comm)
     if not a.no_fit:
@@ -254,6 +350,9 @@ def main(argv=None):
         # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
         _qpca_extra(extra, "qpca_10Mx256_full_fit_s", sa, comm, dev, "full")
         _qpca_extra(extra, "qpca_10Mx256_full_truetomo_fit_s", sa, comm, dev, "full",
+                    true_tomography=True)
+        _qpca_extra(extra, "qpca_10Mx256_randomized_fit_s", sa, comm, dev, "randomized")
+        _qpca_extra(extra, "qpca_10Mx256_randomized_truetomo_fit_s", sa, comm, dev, "randomized",
                     true_tomography=True)
         del X, sa
         torch.cuda.empty_cache()
@@ -288,6 +387,12 @@ def main(argv=None):
                        "parallelism": f"dp{comm.world_size}"},
             "extra": extra,
         }
+        if "ipe_samples_iter_per_s" in extra:
+            # the reference's DEFAULT distance mode (true_distance_estimate=True)
+            out["co_headline"] = {
+                "metric": "q-means IPE (true_distance_estimate) samples*iter/s",
+                "value": extra["ipe_samples_iter_per_s"], "unit": "samples*iter/s",
+                "ms_per_step": extra.get("ipe_ms_per_step")}
         print(json.dumps(out), flush=True)
     if comm.distributed:
         import torch.distributed as dist

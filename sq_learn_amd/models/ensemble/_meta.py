@@ -15,6 +15,8 @@ import numbers
 from abc import ABCMeta, abstractmethod
 from copy import deepcopy
 
+from ...parallel.tasks import Parallel
+from ...utils.fixes import delayed
 import numpy as np
 
 from ...base import (BaseEstimator, ClassifierMixin, MetaEstimatorMixin, OutlierMixin,
@@ -25,6 +27,13 @@ from ...utils.validation import check_is_fitted, check_random_state
 
 MAX_INT = np.iinfo(np.int32).max
 
+
+
+def _fit_member(est, X, y, sample_weight):
+    """One ensemble member's fit (a task of the task layer)."""
+    if sample_weight is None:
+        return est.fit(X, y)
+    return est.fit(X, y, sample_weight=sample_weight)
 
 def _np(a):
     return a.detach().cpu().numpy() if hasattr(a, "detach") else np.asarray(a)
@@ -151,7 +160,8 @@ class BaseBagging(MetaEstimatorMixin, BaseEstimator):
         seeds = rs.randint(MAX_INT, size=n_more)
         self._seeds = np.concatenate([self._seeds, seeds])
         sw_ok = _accepts_sample_weight(base)
-        for seed in seeds:
+
+        def fit_one(seed):
             est = clone(base)
             _set_random_states(est, seed)
             r = check_random_state(seed)
@@ -168,6 +178,12 @@ class BaseBagging(MetaEstimatorMixin, BaseEstimator):
                 est.fit(X[:, feats], y, sample_weight=w)
             else:
                 est.fit(X[idx][:, feats], y[idx])
+            return est, feats
+
+        # members are independent (seeded per member): the task layer fans
+        # them out over n_jobs threads / the node's GPUs (reference
+        # ensemble/_bagging.py:382 Parallel(n_jobs))
+        for est, feats in Parallel(n_jobs=self.n_jobs)(delayed(fit_one)(sd) for sd in seeds):
             self.estimators_.append(est)
             self.estimators_features_.append(feats)
         if self.oob_score:
@@ -673,11 +689,10 @@ class _BaseVoting(TransformerMixin, MetaEstimatorMixin, _BaseComposition):
                              "%d estimators" % (len(self.weights), len(self.estimators)))
         self.estimators_ = []
         self.named_estimators_ = {}
-        for n, e in self.estimators:
-            if e == "drop":
-                continue
-            c = clone(e)
-            c.fit(X, y) if sample_weight is None else c.fit(X, y, sample_weight=sample_weight)
+        live = [(n, e) for n, e in self.estimators if e != "drop"]
+        fitted = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_member)(clone(e), X, y, sample_weight) for _, e in live)
+        for (n, _), c in zip(live, fitted):
             self.estimators_.append(c)
             self.named_estimators_[n] = c
         if hasattr(self.estimators_[0], "n_features_in_"):
@@ -806,11 +821,10 @@ class _BaseStacking(TransformerMixin, MetaEstimatorMixin, _BaseComposition):
             else self._default_final()
         self.estimators_ = []
         self.named_estimators_ = {}
-        for n, e in self.estimators:
-            if e == "drop":
-                continue
-            c = clone(e)
-            c.fit(X, y) if sample_weight is None else c.fit(X, y, sample_weight=sample_weight)
+        live_named = [(n, e) for n, e in self.estimators if e != "drop"]
+        fitted = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_member)(clone(e), X, y, sample_weight) for _, e in live_named)
+        for (n, _), c in zip(live_named, fitted):
             self.estimators_.append(c)
             self.named_estimators_[n] = c
         meth = self.stack_method if isinstance(self.stack_method, str) else None

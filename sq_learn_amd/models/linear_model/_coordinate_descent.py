@@ -73,9 +73,11 @@ def enet_path(X, y, *, l1_ratio=0.5, eps=1e-3, n_alphas=100, alphas=None, precom
     X = _as_dense64(X)
     y = np.asarray(y, dtype=np.float64)
     n_samples, n_features = X.shape
-    multi = y.ndim == 2 and y.shape[1] > 1
+    multi = y.ndim == 2
     if multi:
-        raise NotImplementedError("multi-output paths: fit one target at a time")
+        return _enet_path_multi_output(X, y, l1_ratio=l1_ratio, eps=eps, n_alphas=n_alphas,
+                                       alphas=alphas, Xy=Xy, coef_init=coef_init,
+                                       return_n_iter=return_n_iter, positive=positive, **params)
     y = y.ravel()
     tol = params.get("tol", 1e-4)
     max_iter = params.get("max_iter", 1000)
@@ -122,6 +124,45 @@ def enet_path(X, y, *, l1_ratio=0.5, eps=1e-3, n_alphas=100, alphas=None, precom
                           ConvergenceWarning)
         coefs[:, i] = w
         dual_gaps[i] = gap
+        n_iters.append(int(n_it))
+    if return_n_iter:
+        return alphas, coefs, dual_gaps, n_iters
+    return alphas, coefs, dual_gaps
+
+
+def _enet_path_multi_output(X, y, *, l1_ratio, eps, n_alphas, alphas, Xy, coef_init,
+                            return_n_iter, positive, **params):
+    """Multi-output path (reference ``linear_model/_coordinate_descent.py:
+    452-498``): the multi-task (L2,1) coordinate descent of
+    MultiTaskElasticNet warm-started along the alphas; coefs [n_targets,
+    n_features, n_alphas], dual gaps rescaled by 1 / n_samples."""
+    from ._lm_extra import _mt_cd
+    if positive:
+        raise ValueError("positive=True is not allowed for multi-output (y.ndim != 1)")
+    n_samples, n_features = X.shape
+    n_outputs = y.shape[1]
+    tol = params.get("tol", 1e-4)
+    max_iter = params.get("max_iter", 1000)
+    rng = check_random_state(params.get("random_state", None))
+    selection = params.get("selection", "cyclic")
+    if selection not in ("random", "cyclic"):
+        raise ValueError("selection should be either random or cyclic.")
+    if alphas is None:
+        alphas = _alpha_grid(X, y, Xy=Xy, l1_ratio=l1_ratio, fit_intercept=False, eps=eps,
+                             n_alphas=n_alphas)
+    else:
+        alphas = np.sort(np.asarray(alphas, dtype=np.float64))[::-1]
+    coefs = np.empty((n_outputs, n_features, len(alphas)), dtype=np.float64)
+    dual_gaps = np.empty(len(alphas))
+    n_iters = []
+    W = (np.zeros((n_outputs, n_features)) if coef_init is None
+         else np.array(coef_init, dtype=np.float64).reshape(n_outputs, n_features))
+    for i, alpha in enumerate(alphas):
+        l1 = float(alpha * l1_ratio * n_samples)
+        l2 = float(alpha * (1.0 - l1_ratio) * n_samples)
+        W, gap, _, n_it = _mt_cd(W, l1, l2, X, y, max_iter, tol, rng, selection == "random")
+        coefs[..., i] = W
+        dual_gaps[i] = gap / n_samples
         n_iters.append(int(n_it))
     if return_n_iter:
         return alphas, coefs, dual_gaps, n_iters

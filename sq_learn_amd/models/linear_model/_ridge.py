@@ -254,8 +254,26 @@ class RidgeCV(RegressorMixin, LinearModel):
         if self.scoring is None:
             scores = [-(e ** 2).mean(0).cpu().numpy() for e in errs]     # per target
         else:
-            from ...model_selection._validation import _get_scorer  # pragma: no cover
-            raise NotImplementedError("custom scoring with the built-in LOO")
+            # a user scorer on the leave-one-out predictions (reference
+            # _ridge.py:1518-1535): predictions = y - LOO residual, scored
+            # through an identity "estimator" whose predict returns its input,
+            # per target when alpha_per_target, else on the raveled arrays
+            from ...model_selection._validation import get_scorer
+            scorer = get_scorer(self.scoring)
+            Y = np.asarray(yc, dtype=np.float64).reshape(yc.shape[0], -1)
+            preds = [Y - e.cpu().numpy().reshape(Y.shape) for e in errs]
+            ident = _IdentityRegressor()
+            if isinstance(self, LinearClassifierMixin):
+                # RidgeClassifierCV: the class of the largest LOO score
+                # against the true class (reference _ridge.py:1546-1551)
+                ic = _IdentityClassifier(np.arange(Y.shape[1]))
+                scores = [np.full(Y.shape[1], scorer(ic, P, Y.argmax(axis=1))) for P in preds]
+            elif self.alpha_per_target and Y.shape[1] > 1:
+                scores = [np.array([scorer(ident, P[:, j], Y[:, j]) for j in range(Y.shape[1])])
+                          for P in preds]
+            else:
+                scores = [np.full(Y.shape[1], scorer(ident, P.ravel(), Y.ravel()))
+                          for P in preds]
         scores = np.stack(scores)                                    # (n_alphas, n_targets)
         if self.alpha_per_target and scores.shape[1] > 1:
             best = scores.argmax(0)
@@ -267,12 +285,41 @@ class RidgeCV(RegressorMixin, LinearModel):
             self.alpha_ = float(alphas[best])
             self.best_score_ = float(tot[best])
         if self.store_cv_values:
-            cvv = np.stack([(e ** 2).cpu().numpy() for e in errs], axis=-1)
+            if self.scoring is None:
+                cvv = np.stack([(e ** 2).cpu().numpy() for e in errs], axis=-1)
+            else:   # the reference stores the LOO predictions with a scorer
+                Y = np.asarray(yc, dtype=np.float64).reshape(yc.shape[0], -1)
+                cvv = np.stack([Y - e.cpu().numpy().reshape(Y.shape) for e in errs], axis=-1)
             self.cv_values_ = cvv[:, 0, :] if y.ndim == 1 else cvv
         coef = _solve(Xc, yc, self.alpha_, "svd", self._device()).cpu().numpy()
         self.coef_ = coef.ravel() if y.ndim == 1 else coef
         self._set_intercept(X_offset, y_offset, X_scale)
         return self
+
+
+class _IdentityRegressor:
+    """Scorer adapter: ``predict`` / ``decision_function`` return their input
+    (the LOO predictions themselves; reference ``_ridge.py:1433``)."""
+
+    def decision_function(self, y_predict):
+        return y_predict
+
+    def predict(self, y_predict):
+        return y_predict
+
+
+class _IdentityClassifier(LinearClassifierMixin):
+    """Scorer adapter of RidgeClassifierCV: ``decision_function`` returns its
+    input, ``predict`` the class of its largest column."""
+
+    def __init__(self, classes):
+        self.classes_ = classes
+
+    def decision_function(self, y_predict):
+        return y_predict
+
+    def predict(self, y_predict):
+        return self.classes_[np.asarray(y_predict).argmax(axis=1)]
 
 
 class RidgeClassifierCV(LinearClassifierMixin, RidgeCV):

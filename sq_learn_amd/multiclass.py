@@ -3,14 +3,16 @@
 vote + normalised-confidence tie breaking of ``_ovr_decision_function``
 (reference utils/multiclass.py:442), ``OutputCodeClassifier`` :790.
 
-Sub-estimators are independent; when they run on the GPU each one keeps
-its data resident, so they are fitted sequentially in this process (the
-device is already saturated by one fit) - ``n_jobs`` is accepted for API
-compatibility."""
+Sub-estimators are independent tasks of the task layer
+(``parallel/tasks.py``): ``n_jobs`` worker threads, task i pinned to GPU
+i mod n_gpus when several GPUs are visible (reference ``Parallel(n_jobs)``
+at multiclass.py:281, 339, 641, 696)."""
 
 import numpy as np
 import scipy.sparse as sp
 
+from .parallel.tasks import Parallel
+from .utils.fixes import delayed
 from .base import BaseEstimator, ClassifierMixin, MetaEstimatorMixin, clone, is_regressor
 from .metrics import euclidean_distances
 from .preprocessing import LabelBinarizer
@@ -96,10 +98,13 @@ class OneVsRestClassifier(MetaEstimatorMixin, ClassifierMixin, BaseEstimator):
         Y = Y.tocsc() if sp.issparse(Y) else sp.csc_matrix(Y)
         self.classes_ = self.label_binarizer_.classes_
         cols = (np.asarray(col.toarray()).ravel() for col in Y.T)
-        self.estimators_ = [_fit_binary(self.estimator, X, c,
-                                        classes=["not %s" % self.label_binarizer_.classes_[i],
-                                                 self.label_binarizer_.classes_[i]])
-                            for i, c in enumerate(cols)]
+        # one binary problem per class, fanned out by the task layer
+        # (reference multiclass.py:281 Parallel(n_jobs))
+        self.estimators_ = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_binary)(self.estimator, X, c,
+                                 classes=["not %s" % self.label_binarizer_.classes_[i],
+                                          self.label_binarizer_.classes_[i]])
+            for i, c in enumerate(cols))
         if hasattr(self.estimators_[0], "n_features_in_"):
             self.n_features_in_ = self.estimators_[0].n_features_in_
         return self
@@ -189,8 +194,9 @@ class OneVsOneClassifier(MetaEstimatorMixin, ClassifierMixin, BaseEstimator):
         if len(self.classes_) == 1:
             raise ValueError("OneVsOneClassifier can not be fit when only one class is present.")
         n = self.classes_.shape[0]
-        fits = [_fit_ovo_binary(self.estimator, X, y, self.classes_[i], self.classes_[j])
-                for i in range(n) for j in range(i + 1, n)]
+        fits = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_ovo_binary)(self.estimator, X, y, self.classes_[i], self.classes_[j])
+            for i in range(n) for j in range(i + 1, n))   # reference multiclass.py:641
         self.estimators_ = [f[0] for f in fits]
         self.pairwise_indices_ = None
         self.n_features_in_ = X.shape[1]
@@ -265,7 +271,8 @@ class OutputCodeClassifier(MetaEstimatorMixin, ClassifierMixin, BaseEstimator):
             self.code_book_[self.code_book_ != 1] = 0
         cls_idx = {c: i for i, c in enumerate(self.classes_)}
         Y = np.array([self.code_book_[cls_idx[v]] for v in y], dtype=int)
-        self.estimators_ = [_fit_binary(self.estimator, X, Y[:, i]) for i in range(Y.shape[1])]
+        self.estimators_ = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_binary)(self.estimator, X, Y[:, i]) for i in range(Y.shape[1]))
         self.n_features_in_ = X.shape[1]
         return self
 

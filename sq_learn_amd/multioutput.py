@@ -5,6 +5,8 @@ estimator per target column) and the chains ``ClassifierChain`` :540 /
 targets - true targets at fit time, or out-of-fold predictions with
 ``cv`` - and predictions at inference time)."""
 
+from .parallel.tasks import Parallel
+from .utils.fixes import delayed
 import numpy as np
 import scipy.sparse as sp
 
@@ -28,6 +30,12 @@ def _has_est(attr):
     return check
 
 
+def _fit_estimator(est, X, y, sample_weight, fit_params):
+    if sample_weight is not None:
+        return est.fit(X, y, sample_weight=sample_weight, **fit_params)
+    return est.fit(X, y, **fit_params)
+
+
 class _MultiOutputEstimator(MetaEstimatorMixin, MultiOutputMixin, BaseEstimator):
     def __init__(self, estimator, *, n_jobs=None):
         self.estimator = estimator
@@ -40,14 +48,11 @@ class _MultiOutputEstimator(MetaEstimatorMixin, MultiOutputMixin, BaseEstimator)
                              "but has only one.")
         if is_classifier(self):
             self.classes_ = []
-        self.estimators_ = []
-        for j in range(y.shape[1]):
-            e = clone(self.estimator)
-            if sample_weight is not None:
-                e.fit(X, y[:, j], sample_weight=sample_weight, **fit_params)
-            else:
-                e.fit(X, y[:, j], **fit_params)
-            self.estimators_.append(e)
+        # one independent fit per output, fanned out by the task layer
+        # (reference multioutput.py:186 Parallel(n_jobs))
+        self.estimators_ = Parallel(n_jobs=self.n_jobs)(
+            delayed(_fit_estimator)(clone(self.estimator), X, y[:, j], sample_weight, fit_params)
+            for j in range(y.shape[1]))
         if is_classifier(self):
             self.classes_ = [e.classes_ for e in self.estimators_]
         if hasattr(self.estimators_[0], "n_features_in_"):

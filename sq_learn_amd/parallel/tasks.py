@@ -20,15 +20,71 @@ failing task's exception (in task order) is re-raised.
     scores = Parallel(n_jobs=4)(delayed(fit_and_score)(clone(est), f) for f in folds)
 """
 
+import contextlib
 import os
+import threading
 from concurrent.futures import ThreadPoolExecutor
 
 from .._config import get_config
 from ..utils.fixes import _FuncWrapper
 
+# ------------------------------------------------------------- backends
+# A backend turns a list of task thunks into results.  'threading' (the
+# default: worker threads, task i pinned to GPU i mod n_gpus) and
+# 'sequential' are built in; joblib's process backends ('loky',
+# 'multiprocessing') map to 'threading' - the heavy work of a task is HIP
+# kernels or the ctypes host library with the GIL released, and a process
+# backend would re-exec workers on a GPU host.  register_parallel_backend adds
+# a backend from a factory returning a concurrent.futures-style executor
+# (``submit`` + ``shutdown``), e.g. a ProcessPoolExecutor for pure-python
+# CPU tasks.
+_BACKENDS = {}
+_DEFAULT = {"name": "threading"}
+_LOCAL = threading.local()
+
+
+def register_parallel_backend(name, factory, make_default=False):
+    """Register ``factory(n_jobs) -> executor`` under ``name`` (reference
+    ``utils/__init__.py:50``, joblib's register_parallel_backend)."""
+    if not callable(factory):
+        raise TypeError("factory must be callable")
+    _BACKENDS[str(name)] = factory
+    if make_default:
+        _DEFAULT["name"] = str(name)
+
+
+def _active():
+    stack = getattr(_LOCAL, "stack", None)
+    return stack[-1] if stack else (_DEFAULT["name"], None, {})
+
+
+@contextlib.contextmanager
+def parallel_backend(backend, n_jobs=-1, inner_max_num_threads=None, **backend_params):
+    """Context manager selecting the task backend and its default n_jobs for
+    the ``Parallel`` calls inside it (reference ``utils/__init__.py:49``,
+    joblib's parallel_backend): ``Parallel(n_jobs=None)`` then uses
+    ``n_jobs``.  Thread-local, nestable."""
+    name = str(backend)
+    if name not in ("threading", "sequential", "loky", "multiprocessing") and name not in _BACKENDS:
+        raise ValueError(f"Invalid backend: {backend!r}")
+    stack = getattr(_LOCAL, "stack", None)
+    if stack is None:
+        stack = _LOCAL.stack = []
+    stack.append((name, n_jobs, dict(backend_params)))
+    try:
+        yield name, n_jobs
+    finally:
+        stack.pop()
+
 
 def effective_n_jobs(n_jobs=None):
-    """joblib's convention: None -> 1, -1 -> all CPUs, -k -> CPUs + 1 - k."""
+    """joblib's convention: None -> the active backend's n_jobs (1 outside a
+    parallel_backend context), -1 -> all CPUs, -k -> CPUs + 1 - k."""
+    if n_jobs is None:
+        name, ctx_jobs, _ = _active()
+        if name == "sequential":
+            return 1
+        n_jobs = ctx_jobs
     if n_jobs is None or n_jobs == 0:
         return 1
     n_jobs = int(n_jobs)
@@ -63,6 +119,7 @@ class Parallel:
         self.n_jobs = n_jobs
         self.devices = devices
         self.verbose = verbose
+        self.backend = None if backend in (None, "loky", "multiprocessing") else str(backend)
 
     @staticmethod
     def _run(task, gpu):
@@ -79,9 +136,17 @@ class Parallel:
 
     def __call__(self, iterable):
         tasks = list(iterable)
+        name = self.backend or _active()[0]
         n = min(effective_n_jobs(self.n_jobs), max(len(tasks), 1))
-        if n <= 1:
+        if n <= 1 or name == "sequential":
             return [self._run(t, None) for t in tasks]
+        if name in _BACKENDS:
+            ex = _BACKENDS[name](n)
+            try:
+                futures = [ex.submit(t[0], *t[1], **t[2]) for t in tasks]
+                return [f.result() for f in futures]
+            finally:
+                ex.shutdown(wait=True)
         slots = _gpu_slots(self.devices)
         gpus = [slots[i % len(slots)] if slots else None for i in range(len(tasks))]
         with ThreadPoolExecutor(max_workers=n, thread_name_prefix="sq-task") as ex:
@@ -89,4 +154,4 @@ class Parallel:
             return [f.result() for f in futures]
 
 
-__all__ = ["Parallel", "effective_n_jobs"]
+__all__ = ["Parallel", "effective_n_jobs", "parallel_backend", "register_parallel_backend"]

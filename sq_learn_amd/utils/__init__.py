@@ -62,6 +62,9 @@ from .validation import (check_array, check_consistent_length, check_random_stat
                          check_scalar, check_X_y, column_or_1d, check_memory,
                          check_non_negative, has_fit_parameter)
 
+from ..exceptions import DataConversionWarning  # noqa: E402,F401
+from ..parallel.tasks import parallel_backend, register_parallel_backend  # noqa: E402,F401
+
 from ._aliases import alias_reference_layout  # noqa: E402
 
 alias_reference_layout(__name__)
