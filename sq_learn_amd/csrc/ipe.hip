@@ -248,20 +248,206 @@ SQ_DEV float ipe_distance(float ipf, double nx2, double ny2, double eps, int Q, 
   return (float)(2.0 * S * at);
 }
 
+// ---------------------------------------------------------------- pruning
+// A pair can change a row's label only if its estimate D~ is <= the row's
+// best estimate so far, thr.  For odd Q the median's value class t (values
+// increase with t = min(j, M - j)) is <= t_b = max{t : D~(t) <= thr} iff at
+// least h = (Q+1)/2 of the Q draws fall in L = {bins of class <= t_b}:
+// P(in L) = pi_L = P(Bin(Q, p_L) >= h), p_L the Fejer mass of L.  Every bin of
+// L lies >= m = omega - t_b bins from omega, and the Fejer pmf is
+// sin^2(pi phi) / (M^2 sin^2(pi delta / M)) <= 1 / (4 delta^2) (Jordan), so
+// p_L <= pbar = (1/m + 1/m^2) / 2 and pi_L <= pibar = P(Bin(Q, pbar) >= h).
+// The sampler draws u (53 bits) once: u >= pibar -> the pair loses (exactly
+// the event u >= pi_L, which contains it); otherwise p_L and pi_L are summed
+// exactly, u >= pi_L loses, and u < pi_L gives the number c >= h of draws in
+// L (P(C = c | C >= h), inverted with the same u) and the median = the h-th
+// smallest of c iid draws from the Fejer law restricted to L: F_L^-1(p_L V),
+// V ~ Beta(h, c - h + 1) from a fresh uniform.  Exact law of "D~ if <= thr";
+// the cost of a losing pair is an fp32 bound plus one Philox block.
+
+// x = G^-1(u), G(x) = P(Bin(c, x) >= h): the h-th order statistic of c uniforms
+SQ_DEV double order_stat_inv(double u, int c, int h) {
+  if (c == 1) return u;
+  double cq = (double)c;                  // c C(c-1, h-1)
+  for (int i = 1; i < h; ++i) cq = cq * (double)(c - i) / (double)i;
+  double lo = 0.0, hi = 1.0;
+  const double mean = (double)h / (c + 1.0);
+  const double sd = sqrt(mean * (1.0 - mean) / (c + 2.0));
+  double x = mean + 1.4142135623730951 * sd * (double)erfinvf((float)(2.0 * u - 1.0));
+  x = fmin(fmax(x, 1e-12), 1.0 - 1e-12);
+  for (int it = 0; it < 60; ++it) {
+    const double g = binom_upper_tail(x, c, h) - u;
+    if (g > 0.0) hi = x; else lo = x;
+    double dens = cq;
+    for (int i = 0; i < h - 1; ++i) dens *= x;
+    for (int i = 0; i < c - h; ++i) dens *= 1.0 - x;
+    double xn = dens > 0.0 ? x - g / dens : 0.5 * (lo + hi);
+    if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+    const bool done = fabs(xn - x) <= 1e-15 * fmax(fmin(x, 1.0 - x), 1e-300) || hi - lo <= 1e-16;
+    x = xn;
+    if (done) break;
+  }
+  return x;
+}
+
+// the rare branch of the pruned sampler (u < pibar): exact p_L, pi_L, c and
+// the restricted-law median by class walks (fp64 angle-addition recurrence)
+SQ_DEV float ipe_pruned_exact(double ip, double S, double eps, int Q, float thr, double u,
+                              WordStream& ws) {
+  const double PI = 3.14159265358979323846;
+  double a = (S - 2.0 * ip) / (2.0 * S);
+  if (fabs(a) <= 1e-15) a = 0.0;
+  a = fmin(fmax(a, 0.0), 1.0);
+  const double eps_a = eps * fmax(1.0, fabs(ip)) / S;
+  long long M = ae_bins(eps_a);
+  if (M > (1LL << 40)) M = 1LL << 40;
+  if (M < 1) M = 1;
+  const double Md = (double)M;
+  const double omega = Md * asin(sqrt(a)) / PI;
+  const double fl = floor(omega);
+  const double phi = omega - fl;
+  const float INF = __builtin_inff();
+  if (phi == 0.0) {   // point mass on the class of bin floor(omega)
+    long long j = (long long)fl % M;
+    if (j < 0) j += M;
+    const long long t = j < M - j ? j : M - j;
+    const double s = sin(PI * (double)t / Md);
+    const float v = (float)(2.0 * S * s * s);
+    return v <= thr ? v : INF;
+  }
+  const double sp = sin(PI * phi);
+  const double num = sp * sp / (Md * Md);
+  double sa, ca, sb, cb;
+  sincos(PI / Md, &sa, &ca);
+  sincos(PI * omega / Md, &sb, &cb);
+  const long long tmax = M / 2;
+  const int h = (Q + 1) / 2;
+  // pass 1: p_L = mass of the classes whose value is <= thr
+  double st = 0.0, ct = 1.0, F = 0.0;
+  long long tb = -1;
+  for (long long t = 0; t <= tmax; ++t) {
+    if ((float)(2.0 * S * st * st) > thr) break;
+    const double sm = st * cb - ct * sb;
+    double mass = num / (sm * sm);
+    if (t != 0 && 2 * t != M) {
+      const double spl = st * cb + ct * sb;
+      mass += num / (spl * spl);
+    }
+    F += mass;
+    tb = t;
+    const double nst = st * ca + ct * sa;
+    ct = ct * ca - st * sa;
+    st = nst;
+  }
+  if (tb < 0) return INF;
+  const double pL = fmin(F, 1.0);
+  if (!(u < binom_upper_tail(pL, Q, h))) return INF;
+  // c = number of draws in L given >= h of them: P(C >= c) > u >= P(C >= c + 1)
+  int c = h;
+  {
+    const double q = 1.0 - pL;
+    double tail = 0.0;
+    for (int cc = Q; cc >= h; --cc) {
+      double pm = 1.0;   // C(Q, cc) pL^cc q^(Q - cc)
+      for (int i = 0; i < cc; ++i) pm *= pL * (double)(Q - i) / (double)(i + 1);
+      for (int i = 0; i < Q - cc; ++i) pm *= q;
+      tail += pm;
+      if (tail > u) { c = cc; break; }
+    }
+  }
+  const uint32_t w0 = ws.next(), w1 = ws.next();
+  const double u2 = ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
+                    (1.0 / 9007199254740992.0);
+  const double target = pL * order_stat_inv(u2, c, h);
+  // pass 2: the restricted-law inverse CDF
+  st = 0.0; ct = 1.0; F = 0.0;
+  double v = 0.0;
+  for (long long t = 0; t <= tb; ++t) {
+    const double sm = st * cb - ct * sb;
+    double mass = num / (sm * sm);
+    if (t != 0 && 2 * t != M) {
+      const double spl = st * cb + ct * sb;
+      mass += num / (spl * spl);
+    }
+    F += mass;
+    v = st * st;
+    if (F >= target) break;
+    const double nst = st * ca + ct * sa;
+    ct = ct * ca - st * sa;
+    st = nst;
+  }
+  return (float)(2.0 * S * v);
+}
+
+// D~ of the pair when it is <= thr, +inf when it is not (pruned sampler
+// above, odd Q); pairs the fp32 bound cannot separate from thr (m < 3, a ~ 1,
+// t_b beyond the walk cap) take the full sampler.
+SQ_DEV float ipe_distance_thr(float ipf, float nx2, float ny2, double eps, int Q, const RngKey& key,
+                              unsigned long long sid, float thr, int h, float cqh) {
+  const float INF = __builtin_inff();
+  if (thr < INF) {
+    // screen: a, r = thr (1 + 2^-22) / 2S (every D~(t) <= thr has
+    // sin^2(pi t / M) <= r) and eps_a in fp64, rounded once to fp32 (relative
+    // 2^-24); M within a few fp32 ulps, sqrtf / asinf within 2 ulps, covered by
+    // the margins below (the bound on m only has to be a LOWER bound)
+    const double Sd = (double)nx2 + (double)ny2;
+    const double inv = 0.5 / Sd;
+    const float a = (float)((Sd - 2.0 * (double)ipf) * inv);
+    const float r = (float)((double)thr * inv * (1.0 + 2.4e-7));
+    if (Sd > 0.0 && a < 0.99f && r < a) {
+      const float epsa = (float)(eps * fmax(1.0, fabs((double)ipf)) * 2.0 * inv);
+      const float Mf = fminf(1.5707963f / epsa * (1.0f + sqrtf(1.0f + 4.0f * epsa)), 1.0995116e12f);
+      const float Mlb = floorf(Mf * (1.0f - 1e-5f));
+      const float ra = fmaxf(r, 0.0f);
+      const float beta = asinf(sqrtf(a)), beta_t = asinf(sqrtf(ra));
+      const float marg = 1e-6f * (3.0f + 1.0f / sqrtf(1.0f - a) + 1.0f / sqrtf(1.0f - ra));
+      const float m = Mlb * (beta - beta_t - marg) * 0.31830987f;
+      const float tcap = Mf * beta_t * 0.31830989f;   // ~ t_b: the rare branch walks that far
+      if (m >= 3.0f && tcap <= 65536.0f) {
+        const float pbar = fminf(0.5f * (1.0f / m + 1.0f / (m * m)) * (1.0f + 1e-5f), 1.0f);
+        float pu = cqh;   // union bound C(Q, h) pbar^h >= pibar
+        for (int i = 0; i < h; ++i) pu *= pbar;
+        WordStream ws(key, sid);
+        const uint32_t w0 = ws.next();
+        if ((double)w0 * (1.0 / 4294967296.0) >= (double)pu * (1.0 + 1e-6)) return INF;
+        double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
+        const uint32_t w1 = ws.next();
+        const double u = ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
+                         (1.0 / 9007199254740992.0);
+        if (u >= pib) return INF;
+        return ipe_pruned_exact((double)ipf, (double)nx2 + (double)ny2, eps, Q, thr, u, ws);
+      }
+    }
+  }
+  return ipe_distance(ipf, (double)nx2, (double)ny2, eps, Q, key, sid);
+}
+
+SQ_DEV bool ipe_better(float ob, uint32_t ok, int oj, float b, uint32_t kk, int jj) {
+  return ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)));
+}
+
+// prune = 1 (odd Q): pass 1 sweeps the centroid tiles for the exact fp32
+// distance argmin j* of each row (a hint only), the 16 hint pairs are
+// sampled in full, and pass 2 samples every other pair against the row's
+// running best (initially the hint's D~) with the pruned sampler.
 template <int D4>
 __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     const float* __restrict__ X, long long ldx, const float* __restrict__ Cf,
     const float* __restrict__ xn, const float* __restrict__ cn, int* __restrict__ labels,
     float* __restrict__ mind, long long n, int d, int k, int n_tiles, double eps, int Q,
-    RngKey key, RngKey tie_key, long long row_offset) {
+    RngKey key, RngKey tie_key, long long row_offset, int prune) {
   extern __shared__ __attribute__((aligned(16))) float As[];   // [D4][64] A fragments
   __shared__ float mb[4][16];
   __shared__ uint32_t mk[4][16];
   __shared__ int mj[4][16];
+  __shared__ float hip_[4][16];
+  __shared__ float hv[16];
+  __shared__ int hj[16];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
   const long long row0 = (long long)blockIdx.x * 16;
+  const float INF = __builtin_inff();
   // A fragments (16x16x4 f32) of the workgroup's 16 rows, shared by the 4
   // waves: As[s][l] = x[row0 + (l & 15)][4 s + (l >> 4)]; rows past n clamped
   for (int e = threadIdx.x; e < D4 * 64; e += 256) {
@@ -273,16 +459,84 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   __syncthreads();
   // register i of this lane = pair (row row0 + 4 q4 + i, centroid 16 t + c16)
   f32x4 nx2, best;
-  uint32_t bkey[4];
   int bj[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const long long r = row0 + 4 * q4 + i;
     nx2[i] = xn[r < n ? r : n - 1];
-    best[i] = __builtin_inff();
-    bkey[i] = 0xFFFFFFFFu;
-    bj[i] = 0;
+    best[i] = INF;
+    bj[i] = -1;
   }
+  const int h = (Q + 1) / 2;
+  float cqh = 1.0f;   // C(Q, h)
+  for (int i = 0; i < h; ++i) cqh = cqh * (float)(Q - i) / (float)(i + 1);
+  int hint[4] = {-1, -1, -1, -1};
+  if (prune) {
+    // ---- pass 1: exact fp32 distance argmin (hint), with its inner product
+    f32x4 bd = {INF, INF, INF, INF}, bip = {0.f, 0.f, 0.f, 0.f};
+    int bjj[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+    for (int t = wave; t < n_tiles; t += 4) {
+      const float* bf = Cf + (size_t)t * D4 * 64 + lane;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 16
+      for (int s = 0; s < D4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
+      const int j = t * 16 + c16;
+      if (j < k) {
+        const float ny2 = cn[j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float D = nx2[i] + ny2 - 2.0f * acc[i];
+          if (D < bd[i]) { bd[i] = D; bjj[i] = j; bip[i] = acc[i]; }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float b = bd[i], p = bip[i];
+      int jj = bjj[i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ob = __shfl_xor(b, o, 64), op = __shfl_xor(p, o, 64);
+        const int oj = __shfl_xor(jj, o, 64);
+        if (ob < b || (ob == b && oj < jj)) { b = ob; p = op; jj = oj; }
+      }
+      if (c16 == 0) {
+        mb[wave][4 * q4 + i] = b;
+        mj[wave][4 * q4 + i] = jj;
+        hip_[wave][4 * q4 + i] = p;
+      }
+    }
+    __syncthreads();
+    // the 16 hint pairs, sampled in full: wave w, lanes 0..3 -> row 4 w + lane
+    if (lane < 4) {
+      const int rr = 4 * wave + lane;
+      float b = mb[0][rr], p = hip_[0][rr];
+      int jj = mj[0][rr];
+      for (int w = 1; w < 4; ++w)
+        if (mb[w][rr] < b || (mb[w][rr] == b && mj[w][rr] < jj)) {
+          b = mb[w][rr]; p = hip_[w][rr]; jj = mj[w][rr];
+        }
+      const long long r = row0 + rr;
+      float v = INF;
+      if (r < n && jj < k) {
+        const long long g = row_offset + r;
+        v = ipe_distance(p, (double)xn[r], (double)cn[jj], eps, Q, key,
+                         (unsigned long long)g * (unsigned long long)k + (unsigned long long)jj);
+      } else {
+        jj = -1;
+      }
+      hv[rr] = v;
+      hj[rr] = jj;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hint[i] = hj[4 * q4 + i];
+      if (hint[i] >= 0) { best[i] = hv[4 * q4 + i]; bj[i] = hint[i]; }
+    }
+  }
+  // ---- pass 2 (the only pass without pruning): every pair but the hint
   for (int t = wave; t < n_tiles; t += 4) {   // the waves split the centroid tiles
     const float* bf = Cf + (size_t)t * D4 * 64 + lane;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -291,49 +545,52 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
     const int j = t * 16 + c16;
     if (j < k) {   // padded centroid columns do nothing (no MFMA / sync below)
-      const double ny2 = (double)cn[j];
+      const float ny2 = cn[j];
       // one inlined copy of the sampler: the 4 pairs rotate through slot 0
 #pragma nounroll
       for (int i = 0; i < 4; ++i) {
         const long long r = row0 + 4 * q4 + i;
-        if (r < n) {
+        if (r < n && j != hint[0]) {
           const long long g = row_offset + r;
-          const float dt = ipe_distance(acc[0], (double)nx2[0], ny2, eps, Q, key,
-                                        (unsigned long long)g * (unsigned long long)k +
-                                            (unsigned long long)j);
-          const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
-          if (dt < best[0] || (dt == best[0] && (tk < bkey[0] || (tk == bkey[0] && j < bj[0])))) {
+          const unsigned long long sid = (unsigned long long)g * (unsigned long long)k + (unsigned long long)j;
+          const float dt = prune ? ipe_distance_thr(acc[0], nx2[0], ny2, eps, Q, key, sid, best[0], h, cqh)
+                                 : ipe_distance(acc[0], (double)nx2[0], (double)ny2, eps, Q, key, sid);
+          bool take = dt < best[0];
+          if (!take && dt == best[0] && dt < INF) {   // tie: the random keys decide (rare)
+            const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
+            const uint32_t bk = band_key(tie_key, g, (uint32_t)bj[0]);
+            take = tk < bk || (tk == bk && j < bj[0]);
+          }
+          if (take) {
             best[0] = dt;
-            bkey[0] = tk;
             bj[0] = j;
           }
         }
         acc = acc.yzwx;
         nx2 = nx2.yzwx;
         best = best.yzwx;
-        const uint32_t k0 = bkey[0];
-        bkey[0] = bkey[1]; bkey[1] = bkey[2]; bkey[2] = bkey[3]; bkey[3] = k0;
         const int j0 = bj[0];
         bj[0] = bj[1]; bj[1] = bj[2]; bj[2] = bj[3]; bj[3] = j0;
+        const int h0 = hint[0];
+        hint[0] = hint[1]; hint[1] = hint[2]; hint[2] = hint[3]; hint[3] = h0;
       }
     }
   }
   // merge the 16 lanes (centroid classes) holding each row, then the 4 waves
   // (the order (D~, tie key, j) is total: any merge order gives the same pick)
-  auto better = [](float ob, uint32_t ok, int oj, float b, uint32_t kk, int jj) {
-    return ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)));
-  };
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float b = best[i];
-    uint32_t kk = bkey[i];
     int jj = bj[i];
+    const long long g = row_offset + row0 + 4 * q4 + i;
+    uint32_t kk = jj >= 0 ? band_key(tie_key, g, (uint32_t)jj) : 0xFFFFFFFFu;
+    if (jj < 0) jj = 0x7fffffff;
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) {
       const float ob = __shfl_xor(b, o, 64);
       const uint32_t ok = (uint32_t)__shfl_xor((int)kk, o, 64);
       const int oj = __shfl_xor(jj, o, 64);
-      if (better(ob, ok, oj, b, kk, jj)) {
+      if (ipe_better(ob, ok, oj, b, kk, jj)) {
         b = ob;
         kk = ok;
         jj = oj;
@@ -352,14 +609,14 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     uint32_t kk = mk[0][rr];
     int jj = mj[0][rr];
     for (int w = 1; w < 4; ++w)
-      if (better(mb[w][rr], mk[w][rr], mj[w][rr], b, kk, jj)) {
+      if (ipe_better(mb[w][rr], mk[w][rr], mj[w][rr], b, kk, jj)) {
         b = mb[w][rr];
         kk = mk[w][rr];
         jj = mj[w][rr];
       }
     const long long r = row0 + rr;
     if (r < n) {
-      labels[r] = jj;
+      labels[r] = jj < k ? jj : 0;
       mind[r] = b;
     }
   }
@@ -373,7 +630,7 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
                             const void* cn, void* labels, void* mind, long long n, int d, int d_pad,
                             int k, int k_pad, double eps, int Q, unsigned k0, unsigned k1,
                             unsigned s0, unsigned s1, unsigned t0, unsigned t1, unsigned ts0,
-                            unsigned ts1, long long row_offset, void* stream) {
+                            unsigned ts1, long long row_offset, int prune, void* stream) {
   if (n <= 0) return 0;
   if (Q < 1 || Q > kIpeMaxQ || k < 1 || k_pad % 16 != 0 || k_pad < k || d < 1 || d > d_pad ||
       ldx < d)
@@ -387,7 +644,8 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
     hipLaunchKernelGGL(ipe_fused_kernel<DP / 4>, dim3((unsigned)blocks), dim3(256),            \
                        (size_t)DP * 64, (hipStream_t)stream, (const float*)X, ldx,            \
                        (const float*)Cf, (const float*)xn, (const float*)cn, (int*)labels,    \
-                       (float*)mind, n, d, k, nt, eps, Q, key, tie, row_offset);              \
+                       (float*)mind, n, d, k, nt, eps, Q, key, tie, row_offset,  \
+                       prune && (Q & 1));              \
     break;
   switch (d_pad) {
     CASE(32)

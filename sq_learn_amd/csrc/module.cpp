@@ -39,7 +39,7 @@ __attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, lo
 __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, const void*, const void*,
                                        void*, void*, long long, int, int, int, int, double, int,
                                        unsigned, unsigned, unsigned, unsigned, unsigned, unsigned,
-                                       unsigned, unsigned, long long, void*);
+                                       unsigned, unsigned, long long, int, void*);
 __attribute__((weak)) int sq_centroid_delta(const void*, const void*, const void*, void*, void*,
                                             void*, long long, int, int, int, int, void*, void*,
                                             void*, void*);
@@ -268,14 +268,14 @@ static PyObject* py_gram64(PyObject*, PyObject* a) {
 
 static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
   unsigned long long X, Cf, xn, cn, lab, mind, st; long long ldx, n, roff; int d, dp, k, kp, Q;
-  double eps; unsigned k0, k1, s0, s1, t0, t1, ts0, ts1;
-  if (!PyArg_ParseTuple(a, "KLKKKKKLiiiidiIIIIIIIILK", &X, &ldx, &Cf, &xn, &cn, &lab, &mind, &n,
+  double eps; unsigned k0, k1, s0, s1, t0, t1, ts0, ts1; int prune;
+  if (!PyArg_ParseTuple(a, "KLKKKKKLiiiidiIIIIIIIILiK", &X, &ldx, &Cf, &xn, &cn, &lab, &mind, &n,
                         &d, &dp, &k, &kp, &eps, &Q, &k0, &k1, &s0, &s1, &t0, &t1, &ts0, &ts1,
-                        &roff, &st))
+                        &roff, &prune, &st))
     return nullptr;
   CHECK(sq_ipe_fused)
   return ret(sq_ipe_fused(P(X), ldx, P(Cf), P(xn), P(cn), P(lab), P(mind), n, d, dp, k, kp, eps, Q,
-                          k0, k1, s0, s1, t0, t1, ts0, ts1, roff, P(st)));
+                          k0, k1, s0, s1, t0, t1, ts0, ts1, roff, prune, P(st)));
 }
 
 static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {

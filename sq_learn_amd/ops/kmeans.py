@@ -257,10 +257,14 @@ def ipe_center_fragments(C, k_pad, d_pad):
 
 
 def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie_key: RngKey,
-                     row_offset, labels, mind):
+                     row_offset, labels, mind, prune=True):
     """Fused IPE E-step (csrc/ipe.hip): exact fp32 MFMA inner products, the
     median-of-Q amplitude-estimation distance per pair in the epilogue,
-    per-row argmin with random ties; G is never materialised."""
+    per-row argmin with random ties; G is never materialised.  ``prune``
+    (odd Q): a first sweep finds each row's exact-distance argmin, whose
+    pair is sampled first; every other pair is then sampled with the exact
+    threshold sampler (a pair whose estimate cannot reach the row's best
+    costs one fp32 bound and one Philox block) - same law as prune=False."""
     n, d = X.shape
     assert X.dtype == torch.float32 and X.stride(1) == 1
     assert xn.dtype == torch.float32 and cn.dtype == torch.float32 and xn.numel() >= n
@@ -269,7 +273,7 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
                                 cn.data_ptr(), labels.data_ptr(), mind.data_ptr(), n, d, d_pad, k,
                                 k_pad, float(eps), int(Q), key.k0, key.k1, key.s0, key.s1,
                                 tie_key.k0, tie_key.k1, tie_key.s0, tie_key.s1, int(row_offset),
-                                nat.stream_handle(X.device))
+                                int(bool(prune)), nat.stream_handle(X.device))
     if rc:
         raise RuntimeError(f"ipe_fused failed (hip error {rc})")
 

@@ -190,3 +190,93 @@ def test_ipe_fused_argmin_wide(cuda):
                        RngKey(7, "ipe", 0), RngKey(7, "band_select", 0), 0, lab, mind)
     D = ((X[:, None, :] - centers[None]) ** 2).sum(-1)
     assert np.mean(lab.cpu().numpy() == D.argmin(1)) > 0.99
+
+
+# ------------------------------------------------------------------ pruning
+def _run_rows(x, C, n, eps, Q, cuda, seed, prune):
+    d = x.size
+    dp = 32
+    while dp < d:
+        dp *= 2
+    k = C.shape[0]
+    kp = -(-k // 16) * 16
+    X = torch.tensor(np.tile(x, (n, 1)), dtype=torch.float32, device=cuda)
+    Ct = torch.tensor(C, dtype=torch.float32, device=cuda)
+    xn = (X.double() ** 2).sum(1).float()
+    cn = (Ct.double() ** 2).sum(1).float()
+    lab = torch.empty(n, dtype=torch.int32, device=cuda)
+    mind = torch.empty(n, dtype=torch.float32, device=cuda)
+    K.ipe_fused_native(X, K.ipe_center_fragments(Ct, kp, dp), xn, cn, k, kp, dp, eps, Q,
+                       RngKey(seed, "ipe", 0), RngKey(seed, "band_select", 0), 0, lab, mind,
+                       prune=prune)
+    torch.cuda.synchronize()
+    ip = (Ct.double() @ X[0].double()).cpu().numpy()
+    return lab.cpu().numpy(), mind.double().cpu().numpy(), float(xn[0]), cn.double().cpu().numpy(), ip
+
+
+@pytest.mark.parametrize("Q,s1", [(3, 1.6), (1, 2.0)])
+def test_ipe_pruned_two_centroid_exact_law(cuda, Q, s1):
+    """Pair 0 is the exact-distance argmin (the hint, sampled in full); pair 1
+    sits a few bins above it, so the pruned sampler's bound rejects most of
+    its draws and its rare exact branch decides the rest.  The joint law of
+    (label, min D~) is the exact law of min(V0, V1) of two independent
+    median-of-Q AE estimates."""
+    rng = np.random.default_rng(11)
+    d, eps = 48, 0.02
+    x = rng.standard_normal(d).astype(np.float32)
+    u = rng.standard_normal(d)
+    u -= (u @ x) / (x @ x) * x
+    u /= np.linalg.norm(u)
+    c0 = (x + 0.9 * u).astype(np.float32)
+    c1 = (x - s1 * u).astype(np.float32)      # pair 1 ~ 5-9 bins above pair 0
+    n = 1_000_000
+    lab, mind, nx2, cn, ip = _run_rows(x, np.stack([c0, c1]), n, eps, Q, cuda, 0, True)
+    M0, v0, p0 = _exact_law(ip[0], nx2, cn[0], eps, Q)
+    M1, v1, p1 = _exact_law(ip[1], nx2, cn[1], eps, Q)
+    # P(V1 < V0) and the joint cells (label, value)
+    F1 = np.array([p1[v1 < v].sum() for v in v0])          # P(V1 < v)
+    G0 = np.array([p0[v0 > v].sum() for v in v1])          # P(V0 > v)
+    cells_e = np.concatenate([p0 * (1 - F1), p1 * G0])
+    vals = np.concatenate([v0, v1])
+    labs = np.concatenate([np.zeros_like(v0), np.ones_like(v1)])
+    P1 = (p1 * G0).sum()
+    assert 1e-4 < P1 < 0.2, P1        # the pruned pair does win sometimes
+    obs = np.zeros(len(vals))
+    for L in (0, 1):
+        sel = lab == L
+        cand = np.where(labs == L)[0]
+        idx = cand[np.argmin(np.abs(mind[sel][:, None] - vals[cand][None, :]), axis=1)]
+        assert np.allclose(mind[sel], vals[idx], rtol=2e-6, atol=1e-5)
+        obs += np.bincount(idx, minlength=len(vals))
+    n1 = int((lab == 1).sum())
+    assert abs(n1 - n * P1) <= 5 * math.sqrt(n * P1 * (1 - P1)) + 1, (n1, n * P1)
+    exp = cells_e * n
+    big = exp >= 5
+    o = np.append(obs[big], obs[~big].sum())
+    e = np.append(exp[big], exp[~big].sum())
+    chi2 = ((o - e) ** 2 / e).sum()
+    assert stats.chi2.sf(chi2, len(e) - 1) > 1e-4
+
+
+def test_ipe_pruned_matches_unpruned_law_many_centroids(cuda):
+    """k = 40 centroids over 3 tiles (waves split them, the hint merge runs
+    across lanes and waves): the (label, D~) law with pruning equals the
+    full sampler's (two-sample chi^2, independent seeds)."""
+    rng = np.random.default_rng(12)
+    d, k, eps, Q = 40, 40, 0.1, 13
+    x = rng.standard_normal(d).astype(np.float32)
+    C = (x[None] + rng.uniform(0.7, 1.3, (k, 1)) * rng.standard_normal((k, d)) / math.sqrt(d) * 1.5)
+    C = C.astype(np.float32)
+    n = 400_000
+    la, ma, *_ = _run_rows(x, C, n, eps, Q, cuda, 1, True)
+    lb, mb, *_ = _run_rows(x, C, n, eps, Q, cuda, 2, False)
+    ka = la.astype(np.int64) * 10**9 + np.round(ma * 1e3).astype(np.int64)
+    kb = lb.astype(np.int64) * 10**9 + np.round(mb * 1e3).astype(np.int64)
+    keys, inv = np.unique(np.concatenate([ka, kb]), return_inverse=True)
+    ca = np.bincount(inv[:n], minlength=len(keys))
+    cb = np.bincount(inv[n:], minlength=len(keys))
+    keep = (ca + cb) >= 20
+    table = np.stack([np.append(ca[keep], ca[~keep].sum()), np.append(cb[keep], cb[~keep].sum())])
+    table = table[:, table.sum(0) > 0]
+    assert table.shape[1] >= 3
+    assert stats.chi2_contingency(table)[1] > 1e-4
