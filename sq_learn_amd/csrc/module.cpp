@@ -32,9 +32,13 @@ __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void
                                            void*, const void*, const void*, int, int, void*);
 __attribute__((weak)) int sq_fast_centroids(void*, const void*, const void*, int, int, int, void*,
                                             void*, void*, void*);
-// gram64.hip
-__attribute__((weak)) int sq_gram64(const void*, int, long long, const void*, long long, int, void*,
-                                    int, void*);
+// tsgemm64.hip
+__attribute__((weak)) int sq_xtx(const void*, int, long long, const void*, int, const void*, int,
+                                 long long, const void*, int, long long, int, int, void*, void*,
+                                 int, void*);
+__attribute__((weak)) int sq_xtx_geometry(int, int, int, int*, int*, int*);
+__attribute__((weak)) int sq_xw(const void*, int, long long, const void*, long long, int,
+                                const void*, long long, int, int, void*, int, long long, void*);
 // ipe.hip
 __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, const void*, const void*,
                                        void*, void*, long long, int, int, int, int, double, int,
@@ -116,12 +120,8 @@ __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void
                  long long m, int k, long long ldG, double eps, int Q, unsigned k0, unsigned k1,
                  unsigned s0, unsigned s1, long long row_offset, void* stream);
 // linalg.hip
-__attribute__((weak)) int sq_gram_bf16(const void*, int, void*, const void*, long long, int, void*,
-                                       long long, void*);
-__attribute__((weak)) int sq_power_iter(const void*, int, const void*, void*, const void*, long long,
-                                        int, int, void*, int, void*);
-__attribute__((weak)) int sq_mu_sums(const void*, int, const void*, int, void*, void*, void*, int,
-                                     long long, int, void*);
+__attribute__((weak)) int sq_mu_sums(const void*, int, long long, const void*, int, void*, void*,
+                                     void*, int, void*, long long, int, void*);
 __attribute__((weak)) int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream);
 // knn.hip
 __attribute__((weak)) int sq_knn_topk(const void* D, void* outd, void* outi, long long m, int nref, long long ldD, int kk,
@@ -258,12 +258,32 @@ static PyObject* py_cluster_inertia(PyObject*, PyObject* a) {
   return ret(sq_cluster_inertia(P(sums), P(cnts), P(q), P(C), k, d, xe, qe, P(part), P(st)));
 }
 
-static PyObject* py_gram64(PyObject*, PyObject* a) {
-  unsigned long long X, mu, part, st; int f64, d, grid; long long ldx, n;
-  if (!PyArg_ParseTuple(a, "KiLKLiKiK", &X, &f64, &ldx, &mu, &n, &d, &part, &grid, &st))
+static PyObject* py_xtx(PyObject*, PyObject* a) {
+  unsigned long long A, mua, B, mub, part, C, st; int ta, da, tb, db, sym, ns, acc;
+  long long lda, ldb, n;
+  if (!PyArg_ParseTuple(a, "KiLKiKiLKiLiiKKiK", &A, &ta, &lda, &mua, &da, &B, &tb, &ldb, &mub,
+                        &db, &n, &sym, &ns, &part, &C, &acc, &st))
     return nullptr;
-  CHECK(sq_gram64)
-  return ret(sq_gram64(P(X), f64, ldx, P(mu), n, d, P(part), grid, P(st)));
+  CHECK(sq_xtx)
+  return ret(sq_xtx(P(A), ta, lda, P(mua), da, P(B), tb, ldb, P(mub), db, n, sym, ns, P(part),
+                    P(C), acc, P(st)));
+}
+
+static PyObject* py_xtx_geometry(PyObject*, PyObject* a) {
+  int da, db, sym, TM, TN, np;
+  if (!PyArg_ParseTuple(a, "iii", &da, &db, &sym)) return nullptr;
+  CHECK(sq_xtx_geometry)
+  sq_xtx_geometry(da, db, sym, &TM, &TN, &np);
+  return Py_BuildValue("(iii)", TM, TN, np);
+}
+
+static PyObject* py_xw(PyObject*, PyObject* a) {
+  unsigned long long A, mu, W, Y, st; int ta, d, l, upper, to; long long lda, n, ldw, ldy;
+  if (!PyArg_ParseTuple(a, "KiLKLiKLiiKiLK", &A, &ta, &lda, &mu, &n, &d, &W, &ldw, &l, &upper,
+                        &Y, &to, &ldy, &st))
+    return nullptr;
+  CHECK(sq_xw)
+  return ret(sq_xw(P(A), ta, lda, P(mu), n, d, P(W), ldw, l, upper, P(Y), to, ldy, P(st)));
 }
 
 static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
@@ -461,28 +481,14 @@ static PyObject* py_ipe_estep(PyObject*, PyObject* a) {
                           roff, P(st)));
 }
 
-static PyObject* py_gram(PyObject*, PyObject* a) {
-  unsigned long long X, G, mean, part, st; int xdt, d; long long n, cap;
-  if (!PyArg_ParseTuple(a, "KiKKLiKLK", &X, &xdt, &G, &mean, &n, &d, &part, &cap, &st))
-    return nullptr;
-  CHECK(sq_gram_bf16)
-  return ret(sq_gram_bf16(P(X), xdt, P(G), P(mean), n, d, P(part), cap, P(st)));
-}
-
-static PyObject* py_power_iter(PyObject*, PyObject* a) {
-  unsigned long long X, Q, Z, mean, part, st; int xdt, d, l, pw; long long n;
-  if (!PyArg_ParseTuple(a, "KiKKKLiiKiK", &X, &xdt, &Q, &Z, &mean, &n, &d, &l, &part, &pw, &st))
-    return nullptr;
-  CHECK(sq_power_iter)
-  return ret(sq_power_iter(P(X), xdt, P(Q), P(Z), P(mean), n, d, l, P(part), pw, P(st)));
-}
-
 static PyObject* py_mu_sums(PyObject*, PyObject* a) {
-  unsigned long long X, qs, rm, cs, part, st; int xdt, nq, pw, d; long long n;
-  if (!PyArg_ParseTuple(a, "KiKiKKKiLiK", &X, &xdt, &qs, &nq, &rm, &cs, &part, &pw, &n, &d, &st))
+  unsigned long long X, qs, rm, cs, part, racc, st; int xdt, nq, pw, d; long long n, ldx;
+  if (!PyArg_ParseTuple(a, "KiLKiKKKiKLiK", &X, &xdt, &ldx, &qs, &nq, &rm, &cs, &part, &pw, &racc,
+                        &n, &d, &st))
     return nullptr;
   CHECK(sq_mu_sums)
-  return ret(sq_mu_sums(P(X), xdt, P(qs), nq, P(rm), P(cs), P(part), pw, n, d, P(st)));
+  return ret(sq_mu_sums(P(X), xdt, ldx, P(qs), nq, P(rm), P(cs), P(part), pw, P(racc), n, d,
+                        P(st)));
 }
 
 static PyObject* py_row_norms(PyObject*, PyObject* a) {
@@ -524,7 +530,9 @@ static PyMethodDef methods[] = {
     {"failure_inject", py_failure_inject, METH_VARARGS, "Bernoulli estimation failure + resampling"},
     {"tomography", py_tomography, METH_VARARGS, "batched shot-based vector tomography"},
     {"mnom_segments", py_mnom_segments, METH_VARARGS, "segmented multinomial (long vectors)"},
-    {"gram64", py_gram64, METH_VARARGS, "fp64 MFMA Gram partials"},
+    {"xtx", py_xtx, METH_VARARGS, "fp64 MFMA (A-mu_a)^T (B-mu_b), split-K + fixed-order finalize"},
+    {"xtx_geometry", py_xtx_geometry, METH_VARARGS, "xtx tile sizes and pair count"},
+    {"xw", py_xw, METH_VARARGS, "fp64 MFMA (A-mu) W"},
     {"bounds_filter", py_bounds_filter, METH_VARARGS, "Hamerly pruning -> active row list"},
     {"fast_centroids", py_fast_centroids, METH_VARARGS, "fastest centroids + Elkan distances"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
@@ -543,8 +551,6 @@ static PyMethodDef methods[] = {
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},
     {"ipe_estep", py_ipe_estep, METH_VARARGS, "IPE-noised distance argmin"},
-    {"gram", py_gram, METH_VARARGS, "G += (X-mean)^T (X-mean)"},
-    {"power_iter", py_power_iter, METH_VARARGS, "Z += (X-m)^T ((X-m) Q) fused"},
     {"mu_sums", py_mu_sums, METH_VARARGS, "mu(A) power sums for a p-grid"},
     {"row_norms", py_row_norms, METH_VARARGS, "squared row norms"},
     {"knn_topk", py_knn_topk, METH_VARARGS, "per-row k smallest"},

@@ -4,8 +4,8 @@
   centred matrix in fp64 - bit-for-bit the reference's ``scipy.linalg.svd``
   semantics (``_qPCA.py:581``, ``_pca.py:437-502``).
 * ``gram``: the MI355X path for tall matrices (n >> d): the d x d Gram
-  (X-mu)^T (X-mu) by the fused fp32-MFMA kernel (one pass over X), one
-  all-reduce, ``eigh`` in fp64 -> S, V; left singular vectors
+  (X-mu)^T (X-mu) by the fp64-MFMA kernel (one pass over X), one
+  all-reduce, host ``eigh`` in fp64 -> S, V; left singular vectors
   U = (X-mu) V S^-1 are materialised only for the retained columns, on the
   shard that owns the rows.
 * ``cholqr2`` (default for tall matrices): sharded CholeskyQR2 in fp64
@@ -13,8 +13,8 @@
   singular values and right vectors to ~eps64 * cond relative, like the
   reference's fp64 LAPACK (the ``gram`` eigenvalues lose eps * cond^2);
   falls back to ``gram`` when cond(X) >~ 1e8 or X is rank deficient.
-* ``randomized``: :func:`utils.extmath.randomized_svd_distributed` (fused
-  power-iteration kernel, CholeskyQR2, K14, C6/C7).
+* ``randomized``: :func:`utils.extmath.randomized_svd_distributed`
+  (fp64-MFMA power iterations and CholeskyQR2, K14, C6/C7).
 """
 
 import numpy as np
@@ -47,7 +47,7 @@ def full_svd(data, mean, k_left, method="auto"):
         if R is None:
             method = "gram"
         else:
-            _, S, Vt = torch.linalg.svd(R)
+            _, S, Vt = torch.linalg.svd(R.cpu())       # d x d, host LAPACK fp64
             return _finish(data, mean, S, Vt, k_left, "cholqr2")
     if method == "exact":
         full = X if data.comm.world_size == 1 else torch.cat(data.comm.all_gather_varlen(X), 0)
@@ -58,11 +58,11 @@ def full_svd(data, mean, k_left, method="auto"):
             U = U[data.row_offset:data.row_offset + data.n_local]
         return SVDResult(S.cpu().numpy(), Vt.cpu().numpy(), U[:, :k_left], "exact")
     # Gram path
-    G = L.gram_local(X, mean.to(torch.float32 if X.device.type == "cuda" else torch.float64))
-    G = G.to(torch.float64)
+    G = L.gram_local(X, mean)                      # fp64 (fp64-MFMA kernel on the GPU)
     data.comm.all_reduce_(G)
+    G = G.cpu()
     G = 0.5 * (G + G.T)
-    ev, V = torch.linalg.eigh(G)
+    ev, V = torch.linalg.eigh(G)                   # d x d, host LAPACK fp64
     ev = ev.flip(0).clamp(min=0.0)
     V = V.flip(1)
     S = torch.sqrt(ev)
@@ -78,12 +78,11 @@ def _finish(data, mean, S, Vt, k_left, method):
     S, Vt = S[:r], Vt[:r]
     k = min(k_left, int((S > S[0] * 1e-12).sum()) if S.numel() else 0) if r else 0
     dt = torch.float64 if X.device.type == "cpu" else torch.float32
-    Vk = Vt[:k].T.to(dt).to(X.device)
+    Vk = Vt[:k].T.to(torch.float64).contiguous()
     Uk = torch.empty((data.n_local, k), dtype=dt, device=X.device)
-    m = mean.to(dt).to(X.device)
-    step = 1 << 20
-    for s in range(0, data.n_local, step):
-        Uk[s:s + step] = (X[s:s + step].to(dt) - m) @ Vk
+    if k and data.n_local:
+        # U = (X - mean) V_k in one fp64-accumulated pass (csrc/tsgemm64.hip xw)
+        L.xw(X if X.stride(1) == 1 else X.contiguous(), Vk.to(X.device), mean=mean, out=Uk)
     if k:
         Uk /= S[:k].to(dt).to(X.device)
     # u-based signs for the retained columns, v-based for the rest

@@ -1,9 +1,11 @@
-"""Row-sharded linear algebra ops: row norms, Gram (X-mu)^T(X-mu), fused
-power iteration (X-mu)^T((X-mu) Q) and the mu(A) power sums.
+"""Row-sharded linear algebra ops: row norms, the fp64 tall-skinny GEMMs
+(A - mu_a)^T (B - mu_b) and (A - mu) W (Gram, CholeskyQR2, power iteration,
+randomized range finder) and the mu(A) power sums.
 
-GPU tensors use the MFMA kernels of ``csrc/linalg.hip``; CPU tensors use
-torch.  All functions return *local* (per-shard) partial results; callers
-reduce them across ranks with one collective.
+GPU tensors use the MFMA kernels of ``csrc/tsgemm64.hip`` (fp64) and
+``csrc/linalg.hip`` (row norms, mu sums); CPU tensors use torch.  All
+functions return *local* (per-shard) partial results; callers reduce them
+across ranks with one collective.
 """
 
 import torch
@@ -31,82 +33,135 @@ def row_norms_sq(X, out=None):
     return r
 
 
+# ------------------------------------------------ fp64-MFMA tall-skinny GEMMs
+_XTX_TARGET_WGS = 1024        # 2-3 resident workgroups per CU (LDS-bound), 256 CUs
+_XTX_MAX_SPLITS = 512
+_CHUNK_BYTES = 4 << 30        # fp64 row-chunk buffers of the two-kernel passes
+_part_cache = {}
+
+
+def _part(device, numel):
+    """Reusable fp64 workspace for the xtx split partials (one per device)."""
+    buf = _part_cache.get(device)
+    if buf is None or buf.numel() < numel:
+        buf = torch.empty(max(numel, 1), dtype=torch.float64, device=device)
+        _part_cache[device] = buf
+    return buf
+
+
+def _mean64(m, device):
+    return None if m is None else m.to(device=device, dtype=torch.float64).contiguous()
+
+
+def xtx(A, B=None, mean_a=None, mean_b=None, out=None, accumulate=False):
+    """C = (A - mean_a)^T (B - mean_b) in fp64 (``B=None``: the symmetric Gram
+    of A).  GPU: csrc/tsgemm64.hip (fp64 MFMA, split-K over row ranges,
+    fixed-order partial sums: deterministic; any feature count, fp32 / bf16 /
+    fp64 inputs with row stride).  ``out`` (+= when ``accumulate``) lets
+    chunked callers sum several row blocks.  Returns the LOCAL partial."""
+    sym = B is None
+    n, da = A.shape
+    db = da if sym else B.shape[1]
+    if not sym:
+        assert B.shape[0] == n
+    dev = A.device
+    if out is None:
+        out = torch.zeros((da, db), dtype=torch.float64, device=dev)
+        accumulate = False
+    if not nat.use_native(A):
+        Ac = A.to(torch.float64)
+        if mean_a is not None:
+            Ac = Ac - mean_a.to(torch.float64)
+        if sym:
+            Bc = Ac
+        else:
+            Bc = B.to(torch.float64)
+            if mean_b is not None:
+                Bc = Bc - mean_b.to(torch.float64)
+        r = Ac.T @ Bc
+        if accumulate:
+            out += r
+        else:
+            out.copy_(r)
+        return out
+    assert A.stride(1) == 1 and (sym or B.stride(1) == 1)
+    TM, TN, npairs = nat.native().xtx_geometry(da, db, int(sym))
+    splits = max(8, min(-(-_XTX_TARGET_WGS // npairs), -(-max(n, 1) // 256), _XTX_MAX_SPLITS))
+    splits = -(-splits // 8) * 8
+    part = _part(dev, splits * npairs * TM * TN)
+    ma, mb = _mean64(mean_a, dev), (None if sym else _mean64(mean_b, dev))
+    Bt = A if sym else B
+    rc = nat.native().xtx(A.data_ptr(), nat.dtype_code(A), A.stride(0), nat.ptr(ma), da,
+                          Bt.data_ptr(), nat.dtype_code(Bt), Bt.stride(0), nat.ptr(mb), db, n,
+                          int(sym), splits, part.data_ptr(), out.data_ptr(), int(accumulate),
+                          nat.stream_handle(dev))
+    if rc:
+        raise RuntimeError(f"xtx failed (hip error {rc})")
+    return out
+
+
+def xw(A, W, mean=None, upper=False, out_dtype=torch.float64, out=None):
+    """Y = (A - mean) W, W (d x l) applied in fp64 (csrc/tsgemm64.hip on the
+    GPU; ``upper``: W is upper triangular and its zero block is skipped)."""
+    n, d = A.shape
+    l = W.shape[1]
+    dev = A.device
+    if out is None:
+        out = torch.empty((n, l), dtype=out_dtype, device=dev)
+    if not nat.use_native(A):
+        Ac = A.to(torch.float64)
+        if mean is not None:
+            Ac = Ac - mean.to(torch.float64)
+        out.copy_(Ac @ W.to(torch.float64))
+        return out
+    assert A.stride(1) == 1 and out.stride(1) == 1 and out.dtype in (torch.float32, torch.float64)
+    Wd = W.to(device=dev, dtype=torch.float64).contiguous()
+    m = _mean64(mean, dev)
+    rc = nat.native().xw(A.data_ptr(), nat.dtype_code(A), A.stride(0), nat.ptr(m), n, d,
+                         Wd.data_ptr(), Wd.stride(0), l, int(bool(upper)), out.data_ptr(),
+                         1 if out.dtype == torch.float64 else 0, out.stride(0),
+                         nat.stream_handle(dev))
+    if rc:
+        raise RuntimeError(f"xw failed (hip error {rc})")
+    return out
+
+
 def gram_local(X, mean):
-    """Local partial of G = (X - mean)^T (X - mean) (fp32 on GPU, f64 on CPU)."""
+    """Local partial of G = (X - mean)^T (X - mean) in fp64 (:func:`xtx`)."""
+    return xtx(X, mean_a=mean)
+
+
+def _chunk(cols, chunk_rows):
+    return chunk_rows if chunk_rows else max(1 << 16, _CHUNK_BYTES // (8 * max(cols, 1)))
+
+
+def gram64_local(X, mean=None, W=None, chunk_rows=None):
+    """Local partial of G = ((X - mean) W)^T ((X - mean) W) accumulated in
+    fp64: pass 1 of CholeskyQR2 (W = None) is one :func:`xtx` over X; pass 2
+    forms Y = (X - mean) W1 (W1 = R1^-1 upper triangular) chunk by chunk with
+    :func:`xw` into an fp64 buffer and accumulates Y^T Y (no library GEMM, no
+    fp64 copy of X)."""
     n, d = X.shape
-    if nat.use_native(X) and X.dtype in (torch.float32, torch.bfloat16):
-        X = X.contiguous()
-        G = torch.zeros((d, d), dtype=torch.float32, device=X.device)
-        m = mean.to(torch.float32).contiguous()
-        # per-split partial tiles, reduced in a fixed order (deterministic)
-        side = (d + 63) // 64
-        cap = max(1, 2048 // (side * (side + 1) // 2)) * (side * (side + 1) // 2) * 64 * 64
-        part = torch.empty(cap, dtype=torch.float32, device=X.device)
-        nat.native().gram(X.data_ptr(), nat.dtype_code(X), G.data_ptr(), m.data_ptr(), n, d,
-                          part.data_ptr(), cap, nat.stream_handle(X.device))
-        # kernel fills the upper triangle tiles; mirror
-        iu = torch.triu_indices(d, d, 1, device=X.device)
-        G[iu[1], iu[0]] = G[iu[0], iu[1]]
+    if W is None:
+        return xtx(X, mean_a=mean)
+    dw = W.shape[1]
+    chunk_rows = _chunk(dw, chunk_rows)
+    G = torch.zeros((dw, dw), dtype=torch.float64, device=X.device)
+    if n == 0:
         return G
-    Xc = X.to(torch.float64) - mean.to(torch.float64)
-    return Xc.T @ Xc
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    buf = torch.empty((min(n, chunk_rows), dw), dtype=torch.float64, device=X.device)
+    for s in range(0, n, chunk_rows):
+        e = min(n, s + chunk_rows)
+        Y = xw(X[s:e], W, mean=mean, upper=True, out=buf[:e - s])
+        xtx(Y, out=G, accumulate=True)
+    return G
 
 
 def gram64_native(X, mean=None):
-    """G = (X - mean)^T (X - mean) in fp64 on the matrix cores
-    (csrc/gram64.hip, v_mfma_f64_16x16x4_f64): per-workgroup partial upper
-    blocks summed in a fixed order (deterministic); X fp32 or fp64, d <= 256."""
-    n, d = X.shape
-    assert X.dtype in (torch.float32, torch.float64, torch.bfloat16) and X.stride(1) == 1 and d <= 256
-    code = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2}[X.dtype]
-    if n == 0:   # an empty shard contributes an exact zero (the kernel writes nothing)
-        return torch.zeros((d, d), dtype=torch.float64, device=X.device)
-    nb = (d + 15) // 16
-    nblk = nb * (nb + 1) // 2
-    grid = int(max(1, min(256, (n + 255) // 256)))
-    part = torch.empty((grid, nblk, 16, 16), dtype=torch.float64, device=X.device)
-    mu = None if mean is None else mean.to(torch.float64).to(X.device).contiguous()
-    rc = nat.native().gram64(X.data_ptr(), code, X.stride(0),
-                             0 if mu is None else mu.data_ptr(), n, d, part.data_ptr(), grid,
-                             nat.stream_handle(X.device))
-    if rc:
-        raise RuntimeError(f"gram64 failed (hip error {rc})")
-    blocks = part.sum(0)                                   # [nblk, 16, 16], fixed order
-    # scatter the upper blocks and their transposes in two indexed copies
-    # (was one tiny copy per block: ~270 launches per call)
-    iu = torch.triu_indices(nb, nb, device=X.device)
-    G4 = torch.zeros((nb, nb, 16, 16), dtype=torch.float64, device=X.device)
-    G4[iu[1], iu[0]] = blocks.transpose(1, 2)
-    G4[iu[0], iu[1]] = blocks                              # diagonal blocks: the upper copy
-    return G4.permute(0, 2, 1, 3).reshape(nb * 16, nb * 16)[:d, :d].contiguous()
-
-
-def gram64_local(X, mean=None, W=None, chunk_rows=1 << 19):
-    """Local partial of G = ((X - mean) W)^T ((X - mean) W) accumulated in
-    fp64.  GPU: the fp64-MFMA kernel (:func:`gram64_native`) on X (pass 1)
-    or on row chunks of (X - mean) W formed by library DGEMM (pass 2); CPU:
-    torch fp64.  The building block of the fp64-faithful sharded
-    CholeskyQR2 (:func:`cholqr2_r`)."""
-    n, d = X.shape
-    dw = d if W is None else W.shape[1]
-    native = (nat.use_native(X) and X.dtype in (torch.float32, torch.float64, torch.bfloat16)
-              and d <= 256 and dw <= 256 and X.stride(1) == 1)
-    if native and W is None:
-        return gram64_native(X, mean)
-    G = torch.zeros((dw, dw), dtype=torch.float64, device=X.device)
-    m = None if mean is None else mean.to(torch.float64).to(X.device)
-    Wd = None if W is None else W.to(torch.float64).to(X.device)
-    for s in range(0, n, chunk_rows):
-        Xc = X[s:s + chunk_rows].to(torch.float64)
-        if m is not None:
-            Xc = Xc - m
-        if Wd is not None:
-            Xc = Xc @ Wd
-        if native:
-            G += gram64_native(Xc.contiguous())
-        else:
-            G.addmm_(Xc.T, Xc)
-    return G
+    """G = (X - mean)^T (X - mean) in fp64 on the matrix cores (any d)."""
+    return xtx(X, mean_a=mean)
 
 
 def cholqr2_r(X, comm, mean=None):
@@ -116,45 +171,47 @@ def cholqr2_r(X, comm, mean=None):
     singular values of R are those of X to ~eps64 * cond(X) relative (the
     Gram eigenvalues alone: eps * cond^2).  Returns None when the first
     Cholesky fails (cond(X) >~ 1e8 or rank deficient): callers fall back to
-    the Gram eigenvalues."""
-    G1 = comm.all_reduce_(gram64_local(X, mean))
+    the Gram eigenvalues.  The d x d factorisations run on the host (LAPACK
+    fp64)."""
+    G1 = comm.all_reduce_(gram64_local(X, mean)).cpu()
     G1 = 0.5 * (G1 + G1.T)
     R1, info = torch.linalg.cholesky_ex(G1, upper=True)
     if int(info) != 0:
         return None
-    eye = torch.eye(G1.shape[0], dtype=torch.float64, device=G1.device)
+    eye = torch.eye(G1.shape[0], dtype=torch.float64)
     W1 = torch.linalg.solve_triangular(R1, eye, upper=True)
-    G2 = comm.all_reduce_(gram64_local(X, mean, W1))
+    G2 = comm.all_reduce_(gram64_local(X, mean, W1.to(X.device))).cpu()
     G2 = 0.5 * (G2 + G2.T)
     R2, info = torch.linalg.cholesky_ex(G2, upper=True)
     if int(info) != 0:
         return None
-    return R2 @ R1
+    return (R2 @ R1).to(X.device)
 
 
-def power_iter_local(X, Q, mean):
-    """Local partial of Z = (X - mean)^T ((X - mean) Q)  (one pass over X)."""
+def power_iter_local(X, Q, mean, chunk_rows=None):
+    """Local partial of Z = (X - mean)^T ((X - mean) Q) in fp64: per row
+    chunk Y = (X - mean) Q by :func:`xw` (fp64, stays in a reused buffer),
+    then Z += (X - mean)^T Y by :func:`xtx`."""
     n, d = X.shape
     l = Q.shape[1]
-    if nat.use_native(X) and X.dtype in (torch.float32, torch.bfloat16) and d <= 256 and l <= 64:
-        X = X.contiguous()
-        Z = torch.zeros((d, l), dtype=torch.float32, device=X.device)
-        Qc = Q.to(torch.float32).contiguous()
-        m = mean.to(torch.float32).contiguous()
-        wgs = 256   # per-WG partials summed in a fixed order (deterministic)
-        part = torch.empty((wgs, d, l), dtype=torch.float32, device=X.device)
-        nat.native().power_iter(X.data_ptr(), nat.dtype_code(X), Qc.data_ptr(), Z.data_ptr(),
-                                m.data_ptr(), n, d, l, part.data_ptr(), wgs,
-                                nat.stream_handle(X.device))
+    chunk_rows = _chunk(l, chunk_rows)
+    Z = torch.zeros((d, l), dtype=torch.float64, device=X.device)
+    if n == 0:
         return Z
-    acc = torch.float64 if X.device.type == "cpu" else torch.float32
-    Z = torch.zeros((d, l), dtype=acc, device=X.device)
-    Qa = Q.to(acc)
-    ma = mean.to(acc)
-    step = 1 << 20
-    for s in range(0, n, step):
-        Xc = X[s:s + step].to(acc) - ma
-        Z += Xc.T @ (Xc @ Qa)
+    if not nat.use_native(X):
+        Qd = Q.to(torch.float64)
+        md = mean.to(torch.float64)
+        for s in range(0, n, chunk_rows):
+            Xc = X[s:s + chunk_rows].to(torch.float64) - md
+            Z += Xc.T @ (Xc @ Qd)
+        return Z
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    buf = torch.empty((min(n, chunk_rows), l), dtype=torch.float64, device=X.device)
+    for s in range(0, n, chunk_rows):
+        e = min(n, s + chunk_rows)
+        Y = xw(X[s:e], Q, mean=mean, out=buf[:e - s])
+        xtx(X[s:e], Y, mean_a=mean, out=Z, accumulate=True)
     return Z
 
 
@@ -167,16 +224,21 @@ def mu_power_sums_local(X, exponents):
     n, d = X.shape
     q = torch.tensor(exponents, dtype=torch.float32)
     nq = len(exponents)
-    if nat.use_native(X) and X.dtype in (torch.float32, torch.bfloat16) and d <= 256 and nq <= 12:
-        X = X.contiguous()
+    if nat.use_native(X) and X.dtype in (torch.float32, torch.bfloat16) and nq <= 12:
+        if X.stride(1) != 1:
+            X = X.contiguous()
         qd = q.to(X.device)
         rowmax = torch.zeros(nq, dtype=torch.float32, device=X.device)
         colsum = torch.zeros((nq, d), dtype=torch.float32, device=X.device)
         wgs = 1024   # per-WG partials, summed in a fixed order (deterministic)
         part = torch.empty((wgs, nq, d), dtype=torch.float32, device=X.device)
-        nat.native().mu_sums(X.data_ptr(), nat.dtype_code(X), qd.data_ptr(), nq, rowmax.data_ptr(),
-                             colsum.data_ptr(), part.data_ptr(), wgs, n, d,
-                             nat.stream_handle(X.device))
+        # d > 512: row power sums carried across the 512-column blocks
+        racc = torch.zeros((nq, n), dtype=torch.float32, device=X.device) if d > 512 else None
+        rc = nat.native().mu_sums(X.data_ptr(), nat.dtype_code(X), X.stride(0), qd.data_ptr(), nq,
+                                  rowmax.data_ptr(), colsum.data_ptr(), part.data_ptr(), wgs,
+                                  nat.ptr(racc), n, d, nat.stream_handle(X.device))
+        if rc:
+            raise RuntimeError(f"mu_sums failed (hip error {rc})")
         return rowmax.double(), colsum.double()
     A = X.abs().to(torch.float64)
     rowmax = torch.zeros(nq, dtype=torch.float64, device=X.device)

@@ -158,9 +158,15 @@ def randomized_svd(M, n_components, *, n_oversamples=10, n_iter="auto",
 # ------------------------------------------------------- distributed path
 def randomized_svd_distributed(X_local, mean, n_components, comm, *, n_oversamples=10,
                                n_iter="auto", seed=0, flip_sign=True, n_rows=None, d=None):
-    """Randomized SVD of the centred row-sharded matrix (X - mean).
+    """Randomized SVD of the centred row-sharded matrix (X - mean)
+    (``utils/extmath.py:161-242`` of the reference, Halko et al.).
 
-    Returns (U_local [n_loc, k], s [k], Vt [k, d]) as tensors."""
+    Every pass over the n rows is an fp64-MFMA tall-skinny kernel
+    (ops/linalg.py xw / xtx -> csrc/tsgemm64.hip on the GPU): power
+    iterations Z <- qr((X-mu)^T ((X-mu) Z)), Y = (X-mu) Z, two CholeskyQR
+    passes Y <- Y R^-1, B^T = (X-mu)^T Y, U = Y Uhat.  The small d x l / l x l
+    factorisations (QR, Cholesky, SVD) run on the host in fp64 LAPACK; one
+    all-reduce per pass.  Returns (U_local [n_loc, k] fp64, s [k], Vt [k, d])."""
     from ..ops import linalg as L
     from ..ops.random import philox_normal
     from ..runtime.rng import RngKey
@@ -172,46 +178,35 @@ def randomized_svd_distributed(X_local, mean, n_components, comm, *, n_oversampl
     if n_iter == "auto":
         n_iter = 7 if k < 0.1 * min(n_glob, d) else 4
     dev = X_local.device
-    wdt = torch.float64 if dev.type == "cpu" else torch.float32
-    Z = philox_normal((d, l), RngKey(seed, "gaussian", 0), dtype=torch.float64, device="cpu").to(dev)
-    Z = Z.to(wdt)
-    m = mean.to(wdt).to(dev)
+    if X_local.stride(1) != 1:
+        X_local = X_local.contiguous()
+    Z = philox_normal((d, l), RngKey(seed, "gaussian", 0), dtype=torch.float64, device="cpu")
     for _ in range(n_iter):
-        Zn = L.power_iter_local(X_local, Z, m).to(torch.float64)
-        comm.all_reduce_(Zn)
+        Zn = comm.all_reduce_(L.power_iter_local(X_local, Z.to(dev), mean)).cpu()
         Z, _ = torch.linalg.qr(Zn)
-        Z = Z.to(wdt)
-    # Y = (X - mu) Z, CholeskyQR2 orthonormalisation
-    step = 1 << 20
-    Y = torch.empty((n_loc, l), dtype=wdt, device=dev)
-    for s in range(0, n_loc, step):
-        Y[s:s + step] = (X_local[s:s + step].to(wdt) - m) @ Z
-    R_tot = torch.eye(l, dtype=torch.float64, device=dev)
+    # Y = (X - mu) Z, then CholeskyQR2: Y <- Y R^-1 twice (fp64 throughout)
+    Y = L.xw(X_local, Z.to(dev), mean=mean)
+    Y2 = torch.empty_like(Y)
     for _ in range(2):
-        G = (Y.T.to(torch.float64) @ Y.to(torch.float64)) if dev.type == "cpu" else (Y.T @ Y).to(torch.float64)
-        comm.all_reduce_(G)
+        G = comm.all_reduce_(L.xtx(Y)).cpu()
         G = 0.5 * (G + G.T)
         jitter = 0.0
         for _try in range(5):
-            try:
-                R = torch.linalg.cholesky(G + jitter * torch.eye(l, dtype=G.dtype, device=dev)).T
+            R, info = torch.linalg.cholesky_ex(G + jitter * torch.eye(l, dtype=G.dtype), upper=True)
+            if int(info) == 0:
                 break
-            except Exception:
-                jitter = max(jitter * 10, 1e-12 * float(G.diagonal().max()))
-        Rinv = torch.linalg.inv(R)
-        Y = (Y.to(torch.float64) @ Rinv).to(wdt)
-        R_tot = R @ R_tot
-    # B = Q^T (X - mu)  (l x d)
-    B = torch.zeros((l, d), dtype=torch.float64, device=dev)
-    for s in range(0, n_loc, step):
-        B += (Y[s:s + step].T.to(torch.float64) @ (X_local[s:s + step].to(torch.float64) - m.double()))
-    comm.all_reduce_(B)
+            jitter = max(jitter * 10, 1e-12 * float(G.diagonal().max()))
+        Rinv = torch.linalg.solve_triangular(R, torch.eye(l, dtype=R.dtype), upper=True)
+        L.xw(Y, Rinv.to(dev), upper=True, out=Y2)
+        Y, Y2 = Y2, Y
+    # B = Q^T (X - mu) (l x d), as (X - mu)^T Q (d x l: the tall side on the tile rows)
+    B = comm.all_reduce_(L.xtx(X_local, Y, mean_a=mean)).cpu().T
     Uhat, sv, Vt = torch.linalg.svd(B, full_matrices=False)
-    U = (Y.to(torch.float64) @ Uhat)
-    U, Vt = U[:, :k], Vt[:k]
+    U = L.xw(Y, Uhat[:, :k].contiguous().to(dev))
+    Vt = Vt[:k].to(dev)
     if flip_sign:
         U, Vt = svd_flip_distributed(U, Vt, comm)
-    return U, sv[:k], Vt
+    return U, sv[:k].to(dev), Vt
 
 
 # --------------------------------------------------------- PPCA dimension
