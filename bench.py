@@ -56,6 +56,7 @@ def parse(argv=None):
                     help="timed Lloyd steps of the IPE (true_distance_estimate) extra; 0 = skip")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-hard", action="store_true", help="skip the overlapping-blobs extra")
+    ap.add_argument("--no-mnist", action="store_true", help="skip the 70k x 784 (config 4) extra")
     return ap.parse_args(argv)
 
 
@@ -213,6 +214,53 @@ def _hard_extra(extra, a, comm, dev):
         extra["hard_error"] = repr(e)[:200]
 
 
+def _mnist_extra(extra, a, comm, dev):
+    """BASELINE config 4 shape (MNIST 70k x 784, k = 10; synthetic blobs of
+    that shape): wall-clock of the classical KMeans (k-means++, certified
+    fp32 E-step at d_pad = 1024) and PCA (50 components, CholeskyQR2 on the
+    fp64-MFMA Gram kernels) fits, and the q-means Lloyd step (delta-means +
+    tomography noise) on the same matrix."""
+    try:
+        from sq_learn_amd.parallel.comm import shard_bounds
+        from sq_learn_amd.parallel.sharding import ShardedArray
+        from sq_learn_amd.utils.datasets import make_blobs_device
+        from sq_learn_amd.models.cluster import KMeans, QMeans
+        from sq_learn_amd.models.decomposition import PCA
+        n, d, k = 70_000, 784, 10
+        s0, s1 = shard_bounds(n, comm.rank, comm.world_size)
+        X, _ = make_blobs_device(n, d, centers=k, cluster_std=4.0, center_box=(0.0, 8.0),
+                                 seed=a.seed + 7, device=dev, dtype=torch.float32,
+                                 row_range=(s0, s1))
+        sa = ShardedArray(X, n, s0, comm)
+
+        def wall(fn):
+            fn()   # warm (kernel load, workspace allocation)
+            _sync(dev)
+            comm.barrier()
+            t0 = time.perf_counter()
+            r = fn()
+            _sync(dev)
+            comm.barrier()
+            return _max_over_ranks(comm, dev, time.perf_counter() - t0), r
+
+        t, km = wall(lambda: KMeans(n_clusters=k, n_init=1, max_iter=30, random_state=0,
+                                    device=dev).fit(sa))
+        extra["mnist70kx784_kmeans_fit_s"] = t
+        extra["mnist70kx784_kmeans_n_iter"] = int(km.n_iter_)
+        t, _ = wall(lambda: PCA(n_components=50, random_state=0, device=dev).fit(sa))
+        extra["mnist70kx784_pca50_fit_s"] = t
+        t, qm = wall(lambda: QMeans(n_clusters=k, delta=a.delta, true_distance_estimate=False,
+                                    intermediate_error=True, true_tomography=False, n_init=1,
+                                    max_iter=20, tol=0.0, random_state=0, device=dev).fit(sa))
+        extra["mnist70kx784_qmeans_fit_s"] = t
+        extra["mnist70kx784_qmeans_lloyd_ms_per_step"] = round(
+            1e3 * getattr(qm, "fit_phase_s_", {}).get("lloyd_s", float("nan")) / max(qm.n_iter_, 1), 4)
+        del X, sa
+        torch.cuda.empty_cache()
+    except Exception as e:
+        extra["mnist_error"] = repr(e)[:200]
+
+
 def _fit_extra(extra, a, sa, comm, dev, init):
     """Wall-clock of a whole QMeans.fit (prelude: eta, mu(A), condition
     number; centring; initialisation; ``fit_iters`` Lloyd iterations with
@@ -341,6 +389,8 @@ def main(argv=None):
         _ipe_extra(extra, a, X, comm, dev, start, C0)
     if gpu and not a.no_hard:
         _hard_extra(extra, a, comm, dev)
+    if gpu and not a.no_mnist:
+        _mnist_extra(extra, a, comm, dev)
     from sq_learn_amd.parallel.sharding import ShardedArray
     sa = ShardedArray(X, a.n, start, comm)
     if not a.no_fit:

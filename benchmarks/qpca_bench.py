@@ -1,6 +1,6 @@
 """qPCA full fit with the quantum extras on the headline matrix (10M x 256
 fp32, 1 GPU): wall-clock of the second (warm) fit.
-python benchmarks/qpca_bench.py [--n N --solver full|randomized]"""
+python benchmarks/qpca_bench.py [--n N --d D --bf16 --lowrank --solver full|randomized]"""
 import argparse
 import time
 
@@ -16,10 +16,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--solver", default="full")
+    ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--lowrank", action="store_true",
+                    help="BASELINE config 2 data: low rank (32) + tail, as bench.py")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    X, _ = make_blobs_device(a.n, 256, centers=1024, cluster_std=1.0, seed=1, device=dev,
-                             dtype=torch.float32)
+    dt = torch.bfloat16 if a.bf16 else torch.float32
+    if a.lowrank:
+        from sq_learn_amd.utils.datasets import make_low_rank_device
+        X = make_low_rank_device(a.n, a.d, effective_rank=32, tail_strength=0.3, seed=2024,
+                                 device=dev, dtype=dt)
+    else:
+        X, _ = make_blobs_device(a.n, a.d, centers=1024, cluster_std=1.0, seed=1, device=dev,
+                                 dtype=dt)
     sa = ShardedArray(X, a.n, 0, Comm(None))
     q = QPCA(n_components=16, svd_solver=a.solver, random_state=0, device=dev).fit(sa)
     theta = 0.5 * float(q.singular_values_[15])

@@ -69,7 +69,7 @@ def main():
                 continue
             for c, v in sorted(cs.items()):
                 print(f"| `{k}` | {c} | {v:.4g} |")
-            if "SQ_INSTS_MFMA" in cs and "SQ_INSTS_VALU" in cs:
+            if cs.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in cs:
                 print(f"| `{k}` | VALU/MFMA (incl. MFMA) | {cs['SQ_INSTS_VALU'] / cs['SQ_INSTS_MFMA']:.2f} |")
             if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs:
                 # busy cycles are summed over all SIMDs (1024) ; GRBM over 8 XCDs

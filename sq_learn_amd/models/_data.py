@@ -171,8 +171,8 @@ def sigma_min(data: Data, mean=None):
         return float(s.min()) if s.numel() else 0.0
     R = L.cholqr2_r(data.X, data.comm, mean)
     if R is not None:
-        return float(torch.linalg.svdvals(R).min())
-    G = data.comm.all_reduce_(L.gram64_local(data.X, mean))
+        return float(torch.linalg.svdvals(R.cpu()).min())      # d x d, host LAPACK
+    G = data.comm.all_reduce_(L.gram64_local(data.X, mean)).cpu()
     ev = torch.linalg.eigvalsh(0.5 * (G + G.T))
     return float(torch.sqrt(ev.clamp(min=0.0)).min())
 

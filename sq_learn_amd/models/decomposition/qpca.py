@@ -39,6 +39,7 @@ from ...quantum import cost_model
 from .._data import as_data, global_mean_var, best_mu_distributed
 from ._base import _BasePCA, _as_out
 from ._svd import full_svd, truncated_svd
+from ...ops import linalg as L
 
 log = logging.getLogger("sq_learn_amd.qpca")
 
@@ -246,7 +247,12 @@ class QPCA(_BasePCA):
         V = torch.as_tensor(self.all_components[:k].T, dtype=dt, device=data.device)
         S = torch.as_tensor(np.asarray(self.explained_variance_all[:k] * (data.n_global - 1)) ** 0.5,
                             dtype=dt, device=data.device)
-        return ((data.X.to(dt) - mean.to(dt).to(data.device)) @ V) / S
+        if data.device.type == "cpu":
+            return ((data.X.to(dt) - mean.to(dt).to(data.device)) @ V) / S
+        # (X - mean) V in one fp64-accumulated pass (csrc/tsgemm64.hip xw)
+        X = data.X if data.X.stride(1) == 1 else data.X.contiguous()
+        U = L.xw(X, V.double(), mean=mean, out_dtype=dt)
+        return U / S
 
     def _fit_truncated(self, data, n_components, svd_solver):
         n_samples, n_features = data.n_global, data.d
