@@ -38,24 +38,52 @@ namespace sq {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+constexpr double binom_c(int n, int i) {
+  double c = 1.0;
+  for (int t = 1; t <= i; ++t) c = c * (double)(n - i + t) / (double)t;
+  return c;
+}
+
 constexpr int kIpeMaxQ = 15;
 constexpr int kIpeWalkM = 128;
 
-// P(Binomial(Q, F) >= h)
+// binomial coefficients C(n, i), n < 16 (uniform indices: scalar loads)
+__constant__ double kBinom[16][16] = {
+#define R(n) {C_(n,0),C_(n,1),C_(n,2),C_(n,3),C_(n,4),C_(n,5),C_(n,6),C_(n,7),C_(n,8),C_(n,9),C_(n,10),C_(n,11),C_(n,12),C_(n,13),C_(n,14),C_(n,15)}
+#define C_(n, i) ((i) > (n) ? 0.0 : binom_c(n, i))
+    R(0), R(1), R(2), R(3), R(4), R(5), R(6), R(7),
+    R(8), R(9), R(10), R(11), R(12), R(13), R(14), R(15)
+#undef C_
+#undef R
+};
+
+// P(Binomial(Q, F) >= h) = F^h sum_{m=0}^{Q-h} C(Q, h+m) F^m G^(Q-h-m),
+// G = 1 - F: a homogeneous Horner scheme (one mul + one fma per term, all
+// terms positive: no cancellation, no division)
 SQ_DEV double binom_upper_tail(double F, int Q, int h) {
-  // sum_{i=h}^{Q} C(Q,i) F^i (1-F)^(Q-i) by the recurrence of the pmf terms
-  const double G = 1.0 - F;
   if (F <= 0.0) return 0.0;
   if (F >= 1.0) return 1.0;
-  double term = 1.0;                      // C(Q,0) G^Q, built up below
-  for (int i = 0; i < Q; ++i) term *= G;
-  const double ratio = F / G;
-  double tail = 0.0;
-  for (int i = 0; i <= Q; ++i) {
-    if (i >= h) tail += term;
-    term *= ratio * (double)(Q - i) / (double)(i + 1);
+  const double G = 1.0 - F;
+  const int nt = Q - h;
+  double b = kBinom[Q][Q];
+  double gp = 1.0;
+  for (int m = nt - 1; m >= 0; --m) {
+    gp *= G;
+    b = fma(b, F, kBinom[Q][h + m] * gp);
   }
-  return tail;
+  double fh = 1.0;
+  for (int i = 0; i < h; ++i) fh *= F;
+  return fh * b;
+}
+
+// 1 / x to full fp64 precision: v_rcp_f64 + two Newton steps (the IEEE
+// division sequence is ~3x longer)
+SQ_DEV double rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
 }
 
 // The median of Q (odd) iid draws T_1..T_Q with CDF F is F^-1(U_(h)), h =
@@ -116,10 +144,10 @@ SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
   double v = 0.0;
   for (long long t = 0; t <= tmax; ++t) {
     const double sm = st * cb - ct * sb;   // sin(t alpha - beta): bin t
-    double mass = num / (sm * sm);
+    double mass = num * rcp64(sm * sm);
     if (t != 0 && 2 * t != M) {
       const double spl = st * cb + ct * sb;   // sin(t alpha + beta): bin M - t
-      mass += num / (spl * spl);
+      mass += num * rcp64(spl * spl);
     }
     F += mass;
     v = st * st;
@@ -379,47 +407,52 @@ SQ_DEV float ipe_pruned_exact(double ip, double S, double eps, int Q, float thr,
   return (float)(2.0 * S * v);
 }
 
-// D~ of the pair when it is <= thr, +inf when it is not (pruned sampler
-// above, odd Q); pairs the fp32 bound cannot separate from thr (m < 3, a ~ 1,
-// t_b beyond the walk cap) take the full sampler.
-SQ_DEV float ipe_distance_thr(float ipf, float nx2, float ny2, double eps, int Q, const RngKey& key,
-                              unsigned long long sid, float thr, int h, float cqh) {
+// Screen of one pair against thr (odd Q, finite thr): returns true with dt =
+// D~ when it is <= thr or +inf when it is not (the pruned sampler above);
+// false when the fp32 bound cannot separate the pair from thr (m < 3, a ~ 1,
+// t_b beyond the walk cap, or no threshold yet): the pair needs the full
+// sampler, which the caller defers to the wave's queue.
+SQ_DEV bool ipe_screen(float ipf, float nx2, float ny2, double eps, int Q, const RngKey& key,
+                       unsigned long long sid, float thr, int h, float cqh, float& dt) {
   const float INF = __builtin_inff();
-  if (thr < INF) {
-    // screen: a, r = thr (1 + 2^-22) / 2S (every D~(t) <= thr has
-    // sin^2(pi t / M) <= r) and eps_a in fp64, rounded once to fp32 (relative
-    // 2^-24); M within a few fp32 ulps, sqrtf / asinf within 2 ulps, covered by
-    // the margins below (the bound on m only has to be a LOWER bound)
-    const double Sd = (double)nx2 + (double)ny2;
-    const double inv = 0.5 / Sd;
-    const float a = (float)((Sd - 2.0 * (double)ipf) * inv);
-    const float r = (float)((double)thr * inv * (1.0 + 2.4e-7));
-    if (Sd > 0.0 && a < 0.99f && r < a) {
-      const float epsa = (float)(eps * fmax(1.0, fabs((double)ipf)) * 2.0 * inv);
-      const float Mf = fminf(1.5707963f / epsa * (1.0f + sqrtf(1.0f + 4.0f * epsa)), 1.0995116e12f);
-      const float Mlb = floorf(Mf * (1.0f - 1e-5f));
-      const float ra = fmaxf(r, 0.0f);
-      const float beta = asinf(sqrtf(a)), beta_t = asinf(sqrtf(ra));
-      const float marg = 1e-6f * (3.0f + 1.0f / sqrtf(1.0f - a) + 1.0f / sqrtf(1.0f - ra));
-      const float m = Mlb * (beta - beta_t - marg) * 0.31830987f;
-      const float tcap = Mf * beta_t * 0.31830989f;   // ~ t_b: the rare branch walks that far
-      if (m >= 3.0f && tcap <= 65536.0f) {
-        const float pbar = fminf(0.5f * (1.0f / m + 1.0f / (m * m)) * (1.0f + 1e-5f), 1.0f);
-        float pu = cqh;   // union bound C(Q, h) pbar^h >= pibar
-        for (int i = 0; i < h; ++i) pu *= pbar;
-        WordStream ws(key, sid);
-        const uint32_t w0 = ws.next();
-        if ((double)w0 * (1.0 / 4294967296.0) >= (double)pu * (1.0 + 1e-6)) return INF;
-        double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
-        const uint32_t w1 = ws.next();
-        const double u = ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
-                         (1.0 / 9007199254740992.0);
-        if (u >= pib) return INF;
-        return ipe_pruned_exact((double)ipf, (double)nx2 + (double)ny2, eps, Q, thr, u, ws);
-      }
-    }
-  }
-  return ipe_distance(ipf, (double)nx2, (double)ny2, eps, Q, key, sid);
+  if (!(thr < INF) || !(Q & 1)) return false;
+  // fp32 screen, every quantity within a few ulps (v_rcp / v_sqrt: 1 ulp):
+  // a (abs. error < 1e-6 for the fp32 S, ip of the MFMA), r = thr / 2S
+  // (1 + 2^-22: every D~(t) <= thr has sin^2(pi t / M) <= r), eps_a, M.
+  // sin(beta - beta_t) = sqrt(a (1 - r)) - sqrt(r (1 - a)) <= beta - beta_t
+  // gives a LOWER bound on m = M (beta - beta_t) / pi; the margin covers the
+  // rounding (a >= 1e-4: d sqrt(a) <= 1e-6 / 0.02).
+  const float S = nx2 + ny2;
+  if (!(S > 0.0f)) return false;
+  const float inv = 0.5f * __builtin_amdgcn_rcpf(S);
+  const float a = (S - 2.0f * ipf) * inv;
+  const float r = fmaxf(thr * inv * (1.0f + 4.8e-7f), 0.0f);
+  if (!(a < 0.99f && a > 1e-4f && r < a)) return false;
+  const float epsa = (float)eps * fmaxf(1.0f, fabsf(ipf)) * 2.0f * inv;
+  const float Mf = fminf(1.5707963f * __builtin_amdgcn_rcpf(epsa) *
+                             (1.0f + __builtin_amdgcn_sqrtf(1.0f + 4.0f * epsa)),
+                         1.0995116e12f);
+  const float Mlb = floorf(Mf * (1.0f - 2e-5f));
+  const float sd = __builtin_amdgcn_sqrtf(a * (1.0f - r)) - __builtin_amdgcn_sqrtf(r * (1.0f - a));
+  const float m = Mlb * (sd - 4e-5f) * 0.31830987f;
+  // t_b <= (M / pi) asin(sqrt r) <= M sqrt(r) / 2: the rare branch's walk
+  const float tcap = 0.5f * Mf * __builtin_amdgcn_sqrtf(r);
+  if (!(m >= 3.0f && tcap <= 1048576.0f)) return false;
+  const float rm = __builtin_amdgcn_rcpf(m);
+  const float pbar = fminf(0.5f * rm * (1.0f + rm) * (1.0f + 2e-5f), 1.0f);
+  // union bound C(Q, h) pbar^h >= pibar (exp2 / log2 within 2^-20)
+  const float pu = cqh * __builtin_amdgcn_exp2f((float)h * __builtin_amdgcn_logf(pbar)) * (1.0f + 1e-4f);
+  WordStream ws(key, sid);
+  const uint32_t w0 = ws.next();
+  dt = INF;
+  if ((float)w0 * 2.3283064e-10f >= pu) return true;
+  const double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
+  const uint32_t w1 = ws.next();
+  const double u = ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
+                   (1.0 / 9007199254740992.0);
+  if (u >= pib) return true;
+  dt = ipe_pruned_exact((double)ipf, (double)nx2 + (double)ny2, eps, Q, thr, u, ws);
+  return true;
 }
 
 SQ_DEV bool ipe_better(float ob, uint32_t ok, int oj, float b, uint32_t kk, int jj) {
@@ -443,6 +476,10 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   __shared__ float hip_[4][16];
   __shared__ float hv[16];
   __shared__ int hj[16];
+  // per-lane queues of the pairs that need the full sampler ([slot][thread])
+  constexpr int QCAP = D4 <= 128 ? 8 : 5;
+  __shared__ uint32_t qj[QCAP * 256];
+  __shared__ float qip[QCAP * 256];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
@@ -459,7 +496,7 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   __syncthreads();
   // register i of this lane = pair (row row0 + 4 q4 + i, centroid 16 t + c16)
   f32x4 nx2, best;
-  int bj[4];
+  int bj[4];   // runtime-indexed only through unrolled selects (no scratch)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const long long r = row0 + 4 * q4 + i;
@@ -470,6 +507,47 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   const int h = (Q + 1) / 2;
   float cqh = 1.0f;   // C(Q, h)
   for (int i = 0; i < h; ++i) cqh = cqh * (float)(Q - i) / (float)(i + 1);
+  // Pairs that need the full sampler go to this lane's LDS queue and are
+  // sampled by a wave-wide drain (one inlined copy of the sampler): the
+  // expensive path runs max(queue length) times per wave instead of once per
+  // step in which ANY lane meets such a pair.
+  int qn = 0;
+  auto consider = [&](int i, int j, float dt) {
+    // row slot i (compile-time after unrolling) takes (dt, j) if better
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      if (ii == i) {
+        const long long g = row_offset + row0 + 4 * q4 + ii;
+        bool take = dt < best[ii];
+        if (!take && dt == best[ii] && dt < INF) {   // tie: the random keys decide (rare)
+          const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
+          const uint32_t bk = band_key(tie_key, g, (uint32_t)bj[ii]);
+          take = tk < bk || (tk == bk && j < bj[ii]);
+        }
+        if (take) {
+          best[ii] = dt;
+          bj[ii] = j;
+        }
+      }
+    }
+  };
+  auto drain = [&]() {
+    while (__ballot(qn > 0) != 0ull) {   // wave-uniform
+      if (qn > 0) {
+        --qn;
+        const uint32_t pj = qj[qn * 256 + threadIdx.x];
+        const float ip = qip[qn * 256 + threadIdx.x];
+        const int i = (int)(pj >> 30), j = (int)(pj & 0x3fffffffu);
+        float nxi = nx2[0];
+#pragma unroll
+        for (int ii = 1; ii < 4; ++ii) nxi = i == ii ? nx2[ii] : nxi;
+        const long long g = row_offset + row0 + 4 * q4 + i;
+        const float dt = ipe_distance(ip, (double)nxi, (double)cn[j], eps, Q, key,
+                                      (unsigned long long)g * (unsigned long long)k + (unsigned long long)j);
+        consider(i, j, dt);
+      }
+    }
+  };
   int hint[4] = {-1, -1, -1, -1};
   if (prune) {
     // ---- pass 1: exact fp32 distance argmin (hint), with its inner product
@@ -508,71 +586,103 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       }
     }
     __syncthreads();
-    // the 16 hint pairs, sampled in full: wave w, lanes 0..3 -> row 4 w + lane
-    if (lane < 4) {
-      const int rr = 4 * wave + lane;
-      float b = mb[0][rr], p = hip_[0][rr];
-      int jj = mj[0][rr];
-      for (int w = 1; w < 4; ++w)
-        if (mb[w][rr] < b || (mb[w][rr] == b && mj[w][rr] < jj)) {
-          b = mb[w][rr]; p = hip_[w][rr]; jj = mj[w][rr];
-        }
-      const long long r = row0 + rr;
-      float v = INF;
-      if (r < n && jj < k) {
-        const long long g = row_offset + r;
-        v = ipe_distance(p, (double)xn[r], (double)cn[jj], eps, Q, key,
-                         (unsigned long long)g * (unsigned long long)k + (unsigned long long)jj);
-      } else {
-        jj = -1;
-      }
-      hv[rr] = v;
-      hj[rr] = jj;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      hint[i] = hj[4 * q4 + i];
-      if (hint[i] >= 0) { best[i] = hv[4 * q4 + i]; bj[i] = hint[i]; }
-    }
   }
-  // ---- pass 2 (the only pass without pruning): every pair but the hint
-  for (int t = wave; t < n_tiles; t += 4) {   // the waves split the centroid tiles
-    const float* bf = Cf + (size_t)t * D4 * 64 + lane;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 16
-    for (int s = 0; s < D4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
-    const int j = t * 16 + c16;
-    if (j < k) {   // padded centroid columns do nothing (no MFMA / sync below)
-      const float ny2 = cn[j];
-      // one inlined copy of the sampler: the 4 pairs rotate through slot 0
-#pragma nounroll
-      for (int i = 0; i < 4; ++i) {
-        const long long r = row0 + 4 * q4 + i;
-        if (r < n && j != hint[0]) {
-          const long long g = row_offset + r;
-          const unsigned long long sid = (unsigned long long)g * (unsigned long long)k + (unsigned long long)j;
-          const float dt = prune ? ipe_distance_thr(acc[0], nx2[0], ny2, eps, Q, key, sid, best[0], h, cqh)
-                                 : ipe_distance(acc[0], (double)nx2[0], (double)ny2, eps, Q, key, sid);
-          bool take = dt < best[0];
-          if (!take && dt == best[0] && dt < INF) {   // tie: the random keys decide (rare)
-            const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
-            const uint32_t bk = band_key(tie_key, g, (uint32_t)bj[0]);
-            take = tk < bk || (tk == bk && j < bj[0]);
+  // ---- pass 2: every pair but the hint (the only pass without pruning).
+  // Pairs the screen resolves cost an fp32 bound + one Philox block; the
+  // others go to the lane's queue.  Step -1 (prune) queues the 16 hint pairs
+  // (row 4 q4 + w taken by lane (q4, c16 = 0) of wave w, as its row slot w)
+  // and publishes their samples as every row's starting threshold.  The
+  // queue is drained at ONE call site (one inlined copy of the full
+  // sampler): after the hint step, when a lane could overflow on the next
+  // tile, and after the wave's last tile.  Thresholds are always values of
+  // pairs already sampled (exact); queued pairs join the running best when
+  // drained.
+  const int ntl = wave < n_tiles ? (n_tiles - wave + 3) / 4 : 0;   // this wave's tiles
+  bool queued = false;
+  int jh = -1;
+  for (int stp = prune ? -1 : 0; stp < ntl; ++stp) {
+    if (stp < 0) {
+      if (c16 == 0) {
+        const int rr = 4 * q4 + wave;
+        float b = mb[0][rr], p = hip_[0][rr];
+        int jj = mj[0][rr];
+        for (int w = 1; w < 4; ++w)
+          if (mb[w][rr] < b || (mb[w][rr] == b && mj[w][rr] < jj)) {
+            b = mb[w][rr]; p = hip_[w][rr]; jj = mj[w][rr];
           }
-          if (take) {
-            best[0] = dt;
-            bj[0] = j;
-          }
+        if (row0 + rr < n && jj < k) {
+          qj[threadIdx.x] = ((uint32_t)wave << 30) | (uint32_t)jj;
+          qip[threadIdx.x] = p;
+          qn = 1;
+          queued = true;
+          jh = jj;
         }
-        acc = acc.yzwx;
-        nx2 = nx2.yzwx;
-        best = best.yzwx;
-        const int j0 = bj[0];
-        bj[0] = bj[1]; bj[1] = bj[2]; bj[2] = bj[3]; bj[3] = j0;
-        const int h0 = hint[0];
-        hint[0] = hint[1]; hint[1] = hint[2]; hint[2] = hint[3]; hint[3] = h0;
+      }
+    } else {
+      const int t = wave + 4 * stp;
+      const float* bf = Cf + (size_t)t * D4 * 64 + lane;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 16
+      for (int s = 0; s < D4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
+      const int j = t * 16 + c16;
+      if (j < k) {   // padded centroid columns do nothing
+        const float ny2 = cn[j];
+        // one inlined copy of the screen: the 4 pairs rotate through slot 0
+        // (back in place after the 4 steps)
+#pragma nounroll
+        for (int i = 0; i < 4; ++i) {
+          const long long r = row0 + 4 * q4 + i;
+          if (r < n && j != hint[0]) {
+            const long long g = row_offset + r;
+            float dt;
+            if (prune && ipe_screen(acc[0], nx2[0], ny2, eps, Q, key,
+                                    (unsigned long long)g * (unsigned long long)k + (unsigned long long)j,
+                                    best[0], h, cqh, dt)) {
+              bool take = dt < best[0];
+              if (!take && dt == best[0] && dt < INF) {   // tie: the random keys decide (rare)
+                const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
+                const uint32_t bk = band_key(tie_key, g, (uint32_t)bj[0]);
+                take = tk < bk || (tk == bk && j < bj[0]);
+              }
+              if (take) {
+                best[0] = dt;
+                bj[0] = j;
+              }
+            } else {
+              qj[qn * 256 + threadIdx.x] = ((uint32_t)i << 30) | (uint32_t)j;
+              qip[qn * 256 + threadIdx.x] = acc[0];
+              ++qn;
+            }
+          }
+          acc = acc.yzwx;
+          nx2 = nx2.yzwx;
+          best = best.yzwx;
+          const int j0 = bj[0];
+          bj[0] = bj[1]; bj[1] = bj[2]; bj[2] = bj[3]; bj[3] = j0;
+          const int h0 = hint[0];
+          hint[0] = hint[1]; hint[1] = hint[2]; hint[2] = hint[3]; hint[3] = h0;
+        }
+      }
+    }
+    // drain: after the hint step, when a lane could overflow on the next
+    // tile (room for 4 more), after the last tile
+    const bool flush = stp < 0 || stp == ntl - 1 || qn > QCAP - 4;
+    if (__ballot(flush && qn > 0) != 0ull) drain();
+    if (stp < 0) {
+      if (c16 == 0) {
+        float v = best[0];
+#pragma unroll
+        for (int ii = 1; ii < 4; ++ii) v = wave == ii ? best[ii] : v;
+        hv[4 * q4 + wave] = queued ? v : INF;
+        hj[4 * q4 + wave] = queued ? jh : -1;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        hint[i] = hj[4 * q4 + i];
+        best[i] = hint[i] >= 0 ? hv[4 * q4 + i] : INF;
+        bj[i] = hint[i];
       }
     }
   }
