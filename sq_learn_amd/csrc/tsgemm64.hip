@@ -46,20 +46,21 @@ template <> struct Store<double> { using type = double; };
 
 // the MFMAs of one 16-k-row panel pair: As[k][lda_s], Bs[k][ldb_s]; each
 // operand is widened and centred (per-lane column mean, in registers)
-template <int WM, int WN, typename SA, typename SB>
+template <int PK, int WM, int WN, typename SA, typename SB>
 SQ_DEV void panel_mfma(const SA* __restrict__ As, const SB* __restrict__ Bs, int lda_s, int ldb_s,
                        int wm, int wn, int lane, const double (&ma)[WM], const double (&mb)[WN],
-                       f64x4 (&acc)[WM][WN], bool tri, int kvalid) {
+                       f64x4 (&acc)[WM][WN], int kvalid) {
   const int c16 = lane & 15, q4 = lane >> 4;
 #pragma unroll
-  for (int kk = 0; kk < kPK / 4; ++kk) {
+  for (int kk = 0; kk < PK / 4; ++kk) {
     double a[WM], b[WN];
     // k-rows past the split's end hold 0, which centring would turn into
-    // -mu: their A operand is forced to 0 so they add nothing
-    const bool kv = 4 * kk + q4 < kvalid;
+    // -mu: their A operand is forced to 0 so they add nothing (a select
+    // after an unconditional LDS read: no exec-mask branch in the loop)
+    const double kv = 4 * kk + q4 < kvalid ? 1.0 : 0.0;
 #pragma unroll
     for (int i = 0; i < WM; ++i)
-      a[i] = kv ? (double)As[(4 * kk + q4) * lda_s + (wm * WM + i) * 16 + c16] - ma[i] : 0.0;
+      a[i] = ((double)As[(4 * kk + q4) * lda_s + (wm * WM + i) * 16 + c16] - ma[i]) * kv;
 #pragma unroll
     for (int j = 0; j < WN; ++j)
       b[j] = (double)Bs[(4 * kk + q4) * ldb_s + (wn * WN + j) * 16 + c16] - mb[j];
@@ -67,8 +68,7 @@ SQ_DEV void panel_mfma(const SA* __restrict__ As, const SB* __restrict__ Bs, int
     for (int i = 0; i < WM; ++i)
 #pragma unroll
       for (int j = 0; j < WN; ++j)
-        if (!tri || wm * WM + i <= wn * WN + j)   // wave-uniform (diagonal tiles)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -80,11 +80,12 @@ SQ_DEV void panel_mfma(const SA* __restrict__ As, const SB* __restrict__ Bs, int
 //    contiguous: conflict-free);
 //  * fp64: thread t -> row t / 32, columns (t % 32) + 32 e (8-B loads, a
 //    wave reads 256 contiguous bytes per row; ds_write_b64 lanes contiguous).
-template <typename T, int TC, bool VEC>
+template <typename T, int TC, bool VEC, int PK = kPK>
 struct RowPanel {
   using S = typename Store<T>::type;
   static constexpr bool F64 = sizeof(T) == 8;
-  static constexpr int V = (kPK * TC) / kThreads;   // 1, 2 or 4
+  static_assert(!F64 || PK == 16, "fp64 panels: 32 threads per 16-row panel row");
+  static constexpr int V = (PK * TC) / kThreads;   // 1, 2, 4 (8 for 32-row fp32 panels)
   static constexpr int TPR = F64 ? 32 : TC / V;     // threads per panel row
   static constexpr int LD = TC + 16;
   S v[V];
@@ -103,6 +104,24 @@ struct RowPanel {
     } else {
       const int col = c0 + (t % TPR) * V;
       const int lim = rok ? ncols - col : 0;
+      if (VEC && V == 8 && lim >= 8) {
+        if constexpr (sizeof(T) == 4) {
+          const float4 x = *reinterpret_cast<const float4*>(p + col);
+          const float4 y = *reinterpret_cast<const float4*>(p + col + 4);
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+          v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+          return;
+        } else {
+          const uint4 x = *reinterpret_cast<const uint4*>(p + col);
+          const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] = bf16_to_f32((uint16_t)(w4[e] & 0xFFFFu));
+            v[2 * e + 1] = bf16_to_f32((uint16_t)(w4[e] >> 16));
+          }
+          return;
+        }
+      }
       if (VEC && V == 4 && lim >= 4) {
         if constexpr (sizeof(T) == 4) {
           const float4 x = *reinterpret_cast<const float4*>(p + col);
@@ -126,6 +145,10 @@ struct RowPanel {
     if constexpr (F64) {
 #pragma unroll
       for (int e = 0; e < V; ++e) dst[(t / 32) * LD + (t % 32) + 32 * e] = v[e];
+    } else if constexpr (V == 8) {
+      float* q = dst + (t / TPR) * LD + (t % TPR) * 8;
+      *reinterpret_cast<float4*>(q) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(q + 4) = make_float4(v[4], v[5], v[6], v[7]);
     } else if constexpr (V == 4) {
       *reinterpret_cast<float4*>(dst + (t / TPR) * LD + (t % TPR) * 4) =
           make_float4(v[0], v[1], v[2], v[3]);
@@ -143,12 +166,15 @@ __global__ void __launch_bounds__(kThreads, 4) xtx_kernel(
     const TB* __restrict__ B, long long ldb, const double* __restrict__ mub, int db, long long n,
     int n_splits, int n_pairs, int ntb, double* __restrict__ part) {
   constexpr int TM = 64 * WM, TN = 32 * WN;
-  using PA = RowPanel<TA, TM, VEC>;
-  using PB = RowPanel<TB, TN, VEC>;
+  // 32-row panels when both operands stage as fp32 (half the barriers per
+  // MFMA; 74 KiB of LDS), 16 for fp64 operands
+  constexpr int PK = (sizeof(TA) < 8 && sizeof(TB) < 8) ? 32 : 16;
+  using PA = RowPanel<TA, TM, VEC, PK>;
+  using PB = RowPanel<TB, TN, VEC, PK>;
   using SA = typename PA::S;
   using SB = typename PB::S;
-  __shared__ __attribute__((aligned(16))) SA As[2][kPK * PA::LD];
-  __shared__ __attribute__((aligned(16))) SB Bs[2][kPK * PB::LD];
+  __shared__ __attribute__((aligned(16))) SA As[2][PK * PA::LD];
+  __shared__ __attribute__((aligned(16))) SB Bs[2][PK * PB::LD];
   // XCD-aware item: the 8 XCDs take splits s = xcd mod 8, so every tile pair
   // of a split (the same rows) runs in one XCD's L2
   const int b = blockIdx.x;
@@ -166,6 +192,8 @@ __global__ void __launch_bounds__(kThreads, 4) xtx_kernel(
     J = p % ntb;
   }
   const bool diag = SYM && I == J;
+  const int wv = threadIdx.x >> 6;
+  const bool below = diag && (wv & 3) * WM > (wv >> 2) * WN + WN - 1;   // wave-uniform
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w & 3, wn = w >> 2;
   const int c16 = lane & 15, q4 = lane >> 4;
@@ -173,18 +201,21 @@ __global__ void __launch_bounds__(kThreads, 4) xtx_kernel(
   const long long r_begin = (long long)s * per;
   const long long r_end = r_begin + per < n ? r_begin + per : n;
   const int a0 = I * TM, b0 = J * TN;
-  // the column means of this lane's operand columns (constant over the rows)
+  // the column means of this lane's operand columns (constant over the
+  // rows), staged through LDS and read into registers before any panel load
+  // is in flight (a global load here would make the compiler drain the
+  // prefetch queue - vmcnt(0) - inside the MFMA loop)
+  __shared__ double smu[TM + TN];
+  for (int c = threadIdx.x; c < TM + TN; c += kThreads) {
+    const int ca = a0 + c, cb = b0 + c - TM;
+    smu[c] = c < TM ? (mua && ca < da ? mua[ca] : 0.0) : (mub && cb < db ? mub[cb] : 0.0);
+  }
+  __syncthreads();
   double ma[WM], mb[WN];
 #pragma unroll
-  for (int i = 0; i < WM; ++i) {
-    const int c = a0 + (wm * WM + i) * 16 + c16;
-    ma[i] = mua && c < da ? mua[c] : 0.0;
-  }
+  for (int i = 0; i < WM; ++i) ma[i] = smu[(wm * WM + i) * 16 + c16];
 #pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int c = b0 + (wn * WN + j) * 16 + c16;
-    mb[j] = mub && c < db ? mub[c] : 0.0;
-  }
+  for (int j = 0; j < WN; ++j) mb[j] = smu[TM + (wn * WN + j) * 16 + c16];
   f64x4 acc[WM][WN];
 #pragma unroll
   for (int i = 0; i < WM; ++i)
@@ -194,7 +225,7 @@ __global__ void __launch_bounds__(kThreads, 4) xtx_kernel(
   PB pb;
   const TB* Bsrc = SYM ? (const TB*)A : B;
   const long long ldbs = SYM ? lda : ldb;
-  const int npan = r_end > r_begin ? (int)((r_end - r_begin + kPK - 1) / kPK) : 0;
+  const int npan = r_end > r_begin ? (int)((r_end - r_begin + PK - 1) / PK) : 0;
   if (npan > 0) {
     pa.load(A, lda, r_begin, r_end, a0, da);
     if (!diag) pb.load(Bsrc, ldbs, r_begin, r_end, b0, db);
@@ -206,16 +237,19 @@ __global__ void __launch_bounds__(kThreads, 4) xtx_kernel(
     const int cur = st & 1;
     const bool more = st + 1 < npan;
     if (more) {   // next panel: global -> registers, in flight during the MFMAs
-      const long long r = r_begin + (long long)(st + 1) * kPK;
+      const long long r = r_begin + (long long)(st + 1) * PK;
       pa.load(A, lda, r, r_end, a0, da);
       if (!diag) pb.load(Bsrc, ldbs, r, r_end, b0, db);
     }
     // SYM diagonal tile: B = the A panel (SYM: TA == TB and TM == TN, one
-    // inlined copy of the MFMA loop with a runtime operand source)
+    // inlined copy of the MFMA loop with a runtime operand source); the
+    // waves whose whole sub-tile lies below the diagonal skip the MFMAs (the
+    // finalize reads the upper triangle only)
     const SB* bsrc = diag ? (const SB*)As[cur] : Bs[cur];
-    const long long left = r_end - (r_begin + (long long)st * kPK);
-    panel_mfma<WM, WN>(As[cur], bsrc, PA::LD, PB::LD, wm, wn, lane, ma, mb, acc, diag,
-                       left < kPK ? (int)left : kPK);
+    const long long left = r_end - (r_begin + (long long)st * PK);
+    if (!below)
+      panel_mfma<PK, WM, WN>(As[cur], bsrc, PA::LD, PB::LD, wm, wn, lane, ma, mb, acc,
+                             left < PK ? (int)left : PK);
     if (more) {
       pa.store(As[cur ^ 1]);
       if (!diag) pb.store(Bs[cur ^ 1]);
