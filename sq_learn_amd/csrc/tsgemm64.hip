@@ -38,6 +38,16 @@ SQ_DEV double widen(uint16_t v) { return (double)bf16_to_f32(v); }
 
 constexpr int kPK = 16;      // k-rows per LDS panel (4 MFMA k-steps)
 constexpr int kThreads = 512;
+// build-time knobs for the variant sweep (benchmarks/tsgemm_variants.py)
+#ifndef SQ_TS_WPE
+#define SQ_TS_WPE 4          // min waves per SIMD (4: 128 VGPRs, 2 workgroups per CU)
+#endif
+#ifndef SQ_TS_PK32
+#define SQ_TS_PK32 1         // 32-row panels for fp32-staged operands
+#endif
+#ifndef SQ_TS_PREFETCH
+#define SQ_TS_PREFETCH 1     // next k-step's LDS operands read before this step's MFMAs
+#endif
 
 // LDS storage of a panel element: fp32 / bf16 inputs are kept as raw fp32
 // (exact), fp64 inputs as fp64; the centring happens at operand read
@@ -51,19 +61,39 @@ SQ_DEV void panel_mfma(const SA* __restrict__ As, const SB* __restrict__ Bs, int
                        int wm, int wn, int lane, const double (&ma)[WM], const double (&mb)[WN],
                        f64x4 (&acc)[WM][WN], int kvalid) {
   const int c16 = lane & 15, q4 = lane >> 4;
+  const SA* pa = As + q4 * lda_s + wm * WM * 16 + c16;
+  const SB* pb = Bs + q4 * ldb_s + wn * WN * 16 + c16;
+  // the raw operands of k-step kk + 1 are read from LDS before the MFMAs of
+  // k-step kk are issued (their latency hides behind those MFMAs)
+  SA ra[WM];
+  SB rb[WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i) ra[i] = pa[i * 16];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) rb[j] = pb[j * 16];
 #pragma unroll
   for (int kk = 0; kk < PK / 4; ++kk) {
-    double a[WM], b[WN];
+    if (!SQ_TS_PREFETCH && kk > 0) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i) ra[i] = pa[(4 * kk) * lda_s + i * 16];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) rb[j] = pb[(4 * kk) * ldb_s + j * 16];
+    }
     // k-rows past the split's end hold 0, which centring would turn into
-    // -mu: their A operand is forced to 0 so they add nothing (a select
-    // after an unconditional LDS read: no exec-mask branch in the loop)
+    // -mu: their A operand is forced to 0 so they add nothing (a select,
+    // no exec-mask branch in the loop)
     const double kv = 4 * kk + q4 < kvalid ? 1.0 : 0.0;
+    double a[WM], b[WN];
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
-      a[i] = ((double)As[(4 * kk + q4) * lda_s + (wm * WM + i) * 16 + c16] - ma[i]) * kv;
+    for (int i = 0; i < WM; ++i) a[i] = ((double)ra[i] - ma[i]) * kv;
 #pragma unroll
-    for (int j = 0; j < WN; ++j)
-      b[j] = (double)Bs[(4 * kk + q4) * ldb_s + (wn * WN + j) * 16 + c16] - mb[j];
+    for (int j = 0; j < WN; ++j) b[j] = (double)rb[j] - mb[j];
+    if (SQ_TS_PREFETCH && kk + 1 < PK / 4) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i) ra[i] = pa[(4 * (kk + 1)) * lda_s + i * 16];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) rb[j] = pb[(4 * (kk + 1)) * ldb_s + j * 16];
+    }
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
@@ -161,14 +191,14 @@ struct RowPanel {
 };
 
 template <typename TA, typename TB, int WM, int WN, bool SYM, bool VEC>
-__global__ void __launch_bounds__(kThreads, 4) xtx_kernel(
+__global__ void __launch_bounds__(kThreads, SQ_TS_WPE) xtx_kernel(
     const TA* __restrict__ A, long long lda, const double* __restrict__ mua, int da,
     const TB* __restrict__ B, long long ldb, const double* __restrict__ mub, int db, long long n,
     int n_splits, int n_pairs, int ntb, double* __restrict__ part) {
   constexpr int TM = 64 * WM, TN = 32 * WN;
   // 32-row panels when both operands stage as fp32 (half the barriers per
   // MFMA; 74 KiB of LDS), 16 for fp64 operands
-  constexpr int PK = (sizeof(TA) < 8 && sizeof(TB) < 8) ? 32 : 16;
+  constexpr int PK = (SQ_TS_PK32 && sizeof(TA) < 8 && sizeof(TB) < 8) ? 32 : 16;
   using PA = RowPanel<TA, TM, VEC, PK>;
   using PB = RowPanel<TB, TN, VEC, PK>;
   using SA = typename PA::S;
@@ -379,7 +409,7 @@ SQ_DEV void panel_mfma_xw(const double* __restrict__ As, const double* __restric
 }
 
 template <typename T, typename TO, int WM, int WN, bool VEC>
-__global__ void __launch_bounds__(kThreads, 4) xw_kernel(
+__global__ void __launch_bounds__(kThreads, SQ_TS_WPE) xw_kernel(
     const T* __restrict__ A, long long lda, const double* __restrict__ mu, long long n, int d,
     const double* __restrict__ W, long long ldw, int l, int upper, TO* __restrict__ Y,
     long long ldy) {
