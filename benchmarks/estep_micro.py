@@ -21,6 +21,9 @@ ap.add_argument("--delta", type=float, default=0.5)
 ap.add_argument("--what", default="estep", choices=["estep", "reduce", "both"])
 ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16", "x64"])
 ap.add_argument("--bounds", action="store_true", help="x64: write the Hamerly bounds too")
+ap.add_argument("--stamps", action="store_true",
+                help="x64 diagnostic variant (-DSQ_X64_STAMP=1 via SQ_NATIVE_VARIANT): "
+                     "print the per-wave phase split of the last launch")
 a = ap.parse_args()
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
@@ -74,3 +77,24 @@ for name in (["estep", "reduce"] if a.what == "both" else [a.what]):
     fl = 2.0 * a.n * a.k * dp
     print(f"{a.prec} {name}: {ms:.3f} ms  ({fl / ms / 1e9:.1f} TFLOP/s equiv)  "
           f"counts(ovf,dense)={buf.counts.tolist()}")
+if a.stamps:
+    import ctypes
+    import numpy as np
+    lib = ctypes.CDLL(os.environ["SQ_NATIVE_VARIANT"])
+    torch.cuda.synchronize()
+    run_estep()
+    torch.cuda.synchronize()
+    buf_h = np.zeros((8192, 12), dtype=np.uint64)
+    assert lib.sq_x64_stamps(ctypes.c_void_p(buf_h.ctypes.data), 8192) == 0
+    w = buf_h[buf_h[:, 0] > 0].astype(np.float64)
+    tot = w[:, 0].mean()
+    names = ["total", "sweep", "tile sync", "first-tile sync", "row-set epilogue", "blocks",
+             "stage() issue", "epilogue: min + cand lists", "A-load issue",
+             "  - row min + T", "  - cand loop", "  - ub/lb + lgkm wait"]
+    print(f"stamps over {len(w)} waves (shader cycles, mean per wave):")
+    for i, nm in enumerate(names):
+        v = w[:, i].mean()
+        extra = "" if i in (0, 5) else f"  {100 * v / tot:.1f}% of total"
+        per = "" if i == 5 else f"  {v / max(w[:, 5].mean(), 1):.0f} per block"
+        print(f"  {nm:18s} {v:14.0f}{extra}{per}")
+

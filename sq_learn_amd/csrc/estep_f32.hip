@@ -408,6 +408,22 @@ constexpr int kX64Waves = SQ_X64_NW;   // waves per workgroup (8: 2 per SIMD, sp
 #endif
 constexpr int kX64Ring = SQ_X64_RING;  // centroid-tile LDS slots (3: 2 tiles in flight)
 
+// Diagnostic build only (-DSQ_X64_STAMP=1, a variant library): per-wave
+// s_memtime sums of the kernel's phases go to a buffer of their own (never an
+// output), read back by sq_x64_stamps().  [wave][0 total, 1 sweep, 2 tile-sync
+// waits, 3 first-tile sync of a block (row-operand loads), 4 row-set epilogue,
+// 5 blocks, 6 stage() issue, 7 epilogue up to the candidate lists, 8 A-load
+// issue at block end]
+#ifndef SQ_X64_STAMP
+#define SQ_X64_STAMP 0
+#endif
+#if SQ_X64_STAMP
+constexpr int kStampWaves = 8192;
+constexpr int kStampN = 12;
+__device__ unsigned long long g_x64_stamps[kStampWaves * kStampN];
+#define SQ_STAMP_NOW() __builtin_amdgcn_s_memtime()
+#endif
+
 // Tile geometry of the certified filter: a 64-centroid tile is KT = KSD + 1
 // k-steps (d_pad / 16 data steps + the norm step) of 2 KiB each.  Up to
 // d_pad = 256 a whole tile is one LDS ring slot; above, the tile is staged in
@@ -428,6 +444,9 @@ struct X64Geom {
 // A fragments fit the registers; 1 above d_pad = 256.
 #ifndef SQ_X64_RS
 #define SQ_X64_RS 2
+#endif
+#ifndef SQ_X64_PFD
+#define SQ_X64_PFD 2   // B-fragment read distance of the row-set sweep (k-steps)
 #endif
 template <int KSD>
 struct X64RowSets {
@@ -525,6 +544,15 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   };
   f16x8 aug = (f16x8)0;
   if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
+  // |x|^2 of the row whose reduced minimum this lane ends with (rl_own of
+  // each row set), loaded with the block's A operand so the epilogue does not
+  // wait on a dependent global load
+  const int rl_lane = ((r32 >> 1) & 3) + 8 * ((r32 >> 1) >> 2) + 4 * half;
+  float xn_cur[RS], xn_nxt[RS];
+  auto load_xn = [&](long long b, float (&dst)[RS]) {
+#pragma unroll
+    for (int st = 0; st < RS; ++st) dst[st] = xn[row_at(b * ROWS + (wave * RS + st) * 32 + rl_lane)];
+  };
 
   float m1[RS][16], m2[RS][16], m3[RS][16];
   const int lane_off = (half * 64 + r32) * 16;
@@ -590,13 +618,28 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   // only retires the tile staged one step earlier - vmcnt(PPW) leaves this
   // step's glds in flight across the raw s_barrier (no __syncthreads: its
   // fence would drain them).
+#if SQ_X64_STAMP
+  unsigned long long st_sync = 0, st_sync0 = 0, st_post = 0, st_sweep = 0, st_blocks = 0;
+  unsigned long long st_stage = 0, st_cand = 0, st_aload = 0, st_rmin = 0, st_cl = 0, st_ub = 0;
+  const unsigned long long st_t0 = SQ_STAMP_NOW();
+  bool st_first = true;
+#endif
   auto sync_tile = [&]() {
+#if SQ_X64_STAMP
+    const unsigned long long sa = SQ_STAMP_NOW();
+#endif
     if constexpr (RING == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
     }
     __builtin_amdgcn_s_barrier();
+#if SQ_X64_STAMP
+    const unsigned long long sw = SQ_STAMP_NOW() - sa;
+    st_sync += sw;
+    if (st_first) st_sync0 += sw;
+    st_first = false;
+#endif
   };
 
   // one tile = NS sub-steps, each: stage the unit RING - 1 ahead, MFMAs on
@@ -618,6 +661,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   stage(0);
   if constexpr (RING == 3) stage(1);
   load_a(blk);
+  load_xn(blk, xn_cur);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
@@ -626,9 +670,6 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     for (int st = 0; st < RS; ++st)
 #pragma unroll
       for (int i = 0; i < 16; ++i) m1[st][i] = m2[st][i] = m3[st][i] = __builtin_inff();
-    if (lane < 32)
-#pragma unroll
-      for (int st = 0; st < RS; ++st) cnt_all[(wave * RS + st) * 32 + lane] = 0;
     if constexpr (RS == 1) {
       Acc pA, pB;
       tile(pA, pA, 0, false);
@@ -636,6 +677,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
       while (true) {
         if (t + 1 >= n_tiles) {
           load_a(blk + gridDim.x);   // clamped rows: unconditional (no phi on ah)
+          load_xn(blk + gridDim.x, xn_nxt);
           epi_all(pA, t);
           break;
         }
@@ -643,6 +685,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
         ++t;
         if (t + 1 >= n_tiles) {
           load_a(blk + gridDim.x);
+          load_xn(blk + gridDim.x, xn_nxt);
           epi_all(pB, t);
           break;
         }
@@ -655,21 +698,30 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
       // during the next half's MFMAs - two RS x 16-register accumulator sets
       // live instead of four
       f32x16 cA[RS], cB[RS];
-      auto pass = [&](const unsigned char* cur, int h, f32x16 (&acc)[RS], const f32x16 (&o)[RS],
-                      uint32_t qo, bool do_epi) {
+      // B fragments stream through a ring of PFD + 1 registers, PFD k-steps
+      // ahead of their MFMAs (one k-step of cover - a single MFMA pair - left
+      // the ds_read_b128 latency exposed at every k-step); the two column
+      // halves of a tile are one stream of 2 KT fragments, so the second
+      // half's first reads are in flight during the first half's last MFMAs
+      constexpr int PFD = SQ_X64_PFD;
+      constexpr int NB = PFD + 1;
+      f16x8 bq[NB];
+      auto frag = [&](const unsigned char* cur, int g) -> f16x8 {
+        return ldb(cur + lane_off + (g / KT) * 512 + (g % KT) * 2048);
+      };
+      auto pass = [&](auto H_, const unsigned char* cur, f32x16 (&acc)[RS],
+                      const f32x16 (&o)[RS], uint32_t qo, bool do_epi) {
+        constexpr int h = decltype(H_)::value;
 #pragma unroll
         for (int st = 0; st < RS; ++st) acc[st] = (f32x16){0};
-        const unsigned char* hb = cur + lane_off + h * 512;
-        f16x8 b[2];
-        b[0] = ldb(hb);
 #pragma unroll
         for (int ks = 0; ks < KT; ++ks) {
-          const int c = ks & 1, nx = c ^ 1;
-          if (ks + 1 < KT) b[nx] = ldb(hb + (ks + 1) * 2048);
+          const int g = h * KT + ks;
+          if (g + PFD < 2 * KT) bq[(g + PFD) % NB] = frag(cur, g + PFD);
 #pragma unroll
           for (int st = 0; st < RS; ++st)
-            acc[st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ks < KSD ? ah[st][ks] : aug, b[c],
-                                                             acc[st], 0, 0, 0);
+            acc[st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ks < KSD ? ah[st][ks] : aug,
+                                                             bq[g % NB], acc[st], 0, 0, 0);
           if (do_epi) {
 #pragma unroll
             for (int e = (ks * 16 * RS) / KT; e < ((ks + 1) * 16 * RS) / KT; ++e)
@@ -687,24 +739,53 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
           for (int i = 0; i < 16; ++i) ins(st, i, o[st][i], qo);
       };
       static_assert(NS == 1, "row sets need whole tiles per LDS slot");
+#if SQ_X64_STAMP
+      const unsigned long long sw0 = SQ_STAMP_NOW();
+      st_first = true;
+      ++st_blocks;
+#endif
       for (int t = 0; t < n_tiles; ++t) {
+#if SQ_X64_STAMP
+        const unsigned long long sg0 = SQ_STAMP_NOW();
+#endif
         stage(U + RING - 1);
+#if SQ_X64_STAMP
+        st_stage += SQ_STAMP_NOW() - sg0;
+#endif
         // half 0 of tile t (with the previous tile's half 1), then half 1
         // (with this tile's half 0); packed index q = 2 t + half
-        pass(buf(U), 0, cA, cB, (uint32_t)(2 * t - 1), t > 0);
-        pass(buf(U), 1, cB, cA, (uint32_t)(2 * t), true);
+#pragma unroll
+        for (int j = 0; j < PFD; ++j) bq[j] = frag(buf(U), j);
+        pass(std::integral_constant<int, 0>{}, buf(U), cA, cB, (uint32_t)(2 * t - 1), t > 0);
+        pass(std::integral_constant<int, 1>{}, buf(U), cB, cA, (uint32_t)(2 * t), true);
         sync_tile();
         ++U;
       }
+#if SQ_X64_STAMP
+      const unsigned long long sl0 = SQ_STAMP_NOW();
+#endif
       load_a(blk + gridDim.x);   // clamped rows: unconditional
+      load_xn(blk + gridDim.x, xn_nxt);
+#if SQ_X64_STAMP
+      st_aload += SQ_STAMP_NOW() - sl0;
+#endif
       drain(cB, (uint32_t)(2 * n_tiles - 1));
+#if SQ_X64_STAMP
+      st_sweep += SQ_STAMP_NOW() - sw0;
+#endif
     }
+#if SQ_X64_STAMP
+    const unsigned long long sp0 = SQ_STAMP_NOW();
+#endif
 
     // ---- per row set: row minimum, candidates, bounds, classification (a
     // runtime loop: one copy of the code; the set's top-3 lists are selected
     // by value into ms1..ms3 - compile-time register indices only)
 #pragma nounroll
     for (int st = 0; st < RS; ++st) {
+#if SQ_X64_STAMP
+    const unsigned long long sc0 = SQ_STAMP_NOW();
+#endif
     const long long row0 = blk * ROWS + (wave * RS + st) * 32;
     int* cand = cand_all + (wave * RS + st) * 32 * kMaxCand;
     int* cnt = cnt_all + (wave * RS + st) * 32;
@@ -744,8 +825,9 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     const float rmin = row_min(R);
     const int irow = r32 >> 1;
     const int rl_own = (irow & 3) + 8 * (irow >> 2) + 4 * half;
-    const long long g_own = row_at(row0 + rl_own);
-    const float xn_own = xn[g_own];
+    float xn_own = xn_cur[0];
+#pragma unroll
+    for (int o = 1; o < RS; ++o) xn_own = st == o ? xn_cur[o] : xn_own;
     const float xsv = alpha * sqrtf(xn_own) * (1.0f + 0x1p-16f);
     const float prod = xsv * Ch;
     const float mag = 0.25f * Ch * Ch + prod;
@@ -754,6 +836,10 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
 
     // ---- candidates -> LDS list of their row (C/D layout: register i of this
     // lane is row (i & 3) + 8 (i >> 2) + 4 half, column class r32)
+#if SQ_X64_STAMP
+    const unsigned long long sc1 = SQ_STAMP_NOW();
+    st_rmin += sc1 - sc0;
+#endif
     float nc[16];   // per register: this lane's smallest NON-candidate value
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -764,15 +850,22 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
         const uint32_t q = __float_as_uint(p) & qmask;
         return (int)((q >> 1) * kTileN + (q & 1u) * 32u) + r32;
       };
-      if (ms3[i] <= T) atomicAdd(&cnt[rl], kMaxCand + 1);   // lane may hide more: dense
-      if (ms1[i] <= T) {
-        const int s = atomicAdd(&cnt[rl], 1);
-        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(ms1[i]);
-      }
-      if (ms2[i] <= T) {
-        const int s = atomicAdd(&cnt[rl], 1);
-        if (s < kMaxCand) cand[rl * kMaxCand + s] = jof(ms2[i]);
-      }
+      // the 32 lanes of this half hold the whole row rl (one register each):
+      // wave ballots give its candidate count and every candidate's list slot
+      // (lane order) - no LDS atomics; each row's count is written once
+      const unsigned long long b1 = __ballot(ms1[i] <= T), b2 = __ballot(ms2[i] <= T);
+      const unsigned long long b3 = __ballot(ms3[i] <= T);   // lane may hide more: dense
+      const uint32_t b1l = (uint32_t)b1, b1h = (uint32_t)(b1 >> 32);
+      const uint32_t b2l = (uint32_t)b2, b2h = (uint32_t)(b2 >> 32);
+      const int c1 = __popc(half ? b1h : b1l), c2 = __popc(half ? b2h : b2l);
+      const bool d3 = (half ? (uint32_t)(b3 >> 32) : (uint32_t)b3) != 0u;
+      const int s1 = (int)__builtin_amdgcn_mbcnt_hi(b1h, __builtin_amdgcn_mbcnt_lo(b1l, 0u)) -
+                     (half ? __popc(b1l) : 0);
+      const int s2 = c1 + (int)__builtin_amdgcn_mbcnt_hi(b2h, __builtin_amdgcn_mbcnt_lo(b2l, 0u)) -
+                     (half ? __popc(b2l) : 0);
+      if (ms1[i] <= T && s1 < kMaxCand) cand[rl * kMaxCand + s1] = jof(ms1[i]);
+      if (ms2[i] <= T && s2 < kMaxCand) cand[rl * kMaxCand + s2] = jof(ms2[i]);
+      if (r32 == 0) cnt[rl] = c1 + c2 + (d3 ? kMaxCand + 1 : 0);
     }
     // Hamerly bounds of this row (distances, not squared): ub >= |x - c_min|,
     // lb <= distance to every NON-candidate centroid (the smallest filter
@@ -780,6 +873,10 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     // smallest), from D = |x|^2 + D'/alpha^2 with an fp32 margin.  A
     // multi-candidate row whose non-candidates stay beyond the band under
     // the next centroid shifts keeps its candidate set (bounds_filter).
+#if SQ_X64_STAMP
+    const unsigned long long sc2 = SQ_STAMP_NOW();
+    st_cl += sc2 - sc1;
+#endif
     float ub_own = 0.f, lb_own = 0.f;
     if (ub) {
       const float ncmin = row_min(nc);
@@ -792,6 +889,10 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+#if SQ_X64_STAMP
+    st_cand += SQ_STAMP_NOW() - sc0;
+    st_ub += SQ_STAMP_NOW() - sc2;
+#endif
 
     // ---- classify the wave's 32 rows (lane r32 < 32 owns row r32)
     const bool valid = row0 + r32 < ne;
@@ -845,8 +946,22 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     }   // row sets
+#pragma unroll
+    for (int st = 0; st < RS; ++st) xn_cur[st] = xn_nxt[st];
+#if SQ_X64_STAMP
+    st_post += SQ_STAMP_NOW() - sp0;
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if SQ_X64_STAMP
+  const int sidx = blockIdx.x * NW + wave;
+  if (lane == 0 && sidx < kStampWaves) {
+    unsigned long long* o = g_x64_stamps + (size_t)sidx * kStampN;
+    o[0] = SQ_STAMP_NOW() - st_t0; o[1] = st_sweep; o[2] = st_sync; o[3] = st_sync0;
+    o[4] = st_post; o[5] = st_blocks; o[6] = st_stage; o[7] = st_cand; o[8] = st_aload;
+    o[9] = st_rmin; o[10] = st_cl; o[11] = st_ub;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1643,6 +1758,21 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   if (rc) return rc;
   return (int)hipGetLastError();
 }
+
+#if SQ_X64_STAMP
+// diagnostic builds: copy the per-wave phase sums (see g_x64_stamps) to host
+int sq_x64_stamps(void* host, int n_waves) {
+  const int m = n_waves < kStampWaves ? n_waves : kStampWaves;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x64_stamps),
+                                  (size_t)m * kStampN * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+int sq_x64_stamps_clear() {
+  static unsigned long long zeros[kStampWaves * kStampN];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_x64_stamps), zeros, sizeof(zeros), 0,
+                                hipMemcpyHostToDevice);
+}
+#endif
 
 int sq_fill_mind(const void* X, int ldx, const void* Cm, int d, const void* labels, void* mind,
                  long long n, void* stream) {
