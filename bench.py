@@ -350,6 +350,10 @@ def main(argv=None):
     if eng.fast and gpu:
         cnt = eng.buf.counts.tolist()
         extra["overflow_rows_last"], extra["dense_rows_last"] = int(cnt[0]), int(cnt[1])
+        extra["multi_rows_last"] = int(cnt[2])   # rows re-checked over their candidate sets
+        xf = getattr(eng.buf, "exact_flag", None)
+        if xf is not None and cnt[2] > 0:   # of which the fp32 screen left to the fp64 pass
+            extra["multi_fp64_rows_last"] = int((xf[:int(cnt[2])] != 0).sum())
         # per-phase ms of 3 more (untimed) iterations, CUDA events per phase
         ph = {}
         for _ in range(3):

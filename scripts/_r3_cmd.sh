@@ -1,4 +1,6 @@
 export TMPDIR=/tmp
+B="python bench.py --warmup 5 --no-fit --no-qpca --no-mnist --ipe-steps 0"
 scripts/gpu_steps.sh \
- "stamps|200|SQ_NATIVE_VARIANT=sq_learn_amd/_variants/_C_stamp.so python benchmarks/estep_micro.py --prec x64 --iters 3 --stamps --bounds" \
- "tl10M|300|rm -rf /tmp/tl && rocprofv3 --kernel-trace --output-format csv -d /tmp/tl -o tl -- python3 bench.py --steps 20 --warmup 5 --no-fit --no-qpca --ipe-steps 0 --no-hard --no-mnist > gpurun_out/tl10_bench.log 2>&1 && python3 scripts/prof_timeline.py /tmp/tl --marker bounds_filter --last 4 > gpurun_out/timeline_10M.md"
+ "etests|500|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_estep_precision_gpu.py tests/test_mstep_incremental_gpu.py tests/test_kmeans_gpu.py tests/test_distributed_gpu.py" \
+ "bench|300|$B" \
+ "tl10M|300|rm -rf /tmp/tl && rocprofv3 --kernel-trace --output-format csv -d /tmp/tl -o tl -- python3 bench.py --steps 20 --warmup 5 --no-fit --no-qpca --ipe-steps 0 --no-hard --no-mnist > gpurun_out/tl10_bench.log 2>&1 && python3 scripts/prof_timeline.py /tmp/tl --marker bounds_filter --last 3 > gpurun_out/timeline_10M.md"

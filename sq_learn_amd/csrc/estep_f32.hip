@@ -484,7 +484,7 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
   constexpr int PPW = (PIECES + NW - 1) / NW;   // glds per wave per stage (uniform: counted vmcnt)
   auto buf = [&](int g) -> unsigned char* { return smem + (g % RING) * SLOT; };
   int* cand_all = reinterpret_cast<int*>(smem + RING * SLOT);        // [NW][RS][32][kMaxCand]
-  int* cnt_all = cand_all + NW * RS * 32 * kMaxCand;                  // [NW][RS][32]
+  int* cnt_all = cand_all + NW * RS * 32 * kMaxCand;                  // [NW][RS][32], then [NW][64] dump slots
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -841,9 +841,17 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
     st_rmin += sc1 - sc0;
 #endif
     float nc[16];   // per register: this lane's smallest NON-candidate value
+    // the 16 row thresholds of this lane's registers: all 16 reads in flight
+    // before the first use (one LDS latency, not 16 in a chain)
+    float Tr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Tr[i] = __shfl(T_own, 32 * half + 2 * i, 64);
+    // per-lane dump slot: the list / count stores below are unconditional
+    // (a lane with nothing to store writes here) - no exec-mask branches
+    int* const sink = cnt_all + NW * RS * 32 + wave * 64 + lane;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float T = __shfl(T_own, 32 * half + 2 * i, 64);
+      const float T = Tr[i];
       nc[i] = ms1[i] > T ? ms1[i] : (ms2[i] > T ? ms2[i] : ms3[i]);
       const int rl = (i & 3) + 8 * (i >> 2) + 4 * half;
       auto jof = [&](float p) -> int {
@@ -863,9 +871,9 @@ __global__ void __launch_bounds__(kX64Waves * 64) estep_x64_kernel(
                      (half ? __popc(b1l) : 0);
       const int s2 = c1 + (int)__builtin_amdgcn_mbcnt_hi(b2h, __builtin_amdgcn_mbcnt_lo(b2l, 0u)) -
                      (half ? __popc(b2l) : 0);
-      if (ms1[i] <= T && s1 < kMaxCand) cand[rl * kMaxCand + s1] = jof(ms1[i]);
-      if (ms2[i] <= T && s2 < kMaxCand) cand[rl * kMaxCand + s2] = jof(ms2[i]);
-      if (r32 == 0) cnt[rl] = c1 + c2 + (d3 ? kMaxCand + 1 : 0);
+      *((ms1[i] <= T && s1 < kMaxCand) ? cand + rl * kMaxCand + s1 : sink) = jof(ms1[i]);
+      *((ms2[i] <= T && s2 < kMaxCand) ? cand + rl * kMaxCand + s2 : sink) = jof(ms2[i]);
+      *(r32 == 0 ? cnt + rl : sink) = c1 + c2 + (d3 ? kMaxCand + 1 : 0);
     }
     // Hamerly bounds of this row (distances, not squared): ub >= |x - c_min|,
     // lb <= distance to every NON-candidate centroid (the smallest filter
@@ -1016,39 +1024,46 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     if (i >= n) break;
     const int l = labels[i];
     const double u = (double)ub[i] + (l >= 0 ? shift[l] : 1e300);
-    double w = (double)lb[i] - sm;
-    // the nf fastest centroids (excluded from sm): the better of Elkan's
-    // bound through the label, |x - c_f'| >= |c_l' - c_f'| - |x - c_l'| >=
-    // cc[l][f] - u, and the moved lower bound lb - s_f
-    if (l >= 0 && nf > 0 && w > 0.0) {   // (w <= 0: active anyway)
-      const double lb0 = (double)lb[i];
-      // cheap form first: every fast centroid is at least cmin[l] from the
-      // label and moved at most s_F = max_f s_f
-      const double wc = fmin(w, fmax((double)cc[(size_t)k * nf + l] - u, lb0 - sf_s[nf]));
-      if (wc > 0.0 && wc * wc - u * u > delta * (1.0 + 1e-9) + 1e-30) {
-        w = wc;
-      } else {   // per fast centroid (tighter)
-        const float* cl = cc + (size_t)l * nf;
-        if ((nf & 3) == 0) {
-          for (int f = 0; f < nf; f += 4) {
-            const float4 c4 = *reinterpret_cast<const float4*>(cl + f);
-            w = fmin(w, fmax((double)c4.x - u, lb0 - sf_s[f]));
-            w = fmin(w, fmax((double)c4.y - u, lb0 - sf_s[f + 1]));
-            w = fmin(w, fmax((double)c4.z - u, lb0 - sf_s[f + 2]));
-            w = fmin(w, fmax((double)c4.w - u, lb0 - sf_s[f + 3]));
+    const int mf = mflag[i];
+    // the moved lower bound lb0 -> w (every centroid except the label)
+    auto wbound = [&](double lb0) -> double {
+      double w = lb0 - sm;
+      // the nf fastest centroids (excluded from sm): the better of Elkan's
+      // bound through the label, |x - c_f'| >= |c_l' - c_f'| - |x - c_l'| >=
+      // cc[l][f] - u, and the moved lower bound lb - s_f
+      if (l >= 0 && nf > 0 && w > 0.0) {   // (w <= 0: active anyway)
+        // cheap form first: every fast centroid is at least cmin[l] from the
+        // label and moved at most s_F = max_f s_f
+        const double wc = fmin(w, fmax((double)cc[(size_t)k * nf + l] - u, lb0 - sf_s[nf]));
+        if (wc > 0.0 && wc * wc - u * u > delta * (1.0 + 1e-9) + 1e-30) {
+          w = wc;
+        } else {   // per fast centroid (tighter)
+          const float* cl = cc + (size_t)l * nf;
+          if ((nf & 3) == 0) {
+            for (int f = 0; f < nf; f += 4) {
+              const float4 c4 = *reinterpret_cast<const float4*>(cl + f);
+              w = fmin(w, fmax((double)c4.x - u, lb0 - sf_s[f]));
+              w = fmin(w, fmax((double)c4.y - u, lb0 - sf_s[f + 1]));
+              w = fmin(w, fmax((double)c4.z - u, lb0 - sf_s[f + 2]));
+              w = fmin(w, fmax((double)c4.w - u, lb0 - sf_s[f + 3]));
+            }
+          } else {
+            for (int f = 0; f < nf; ++f) w = fmin(w, fmax((double)cl[f] - u, lb0 - sf_s[f]));
           }
-        } else {
-          for (int f = 0; f < nf; ++f) w = fmin(w, fmax((double)cl[f] - u, lb0 - sf_s[f]));
         }
       }
-    }
-    const bool a = !(l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30);
-    if (a) {
+      return w;
+    };
+    auto holds = [&](double w) {
+      return l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30;
+    };
+    const double w = wbound((double)lb[i]);
+    if (!holds(w)) {
       act |= 1ull << p;
     } else {
       ub[i] = (float)u * (1.0f + 0x1p-22f);
       lb[i] = (float)w * (1.0f - 0x1p-22f);
-      if (mflag[i]) rec |= 1ull << p;
+      if (mf) rec |= 1ull << p;
     }
   }
   // block-wide exclusive scan of both per-thread counts (packed 16 | 16 bits:
@@ -1318,14 +1333,17 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
 //   in : D32_c + B_c <= min_j (D32_j - B_j) + delta,
 //   out: D32_c - B_c >  min_j (D32_j + B_j) + delta.
 // A row whose band is certainly {argmin} is done here (label = argmin,
-// corr = 0 - the memset value, mind = D32, ub from D32 + B); every other row
-// (a wider band: its kappa pick and correction need the exact values, or an
-// uncertain member) is flagged for recheck_rows_kernel (fp64).
-// fp32 sub/fma instead of fp64 cvt/sub/fma: the re-check is VALU bound.
+// corr = 0 - the memset value, ub from D32 + B; mind is not needed by the
+// incremental steps that run the screen); every other row (a wider band: its
+// kappa pick and correction need the exact values, or an uncertain member)
+// is flagged for recheck_rows_kernel (fp64).
+// The kernel is bound by memory transactions per row (the list entry, the
+// per-row candidate record, the row, the scattered label / bound stores),
+// not by arithmetic: loads are software-pipelined across steps.
 #ifndef SQ_SCREEN_LPR
 #define SQ_SCREEN_LPR 16
 #endif
-template <int DX, int LPR>
+template <int DX, int LPR, bool UB>
 __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
@@ -1340,57 +1358,117 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
   const long long cnt = min((long long)*multi_count, cap);
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  auto cdist32 = [&](const float4 (&xv)[F4], int j) -> float {
-    const float* cr = Cm + (size_t)j * DX;
+  // group-contiguous float4 slices of a row: coalesced
+  auto ldrow = [&](const float* r, float4 (&v)[F4]) {
+#pragma unroll
+    for (int q = 0; q < F4; ++q)
+      v[q] = (4 * (q * LPR + sub) < DX) ? *reinterpret_cast<const float4*>(r + 4 * (q * LPR + sub))
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto sqd = [&](const float4 (&xv)[F4], const float4 (&cv)[F4]) -> float {
     float s = 0.0f;
 #pragma unroll
     for (int q = 0; q < F4; ++q) {
-      if (4 * (q * LPR + sub) < DX) {   // group-contiguous float4s: coalesced
-        const float4 cv = *reinterpret_cast<const float4*>(cr + 4 * (q * LPR + sub));
-        const float e0 = xv[q].x - cv.x, e1 = xv[q].y - cv.y;
-        const float e2 = xv[q].z - cv.z, e3 = xv[q].w - cv.w;
-        s = fmaf(e0, e0, fmaf(e1, e1, fmaf(e2, e2, fmaf(e3, e3, s))));
-      }
+      const float e0 = xv[q].x - cv[q].x, e1 = xv[q].y - cv[q].y;
+      const float e2 = xv[q].z - cv[q].z, e3 = xv[q].w - cv[q].w;
+      s = fmaf(e0, e0, fmaf(e1, e1, fmaf(e2, e2, fmaf(e3, e3, s))));
     }
     return s;
   };
   // each wave walks a CONTIGUOUS slice of the list (rows in ascending
-  // order within a 4K-row chunk): few pages of X live per CU at a time
+  // order within a 4K-row chunk): few pages of X live per CU at a time.
+  // Three-stage software pipeline over the wave's steps (RPW rows each) -
+  // the list entry of step s + 2, the candidate list and the row of step
+  // s + 1 and the first two candidate centroids of step s + 1 are in flight
+  // while step s computes (the chain list -> candidates -> centroid rows was
+  // three dependent memory latencies per step)
   const long long per = ((cnt + nw - 1) / nw + RPW - 1) / RPW * RPW;
+  const long long e_beg = gw * per;
   const long long e_end = min(cnt, (gw + 1) * per);
-  for (long long base = gw * per; base < e_end; base += RPW) {
+  if (e_beg >= e_end) return;
+  // every load below is unconditional (clamped to a valid entry / record;
+  // the values are masked afterwards): a load under a data-dependent branch
+  // makes the compiler drain vmcnt(0) - the whole pipeline - before it
+  // entries past the wave's slice mirror its last entry: the same inputs give
+  // the same results, so the stores below can be unconditional (identical
+  // values to identical addresses) - no exec-masked store, exact vmcnt counts
+  auto load_g = [&](long long base) -> long long {
     const long long e = base + lane / LPR;
-    const bool live = e < e_end;
-    const long long g = live ? mrows[e] : 0;
-    const int* mc = mcand + g * (kMaxCand + 1);
-    const int c_r = live ? mc[0] : 0;
+    return mrows[e < e_end ? e : e_end - 1];
+  };
+  struct Rw {
+    long long g;
+    int c_r, myj, j0, j1;   // raw record words: masked by c_r at use
+  };
+  auto load_c = [&](long long g) -> Rw {
+    Rw r;
+    r.g = g;
+    const int* mc = mcand + (g >= 0 ? g : 0) * (kMaxCand + 1);
+    r.c_r = mc[0];
+    r.myj = mc[1 + sub];
+    r.j0 = mc[1];
+    r.j1 = mc[2];
+    return r;
+  };
+  auto fix = [&](Rw& r) {   // once the record has landed
+    r.c_r = r.g >= 0 ? min(max(r.c_r, 0), kMaxCand) : 0;
+    r.myj = sub < r.c_r ? r.myj : 0;
+    r.j0 = r.c_r > 0 ? r.j0 : 0;
+    r.j1 = r.c_r > 1 ? r.j1 : r.j0;
+  };
+  // two register sets (A: the step being computed, B: the next step's loads)
+  // swap roles every step; the loop is unrolled by two so no register copy
+  // (a copy of a loaded register waits for its load) sits between steps
+  float4 xA[F4], c0A[F4], c1A[F4], xB[F4], c0B[F4], c1B[F4];
+  // list entries run two steps ahead of the candidate records: the entry a
+  // step's record load needs was issued a whole step of unconditional loads
+  // earlier, so its vmcnt wait does not cover the previous step's
+  // (conditional) stores
+  long long g2 = load_g(e_beg + RPW), g3 = load_g(e_beg + 2 * RPW);
+  Rw rA = load_c(load_g(e_beg)), rB;
+  fix(rA);
+  ldrow(X + (size_t)(rA.g >= 0 ? rA.g : 0) * DX, xA);
+  ldrow(Cm + (size_t)rA.j0 * DX, c0A);
+  ldrow(Cm + (size_t)rA.j1 * DX, c1A);
+  auto step = [&](long long base, Rw& cur, const float4 (&xv)[F4], const float4 (&c0)[F4],
+                  const float4 (&c1)[F4], Rw& nxt, float4 (&xn_)[F4], float4 (&c0n)[F4],
+                  float4 (&c1n)[F4]) {
+    // stage 1 / 2 for the next steps
+    const long long g4 = load_g(base + 3 * RPW);
+    nxt = load_c(g2);
+    ldrow(X + (size_t)(nxt.g >= 0 ? nxt.g : 0) * DX, xn_);
+    // ---- step base: the candidates' fp32 squared distances
+    const long long e = min(base + lane / LPR, e_end - 1);
+    const bool live = true;
+    const long long g = cur.g;
+    const int c_r = cur.c_r;
     const bool fits = c_r <= LPR;   // one candidate per lane of the group
     const bool mine = sub < c_r;
-    const int myj = mine ? mc[1 + sub] : 0;
-    float4 xv[F4];
-    const float* xr = X + (size_t)g * DX;
-#pragma unroll
-    for (int q = 0; q < F4; ++q)
-      xv[q] = (4 * (q * LPR + sub) < DX)
-                  ? *reinterpret_cast<const float4*>(xr + 4 * (q * LPR + sub))
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
     int cmax = c_r;
 #pragma unroll
     for (int o = LPR; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
     cmax = min(cmax, LPR);
-    float dme = __builtin_inff();
-    for (int c = 0; c < cmax; c += 2) {
-      const int j0 = __shfl(myj, gbase + c, 64);
-      const int j1 = __shfl(myj, gbase + min(c + 1, LPR - 1), 64);
-      float s0 = cdist32(xv, c < c_r ? j0 : 0);
-      float s1 = cdist32(xv, c + 1 < c_r ? j1 : 0);
+    float s0 = sqd(xv, c0), s1 = sqd(xv, c1);
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+    }
+    float dme = sub == 0 ? s0 : (sub == 1 ? s1 : __builtin_inff());
+    for (int c = 2; c < cmax; c += 2) {   // rows with more than two candidates (rare)
+      const int ja = __shfl(cur.myj, gbase + c, 64);
+      const int jb = __shfl(cur.myj, gbase + min(c + 1, LPR - 1), 64);
+      float4 ca[F4], cb[F4];
+      ldrow(Cm + (size_t)(c < c_r ? ja : 0) * DX, ca);
+      ldrow(Cm + (size_t)(c + 1 < c_r ? jb : 0) * DX, cb);
+      float sa = sqd(xv, ca), sb = sqd(xv, cb);
 #pragma unroll
       for (int o = 1; o < LPR; o <<= 1) {
-        s0 += __shfl_xor(s0, o, 64);
-        s1 += __shfl_xor(s1, o, 64);
+        sa += __shfl_xor(sa, o, 64);
+        sb += __shfl_xor(sb, o, 64);
       }
-      if (sub == c) dme = s0;
-      if (sub == c + 1) dme = s1;
+      if (sub == c) dme = sa;
+      if (sub == c + 1) dme = sb;
     }
     const double B = (double)dme * 0x1p-18 + 1e-30;
     const double lo = mine ? (double)dme - B : 1e300, hi = mine ? (double)dme + B : 1e300;
@@ -1407,16 +1485,33 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const bool unsure = !fits || (__ballot(mine && !cin && !cout) & gmask) != 0;
     const bool done = live && !unsure && __popcll(inm) == 1;
     const int plane = inm ? __ffsll((long long)inm) - 1 : gbase;
-    const int pick = __shfl(myj, plane, 64);
-    const float dpick = __shfl(dme, plane, 64);
+    const int pick = __shfl(cur.myj, plane, 64);
     const double hpick = __shfl(hi, plane, 64);
-    if (done && sub == 0) {
-      labels[g] = pick;
-      mind[g] = dpick;
-      if (ub) ub[g] = (float)sqrt(hpick) * (1.0f + 0x1p-20f);
-    }
+    fix(nxt);
+    // stage 3 for the next step (its first two candidate centroids) BEFORE
+    // this step's stores: vmcnt retires in issue order, so a load issued
+    // after the scattered stores would make the next step wait for them
+    ldrow(Cm + (size_t)nxt.j0 * DX, c0n);
+    ldrow(Cm + (size_t)nxt.j1 * DX, c1n);
+    __builtin_amdgcn_sched_barrier(0);
+    // every lane of the group stores its row's values unconditionally: a row
+    // that is not done gets placeholder values that recheck_rows_kernel
+    // overwrites (it rewrites labels / mind / ub of every flagged row).  No
+    // mind store: the screen runs only in incremental steps, whose inertia
+    // comes from the cluster statistics and the corrections (each scattered
+    // 4-B store is one more memory transaction per row - the kernel's bound)
+    labels[g] = pick;
+    if constexpr (UB) ub[g] = (float)sqrt(hpick) * (1.0f + 0x1p-20f);
     // the rest -> flagged for the fp64 pass (a per-entry byte: no atomics)
-    if (live && sub == 0) xflag[e] = done ? 0 : 1;
+    xflag[e] = done ? 0 : 1;
+    __builtin_amdgcn_sched_barrier(0);
+    g2 = g3;
+    g3 = g4;
+  };
+  for (long long base = e_beg; base < e_end; base += 2 * RPW) {
+    step(base, rA, xA, c0A, c1A, rB, xB, c0B, c1B);
+    if (base + RPW >= e_end) break;
+    step(base + RPW, rB, xB, c0B, c1B, rA, xA, c0A, c1A);
   }
 }
 
@@ -1475,11 +1570,28 @@ __global__ void __launch_bounds__(256) fill_mind_kernel(const float* __restrict_
 __global__ void __launch_bounds__(256) sum_f32_blocks_kernel(const float* __restrict__ v,
                                                              long long n, double* __restrict__ part) {
   __shared__ double red[256];
-  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  // block ranges in whole 1024-float pieces (16-B aligned float4 loads; v is
+  // a 256-B aligned allocation), 4 independent float4 loads in flight per
+  // thread; fixed association (deterministic)
+  const long long per = (n + (long long)gridDim.x * 1024 - 1) / ((long long)gridDim.x * 1024) * 1024;
   const long long b = (long long)blockIdx.x * per, e = min(n, b + per);
-  double s = 0.0;
-  for (long long i = b + threadIdx.x; i < e; i += 256) s += (double)v[i];
-  red[threadIdx.x] = s;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  const long long e4 = b < e ? b + (e - b) / 4 * 4 : b;
+  const float4* v4 = reinterpret_cast<const float4*>(v);
+  long long i = b / 4 + threadIdx.x;
+  for (; i + 768 < e4 / 4; i += 1024) {
+    const float4 a = v4[i], c = v4[i + 256], f = v4[i + 512], g = v4[i + 768];
+    s0 += ((double)a.x + (double)a.y) + ((double)a.z + (double)a.w);
+    s1 += ((double)c.x + (double)c.y) + ((double)c.z + (double)c.w);
+    s2 += ((double)f.x + (double)f.y) + ((double)f.z + (double)f.w);
+    s3 += ((double)g.x + (double)g.y) + ((double)g.z + (double)g.w);
+  }
+  for (; i < e4 / 4; i += 256) {
+    const float4 a = v4[i];
+    s0 += ((double)a.x + (double)a.y) + ((double)a.z + (double)a.w);
+  }
+  for (long long t = e4 + threadIdx.x; t < e; t += 256) s1 += (double)v[t];
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
@@ -1604,7 +1716,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   constexpr int NW = kX64Waves;
   constexpr int RS = X64RowSets<KSD>::value;
   const size_t lds =
-      kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * RS * 32 * (kMaxCand + 1) * 4;
+      kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * RS * 32 * (kMaxCand + 1) * 4 +
+      (size_t)NW * 64 * 4;   // + per-lane dump slots
   auto kern = estep_x64_kernel<KSD, RS>;
   static bool attr = false;
   if (!attr) {
@@ -1637,11 +1750,22 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   // with xrows the fp32 screen first, the fp64 pass over what it left
   const long long rblocks = (n / 16 + 63) / 64;
   const unsigned rgrid = (unsigned)(rblocks < 4096 ? (rblocks > 0 ? rblocks : 1) : 4096);
-  if (xflag)
-    hipLaunchKernelGGL((recheck_fast_kernel<KSD * 16, SQ_SCREEN_LPR>), dim3(rgrid), dim3(256), 0, st,
-                       (const float*)X, (const float*)Cm, (const long long*)mrows,
-                       (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
-                       delta, (float*)ub, (unsigned char*)xflag);
+  if (xflag) {
+    // one resident round of long-lived waves (each walks its slice with the
+    // load pipeline warm) instead of several rounds of short ones
+    static int sgrid = 0;
+    if (sgrid == 0) {
+      const char* e = getenv("SQ_SCREEN_GRID");
+      sgrid = e ? atoi(e) : 1024;
+      if (sgrid <= 0) sgrid = 4096;
+    }
+    const unsigned fgrid2 = (unsigned)(rblocks < sgrid ? (rblocks > 0 ? rblocks : 1) : sgrid);
+    auto fk = ub ? recheck_fast_kernel<KSD * 16, SQ_SCREEN_LPR, true>
+                 : recheck_fast_kernel<KSD * 16, SQ_SCREEN_LPR, false>;
+    hipLaunchKernelGGL(fk, dim3(fgrid2), dim3(256), 0, st, (const float*)X, (const float*)Cm,
+                       (const long long*)mrows, (const int*)mcand, (const int*)multi_count,
+                       (int*)labels, (float*)mind, n, delta, (float*)ub, (unsigned char*)xflag);
+  }
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,
                      (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
@@ -1790,7 +1914,7 @@ int sq_fill_mind(const void* X, int ldx, const void* Cm, int d, const void* labe
 int sq_sum_f32(const void* v, long long n, void* part, int extra, void* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int blocks = 512;
-  if (extra < 0) return (int)hipErrorInvalidValue;
+  if (extra < 0 || ((uintptr_t)v & 15u) != 0) return (int)hipErrorInvalidValue;   // float4 loads
   hipLaunchKernelGGL(sum_f32_blocks_kernel, dim3(blocks), dim3(256), 0, st, (const float*)v, n,
                      (double*)part);
   return sq_sum_partials(part, blocks + extra, out, st);

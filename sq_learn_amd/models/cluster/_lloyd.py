@@ -306,7 +306,8 @@ class LloydEngine:
                                                self.row_offset, self.buf,
                                                bounds=(self.ub, self.lb) if self.bounds else None,
                                                rows=rows, zero_counts=rows is None,
-                                               screen=self.incremental and not full)
+                                               screen=self.incremental and not full
+                                               and os.environ.get("SQ_SCREEN", "1") != "0")
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):
