@@ -1114,10 +1114,16 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(rcount, 0, sizeof(int), st);
-  const bool big = n >= 4096LL * 1024;
-  const long long chunk = big ? 4096 : 1024;
-  const long long blocks = (n + chunk - 1) / chunk;
-  hipLaunchKernelGGL(big ? bounds_filter_kernel<16> : bounds_filter_kernel<4>, dim3((unsigned)blocks),
+  // rows per thread: the smallest PER whose grid fits ONE resident round
+  // (8 workgroups of 256 threads per CU at 62 VGPRs, 256 CUs): a second,
+  // mostly empty round doubled the kernel at 10M rows (2442 blocks of 4096)
+  auto pick = [&](int per) { return (n + per * 256LL - 1) / (per * 256LL) <= 2048; };
+  const int per = pick(4) ? 4 : pick(8) ? 8 : pick(16) ? 16 : pick(20) ? 20 : pick(32) ? 32 : 64;
+  const long long blocks = (n + per * 256LL - 1) / (per * 256LL);
+  auto kern = per == 4 ? bounds_filter_kernel<4> : per == 8 ? bounds_filter_kernel<8>
+            : per == 16 ? bounds_filter_kernel<16> : per == 20 ? bounds_filter_kernel<20>
+            : per == 32 ? bounds_filter_kernel<32> : bounds_filter_kernel<64>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks),
                      dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
                      (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
                      (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
@@ -1713,37 +1719,52 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
                             void* ub, void* lb, void* mflag, void* xflag) {
-  constexpr int NW = kX64Waves;
-  constexpr int RS = X64RowSets<KSD>::value;
-  const size_t lds =
-      kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * RS * 32 * (kMaxCand + 1) * 4 +
-      (size_t)NW * 64 * 4;   // + per-lane dump slots
-  auto kern = estep_x64_kernel<KSD, RS>;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  static int resident = 0;
-  if (resident == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NW * 64, lds);
-    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
-  }
+  // list mode (the rows the bounds could not prune): one row set per wave -
+  // half the rows per workgroup, so a short list (the per-GPU share of a
+  // strong-scaled run) finishes in one half-length sweep; a full sweep keeps
+  // the two row sets that halve the centroid staging per row
   int qbits = 1;
   while ((1 << qbits) < 2 * (k_pad / kTileN)) ++qbits;
-  const long long nblk = (n + NW * 32 * RS - 1) / (NW * 32 * RS);
-  // list mode: the row count is on the device - every resident slot launches
-  const unsigned grid = (unsigned)(nblk < resident && !rlist ? nblk : resident);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const _Float16*)Xh,
-                     (const float*)X, (const _Float16*)C, (const float*)Cm, (const float*)xn,
-                     (const float*)cmax2, (int*)labels, (float*)mind, (long long*)dense_rows,
-                     (int*)dense_count, (long long*)mrows, (int*)mcand, (int*)multi_count, n,
-                     k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits,
-                     (const long long*)rlist, (const int*)rcount, (float*)ub, (float*)lb,
-                     (int*)mflag);
+  auto go = [&](auto RS_) {
+    constexpr int RS = decltype(RS_)::value;
+    constexpr int NW = kX64Waves;
+    const size_t lds =
+        kX64Ring * (size_t)X64Geom<KSD>::SLOT + (size_t)NW * RS * 32 * (kMaxCand + 1) * 4 +
+        (size_t)NW * 64 * 4;   // + per-lane dump slots
+    auto kern = estep_x64_kernel<KSD, RS>;
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024);
+      attr = true;
+    }
+    static int resident = 0;
+    if (resident == 0) {
+      int dev = 0, cus = 0, per_cu = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NW * 64, lds);
+      resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+    }
+    const long long nblk = (n + NW * 32 * RS - 1) / (NW * 32 * RS);
+    // list mode: the row count is on the device - every resident slot launches
+    const unsigned grid = (unsigned)(nblk < resident && !rlist ? nblk : resident);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, (const _Float16*)Xh,
+                       (const float*)X, (const _Float16*)C, (const float*)Cm, (const float*)xn,
+                       (const float*)cmax2, (int*)labels, (float*)mind, (long long*)dense_rows,
+                       (int*)dense_count, (long long*)mrows, (int*)mcand, (int*)multi_count, n,
+                       k_pad, alpha, delta_s, key, row_offset, dense_cap, qbits,
+                       (const long long*)rlist, (const int*)rcount, (float*)ub, (float*)lb,
+                       (int*)mflag);
+  };
+  static const bool list_rs1 = [] {
+    const char* e = getenv("SQ_X64_LIST_RS1");
+    return !(e && e[0] == '0');
+  }();
+  if (rlist && list_rs1)
+    go(std::integral_constant<int, 1>{});
+  else
+    go(std::integral_constant<int, X64RowSets<KSD>::value>{});
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   // the re-check: one pass over the multi list (count read on the device);

@@ -8,6 +8,8 @@ functions return *local* (per-shard) partial results; callers reduce them
 across ranks with one collective.
 """
 
+import os
+
 import torch
 
 from . import _native as nat
@@ -36,7 +38,10 @@ def row_norms_sq(X, out=None):
 # ------------------------------------------------ fp64-MFMA tall-skinny GEMMs
 _XTX_TARGET_WGS = 1024        # 2-3 resident workgroups per CU (LDS-bound), 256 CUs
 _XTX_MAX_SPLITS = 512
-_CHUNK_BYTES = 4 << 30        # fp64 row-chunk buffers of the two-kernel passes
+# fp64 row-chunk buffers of the two-kernel passes (X W into a chunk, then the
+# chunk's Gram): 128 MiB chunks stay in the 256 MB Infinity Cache between the
+# producing and the consuming kernel instead of a round trip through HBM
+_CHUNK_BYTES = int(os.environ.get("SQ_CHUNK_MB", "128")) << 20
 _part_cache = {}
 
 
