@@ -1354,7 +1354,7 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
     float* __restrict__ mind, long long cap, double delta, float* __restrict__ ub,
-    unsigned char* __restrict__ xflag) {
+    unsigned char* __restrict__ xflag, int il) {
   constexpr int RPW = 64 / LPR;   // rows per wave step
   constexpr int FPL = DX / LPR;
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
@@ -1388,20 +1388,27 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
   // s + 1 and the first two candidate centroids of step s + 1 are in flight
   // while step s computes (the chain list -> candidates -> centroid rows was
   // three dependent memory latencies per step)
+  // step s of a wave covers RPW list entries: a contiguous slice per wave
+  // (il = 0), or interleaved - step s of every wave inside one window of
+  // nw * RPW entries (il = 1: the rows in flight chip-wide stay within a few
+  // MB of X and of the candidate records, TLB locality)
   const long long per = ((cnt + nw - 1) / nw + RPW - 1) / RPW * RPW;
   const long long e_beg = gw * per;
-  const long long e_end = min(cnt, (gw + 1) * per);
-  if (e_beg >= e_end) return;
+  const long long lim = il ? cnt : min(cnt, (gw + 1) * per);
+  const long long nsteps = il ? (gw * RPW < cnt ? (cnt - gw * RPW + nw * RPW - 1) / (nw * RPW) : 0)
+                              : (e_beg < lim ? (lim - e_beg + RPW - 1) / RPW : 0);
+  if (nsteps <= 0) return;
+  auto entry = [&](long long st) -> long long {
+    const long long e = (il ? (st * nw + gw) * RPW : e_beg + st * RPW) + lane / LPR;
+    return e < lim ? e : lim - 1;
+  };
   // every load below is unconditional (clamped to a valid entry / record;
   // the values are masked afterwards): a load under a data-dependent branch
   // makes the compiler drain vmcnt(0) - the whole pipeline - before it
   // entries past the wave's slice mirror its last entry: the same inputs give
   // the same results, so the stores below can be unconditional (identical
   // values to identical addresses) - no exec-masked store, exact vmcnt counts
-  auto load_g = [&](long long base) -> long long {
-    const long long e = base + lane / LPR;
-    return mrows[e < e_end ? e : e_end - 1];
-  };
+  auto load_g = [&](long long st) -> long long { return mrows[entry(st)]; };
   struct Rw {
     long long g;
     int c_r, myj, j0, j1;   // raw record words: masked by c_r at use
@@ -1430,21 +1437,21 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
   // step's record load needs was issued a whole step of unconditional loads
   // earlier, so its vmcnt wait does not cover the previous step's
   // (conditional) stores
-  long long g2 = load_g(e_beg + RPW), g3 = load_g(e_beg + 2 * RPW);
-  Rw rA = load_c(load_g(e_beg)), rB;
+  long long g2 = load_g(1), g3 = load_g(2);
+  Rw rA = load_c(load_g(0)), rB;
   fix(rA);
   ldrow(X + (size_t)(rA.g >= 0 ? rA.g : 0) * DX, xA);
   ldrow(Cm + (size_t)rA.j0 * DX, c0A);
   ldrow(Cm + (size_t)rA.j1 * DX, c1A);
-  auto step = [&](long long base, Rw& cur, const float4 (&xv)[F4], const float4 (&c0)[F4],
+  auto step = [&](long long st, Rw& cur, const float4 (&xv)[F4], const float4 (&c0)[F4],
                   const float4 (&c1)[F4], Rw& nxt, float4 (&xn_)[F4], float4 (&c0n)[F4],
                   float4 (&c1n)[F4]) {
     // stage 1 / 2 for the next steps
-    const long long g4 = load_g(base + 3 * RPW);
+    const long long g4 = load_g(st + 3);
     nxt = load_c(g2);
     ldrow(X + (size_t)(nxt.g >= 0 ? nxt.g : 0) * DX, xn_);
     // ---- step base: the candidates' fp32 squared distances
-    const long long e = min(base + lane / LPR, e_end - 1);
+    const long long e = entry(st);
     const bool live = true;
     const long long g = cur.g;
     const int c_r = cur.c_r;
@@ -1514,10 +1521,10 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     g2 = g3;
     g3 = g4;
   };
-  for (long long base = e_beg; base < e_end; base += 2 * RPW) {
-    step(base, rA, xA, c0A, c1A, rB, xB, c0B, c1B);
-    if (base + RPW >= e_end) break;
-    step(base + RPW, rB, xB, c0B, c1B, rA, xA, c0A, c1A);
+  for (long long st = 0; st < nsteps; st += 2) {
+    step(st, rA, xA, c0A, c1A, rB, xB, c0B, c1B);
+    if (st + 1 >= nsteps) break;
+    step(st + 1, rB, xB, c0B, c1B, rA, xA, c0A, c1A);
   }
 }
 
@@ -1774,8 +1781,10 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   if (xflag) {
     // one resident round of long-lived waves (each walks its slice with the
     // load pipeline warm) instead of several rounds of short ones
-    static int sgrid = 0;
+    static int sgrid = 0, sil = 0;
     if (sgrid == 0) {
+      const char* ei = getenv("SQ_SCREEN_IL");
+      sil = ei ? atoi(ei) : 0;
       const char* e = getenv("SQ_SCREEN_GRID");
       sgrid = e ? atoi(e) : 1024;
       if (sgrid <= 0) sgrid = 4096;
@@ -1785,7 +1794,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                  : recheck_fast_kernel<KSD * 16, SQ_SCREEN_LPR, false>;
     hipLaunchKernelGGL(fk, dim3(fgrid2), dim3(256), 0, st, (const float*)X, (const float*)Cm,
                        (const long long*)mrows, (const int*)mcand, (const int*)multi_count,
-                       (int*)labels, (float*)mind, n, delta, (float*)ub, (unsigned char*)xflag);
+                       (int*)labels, (float*)mind, n, delta, (float*)ub, (unsigned char*)xflag,
+                       sil);
   }
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,
