@@ -161,11 +161,19 @@ class BaseForest(BaseEstimator):
         split_seeds = [check_random_state(s).randint(0, RAND_R_MAX) for s in tree_seeds]
         n_threads = 0 if self.n_jobs in (None, -1) else max(1, int(self.n_jobs))
         if weights is not None and np.any(mwl != mwl[0]):
-            fitted = []
-            for j in range(len(trees)):
-                params["min_weight_leaf"] = mwl[j]
-                fitted += build_trees(X, y, weights[j:j + 1], n_classes, params,
-                                      split_seeds[j:j + 1], n_threads=1)
+            # per-tree leaf-weight floors: one native build per tree, fanned
+            # out over the task layer (reference ``_forest.py:396``
+            # ``Parallel(n_jobs, prefer="threads")``; the ctypes build releases
+            # the GIL, so worker threads run the trees concurrently)
+            from ...parallel.tasks import Parallel
+            from ...utils.fixes import delayed
+
+            def one(j):
+                pj = dict(params, min_weight_leaf=mwl[j])
+                return build_trees(X, y, weights[j:j + 1], n_classes, pj, split_seeds[j:j + 1],
+                                   n_threads=1)[0]
+
+            fitted = Parallel(n_jobs=self.n_jobs)(delayed(one)(j) for j in range(len(trees)))
         else:
             if weights is not None:
                 params["min_weight_leaf"] = float(mwl[0])

@@ -101,3 +101,18 @@ def test_parallel_backend_context_and_registry():
         with parallel_backend("no_such_backend"):
             pass
     assert issubclass(DataConversionWarning, UserWarning)
+
+
+def test_forest_per_tree_builds_fan_out_identically():
+    """Bootstrap + min_weight_fraction_leaf gives every tree its own leaf
+    weight floor: one native build per tree over the task layer
+    (reference ``ensemble/_forest.py:396``); n_jobs must not change a tree."""
+    import numpy as np
+    from sq_learn_amd.models.ensemble._forest import RandomForestClassifier
+    X = np.random.RandomState(0).randn(400, 6)
+    y = (X[:, 0] + X[:, 1] > 0).astype(int)
+    kw = dict(n_estimators=6, min_weight_fraction_leaf=0.05, random_state=0)
+    a = RandomForestClassifier(n_jobs=1, **kw).fit(X, y)
+    b = RandomForestClassifier(n_jobs=3, **kw).fit(X, y)
+    np.testing.assert_array_equal(a.predict_proba(X), b.predict_proba(X))
+    assert [e.tree_.node_count for e in a.estimators_] == [e.tree_.node_count for e in b.estimators_]
