@@ -1483,23 +1483,29 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
       if (sub == c) dme = sa;
       if (sub == c + 1) dme = sb;
     }
-    const double B = (double)dme * 0x1p-18 + 1e-30;
-    const double lo = mine ? (double)dme - B : 1e300, hi = mine ? (double)dme + B : 1e300;
-    double minlo = lo, minhi = hi;
+    // fp32 interval [lo, hi] around the exact D: the distance bound is
+    // 2^-18 D; 2^-16 D + 2^-20 delta also absorbs the fp32 roundings of these
+    // products and of the (min + delta) sums below (each <= 2^-24 of a
+    // magnitude <= D + delta)
+    const float dlt = (float)delta;
+    const float slack = dme * 0x1p-16f + dlt * 0x1p-20f + 1e-30f;
+    const float lo = mine ? dme - slack : __builtin_inff();
+    const float hi = mine ? dme + slack : __builtin_inff();
+    float minlo = lo, minhi = hi;
 #pragma unroll
     for (int o = 1; o < LPR; o <<= 1) {
-      minlo = fmin(minlo, __shfl_xor(minlo, o, 64));
-      minhi = fmin(minhi, __shfl_xor(minhi, o, 64));
+      minlo = fminf(minlo, __shfl_xor(minlo, o, 64));
+      minhi = fminf(minhi, __shfl_xor(minhi, o, 64));
     }
-    const bool cin = mine && hi <= minlo + delta;
-    const bool cout = mine && lo > minhi + delta;
+    const bool cin = mine && hi <= minlo + dlt;
+    const bool cout = mine && lo > minhi + dlt;
     const unsigned long long gmask = ((1ull << LPR) - 1ull) << gbase;
     const unsigned long long inm = __ballot(cin) & gmask;
     const bool unsure = !fits || (__ballot(mine && !cin && !cout) & gmask) != 0;
     const bool done = live && !unsure && __popcll(inm) == 1;
     const int plane = inm ? __ffsll((long long)inm) - 1 : gbase;
     const int pick = __shfl(cur.myj, plane, 64);
-    const double hpick = __shfl(hi, plane, 64);
+    const float hpick = __shfl(hi, plane, 64);
     fix(nxt);
     // stage 3 for the next step (its first two candidate centroids) BEFORE
     // this step's stores: vmcnt retires in issue order, so a load issued
@@ -1514,7 +1520,7 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     // comes from the cluster statistics and the corrections (each scattered
     // 4-B store is one more memory transaction per row - the kernel's bound)
     labels[g] = pick;
-    if constexpr (UB) ub[g] = (float)sqrt(hpick) * (1.0f + 0x1p-20f);
+    if constexpr (UB) ub[g] = sqrtf(hpick) * (1.0f + 0x1p-20f);
     // the rest -> flagged for the fp64 pass (a per-entry byte: no atomics)
     xflag[e] = done ? 0 : 1;
     __builtin_amdgcn_sched_barrier(0);
