@@ -329,6 +329,10 @@ def main(argv=None):
         labels, sc = eng.step()
         return sc.tolist()          # convergence read-back, as in fit()
 
+    # as in QMeans.fit: the next iteration's E-step is enqueued before the
+    # read-back (LloydEngine.pipeline)
+    eng.pipeline = True
+
     for _ in range(a.warmup):
         step()
     comm.barrier()
@@ -347,6 +351,8 @@ def main(argv=None):
              "delta": a.delta, "k": a.k, "d": a.d,
              "precision": ("certified fp64 delta-band labels (fp16 MFMA filter + fp64 re-check)"
                            if a.dtype == "fp32" else "bf16 operands (approximate band edges)")}
+    eng.pipeline = False
+    eng.drop_pending()
     if eng.fast and gpu:
         cnt = eng.buf.counts.tolist()
         extra["overflow_rows_last"], extra["dense_rows_last"] = int(cnt[0]), int(cnt[1])

@@ -47,6 +47,21 @@ from ...parallel.comm import Comm
 from ...utils import tracing
 
 
+class _HostScalars:
+    """The iteration's scalars in pinned host memory, valid once ``event``
+    has completed (pipelined steps: the read must not wait for the next
+    iteration's E-step, already enqueued behind the copy)."""
+
+    __slots__ = ("host", "event")
+
+    def __init__(self, host, event):
+        self.host, self.event = host, event
+
+    def tolist(self):
+        self.event.synchronize()
+        return self.host.tolist()
+
+
 class LloydEngine:
     def __init__(self, X, k, *, delta=0.0, true_distance_estimate=False, intermediate_error=False,
                  true_tomography=False, tomography_kw=None, sample_weight=None, seed=0,
@@ -72,6 +87,14 @@ class LloydEngine:
         self.d_pad = K.pad_features(self.d)
         self.restart = 0
         self.it = 0
+        # pipeline: step() enqueues the NEXT iteration's E-step right after
+        # its M-step (same key, same order of device work), so the GPU has
+        # work while the host reads the iteration's scalars and re-enters the
+        # loop (no per-iteration bubble); opt-in by the loop owner
+        self.pipeline = False
+        self._pending = None
+        self._label_snap = None
+        self._sc_ring = None
         self.relocate_empty = bool(relocate_empty)
         self.n_relocated = 0
         self.failure_prob = float(failure_prob or 0.0)
@@ -236,7 +259,14 @@ class LloydEngine:
         return RngKey(self.seed, purpose, (self.restart << 24) | (it & 0xFFFFFF))
 
     # ---------------------------------------------------------- state
+    def drop_pending(self):
+        """Forget a speculative next-iteration E-step (its device work has
+        run; re-running that E-step is exact: bounds moved twice stay valid
+        bounds, every processed row gets the same label)."""
+        self._pending = None
+
     def set_centers(self, C):
+        self._pending = None
         C = C.to(self.device)
         self.inc_valid = False   # the incremental M-step restarts from scratch
         self.bounds_valid = False
@@ -267,6 +297,7 @@ class LloydEngine:
         return {"C_bf16": self.C_bf16, "cn": self.cn}
 
     def restore_tensors(self, d):
+        self._pending = None
         self.inc_valid = False
         self.bounds_valid = False
         if self.fast and self.C_op is not None and "C_op" in d:
@@ -279,6 +310,7 @@ class LloydEngine:
     def estep(self, C=None):
         """Labels and min distances for the current (or given) centres;
         returns (labels, mind, local_inertia_tensor)."""
+        self._pending = None
         if C is not None:
             self.set_centers(C)
         lab, mind, inertia = self._estep(self._key("band_select"), full=True)
@@ -578,6 +610,7 @@ class LloydEngine:
         all-reduce, finalize; plus the host wall of the whole step including
         the scalar read-back.  Returns {phase: ms}."""
         import time
+        self._pending = None
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         t0 = time.perf_counter()
         ev[0].record()
@@ -664,7 +697,11 @@ class LloydEngine:
         the iteration's single device->host read carries the number of
         empty clusters of the M-step's (global) counts as well, and only when
         it is non-zero is the M-step re-run after the relocation."""
-        labels, mind, inertia = self._estep(self._key("band_select"))
+        if self._pending is not None:
+            labels, mind, inertia = self._pending
+            self._pending = None
+        else:
+            labels, mind, inertia = self._estep(self._key("band_select"))
         if self.failure_prob > 0:
             # SURVEY.md §5.3: Bernoulli estimation failures (+ resampling)
             failure_inject_(labels, self.k, self.failure_prob, self.failure_attempts,
@@ -682,4 +719,22 @@ class LloydEngine:
                                   torch.zeros(1, dtype=torch.float64, device=sc.device)]).cpu()
             sc = vals
         self.it += 1
+        if self.pipeline and self.fast and not self.relocate_empty:
+            # the iteration's scalars go to pinned host memory BEFORE the next
+            # E-step is enqueued (a plain .tolist() would wait for that E-step
+            # too); the caller's .tolist() waits on this event only
+            if self._sc_ring is None:
+                self._sc_ring = [(torch.empty(sc.numel(), dtype=sc.dtype, pin_memory=True),
+                                  torch.cuda.Event()) for _ in range(2)]
+            host, ev = self._sc_ring[self.it & 1]
+            host.copy_(sc.reshape(-1), non_blocking=True)
+            ev.record()
+            # the caller keeps this iteration's labels: a device snapshot
+            # before the next E-step rewrites the buffer
+            if self._label_snap is None or self._label_snap.shape != labels.shape:
+                self._label_snap = torch.empty_like(labels)
+            self._label_snap.copy_(labels)
+            labels = self._label_snap
+            self._pending = self._estep(self._key("band_select"))
+            sc = _HostScalars(host, ev)
         return labels, sc

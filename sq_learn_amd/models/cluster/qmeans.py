@@ -339,6 +339,9 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             best_labels = resume["best_labels"].to(engine.device)
             shift = resume["shift"]
         ckpt = getattr(self, "_ckpt_ctx", {}).get("ckpt")
+        # next-iteration E-step enqueued before the scalar read (not with
+        # checkpoints: a saved state must not include a speculative E-step)
+        engine.pipeline = ckpt is None
         it = first - 1
         for it in range(first, self.max_iter):
             labels, sc = engine.step()
@@ -356,6 +359,8 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                 break
             if ckpt is not None and ckpt.due(it):
                 self._save_checkpoint(engine, it, shift, best_inertia, best_centers, best_labels)
+        engine.pipeline = False
+        engine.drop_pending()
         it = max(it, first)
         if shift > 0:
             labels, _, inertia_t = engine.estep(best_centers)
