@@ -225,6 +225,33 @@ def kmeans_parallel(data: Data, n_clusters, random_state, x_squared_norms=None, 
     return centers, None
 
 
+def permutation_head(random_state, n, k):
+    """``random_state.permutation(n)[:k]`` with the identical draws and the
+    identical generator state afterwards (the reference's 'random' init,
+    ``_kmeans.py`` ``_init_centroids``), run natively for large n
+    (``csrc/host/mt_permutation.cpp``: the legacy MT19937 Fisher-Yates pass
+    over int32 instead of numpy's over int64).  Falls back to numpy for
+    generators that are not a legacy MT19937 RandomState."""
+    n, k = int(n), int(k)
+    try:
+        st = random_state.get_state()
+    except AttributeError:
+        st = None
+    if (st is None or not isinstance(st, tuple) or st[0] != "MT19937" or n < (1 << 16)
+            or n >= (1 << 31)):
+        return random_state.permutation(n)[:k]
+    from ...ops import _host
+    key = np.array(st[1], dtype=np.uint32).copy()
+    pos = np.array([int(st[2])], dtype=np.int32)
+    out = np.empty(max(k, 1), dtype=np.int64)
+    rc = _host.lib().sqh_mt_permutation_head(_host.ptr(key), _host.ptr(pos), n, k,
+                                              _host.ptr(out))
+    if rc:
+        raise RuntimeError("sqh_mt_permutation_head failed")
+    random_state.set_state(("MT19937", key, int(pos[0]), st[3], st[4]))
+    return out[:k]
+
+
 def random_init(data: Data, n_clusters, random_state):
-    seeds = random_state.permutation(data.n_global)[:n_clusters]
+    seeds = permutation_head(random_state, data.n_global, n_clusters)
     return gather_rows(data, seeds), seeds

@@ -25,6 +25,7 @@ _F = ctypes.c_float
 
 _SIGS = {
     "sqh_murmur_i32": (None, [_P, _LL, _U, _P]),
+    "sqh_mt_permutation_head": (_I, [_P, _P, _LL, _LL, _P]),
     "sqh_murmur_bytes": (None, [_P, _P, _LL, _U, _P]),
     "sqh_hash_features": (None, [_P, _P, _P, _LL, _LL, _I, _U, _P, _P]),
     "sqh_pava_f64": (None, [_P, _P, _LL]),

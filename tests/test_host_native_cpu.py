@@ -321,3 +321,20 @@ def test_agglomerative_threshold_precomputed_and_features():
                                fb.inverse_transform(fb.transform(X)))
     with pytest.raises(ValueError):
         AgglomerativeClustering(2, linkage="ward", affinity="manhattan").fit(X)
+
+
+def test_mt_permutation_head_matches_numpy():
+    """The native head of RandomState.permutation(n): same indices and the
+    same generator state afterwards (later draws continue identically)."""
+    import numpy as np
+    from sq_learn_amd.models.cluster._init import permutation_head
+    for seed, n, k in [(0, 70000, 10), (7, 1 << 17, 1024), (123, 300001, 5), (2024, 2_000_000, 256)]:
+        a = np.random.RandomState(seed)
+        b = np.random.RandomState(seed)
+        a.rand(3)   # a stream that is not at position 0
+        b.rand(3)
+        ref = a.permutation(n)[:k]
+        got = permutation_head(b, n, k)
+        np.testing.assert_array_equal(ref, got)
+        np.testing.assert_array_equal(a.randint(0, 1 << 30, 16), b.randint(0, 1 << 30, 16))
+        assert a.rand() == b.rand()
