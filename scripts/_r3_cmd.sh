@@ -1,3 +1,5 @@
 export TMPDIR=/tmp
 scripts/gpu_steps.sh \
- "ptest|300|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_pipeline_gpu.py"
+ "gputest|700|python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread" \
+ "smoke|180|python -c \"import __graft_entry__ as g; g.smoke()\"" \
+ "bench|400|python bench.py --warmup 5"
