@@ -1,3 +1,3 @@
 export TMPDIR=/tmp
-scripts/gpu_steps.sh \
- "ab|500|for v in cur nw8 cur nw8; do echo \$v; if [ \$v = nw8 ]; then export SQ_NATIVE_VARIANT=sq_learn_amd/_variants/_C_nw8.so; else unset SQ_NATIVE_VARIANT; fi; timeout -k 10 100 python benchmarks/estep_micro.py --prec x64 --iters 5 | grep x64; done"
+rm -f gpurun_out/pmc_x64.md
+NO_TIMELINE=1 timeout -k 10 400 scripts/prof_r3.sh
