@@ -1,3 +1,5 @@
 export TMPDIR=/tmp
-rm -f gpurun_out/pmc_x64.md
-NO_TIMELINE=1 timeout -k 10 400 scripts/prof_r3.sh
+scripts/gpu_steps.sh \
+ "gputest|700|python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread" \
+ "smoke|180|python -c \"import __graft_entry__ as g; g.smoke()\"" \
+ "bench|400|python bench.py --warmup 5"
