@@ -128,9 +128,13 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
                           intermediate_error=True, true_tomography=False, seed=a.seed, comm=comm,
                           row_offset=start, gemm_precision="fp32")
         eng.set_centers(C0)
-        eng.step()[1].tolist()
         _sync(dev)
         comm.barrier()
+        t0 = time.perf_counter()
+        eng.step()[1].tolist()    # no label hints yet: the first-sweep hints
+        _sync(dev)
+        comm.barrier()
+        extra["ipe_first_step_ms"] = _max_over_ranks(comm, dev, (time.perf_counter() - t0) * 1e3)
         t0 = time.perf_counter()
         for _ in range(a.ipe_steps):
             eng.step()[1].tolist()
@@ -140,10 +144,55 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
         extra["ipe_samples_iter_per_s"] = a.n * a.ipe_steps / el
         extra["ipe_ms_per_step"] = el / a.ipe_steps * 1e3
         extra["ipe_pairs_per_s"] = a.n * a.k * a.ipe_steps / el
+        # one more (untimed) step with the screen's pair counters
+        eng.ipe_stats = torch.zeros(5, dtype=torch.int64, device=dev)
+        eng.step()[1].tolist()
+        st = eng.ipe_stats.double()
+        comm.all_reduce_(st)
+        tot = float(a.n) * a.k
+        extra["ipe_screen"] = {"screened_frac": float(st[0]) / tot,
+                               "full_sampler_frac": float(st[1]) / tot,
+                               "fires": int(st[2]), "fires_exact_branch": int(st[3]),
+                               "first_sweep_wgs": int(st[4])}
         del eng
         torch.cuda.empty_cache()
     except Exception as e:
         extra["ipe_error"] = repr(e)[:200]
+
+
+def _share8_extra(extra, a, X, comm, dev):
+    """The per-GPU share of an 8-GPU run (rows n / 8) stepped on this GPU:
+    the same pipelined, pruned, incremental headline iteration on the first
+    n / 8 rows (the N = 8 per-rank compute cost; the all-reduce is a no-op
+    here)."""
+    try:
+        from sq_learn_amd.models.cluster._lloyd import LloydEngine
+        from sq_learn_amd.models._data import Data, gather_rows
+        m = a.n // 8
+        Xs = X[:m]
+        data = Data(Xs, m, 0, comm, "sharded")
+        C0 = gather_rows(data, np.random.RandomState(a.seed).choice(m, a.k, replace=False))
+        eng = LloydEngine(Xs, a.k, delta=a.delta, true_distance_estimate=False,
+                          intermediate_error=True, true_tomography=False, seed=a.seed, comm=comm,
+                          row_offset=0, gemm_precision=a.dtype)
+        eng.set_centers(C0)
+        eng.pipeline = True
+        for _ in range(max(a.warmup, 3)):
+            eng.step()[1].tolist()
+        _sync(dev)
+        t0 = time.perf_counter()
+        steps = max(a.steps, 10)
+        for _ in range(steps):
+            eng.step()[1].tolist()
+        _sync(dev)
+        extra["share8_rows"] = m
+        extra["share8_ms_per_step"] = (time.perf_counter() - t0) / steps * 1e3
+        eng.pipeline = False
+        eng.drop_pending()
+        del eng
+        torch.cuda.empty_cache()
+    except Exception as e:
+        extra["share8_error"] = repr(e)[:200]
 
 
 def _hard_extra(extra, a, comm, dev):
@@ -261,15 +310,16 @@ def _mnist_extra(extra, a, comm, dev):
         extra["mnist_error"] = repr(e)[:200]
 
 
-def _fit_extra(extra, a, sa, comm, dev, init):
+def _fit_extra(extra, a, sa, comm, dev, init, ipe=False, name=None):
     """Wall-clock of a whole QMeans.fit (prelude: eta, mu(A), condition
     number; centring; initialisation; ``fit_iters`` Lloyd iterations with
     tol = 0; final E-step) on the same matrix (BASELINE: fit wall-clock at a
-    fixed max_iter)."""
-    name = f"fit_wall_s_{init.replace('|', 'par').replace('+', 'pp')}_{a.fit_iters}it"
+    fixed max_iter).  ``ipe``: the reference's DEFAULT distance mode
+    (``true_distance_estimate=True``, ``_dmeans.py:1016-1039``)."""
+    name = name or f"fit_wall_s_{init.replace('|', 'par').replace('+', 'pp')}_{a.fit_iters}it"
     try:
         from sq_learn_amd.models.cluster import QMeans
-        kw = dict(n_clusters=a.k, delta=a.delta, true_distance_estimate=False,
+        kw = dict(n_clusters=a.k, delta=a.delta, true_distance_estimate=bool(ipe),
                   intermediate_error=True, true_tomography=False, init=init, n_init=1,
                   max_iter=a.fit_iters, tol=0.0, random_state=a.seed, device=dev,
                   gemm_precision=a.dtype)
@@ -395,6 +445,8 @@ def main(argv=None):
     del eng
     if gpu:
         torch.cuda.empty_cache()
+    if gpu and comm.world_size == 1 and a.n >= 8 * 4096:
+        _share8_extra(extra, a, X, comm, dev)
     if a.ipe_steps > 0 and gpu:
         _ipe_extra(extra, a, X, comm, dev, start, C0)
     if gpu and not a.no_hard:
@@ -406,6 +458,11 @@ def main(argv=None):
     if not a.no_fit:
         for init in ("random", "k-means||", "k-means++"):
             _fit_extra(extra, a, sa, comm, dev, init)
+        if gpu and a.ipe_steps > 0:
+            # the reference defaults: k-means++ init + IPE ("l2-sampled")
+            # distances, n_init = 1, fit_iters iterations, tol = 0
+            _fit_extra(extra, a, sa, comm, dev, "k-means++", ipe=True,
+                       name="fit_wall_s_refdefault")
     if not a.no_qpca and gpu:
         # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
         _qpca_extra(extra, "qpca_10Mx256_full_fit_s", sa, comm, dev, "full")

@@ -37,6 +37,7 @@
 namespace sq {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr double binom_c(int n, int i) {
   double c = 1.0;
@@ -277,21 +278,20 @@ SQ_DEV float ipe_distance(float ipf, double nx2, double ny2, double eps, int Q, 
 }
 
 // ---------------------------------------------------------------- pruning
-// A pair can change a row's label only if its estimate D~ is <= the row's
-// best estimate so far, thr.  For odd Q the median's value class t (values
-// increase with t = min(j, M - j)) is <= t_b = max{t : D~(t) <= thr} iff at
-// least h = (Q+1)/2 of the Q draws fall in L = {bins of class <= t_b}:
-// P(in L) = pi_L = P(Bin(Q, p_L) >= h), p_L the Fejer mass of L.  Every bin of
-// L lies >= m = omega - t_b bins from omega, and the Fejer pmf is
-// sin^2(pi phi) / (M^2 sin^2(pi delta / M)) <= 1 / (4 delta^2) (Jordan), so
-// p_L <= pbar = (1/m + 1/m^2) / 2 and pi_L <= pibar = P(Bin(Q, pbar) >= h).
-// The sampler draws u (53 bits) once: u >= pibar -> the pair loses (exactly
-// the event u >= pi_L, which contains it); otherwise p_L and pi_L are summed
-// exactly, u >= pi_L loses, and u < pi_L gives the number c >= h of draws in
-// L (P(C = c | C >= h), inverted with the same u) and the median = the h-th
-// smallest of c iid draws from the Fejer law restricted to L: F_L^-1(p_L V),
-// V ~ Beta(h, c - h + 1) from a fresh uniform.  Exact law of "D~ if <= thr";
-// the cost of a losing pair is an fp32 bound plus one Philox block.
+// A pair can change a row's label only if its estimate D~ is <= a value
+// some other pair of the row actually drew, thr.  For odd Q the median's
+// value class t (values increase with t = min(j, M - j)) is <= t_b =
+// max{t : D~(t) <= thr} iff at least h = (Q+1)/2 of the Q draws fall in L =
+// {bins of class <= t_b}: P(in L) = pi_L = P(Bin(Q, p_L) >= h), p_L the
+// Fejer mass of L.  Every bin of L lies >= m = omega - t_b bins from omega,
+// and the Fejer pmf is sin^2(pi phi) / (M^2 sin^2(pi delta / M)) <= 1 /
+// (4 delta^2) (Jordan), so p_L <= pbar = (1/m + 1/m^2) / 2 and pi_L <= pibar =
+// P(Bin(Q, pbar) >= h).  Given u uniform on [0, b) with b >= pibar, the pair
+// loses when u >= pibar; otherwise p_L and pi_L are summed exactly, u >= pi_L
+// loses, and u < pi_L gives the number c >= h of draws in L (P(C = c | C >=
+// h), inverted with the same u) and the median = the h-th smallest of c iid
+// draws from the Fejer law restricted to L: F_L^-1(p_L V), V ~ Beta(h, c - h
+// + 1) from a fresh uniform.  Exact law of "D~ if <= thr" (ipe_pruned_exact).
 
 // x = G^-1(u), G(x) = P(Bin(c, x) >= h): the h-th order statistic of c uniforms
 SQ_DEV double order_stat_inv(double u, int c, int h) {
@@ -407,68 +407,111 @@ SQ_DEV float ipe_pruned_exact(double ip, double S, double eps, int Q, float thr,
   return (float)(2.0 * S * v);
 }
 
-// Screen of one pair against thr (odd Q, finite thr): returns true with dt =
-// D~ when it is <= thr or +inf when it is not (the pruned sampler above);
-// false when the fp32 bound cannot separate the pair from thr (m < 3, a ~ 1,
-// t_b beyond the walk cap, or no threshold yet): the pair needs the full
-// sampler, which the caller defers to the wave's queue.
-SQ_DEV bool ipe_screen(float ipf, float nx2, float ny2, double eps, int Q, const RngKey& key,
-                       unsigned long long sid, float thr, int h, float cqh, float& dt) {
-  const float INF = __builtin_inff();
-  if (!(thr < INF) || !(Q & 1)) return false;
-  // fp32 screen, every quantity within a few ulps (v_rcp / v_sqrt: 1 ulp):
-  // a (abs. error < 1e-6 for the fp32 S, ip of the MFMA), r = thr / 2S
-  // (1 + 2^-22: every D~(t) <= thr has sin^2(pi t / M) <= r), eps_a, M.
-  // sin(beta - beta_t) = sqrt(a (1 - r)) - sqrt(r (1 - a)) <= beta - beta_t
-  // gives a LOWER bound on m = M (beta - beta_t) / pi; the margin covers the
-  // rounding (a >= 1e-4: d sqrt(a) <= 1e-6 / 0.02).
+// ------------------------------------------------- hazard-budget screening
+// Every pair of a row is screened against the row's FIXED threshold thr =
+// the sampled estimate of its hint pair (the exact-distance argmin of pass
+// 1, or the previous iteration's label).  pibar_j (above) bounds the
+// probability that pair j's estimate reaches thr; instead of one uniform per
+// pair (u < pibar_j), the pairs of one stream (row g, centroid class
+// (j / 16) mod 4, j mod 16: the pairs one lane sweeps for that row, in tile
+// order) form a sequence of independent Bernoulli(b_j) events,
+// b_j = 1 - exp(-H_j), H_j = ceil(2^32 * pu_j (1 + 2^-10)) 2^-32 >= -log(1 - pu_j),
+// pu_j >= pibar_j the fp32 union bound: one Exp(1) budget per stream, spent
+// by the integer hazards H_j, fires at the pair where it runs out
+// (memoryless: exactly the Bernoulli(b_j) law per pair).  A fired pair is
+// thinned: u = U b_j, U uniform -> u is uniform on [0, b_j), so u >= pibar
+// loses and u < pibar runs the exact branch above (u uniform on [0, pi_L)
+// given u < pi_L: the exact law of "D~ if <= thr").  A far pair costs the
+// fp32 bound and an integer subtract; fires are rare (sum of hazards <<
+// 1 per stream), and a new budget is drawn only after one.  The outcome of
+// each pair depends on (thr, its stream) only - never on the order in which
+// the lanes' queues drain - so labels are identical however the rows are
+// grouped into workgroups or sharded over ranks.
+
+struct IpeScreen {
+  float kq;       // 1 / (sqrt(2) eps), rounded down
+  float inv_eps;  // 1 / eps, rounded up
+  float cqh;      // C(Q, h), rounded up
+  int h;
+};
+
+// upper bound on sqrt(x (1 + 2^-23)) (the class-value rounding of thr)
+SQ_DEV float ipe_sthr(float x) { return __builtin_amdgcn_sqrtf(x) * 1.000001f; }
+
+// The fp32 hazard of one pair against thr (sthr = ipe_sthr(thr)):
+// true -> hq = its integer hazard (units 2^-32) and pbar; false -> the pair
+// needs the full sampler (D~ competitive with thr, degenerate a, huge walk).
+//   S = |x|^2 + |c|^2, D = S - 2 ip = 2 S a;  asin(y) - asin(x) >= y - x, so
+//   every bin t of a class with value <= thr lies m >= (M / pi)(sqrt a - sqrt r)
+//   >= sqrt(S) (sqrt D - sqrt thr') / (sqrt2 eps max(1, |ip|)) bins below omega
+//   (M >= pi / eps_a = pi S / (eps max(1, |ip|)));  D >= S 2^-12 keeps the
+//   fp32 relative error of D below 7.4e-4 (the sqrt(D) margin 4.9e-4 covers
+//   its half); every other product carries its ulps in the 3e-6 margin.
+SQ_DEV bool ipe_hazard(float ip, float nx2, float ny2, float sthr, const IpeScreen& sc,
+                       uint32_t& hq, float& pbar) {
+#pragma clang fp contract(off)   // the drain recomputes hq bit for bit
   const float S = nx2 + ny2;
-  if (!(S > 0.0f)) return false;
-  const float inv = 0.5f * __builtin_amdgcn_rcpf(S);
-  const float a = (S - 2.0f * ipf) * inv;
-  const float r = fmaxf(thr * inv * (1.0f + 4.8e-7f), 0.0f);
-  if (!(a < 0.99f && a > 1e-4f && r < a)) return false;
-  const float epsa = (float)eps * fmaxf(1.0f, fabsf(ipf)) * 2.0f * inv;
-  const float Mf = fminf(1.5707963f * __builtin_amdgcn_rcpf(epsa) *
-                             (1.0f + __builtin_amdgcn_sqrtf(1.0f + 4.0f * epsa)),
-                         1.0995116e12f);
-  const float Mlb = floorf(Mf * (1.0f - 2e-5f));
-  const float sd = __builtin_amdgcn_sqrtf(a * (1.0f - r)) - __builtin_amdgcn_sqrtf(r * (1.0f - a));
-  const float m = Mlb * (sd - 4e-5f) * 0.31830987f;
-  // t_b <= (M / pi) asin(sqrt r) <= M sqrt(r) / 2: the rare branch's walk
-  const float tcap = 0.5f * Mf * __builtin_amdgcn_sqrtf(r);
-  if (!(m >= 3.0f && tcap <= 1048576.0f)) return false;
-  const float rm = __builtin_amdgcn_rcpf(m);
-  const float pbar = fminf(0.5f * rm * (1.0f + rm) * (1.0f + 2e-5f), 1.0f);
-  // union bound C(Q, h) pbar^h >= pibar (exp2 / log2 within 2^-20)
-  const float pu = cqh * __builtin_amdgcn_exp2f((float)h * __builtin_amdgcn_logf(pbar)) * (1.0f + 1e-4f);
-  WordStream ws(key, sid);
-  const uint32_t w0 = ws.next();
-  dt = INF;
-  if ((float)w0 * 2.3283064e-10f >= pu) return true;
-  const double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
-  const uint32_t w1 = ws.next();
-  const double u = ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
-                   (1.0 / 9007199254740992.0);
-  if (u >= pib) return true;
-  dt = ipe_pruned_exact((double)ipf, (double)nx2 + (double)ny2, eps, Q, thr, u, ws);
+  const float D = fmaf(-2.0f, ip, S);
+  if (!(D >= S * 2.44140625e-4f && D <= S * 1.998046875f)) return false;
+  const float sD = __builtin_amdgcn_sqrtf(D) * (1.0f - 4.8828125e-4f);
+  const float ra = __builtin_amdgcn_rcpf(fmaxf(1.0f, fabsf(ip)));
+  const float P = __builtin_amdgcn_sqrtf(S) * ra * sc.kq;
+  const float m = (sD - sthr) * P * (1.0f - 3e-6f);
+  // t_b <= M sqrt(r) / 2, M <= pi / eps_a + pi + 1: the exact branch's walk
+  const float tcap = fmaf(1.571f * sthr, P, 2.2f);
+  // M below its 2^40 cap
+  const float Mq = S * ra * sc.inv_eps;
+  if (!(m >= 3.0f && tcap <= 1048576.0f && Mq < 6.0e10f)) return false;
+  const float rm = __builtin_amdgcn_rcpf(m) * 1.000001f;
+  pbar = fminf(0.5f * rm * (1.0f + rm) * 1.00002f, 1.0f);
+  // C(Q, h) pbar^h by binary powering (h <= 8: at most 6 roundings)
+  const float p2 = pbar * pbar, p4 = p2 * p2;
+  float pw = (sc.h & 1) ? pbar : 1.0f;
+  if (sc.h & 2) pw *= p2;
+  if (sc.h & 4) pw *= p4;
+  if (sc.h & 8) pw *= p4 * p4;
+  const float pu = sc.cqh * pw * 1.00001f;
+  // -log(1 - pu) <= pu (1 + pu) <= pu (1 + 2^-10): 2^32 H < 2^22.01, so 256
+  // pairs of one stream never exhaust a capped (2^31) budget
+  if (!(pu < 9.765625e-4f)) return false;
+  hq = (uint32_t)(pu * 1.001f * 4294967296.0f) + 1u;
   return true;
+}
+
+// 53-bit uniform in (0, 1) from two words
+SQ_DEV double u53(uint32_t w0, uint32_t w1) {
+  return ((double)(((unsigned long long)w0 << 21) ^ (unsigned long long)(w1 >> 11)) + 0.5) *
+         (1.0 / 9007199254740992.0);
+}
+
+// an Exp(1) budget in units of 2^-32, capped at 2^31 (= E >= 1/2: more than
+// 256 capped hazards can spend)
+SQ_DEV uint32_t ipe_budget(uint32_t w0, uint32_t w1) {
+  const double U = u53(w0, w1);
+  if (U <= 0.6065306597126334) return 0x80000000u;   // exp(-1/2)
+  return (uint32_t)(-log(U) * 4294967296.0);
 }
 
 SQ_DEV bool ipe_better(float ob, uint32_t ok, int oj, float b, uint32_t kk, int jj) {
   return ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)));
 }
 
-// prune = 1 (odd Q): pass 1 sweeps the centroid tiles for the exact fp32
-// distance argmin j* of each row (a hint only), the 16 hint pairs are
-// sampled in full, and pass 2 samples every other pair against the row's
-// running best (initially the hint's D~) with the pruned sampler.
-template <int D4>
+// Layout per lane: register i holds pair (row row0 + 4 q4 + i, centroid
+// 16 t + c16) of tile t.  prune = 1 (odd Q): each row's hint pair is sampled
+// in full first (hint = hint_labels[row] when valid - the previous
+// iteration's label, its inner product by a direct fp32 dot product - else
+// the pass-1 exact fp32 distance argmin), its estimate is the row's fixed
+// threshold, and every other pair is screened by its hazard.  stats
+// (nullable, 5 x u64): screened, full-sampler pairs, fires, fires reaching
+// the exact branch, workgroups running pass 1.
+template <int D4, bool STATS>
 __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     const float* __restrict__ X, long long ldx, const float* __restrict__ Cf,
+    const float* __restrict__ C, const int* __restrict__ hint_labels,
     const float* __restrict__ xn, const float* __restrict__ cn, int* __restrict__ labels,
     float* __restrict__ mind, long long n, int d, int k, int n_tiles, double eps, int Q,
-    RngKey key, RngKey tie_key, long long row_offset, int prune) {
+    RngKey key, RngKey tie_key, RngKey skip_key, IpeScreen sc, long long row_offset, int prune,
+    unsigned long long* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) float As[];   // [D4][64] A fragments
   __shared__ float mb[4][16];
   __shared__ uint32_t mk[4][16];
@@ -476,15 +519,23 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   __shared__ float hip_[4][16];
   __shared__ float hv[16];
   __shared__ int hj[16];
-  // per-lane queues of the pairs that need the full sampler ([slot][thread])
-  constexpr int QCAP = D4 <= 128 ? 8 : 5;
+  __shared__ int lh[16];
+  __shared__ float lip[16];
+  // per-lane queues of the pairs that need the full sampler or fired
+  // ([slot][thread]; entry = row slot (2 bits) | fired (1 bit) | centroid)
+  constexpr int QCAP = D4 <= 128 ? 8 : 3;
   __shared__ uint32_t qj[QCAP * 256];
   __shared__ float qip[QCAP * 256];
+  // the lane's running (best D~, label) of its 4 row slots ([slot][thread]):
+  // touched only by the drains and the final merge, so they live in LDS
+  __shared__ float bestv[4 * 256];
+  __shared__ int bestj[4 * 256];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
   const long long row0 = (long long)blockIdx.x * 16;
   const float INF = __builtin_inff();
+  uint32_t st_scr = 0, st_full = 0, st_fire = 0, st_exact = 0;
   // A fragments (16x16x4 f32) of the workgroup's 16 rows, shared by the 4
   // waves: As[s][l] = x[row0 + (l & 15)][4 s + (l >> 4)]; rows past n clamped
   for (int e = threadIdx.x; e < D4 * 64; e += 256) {
@@ -495,61 +546,35 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   }
   __syncthreads();
   // register i of this lane = pair (row row0 + 4 q4 + i, centroid 16 t + c16)
-  f32x4 nx2, best;
-  int bj[4];   // runtime-indexed only through unrolled selects (no scratch)
+  f32x4 nx2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const long long r = row0 + 4 * q4 + i;
     nx2[i] = xn[r < n ? r : n - 1];
-    best[i] = INF;
-    bj[i] = -1;
+    bestv[i * 256 + threadIdx.x] = INF;
+    bestj[i * 256 + threadIdx.x] = -1;
   }
-  const int h = (Q + 1) / 2;
-  float cqh = 1.0f;   // C(Q, h)
-  for (int i = 0; i < h; ++i) cqh = cqh * (float)(Q - i) / (float)(i + 1);
-  // Pairs that need the full sampler go to this lane's LDS queue and are
-  // sampled by a wave-wide drain (one inlined copy of the sampler): the
-  // expensive path runs max(queue length) times per wave instead of once per
-  // step in which ANY lane meets such a pair.
-  int qn = 0;
-  auto consider = [&](int i, int j, float dt) {
-    // row slot i (compile-time after unrolling) takes (dt, j) if better
+  // label hints: lanes (q4, c16) of wave w take row 4 q4 + w (the row their
+  // lane (q4, 0) samples in step -1), 16 lanes per fp32 dot product
+  bool need_p1 = prune != 0;
+  if (prune && hint_labels) {
+    const int rr = 4 * q4 + wave;
+    const long long r = row0 + rr;
+    const int l = r < n ? hint_labels[r] : 0;
+    const bool ok = r >= n || (l >= 0 && l < k);
+    float s = 0.0f;
+    if (r < n && ok)
+      for (int f = c16; f < d; f += 16)
+        s = fmaf(As[(f >> 2) * 64 + ((f & 3) << 4) + rr], C[(size_t)l * d + f], s);
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      if (ii == i) {
-        const long long g = row_offset + row0 + 4 * q4 + ii;
-        bool take = dt < best[ii];
-        if (!take && dt == best[ii] && dt < INF) {   // tie: the random keys decide (rare)
-          const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
-          const uint32_t bk = band_key(tie_key, g, (uint32_t)bj[ii]);
-          take = tk < bk || (tk == bk && j < bj[ii]);
-        }
-        if (take) {
-          best[ii] = dt;
-          bj[ii] = j;
-        }
-      }
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (c16 == 0) {
+      lh[rr] = r < n ? (ok ? l : -2) : -1;
+      lip[rr] = s;
     }
-  };
-  auto drain = [&]() {
-    while (__ballot(qn > 0) != 0ull) {   // wave-uniform
-      if (qn > 0) {
-        --qn;
-        const uint32_t pj = qj[qn * 256 + threadIdx.x];
-        const float ip = qip[qn * 256 + threadIdx.x];
-        const int i = (int)(pj >> 30), j = (int)(pj & 0x3fffffffu);
-        float nxi = nx2[0];
-#pragma unroll
-        for (int ii = 1; ii < 4; ++ii) nxi = i == ii ? nx2[ii] : nxi;
-        const long long g = row_offset + row0 + 4 * q4 + i;
-        const float dt = ipe_distance(ip, (double)nxi, (double)cn[j], eps, Q, key,
-                                      (unsigned long long)g * (unsigned long long)k + (unsigned long long)j);
-        consider(i, j, dt);
-      }
-    }
-  };
-  int hint[4] = {-1, -1, -1, -1};
-  if (prune) {
+    need_p1 = __syncthreads_or(!ok) != 0;
+  }
+  if (need_p1) {
     // ---- pass 1: exact fp32 distance argmin (hint), with its inner product
     f32x4 bd = {INF, INF, INF, INF}, bip = {0.f, 0.f, 0.f, 0.f};
     int bjj[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
@@ -564,8 +589,8 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
         const float ny2 = cn[j];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float D = nx2[i] + ny2 - 2.0f * acc[i];
-          if (D < bd[i]) { bd[i] = D; bjj[i] = j; bip[i] = acc[i]; }
+          const float Dd = nx2[i] + ny2 - 2.0f * acc[i];
+          if (Dd < bd[i]) { bd[i] = Dd; bjj[i] = j; bip[i] = acc[i]; }
         }
       }
     }
@@ -587,30 +612,120 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     }
     __syncthreads();
   }
-  // ---- pass 2: every pair but the hint (the only pass without pruning).
-  // Pairs the screen resolves cost an fp32 bound + one Philox block; the
-  // others go to the lane's queue.  Step -1 (prune) queues the 16 hint pairs
-  // (row 4 q4 + w taken by lane (q4, c16 = 0) of wave w, as its row slot w)
-  // and publishes their samples as every row's starting threshold.  The
-  // queue is drained at ONE call site (one inlined copy of the full
-  // sampler): after the hint step, when a lane could overflow on the next
-  // tile, and after the wave's last tile.  Thresholds are always values of
-  // pairs already sampled (exact); queued pairs join the running best when
-  // drained.
+  // hazard budgets of this lane's 4 streams (row g, class wave, column c16)
+  // (vector registers written through selects only: never addressable)
+  u32x4 bud = {0u, 0u, 0u, 0u};
+  f32x4 sthr = {INF, INF, INF, INF};   // the thresholds themselves stay in hv
+  auto stream_id = [&](int i) -> unsigned long long {
+    const long long g = row_offset + row0 + 4 * q4 + i;
+    return (unsigned long long)g * 64ull + (unsigned long long)(wave * 16 + c16);
+  };
+  if (prune) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      WordStream ws(skip_key, stream_id(i));
+      const uint32_t w0 = ws.next(), w1 = ws.next();
+      bud[i] = ipe_budget(w0, w1);
+    }
+  }
+  int qn = 0;
+  auto consider = [&](int i, int j, float dt) {
+    // row slot i takes (dt, j) if better
+    const int e = i * 256 + threadIdx.x;
+    const float b = bestv[e];
+    const int bjj = bestj[e];
+    bool take = dt < b;
+    if (!take && dt == b && dt < INF) {   // tie: the random keys decide (rare)
+      const long long g = row_offset + row0 + 4 * q4 + i;
+      const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
+      const uint32_t bk = band_key(tie_key, g, (uint32_t)bjj);
+      take = tk < bk || (tk == bk && j < bjj);
+    }
+    if (take) {
+      bestv[e] = dt;
+      bestj[e] = j;
+    }
+  };
+  // Pairs that need the full sampler (and fired pairs) go to this lane's LDS
+  // queue and are resolved by a wave-wide drain (one inlined copy of the
+  // samplers): the expensive paths run max(queue length) times per wave.
+  auto drain = [&](int stp) {
+    while (__ballot(qn > 0) != 0ull) {   // wave-uniform
+      if (qn > 0) {
+        --qn;
+        const uint32_t pj = qj[qn * 256 + threadIdx.x];
+        const float ip = qip[qn * 256 + threadIdx.x];
+        const int i = (int)(pj >> 30), j = (int)(pj & 0x1fffffffu);
+        const bool fired = (pj >> 29) & 1u;
+        float nxi = nx2[0], si = sthr[0];
+#pragma unroll
+        for (int ii = 1; ii < 4; ++ii) {
+          nxi = i == ii ? nx2[ii] : nxi;
+          si = i == ii ? sthr[ii] : si;
+        }
+        const long long g = row_offset + row0 + 4 * q4 + i;
+        float dt;
+        if (!fired) {
+          if (STATS) ++st_full;
+          dt = ipe_distance(ip, (double)nxi, (double)cn[j], eps, Q, key,
+                            (unsigned long long)g * (unsigned long long)k + (unsigned long long)j);
+        } else {
+          // the same hazard as at the screen (same inputs, same code)
+          uint32_t hq = 0;
+          float pbar = 1.0f;
+          ipe_hazard(ip, nxi, cn[j], si, sc, hq, pbar);
+          WordStream ws(skip_key, stream_id(i));
+          ws.b = (uint32_t)(2 * stp + 1);
+          const uint32_t w0 = ws.next(), w1 = ws.next(), w2 = ws.next(), w3 = ws.next();
+          const uint32_t nb = ipe_budget(w0, w1);   // the stream's next budget
+          bud.x = i == 0 ? nb : bud.x;
+          bud.y = i == 1 ? nb : bud.y;
+          bud.z = i == 2 ? nb : bud.z;
+          bud.w = i == 3 ? nb : bud.w;
+          const double beff = -expm1(-(double)hq * (1.0 / 4294967296.0));
+          const double u = u53(w2, w3) * beff;
+          const int h = (Q + 1) / 2;
+          const double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
+          dt = INF;
+          if (u < pib) {
+            if (STATS) ++st_exact;
+            dt = ipe_pruned_exact((double)ip, (double)nxi + (double)cn[j], eps, Q, hv[4 * q4 + i],
+                                  u, ws);
+          }
+        }
+        consider(i, j, dt);
+      }
+    }
+  };
+  // the 4 slots' hint centroids, 16 bits each (k_pad <= 16384; 0xFFFF: none)
+  uint32_t hint01 = 0xFFFFFFFFu, hint23 = 0xFFFFFFFFu;
+  // ---- step -1 (prune): the 16 hint pairs (row 4 q4 + w taken by lane
+  // (q4, c16 = 0) of wave w) sampled in full; their estimates become the
+  // rows' thresholds.  Steps >= 0: the tiles of this wave.
   const int ntl = wave < n_tiles ? (n_tiles - wave + 3) / 4 : 0;   // this wave's tiles
   bool queued = false;
   int jh = -1;
   for (int stp = prune ? -1 : 0; stp < ntl; ++stp) {
+    bool fired = false;
     if (stp < 0) {
       if (c16 == 0) {
         const int rr = 4 * q4 + wave;
-        float b = mb[0][rr], p = hip_[0][rr];
-        int jj = mj[0][rr];
-        for (int w = 1; w < 4; ++w)
-          if (mb[w][rr] < b || (mb[w][rr] == b && mj[w][rr] < jj)) {
-            b = mb[w][rr]; p = hip_[w][rr]; jj = mj[w][rr];
-          }
-        if (row0 + rr < n && jj < k) {
+        int jj = -1;
+        float p = 0.0f;
+        const int lab = hint_labels ? lh[rr] : -2;
+        if (lab >= 0) {
+          jj = lab;
+          p = lip[rr];
+        } else if (lab == -2) {
+          float b = mb[0][rr];
+          p = hip_[0][rr];
+          jj = mj[0][rr];
+          for (int w = 1; w < 4; ++w)
+            if (mb[w][rr] < b || (mb[w][rr] == b && mj[w][rr] < jj)) {
+              b = mb[w][rr]; p = hip_[w][rr]; jj = mj[w][rr];
+            }
+        }
+        if (row0 + rr < n && jj >= 0 && jj < k) {
           qj[threadIdx.x] = ((uint32_t)wave << 30) | (uint32_t)jj;
           qip[threadIdx.x] = p;
           qn = 1;
@@ -628,61 +743,60 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       const int j = t * 16 + c16;
       if (j < k) {   // padded centroid columns do nothing
         const float ny2 = cn[j];
-        // one inlined copy of the screen: the 4 pairs rotate through slot 0
-        // (back in place after the 4 steps)
-#pragma nounroll
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
           const long long r = row0 + 4 * q4 + i;
-          if (r < n && j != hint[0]) {
-            const long long g = row_offset + r;
-            float dt;
-            if (prune && ipe_screen(acc[0], nx2[0], ny2, eps, Q, key,
-                                    (unsigned long long)g * (unsigned long long)k + (unsigned long long)j,
-                                    best[0], h, cqh, dt)) {
-              bool take = dt < best[0];
-              if (!take && dt == best[0] && dt < INF) {   // tie: the random keys decide (rare)
-                const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
-                const uint32_t bk = band_key(tie_key, g, (uint32_t)bj[0]);
-                take = tk < bk || (tk == bk && j < bj[0]);
+          const uint32_t hnt = ((i < 2 ? hint01 : hint23) >> (16 * (i & 1))) & 0xFFFFu;
+          if (r < n && (uint32_t)j != hnt) {
+            bool full = true;
+            if (prune) {
+              uint32_t hq;
+              float pbar;
+              if (ipe_hazard(acc[i], nx2[i], ny2, sthr[i], sc, hq, pbar)) {
+                full = false;
+                if (hq > bud[i]) {   // the stream's budget runs out here: the pair fired
+                  qj[qn * 256 + threadIdx.x] = ((uint32_t)i << 30) | (1u << 29) | (uint32_t)j;
+                  qip[qn * 256 + threadIdx.x] = acc[i];
+                  ++qn;
+                  if (STATS) ++st_fire;
+                  fired = true;
+                } else {
+                  bud[i] -= hq;
+                  if (STATS) ++st_scr;
+                }
               }
-              if (take) {
-                best[0] = dt;
-                bj[0] = j;
-              }
-            } else {
+            }
+            if (full) {
               qj[qn * 256 + threadIdx.x] = ((uint32_t)i << 30) | (uint32_t)j;
-              qip[qn * 256 + threadIdx.x] = acc[0];
+              qip[qn * 256 + threadIdx.x] = acc[i];
               ++qn;
             }
           }
-          acc = acc.yzwx;
-          nx2 = nx2.yzwx;
-          best = best.yzwx;
-          const int j0 = bj[0];
-          bj[0] = bj[1]; bj[1] = bj[2]; bj[2] = bj[3]; bj[3] = j0;
-          const int h0 = hint[0];
-          hint[0] = hint[1]; hint[1] = hint[2]; hint[2] = hint[3]; hint[3] = h0;
         }
       }
     }
-    // drain: after the hint step, when a lane could overflow on the next
-    // tile (room for 4 more), after the last tile
-    const bool flush = stp < 0 || stp == ntl - 1 || qn > QCAP - 4;
-    if (__ballot(flush && qn > 0) != 0ull) drain();
+    // drain: after the hint step, after a fire (the stream's next budget is
+    // drawn there, before its next pair), when a lane could overflow on the
+    // next tile (room for 4 more), after the last tile
+    const bool flush = stp < 0 || stp == ntl - 1 || qn > QCAP - 4 || fired;
+    if (__ballot(flush && qn > 0) != 0ull) drain(stp);
     if (stp < 0) {
       if (c16 == 0) {
-        float v = best[0];
-#pragma unroll
-        for (int ii = 1; ii < 4; ++ii) v = wave == ii ? best[ii] : v;
-        hv[4 * q4 + wave] = queued ? v : INF;
+        hv[4 * q4 + wave] = queued ? bestv[wave * 256 + threadIdx.x] : INF;
         hj[4 * q4 + wave] = queued ? jh : -1;
       }
       __syncthreads();
+      hint01 = hint23 = 0u;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        hint[i] = hj[4 * q4 + i];
-        best[i] = hint[i] >= 0 ? hv[4 * q4 + i] : INF;
-        bj[i] = hint[i];
+        const int hi = hj[4 * q4 + i];
+        const float b = hi >= 0 ? hv[4 * q4 + i] : INF;
+        bestv[i * 256 + threadIdx.x] = b;
+        bestj[i * 256 + threadIdx.x] = hi;
+        sthr[i] = ipe_sthr(b);
+        const uint32_t h16 = hi >= 0 ? (uint32_t)hi : 0xFFFFu;
+        if (i < 2) hint01 |= h16 << (16 * i);
+        else hint23 |= h16 << (16 * (i - 2));
       }
     }
   }
@@ -690,8 +804,8 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   // (the order (D~, tie key, j) is total: any merge order gives the same pick)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    float b = best[i];
-    int jj = bj[i];
+    float b = bestv[i * 256 + threadIdx.x];
+    int jj = bestj[i * 256 + threadIdx.x];
     const long long g = row_offset + row0 + 4 * q4 + i;
     uint32_t kk = jj >= 0 ? band_key(tie_key, g, (uint32_t)jj) : 0xFFFFFFFFu;
     if (jj < 0) jj = 0x7fffffff;
@@ -730,32 +844,62 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       mind[r] = b;
     }
   }
+  if (STATS) {
+    const uint32_t v[4] = {st_scr, st_full, st_fire, st_exact};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t s = v[c];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o, 64);
+      if (lane == c) atomicAdd(stats + c, (unsigned long long)s);
+    }
+    if (threadIdx.x == 4 && need_p1) atomicAdd(stats + 4, 1ull);
+  }
 }
 
 }  // namespace sq
 
 using namespace sq;
 
-extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const void* xn,
-                            const void* cn, void* labels, void* mind, long long n, int d, int d_pad,
-                            int k, int k_pad, double eps, int Q, unsigned k0, unsigned k1,
-                            unsigned s0, unsigned s1, unsigned t0, unsigned t1, unsigned ts0,
-                            unsigned ts1, long long row_offset, int prune, void* stream) {
+extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const void* C,
+                            const void* hint_labels, const void* xn, const void* cn, void* labels,
+                            void* mind, long long n, int d, int d_pad, int k, int k_pad, double eps,
+                            int Q, unsigned k0, unsigned k1, unsigned s0, unsigned s1, unsigned t0,
+                            unsigned t1, unsigned ts0, unsigned ts1, unsigned q0, unsigned q1,
+                            unsigned qs0, unsigned qs1, long long row_offset, int prune,
+                            void* stats, void* stream) {
   if (n <= 0) return 0;
-  if (Q < 1 || Q > kIpeMaxQ || k < 1 || k_pad % 16 != 0 || k_pad < k || d < 1 || d > d_pad ||
-      ldx < d)
+  if (Q < 1 || Q > kIpeMaxQ || k < 1 || k_pad % 16 != 0 || k_pad < k || k_pad > 16384 || d < 1 ||
+      d > d_pad || ldx < d || !(eps > 0.0) || (hint_labels && !C))
     return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   RngKey tie{t0, t1, ts0, ts1};
+  RngKey skip{q0, q1, qs0, qs1};
+  IpeScreen sc;
+  const int h = (Q + 1) / 2;
+  double cq = 1.0;
+  for (int i = 0; i < h; ++i) cq = cq * (double)(Q - i) / (double)(i + 1);
+  sc.h = h;
+  sc.cqh = (float)cq * (1.0f + 1e-6f);
+  sc.kq = (float)(1.0 / (1.4142135623730951 * eps)) * (1.0f - 1e-6f);
+  sc.inv_eps = (float)(1.0 / eps) * (1.0f + 1e-6f);
   const long long blocks = (n + 15) / 16;
   const int nt = k_pad / 16;
-#define CASE(DP)                                                                              \
-  case DP:                                                                                    \
-    hipLaunchKernelGGL(ipe_fused_kernel<DP / 4>, dim3((unsigned)blocks), dim3(256),            \
-                       (size_t)DP * 64, (hipStream_t)stream, (const float*)X, ldx,            \
-                       (const float*)Cf, (const float*)xn, (const float*)cn, (int*)labels,    \
-                       (float*)mind, n, d, k, nt, eps, Q, key, tie, row_offset,  \
-                       prune && (Q & 1));              \
+  const int pr = (prune && (Q & 1)) ? 1 : 0;
+  const dim3 grid((unsigned)blocks);
+  hipStream_t hs = (hipStream_t)stream;
+#define CASE(DP)                                                                                \
+  case DP:                                                                                      \
+    if (stats)                                                                                  \
+      ipe_fused_kernel<DP / 4, true><<<grid, 256, (size_t)DP * 64, hs>>>(                       \
+          (const float*)X, ldx, (const float*)Cf, (const float*)C, (const int*)hint_labels,     \
+          (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, nt, eps, Q,  \
+          key, tie, skip, sc, row_offset, pr, (unsigned long long*)stats);                      \
+    else                                                                                        \
+      ipe_fused_kernel<DP / 4, false><<<grid, 256, (size_t)DP * 64, hs>>>(                      \
+          (const float*)X, ldx, (const float*)Cf, (const float*)C, (const int*)hint_labels,     \
+          (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, nt, eps, Q,  \
+          key, tie, skip, sc, row_offset, pr, nullptr);                                         \
     break;
   switch (d_pad) {
     CASE(32)

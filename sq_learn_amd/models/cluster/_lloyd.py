@@ -383,21 +383,33 @@ class LloydEngine:
         ipe_key = self._key("ipe")
         if self.device.type == "cuda" and self.d <= 1024 and self.Xf.dtype == torch.float32 \
                 and self.Xf.stride(1) == 1 and self.ipe_Q <= 15:
-            # fused kernel: fp32 MFMA inner products + per-pair median-of-Q AE
+            # fused kernel: fp32 MFMA inner products + per-pair median-of-Q AE.
+            # The previous E-step's labels are the hint pairs (their estimates
+            # seed the pruned screen; any hint gives the same law): two label
+            # buffers alternate, so the labels returned by the last step stay
+            # valid through the next one
             n = self.n
-            labels32 = torch.empty(n, dtype=torch.int32, device=self.device)
+            if getattr(self, "_ipe_lab", None) is None:
+                self._ipe_lab = [torch.full((n,), -1, dtype=torch.int32, device=self.device)
+                                 for _ in range(2)]
+                self._ipe_cur = 0
+                self._ipe_xn = self.xn.float().contiguous()
+            hint = self._ipe_lab[self._ipe_cur]
+            self._ipe_cur ^= 1
+            labels32 = self._ipe_lab[self._ipe_cur]
             mind = torch.empty(n, dtype=torch.float32, device=self.device)
             dp = 32
             while dp < self.d:
                 dp *= 2
             kp = -(-self.k // 16) * 16
-            C32 = self.C.float()
+            C32 = self.C.float().contiguous()
             cn = (C32 * C32).sum(1).contiguous()
             with tracing.range("ipe_fused"):
-                K.ipe_fused_native(self.Xf, K.ipe_center_fragments(C32, kp, dp),
-                                   self.xn.float().contiguous(), cn, self.k, kp, dp, eps,
-                                   self.ipe_Q, ipe_key, self._key("band_select"), self.row_offset,
-                                   labels32, mind)
+                K.ipe_fused_native(self.Xf, K.ipe_center_fragments(C32, kp, dp), self._ipe_xn, cn,
+                                   self.k, kp, dp, eps, self.ipe_Q, ipe_key,
+                                   self._key("band_select"), self.row_offset, labels32, mind,
+                                   C=C32, hint_labels=hint, skip_key=self._key("ipe_skip"),
+                                   stats=getattr(self, "ipe_stats", None))
             return labels32, mind, mind.double().sum().reshape(1)
         if self.device.type == "cuda":
             n = self.n
@@ -679,11 +691,15 @@ class LloydEngine:
         newlab = empty[mine]
         if li.numel():
             if getattr(self, "incremental", False) and self.buf.corr is not None:
-                # the per-cluster inertia counts a row at its label's (old)
-                # centre: bring a relocated row back to its min distance
+                # the per-cluster inertia counts a row at its label's centre
+                # plus its correction (min - label distance, non-zero when
+                # delta > 0 picked a band member other than the argmin): the
+                # row moves to the empty cluster's centre, so its correction
+                # grows by d(old label) - d(new label) and it still adds its
+                # minimum distance
                 xr = X[li].double()
                 dnew = ((xr - C[newlab]) ** 2).sum(1)
-                self.buf.corr[li] = (d[li] - dnew).to(self.buf.corr.dtype)
+                self.buf.corr[li] += (d[li] - dnew).to(self.buf.corr.dtype)
             labels[li] = newlab.to(labels.dtype)
             if getattr(self, "bounds", False):
                 self.lb[li] = 0.0   # label moved: re-evaluate next E-step

@@ -257,23 +257,43 @@ def ipe_center_fragments(C, k_pad, d_pad):
 
 
 def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie_key: RngKey,
-                     row_offset, labels, mind, prune=True):
+                     row_offset, labels, mind, prune=True, C=None, hint_labels=None,
+                     skip_key: RngKey = None, stats=None):
     """Fused IPE E-step (csrc/ipe.hip): exact fp32 MFMA inner products, the
     median-of-Q amplitude-estimation distance per pair in the epilogue,
     per-row argmin with random ties; G is never materialised.  ``prune``
-    (odd Q): a first sweep finds each row's exact-distance argmin, whose
-    pair is sampled first; every other pair is then sampled with the exact
-    threshold sampler (a pair whose estimate cannot reach the row's best
-    costs one fp32 bound and one Philox block) - same law as prune=False."""
+    (odd Q): each row's hint pair is sampled first - ``hint_labels[row]``
+    (int32, e.g. the previous iteration's labels; needs the plain fp32
+    centroids ``C``) when valid, else the exact fp32 distance argmin of a
+    first MFMA sweep - and its estimate is the row's threshold; every other
+    pair is screened by its fp32 hazard against that threshold, spending an
+    Exp(1) budget per (row, lane) stream keyed by ``skip_key``; only pairs
+    whose budget runs out (thinned to the exact law) or that are competitive
+    pay a sampler - same law as prune=False.  ``stats`` (int64[5], optional,
+    accumulated): screened pairs, full-sampler pairs, fires, fires reaching
+    the exact branch, workgroups that ran the first sweep."""
     n, d = X.shape
     assert X.dtype == torch.float32 and X.stride(1) == 1
     assert xn.dtype == torch.float32 and cn.dtype == torch.float32 and xn.numel() >= n
     assert Cfrag.numel() == k_pad * d_pad and labels.dtype == torch.int32
-    rc = nat.native().ipe_fused(X.data_ptr(), X.stride(0), Cfrag.data_ptr(), xn.data_ptr(),
-                                cn.data_ptr(), labels.data_ptr(), mind.data_ptr(), n, d, d_pad, k,
-                                k_pad, float(eps), int(Q), key.k0, key.k1, key.s0, key.s1,
-                                tie_key.k0, tie_key.k1, tie_key.s0, tie_key.s1, int(row_offset),
-                                int(bool(prune)), nat.stream_handle(X.device))
+    if hint_labels is not None:
+        assert C is not None and C.dtype == torch.float32 and C.is_contiguous()
+        assert tuple(C.shape) == (k, d) and hint_labels.dtype == torch.int32
+        assert hint_labels.numel() >= n
+    if stats is not None:
+        assert stats.dtype == torch.int64 and stats.numel() >= 5 and stats.is_contiguous()
+    if skip_key is None:
+        skip_key = key.derive(purpose="ipe_skip")
+    rc = nat.native().ipe_fused(X.data_ptr(), X.stride(0), Cfrag.data_ptr(),
+                                0 if C is None else C.data_ptr(),
+                                0 if hint_labels is None else hint_labels.data_ptr(),
+                                xn.data_ptr(), cn.data_ptr(), labels.data_ptr(), mind.data_ptr(), n,
+                                d, d_pad, k, k_pad, float(eps), int(Q), key.k0, key.k1, key.s0,
+                                key.s1, tie_key.k0, tie_key.k1, tie_key.s0, tie_key.s1,
+                                skip_key.k0, skip_key.k1, skip_key.s0, skip_key.s1,
+                                int(row_offset), int(bool(prune)),
+                                0 if stats is None else stats.data_ptr(),
+                                nat.stream_handle(X.device))
     if rc:
         raise RuntimeError(f"ipe_fused failed (hip error {rc})")
 

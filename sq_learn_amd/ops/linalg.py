@@ -42,16 +42,14 @@ _XTX_MAX_SPLITS = 512
 # chunk's Gram): 128 MiB chunks stay in the 256 MB Infinity Cache between the
 # producing and the consuming kernel instead of a round trip through HBM
 _CHUNK_BYTES = int(os.environ.get("SQ_CHUNK_MB", "128")) << 20
-_part_cache = {}
 
 
 def _part(device, numel):
-    """Reusable fp64 workspace for the xtx split partials (one per device)."""
-    buf = _part_cache.get(device)
-    if buf is None or buf.numel() < numel:
-        buf = torch.empty(max(numel, 1), dtype=torch.float64, device=device)
-        _part_cache[device] = buf
-    return buf
+    """fp64 workspace for the xtx split partials, from torch's caching
+    allocator on the current stream (reused block, no allocation cost after
+    the first call; stream-ordered, so concurrent calls on different streams
+    never share partials)."""
+    return torch.empty(max(numel, 1), dtype=torch.float64, device=device)
 
 
 def _mean64(m, device):

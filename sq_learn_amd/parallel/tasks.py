@@ -122,7 +122,16 @@ class Parallel:
         self.backend = None if backend in (None, "loky", "multiprocessing") else str(backend)
 
     @staticmethod
-    def _run(task, gpu):
+    def _run(task, gpu, ctx=None):
+        if ctx is not None:
+            # the caller's parallel_backend stack, so a nested Parallel inside
+            # a worker sees the same backend / n_jobs (the stack is thread-local)
+            prev = getattr(_LOCAL, "stack", None)
+            _LOCAL.stack = list(ctx)
+            try:
+                return Parallel._run(task, gpu)
+            finally:
+                _LOCAL.stack = prev
         fn, args, kwargs = task
         if gpu is None:
             return fn(*args, **kwargs)
@@ -140,17 +149,20 @@ class Parallel:
         n = min(effective_n_jobs(self.n_jobs), max(len(tasks), 1))
         if n <= 1 or name == "sequential":
             return [self._run(t, None) for t in tasks]
+        # task i -> GPU i mod n_gpus (+ per-task device config), for the
+        # built-in threading backend and registered executors alike
+        slots = _gpu_slots(self.devices)
+        gpus = [slots[i % len(slots)] if slots else None for i in range(len(tasks))]
+        ctx = list(getattr(_LOCAL, "stack", None) or [])
         if name in _BACKENDS:
             ex = _BACKENDS[name](n)
             try:
-                futures = [ex.submit(t[0], *t[1], **t[2]) for t in tasks]
+                futures = [ex.submit(Parallel._run, t, g, ctx) for t, g in zip(tasks, gpus)]
                 return [f.result() for f in futures]
             finally:
                 ex.shutdown(wait=True)
-        slots = _gpu_slots(self.devices)
-        gpus = [slots[i % len(slots)] if slots else None for i in range(len(tasks))]
         with ThreadPoolExecutor(max_workers=n, thread_name_prefix="sq-task") as ex:
-            futures = [ex.submit(self._run, t, g) for t, g in zip(tasks, gpus)]
+            futures = [ex.submit(self._run, t, g, ctx) for t, g in zip(tasks, gpus)]
             return [f.result() for f in futures]
 
 

@@ -43,6 +43,8 @@ PURPOSE = {
     "data": 0x0008,          # synthetic data generators
     "gaussian": 0x0009,      # plain normal draws (randomized SVD test matrix)
     "ipe": 0x000A,           # inner product estimation
+    "ipe_skip": 0x000B,      # IPE hazard budgets / thinning of the pruned screen
+    "kmpp": 0x000C,          # reserved: k-means++ device streams
 }
 
 

@@ -193,7 +193,7 @@ def test_ipe_fused_argmin_wide(cuda):
 
 
 # ------------------------------------------------------------------ pruning
-def _run_rows(x, C, n, eps, Q, cuda, seed, prune):
+def _run_rows(x, C, n, eps, Q, cuda, seed, prune, hint=None, stats=None):
     d = x.size
     dp = 32
     while dp < d:
@@ -206,9 +206,14 @@ def _run_rows(x, C, n, eps, Q, cuda, seed, prune):
     cn = (Ct.double() ** 2).sum(1).float()
     lab = torch.empty(n, dtype=torch.int32, device=cuda)
     mind = torch.empty(n, dtype=torch.float32, device=cuda)
+    hl = None
+    if hint is not None:
+        hl = torch.as_tensor(np.broadcast_to(np.asarray(hint, dtype=np.int32), (n,)).copy(),
+                             device=cuda)
     K.ipe_fused_native(X, K.ipe_center_fragments(Ct, kp, dp), xn, cn, k, kp, dp, eps, Q,
                        RngKey(seed, "ipe", 0), RngKey(seed, "band_select", 0), 0, lab, mind,
-                       prune=prune)
+                       prune=prune, C=Ct if hl is not None else None, hint_labels=hl,
+                       stats=stats)
     torch.cuda.synchronize()
     ip = (Ct.double() @ X[0].double()).cpu().numpy()
     return lab.cpu().numpy(), mind.double().cpu().numpy(), float(xn[0]), cn.double().cpu().numpy(), ip
@@ -280,3 +285,141 @@ def test_ipe_pruned_matches_unpruned_law_many_centroids(cuda):
     table = table[:, table.sum(0) > 0]
     assert table.shape[1] >= 3
     assert stats.chi2_contingency(table)[1] > 1e-4
+
+
+# ------------------------------------------------- hazard-budget screening
+def _fire_case(d=96, K_=64):
+    """Q = 1, M ~ 6-8k bins: pair 0 near, 63 identical competitors (same
+    |c|, same x.c) ~ 800 bins above it: each competitor's hazard ~ 9e-4, so
+    ~5 % of the rows fire at least once; ~0.4 % are won by a competitor."""
+    rng = np.random.default_rng(21)
+    x = rng.standard_normal(d)
+    B = rng.standard_normal((d, K_))
+    B -= np.outer(x, x @ B) / (x @ x)
+    Qm, _ = np.linalg.qr(B)                      # K_ orthonormal directions, all orthogonal to x
+    C = np.empty((K_, d))
+    C[0] = x + 0.9 * Qm[:, 0]
+    C[1:] = x[None] - 4.0 * Qm[:, 1:].T
+    return x.astype(np.float32), C.astype(np.float32)
+
+
+def _competitor_law(x, C, eps):
+    """Exact joint law of (label == 0, min D~) for Q = 1: pair 0 against
+    K - 1 iid competitors (pair 1's law)."""
+    xd = x.astype(np.float64)
+    Cd = C.astype(np.float64)
+    nx2 = float(xd @ xd)
+    Kc = C.shape[0] - 1
+
+    def classes(ip, ny2):
+        S = nx2 + ny2
+        a = min(max((S - 2 * ip) / (2 * S), 0.0), 1.0)
+        M = int(ae_bins(a, eps * max(1.0, abs(ip)) / S))
+        om = M * math.asin(math.sqrt(a)) / math.pi
+        p = fejer_pmf(om, M)
+        p = p / p.sum()
+        t = np.minimum(np.arange(M), M - np.arange(M))
+        return 2 * S * np.sin(np.pi * np.arange(M // 2 + 1) / M) ** 2, np.bincount(t, weights=p)
+
+    v0, p0 = classes(float(Cd[0] @ xd), float(Cd[0] @ Cd[0]))
+    v1, p1 = classes(float(Cd[1] @ xd), float(Cd[1] @ Cd[1]))
+    gt1 = lambda v: p1[v1 > v].sum()
+    ge1 = lambda v: p1[v1 >= v].sum()
+    gt0 = lambda v: p0[v0 > v].sum()
+    cells0 = np.array([p0[i] * gt1(v) ** Kc for i, v in enumerate(v0)])
+    cells1 = np.array([(ge1(w) ** Kc - gt1(w) ** Kc) * gt0(w) for w in v1])
+    return v0, cells0, v1, cells1
+
+
+@pytest.mark.parametrize("hint", [None, 0, 5])
+def test_ipe_hazard_fire_path_exact_law(cuda, hint):
+    """The hazard budgets fire on ~5 % of the rows (Q = 1: the Fejer bound
+    is within a small factor of the true tail, so fired pairs really win
+    sometimes): the joint (label is 0, min D~) law of 1M rows is the exact
+    law, with the pass-1 hint, the right label hint and a wrong label hint
+    (competitor 5 sampled first)."""
+    eps = 0.001
+    x, C = _fire_case()
+    n = 1_000_000
+    st = torch.zeros(5, dtype=torch.int64, device=cuda)
+    lab, mind, *_ = _run_rows(x, C, n, eps, 1, cuda, 3, True, hint=hint, stats=st)
+    scr, full, fires, exact, p1 = st.tolist()
+    assert fires > 0.01 * n and exact > 0.001 * n, st.tolist()
+    assert (p1 > 0) == (hint is None)
+    v0, c0, v1, c1 = _competitor_law(x, C, eps)
+    vals = np.concatenate([v0, v1])
+    cells = np.concatenate([c0, c1])
+    assert abs(cells.sum() - 1.0) < 1e-9
+    obs = np.zeros(len(vals))
+    for L, cand in ((True, np.arange(len(v0))), (False, len(v0) + np.arange(len(v1)))):
+        sel = (lab == 0) if L else (lab != 0)
+        idx = cand[np.argmin(np.abs(mind[sel][:, None] - vals[cand][None, :]), axis=1)]
+        assert np.allclose(mind[sel], vals[idx], rtol=2e-6, atol=1e-5)
+        obs += np.bincount(idx, minlength=len(vals))
+    P_other = c1.sum()
+    n1 = int((lab != 0).sum())
+    assert abs(n1 - n * P_other) <= 5 * math.sqrt(n * P_other * (1 - P_other)) + 1, (n1, n * P_other)
+    exp = cells * n
+    big = exp >= 5
+    o = np.append(obs[big], obs[~big].sum())
+    e = np.append(exp[big], exp[~big].sum())
+    chi2 = ((o - e) ** 2 / e).sum()
+    assert stats.chi2.sf(chi2, len(e) - 1) > 1e-4
+
+
+def test_ipe_hint_labels_match_unpruned_law(cuda):
+    """Label hints (right, wrong, out of range -> first sweep) leave the
+    (label, D~) law of the k = 40 case unchanged (two-sample chi^2 against the
+    full sampler)."""
+    rng = np.random.default_rng(12)
+    d, k, eps, Q = 40, 40, 0.1, 13
+    x = rng.standard_normal(d).astype(np.float32)
+    C = (x[None] + rng.uniform(0.7, 1.3, (k, 1)) * rng.standard_normal((k, d)) / math.sqrt(d) * 1.5)
+    C = C.astype(np.float32)
+    n = 400_000
+    lb, mb, *_ = _run_rows(x, C, n, eps, Q, cuda, 2, False)
+    kb = lb.astype(np.int64) * 10**9 + np.round(mb * 1e3).astype(np.int64)
+    for seed, hint in ((4, int(((C - x) ** 2).sum(1).argmin())), (5, 17), (6, 999)):
+        la, ma, *_ = _run_rows(x, C, n, eps, Q, cuda, seed, True, hint=hint)
+        ka = la.astype(np.int64) * 10**9 + np.round(ma * 1e3).astype(np.int64)
+        keys, inv = np.unique(np.concatenate([ka, kb]), return_inverse=True)
+        ca = np.bincount(inv[:n], minlength=len(keys))
+        cb = np.bincount(inv[n:], minlength=len(keys))
+        keep = (ca + cb) >= 20
+        table = np.stack([np.append(ca[keep], ca[~keep].sum()), np.append(cb[keep], cb[~keep].sum())])
+        table = table[:, table.sum(0) > 0]
+        assert table.shape[1] >= 3
+        assert stats.chi2_contingency(table)[1] > 1e-4, hint
+
+
+@pytest.mark.parametrize("with_hint", [False, True])
+def test_ipe_pruned_rows_invariant_to_grouping(cuda, with_hint):
+    """Every pair's outcome depends on its row's threshold and its own
+    stream only: the rows of a shard that starts at global row 7 (another
+    workgroup grouping, another lane per row) get bit-identical labels and
+    estimates - the property behind sharded fits equal to one rank's."""
+    rng = np.random.default_rng(31)
+    n, d, k, eps, Q = 6000, 64, 200, 0.25, 13
+    ctr = rng.standard_normal((20, d)) * 3
+    X = (ctr[rng.integers(0, 20, n)] + rng.standard_normal((n, d))).astype(np.float32)
+    Cn = (ctr[rng.integers(0, 20, k)] + 0.5 * rng.standard_normal((k, d))).astype(np.float32)
+    Xt = torch.tensor(X, device=cuda)
+    Ct = torch.tensor(Cn, device=cuda)
+    xn = (Xt * Xt).sum(1)
+    cn = (Ct * Ct).sum(1)
+    kp, dp = 208, 64
+    frag = K.ipe_center_fragments(Ct, kp, dp)
+    hint = torch.tensor(rng.integers(0, k, n).astype(np.int32), device=cuda) if with_hint else None
+    outs = []
+    for off in (0, 7):
+        m = n - off
+        lab = torch.empty(m, dtype=torch.int32, device=cuda)
+        mind = torch.empty(m, dtype=torch.float32, device=cuda)
+        K.ipe_fused_native(Xt[off:], frag, xn[off:].contiguous(), cn, k, kp, dp, eps, Q,
+                           RngKey(9, "ipe", 1), RngKey(9, "band_select", 1), off, lab, mind,
+                           C=Ct if with_hint else None,
+                           hint_labels=hint[off:].contiguous() if with_hint else None)
+        outs.append((lab.cpu().numpy(), mind.cpu().numpy()))
+    torch.cuda.synchronize()
+    assert np.array_equal(outs[0][0][7:], outs[1][0])
+    assert np.array_equal(outs[0][1][7:], outs[1][1])

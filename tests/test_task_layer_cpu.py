@@ -116,3 +116,35 @@ def test_forest_per_tree_builds_fan_out_identically():
     b = RandomForestClassifier(n_jobs=3, **kw).fit(X, y)
     np.testing.assert_array_equal(a.predict_proba(X), b.predict_proba(X))
     assert [e.tree_.node_count for e in a.estimators_] == [e.tree_.node_count for e in b.estimators_]
+
+
+def test_nested_parallel_inherits_backend_and_registered_backend_pins():
+    """A Parallel inside a worker task sees the caller's parallel_backend
+    (the context stack travels with the task), and registered executors run
+    tasks through the same per-task wrapper as the threading backend."""
+    seen = []
+
+    def inner(i):
+        seen.append(effective_n_jobs(None))
+        return i
+
+    def outer(i):
+        return sum(Parallel(n_jobs=None)(delayed(inner)(j) for j in range(2)))
+
+    with parallel_backend("threading", n_jobs=3):
+        out = Parallel(n_jobs=2)(delayed(outer)(i) for i in range(4))
+    assert out == [1, 1, 1, 1]
+    assert seen and all(v == 3 for v in seen)
+
+    calls = []
+
+    class Exec(ThreadPoolExecutor):
+        def submit(self, fn, *a, **kw):
+            calls.append(getattr(fn, "__name__", ""))
+            return super().submit(fn, *a, **kw)
+
+    register_parallel_backend("pinned_exec", lambda n: Exec(max_workers=n))
+    with parallel_backend("pinned_exec", n_jobs=2):
+        r = Parallel(n_jobs=2)(delayed(lambda v: v * 2)(i) for i in range(3))
+    assert r == [0, 2, 4]
+    assert calls and all(c == "_run" for c in calls)
