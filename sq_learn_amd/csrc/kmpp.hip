@@ -1,71 +1,357 @@
-// Greedy k-means++ trial pass (reference sklearn/cluster/
-// _kmeans.py:153-247 and _dmeans.py:153-247): for the t candidate centres of
-// one step, every row's squared distance to each candidate and the t trial
-// potentials  sum_i w_i min(closest_i, |x_i - c_t|^2)  in ONE pass over X.
+// Exact accelerated greedy k-means++ (reference
+// sklearn/cluster/_kmeans.py:153-247 and _dmeans.py:153-247).
 //
-// The step is HBM-bound (k - 1 sequential passes over the whole matrix, t
-// <= 16 candidates, 2 t flops per loaded byte), so the kernel is shaped for
-// the stream: a wave owns 64 rows (one per lane for the arithmetic), loads
-// them as coalesced 32-feature tiles (8 rows x 128 B per load instruction,
-// next tile prefetched into registers while the current one is consumed)
-// and transposes them through its own LDS slot; the candidates are
-// wave-uniform (scalar loads / SGPR operands), direct-form fp32
-// distances sum_f (x_f - c_f)^2 (no |x|^2 + |c|^2 - 2 x.c cancellation), fp64
-// potential partials per block in a fixed order (deterministic), and the
-// distances written transposed D[t][n] so the caller picks the winning
-// trial's column contiguously.  Replaces a library GEMM + ~6 torch
-// elementwise passes over [n, t] temporaries per centre.
+// One step = t candidate centres sampled from the current potential, the t
+// trial potentials sum_i w_i min(closest_i, |x_i - c_j|^2), the best trial
+// kept.  The step used to be one full pass over X (k - 1 passes of 10 GB at
+// 10M x 256).  Here a row is read only when a candidate can improve it:
+//
+//  1. triangle screen (kmpp_screen_kernel): each row keeps its nearest chosen
+//     centre a(i) and closest_i = |x_i - C_a|^2.  |c_j - C_a|^2 > 4.01 closest_i
+//     proves |x_i - c_j| > |x_i - C_a| (with the fp32 rounding of both sides
+//     covered), so min(closest_i, D_ij) = closest_i without reading the row.
+//     Rows with a trial left go to the survivor list;
+//  2. certified int8 bound (kmpp_bound_kernel): survivors are read from an
+//     int8 copy (per-row scale s_i, stored error norm e_i >= |x_i - x~_i|):
+//     |x_i - c_j| >= |x~_i - c_j| - e_i with every fp32 rounding of
+//     |x~_i - c_j|^2 bounded; trials still undecided send the row on;
+//  3. exact pass (kmpp_exact_kernel): the fp32 direct-form distances
+//     sum_f (x_f - c_f)^2 (no norm-expansion cancellation) of the remaining
+//     rows; a trial that improves a row (D_ij < closest_i) records D_ij and
+//     adds w_i (closest_i - D_ij) to its per-block improvement sum.
+//
+// Potentials are fixed point: a row's potential is q_i = rint(w_i closest_i
+// scale) with one global power-of-two scale chosen so the total stays below
+// 2^53, so every sum of q's is an exact fp64 integer: the trial potentials
+// P - Delta_j (Delta_j = the improvement sums), the per-block totals and the
+// in-block prefix of the two-level sampler (kmpp_pick_kernel: block by
+// prefix over the block totals, then row by a workgroup scan of that block)
+// are order-independent - the same ids with or without the screens, on any
+// number of ranks.  The best trial's improvements are applied lazily (the
+// next screen / pick reads the improving rows' D from the mask), so no pass
+// touches rows that did not change.
 #include "common.h"
 
 namespace sq {
 
-constexpr int kKppTile = 32;          // features per staged tile (128 B of a row)
+constexpr int kKppTile = 32;          // fp32 features per staged tile (128 B of a row)
 constexpr int kKppStride = 36;        // LDS row stride in floats (16-B aligned, skewed banks)
+constexpr int kKqTile = 64;           // int8 features per staged tile (64 B of a row)
+constexpr int kKqStride = 17;         // LDS row stride in dwords (odd: conflict-free)
 
-template <int TMAX>
-__global__ void __launch_bounds__(256) kmpp_trials_kernel(
-    const float* __restrict__ X, long long ldx, int d, long long n, int t,
-    const float* __restrict__ cand, const double* __restrict__ closest,
-    const double* __restrict__ w, float* __restrict__ D, double* __restrict__ part) {
-  __shared__ double red[4][TMAX];
-  __shared__ __attribute__((aligned(16))) float tile[4][64 * kKppStride];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* my = tile[wave];
-  double pot[TMAX];
+SQ_DEV double kpp_q(float v, double wi, double scale) { return rint((double)v * wi * scale); }
+
+// ------------------------------------------------------------ int8 copy
+// u = rint(x / s) + 128 (s = max|x| / 127), e = |x - s (u - 128)| rounded up,
+// xq2 = |x~|^2 = s^2 |u - 128|^2
+__global__ void __launch_bounds__(256) kmpp_quantize_kernel(
+    const float* __restrict__ X, long long ldx, int d, long long n, uint8_t* __restrict__ Xq,
+    int dq, float* __restrict__ srow, float* __restrict__ erow, float* __restrict__ xq2) {
+  const int lane = threadIdx.x & 63;
+  const long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long i = w; i < n; i += nw) {
+    const float* x = X + i * ldx;
+    float mx = 0.0f;
+    for (int f = lane; f < d; f += 64) mx = fmaxf(mx, fabsf(x[f]));
 #pragma unroll
-  for (int j = 0; j < TMAX; ++j) pot[j] = 0.0;
-  const long long nblk = (n + 63) / 64;                      // 64-row groups, one per wave pass
-  const long long wstride = (long long)gridDim.x * 4;
-  const int ntiles = (d + kKppTile - 1) / kKppTile;
-  // coalesced tile load: lane -> (row r0 + 8 q + (lane >> 3), 16-B chunk lane & 7)
-  const int lrow = lane >> 3, lchunk = lane & 7;
-  float4 nxt[8];
-  auto load_tile = [&](long long r0, int tix) {
-    const int f = tix * kKppTile + lchunk * 4;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      long long r = r0 + q * 8 + lrow;
-      r = r < n ? r : n - 1;
-      nxt[q] = f < d ? *reinterpret_cast<const float4*>(X + r * ldx + f)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const float s = mx > 0.0f ? mx / 127.0f : 1.0f;
+    double e2 = 0.0, q2 = 0.0;
+    for (int f = lane; f < dq; f += 64) {
+      float q = 0.0f;
+      if (f < d) {
+        q = fminf(fmaxf(rintf(x[f] / s), -127.0f), 127.0f);
+        const double r = (double)x[f] - (double)s * (double)q;
+        e2 += r * r;
+        q2 += (double)q * (double)q;
+      }
+      Xq[i * dq + f] = (uint8_t)((int)q + 128);
     }
-  };
-  long long g = (long long)blockIdx.x * 4 + wave;
-  if (g < nblk) load_tile(g * 64, 0);
-  for (; g < nblk; g += wstride) {
-    const long long r0 = g * 64;
-    const long long i = r0 + lane;
+    e2 = wave_sum(e2);
+    q2 = wave_sum(q2);
+    if (lane == 0) {
+      srow[i] = s;
+      erow[i] = (float)(sqrt(e2) * (1.0 + 1e-6)) * 1.000001f;
+      xq2[i] = (float)((double)s * (double)s * q2);
+    }
+  }
+}
+
+// ------------------------------------------------- first centre + scale
+// closest_i = direct-form |x_i - c0|^2, nearest_i = 0, per-block max of
+// w_i closest_i (the caller turns the global max into the fixed-point scale)
+__global__ void __launch_bounds__(256) kmpp_init_kernel(
+    const float* __restrict__ X, long long ldx, int d, long long n, const float* __restrict__ c0,
+    const double* __restrict__ w, float* __restrict__ closest, int* __restrict__ nearest,
+    double* __restrict__ bmax) {
+  __shared__ double red[256];
+  double m = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float* x = X + i * ldx;
+    float acc = 0.0f;
+    for (int f = 0; f < d; f += 4) {
+      const float4 x4 = *reinterpret_cast<const float4*>(x + f);
+      float e = x4.x - c0[f];
+      acc = fmaf(e, e, acc);
+      e = x4.y - c0[f + 1];
+      acc = fmaf(e, e, acc);
+      e = x4.z - c0[f + 2];
+      acc = fmaf(e, e, acc);
+      e = x4.w - c0[f + 3];
+      acc = fmaf(e, e, acc);
+    }
+    closest[i] = acc;
+    nearest[i] = 0;
+    m = fmax(m, (double)acc * (w ? w[i] : 1.0));
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bmax[blockIdx.x] = red[0];
+}
+
+// block b of the fixed row partition (rows [b R, b R + R)): exact fixed-point total
+__global__ void __launch_bounds__(256) kmpp_block_totals_kernel(
+    const float* __restrict__ closest, const double* __restrict__ w, long long n, long long R,
+    double scale, double* __restrict__ block_tot) {
+  __shared__ double red[256];
+  const long long r0 = (long long)blockIdx.x * R;
+  const long long r1 = r0 + R < n ? r0 + R : n;
+  double s = 0.0;
+  for (long long i = r0 + threadIdx.x; i < r1; i += 256) s += kpp_q(closest[i], w ? w[i] : 1.0, scale);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) block_tot[blockIdx.x] = red[0];
+}
+
+// ------------------------------------------- candidate-centre distances
+// grid (t, ceil(c / 64)): cc[j][m] = |cand_j - C_m|^2 (m < c), one wave per
+// centre; blocks (j, 0) also write cinfo[j] = (|c_j|^2, sum c_j, sum |c_j|)
+// and the zero-padded copy candq[j][dq]; the whole grid zeroes delta_part
+// and the list counters.
+__global__ void __launch_bounds__(256) kmpp_cc_kernel(
+    const float* __restrict__ cand, const float* __restrict__ C, int c, int d, int t,
+    float* __restrict__ cc, int ldcc, float* __restrict__ cinfo, float* __restrict__ candq, int dq,
+    double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
+  const int j = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* cj = cand + (size_t)j * d;
+  const long long gid = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+  const long long gsz = (long long)gridDim.x * gridDim.y * 256;
+  for (long long e = gid; e < ndp; e += gsz) delta_part[e] = 0.0;
+  if (gid < 4) counters[gid] = 0;
+  const int m0 = blockIdx.y * 64;
+  for (int m = m0 + wave; m < c && m < m0 + 64; m += 4) {
+    const float* cm = C + (size_t)m * d;
+    float acc = 0.0f;
+    for (int f = lane; f < d; f += 64) {
+      const float e = cj[f] - cm[f];
+      acc = fmaf(e, e, acc);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) cc[(size_t)j * ldcc + m] = acc;
+  }
+  if (blockIdx.y == 0) {
+    __shared__ float red[3][4];
+    float a = 0.f, s = 0.f, b = 0.f;
+    for (int f = threadIdx.x; f < dq; f += 256) {
+      const float v = f < d ? cj[f] : 0.0f;
+      candq[(size_t)j * dq + f] = v;
+      a = fmaf(v, v, a);
+      s += v;
+      b += fabsf(v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o, 64);
+      s += __shfl_xor(s, o, 64);
+      b += __shfl_xor(b, o, 64);
+    }
+    if (lane == 0) { red[0][wave] = a; red[1][wave] = s; red[2][wave] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      cinfo[j * 4 + 0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+      cinfo[j * 4 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+      // |sum c| and sum |c| only enter the bound as upper bounds: round up
+      cinfo[j * 4 + 2] = ((red[2][0] + red[2][1]) + (red[2][2] + red[2][3])) * 1.0001f;
+      cinfo[j * 4 + 3] = 0.0f;
+    }
+  }
+}
+
+// wave-aggregated append of this lane's item when ``take``
+SQ_DEV void wave_append(bool take, int value, int* __restrict__ list, int* __restrict__ counter) {
+  const unsigned long long b = __ballot(take);
+  if (b == 0ull) return;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(counter, (int)__popcll(b));
+  base = __shfl(base, 0, 64);
+  if (take) {
+    const unsigned long long below = b & ((1ull << lane) - 1ull);
+    list[base + (int)__popcll(below)] = value;
+  }
+}
+
+// ---------------------------------------------------- 1. triangle screen
+// lazy update of the previous step's winner (best_prev < 0: none), mask_out
+// cleared, rows with a live trial appended to surv (prune) or exact (!prune)
+__global__ void __launch_bounds__(256) kmpp_screen_kernel(
+    float* __restrict__ closest, int* __restrict__ nearest,
+    const uint16_t* __restrict__ mask_prev, const float* __restrict__ Dprev,
+    const int* __restrict__ best_prev, int c_prev, const float* __restrict__ cc, int ldcc, int t,
+    long long n, uint16_t* __restrict__ mask_out, int* __restrict__ surv, int* __restrict__ exact,
+    int* __restrict__ counters, int prune) {
+  const int bp = best_prev ? *best_prev : -1;
+  for (long long i0 = (long long)blockIdx.x * 256; i0 < n; i0 += (long long)gridDim.x * 256) {
+    const long long i = i0 + threadIdx.x;
+    bool live = false;
+    if (i < n) {
+      float cl = closest[i];
+      int a = nearest[i];
+      if (bp >= 0 && ((mask_prev[i] >> bp) & 1u)) {
+        cl = Dprev[(size_t)bp * n + i];
+        a = c_prev;
+        closest[i] = cl;
+        nearest[i] = a;
+      }
+      mask_out[i] = 0;
+      if (!prune) {
+        live = true;
+      } else if (cl > 0.0f) {
+        const float lim = 4.01f * cl;
+        for (int j = 0; j < t; ++j) live |= !(cc[(size_t)j * ldcc + a] > lim);
+      }
+    }
+    wave_append(live, (int)i, prune ? surv : exact, counters + (prune ? 0 : 1));
+  }
+}
+
+// ------------------------------------------------ 2. certified int8 bound
+template <int TMAX>
+__global__ void __launch_bounds__(256) kmpp_bound_kernel(
+    const uint8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
+    const float* __restrict__ erow, const float* __restrict__ xq2,
+    const float* __restrict__ closest, const float* __restrict__ candq,
+    const float* __restrict__ cinfo, int t, int d, const int* __restrict__ surv,
+    int* __restrict__ exact, int* __restrict__ counters) {
+  __shared__ uint32_t tile[4][64 * kKqStride];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* my = tile[wave];
+  const int cnt = counters[0];
+  const long long nb = (cnt + 63) / 64;
+  const int ntiles = dq / kKqTile + (dq % kKqTile ? 1 : 0);
+  // rigorous fp32 error of the int8 dot products: gamma_d = d u / (1 - d u)
+  const float gam = (float)((double)dq * 5.960464477539063e-08 / (1.0 - (double)dq * 5.960464477539063e-08));
+  const float rel = 3.0f * (float)(d + 2) * 5.960464477539063e-08f + 1e-6f;
+  for (long long b = (long long)blockIdx.x * 4 + wave; b < nb; b += (long long)gridDim.x * 4) {
+    const long long e = b * 64 + lane;
+    const int row = e < cnt ? surv[e] : -1;
     float acc[TMAX];
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) acc[j] = 0.0f;
     for (int tix = 0; tix < ntiles; ++tix) {
-      // stage the landed tile (in-order LDS within the wave: no barrier)
+      // stage: row slot q * 16 + (lane >> 2), 16-B chunk lane & 3
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        *reinterpret_cast<float4*>(my + (q * 8 + lrow) * kKppStride + lchunk * 4) = nxt[q];
-      // prefetch the next tile (or the next row group's first tile)
-      if (tix + 1 < ntiles) load_tile(r0, tix + 1);
-      else if (g + wstride < nblk) load_tile((g + wstride) * 64, 0);
+      for (int q = 0; q < 4; ++q) {
+        const int slot = q * 16 + (lane >> 2);
+        const int r = __shfl(row, slot, 64);
+        const int f = tix * kKqTile + (lane & 3) * 16;
+        uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+        if (r >= 0 && f < dq) v = *reinterpret_cast<const uint4*>(Xq + (size_t)r * dq + f);
+        uint32_t* dst = my + slot * kKqStride + (lane & 3) * 4;
+        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+      }
+      const int f0 = tix * kKqTile;
+      const int nw = min(kKqTile, dq - f0) / 4;
+      for (int k4 = 0; k4 < nw; ++k4) {
+        const uint32_t wv = my[lane * kKqStride + k4];
+        // (v_cvt_f32_ubyte0..3)
+        const float u0 = (float)(wv & 0xFFu), u1 = (float)((wv >> 8) & 0xFFu);
+        const float u2 = (float)((wv >> 16) & 0xFFu), u3 = (float)(wv >> 24);
+        const int f = f0 + 4 * k4;
+#pragma unroll
+        for (int j = 0; j < TMAX; ++j) {
+          if (j < t) {
+            const float* cj = candq + (size_t)j * dq + f;
+            float a = acc[j];
+            a = fmaf(u0, cj[0], a);
+            a = fmaf(u1, cj[1], a);
+            a = fmaf(u2, cj[2], a);
+            a = fmaf(u3, cj[3], a);
+            acc[j] = a;
+          }
+        }
+      }
+    }
+    bool need = false;
+    if (row >= 0) {
+      const float cl = closest[row];
+      const float s = srow[row], er = erow[row], q2 = xq2[row];
+      const float lim = cl * (1.0f + rel);
+#pragma unroll
+      for (int j = 0; j < TMAX; ++j) {
+        if (j < t) {
+          const float cn = cinfo[j * 4 + 0], cs = cinfo[j * 4 + 1], ca = cinfo[j * 4 + 2];
+          // x~ . c = s (sum u c - 128 sum c);  |fl - exact| <= s 383 gamma sum|c| + 3 u |.|
+          const float dot = s * (acc[j] - 128.0f * cs);
+          const float Dq = (q2 + cn) - 2.0f * dot;
+          const float E = 2.0f * s * 400.0f * gam * ca + 1e-6f * (q2 + cn + 2.0f * fabsf(dot));
+          const float lb2 = Dq - E;
+          float lb = 0.0f;
+          if (lb2 > 0.0f) {
+            const float r = __builtin_amdgcn_sqrtf(lb2) * (1.0f - 1e-6f) - er;
+            lb = r > 0.0f ? r * r * (1.0f - 1e-6f) : 0.0f;
+          }
+          need |= !(lb > lim);
+        }
+      }
+    }
+    wave_append(need, row, exact, counters + 1);
+  }
+}
+
+// ------------------------------------------------------- 3. exact pass
+template <int TMAX>
+__global__ void __launch_bounds__(256) kmpp_exact_kernel(
+    const float* __restrict__ X, long long ldx, int d, long long n, int t,
+    const float* __restrict__ cand, const float* __restrict__ closest,
+    const double* __restrict__ w, double scale, const int* __restrict__ exact,
+    const int* __restrict__ counters, uint16_t* __restrict__ mask_out, float* __restrict__ Dout,
+    double* __restrict__ delta_part, long long R) {
+  __shared__ __attribute__((aligned(16))) float tile[4][64 * kKppStride];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* my = tile[wave];
+  const int cnt = counters[1];
+  const long long nb = (cnt + 63) / 64;
+  const int ntiles = (d + kKppTile - 1) / kKppTile;
+  const int lrow = lane >> 3, lchunk = lane & 7;
+  for (long long b = (long long)blockIdx.x * 4 + wave; b < nb; b += (long long)gridDim.x * 4) {
+    const long long e = b * 64 + lane;
+    const int row = e < cnt ? exact[e] : -1;
+    float acc[TMAX];
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) acc[j] = 0.0f;
+    for (int tix = 0; tix < ntiles; ++tix) {
+      // stage: row slot q * 8 + (lane >> 3), 16-B chunk lane & 7
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int slot = q * 8 + lrow;
+        const int r = __shfl(row, slot, 64);
+        const int f = tix * kKppTile + lchunk * 4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r >= 0 && f < d) v = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + f);
+        *reinterpret_cast<float4*>(my + slot * kKppStride + lchunk * 4) = v;
+      }
       const int f0 = tix * kKppTile;
       const int fl = min(kKppTile, d - f0);
 #pragma unroll
@@ -77,39 +363,115 @@ __global__ void __launch_bounds__(256) kmpp_trials_kernel(
         for (int j = 0; j < TMAX; ++j) {
           if (j < t) {
             const float* c = cand + (size_t)j * d + f;
-            float e = x4.x - c[0];
-            acc[j] = fmaf(e, e, acc[j]);
-            e = x4.y - c[1];
-            acc[j] = fmaf(e, e, acc[j]);
-            e = x4.z - c[2];
-            acc[j] = fmaf(e, e, acc[j]);
-            e = x4.w - c[3];
-            acc[j] = fmaf(e, e, acc[j]);
+            float ev = x4.x - c[0];
+            acc[j] = fmaf(ev, ev, acc[j]);
+            ev = x4.y - c[1];
+            acc[j] = fmaf(ev, ev, acc[j]);
+            ev = x4.z - c[2];
+            acc[j] = fmaf(ev, ev, acc[j]);
+            ev = x4.w - c[3];
+            acc[j] = fmaf(ev, ev, acc[j]);
           }
         }
       }
     }
-    if (i < n) {
-      const double cl = closest[i];
-      const double wi = w ? w[i] : 1.0;
+    if (row >= 0) {
+      const float cl = closest[row];
+      const double wi = w ? w[row] : 1.0;
+      const double qcl = kpp_q(cl, wi, scale);
+      const long long blk = (long long)row / R;
+      uint32_t m = 0;
 #pragma unroll
       for (int j = 0; j < TMAX; ++j) {
-        if (j < t) {
-          D[(size_t)j * n + i] = acc[j];
-          pot[j] += wi * fmin(cl, (double)acc[j]);
+        if (j < t && acc[j] < cl) {
+          m |= 1u << j;
+          Dout[(size_t)j * n + row] = acc[j];
+          const double dq = qcl - kpp_q(acc[j], wi, scale);
+          if (dq != 0.0) atomicAdd(delta_part + blk * t + j, dq);
         }
       }
+      mask_out[row] = (uint16_t)m;
     }
   }
-#pragma unroll
-  for (int j = 0; j < TMAX; ++j) {
-    const double s = wave_sum(pot[j]);
-    if (lane == 0) red[wave][j] = s;
+}
+
+// -------------------------------------------------- two-level sampling
+// One workgroup per value v: the first row (in row order) whose inclusive
+// fixed-point prefix reaches v - np.searchsorted(stable_cumsum, v) on the
+// current potentials (after the winning trial of mask / D / best).
+__global__ void __launch_bounds__(256) kmpp_pick_kernel(
+    const double* __restrict__ block_tot, int G, long long R, long long n,
+    const double* __restrict__ vals, const float* __restrict__ closest,
+    const uint16_t* __restrict__ mask, const float* __restrict__ D, const int* __restrict__ best,
+    const double* __restrict__ w, double scale, long long* __restrict__ pos) {
+  __shared__ double sc[256];
+  __shared__ long long found;
+  __shared__ double base;
+  const double v = vals[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int bp = best ? *best : -1;
+  // ---- block: per-thread chunk sums, WG exclusive scan, first crossing
+  const int chunk = (G + 255) / 256;
+  const int g0 = min(G, tid * chunk), g1 = min(G, g0 + chunk);
+  double s = 0.0;
+  for (int g = g0; g < g1; ++g) s += block_tot[g];
+  sc[tid] = s;
+  if (tid == 0) found = (long long)G - 1;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {   // Hillis-Steele inclusive scan (exact integers)
+    const double a = tid >= o ? sc[tid - o] : 0.0;
+    __syncthreads();
+    sc[tid] += a;
+    __syncthreads();
+  }
+  double run = sc[tid] - s;   // exclusive prefix of this thread's chunk
+  long long hit = -1;
+  for (int g = g0; g < g1; ++g) {
+    run += block_tot[g];
+    if (run >= v) { hit = g; break; }
+  }
+  if (hit >= 0) atomicMin(&found, hit);
+  __syncthreads();
+  const long long bsel = found;
+  // exclusive prefix of the chosen block (every thread recomputes the same sum)
+  if (tid == 0) {
+    double p = 0.0;
+    for (long long g = 0; g < bsel; ++g) p += block_tot[g];
+    base = p;
   }
   __syncthreads();
-  if (threadIdx.x < t)
-    part[(size_t)blockIdx.x * t + threadIdx.x] =
-        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  const double resid = v - base;
+  // ---- row within the block
+  const long long r0 = bsel * R;
+  const long long r1 = r0 + R < n ? r0 + R : n;
+  const long long rchunk = (r1 - r0 + 255) / 256;
+  const long long a0 = min(r1, r0 + tid * rchunk), a1 = min(r1, a0 + rchunk);
+  auto qrow = [&](long long i) -> double {
+    float cl = closest[i];
+    if (bp >= 0 && ((mask[i] >> bp) & 1u)) cl = D[(size_t)bp * n + i];
+    return kpp_q(cl, w ? w[i] : 1.0, scale);
+  };
+  s = 0.0;
+  for (long long i = a0; i < a1; ++i) s += qrow(i);
+  __syncthreads();
+  sc[tid] = s;
+  if (tid == 0) found = r1 > r0 ? r1 - 1 : (n > 0 ? n - 1 : 0);
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const double a = tid >= o ? sc[tid - o] : 0.0;
+    __syncthreads();
+    sc[tid] += a;
+    __syncthreads();
+  }
+  run = sc[tid] - s;
+  hit = -1;
+  for (long long i = a0; i < a1; ++i) {
+    run += qrow(i);
+    if (run >= resid) { hit = i; break; }
+  }
+  if (hit >= 0) atomicMin(&found, hit);
+  __syncthreads();
+  if (tid == 0) pos[blockIdx.x] = found;
 }
 
 }  // namespace sq
@@ -118,28 +480,115 @@ using namespace sq;
 
 extern "C" {
 
-// X fp32 [n][ldx] (d <= ldx, d % 4 == 0, 16-B aligned rows), cand fp32 [t][d],
-// closest fp64 [n], w fp64 [n] or null, D fp32 [t][n], part fp64 [grid][t]
-// with grid = sq_kmpp_grid(n).  part rows are summed by the caller.
-int sq_kmpp_grid(long long n) {
-  const long long b = (n + 255) / 256;     // 4 waves x 64 rows per block pass
+static int kpp_grid(long long n) {
+  const long long b = (n + 255) / 256;
   return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
 }
 
-int sq_kmpp_trials(const void* X, long long ldx, int d, long long n, int t, const void* cand,
-                   const void* closest, const void* w, void* D, void* part, void* stream) {
+// Xq uint8 [n][dq] (dq = d rounded up to 16), srow / erow / xq2 fp32 [n]
+int sq_kmpp_quantize(const void* X, long long ldx, int d, long long n, void* Xq, int dq, void* srow,
+                     void* erow, void* xq2, void* stream) {
   if (n <= 0) return 0;
-  if (t <= 0 || t > 16 || d <= 0 || (d & 3) || ldx < d || (ldx & 3)) return (int)hipErrorInvalidValue;
-  const int grid = sq_kmpp_grid(n);
+  if (d <= 0 || dq < d || (dq & 15) || ldx < d) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_quantize_kernel, dim3(kpp_grid(n * 64 / 256 + 1)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)X, ldx, d, n, (uint8_t*)Xq, dq,
+                     (float*)srow, (float*)erow, (float*)xq2);
+  return (int)hipGetLastError();
+}
+
+// closest fp32 [n], nearest int32 [n], bmax fp64 [grid] with grid = sq_kmpp_grid(n)
+int sq_kmpp_grid(long long n) { return kpp_grid(n); }
+
+int sq_kmpp_init(const void* X, long long ldx, int d, long long n, const void* c0, const void* w,
+                 void* closest, void* nearest, void* bmax, void* stream) {
+  if (n <= 0) return 0;
+  if (d <= 0 || (d & 3) || ldx < d || (ldx & 3)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_init_kernel, dim3(kpp_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)X, ldx, d, n, (const float*)c0, (const double*)w,
+                     (float*)closest, (int*)nearest, (double*)bmax);
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_block_totals(const void* closest, const void* w, long long n, long long R, int G,
+                         double scale, void* block_tot, void* stream) {
+  if (G <= 0) return 0;
+  hipLaunchKernelGGL(kmpp_block_totals_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)closest, (const double*)w, n, R, scale, (double*)block_tot);
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_cc(const void* cand, const void* C, int c, int d, int t, void* cc, int ldcc,
+               void* cinfo, void* candq, int dq, void* delta_part, long long ndp, void* counters,
+               void* stream) {
+  if (t < 1 || t > 16 || c < 0 || c > ldcc || dq < d) return (int)hipErrorInvalidValue;
+  const int gy = c > 0 ? (c + 63) / 64 : 1;
+  hipLaunchKernelGGL(kmpp_cc_kernel, dim3(t, gy), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)cand, (const float*)C, c, d, t, (float*)cc, ldcc,
+                     (float*)cinfo, (float*)candq, dq, (double*)delta_part, ndp, (int*)counters);
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_screen(void* closest, void* nearest, const void* mask_prev, const void* Dprev,
+                   const void* best_prev, int c_prev, const void* cc, int ldcc, int t, long long n,
+                   void* mask_out, void* surv, void* exact, void* counters, int prune,
+                   void* stream) {
+  if (n <= 0) return 0;
+  if (t < 1 || t > 16) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_screen_kernel, dim3(kpp_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                     (float*)closest, (int*)nearest, (const uint16_t*)mask_prev,
+                     (const float*)Dprev, (const int*)best_prev, c_prev, (const float*)cc, ldcc,
+                     t, n, (uint16_t*)mask_out, (int*)surv, (int*)exact, (int*)counters, prune);
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_bound(const void* Xq, int dq, const void* srow, const void* erow, const void* xq2,
+                  const void* closest, const void* candq, const void* cinfo, int t, int d,
+                  long long n, const void* surv, void* exact, void* counters, void* stream) {
+  if (n <= 0) return 0;
+  if (t < 1 || t > 16 || (dq & 15) || dq < d) return (int)hipErrorInvalidValue;
+  const int grid = kpp_grid(n);
   hipStream_t st = (hipStream_t)stream;
 #define LAUNCH(TM)                                                                              \
-  hipLaunchKernelGGL(kmpp_trials_kernel<TM>, dim3(grid), dim3(256), 0, st, (const float*)X,   \
-                     ldx, d, n, t, (const float*)cand, (const double*)closest,                 \
-                     (const double*)w, (float*)D, (double*)part)
+  hipLaunchKernelGGL(kmpp_bound_kernel<TM>, dim3(grid), dim3(256), 0, st, (const uint8_t*)Xq,  \
+                     dq, (const float*)srow, (const float*)erow, (const float*)xq2,            \
+                     (const float*)closest, (const float*)candq, (const float*)cinfo, t, d,    \
+                     (const int*)surv, (int*)exact, (int*)counters)
   if (t <= 4) LAUNCH(4);
   else if (t <= 8) LAUNCH(8);
   else LAUNCH(16);
 #undef LAUNCH
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_exact(const void* X, long long ldx, int d, long long n, int t, const void* cand,
+                  const void* closest, const void* w, double scale, const void* exact,
+                  const void* counters, void* mask_out, void* Dout, void* delta_part, long long R,
+                  void* stream) {
+  if (n <= 0) return 0;
+  if (t < 1 || t > 16 || d <= 0 || (d & 3) || ldx < d || (ldx & 3) || R <= 0)
+    return (int)hipErrorInvalidValue;
+  const int grid = kpp_grid(n);
+  hipStream_t st = (hipStream_t)stream;
+#define LAUNCH(TM)                                                                              \
+  hipLaunchKernelGGL(kmpp_exact_kernel<TM>, dim3(grid), dim3(256), 0, st, (const float*)X, ldx, \
+                     d, n, t, (const float*)cand, (const float*)closest, (const double*)w,     \
+                     scale, (const int*)exact, (const int*)counters, (uint16_t*)mask_out,      \
+                     (float*)Dout, (double*)delta_part, R)
+  if (t <= 4) LAUNCH(4);
+  else if (t <= 8) LAUNCH(8);
+  else LAUNCH(16);
+#undef LAUNCH
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_pick(const void* block_tot, int G, long long R, long long n, const void* vals, int t,
+                 const void* closest, const void* mask, const void* D, const void* best,
+                 const void* w, double scale, void* pos, void* stream) {
+  if (t < 1 || G < 1 || n <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_pick_kernel, dim3(t), dim3(256), 0, (hipStream_t)stream,
+                     (const double*)block_tot, G, R, n, (const double*)vals,
+                     (const float*)closest, (const uint16_t*)mask, (const float*)D,
+                     (const int*)best, (const double*)w, scale, (long long*)pos);
   return (int)hipGetLastError();
 }
 

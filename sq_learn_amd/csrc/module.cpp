@@ -103,8 +103,26 @@ __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const
 __attribute__((weak)) int sq_sum_f32(const void*, long long, void*, int, void*, void*);
 // kmpp.hip
 __attribute__((weak)) int sq_kmpp_grid(long long);
-__attribute__((weak)) int sq_kmpp_trials(const void*, long long, int, long long, int, const void*,
-                                         const void*, const void*, void*, void*, void*);
+__attribute__((weak)) int sq_kmpp_quantize(const void*, long long, int, long long, void*, int, void*,
+                                           void*, void*, void*);
+__attribute__((weak)) int sq_kmpp_init(const void*, long long, int, long long, const void*,
+                                       const void*, void*, void*, void*, void*);
+__attribute__((weak)) int sq_kmpp_block_totals(const void*, const void*, long long, long long, int,
+                                               double, void*, void*);
+__attribute__((weak)) int sq_kmpp_cc(const void*, const void*, int, int, int, void*, int, void*,
+                                     void*, int, void*, long long, void*, void*);
+__attribute__((weak)) int sq_kmpp_screen(void*, void*, const void*, const void*, const void*, int,
+                                         const void*, int, int, long long, void*, void*, void*,
+                                         void*, int, void*);
+__attribute__((weak)) int sq_kmpp_bound(const void*, int, const void*, const void*, const void*,
+                                        const void*, const void*, const void*, int, int,
+                                        long long, const void*, void*, void*, void*);
+__attribute__((weak)) int sq_kmpp_exact(const void*, long long, int, long long, int, const void*,
+                                        const void*, const void*, double, const void*,
+                                        const void*, void*, void*, void*, long long, void*);
+__attribute__((weak)) int sq_kmpp_pick(const void*, int, long long, long long, const void*, int,
+                                       const void*, const void*, const void*, const void*,
+                                       const void*, double, void*, void*);
 // estep_f32.hip
 __attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, void*, void*, void*,
                                        void*, void*, int, void*, long long, int, int, double,
@@ -409,13 +427,79 @@ static PyObject* py_kmpp_grid(PyObject*, PyObject* a) {
   return PyLong_FromLong(sq_kmpp_grid(n));
 }
 
-static PyObject* py_kmpp_trials(PyObject*, PyObject* a) {
-  unsigned long long X, cand, closest, w, D, part, st; long long ldx, n; int d, t;
-  if (!PyArg_ParseTuple(a, "KLiLiKKKKKK", &X, &ldx, &d, &n, &t, &cand, &closest, &w, &D, &part,
-                        &st))
+static PyObject* py_kmpp_quantize(PyObject*, PyObject* a) {
+  unsigned long long X, Xq, sr, er, q2, st; long long ldx, n; int d, dq;
+  if (!PyArg_ParseTuple(a, "KLiLKiKKKK", &X, &ldx, &d, &n, &Xq, &dq, &sr, &er, &q2, &st))
     return nullptr;
-  CHECK(sq_kmpp_trials)
-  return ret(sq_kmpp_trials(P(X), ldx, d, n, t, P(cand), P(closest), P(w), P(D), P(part), P(st)));
+  CHECK(sq_kmpp_quantize)
+  return ret(sq_kmpp_quantize(P(X), ldx, d, n, P(Xq), dq, P(sr), P(er), P(q2), P(st)));
+}
+
+static PyObject* py_kmpp_init(PyObject*, PyObject* a) {
+  unsigned long long X, c0, w, cl, nr, bm, st; long long ldx, n; int d;
+  if (!PyArg_ParseTuple(a, "KLiLKKKKKK", &X, &ldx, &d, &n, &c0, &w, &cl, &nr, &bm, &st))
+    return nullptr;
+  CHECK(sq_kmpp_init)
+  return ret(sq_kmpp_init(P(X), ldx, d, n, P(c0), P(w), P(cl), P(nr), P(bm), P(st)));
+}
+
+static PyObject* py_kmpp_block_totals(PyObject*, PyObject* a) {
+  unsigned long long cl, w, bt, st; long long n, R; int G; double scale;
+  if (!PyArg_ParseTuple(a, "KKLLidKK", &cl, &w, &n, &R, &G, &scale, &bt, &st)) return nullptr;
+  CHECK(sq_kmpp_block_totals)
+  return ret(sq_kmpp_block_totals(P(cl), P(w), n, R, G, scale, P(bt), P(st)));
+}
+
+static PyObject* py_kmpp_cc(PyObject*, PyObject* a) {
+  unsigned long long cand, C, cc, ci, cq, dp, cnt, st; int c, d, t, ldcc, dq; long long ndp;
+  if (!PyArg_ParseTuple(a, "KKiiiKiKKiKLKK", &cand, &C, &c, &d, &t, &cc, &ldcc, &ci, &cq, &dq, &dp,
+                        &ndp, &cnt, &st))
+    return nullptr;
+  CHECK(sq_kmpp_cc)
+  return ret(sq_kmpp_cc(P(cand), P(C), c, d, t, P(cc), ldcc, P(ci), P(cq), dq, P(dp), ndp, P(cnt),
+                        P(st)));
+}
+
+static PyObject* py_kmpp_screen(PyObject*, PyObject* a) {
+  unsigned long long cl, nr, mp, Dp, bp, cc, mo, sv, ex, cnt, st; int cp, ldcc, t, prune;
+  long long n;
+  if (!PyArg_ParseTuple(a, "KKKKKiKiiLKKKKiK", &cl, &nr, &mp, &Dp, &bp, &cp, &cc, &ldcc, &t, &n,
+                        &mo, &sv, &ex, &cnt, &prune, &st))
+    return nullptr;
+  CHECK(sq_kmpp_screen)
+  return ret(sq_kmpp_screen(P(cl), P(nr), P(mp), P(Dp), P(bp), cp, P(cc), ldcc, t, n, P(mo), P(sv),
+                            P(ex), P(cnt), prune, P(st)));
+}
+
+static PyObject* py_kmpp_bound(PyObject*, PyObject* a) {
+  unsigned long long Xq, sr, er, q2, cl, cq, ci, sv, ex, cnt, st; int dq, t, d; long long n;
+  if (!PyArg_ParseTuple(a, "KiKKKKKKiiLKKKK", &Xq, &dq, &sr, &er, &q2, &cl, &cq, &ci, &t, &d, &n,
+                        &sv, &ex, &cnt, &st))
+    return nullptr;
+  CHECK(sq_kmpp_bound)
+  return ret(sq_kmpp_bound(P(Xq), dq, P(sr), P(er), P(q2), P(cl), P(cq), P(ci), t, d, n, P(sv),
+                           P(ex), P(cnt), P(st)));
+}
+
+static PyObject* py_kmpp_exact(PyObject*, PyObject* a) {
+  unsigned long long X, cand, cl, w, ex, cnt, mo, Do, dp, st; long long ldx, n, R; int d, t;
+  double scale;
+  if (!PyArg_ParseTuple(a, "KLiLiKKKdKKKKKLK", &X, &ldx, &d, &n, &t, &cand, &cl, &w, &scale, &ex,
+                        &cnt, &mo, &Do, &dp, &R, &st))
+    return nullptr;
+  CHECK(sq_kmpp_exact)
+  return ret(sq_kmpp_exact(P(X), ldx, d, n, t, P(cand), P(cl), P(w), scale, P(ex), P(cnt), P(mo),
+                           P(Do), P(dp), R, P(st)));
+}
+
+static PyObject* py_kmpp_pick(PyObject*, PyObject* a) {
+  unsigned long long bt, v, cl, m, D, b, w, pos, st; int G, t; long long R, n; double scale;
+  if (!PyArg_ParseTuple(a, "KiLLKiKKKKKdKK", &bt, &G, &R, &n, &v, &t, &cl, &m, &D, &b, &w, &scale,
+                        &pos, &st))
+    return nullptr;
+  CHECK(sq_kmpp_pick)
+  return ret(sq_kmpp_pick(P(bt), G, R, n, P(v), t, P(cl), P(m), P(D), P(b), P(w), scale, P(pos),
+                          P(st)));
 }
 
 static PyObject* py_sum_f32(PyObject*, PyObject* a) {
@@ -550,7 +634,14 @@ static PyMethodDef methods[] = {
     {"fill_mind", py_fill_mind, METH_VARARGS, "exact distance to the label for marked rows"},
     {"sum_f32", py_sum_f32, METH_VARARGS, "deterministic sum of a float vector"},
     {"kmpp_grid", py_kmpp_grid, METH_VARARGS, "k-means++ trial pass grid size"},
-    {"kmpp_trials", py_kmpp_trials, METH_VARARGS, "k-means++ trial distances + potentials"},
+    {"kmpp_quantize", py_kmpp_quantize, METH_VARARGS, "k-means++ int8 row copy + error norms"},
+    {"kmpp_init", py_kmpp_init, METH_VARARGS, "k-means++ first centre distances"},
+    {"kmpp_block_totals", py_kmpp_block_totals, METH_VARARGS, "k-means++ fixed-point block totals"},
+    {"kmpp_cc", py_kmpp_cc, METH_VARARGS, "k-means++ candidate-centre distances"},
+    {"kmpp_screen", py_kmpp_screen, METH_VARARGS, "k-means++ triangle screen + lazy update"},
+    {"kmpp_bound", py_kmpp_bound, METH_VARARGS, "k-means++ certified int8 bound"},
+    {"kmpp_exact", py_kmpp_exact, METH_VARARGS, "k-means++ exact fp32 trial distances"},
+    {"kmpp_pick", py_kmpp_pick, METH_VARARGS, "k-means++ two-level potential sampling"},
     {"rows_f64", py_rows_f64, METH_VARARGS, "exact fp64 E-step over a row list (fp64 MFMA)"},
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},

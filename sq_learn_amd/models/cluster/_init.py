@@ -13,12 +13,13 @@ current potential, the candidate ids, the argmin over trials and the
 closest-distance column are device tensors; the data-dependent parts are
 two small collectives per centre on a multi-rank run (owner-contributes
 all-reduce of the t packed candidate rows + ids, all-gather of the per-rank
-t trial potentials, which also carries the next prefix of shard totals).  The per-centre
-work is one pass over the shard: on the GPU the fused trial kernel
-(``csrc/kmpp.hip``: direct-form fp32 distances to the t candidates, the
-t potentials as fixed-order fp64 block partials, distances written
-transposed so the winner's column is contiguous); elsewhere ``X C^T``
-(library GEMM) with the min / sum epilogue in torch.
+t trial potentials, which also carries the next prefix of shard totals).  On
+the GPU each centre reads only the rows a candidate can improve
+(``csrc/kmpp.hip``: a triangle-inequality screen against each row's nearest
+chosen centre, a certified bound from an int8 copy of the rows, exact
+direct-form fp32 distances for the rest; fixed-point potentials so the
+result does not depend on the screens or the rank count); elsewhere
+``X C^T`` (library GEMM) with the min / sum epilogue in torch.
 
 ``kmeans_parallel`` is k-means|| (Bahmani et al. 2012), an option the
 reference does not have: O(log phi) oversampling rounds of ~l = 2k rows
@@ -88,12 +89,100 @@ def _pick_candidates(data: Data, cs, prefix, sizes, vals, xdtype):
     return packed[:, :d].to(xdtype), ids
 
 
+def _pick_candidates_native(data: Data, state, prefix, sizes, vals, xdtype):
+    """``_pick_candidates`` with the local search done by the device
+    two-level sampler (``KmppState.pick``: fixed-point block totals, then a
+    workgroup scan of the block) instead of a cumulative sum over the shard."""
+    comm = data.comm
+    X = data.X
+    t = vals.shape[0]
+    d = data.d
+    if comm.world_size == 1:
+        pos = state.pick(vals).clamp(0, max(data.n_local - 1, 0))
+        return X[pos].to(xdtype), (pos + data.row_offset).clamp(0, data.n_global - 1)
+    ends = prefix[1:]
+    ok = (ends[None, :] >= vals[:, None]) & (sizes[None, :] > 0)          # [t, W]
+    nz = torch.nonzero(sizes > 0)
+    last = nz[-1, 0] if nz.numel() else torch.zeros((), dtype=torch.int64, device=vals.device)
+    owner = torch.where(ok.any(1), ok.to(torch.int32).argmax(1).to(torch.int64), last)
+    local_vals = vals - prefix[comm.rank]
+    wd = torch.float64
+    packed = torch.zeros((t, d + 1), dtype=wd, device=X.device)
+    if data.n_local > 0:
+        pos = state.pick(local_vals).clamp(0, data.n_local - 1)
+        mine = (owner == comm.rank)
+        packed[:, :d] = torch.where(mine[:, None], X[pos].to(wd), torch.zeros((), dtype=wd,
+                                                                             device=X.device))
+        packed[:, d] = torch.where(mine, (pos + data.row_offset).to(wd),
+                                   torch.zeros((), dtype=wd, device=X.device))
+    comm.all_reduce_(packed)   # ids < 2^53: exact in fp64
+    ids = packed[:, d].round().to(torch.int64).clamp(0, data.n_global - 1)
+    return packed[:, :d].to(xdtype), ids
+
+
+def _kmeans_plusplus_native(data: Data, k, rs, t, w, prune, stats=None):
+    """The exact accelerated k-means++ on the device (csrc/kmpp.hip, see
+    ``ops.kmeans.KmppState``): per centre one pick (two-level sampling of
+    the t candidates), one trial pass that reads only the rows a candidate
+    can improve, two small collectives on a multi-rank run; potentials in
+    exact fixed point (identical results with or without the screens and on
+    any number of ranks)."""
+    from ...ops.kmeans import KmppState
+    X = data.X
+    comm = data.comm
+    dev = X.device
+    n = data.n_global
+    center_id = int(rs.randint(n))
+    draws = torch.as_tensor(rs.random_sample((max(k - 1, 0), t)), dtype=torch.float64, device=dev)
+    ids = torch.empty(k, dtype=torch.int64, device=dev)
+    ids[0] = center_id
+    c0 = gather_rows(data, [center_id]).to(torch.float32)
+    centers = torch.empty((k, data.d), dtype=torch.float32, device=dev)
+    centers[0] = c0[0]
+    state = KmppState(X, k, t, w=w, prune=prune)
+    mx = state.first_centre(c0[0])
+    comm.all_reduce_(mx, op="max")
+    P = state.set_scale(mx.item(), n)                                   # local total [1]
+    ts = torch.cat([P, torch.tensor([float(data.n_local)], dtype=torch.float64, device=dev)])
+    g = torch.stack(comm.all_gather(ts))                                  # [W, 2]
+    totals, sizes = g[:, 0].contiguous(), g[:, 1].contiguous()
+    W = comm.world_size
+    zero = torch.zeros(1, dtype=torch.float64, device=dev)
+    for c in range(1, k):
+        prefix = torch.cat([zero, torch.cumsum(totals, 0)])
+        vals = draws[c - 1] * prefix[-1]
+        cands, cand_ids = _pick_candidates_native(data, state, prefix, sizes, vals, torch.float32)
+        delta = state.trials(cands, centers, c)
+        pots_loc = P - delta                                              # exact integers
+        if W > 1:
+            allp = torch.stack(comm.all_gather(pots_loc.reshape(t)))     # [W, t]
+            pots = allp.sum(0)
+        else:
+            allp = pots_loc.reshape(1, t)
+            pots = pots_loc
+        best = torch.argmin(pots)
+        totals = allp.index_select(1, best.reshape(1))[:, 0].contiguous()
+        P = totals[comm.rank:comm.rank + 1].clone()
+        state.apply(best, c)
+        centers[c] = cands.index_select(0, best.reshape(1))[0]
+        ids[c] = cand_ids.index_select(0, best.reshape(1))[0]
+        if stats is not None:
+            stats.append(state.list_counts())
+    return centers, ids.cpu().numpy()
+
+
 def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
-                    n_local_trials=None, sample_weight=None):
+                    n_local_trials=None, sample_weight=None, prune=None, stats=None):
     """Returns (centers [k, d] tensor on the data device, global indices).
 
     ``sample_weight`` (framework extension, used by k-means||): the potential
     of a row is w * d^2.
+
+    GPU (fp32 rows, d % 4 == 0): the exact accelerated k-means++ of
+    ``_kmeans_plusplus_native`` (``prune``: the triangle / int8 screens,
+    default on; ``SQ_KMPP_PRUNE=0`` turns them off; ``stats``: a list that
+    receives per centre [survivor rows, exact rows]).  Elsewhere the torch
+    path below.
 
     Collectives on a multi-rank run: TWO per centre, both tiny and with no
     host synchronisation - the all-reduce of the packed candidate rows + ids
@@ -102,6 +191,7 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     (summed in rank order, identical on every rank) and, at the winning
     trial, every shard's new potential total - the prefix the next centre's
     search needs (the former separate all-gather of the shard totals)."""
+    import os
     X = data.X
     comm = data.comm
     n = data.n_global
@@ -111,13 +201,20 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
         n_local_trials = 2 + int(np.log(k))
     t = int(n_local_trials)
     Xf = X if X.dtype in (torch.float32, torch.float64) else X.float()
+    rs = random_state
+    w = None if sample_weight is None else sample_weight.to(torch.float64).to(dev).contiguous()
+    native = (dev.type == "cuda" and Xf.dtype == torch.float32 and Xf.dim() == 2
+              and Xf.stride(1) == 1 and Xf.stride(0) % 4 == 0 and data.d % 4 == 0
+              and Xf.data_ptr() % 16 == 0 and 1 <= t <= 16 and k >= 1)
+    if native:
+        if prune is None:
+            prune = os.environ.get("SQ_KMPP_PRUNE", "1") != "0"
+        return _kmeans_plusplus_native(data, k, rs, t, w, bool(prune), stats)
     if x_squared_norms is None:
         x_squared_norms = L.row_norms_sq(X)
     xn = x_squared_norms.to(Xf.dtype)
-    rs = random_state
     center_id = int(rs.randint(n))
     draws = torch.as_tensor(rs.random_sample((max(k - 1, 0), t)), dtype=torch.float64, device=dev)
-    w = None if sample_weight is None else sample_weight.to(torch.float64).to(dev).contiguous()
     ids = torch.empty(k, dtype=torch.int64, device=dev)
     ids[0] = center_id
     c0 = gather_rows(data, [center_id]).to(Xf.dtype)
@@ -134,13 +231,6 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
                                                    device=dev)])
     g = torch.stack(comm.all_gather(ts))                                  # [W, 2]
     totals, sizes = g[:, 0].contiguous(), g[:, 1].contiguous()
-    # fused HIP trial pass (csrc/kmpp.hip): one HBM pass over the shard per
-    # centre, no [n, t] temporaries; the torch path below is the CPU / odd-
-    # shape fallback
-    native = (dev.type == "cuda" and Xf.dtype == torch.float32 and Xf.dim() == 2
-              and Xf.stride(1) == 1 and Xf.stride(0) == data.d and data.d % 4 == 0
-              and Xf.data_ptr() % 16 == 0 and 1 <= t <= 16)
-    D = part = None
     zero = torch.zeros(1, dtype=torch.float64, device=dev)
     for c in range(1, k):
         prefix = torch.cat([zero, torch.cumsum(totals, 0)])
@@ -148,21 +238,15 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
         vals = draws[c - 1] * current_pot
         cs = torch.cumsum(pot_rows, 0)
         cands, cand_ids = _pick_candidates(data, cs, prefix, sizes, vals, Xf.dtype)
-        if native:
-            D, pots_loc = K.kmpp_trials_native(Xf, cands.contiguous(), closest, w, D, part)
-        else:
-            newd = torch.minimum(closest[:, None], _sq_dist(Xf, cands, xn).double())   # [n_loc, t]
-            pots_loc = (newd if w is None else newd * w[:, None]).sum(0)
+        newd = torch.minimum(closest[:, None], _sq_dist(Xf, cands, xn).double())   # [n_loc, t]
+        pots_loc = (newd if w is None else newd * w[:, None]).sum(0)
         allp = torch.stack(comm.all_gather(pots_loc.reshape(t)))          # [W, t]
         pots = allp[0].clone()
         for r in range(1, W):                                             # rank order: replicated
             pots += allp[r]
         best = torch.argmin(pots)
         totals = allp.index_select(1, best.reshape(1))[:, 0].contiguous()
-        if native:
-            closest = torch.minimum(closest, D.index_select(0, best.reshape(1))[0].double())
-        else:
-            closest = newd.index_select(1, best.reshape(1))[:, 0].contiguous()
+        closest = newd.index_select(1, best.reshape(1))[:, 0].contiguous()
         pot_rows = closest if w is None else closest * w
         centers[c] = cands.index_select(0, best.reshape(1))[0]
         ids[c] = cand_ids.index_select(0, best.reshape(1))[0]

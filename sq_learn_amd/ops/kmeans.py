@@ -741,31 +741,152 @@ def sum_f32_native(v, n, part, out, extra=0):
         raise RuntimeError(f"sum_f32 failed (hip error {rc})")
 
 
-# ------------------------------------------------- k-means++ trial pass
-def kmpp_trials_native(Xf, cand, closest, w=None, D=None, part=None):
-    """One greedy k-means++ step's trial pass (csrc/kmpp.hip): returns
-    (D fp32 [t, n] squared distances of every row to every candidate,
-    pots fp64 [t] = sum_i w_i min(closest_i, D[j, i]) over this shard,
-    summed over the kernel's block partials in a fixed order).  ``D`` /
-    ``part`` may be passed in to reuse buffers."""
-    n, ldx = Xf.shape
-    t, d = cand.shape
-    if n == 0:
-        return (torch.empty((t, 0), dtype=torch.float32, device=Xf.device),
-                torch.zeros(t, dtype=torch.float64, device=Xf.device))
-    assert Xf.dtype == torch.float32 and Xf.stride(1) == 1 and Xf.stride(0) == ldx
-    assert cand.dtype == torch.float32 and cand.is_contiguous() and d == ldx and d % 4 == 0
-    assert Xf.data_ptr() % 16 == 0 and 1 <= t <= 16
-    assert closest.dtype == torch.float64 and closest.numel() == n and closest.is_contiguous()
-    assert w is None or (w.dtype == torch.float64 and w.numel() == n and w.is_contiguous())
-    m = nat.native()
-    grid = m.kmpp_grid(int(n))
-    if D is None or D.shape != (t, n):
-        D = torch.empty((t, n), dtype=torch.float32, device=Xf.device)
-    if part is None or part.numel() < grid * t:
-        part = torch.empty(grid * t, dtype=torch.float64, device=Xf.device)
-    m.kmpp_trials(Xf.data_ptr(), int(ldx), int(d), int(n), int(t), cand.data_ptr(),
-                  closest.data_ptr(), 0 if w is None else w.data_ptr(), D.data_ptr(),
-                  part.data_ptr(), nat.stream_handle(Xf.device))
-    pots = part[:grid * t].view(grid, t).sum(0)
-    return D, pots
+# ------------------------------------------------- k-means++ (exact, pruned)
+class KmppState:
+    """Device state of the exact accelerated k-means++ (csrc/kmpp.hip) on
+    one shard: per-row closest distance (fp32) and nearest chosen centre, the
+    int8 row copy of the certified bound, the two (mask, D) buffers of the
+    lazily applied winner, the survivor / exact row lists, the fixed-point
+    block totals of the two-level sampler.  ``prune=False`` sends every row
+    through the exact pass (same results: the screens only skip rows whose
+    minimum provably stays the same)."""
+
+    def __init__(self, Xf, k, t, w=None, prune=True):
+        n, d = Xf.shape
+        dev = Xf.device
+        assert Xf.dtype == torch.float32 and Xf.stride(1) == 1 and d % 4 == 0
+        assert Xf.stride(0) % 4 == 0 and Xf.data_ptr() % 16 == 0 and 1 <= t <= 16
+        self.X, self.n, self.d, self.t, self.k = Xf, n, d, t, int(k)
+        self.ldx = Xf.stride(0)
+        self.w = None if w is None else w.to(device=dev, dtype=torch.float64).contiguous()
+        self.prune = bool(prune) and d <= 8192
+        self.dq = -(-d // 16) * 16
+        self.dev = dev
+        m = nat.native()
+        self.m = m
+        self.st = nat.stream_handle(dev)
+        G0 = m.kmpp_grid(max(n, 1))
+        self.R = max(1, -(-n // G0))
+        self.G = max(1, -(-n // self.R))
+        if self.prune and n:
+            self.Xq = torch.empty((n, self.dq), dtype=torch.uint8, device=dev)
+            self.srow = torch.empty(n, dtype=torch.float32, device=dev)
+            self.erow = torch.empty(n, dtype=torch.float32, device=dev)
+            self.xq2 = torch.empty(n, dtype=torch.float32, device=dev)
+            _rc(m.kmpp_quantize(Xf.data_ptr(), self.ldx, d, n, self.Xq.data_ptr(), self.dq,
+                                self.srow.data_ptr(), self.erow.data_ptr(), self.xq2.data_ptr(),
+                                self.st), "kmpp_quantize")
+        nn = max(n, 1)
+        self.closest = torch.empty(nn, dtype=torch.float32, device=dev)
+        self.nearest = torch.zeros(nn, dtype=torch.int32, device=dev)
+        self.mask = [torch.zeros(nn, dtype=torch.int16, device=dev) for _ in range(2)]
+        self.D = [torch.empty((t, nn), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.surv = torch.empty(nn, dtype=torch.int32, device=dev)
+        self.exact = torch.empty(nn, dtype=torch.int32, device=dev)
+        self.counters = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.cc = torch.zeros((t, self.k), dtype=torch.float32, device=dev)
+        self.cinfo = torch.zeros((t, 4), dtype=torch.float32, device=dev)
+        self.candq = torch.zeros((t, self.dq), dtype=torch.float32, device=dev)
+        self.delta = torch.zeros((self.G, t), dtype=torch.float64, device=dev)
+        self.block_tot = torch.zeros(self.G, dtype=torch.float64, device=dev)
+        self.pos = torch.zeros(t, dtype=torch.int64, device=dev)
+        self.cur = 0            # index of the (mask, D) pair the next trial pass writes
+        self.best = None        # device int32 [1]: the last step's winning trial
+        self.c_last = -1        # centre index of that winner
+        self.scale = 1.0
+
+    def first_centre(self, c0):
+        """closest / nearest for the first centre; returns the local max of
+        w * closest (device fp64 [1]) for the global fixed-point scale."""
+        bmax = torch.zeros(self.m.kmpp_grid(max(self.n, 1)), dtype=torch.float64, device=self.dev)
+        if self.n:
+            c0 = c0.to(torch.float32).contiguous()
+            _rc(self.m.kmpp_init(self.X.data_ptr(), self.ldx, self.d, self.n, c0.data_ptr(),
+                                 0 if self.w is None else self.w.data_ptr(),
+                                 self.closest.data_ptr(), self.nearest.data_ptr(), bmax.data_ptr(),
+                                 self.st), "kmpp_init")
+        return bmax.max().reshape(1)
+
+    def set_scale(self, max_pot, n_global):
+        """Power-of-two fixed-point scale with n_global * max_pot * scale <=
+        2^52 (every potential sum an exact fp64 integer); returns this
+        shard's total (device fp64 [1])."""
+        mx = float(max_pot)
+        self.scale = 1.0 if not mx > 0.0 else 2.0 ** math.floor(
+            math.log2(2.0 ** 52 / (max(n_global, 1) * mx)))
+        if self.n:
+            _rc(self.m.kmpp_block_totals(self.closest.data_ptr(),
+                                         0 if self.w is None else self.w.data_ptr(), self.n,
+                                         self.R, self.G, self.scale, self.block_tot.data_ptr(),
+                                         self.st), "kmpp_block_totals")
+        return self.block_tot.sum().reshape(1)
+
+    def pick(self, vals):
+        """Local rows of the potential values ``vals`` (device fp64 [t]):
+        first row whose inclusive prefix reaches each value."""
+        t = vals.numel()
+        if self.n == 0:
+            return torch.zeros(t, dtype=torch.int64, device=self.dev)
+        assert t <= self.pos.numel()
+        vals = vals.to(torch.float64).contiguous()
+        prev = 1 - self.cur
+        _rc(self.m.kmpp_pick(self.block_tot.data_ptr(), self.G, self.R, self.n, vals.data_ptr(), t,
+                             self.closest.data_ptr(), self.mask[prev].data_ptr(),
+                             self.D[prev].data_ptr(),
+                             0 if self.best is None else self.best.data_ptr(),
+                             0 if self.w is None else self.w.data_ptr(), self.scale,
+                             self.pos.data_ptr(), self.st), "kmpp_pick")
+        return self.pos[:t].clone()
+
+    def trials(self, cand, centers, c):
+        """Trial pass for the candidates ``cand`` [t, d] against the ``c``
+        centres chosen so far (``centers[:c]``): returns Delta (device fp64
+        [t]), the fixed-point improvement of each trial over this shard."""
+        t = cand.shape[0]
+        assert t == self.t and 1 <= c <= self.k
+        cand = cand.to(torch.float32).contiguous()
+        Cc = (centers if centers.dtype == torch.float32 else centers.float()).contiguous()
+        m, st = self.m, self.st
+        prev, cur = 1 - self.cur, self.cur
+        _rc(m.kmpp_cc(cand.data_ptr(), Cc.data_ptr(), int(c), self.d, t, self.cc.data_ptr(), self.k,
+                      self.cinfo.data_ptr(), self.candq.data_ptr(), self.dq, self.delta.data_ptr(),
+                      self.delta.numel(), self.counters.data_ptr(), st), "kmpp_cc")
+        if self.n:
+            _rc(m.kmpp_screen(self.closest.data_ptr(), self.nearest.data_ptr(),
+                              self.mask[prev].data_ptr(), self.D[prev].data_ptr(),
+                              0 if self.best is None else self.best.data_ptr(), self.c_last,
+                              self.cc.data_ptr(), self.k, t, self.n, self.mask[cur].data_ptr(),
+                              self.surv.data_ptr(), self.exact.data_ptr(),
+                              self.counters.data_ptr(), int(self.prune), st), "kmpp_screen")
+            if self.prune:
+                _rc(m.kmpp_bound(self.Xq.data_ptr(), self.dq, self.srow.data_ptr(),
+                                 self.erow.data_ptr(), self.xq2.data_ptr(),
+                                 self.closest.data_ptr(), self.candq.data_ptr(),
+                                 self.cinfo.data_ptr(), t, self.d, self.n, self.surv.data_ptr(),
+                                 self.exact.data_ptr(), self.counters.data_ptr(), st),
+                    "kmpp_bound")
+            _rc(m.kmpp_exact(self.X.data_ptr(), self.ldx, self.d, self.n, t, cand.data_ptr(),
+                             self.closest.data_ptr(), 0 if self.w is None else self.w.data_ptr(),
+                             self.scale, self.exact.data_ptr(), self.counters.data_ptr(),
+                             self.mask[cur].data_ptr(), self.D[cur].data_ptr(),
+                             self.delta.data_ptr(), self.R, st), "kmpp_exact")
+        return self.delta.sum(0)
+
+    def apply(self, best, c):
+        """The winning trial (device int64 scalar) of centre ``c``: block
+        totals lose its improvements; its rows are updated lazily by the next
+        screen / pick."""
+        self.block_tot -= self.delta.index_select(1, best.reshape(1))[:, 0]
+        self.best = best.reshape(1).to(torch.int32)
+        self.c_last = int(c)
+        self.cur ^= 1
+
+    def list_counts(self):
+        """[survivors of the triangle screen, rows of the exact pass] of the
+        last trial pass (host read; diagnostics)."""
+        return self.counters[:2].tolist()
+
+
+def _rc(rc, name):
+    if rc:
+        raise RuntimeError(f"{name} failed (hip error {rc})")

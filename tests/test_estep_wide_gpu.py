@@ -174,3 +174,18 @@ def test_qmeans_mnist_shape():
                  n_init=1, max_iter=10, random_state=0, device="cuda:0").fit(X)
     assert est.labels_.shape == (n,) and np.isfinite(est.inertia_)
     assert len(np.unique(est.labels_)) == k
+    # the final E-step ran on the centred fp32 rows at the returned centres:
+    # every label is a member of the fp64 delta-band there (rows within
+    # rounding of the band edge aside) and the inertia is the sum of the fp64
+    # minimum distances
+    mean = torch.from_numpy(np.asarray(est._mean, dtype=np.float64))
+    Xc = (torch.from_numpy(X) - mean.float()).double().cuda()
+    C = (torch.from_numpy(est.cluster_centers_) - mean).cuda()
+    D = _cdist2(Xc, C)
+    mn = D.min(1).values
+    near = _near_edge(D, mn, 0.5, rel=1e-7)
+    lab = torch.from_numpy(est.labels_.astype(np.int64)).cuda()
+    inband = D.gather(1, lab[:, None])[:, 0] <= mn + 0.5
+    assert int((~inband & ~near).sum()) == 0
+    assert int(near.sum()) < n // 1000
+    assert est.inertia_ == pytest.approx(float(mn.sum()), rel=1e-6)
