@@ -57,6 +57,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-hard", action="store_true", help="skip the overlapping-blobs extra")
     ap.add_argument("--no-mnist", action="store_true", help="skip the 70k x 784 (config 4) extra")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip the qPCA -> q-means pipeline (config 5) extra")
+    ap.add_argument("--pipeline-rows", type=int, default=50_000_000)
     return ap.parse_args(argv)
 
 
@@ -310,6 +313,22 @@ def _mnist_extra(extra, a, comm, dev):
         extra["mnist_error"] = repr(e)[:200]
 
 
+def _pipeline_extra(extra, a, comm, dev):
+    """BASELINE config 5: qPCA -> q-means on 50M x 128 (bf16, low rank + tail)
+    with failure-probability resampling (benchmarks/pipeline_bench.py
+    run_pipeline): per-stage seconds."""
+    try:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "benchmarks"))
+        from pipeline_bench import run_pipeline
+        res = run_pipeline(comm, dev, a.pipeline_rows)
+        tag = f"pipeline_{a.pipeline_rows // 1_000_000}Mx128"
+        for kk, v in res.items():
+            extra[f"{tag}_{kk}"] = round(v, 4) if isinstance(v, float) else v
+        torch.cuda.empty_cache()
+    except Exception as e:
+        extra["pipeline_error"] = repr(e)[:200]
+
+
 def _fit_extra(extra, a, sa, comm, dev, init, ipe=False, name=None):
     """Wall-clock of a whole QMeans.fit (prelude: eta, mu(A), condition
     number; centring; initialisation; ``fit_iters`` Lloyd iterations with
@@ -484,6 +503,10 @@ def main(argv=None):
         _qpca_extra(extra, "qpca_1Mx512_randomized_fit_s", sa2, comm, dev, "randomized")
         _qpca_extra(extra, "qpca_1Mx512_randomized_truetomo_fit_s", sa2, comm, dev, "randomized",
                     true_tomography=True)
+        del X2, sa2
+        torch.cuda.empty_cache()
+    if gpu and not a.no_pipeline:
+        _pipeline_extra(extra, a, comm, dev)
 
     if rank == 0:
         out = {

@@ -7,12 +7,16 @@ resampling, row-sharded over the GPUs of one node.
 
 Steps (all on device, sharded rows, RCCL collectives):
   1. synthetic 50M x 128 low-rank-plus-tail matrix (bf16, generated per shard);
-  2. qPCA(n_components=r, svd_solver='full') fit: Gram MFMA kernel + one
-     d x d all-reduce + eigh, CPE singular-value estimates;
-  3. projection X V^T of every shard (library GEMM);
+  2. qPCA(n_components=r, svd_solver='full') fit: fp64-MFMA Gram / CholeskyQR2
+     (csrc/tsgemm64.hip xtx / xw) + one d x d all-reduce, CPE singular-value
+     estimates;
+  3. projection (X - mean) V^T of every shard: the fp64-MFMA xw kernel with
+     the mean fused (bf16 rows read directly, fp32 output);
   4. q-means (delta-means, k clusters, Gaussian tomography noise) on the
-     projected data with failure_prob p and failure_policy='resample'.
-Prints one JSON line with the wall-clock of each stage and the fit rates.
+     projected data with failure_prob p and failure_policy='resample' - the
+     pruned, incremental Lloyd step (failure injection keeps both).
+Prints one JSON line with the wall-clock of each stage and the fit rates
+(``run_pipeline`` is also the bench.py ``pipeline_*`` extra).
 Sizing: 50M x 128 bf16 = 12.8 GB in total, 1.6 GB per GPU at 8 GPUs.
 """
 
@@ -27,6 +31,69 @@ import torch
 sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
 
 
+def run_pipeline(comm, dev, n, d=128, r=32, k=256, iters=10, failure_prob=0.01, seed=7):
+    """The four stages on this rank's shard; returns {stage: seconds (max
+    over ranks)} plus the fit diagnostics."""
+    from sq_learn_amd.parallel.comm import shard_bounds
+    from sq_learn_amd.parallel.sharding import ShardedArray
+    from sq_learn_amd.utils.datasets import make_low_rank_device
+    from sq_learn_amd.decomposition import QPCA
+    from sq_learn_amd.cluster import QMeans
+    from sq_learn_amd.ops import linalg as L
+
+    start, stop = shard_bounds(n, comm.rank, comm.world_size)
+
+    def sync():
+        torch.cuda.synchronize()
+        comm.barrier()
+
+    times = {}
+    t = time.perf_counter()
+    # rows of norm ~8 (make_low_rank rows have norm ~ sqrt(rank / n)): squared
+    # distances are O(10-100), so the delta = 0.5 band is a narrow band, as in
+    # the reference's experiments on normalised data
+    X = make_low_rank_device(n, d, effective_rank=r // 2, tail_strength=0.2, seed=seed,
+                             device=dev, dtype=torch.float32, row_range=(start, stop))
+    X = (X * (2.0 * (n ** 0.5))).to(torch.bfloat16)
+    sync()
+    times["generate_s"] = time.perf_counter() - t
+
+    t = time.perf_counter()
+    q = QPCA(n_components=r, svd_solver="full", random_state=0, device=dev)
+    q.fit(ShardedArray(X, n, start, comm))
+    sync()
+    times["qpca_fit_s"] = time.perf_counter() - t
+
+    t = time.perf_counter()
+    V = torch.as_tensor(q.components_, dtype=torch.float64, device=dev)
+    mu = torch.as_tensor(q.mean_, dtype=torch.float64, device=dev)
+    Z = L.xw(X, V.T.contiguous(), mean=mu, out_dtype=torch.float32)
+    del X
+    torch.cuda.empty_cache()
+    sync()
+    times["project_s"] = time.perf_counter() - t
+
+    t = time.perf_counter()
+    km = QMeans(n_clusters=k, n_init=1, max_iter=iters, tol=0.0, init="random", delta=0.5,
+                true_distance_estimate=False, intermediate_error=True, true_tomography=False,
+                failure_prob=failure_prob, failure_policy="resample", failure_max_attempts=3,
+                random_state=0, compute_prelude=False, device=dev)
+    km.fit(ShardedArray(Z, n, start, comm))
+    sync()
+    times["qmeans_fit_s"] = time.perf_counter() - t
+    del Z
+    torch.cuda.empty_cache()
+
+    el = torch.tensor([times[kk] for kk in sorted(times)], dtype=torch.float64, device=dev)
+    comm.all_reduce_(el, op="max")
+    times = dict(zip(sorted(times), el.tolist()))
+    times["total_s"] = sum(times.values())
+    times.update(iters=int(km.n_iter_), failed_rows=int(km.n_failed_rows_),
+                 estimations=int(km.n_estimations_),
+                 qmeans_samples_iter_per_s=n * km.n_iter_ / times["qmeans_fit_s"])
+    return times
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=50_000_000)
@@ -38,72 +105,19 @@ def main():
     ap.add_argument("--seed", type=int, default=7)
     a = ap.parse_args()
 
-    from sq_learn_amd.parallel.comm import Comm, init_distributed, shard_bounds
-    from sq_learn_amd.parallel.sharding import ShardedArray
-    from sq_learn_amd.utils.datasets import make_low_rank_device
-    from sq_learn_amd.decomposition import QPCA
-    from sq_learn_amd.cluster import QMeans
+    from sq_learn_amd.parallel.comm import Comm, init_distributed
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     comm = init_distributed() if world > 1 else Comm(None)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
-    start, stop = shard_bounds(a.n, comm.rank, comm.world_size)
-
-    def sync():
-        torch.cuda.synchronize()
-        comm.barrier()
-
-    times = {}
-    t = time.perf_counter()
-    # rows of norm ~8 (make_low_rank rows have norm ~ sqrt(rank / n)): squared
-    # distances are O(10-100), so the delta = 0.5 band is a narrow band, as in
-    # the reference's experiments on normalised data
-    X = make_low_rank_device(a.n, a.d, effective_rank=a.r // 2, tail_strength=0.2, seed=a.seed,
-                             device=dev, dtype=torch.float32, row_range=(start, stop))
-    X = (X * (2.0 * (a.n ** 0.5))).to(torch.bfloat16)
-    sync()
-    times["generate_s"] = time.perf_counter() - t
-
-    t = time.perf_counter()
-    q = QPCA(n_components=a.r, svd_solver="full", random_state=0, device=dev)
-    q.fit(ShardedArray(X, a.n, start, comm))
-    sync()
-    times["qpca_fit_s"] = time.perf_counter() - t
-
-    t = time.perf_counter()
-    V = torch.as_tensor(q.components_, dtype=torch.float32, device=dev)
-    mu = torch.as_tensor(q.mean_, dtype=torch.float32, device=dev)
-    Z = torch.empty((stop - start, a.r), dtype=torch.bfloat16, device=dev)
-    step = 1 << 22
-    for s in range(0, stop - start, step):
-        Z[s:s + step] = ((X[s:s + step].float() - mu) @ V.T).to(torch.bfloat16)
-    del X
-    torch.cuda.empty_cache()
-    sync()
-    times["project_s"] = time.perf_counter() - t
-
-    t = time.perf_counter()
-    km = QMeans(n_clusters=a.k, n_init=1, max_iter=a.iters, tol=0.0, init="random", delta=0.5,
-                true_distance_estimate=False, intermediate_error=True, true_tomography=False,
-                failure_prob=a.failure_prob, failure_policy="resample", failure_max_attempts=3,
-                random_state=0, compute_prelude=False, device=dev)
-    km.fit(ShardedArray(Z, a.n, start, comm))
-    sync()
-    times["qmeans_fit_s"] = time.perf_counter() - t
-
-    el = torch.tensor([times[k] for k in sorted(times)], dtype=torch.float64, device=dev)
-    comm.all_reduce_(el, op="max")
-    times = dict(zip(sorted(times), el.tolist()))
+    res = run_pipeline(comm, dev, a.n, a.d, a.r, a.k, a.iters, a.failure_prob, a.seed)
     if comm.rank == 0:
         print(json.dumps({
             "metric": "qPCA->q-means pipeline wall-clock (failure-prob resampling)",
             "n_gpus": comm.world_size, "n": a.n, "d": a.d, "r": a.r, "k": a.k,
-            "iters": km.n_iter_, "failure_prob": a.failure_prob,
-            "failed_rows": km.n_failed_rows_, "estimations": km.n_estimations_,
-            "total_s": sum(times.values()), **times,
-            "qmeans_samples_iter_per_s": a.n * km.n_iter_ / times["qmeans_fit_s"],
+            "failure_prob": a.failure_prob, **res,
             "dtype": "bf16", "data": "synthetic low-rank (Philox, per shard)"}), flush=True)
     if comm.distributed:
         import torch.distributed as dist

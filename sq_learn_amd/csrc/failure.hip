@@ -14,7 +14,9 @@ namespace sq {
 
 __global__ void __launch_bounds__(256) failure_inject_kernel(
     int* __restrict__ labels, long long n, int k, float p, int R, RngKey key, RngKey key2,
-    long long row_offset, unsigned long long* __restrict__ counters) {
+    long long row_offset, unsigned long long* __restrict__ counters, float* __restrict__ lb,
+    float* __restrict__ corr, float* __restrict__ mind, const float* __restrict__ X, long long ldx,
+    const float* __restrict__ C, int ldc, int d) {
   unsigned long long attempts = 0, corrupted = 0;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -27,8 +29,26 @@ __global__ void __launch_bounds__(256) failure_inject_kernel(
     attempts += (unsigned long long)(ok ? r + 1 : R);
     if (!ok) {
       int lab = (int)(u01(key2.word(g)) * (float)k);
-      labels[i] = lab < k ? lab : k - 1;
+      lab = lab < k ? lab : k - 1;
+      const int old = labels[i];
+      labels[i] = lab;
       ++corrupted;
+      if (lb) lb[i] = 0.0f;
+      if ((corr || mind) && old >= 0 && old < k && old != lab) {
+        const float* x = X + i * ldx;
+        const float* co = C + (size_t)old * ldc;
+        const float* cn = C + (size_t)lab * ldc;
+        double d_old = 0.0, d_new = 0.0;
+        for (int f = 0; f < d; ++f) {
+          const double a = (double)x[f] - (double)co[f], b = (double)x[f] - (double)cn[f];
+          d_old = fma(a, a, d_old);
+          d_new = fma(b, b, d_new);
+        }
+        if (corr) corr[i] += (float)(d_old - d_new);
+        // a single-candidate row's min distance is filled later from its
+        // label (mind < 0): keep the E-step's minimum instead
+        if (mind && mind[i] < 0.0f) mind[i] = (float)d_old;
+      }
     }
   }
 #pragma unroll
@@ -49,14 +69,18 @@ using namespace sq;
 extern "C" int sq_failure_inject(void* labels, long long n, int k, double p, int R, unsigned k0,
                                  unsigned k1, unsigned s0, unsigned s1, unsigned t0, unsigned t1,
                                  unsigned u0, unsigned u1, long long row_offset, void* counters,
-                                 void* stream) {
+                                 void* lb, void* corr, void* mind, const void* X, long long ldx,
+                                 const void* C, int ldc, int d, void* stream) {
   if (n <= 0) return 0;
-  if (R < 1 || k < 1) return (int)hipErrorInvalidValue;
+  if (R < 1 || k < 1 || ((corr || mind) && (!X || !C || ldx < d || ldc < d)))
+    return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1}, key2{t0, t1, u0, u1};
   long long blocks = (n + 255) / 256;
   unsigned grid = (unsigned)(blocks < 4096 ? blocks : 4096);
   hipLaunchKernelGGL(failure_inject_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      (int*)labels, n, k, (float)p, R, key, key2, row_offset,
-                     (unsigned long long*)counters);
+                     (unsigned long long*)counters, (float*)lb, (float*)corr, (float*)mind,
+                     (const float*)X, ldx,
+                     (const float*)C, ldc, d);
   return (int)hipGetLastError();
 }

@@ -68,7 +68,8 @@ __attribute__((weak)) int sq_elkan_step(const void*, const void*, const void*, c
 // failure.hip
 __attribute__((weak)) int sq_failure_inject(void*, long long, int, double, int, unsigned, unsigned,
                                             unsigned, unsigned, unsigned, unsigned, unsigned,
-                                            unsigned, long long, void*, void*);
+                                            unsigned, long long, void*, void*, void*, void*,
+                                            const void*, long long, const void*, int, int, void*);
 // kmeans.hip
 __attribute__((weak)) int sq_estep_bf16(const void* X, const void* C, void* inertia_part, const void* cn,
                   const void* xn, void* labels, void* mind, void* ovf_rows, void* ovf_count,
@@ -357,14 +358,16 @@ static PyObject* py_elkan_step(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_failure_inject(PyObject*, PyObject* a) {
-  unsigned long long lab, cnt, st; long long n, roff; int k, R; double p;
+  unsigned long long lab, cnt, lb, corr, mind, X, C, st; long long n, roff, ldx; int k, R, ldc, d;
+  double p;
   unsigned k0, k1, s0, s1, t0, t1, u0, u1;
-  if (!PyArg_ParseTuple(a, "KLidiIIIIIIIILKK", &lab, &n, &k, &p, &R, &k0, &k1, &s0, &s1, &t0, &t1,
-                        &u0, &u1, &roff, &cnt, &st))
+  if (!PyArg_ParseTuple(a, "KLidiIIIIIIIILKKKKKLKiiK", &lab, &n, &k, &p, &R, &k0, &k1, &s0, &s1,
+                        &t0, &t1, &u0, &u1, &roff, &cnt, &lb, &corr, &mind, &X, &ldx, &C, &ldc,
+                        &d, &st))
     return nullptr;
   CHECK(sq_failure_inject)
   return ret(sq_failure_inject(P(lab), n, k, p, R, k0, k1, s0, s1, t0, t1, u0, u1, roff, P(cnt),
-                               P(st)));
+                               P(lb), P(corr), P(mind), P(X), ldx, P(C), ldc, d, P(st)));
 }
 
 static PyObject* py_band_select_rows(PyObject*, PyObject* a) {

@@ -226,31 +226,29 @@ class QuadraticDiscriminantAnalysis(ClassifierMixin, BaseEstimator):
                              % n_classes)
         self.priors_ = np.bincount(y) / float(n_samples) if self.priors is None else \
             np.asarray(self.priors)
-        cov, means, scalings, rotations = [], [], [], []
-        for ind in range(n_classes):
-            Xg = X[y == ind]
-            meang = Xg.mean(0)
-            means.append(meang)
-            if len(Xg) == 1:
-                raise ValueError("y has only 1 sample in class %s, covariance is ill defined."
-                                 % str(self.classes_[ind]))
-            Xgc = Xg - meang
-            _, S, Vt = np.linalg.svd(Xgc, full_matrices=False)
-            rank = np.sum(S > self.tol)
-            if rank < n_features:
-                warnings.warn("Variables are collinear")
-            S2 = (S ** 2) / (len(Xg) - 1)
-            S2 = ((1 - self.reg_param) * S2) + self.reg_param
-            if self.store_covariance:
-                cov.append(np.dot(S2 * Vt.T, Vt))
-            scalings.append(S2)
-            rotations.append(Vt.T)
+        geo = [self._class_geometry(X[y == c], self.classes_[c]) for c in range(n_classes)]
+        self.means_ = np.stack([g[0] for g in geo])
+        self.scalings_ = [g[1] for g in geo]
+        self.rotations_ = [g[2] for g in geo]
         if self.store_covariance:
-            self.covariance_ = cov
-        self.means_ = np.asarray(means)
-        self.scalings_ = scalings
-        self.rotations_ = rotations
+            # Sigma_c = R diag(s) R^T of the regularised class covariance
+            self.covariance_ = [(R * s) @ R.T for _, s, R in geo]
         return self
+
+    def _class_geometry(self, Xk, label):
+        """(mean, eigenvalues, eigenvectors as columns) of one class's
+        regularised covariance (1 - reg) Sigma + reg I, from the SVD of the
+        centred class rows (eigenvalues in decreasing order)."""
+        m = Xk.shape[0]
+        if m < 2:
+            raise ValueError("y has only 1 sample in class %s, covariance is ill defined."
+                             % str(label))
+        mu = Xk.mean(axis=0)
+        _, sv, Vt = np.linalg.svd(Xk - mu, full_matrices=False)
+        if np.count_nonzero(sv > self.tol) < Xk.shape[1]:
+            warnings.warn("Variables are collinear")
+        ev = sv * sv / (m - 1)
+        return mu, ev + self.reg_param * (1.0 - ev), Vt.T
 
     def _decision_function(self, X):
         check_is_fitted(self)

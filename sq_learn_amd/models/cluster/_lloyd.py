@@ -184,12 +184,12 @@ class LloydEngine:
         # 512 block partials of the min-distance sums + (incremental M-step)
         # the k per-cluster inertia parts, reduced together in one launch
         self.mind_part = torch.zeros(512 + self.k, dtype=torch.float64, device=dev)
-        # incremental M-step (certified path, unweighted, no failure
-        # injection): only the rows whose label moved are re-read; the
-        # inertia comes from the per-cluster statistics + the E-step's
-        # min-vs-label corrections.  SQ_MSTEP_INCREMENTAL=0 disables it.
+        # incremental M-step (certified path, unweighted): only the rows
+        # whose label moved are re-read; the inertia comes from the
+        # per-cluster statistics + the E-step's min-vs-label corrections
+        # (failure injection moves a corrupted row's correction with its
+        # label).  SQ_MSTEP_INCREMENTAL=0 disables it.
         self.incremental = (self.certified and self.sample_weight is None
-                            and self.failure_prob == 0.0
                             and os.environ.get("SQ_MSTEP_INCREMENTAL", "1") != "0")
         if self.incremental:
             self.prev_labels = torch.full((self.n,), -1, dtype=torch.int32, device=dev)
@@ -200,8 +200,9 @@ class LloydEngine:
             self.qexp = K.fixed_point_exp(self._max_abs ** 2 * self.dm, nr)
         self.inc_valid = False
         # Hamerly pruning of the certified E-step (exact: pruned rows keep a
-        # one-member band); SQ_ESTEP_BOUNDS=0 disables it
-        self.bounds = (self.certified and self.failure_prob == 0.0
+        # one-member band; a row corrupted by failure injection gets lb = 0,
+        # so the next E-step re-evaluates it); SQ_ESTEP_BOUNDS=0 disables it
+        self.bounds = (self.certified
                        and os.environ.get("SQ_ESTEP_BOUNDS", "1") != "0")
         if self.bounds:
             self.ub = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
@@ -719,9 +720,18 @@ class LloydEngine:
         else:
             labels, mind, inertia = self._estep(self._key("band_select"))
         if self.failure_prob > 0:
-            # Bernoulli estimation failures (+ resampling)
+            # Bernoulli estimation failures (+ resampling);
+            # the pruned / incremental step's per-row state follows the label
+            extra = {}
+            if self.fast and getattr(self, "bounds", False):
+                extra["lb"] = self.lb
+            if self.fast and self.C_op is not None and self.certified:
+                Cm = self.C if self.dm == self.d else self._padded_centers()
+                extra.update(X=self.Xm, C=Cm, mind=self.buf.mind)
+                if getattr(self, "incremental", False) and self.buf.corr is not None:
+                    extra["corr"] = self.buf.corr
             failure_inject_(labels, self.k, self.failure_prob, self.failure_attempts,
-                            self._key("failure"), self.row_offset, self.failure_counters)
+                            self._key("failure"), self.row_offset, self.failure_counters, **extra)
         sc = self.mstep(labels, inertia)
         if self.relocate_empty:
             counts = self._last_counts

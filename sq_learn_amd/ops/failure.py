@@ -23,9 +23,15 @@ def _keys(key: RngKey):
     return key, key.derive(sub=(key.stream & ((1 << 48) - 1)) | (1 << 47))
 
 
-def failure_inject_(labels, k, p, attempts, key: RngKey, row_offset, counters):
+def failure_inject_(labels, k, p, attempts, key: RngKey, row_offset, counters, lb=None,
+                    corr=None, X=None, C=None, mind=None):
     """In place on int32/int64 ``labels``; ``counters`` (int64[2] on the same
-    device) += [estimations made, corrupted rows]."""
+    device) += [estimations made, corrupted rows].  Device only: ``lb`` (fp32
+    [n], the Hamerly lower bounds) is zeroed on corrupted rows, and ``corr``
+    (fp32 [n], the incremental M-step's min-vs-label corrections) moves with
+    the label: += |x - C[old]|^2 - |x - C[new]|^2 (``X`` fp32 rows, ``C`` fp32
+    centres of the E-step); ``mind`` (fp32 [n]): a corrupted row whose min
+    distance is still unfilled (< 0) gets |x - C[old]|^2."""
     n = labels.numel()
     if n == 0 or p <= 0:
         if n:
@@ -33,9 +39,20 @@ def failure_inject_(labels, k, p, attempts, key: RngKey, row_offset, counters):
         return labels
     k1, k2 = _keys(key)
     if nat.use_native(labels) and labels.dtype == torch.int32:
+        need = corr is not None or mind is not None
+        if need:
+            assert X is not None and C is not None and X.dtype == torch.float32
+            assert C.dtype == torch.float32 and X.stride(1) == 1 and C.stride(1) == 1
+        d = min(X.shape[1], C.shape[1]) if need else 0
         nat.native().failure_inject(labels.data_ptr(), n, int(k), float(p), int(attempts),
                                     k1.k0, k1.k1, k1.s0, k1.s1, k2.k0, k2.k1, k2.s0, k2.s1,
                                     int(row_offset), counters.data_ptr(),
+                                    0 if lb is None else lb.data_ptr(),
+                                    0 if corr is None else corr.data_ptr(),
+                                    0 if mind is None else mind.data_ptr(),
+                                    X.data_ptr() if need else 0, X.stride(0) if need else 0,
+                                    C.data_ptr() if need else 0, C.stride(0) if need else 0,
+                                    int(d),
                                     nat.stream_handle(labels.device))
         return labels
     dev = labels.device
