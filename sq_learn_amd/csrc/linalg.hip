@@ -23,36 +23,37 @@ template <> SQ_DEV float ld1<uint16_t>(const uint16_t* p, size_t i) { return bf1
 // One v_log per element, one v_exp per (element, exponent); row sums by
 // log2(LPR) xor-shuffles; column sums reduced in LDS per workgroup and
 // written as per-WG partials, summed by mu_colsum_kernel in a fixed order
-// (no float atomics: deterministic).
+// (no float atomics: deterministic).  ``mean`` (fp32 [d_total], nullable):
+// the power sums of |a - mean| (the centred matrix without a centred copy).
 constexpr int MUQ = 12;
 
 template <typename T>
-SQ_DEV void ld8abs(const T* p, bool full, int valid, float v[8]);
+SQ_DEV void ld8raw(const T* p, bool full, int valid, float v[8]);
 template <>
-SQ_DEV void ld8abs<uint16_t>(const uint16_t* p, bool full, int valid, float v[8]) {
+SQ_DEV void ld8raw<uint16_t>(const uint16_t* p, bool full, int valid, float v[8]) {
   if (full) {
     uint4 u = *reinterpret_cast<const uint4*>(p);
     uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[2 * e] = fabsf(__uint_as_float(w[e] << 16));
-      v[2 * e + 1] = fabsf(__uint_as_float(w[e] & 0xFFFF0000u));
+      v[2 * e] = __uint_as_float(w[e] << 16);
+      v[2 * e + 1] = __uint_as_float(w[e] & 0xFFFF0000u);
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(bf16_to_f32(p[e])) : 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = e < valid ? bf16_to_f32(p[e]) : 0.f;
   }
 }
 template <>
-SQ_DEV void ld8abs<float>(const float* p, bool full, int valid, float v[8]) {
+SQ_DEV void ld8raw<float>(const float* p, bool full, int valid, float v[8]) {
   if (full) {
     float4 a = *reinterpret_cast<const float4*>(p);
     float4 b = *reinterpret_cast<const float4*>(p + 4);
-    v[0] = fabsf(a.x); v[1] = fabsf(a.y); v[2] = fabsf(a.z); v[3] = fabsf(a.w);
-    v[4] = fabsf(b.x); v[5] = fabsf(b.y); v[6] = fabsf(b.z); v[7] = fabsf(b.w);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(p[e]) : 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = e < valid ? p[e] : 0.f;
   }
 }
 
@@ -63,7 +64,7 @@ template <typename T, int LPR>
 __global__ void __launch_bounds__(256) mu_sums_kernel(
     const T* __restrict__ X, long long ldx, int col0, int d_total, const float* __restrict__ qs,
     int nq, float* __restrict__ rowmax, float* __restrict__ part, float* __restrict__ rowacc,
-    int final, long long n, int d, long long rows_per_wg) {
+    int final, long long n, int d, long long rows_per_wg, const float* __restrict__ mean) {
   constexpr int RPW = 64 / LPR;              // rows per wave step
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -72,6 +73,10 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
   const int c0 = vl * 8;
   const bool vec = ((ldx % 8) == 0) && ((col0 % 8) == 0) && (c0 + 8 <= d);
   const int valid = d - c0;
+  // this lane's 8 column means (0 without a mean)
+  float mu8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) mu8[e] = (mean && c0 + e < d) ? mean[col0 + c0 + e] : 0.f;
   float q[MUQ];
 #pragma unroll
   for (int i = 0; i < MUQ; ++i) q[i] = i < nq ? qs[i] : 0.f;
@@ -86,11 +91,13 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
   const long long r_end = min(n, r_beg + rows_per_wg);
   for (long long r = r_beg + sg; r < r_end; r += 4 * RPW) {
     float v[8], lg[8];
-    if (c0 < d) ld8abs<T>(X + (size_t)r * ldx + col0 + c0, vec, valid, v);
+    if (c0 < d) ld8raw<T>(X + (size_t)r * ldx + col0 + c0, vec, valid, v);
     else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = 0.f;
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(v[e] - mu8[e]) : 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) lg[e] = __builtin_amdgcn_logf(v[e]);   // log2, -inf at 0
 #pragma unroll
@@ -199,7 +206,7 @@ extern "C" {
 
 int sq_mu_sums(const void* X, int xdtype, long long ldx, const void* qs, int nq, void* rowmax,
                void* colsum, void* part, int part_wgs, void* rowacc, long long n, int d,
-               void* stream) {
+               const void* mean, void* stream) {
   if (n <= 0) return 0;
   if (nq > MUQ || part_wgs < 1 || ldx < d || (d > 512 && !rowacc)) return (int)hipErrorInvalidValue;
   long long wgs = min((long long)part_wgs, max(1LL, (n + 255) / 256));
@@ -216,7 +223,7 @@ int sq_mu_sums(const void* X, int xdtype, long long ldx, const void* qs, int nq,
   case L:                                                                                      \
     hipLaunchKernelGGL((mu_sums_kernel<T, L>), dim3((unsigned)wgs), dim3(256), 0, st,          \
                        (const T*)X, ldx, col0, d, (const float*)qs, nq, (float*)rowmax,        \
-                       (float*)part, racc, final, n, dc, rpw);                                 \
+                       (float*)part, racc, final, n, dc, rpw, (const float*)mean);             \
     break;
     if (xdtype == 0) {
       switch (lpr) { MU_CASE(float, 1) MU_CASE(float, 2) MU_CASE(float, 4) MU_CASE(float, 8)

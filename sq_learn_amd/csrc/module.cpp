@@ -142,7 +142,7 @@ __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void
                  unsigned s0, unsigned s1, long long row_offset, void* stream);
 // linalg.hip
 __attribute__((weak)) int sq_mu_sums(const void*, int, long long, const void*, int, void*, void*,
-                                     void*, int, void*, long long, int, void*);
+                                     void*, int, void*, long long, int, const void*, void*);
 __attribute__((weak)) int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream);
 // knn.hip
 __attribute__((weak)) int sq_knn_topk(const void* D, void* outd, void* outi, long long m, int nref, long long ldD, int kk,
@@ -573,13 +573,13 @@ static PyObject* py_ipe_estep(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_mu_sums(PyObject*, PyObject* a) {
-  unsigned long long X, qs, rm, cs, part, racc, st; int xdt, nq, pw, d; long long n, ldx;
-  if (!PyArg_ParseTuple(a, "KiLKiKKKiKLiK", &X, &xdt, &ldx, &qs, &nq, &rm, &cs, &part, &pw, &racc,
-                        &n, &d, &st))
+  unsigned long long X, qs, rm, cs, part, racc, mean, st; int xdt, nq, pw, d; long long n, ldx;
+  if (!PyArg_ParseTuple(a, "KiLKiKKKiKLiKK", &X, &xdt, &ldx, &qs, &nq, &rm, &cs, &part, &pw, &racc,
+                        &n, &d, &mean, &st))
     return nullptr;
   CHECK(sq_mu_sums)
   return ret(sq_mu_sums(P(X), xdt, ldx, P(qs), nq, P(rm), P(cs), P(part), pw, P(racc), n, d,
-                        P(st)));
+                        P(mean), P(st)));
 }
 
 static PyObject* py_row_norms(PyObject*, PyObject* a) {

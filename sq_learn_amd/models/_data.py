@@ -122,14 +122,16 @@ def prelude_stats(data: Data, mu_start=0.0, mu_end=1.0, mu_step=0.1, condition=T
     return eta, label, mu, cond
 
 
-def best_mu_distributed(data: Data, start=0.0, end=1.0, step=0.05, fro_sq=None, fro_sq_global=None):
+def best_mu_distributed(data: Data, start=0.0, end=1.0, step=0.05, fro_sq=None, fro_sq_global=None,
+                        mean=None):
     """``best_mu`` (``Utility.py:196-231``) over a row-sharded matrix: one
     fused power-sum pass (row-max and column sums for every exponent of the
-    p-grid), then MAX / SUM all-reduces."""
+    p-grid), then MAX / SUM all-reduces.  ``mean``: mu of the centred matrix
+    X - mean, subtracted inside the pass."""
     domain = [i for i in np.arange(start, end, step)] + [end]
     exps = sorted(set([round(float(2 * p), 12) for p in domain] +
                       [round(float(2 * (1 - p)), 12) for p in domain]))
-    rowmax, colsum = L.mu_power_sums_local(data.X, exps)
+    rowmax, colsum = L.mu_power_sums_local(data.X, exps, mean=mean)
     data.comm.all_reduce_(rowmax, op="max")
     data.comm.all_reduce_(colsum, op="sum")
     colmax = colsum.max(dim=1).values
@@ -144,7 +146,8 @@ def best_mu_distributed(data: Data, start=0.0, end=1.0, step=0.05, fro_sq=None, 
         fro = float(np.sqrt(fro_sq_global))
     else:
         if fro_sq is None:
-            fro_sq = float((data.X.double() ** 2).sum())
+            Xd = data.X.double() if mean is None else data.X.double() - mean.double().to(data.device)
+            fro_sq = float((Xd ** 2).sum())
         t = torch.tensor([fro_sq], dtype=torch.float64, device=data.device)
         data.comm.all_reduce_(t)
         fro = float(np.sqrt(t.item()))

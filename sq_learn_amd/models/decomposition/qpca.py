@@ -228,19 +228,14 @@ class QPCA(_BasePCA):
         self.spectral_norm = float(self.singular_values_[0]) if n_components else 0.0
         fro = torch.tensor([float((S ** 2).sum())], dtype=torch.float64)
         self.frob_norm = float(np.sqrt(fro.item()))
-        centred = type(data)(self._centred(data, mean), data.n_global, data.row_offset, data.comm,
-                             data.source_kind)
-        self.norm_muA, self.muA = best_mu_distributed(centred, start=0, end=1.0, step=0.1,
-                                                      fro_sq_global=float((S ** 2).sum()))
+        # mu(A) of the centred matrix with the mean fused into the power-sum
+        # pass (no centred copy of X)
+        self.norm_muA, self.muA = best_mu_distributed(data, start=0, end=1.0, step=0.1,
+                                                      fro_sq_global=float((S ** 2).sum()),
+                                                      mean=mean)
         self._data_for_tomography = data
-        self._quantum_extras(centred)
+        self._quantum_extras()
         return self
-
-    def _centred(self, data, mean):
-        X = data.X
-        if X.dtype == torch.bfloat16:
-            return (X.float() - mean.float().to(X.device)).to(torch.bfloat16)
-        return X - mean.to(X.dtype).to(X.device)
 
     def _left_vectors(self, data, mean, k):
         dt = torch.float64 if data.device.type == "cpu" else torch.float32
@@ -304,15 +299,14 @@ class QPCA(_BasePCA):
             self.all_components = Vt
             self.explained_variance_all = self.explained_variance_
             self.explained_variance_ratio_all = self.explained_variance_ratio_
-            centred = type(data)(self._centred(data, mean), data.n_global, data.row_offset,
-                                 data.comm, data.source_kind)
-            self.norm_muA, self.muA = best_mu_distributed(centred, start=0, end=1.0, step=0.1,
-                                                          fro_sq_global=self.frob_norm ** 2)
-            self._quantum_extras(centred)
+            self.norm_muA, self.muA = best_mu_distributed(data, start=0, end=1.0, step=0.1,
+                                                          fro_sq_global=self.frob_norm ** 2,
+                                                          mean=mean)
+            self._quantum_extras()
         return self
 
     # ------------------------------------------------------- quantum extras
-    def _quantum_extras(self, centred):
+    def _quantum_extras(self):
         k = self._knobs
         if k["condition_number_est"]:
             self.est_cond_number = self.condition_number_estimation(epsilon=k["eps"], delta=k["delta"])
@@ -332,11 +326,11 @@ class QPCA(_BasePCA):
         if k["estimate_least_k"]:
             (self.estimate_least_right_sv, self.estimate_least_left_sv, self.estimate_least_s_values,
              self.estimate_least_fs, self.estimate_least_fs_ratio) = self.least_k_sv_extractors(
-                X=centred, delta=k["delta"], eps=k["eps"], theta=k["theta_minor"], **tkw)
+                X=None, delta=k["delta"], eps=k["eps"], theta=k["theta_minor"], **tkw)
         if k["estimate_all"]:
             (self.estimate_right_sv, self.estimate_left_sv, self.estimate_s_values, self.estimate_fs,
              self.estimate_fs_ratio) = self.topk_sv_extractors(
-                X=centred, delta=k["delta"], eps=k["eps"], theta=k["theta_major"], **tkw)
+                X=None, delta=k["delta"], eps=k["eps"], theta=k["theta_major"], **tkw)
 
     def _cpe_sv(self, sv_scaled, eps_pe, scale_denom, unwrap_eps, gamma):
         """CPE of wrapped singular values (vectorised): theta_i = 2 acos(sv_i)

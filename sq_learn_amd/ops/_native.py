@@ -65,6 +65,20 @@ def use_native(*tensors):
 
 
 def stream_handle(device=None):
+    """Handle of the current torch stream of ``device`` for a native launch,
+    with ``device`` made the calling thread's current device first: a
+    default stream's handle is 0 (the null stream), which HIP resolves
+    against the CURRENT device, so launching for ``cuda:1`` from a thread
+    whose current device is 0 would run on the wrong GPU.  (The HIP current
+    device is per thread: the task layer's per-GPU worker threads and
+    ``torch.cuda.device`` contexts are unaffected elsewhere.)"""
+    if device is not None:
+        dev = torch.device(device)
+        if dev.type == "cuda":
+            idx = dev.index if dev.index is not None else torch.cuda.current_device()
+            if idx != torch.cuda.current_device():
+                torch.cuda.set_device(idx)
+            return torch.cuda.current_stream(idx).cuda_stream
     return torch.cuda.current_stream(device).cuda_stream
 
 

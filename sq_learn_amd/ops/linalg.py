@@ -218,11 +218,13 @@ def power_iter_local(X, Q, mean, chunk_rows=None):
     return Z
 
 
-def mu_power_sums_local(X, exponents):
+def mu_power_sums_local(X, exponents, mean=None):
     """(row_max [nq], col_sums [nq, d]) local partials for mu(A).
 
-    row_max[i] = max_rows sum_j |x_rj|^q_i   (q=0: nonzero count)
-    col_sums[i, j] = sum_rows |x_rj|^q_i
+    row_max[i] = max_rows sum_j |a_rj|^q_i   (q=0: nonzero count)
+    col_sums[i, j] = sum_rows |a_rj|^q_i
+    with a = x - mean (``mean`` [d], optional: fused into the pass, no
+    centred copy of X).
     """
     n, d = X.shape
     q = torch.tensor(exponents, dtype=torch.float32)
@@ -237,13 +239,17 @@ def mu_power_sums_local(X, exponents):
         part = torch.empty((wgs, nq, d), dtype=torch.float32, device=X.device)
         # d > 512: row power sums carried across the 512-column blocks
         racc = torch.zeros((nq, n), dtype=torch.float32, device=X.device) if d > 512 else None
+        mu = None if mean is None else mean.to(device=X.device, dtype=torch.float32).contiguous()
         rc = nat.native().mu_sums(X.data_ptr(), nat.dtype_code(X), X.stride(0), qd.data_ptr(), nq,
                                   rowmax.data_ptr(), colsum.data_ptr(), part.data_ptr(), wgs,
-                                  nat.ptr(racc), n, d, nat.stream_handle(X.device))
+                                  nat.ptr(racc), n, d, nat.ptr(mu), nat.stream_handle(X.device))
         if rc:
             raise RuntimeError(f"mu_sums failed (hip error {rc})")
         return rowmax.double(), colsum.double()
-    A = X.abs().to(torch.float64)
+    A = X.to(torch.float64)
+    if mean is not None:
+        A = A - mean.to(device=X.device, dtype=torch.float64)
+    A = A.abs()
     rowmax = torch.zeros(nq, dtype=torch.float64, device=X.device)
     colsum = torch.zeros((nq, d), dtype=torch.float64, device=X.device)
     nz = A != 0
