@@ -97,6 +97,40 @@ def main(out_path):
             muA_rel=abs(got.muA - ref.muA) / ref.muA,
             cfg_ref=ref_cfg[-1], cfg_got=got_cfg[-1])
 
+    # the reference DEFAULT distance mode: IPE (fused csrc/ipe.hip kernel,
+    # row-keyed hazard streams and label hints), k-means++ init
+    kw = dict(n_clusters=24, delta=0.5, true_distance_estimate=True, intermediate_error=True,
+              true_tomography=False, random_state=5, n_init=1, max_iter=6, tol=0.0,
+              init="k-means++", device=dev)
+    ref = QMeans(**kw).fit(X)
+    got = QMeans(**kw).fit(Xs)
+    res["qmeans_ipe"] = dict(
+        labels_equal=bool(np.array_equal(gather_labels(got.labels_), ref.labels_)),
+        centers_bitwise=bool(np.array_equal(got.cluster_centers_, ref.cluster_centers_)),
+        inertia_rel=abs(got.inertia_ - ref.inertia_) / ref.inertia_,
+        n_iter=[int(got.n_iter_), int(ref.n_iter_)])
+
+    # wide rows: the certified filter at d_pad 512 / 1024 (d = 300, 784) and
+    # the exact fp64 rows kernel beyond it (d = 1100) under k-means||
+    for d_w, init_w in ((300, "k-means++"), (784, "random"), (1100, "k-means||")):
+        Xw, _ = make_blobs(4001, d_w, centers=16, cluster_std=2.0, random_state=d_w)
+        Xw = Xw.astype(np.float32)
+        kw = dict(n_clusters=16, delta=0.5, true_distance_estimate=False, intermediate_error=True,
+                  true_tomography=False, random_state=2, n_init=1, max_iter=8, init=init_w,
+                  device=dev)
+        seen.clear()
+        ref = QMeans(**kw).fit(Xw)
+        ref_cfg = list(seen)
+        seen.clear()
+        got = QMeans(**kw).fit(shard(Xw))
+        got_cfg = list(seen)
+        res[f"qmeans_d{d_w}"] = dict(
+            labels_equal=bool(np.array_equal(gather_labels(got.labels_), ref.labels_)),
+            centers_bitwise=bool(np.array_equal(got.cluster_centers_, ref.cluster_centers_)),
+            inertia_rel=abs(got.inertia_ - ref.inertia_) / ref.inertia_,
+            n_iter=[int(got.n_iter_), int(ref.n_iter_)],
+            cfg_ref=ref_cfg[-1], cfg_got=got_cfg[-1])
+
     # classical KMeans (fp32 certified E-step + empty-cluster relocation):
     # two far initial centres own no rows at the first E-step
     rng = np.random.RandomState(0)

@@ -13,9 +13,13 @@ The analogue of the reference's thread-count invariance test
   fp64 sum whose association follows the shard boundaries (<= 1e-12 rel);
 * classical KMeans with empty-cluster relocation (per-shard top-e +
   all-gather): bit-identical labels and centroids;
+* q-means with the reference's default IPE distances (fused kernel, hazard
+  streams keyed by global row, previous-label hints) and with wide rows
+  (d = 300 / 784 through the certified filter, d = 1100 through the exact
+  fp64 rows kernel under k-means||): bit-identical labels and centroids;
 * CholeskyQR2 sigma_min on the fp64-MFMA Gram, centred and not, and the
-  full qPCA spectrum: fp64 sums over shards, <= 1e-10 rel; the randomized
-  spectrum: fp32 range-finder sums over shards, <= 1e-5 rel;
+  full and randomized qPCA spectra (fp64 end to end): fp64 sums over
+  shards, <= 1e-9 rel;
 * tomography of the row-sharded left singular vectors: Gaussian noise
   keyed by (vector, GLOBAL column) - the single-process draw; true
   tomography (rank-split multinomial) within its delta guarantee.
@@ -53,12 +57,13 @@ def _run(world):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
                f"--master-port={_free_port()}", os.path.join(HERE, "_dist_gpu_worker.py"), out]
-        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
         assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-6000:])
         with open(out) as f:
             return json.load(f)
 
 
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_gpu_fast_path_matches_single_process(world):
     r = _run(world)
@@ -75,6 +80,14 @@ def test_sharded_gpu_fast_path_matches_single_process(world):
         assert q["n_iter"][0] == q["n_iter"][1], (init, q)
         assert q["inertia_rel"] <= 1e-12, (init, q)
         assert q["cond_rel"] <= 1e-10 and q["muA_rel"] <= 1e-12, (init, q)
+    q = res["qmeans_ipe"]
+    assert q["labels_equal"] and q["centers_bitwise"], q
+    assert q["n_iter"][0] == q["n_iter"][1] and q["inertia_rel"] <= 1e-12, q
+    for d_w, fast in ((300, True), (784, True), (1100, False)):
+        q = res[f"qmeans_d{d_w}"]
+        assert q["cfg_got"]["fast"] == fast and q["cfg_ref"]["fast"] == fast, (d_w, q)
+        assert q["labels_equal"] and q["centers_bitwise"], (d_w, q)
+        assert q["n_iter"][0] == q["n_iter"][1] and q["inertia_rel"] <= 1e-12, (d_w, q)
     km = res["kmeans_relocate"]
     assert km["cfg_got"]["fast"] and km["cfg_got"]["relocate"], km
     assert km["distinct"] == 5, km      # both far centres were relocated
