@@ -200,8 +200,9 @@ def _share8_extra(extra, a, X, comm, dev):
 
 def _hard_extra(extra, a, comm, dev):
     """A hard regime for the certified E-step: 1024 strongly overlapping
-    blobs (centres in [-0.1, 0.1]^d, unit spread) so that many rows have
-    several centroids within delta of their minimum.  Reports the steady-state
+    blobs (centres in [-0.1, 0.1]^d, spread 0.4: a mean delta-band of ~3
+    members, ~60 % multi-candidate rows) so that most rows have several
+    centroids within delta of their minimum.  Reports the steady-state
     and unpruned ms per step, the first iteration, the dense / multi-candidate
     row fractions of the last step and the mean delta-band size (fp64, on a
     4096-row sample).  Rows: a.n / 5 (2M at the default)."""
@@ -212,7 +213,7 @@ def _hard_extra(extra, a, comm, dev):
         from sq_learn_amd.models._data import Data, gather_rows
         n = max(a.n // 5, 4096)
         s0, s1 = shard_bounds(n, comm.rank, comm.world_size)
-        X, _ = make_blobs_device(n, a.d, centers=a.blobs, cluster_std=1.0, center_box=(-0.1, 0.1),
+        X, _ = make_blobs_device(n, a.d, centers=a.blobs, cluster_std=0.4, center_box=(-0.1, 0.1),
                                  seed=a.seed + 1, device=dev, dtype=torch.float32,
                                  row_range=(s0, s1))
         data = Data(X, n, s0, comm, "sharded")

@@ -1370,13 +1370,16 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const double* __restr
 // rows]; the overflow counter is reset for the next E-step.
 // With cmax2 != null it also writes max_j cn[j] (the fp16 operand's largest
 // alpha^2 ||c||^2: the certified E-step's error bound for the next iteration).
+// With kept != null, scalars[3] = the rows the iteration's Hamerly filter
+// kept (the host's adaptive-pruning signal, carried by the same read).
 __global__ void __launch_bounds__(256) iter_scalars_kernel(const double* __restrict__ part, int n,
                                                            double* __restrict__ shift,
                                                            const double* __restrict__ inertia,
                                                            int* __restrict__ ovf_count,
                                                            double* __restrict__ scalars,
                                                            const float* __restrict__ cn,
-                                                           float* __restrict__ cmax2) {
+                                                           float* __restrict__ cmax2,
+                                                           const int* __restrict__ kept) {
   __shared__ double red[256];
   __shared__ float redm[256];
   double s = 0.0;
@@ -1406,6 +1409,7 @@ __global__ void __launch_bounds__(256) iter_scalars_kernel(const double* __restr
     } else {
       scalars[2] = 0.0;
     }
+    if (kept) scalars[3] = (double)kept[0];
   }
 }
 
@@ -1926,7 +1930,7 @@ int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, voi
                          void* shift_part, void* cn, void* shift, int k, int d, int k_pad,
                          double noise_b, unsigned k0, unsigned k1, unsigned s0, unsigned s1,
                          int empty_policy, void* scalars, void* ovf_count, void* C_f16,
-                         double alpha, void* cmax2, void* stream) {
+                         double alpha, void* cmax2, const void* kept, void* stream) {
   if (!shift_part) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
   float b = (float)noise_b;
@@ -1940,7 +1944,7 @@ int sq_centroid_finalize(const void* packed, const void* C_old, void* C_new, voi
     hipLaunchKernelGGL(iter_scalars_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
                        (const double*)shift_part, k, (double*)shift,
                        (const double*)packed + (long long)k * d + k, (int*)ovf_count,
-                       (double*)scalars, (const float*)cn, (float*)cmax2);
+                       (double*)scalars, (const float*)cn, (float*)cmax2, (const int*)kept);
   else
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
                        (const double*)shift_part, k, (double*)shift);

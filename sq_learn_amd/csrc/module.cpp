@@ -92,7 +92,7 @@ __attribute__((weak)) int sq_centroid_finalize(const void* packed, const void* C
                          void* C_lo, void* cn, void* shift, int k, int d, int k_pad, double noise_b,
                          unsigned k0, unsigned k1, unsigned s0, unsigned s1, int empty_policy,
                          void* scalars, void* ovf_count, void* C_f16, double alpha, void* cmax2,
-                         void* stream);
+                         const void* kept, void* stream);
 __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, const void*,
                                        const void*, const void*, void*, void*, void*, void*, void*,
                                        void*, void*, void*, void*, void*, void*, void*, void*,
@@ -513,14 +513,16 @@ static PyObject* py_sum_f32(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
-  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, cf, cm2, st; int k, d, kpad, pol;
+  unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, cf, cm2, kp, st; int k, d, kpad, pol;
   double nb, alpha; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKKdKK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
-                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &cf, &alpha, &cm2, &st))
+  if (!PyArg_ParseTuple(a, "KKKKKKKiiidIIIIiKKKdKKK", &pk, &co, &cnw, &cb, &clo, &cn, &sh, &k, &d,
+                        &kpad, &nb, &k0, &k1, &s0, &s1, &pol, &sc, &oc, &cf, &alpha, &cm2, &kp,
+                        &st))
     return nullptr;
   CHECK(sq_centroid_finalize)
   return ret(sq_centroid_finalize(P(pk), P(co), P(cnw), P(cb), P(clo), P(cn), P(sh), k, d, kpad, nb,
-                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(cf), alpha, P(cm2), P(st)));
+                                  k0, k1, s0, s1, pol, P(sc), P(oc), P(cf), alpha, P(cm2), P(kp),
+                                  P(st)));
 }
 
 static PyObject* py_estep_f32(PyObject*, PyObject* a) {

@@ -52,14 +52,17 @@ class _HostScalars:
     has completed (pipelined steps: the read must not wait for the next
     iteration's E-step, already enqueued behind the copy)."""
 
-    __slots__ = ("host", "event")
+    __slots__ = ("host", "event", "sink")
 
-    def __init__(self, host, event):
-        self.host, self.event = host, event
+    def __init__(self, host, event, sink=None):
+        self.host, self.event, self.sink = host, event, sink
 
     def tolist(self):
         self.event.synchronize()
-        return self.host.tolist()
+        vals = self.host.tolist()
+        if self.sink is not None:
+            self.sink(vals)
+        return vals
 
 
 class LloydEngine:
@@ -204,6 +207,15 @@ class LloydEngine:
         # so the next E-step re-evaluates it); SQ_ESTEP_BOUNDS=0 disables it
         self.bounds = (self.certified
                        and os.environ.get("SQ_ESTEP_BOUNDS", "1") != "0")
+        # adaptive pruning: when the filter kept more than keep_max of the
+        # rows, the next E-steps sweep every row directly (bounds still
+        # maintained) and the filter is re-probed every probe_every steps
+        self.keep_max = float(os.environ.get("SQ_ESTEP_KEEP_MAX", "0.6"))
+        self.probe_every = 4
+        self._kept_frac = None
+        self._skips = 0
+        self._filter_ran = False
+        self._minus1 = torch.full((1,), -1, dtype=torch.int32, device=dev)
         if self.bounds:
             self.ub = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
             self.lb = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
@@ -242,7 +254,10 @@ class LloydEngine:
         self.C = torch.zeros((self.k, self.d), dtype=torch.float32, device=dev)
         self.C_new = torch.zeros_like(self.C)
         self.cn = torch.full((self.k_pad,), K.BIG, dtype=torch.float32, device=dev)
-        self.scalars = torch.zeros(3, dtype=torch.float64, device=dev)
+        # [inertia, shift, overflow rows, rows kept by the Hamerly filter
+        # (-1: no filter ran)] - one D2H read per iteration
+        self.scalars = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.scalars[3] = -1.0
         self.weights = (self.sample_weight.to(torch.float32).contiguous()
                         if self.sample_weight is not None else None)
 
@@ -326,7 +341,9 @@ class LloydEngine:
             with tracing.range("estep_x64"):
                 Cp = self.C if self.d == self.d_pad else self._padded_centers()
                 rows = None
-                if self.bounds and self.bounds_valid and not full:
+                self._filter_ran = False
+                if self.bounds and self.bounds_valid and not full and self._use_filter():
+                    self._filter_ran = True
                     K.ensure_multi_buffers(self.buf, self.n, self.device, True)
                     self.buf.counts.zero_()
                     K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
@@ -356,6 +373,27 @@ class LloydEngine:
         if self.ipe:
             return self._estep_ipe(key)
         return self._estep_generic(key)
+
+    def _use_filter(self):
+        """Adaptive Hamerly pruning: run the bounds filter unless the last
+        measured iteration kept more than ``keep_max`` of the rows (then the
+        filter's pass and the row-list indirection cost more than they
+        save); re-probe every ``probe_every`` E-steps."""
+        kf = self._kept_frac
+        if kf is None or kf <= self.keep_max:
+            self._skips = 0
+            return True
+        self._skips += 1
+        if self._skips >= self.probe_every:
+            self._skips = 0
+            return True
+        return False
+
+    def _on_scalars(self, vals):
+        """Host values of an iteration's scalars (called by the pipelined
+        read): records the filter's kept fraction."""
+        if len(vals) > 3 and vals[3] >= 0 and self.n:
+            self._kept_frac = vals[3] / self.n
 
     def _chunk_rows(self):
         wm = 1 << 28  # 256 MiB of distances per chunk
@@ -480,7 +518,9 @@ class LloydEngine:
                                            shift_part=self.shift_part, scalars=self.scalars,
                                            buf=self.buf, C_f16=self.C_op, alpha=self.alpha,
                                            k_pad=self.k_pad,
-                                           cmax2=self.cmax2 if self.C_op is not None else None)
+                                           cmax2=self.cmax2 if self.C_op is not None else None,
+                                           kept=(self.rcount if getattr(self, "_filter_ran", False)
+                                                 else getattr(self, "_minus1", None)))
                 self.C, self.C_new = self.C_new, self.C
                 if self.intermediate_error and self.true_tomography and self.delta > 0:
                     self._true_tomography_centers()
@@ -573,7 +613,8 @@ class LloydEngine:
                                        noise_key, self.empty_policy,
                                        shift_part=self.shift_part, scalars=self.scalars,
                                        buf=self.buf, C_f16=self.C_op, alpha=self.alpha,
-                                       k_pad=self.k_pad, cmax2=self.cmax2)
+                                       k_pad=self.k_pad, cmax2=self.cmax2,
+                                       kept=self.rcount if self._filter_ran else self._minus1)
             self.C, self.C_new = self.C_new, self.C
             if self.intermediate_error and self.true_tomography and self.delta > 0:
                 self._true_tomography_centers()
@@ -762,5 +803,5 @@ class LloydEngine:
             self._label_snap.copy_(labels)
             labels = self._label_snap
             self._pending = self._estep(self._key("band_select"))
-            sc = _HostScalars(host, ev)
+            sc = _HostScalars(host, ev, self._on_scalars)
         return labels, sc

@@ -458,13 +458,16 @@ def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, 
 
 def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, noise_b, key: RngKey,
                              empty_policy=0, shift_part=None, scalars=None, buf=None, C_f16=None,
-                             alpha=1.0, k_pad=None, cmax2=None):
+                             alpha=1.0, k_pad=None, cmax2=None, kept=None):
     """shift[0] = sum_j ||c_j' - c_j||^2 (per-centroid parts summed in a fixed
     order: deterministic); ``shift_part`` is a k-double workspace.
 
     With ``scalars`` (3 doubles) the same launch also writes the iteration's
     [inertia, shift, overflow rows] (inertia from the packed bucket, overflow
-    count from ``buf``, an :class:`EStepBuffers`, whose counter it resets)."""
+    count from ``buf``, an :class:`EStepBuffers`, whose counter it resets);
+    ``kept`` (device int32 [1], needs 4 scalars): scalars[3] = its value."""
+    if kept is not None:
+        assert scalars is not None and scalars.numel() >= 4
     if k_pad is None:
         k_pad = (C_bf16 if C_bf16 is not None else C_f16).shape[0] * 64
     if shift_part is None:
@@ -476,7 +479,7 @@ def centroid_finalize_native(packed, C_old, C_new, C_bf16, cn, shift, k, d, nois
                                    key.s0, key.s1, int(empty_policy),
                                    0 if scalars is None else scalars.data_ptr(),
                                    0 if buf is None else buf.ovf_count.data_ptr(),
-                                   nat.ptr(C_f16), float(alpha), nat.ptr(cmax2),
+                                   nat.ptr(C_f16), float(alpha), nat.ptr(cmax2), nat.ptr(kept),
                                    nat.stream_handle(packed.device))
     if scalars is not None and buf is not None:
         buf.ovf_clean = True

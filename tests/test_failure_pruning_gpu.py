@@ -58,3 +58,36 @@ def test_failure_injection_incremental_matches_full_mstep(monkeypatch):
         assert torch.equal(la, lb)
         assert torch.equal(Ca, Cb)
         assert sa[0] == pytest.approx(sb[0], rel=2e-6)
+
+
+def test_adaptive_filter_skips_and_stays_exact(monkeypatch):
+    """Adaptive pruning: with keep_max = 0 every measured filter pass
+    'kept too much', so the engine sweeps all rows directly (bounds still
+    maintained) and re-probes every 4th E-step; labels and centres equal
+    the always-filtered run's bit for bit, and the kept count travels in
+    the iteration's scalars."""
+    X, C0 = _data(seed=2)
+
+    def run(keep_max):
+        monkeypatch.setenv("SQ_ESTEP_BOUNDS", "1")
+        monkeypatch.setenv("SQ_ESTEP_KEEP_MAX", str(keep_max))
+        eng = LloydEngine(torch.from_numpy(X).cuda(), C0.shape[0], delta=0.5,
+                          intermediate_error=True, seed=4)
+        eng.set_centers(torch.from_numpy(C0).cuda())
+        eng.pipeline = True
+        out, ran = [], []
+        for _ in range(10):
+            labels, sc = eng.step()
+            vals = sc.tolist()
+            out.append((labels.clone().cpu(), eng.centers().clone().cpu(), vals[:2]))
+            ran.append(vals[3] >= 0)
+        eng.pipeline = False
+        eng.drop_pending()
+        return out, ran
+
+    a, ran_a = run(1.0)
+    b, ran_b = run(0.0)
+    assert sum(ran_a) >= 8                 # every E-step after the first filtered
+    assert 0 < sum(ran_b) < sum(ran_a)      # skipped, with periodic probes
+    for (la, Ca, sa), (lb, Cb, sb) in zip(a, b):
+        assert torch.equal(la, lb) and torch.equal(Ca, Cb) and sa == sb
