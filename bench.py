@@ -310,6 +310,16 @@ def _mnist_extra(extra, a, comm, dev):
             1e3 * getattr(qm, "fit_phase_s_", {}).get("lloyd_s", float("nan")) / max(qm.n_iter_, 1), 4)
         del X, sa
         torch.cuda.empty_cache()
+        if comm.world_size == 1:
+            # the reference's driver (MnistTrial.py): qPCA(61) -> quantum
+            # representation (tomography, error 0.8) -> 7-NN, 10-fold CV
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                            "examples"))
+            from mnist_pipeline import run as mnist_run
+            r = mnist_run(device=str(dev), classic=False)
+            for kk in ("qpca_fit_s", "transform_s", "cv_s", "total_s", "accuracy"):
+                extra[f"mnist_pipeline_{kk}"] = round(r[kk], 4)
+            torch.cuda.empty_cache()
     except Exception as e:
         extra["mnist_error"] = repr(e)[:200]
 

@@ -44,6 +44,46 @@ def mnist_like(n, d=784, classes=10, rank=40, seed=0, device="cpu"):
     return X[perm], y[perm].cpu().numpy()
 
 
+def run(n=70_000, error=0.8, components=61, folds=10, device="cpu", preserve_norm=False,
+        classic=True):
+    """The pipeline; returns accuracies and per-stage seconds (also the
+    bench.py ``mnist_pipeline_*`` extra)."""
+    def sync():
+        if str(device).startswith("cuda"):
+            torch.cuda.synchronize()
+
+    X, y = mnist_like(n, device=device)
+    sync()
+    t0 = time.perf_counter()
+    pca = qPCA(svd_solver="full", device=device, preserve_norm_tomography=preserve_norm)
+    pca.n_components = components
+    pca_model = pca.fit(X)
+    sync()
+    t_fit = time.perf_counter() - t0
+    # Transform the features: quantum representation with tomography error
+    t0 = time.perf_counter()
+    X_train_pca = pca_model.transform(X, classic_transform=False, epsilon_delta=error,
+                                      quantum_representation=True, norm="est_representation",
+                                      tomography=True)
+    sync()
+    t_tr = time.perf_counter() - t0
+    est, eps_used, f_norm = X_train_pca["quantum_representation_results"]
+    knn = KNeighborsClassifier(n_neighbors=7, device=device)
+    t0 = time.perf_counter()
+    score = cross_validate(knn, est, y, cv=StratifiedKFold(n_splits=folds, shuffle=True,
+                                                          random_state=1234))
+    sync()
+    t_cv = time.perf_counter() - t0
+    out = dict(accuracy=float(np.average(score["test_score"])), f_norm=float(f_norm),
+               qpca_fit_s=t_fit, transform_s=t_tr, cv_s=t_cv, total_s=t_fit + t_tr + t_cv)
+    if classic:
+        c = cross_validate(KNeighborsClassifier(n_neighbors=7, device=device),
+                           pca_model.transform(X), y,
+                           cv=StratifiedKFold(n_splits=folds, shuffle=True, random_state=1234))
+        out["classic_accuracy"] = float(np.average(c["test_score"]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=70_000)
@@ -55,35 +95,13 @@ def main():
                     help="rescale tomography rows to the true row norms (the reference's real "
                          "tomography returns unit rows, Utility.py:171-176)")
     a = ap.parse_args()
-
-    X, y = mnist_like(a.n, device=a.device)
-    t0 = time.perf_counter()
-    pca = qPCA(svd_solver="full", device=a.device, preserve_norm_tomography=a.preserve_norm)
-    pca.n_components = a.components
-    pca_model = pca.fit(X)
-    t_fit = time.perf_counter() - t0
-    # Transform the features: quantum representation with tomography error
-    t0 = time.perf_counter()
-    X_train_pca = pca_model.transform(X, classic_transform=False, epsilon_delta=a.error,
-                                      quantum_representation=True, norm="est_representation",
-                                      tomography=True)
-    t_tr = time.perf_counter() - t0
-    est, eps_used, f_norm = X_train_pca["quantum_representation_results"]
-    knn = KNeighborsClassifier(n_neighbors=7, device=a.device)
-    t0 = time.perf_counter()
-    score = cross_validate(knn, est, y, cv=StratifiedKFold(n_splits=a.folds, shuffle=True,
-                                                          random_state=1234))
-    t_cv = time.perf_counter() - t0
-    acc = float(np.average(score["test_score"]))
-    classic = cross_validate(KNeighborsClassifier(n_neighbors=7, device=a.device),
-                             pca_model.transform(X), y,
-                             cv=StratifiedKFold(n_splits=a.folds, shuffle=True, random_state=1234))
+    r = run(a.n, a.error, a.components, a.folds, a.device, a.preserve_norm)
     print(f"{a.folds}-fold Cross-validation - Estimated UE")
     print(f"(delta + epsilon): {a.error}")
-    print(f"Error-F_norm-Accuracy: {[[a.error, f_norm, acc]]}")
-    print(f"classical-representation accuracy: {np.average(classic['test_score']):.4f}")
-    print(f"timings: qPCA fit {t_fit:.2f}s, quantum transform {t_tr:.2f}s, CV {t_cv:.2f}s "
-          f"on {a.device}")
+    print(f"Error-F_norm-Accuracy: {[[a.error, r['f_norm'], r['accuracy']]]}")
+    print(f"classical-representation accuracy: {r['classic_accuracy']:.4f}")
+    print(f"timings: qPCA fit {r['qpca_fit_s']:.2f}s, quantum transform {r['transform_s']:.2f}s, "
+          f"CV {r['cv_s']:.2f}s on {a.device}")
 
 
 if __name__ == "__main__":
