@@ -915,11 +915,15 @@ __global__ void __launch_bounds__(256) delta_hist_kernel(const int* __restrict__
     if (dh[j]) atomicAdd(&hist[j], dh[j]);
 }
 
+// Entries carry their label (int2: row, label | out << 30), so the segment
+// pass never gathers labels / prev; the place pass also moves prev to the
+// new labels (only this thread reads these rows' prev, and only before), so
+// no separate prev <- labels copy follows the M-step.
 __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restrict__ labels,
-                                                            const int* __restrict__ prev,
+                                                            int* __restrict__ prev,
                                                             long long n, int k,
                                                             int* __restrict__ cursor,
-                                                            int* __restrict__ perm) {
+                                                            int2* __restrict__ perm) {
   extern __shared__ __attribute__((aligned(16))) int ds2[];
   int* lh = ds2;
   int* base = ds2 + k;
@@ -934,8 +938,8 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
   };
   auto place = [&](long long r, int l, int p) {
     if (l == p) return;
-    if (l >= 0 && l < k) perm[base[l] + atomicAdd(&lh[l], 1)] = (int)(r << 1);
-    if (p >= 0 && p < k) perm[base[p] + atomicAdd(&lh[p], 1)] = (int)((r << 1) | 1);
+    if (l >= 0 && l < k) perm[base[l] + atomicAdd(&lh[l], 1)] = make_int2((int)r, l);
+    if (p >= 0 && p < k) perm[base[p] + atomicAdd(&lh[p], 1)] = make_int2((int)r, p | (1 << 30));
   };
   for (long long r = r0 + 4 * threadIdx.x; r < r1; r += 1024) {
     if (r + 4 <= r1) {
@@ -959,8 +963,14 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
       const int4 p4 = *reinterpret_cast<const int4*>(prev + r);
       place(r, l4.x, p4.x); place(r + 1, l4.y, p4.y);
       place(r + 2, l4.z, p4.z); place(r + 3, l4.w, p4.w);
+      if (l4.x != p4.x || l4.y != p4.y || l4.z != p4.z || l4.w != p4.w)
+        *reinterpret_cast<int4*>(prev + r) = l4;
     } else {
-      for (long long q = r; q < r1; ++q) place(q, labels[q], prev[q]);
+      for (long long q = r; q < r1; ++q) {
+        const int l = labels[q], p = prev[q];
+        place(q, l, p);
+        if (l != p) prev[q] = l;
+      }
     }
   }
 }
@@ -985,10 +995,9 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
 // lane covers features 4 lane + 256 m, m < M, of every entry it streams.
 template <int M>
 __global__ void __launch_bounds__(512) delta_segment_kernel(
-    const float* __restrict__ X, const int* __restrict__ perm, const int* __restrict__ labels,
-    const int* __restrict__ prev, int d, int range, float xscale, double qscale,
-    double* __restrict__ sums, double* __restrict__ counts, double* __restrict__ qsum,
-    const int* __restrict__ valid_end) {
+    const float* __restrict__ X, const int2* __restrict__ perm, int d, int range, float xscale,
+    double qscale, double* __restrict__ sums, double* __restrict__ counts,
+    double* __restrict__ qsum, const int* __restrict__ valid_end) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // range <= 0: the entry count (on the device) is split evenly over the
   // grid - a few moved rows still keep every block busy
@@ -1034,22 +1043,20 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
     }
   };
   for (long long p = p0; p < p1; p += pstep) {
-    int code[U], ll[U];
+    int ll[U], out[U];
     float4 v[U][M];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long q = p + ustep * u;
-      code[u] = q < p1 ? perm[q] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = code[u] >= 0 ? (code[u] >> 1) : 0;
-      ll[u] = code[u] < 0 ? -1 : ((code[u] & 1) ? prev[r] : labels[r]);
+      const int2 e = q < p1 ? perm[q] : make_int2(0, -1);
+      const int r = e.x;
+      ll[u] = e.y < 0 ? -1 : (e.y & 0x3FFFFFFF);
+      out[u] = (e.y >> 30) & 1;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const int c0 = lane * 4 + 256 * m;
-        v[u][m] = (code[u] >= 0 && c0 < d) ? *reinterpret_cast<const float4*>(X + (size_t)r * d + c0)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[u][m] = (ll[u] >= 0 && c0 < d) ? *reinterpret_cast<const float4*>(X + (size_t)r * d + c0)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
 #pragma unroll
@@ -1062,7 +1069,7 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
         for (int m = 0; m < M; ++m) a[m][0] = a[m][1] = a[m][2] = a[m][3] = 0.0;
         aq = cnt = 0.0;
       }
-      const double sg = (code[u] & 1) ? -1.0 : 1.0;
+      const double sg = out[u] ? -1.0 : 1.0;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const float4 x = v[u][m];
@@ -1424,6 +1431,87 @@ __global__ void __launch_bounds__(256) pack_stats_kernel(
   if (i < kd) packed[i] = (double)sums[i] * xq;
   else if (i < kd + k) packed[i] = (double)counts[i - kd] * wq;
   else if (i == kd + k) packed[i] = inertia ? inertia[0] : 0.0;
+}
+
+// The incremental M-step's statistics in two launches (was four):
+// mstep_parts_kernel - blocks [0, nb): fixed-range fp64 partial sums of the
+// E-step's min-vs-label corrections corr[0:n] (the sum_f32_blocks
+// association); blocks [nb, nb + ceil(k / 4)): the per-cluster inertia parts
+// Q_c - 2 c.S_c + n_c |c|^2 (cluster_inertia_kernel);
+// pack_sum_kernel - packs sums / counts (pack_stats_kernel) while block 0
+// sums the nb + k partials (sum_partials association) into inertia[0] and
+// the bucket's tail.
+__global__ void __launch_bounds__(256) mstep_parts_kernel(
+    const float* __restrict__ corr, long long n, int nb, const double* __restrict__ sums,
+    const double* __restrict__ counts, const double* __restrict__ qsum,
+    const float* __restrict__ C, int k, int d, double xunit, double qunit,
+    double* __restrict__ part) {
+  __shared__ double red[256];
+  if ((int)blockIdx.x < nb) {
+    const long long per = (n + (long long)nb * 1024 - 1) / ((long long)nb * 1024) * 1024;
+    const long long b = (long long)blockIdx.x * per, e = min(n, b + per);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    const long long e4 = b < e ? b + (e - b) / 4 * 4 : b;
+    const float4* v4 = reinterpret_cast<const float4*>(corr);
+    long long i = b / 4 + threadIdx.x;
+    for (; i + 768 < e4 / 4; i += 1024) {
+      const float4 a = v4[i], c = v4[i + 256], f = v4[i + 512], g = v4[i + 768];
+      s0 += ((double)a.x + (double)a.y) + ((double)a.z + (double)a.w);
+      s1 += ((double)c.x + (double)c.y) + ((double)c.z + (double)c.w);
+      s2 += ((double)f.x + (double)f.y) + ((double)f.z + (double)f.w);
+      s3 += ((double)g.x + (double)g.y) + ((double)g.z + (double)g.w);
+    }
+    for (; i < e4 / 4; i += 256) {
+      const float4 a = v4[i];
+      s0 += ((double)a.x + (double)a.y) + ((double)a.z + (double)a.w);
+    }
+    for (long long t = e4 + threadIdx.x; t < e; t += 256) s1 += (double)corr[t];
+    red[threadIdx.x] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int c = ((int)blockIdx.x - nb) * 4 + (threadIdx.x >> 6);
+  if (c >= k) return;
+  double cs = 0.0, cc = 0.0;
+  for (int f = lane; f < d; f += 64) {
+    const double cf = (double)C[(size_t)c * d + f];
+    cs = fma(cf, sums[(size_t)c * d + f], cs);
+    cc = fma(cf, cf, cc);
+  }
+  cs = wave_sum(cs);
+  cc = wave_sum(cc);
+  if (lane == 0) part[nb + c] = qsum[c] * qunit - 2.0 * cs * xunit + counts[c] * cc;
+}
+
+__global__ void __launch_bounds__(256) pack_sum_kernel(
+    const double* __restrict__ sums, const double* __restrict__ counts,
+    const double* __restrict__ part, int npart, double* __restrict__ inertia,
+    double* __restrict__ packed, int k, int d, double xq, double wq) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long kd = (long long)k * d;
+  if (i < kd) packed[i] = (double)sums[i] * xq;
+  else if (i < kd + k) packed[i] = (double)counts[i - kd] * wq;
+  if (blockIdx.x == 0) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int t = threadIdx.x; t < npart; t += 256) s += part[t];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      inertia[0] = red[0];
+      packed[kd + k] = red[0];
+    }
+  }
 }
 
 // one workgroup per (padded) centroid row
@@ -1870,7 +1958,8 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
 
 // Incremental fixed-point cluster statistics (see delta_segment_kernel):
 // sums / counts / qsum are UPDATED (not overwritten) by the rows whose label
-// differs from prev; qexp is the quantum of the squared norms.
+// differs from prev, and prev becomes labels; qexp is the quantum of the
+// squared norms; ws_perm holds 2n int2 entries.
 int sq_centroid_delta(const void* X, const void* labels, const void* prev, void* sums,
                       void* counts, void* qsum, long long n, int d, int k, int xexp, int qexp,
                       void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
@@ -1884,7 +1973,7 @@ int sq_centroid_delta(const void* X, const void* labels, const void* prev, void*
   hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)ws_hist, k,
                      (int*)ws_cursor);
   hipLaunchKernelGGL(delta_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
-                     (const int*)labels, (const int*)prev, n, k, (int*)ws_cursor, (int*)ws_perm);
+                     (const int*)labels, (int*)prev, n, k, (int*)ws_cursor, (int2*)ws_perm);
   // entries <= 2n, usually far fewer: a fixed grid shares the scanned total
   const long long cap_blocks = (2 * n + 63) / 64;
   const unsigned grid = (unsigned)(cap_blocks < 2048 ? cap_blocks : 2048);
@@ -1892,9 +1981,9 @@ int sq_centroid_delta(const void* X, const void* labels, const void* prev, void*
              : d <= 512 ? delta_segment_kernel<2>
              : d <= 768 ? delta_segment_kernel<3> : delta_segment_kernel<4>;
   hipLaunchKernelGGL(seg, dim3(grid), dim3(512), 0, st, (const float*)X,
-                     (const int*)ws_perm, (const int*)labels, (const int*)prev, d, 0,
-                     ldexpf(1.0f, -xexp), ldexp(1.0, -qexp), (double*)sums, (double*)counts,
-                     (double*)qsum, (const int*)ws_cursor + (k - 1));
+                     (const int2*)ws_perm, d, 0, ldexpf(1.0f, -xexp), ldexp(1.0, -qexp),
+                     (double*)sums, (double*)counts, (double*)qsum,
+                     (const int*)ws_cursor + (k - 1));
   return (int)hipGetLastError();
 }
 
@@ -1917,6 +2006,25 @@ int sq_pack_stats(const void* sums, const void* counts, const void* inertia, voi
                      (hipStream_t)stream, (const double*)sums, (const double*)counts,
                      (const double*)inertia, (double*)packed, k, d, ldexp(1.0, xexp),
                      ldexp(1.0, wexp));
+  return (int)hipGetLastError();
+}
+
+// corr fp32 [n] (16-B aligned), part fp64 [512 + k]: the incremental
+// M-step's inertia (sum of cluster parts + corrections) and packed bucket
+int sq_mstep_stats(const void* sums, const void* counts, const void* qsum, const void* C, int k,
+                   int d, int xexp, int qexp, const void* corr, long long n, void* part,
+                   void* inertia, void* packed, void* stream) {
+  if (k <= 0 || ((uintptr_t)corr & 15u) != 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = 512;
+  hipLaunchKernelGGL(mstep_parts_kernel, dim3((unsigned)(nb + (k + 3) / 4)), dim3(256), 0, st,
+                     (const float*)corr, n, nb, (const double*)sums, (const double*)counts,
+                     (const double*)qsum, (const float*)C, k, d, ldexp(1.0, xexp),
+                     ldexp(1.0, qexp), (double*)part);
+  const long long tot = (long long)k * d + k;
+  hipLaunchKernelGGL(pack_sum_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                     (const double*)sums, (const double*)counts, (const double*)part, nb + k,
+                     (double*)inertia, (double*)packed, k, d, ldexp(1.0, xexp), 1.0);
   return (int)hipGetLastError();
 }
 

@@ -135,6 +135,9 @@ __attribute__((weak)) int sq_rows_f64(const void*, long long, const void*, long 
                                       long long, int, void*);
 __attribute__((weak)) int sq_centers_f16_operand(const void*, void*, int, int, int, int, double,
                                                  void*);
+__attribute__((weak)) int sq_mstep_stats(const void*, const void*, const void*, const void*, int, int,
+                                         int, int, const void*, long long, void*, void*, void*,
+                                         void*);
 __attribute__((weak)) int sq_pack_stats(const void* sums, const void* counts, const void* inertia,
                                         void* packed, int k, int d, int xexp, int wexp, void*);
 __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void* cn, void* labels, void* mind,
@@ -512,6 +515,17 @@ static PyObject* py_sum_f32(PyObject*, PyObject* a) {
   return ret(sq_sum_f32(P(v), n, P(part), extra, P(out), P(st)));
 }
 
+static PyObject* py_mstep_stats(PyObject*, PyObject* a) {
+  unsigned long long sums, counts, qsum, C, corr, part, inr, packed, st; int k, d, xe, qe;
+  long long n;
+  if (!PyArg_ParseTuple(a, "KKKKiiiiKLKKKK", &sums, &counts, &qsum, &C, &k, &d, &xe, &qe, &corr,
+                        &n, &part, &inr, &packed, &st))
+    return nullptr;
+  CHECK(sq_mstep_stats)
+  return ret(sq_mstep_stats(P(sums), P(counts), P(qsum), P(C), k, d, xe, qe, P(corr), n, P(part),
+                            P(inr), P(packed), P(st)));
+}
+
 static PyObject* py_centroid_finalize(PyObject*, PyObject* a) {
   unsigned long long pk, co, cnw, cb, clo, cn, sh, sc, oc, cf, cm2, kp, st; int k, d, kpad, pol;
   double nb, alpha; unsigned k0, k1, s0, s1;
@@ -634,6 +648,7 @@ static PyMethodDef methods[] = {
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},
+    {"mstep_stats", py_mstep_stats, METH_VARARGS, "incremental M-step inertia + packed bucket"},
     {"estep_f32", py_estep_f32, METH_VARARGS, "fp32-faithful fused E-step (fp16 hi/lo MFMA)"},
     {"estep_x64", py_estep_x64, METH_VARARGS, "certified filter E-step + fp64 re-check"},
     {"fill_mind", py_fill_mind, METH_VARARGS, "exact distance to the label for marked rows"},

@@ -197,7 +197,7 @@ class LloydEngine:
         if self.incremental:
             self.prev_labels = torch.full((self.n,), -1, dtype=torch.int32, device=dev)
             self.qsum = torch.zeros(self.k, dtype=torch.float64, device=dev)
-            self.perm2 = torch.empty(max(2 * self.n, 1), dtype=torch.int32, device=dev)
+            self.perm2 = torch.empty(max(4 * self.n, 1), dtype=torch.int32, device=dev)
             self.buf.corr = torch.zeros(max(self.n, 1), dtype=torch.float32, device=dev)
             nr = int(self._nrows_global)
             self.qexp = K.fixed_point_exp(self._max_abs ** 2 * self.dm, nr)
@@ -589,17 +589,22 @@ class LloydEngine:
                 self.counts.zero_()
                 self.qsum.zero_()
                 self.prev_labels.fill_(-1)
+            # (prev_labels <- labels inside the same pass)
             K.centroid_delta_native(self.Xm, labels, self.prev_labels, self.sums, self.counts,
                                     self.qsum, self.k, self.rws, self.perm2, self.qexp)
-            self.prev_labels.copy_(labels[:self.n])
             self.inc_valid = True
             Cold = self.C if self.dm == self.d else self._padded_centers()
-            K.cluster_inertia_native(self.sums, self.counts, self.qsum, Cold, self.k, self.dm,
-                                     self.rws, self.qexp, self.mind_part[512:512 + self.k])
-            K.sum_f32_native(self.buf.corr, self.n, self.mind_part, inertia, extra=self.k)
-            sums = self.sums if self.dm == self.d else self.sums[:, :self.d].contiguous()
-            K.pack_stats_native(sums, self.counts, inertia, self.packed, self.k, self.d,
-                                self.rws, weighted=False)
+            if self.dm == self.d:
+                # cluster parts + correction sums, then pack + total: 2 launches
+                K.mstep_stats_native(self.sums, self.counts, self.qsum, Cold, self.k, self.dm,
+                                     self.rws, self.qexp, self.buf.corr, self.n, self.mind_part,
+                                     inertia, self.packed)
+            else:
+                K.cluster_inertia_native(self.sums, self.counts, self.qsum, Cold, self.k, self.dm,
+                                         self.rws, self.qexp, self.mind_part[512:512 + self.k])
+                K.sum_f32_native(self.buf.corr, self.n, self.mind_part, inertia, extra=self.k)
+                K.pack_stats_native(self.sums[:, :self.d].contiguous(), self.counts, inertia,
+                                    self.packed, self.k, self.d, self.rws, weighted=False)
         if events is not None:
             events[0].record()
         with tracing.range("allreduce"):

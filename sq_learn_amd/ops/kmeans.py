@@ -426,11 +426,13 @@ def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWork
                           qexp):
     """Incremental fixed-point cluster statistics (csrc/kmeans.hip
     delta_segment_kernel): sums / counts / qsum are UPDATED by the rows whose
-    label differs from ``prev`` (prev = -1: the row enters).  Bit-identical
-    to recomputing them from scratch (exact integer arithmetic in fp64)."""
+    label differs from ``prev`` (prev = -1: the row enters), and ``prev``
+    becomes ``labels`` in the same pass.  Bit-identical to recomputing them
+    from scratch (exact integer arithmetic in fp64).  ``perm2``: int32
+    workspace of 4 n (2 n (row, label) entries)."""
     n, d = X.shape
     assert X.dtype == torch.float32 and X.is_contiguous() and d % 4 == 0 and d <= 1024
-    assert labels.dtype == torch.int32 and prev.dtype == torch.int32 and perm2.numel() >= 2 * n
+    assert labels.dtype == torch.int32 and prev.dtype == torch.int32 and perm2.numel() >= 4 * n
     assert sums.dtype == torch.float64 and sums.numel() >= k * d and qsum.numel() >= k
     rc = nat.native().centroid_delta(X.data_ptr(), labels.data_ptr(), prev.data_ptr(),
                                      sums.data_ptr(), counts.data_ptr(), qsum.data_ptr(), n, d, k,
@@ -448,6 +450,26 @@ def cluster_inertia_native(sums, counts, qsum, C, k, d, ws: ReduceWorkspace, qex
                                       nat.stream_handle(C.device))
     if rc:
         raise RuntimeError(f"cluster_inertia failed (hip error {rc})")
+
+
+def mstep_stats_native(sums, counts, qsum, C, k, d, ws: ReduceWorkspace, qexp, corr, n, part,
+                       inertia, packed):
+    """The incremental M-step's statistics in two launches (csrc/kmeans.hip
+    mstep_parts_kernel + pack_sum_kernel): per-cluster inertia parts at the
+    E-step's centroids C (fp32 [k][d]) and the fixed-range partial sums of
+    the corrections ``corr`` [n] into ``part`` (fp64 >= 512 + k), then the
+    packed all-reduce bucket [sums, counts, inertia] with inertia[0] = the
+    sum of all partials (the same association as cluster_inertia_native +
+    sum_f32_native + pack_stats_native, unweighted)."""
+    assert C.dtype == torch.float32 and C.is_contiguous() and tuple(C.shape) == (k, d)
+    assert part.numel() >= 512 + k and part.dtype == torch.float64
+    assert corr.dtype == torch.float32 and corr.data_ptr() % 16 == 0
+    rc = nat.native().mstep_stats(sums.data_ptr(), counts.data_ptr(), qsum.data_ptr(),
+                                  C.data_ptr(), k, d, ws.xexp, int(qexp), corr.data_ptr(), int(n),
+                                  part.data_ptr(), inertia.data_ptr(), packed.data_ptr(),
+                                  nat.stream_handle(C.device))
+    if rc:
+        raise RuntimeError(f"mstep_stats failed (hip error {rc})")
 
 
 def pack_stats_native(sums, counts, inertia, packed, k, d, ws: ReduceWorkspace, weighted=False):
