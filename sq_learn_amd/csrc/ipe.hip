@@ -523,7 +523,11 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   __shared__ float lip[16];
   // per-lane queues of the pairs that need the full sampler or fired
   // ([slot][thread]; entry = row slot (2 bits) | fired (1 bit) | centroid)
-  constexpr int QCAP = D4 <= 128 ? 8 : 3;
+  // a tile step pushes up to 4 entries per lane and the queue is drained
+  // whenever fewer than 4 slots are free: QCAP >= 4 (at d_pad = 1024 the
+  // 64 KiB of A fragments + 4 slots leave one workgroup per CU)
+  constexpr int QCAP = D4 <= 128 ? 8 : 4;
+  static_assert(QCAP >= 4, "a tile step pushes up to 4 queue entries per lane");
   __shared__ uint32_t qj[QCAP * 256];
   __shared__ float qip[QCAP * 256];
   // the lane's running (best D~, label) of its 4 row slots ([slot][thread]):
