@@ -7,12 +7,15 @@ screen's pair statistics (csrc/ipe.hip ``stats``).
 ``--center`` subtracts the column means first (as QMeans.fit does before
 its Lloyd loop)."""
 import argparse
+import os
+import sys
 import json
 import time
 
 import numpy as np
 import torch
 
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
 from sq_learn_amd.models._data import Data, gather_rows
 from sq_learn_amd.models.cluster._lloyd import LloydEngine
 from sq_learn_amd.parallel.comm import Comm

@@ -3,11 +3,14 @@ wall-clock per centre, with the screens (triangle + certified int8 bound)
 on and off, and the mean survivor / exact-row fractions.
 python benchmarks/kmpp_bench.py [--n N --k K --center --no-unpruned]"""
 import argparse
+import os
+import sys
 import time
 
 import numpy as np
 import torch
 
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
 from sq_learn_amd.models._data import Data
 from sq_learn_amd.models.cluster._init import kmeans_plusplus
 from sq_learn_amd.parallel.comm import Comm

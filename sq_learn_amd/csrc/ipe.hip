@@ -496,6 +496,55 @@ SQ_DEV bool ipe_better(float ob, uint32_t ok, int oj, float b, uint32_t kk, int 
   return ob < b || (ob == b && (ok < kk || (ok == kk && oj < jj)));
 }
 
+// One 16 x 16 tile of inner products (fp32 MFMA, D4 k-steps): the B
+// fragments (L2-resident centroid tile) and A fragments (LDS) of 8 k-steps
+// are loaded before their 8 MFMAs and the next 8 are in flight while those
+// run - one wait per MFMA on a load issued 8 MFMAs earlier, instead of a
+// full L2 round trip before every MFMA.
+template <int D4>
+SQ_DEV f32x4 ipe_tile_ip(const float* __restrict__ As, const float* __restrict__ bf, int lane) {
+  constexpr int B = 8;
+  static_assert(D4 % B == 0, "k-steps in batches of 8");
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float a0[B], b0[B], a1[B], b1[B];
+  // (sched_barrier: the scheduler, squeezed by the kernel's register budget,
+  // would otherwise sink each load next to its MFMA)
+#pragma unroll
+  for (int u = 0; u < B; ++u) {
+    b0[u] = bf[u * 64];
+    a0[u] = As[u * 64 + lane];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s0 = 0; s0 < D4; s0 += 2 * B) {
+    if (s0 + B < D4) {
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        b1[u] = bf[(s0 + B + u) * 64];
+        a1[u] = As[(s0 + B + u) * 64 + lane];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < B; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], b0[u], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s0 + B < D4) {
+      if (s0 + 2 * B < D4) {
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          b0[u] = bf[(s0 + 2 * B + u) * 64];
+          a0[u] = As[(s0 + 2 * B + u) * 64 + lane];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < B; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], b1[u], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  return acc;
+}
+
 // Layout per lane: register i holds pair (row row0 + 4 q4 + i, centroid
 // 16 t + c16) of tile t.  prune = 1 (odd Q): each row's hint pair is sampled
 // in full first (hint = hint_labels[row] when valid - the previous
@@ -583,11 +632,7 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     f32x4 bd = {INF, INF, INF, INF}, bip = {0.f, 0.f, 0.f, 0.f};
     int bjj[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
     for (int t = wave; t < n_tiles; t += 4) {
-      const float* bf = Cf + (size_t)t * D4 * 64 + lane;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 16
-      for (int s = 0; s < D4; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
+      const f32x4 acc = ipe_tile_ip<D4>(As, Cf + (size_t)t * D4 * 64 + lane, lane);
       const int j = t * 16 + c16;
       if (j < k) {
         const float ny2 = cn[j];
@@ -739,11 +784,7 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
       }
     } else {
       const int t = wave + 4 * stp;
-      const float* bf = Cf + (size_t)t * D4 * 64 + lane;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 16
-      for (int s = 0; s < D4; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(As[s * 64 + lane], bf[s * 64], acc, 0, 0, 0);
+      const f32x4 acc = ipe_tile_ip<D4>(As, Cf + (size_t)t * D4 * 64 + lane, lane);
       const int j = t * 16 + c16;
       if (j < k) {   // padded centroid columns do nothing
         const float ny2 = cn[j];

@@ -188,34 +188,44 @@ __global__ void __launch_bounds__(256) kmpp_cc_kernel(
   }
 }
 
-// wave-aggregated append of this lane's item when ``take``
-SQ_DEV void wave_append(bool take, int value, int* __restrict__ list, int* __restrict__ counter) {
+// Row lists are per-block segments: block b of the fixed partition owns
+// list[b R, b R + count[b]) (no global atomics - a single list counter for
+// 10M rows serialised ~156k wave atomics per pass).  Append of this lane's
+// item when ``take``: one LDS atomic per wave.
+SQ_DEV void seg_append(bool take, int value, int* __restrict__ seg, int* lcnt) {
   const unsigned long long b = __ballot(take);
   if (b == 0ull) return;
   const int lane = threadIdx.x & 63;
   int base = 0;
-  if (lane == 0) base = atomicAdd(counter, (int)__popcll(b));
+  if (lane == 0) base = atomicAdd(lcnt, (int)__popcll(b));
   base = __shfl(base, 0, 64);
   if (take) {
     const unsigned long long below = b & ((1ull << lane) - 1ull);
-    list[base + (int)__popcll(below)] = value;
+    seg[base + (int)__popcll(below)] = value;
   }
 }
 
 // ---------------------------------------------------- 1. triangle screen
 // lazy update of the previous step's winner (best_prev < 0: none), mask_out
-// cleared, rows with a live trial appended to surv (prune) or exact (!prune)
+// cleared, rows with a live trial appended to this block's segment of surv
+// (prune) or of exact (!prune); scount / ecount[b] = the segment length.
 __global__ void __launch_bounds__(256) kmpp_screen_kernel(
     float* __restrict__ closest, int* __restrict__ nearest,
     const uint16_t* __restrict__ mask_prev, const float* __restrict__ Dprev,
     const int* __restrict__ best_prev, int c_prev, const float* __restrict__ cc, int ldcc, int t,
-    long long n, uint16_t* __restrict__ mask_out, int* __restrict__ surv, int* __restrict__ exact,
-    int* __restrict__ counters, int prune) {
+    long long n, long long R, uint16_t* __restrict__ mask_out, int* __restrict__ surv,
+    int* __restrict__ exact, int* __restrict__ scount, int* __restrict__ ecount, int prune) {
+  __shared__ int lcnt;
   const int bp = best_prev ? *best_prev : -1;
-  for (long long i0 = (long long)blockIdx.x * 256; i0 < n; i0 += (long long)gridDim.x * 256) {
+  const long long r0 = (long long)blockIdx.x * R;
+  const long long r1 = r0 + R < n ? r0 + R : n;
+  int* seg = (prune ? surv : exact) + r0;
+  if (threadIdx.x == 0) lcnt = 0;
+  __syncthreads();
+  for (long long i0 = r0; i0 < r1; i0 += 256) {
     const long long i = i0 + threadIdx.x;
     bool live = false;
-    if (i < n) {
+    if (i < r1) {
       float cl = closest[i];
       int a = nearest[i];
       if (bp >= 0 && ((mask_prev[i] >> bp) & 1u)) {
@@ -232,8 +242,10 @@ __global__ void __launch_bounds__(256) kmpp_screen_kernel(
         for (int j = 0; j < t; ++j) live |= !(cc[(size_t)j * ldcc + a] > lim);
       }
     }
-    wave_append(live, (int)i, prune ? surv : exact, counters + (prune ? 0 : 1));
+    seg_append(live, (int)i, seg, &lcnt);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) (prune ? scount : ecount)[blockIdx.x] = lcnt;
 }
 
 // ------------------------------------------------ 2. certified int8 bound
@@ -242,20 +254,26 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
     const uint8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
     const float* __restrict__ erow, const float* __restrict__ xq2,
     const float* __restrict__ closest, const float* __restrict__ candq,
-    const float* __restrict__ cinfo, int t, int d, const int* __restrict__ surv,
-    int* __restrict__ exact, int* __restrict__ counters) {
+    const float* __restrict__ cinfo, int t, int d, long long R, const int* __restrict__ surv,
+    const int* __restrict__ scount, int* __restrict__ exact, int* __restrict__ ecount) {
   __shared__ uint32_t tile[4][64 * kKqStride];
+  __shared__ int lcnt;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* my = tile[wave];
-  const int cnt = counters[0];
+  const long long r0 = (long long)blockIdx.x * R;
+  const int cnt = scount[blockIdx.x];
+  const int* sseg = surv + r0;
+  int* eseg = exact + r0;
+  if (threadIdx.x == 0) lcnt = 0;
+  __syncthreads();
   const long long nb = (cnt + 63) / 64;
   const int ntiles = dq / kKqTile + (dq % kKqTile ? 1 : 0);
   // rigorous fp32 error of the int8 dot products: gamma_d = d u / (1 - d u)
   const float gam = (float)((double)dq * 5.960464477539063e-08 / (1.0 - (double)dq * 5.960464477539063e-08));
   const float rel = 3.0f * (float)(d + 2) * 5.960464477539063e-08f + 1e-6f;
-  for (long long b = (long long)blockIdx.x * 4 + wave; b < nb; b += (long long)gridDim.x * 4) {
+  for (long long b = wave; b < nb; b += 4) {
     const long long e = b * 64 + lane;
-    const int row = e < cnt ? surv[e] : -1;
+    const int row = e < cnt ? sseg[e] : -1;
     float acc[TMAX];
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) acc[j] = 0.0f;
@@ -316,8 +334,10 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
         }
       }
     }
-    wave_append(need, row, exact, counters + 1);
+    seg_append(need, row, eseg, &lcnt);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) ecount[blockIdx.x] = lcnt;
 }
 
 // ------------------------------------------------------- 3. exact pass
@@ -326,18 +346,19 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
     const float* __restrict__ X, long long ldx, int d, long long n, int t,
     const float* __restrict__ cand, const float* __restrict__ closest,
     const double* __restrict__ w, double scale, const int* __restrict__ exact,
-    const int* __restrict__ counters, uint16_t* __restrict__ mask_out, float* __restrict__ Dout,
+    const int* __restrict__ ecount, uint16_t* __restrict__ mask_out, float* __restrict__ Dout,
     double* __restrict__ delta_part, long long R) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kKppStride];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* my = tile[wave];
-  const int cnt = counters[1];
+  const int cnt = ecount[blockIdx.x];
+  const int* eseg = exact + (long long)blockIdx.x * R;
   const long long nb = (cnt + 63) / 64;
   const int ntiles = (d + kKppTile - 1) / kKppTile;
   const int lrow = lane >> 3, lchunk = lane & 7;
-  for (long long b = (long long)blockIdx.x * 4 + wave; b < nb; b += (long long)gridDim.x * 4) {
+  for (long long b = wave; b < nb; b += 4) {
     const long long e = b * 64 + lane;
-    const int row = e < cnt ? exact[e] : -1;
+    const int row = e < cnt ? eseg[e] : -1;
     float acc[TMAX];
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) acc[j] = 0.0f;
@@ -424,7 +445,8 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
     sc[tid] += a;
     __syncthreads();
   }
-  double run = sc[tid] - s;   // exclusive prefix of this thread's chunk
+  const double excl = sc[tid] - s;   // exclusive prefix of this thread's chunk
+  double run = excl;
   long long hit = -1;
   for (int g = g0; g < g1; ++g) {
     run += block_tot[g];
@@ -433,10 +455,10 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
   if (hit >= 0) atomicMin(&found, hit);
   __syncthreads();
   const long long bsel = found;
-  // exclusive prefix of the chosen block (every thread recomputes the same sum)
-  if (tid == 0) {
-    double p = 0.0;
-    for (long long g = 0; g < bsel; ++g) p += block_tot[g];
+  // exclusive prefix of the chosen block: from the thread whose chunk holds it
+  if (bsel >= g0 && bsel < g1) {
+    double p = excl;
+    for (long long g = g0; g < bsel; ++g) p += block_tot[g];
     base = p;
   }
   __syncthreads();
@@ -528,31 +550,33 @@ int sq_kmpp_cc(const void* cand, const void* C, int c, int d, int t, void* cc, i
   return (int)hipGetLastError();
 }
 
+// G blocks of R rows (G R >= n); scount / ecount int [G]
 int sq_kmpp_screen(void* closest, void* nearest, const void* mask_prev, const void* Dprev,
                    const void* best_prev, int c_prev, const void* cc, int ldcc, int t, long long n,
-                   void* mask_out, void* surv, void* exact, void* counters, int prune,
-                   void* stream) {
+                   long long R, int G, void* mask_out, void* surv, void* exact, void* scount,
+                   void* ecount, int prune, void* stream) {
   if (n <= 0) return 0;
-  if (t < 1 || t > 16) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmpp_screen_kernel, dim3(kpp_grid(n)), dim3(256), 0, (hipStream_t)stream,
+  if (t < 1 || t > 16 || R <= 0 || G <= 0 || (long long)G * R < n) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_screen_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream,
                      (float*)closest, (int*)nearest, (const uint16_t*)mask_prev,
                      (const float*)Dprev, (const int*)best_prev, c_prev, (const float*)cc, ldcc,
-                     t, n, (uint16_t*)mask_out, (int*)surv, (int*)exact, (int*)counters, prune);
+                     t, n, R, (uint16_t*)mask_out, (int*)surv, (int*)exact, (int*)scount,
+                     (int*)ecount, prune);
   return (int)hipGetLastError();
 }
 
 int sq_kmpp_bound(const void* Xq, int dq, const void* srow, const void* erow, const void* xq2,
                   const void* closest, const void* candq, const void* cinfo, int t, int d,
-                  long long n, const void* surv, void* exact, void* counters, void* stream) {
+                  long long n, long long R, int G, const void* surv, const void* scount,
+                  void* exact, void* ecount, void* stream) {
   if (n <= 0) return 0;
-  if (t < 1 || t > 16 || (dq & 15) || dq < d) return (int)hipErrorInvalidValue;
-  const int grid = kpp_grid(n);
+  if (t < 1 || t > 16 || (dq & 15) || dq < d || R <= 0 || G <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
 #define LAUNCH(TM)                                                                              \
-  hipLaunchKernelGGL(kmpp_bound_kernel<TM>, dim3(grid), dim3(256), 0, st, (const uint8_t*)Xq,  \
+  hipLaunchKernelGGL(kmpp_bound_kernel<TM>, dim3(G), dim3(256), 0, st, (const uint8_t*)Xq,     \
                      dq, (const float*)srow, (const float*)erow, (const float*)xq2,            \
-                     (const float*)closest, (const float*)candq, (const float*)cinfo, t, d,    \
-                     (const int*)surv, (int*)exact, (int*)counters)
+                     (const float*)closest, (const float*)candq, (const float*)cinfo, t, d, R, \
+                     (const int*)surv, (const int*)scount, (int*)exact, (int*)ecount)
   if (t <= 4) LAUNCH(4);
   else if (t <= 8) LAUNCH(8);
   else LAUNCH(16);
@@ -562,17 +586,16 @@ int sq_kmpp_bound(const void* Xq, int dq, const void* srow, const void* erow, co
 
 int sq_kmpp_exact(const void* X, long long ldx, int d, long long n, int t, const void* cand,
                   const void* closest, const void* w, double scale, const void* exact,
-                  const void* counters, void* mask_out, void* Dout, void* delta_part, long long R,
-                  void* stream) {
+                  const void* ecount, void* mask_out, void* Dout, void* delta_part, long long R,
+                  int G, void* stream) {
   if (n <= 0) return 0;
-  if (t < 1 || t > 16 || d <= 0 || (d & 3) || ldx < d || (ldx & 3) || R <= 0)
+  if (t < 1 || t > 16 || d <= 0 || (d & 3) || ldx < d || (ldx & 3) || R <= 0 || G <= 0)
     return (int)hipErrorInvalidValue;
-  const int grid = kpp_grid(n);
   hipStream_t st = (hipStream_t)stream;
 #define LAUNCH(TM)                                                                              \
-  hipLaunchKernelGGL(kmpp_exact_kernel<TM>, dim3(grid), dim3(256), 0, st, (const float*)X, ldx, \
+  hipLaunchKernelGGL(kmpp_exact_kernel<TM>, dim3(G), dim3(256), 0, st, (const float*)X, ldx,    \
                      d, n, t, (const float*)cand, (const float*)closest, (const double*)w,     \
-                     scale, (const int*)exact, (const int*)counters, (uint16_t*)mask_out,      \
+                     scale, (const int*)exact, (const int*)ecount, (uint16_t*)mask_out,        \
                      (float*)Dout, (double*)delta_part, R)
   if (t <= 4) LAUNCH(4);
   else if (t <= 8) LAUNCH(8);

@@ -113,14 +113,15 @@ __attribute__((weak)) int sq_kmpp_block_totals(const void*, const void*, long lo
 __attribute__((weak)) int sq_kmpp_cc(const void*, const void*, int, int, int, void*, int, void*,
                                      void*, int, void*, long long, void*, void*);
 __attribute__((weak)) int sq_kmpp_screen(void*, void*, const void*, const void*, const void*, int,
-                                         const void*, int, int, long long, void*, void*, void*,
-                                         void*, int, void*);
+                                         const void*, int, int, long long, long long, int, void*,
+                                         void*, void*, void*, void*, int, void*);
 __attribute__((weak)) int sq_kmpp_bound(const void*, int, const void*, const void*, const void*,
                                         const void*, const void*, const void*, int, int,
-                                        long long, const void*, void*, void*, void*);
+                                        long long, long long, int, const void*, const void*,
+                                        void*, void*, void*);
 __attribute__((weak)) int sq_kmpp_exact(const void*, long long, int, long long, int, const void*,
                                         const void*, const void*, double, const void*,
-                                        const void*, void*, void*, void*, long long, void*);
+                                        const void*, void*, void*, void*, long long, int, void*);
 __attribute__((weak)) int sq_kmpp_pick(const void*, int, long long, long long, const void*, int,
                                        const void*, const void*, const void*, const void*,
                                        const void*, double, void*, void*);
@@ -467,35 +468,36 @@ static PyObject* py_kmpp_cc(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_kmpp_screen(PyObject*, PyObject* a) {
-  unsigned long long cl, nr, mp, Dp, bp, cc, mo, sv, ex, cnt, st; int cp, ldcc, t, prune;
-  long long n;
-  if (!PyArg_ParseTuple(a, "KKKKKiKiiLKKKKiK", &cl, &nr, &mp, &Dp, &bp, &cp, &cc, &ldcc, &t, &n,
-                        &mo, &sv, &ex, &cnt, &prune, &st))
+  unsigned long long cl, nr, mp, Dp, bp, cc, mo, sv, ex, sc, ec, st; int cp, ldcc, t, G, prune;
+  long long n, R;
+  if (!PyArg_ParseTuple(a, "KKKKKiKiiLLiKKKKKiK", &cl, &nr, &mp, &Dp, &bp, &cp, &cc, &ldcc, &t, &n,
+                        &R, &G, &mo, &sv, &ex, &sc, &ec, &prune, &st))
     return nullptr;
   CHECK(sq_kmpp_screen)
-  return ret(sq_kmpp_screen(P(cl), P(nr), P(mp), P(Dp), P(bp), cp, P(cc), ldcc, t, n, P(mo), P(sv),
-                            P(ex), P(cnt), prune, P(st)));
+  return ret(sq_kmpp_screen(P(cl), P(nr), P(mp), P(Dp), P(bp), cp, P(cc), ldcc, t, n, R, G, P(mo),
+                            P(sv), P(ex), P(sc), P(ec), prune, P(st)));
 }
 
 static PyObject* py_kmpp_bound(PyObject*, PyObject* a) {
-  unsigned long long Xq, sr, er, q2, cl, cq, ci, sv, ex, cnt, st; int dq, t, d; long long n;
-  if (!PyArg_ParseTuple(a, "KiKKKKKKiiLKKKK", &Xq, &dq, &sr, &er, &q2, &cl, &cq, &ci, &t, &d, &n,
-                        &sv, &ex, &cnt, &st))
+  unsigned long long Xq, sr, er, q2, cl, cq, ci, sv, sc, ex, ec, st; int dq, t, d, G;
+  long long n, R;
+  if (!PyArg_ParseTuple(a, "KiKKKKKKiiLLiKKKKK", &Xq, &dq, &sr, &er, &q2, &cl, &cq, &ci, &t, &d, &n,
+                        &R, &G, &sv, &sc, &ex, &ec, &st))
     return nullptr;
   CHECK(sq_kmpp_bound)
-  return ret(sq_kmpp_bound(P(Xq), dq, P(sr), P(er), P(q2), P(cl), P(cq), P(ci), t, d, n, P(sv),
-                           P(ex), P(cnt), P(st)));
+  return ret(sq_kmpp_bound(P(Xq), dq, P(sr), P(er), P(q2), P(cl), P(cq), P(ci), t, d, n, R, G,
+                           P(sv), P(sc), P(ex), P(ec), P(st)));
 }
 
 static PyObject* py_kmpp_exact(PyObject*, PyObject* a) {
-  unsigned long long X, cand, cl, w, ex, cnt, mo, Do, dp, st; long long ldx, n, R; int d, t;
+  unsigned long long X, cand, cl, w, ex, ec, mo, Do, dp, st; long long ldx, n, R; int d, t, G;
   double scale;
-  if (!PyArg_ParseTuple(a, "KLiLiKKKdKKKKKLK", &X, &ldx, &d, &n, &t, &cand, &cl, &w, &scale, &ex,
-                        &cnt, &mo, &Do, &dp, &R, &st))
+  if (!PyArg_ParseTuple(a, "KLiLiKKKdKKKKKLiK", &X, &ldx, &d, &n, &t, &cand, &cl, &w, &scale, &ex,
+                        &ec, &mo, &Do, &dp, &R, &G, &st))
     return nullptr;
   CHECK(sq_kmpp_exact)
-  return ret(sq_kmpp_exact(P(X), ldx, d, n, t, P(cand), P(cl), P(w), scale, P(ex), P(cnt), P(mo),
-                           P(Do), P(dp), R, P(st)));
+  return ret(sq_kmpp_exact(P(X), ldx, d, n, t, P(cand), P(cl), P(w), scale, P(ex), P(ec), P(mo),
+                           P(Do), P(dp), R, G, P(st)));
 }
 
 static PyObject* py_kmpp_pick(PyObject*, PyObject* a) {

@@ -806,8 +806,11 @@ class KmppState:
         self.nearest = torch.zeros(nn, dtype=torch.int32, device=dev)
         self.mask = [torch.zeros(nn, dtype=torch.int16, device=dev) for _ in range(2)]
         self.D = [torch.empty((t, nn), dtype=torch.float32, device=dev) for _ in range(2)]
-        self.surv = torch.empty(nn, dtype=torch.int32, device=dev)
-        self.exact = torch.empty(nn, dtype=torch.int32, device=dev)
+        # per-block row-list segments (block b: rows [b R, b R + count[b]))
+        self.surv = torch.empty(max(self.G * self.R, 1), dtype=torch.int32, device=dev)
+        self.exact = torch.empty(max(self.G * self.R, 1), dtype=torch.int32, device=dev)
+        self.scount = torch.zeros(self.G, dtype=torch.int32, device=dev)
+        self.ecount = torch.zeros(self.G, dtype=torch.int32, device=dev)
         self.counters = torch.zeros(4, dtype=torch.int32, device=dev)
         self.cc = torch.zeros((t, self.k), dtype=torch.float32, device=dev)
         self.cinfo = torch.zeros((t, 4), dtype=torch.float32, device=dev)
@@ -880,21 +883,23 @@ class KmppState:
             _rc(m.kmpp_screen(self.closest.data_ptr(), self.nearest.data_ptr(),
                               self.mask[prev].data_ptr(), self.D[prev].data_ptr(),
                               0 if self.best is None else self.best.data_ptr(), self.c_last,
-                              self.cc.data_ptr(), self.k, t, self.n, self.mask[cur].data_ptr(),
-                              self.surv.data_ptr(), self.exact.data_ptr(),
-                              self.counters.data_ptr(), int(self.prune), st), "kmpp_screen")
+                              self.cc.data_ptr(), self.k, t, self.n, self.R, self.G,
+                              self.mask[cur].data_ptr(), self.surv.data_ptr(),
+                              self.exact.data_ptr(), self.scount.data_ptr(),
+                              self.ecount.data_ptr(), int(self.prune), st), "kmpp_screen")
             if self.prune:
                 _rc(m.kmpp_bound(self.Xq.data_ptr(), self.dq, self.srow.data_ptr(),
                                  self.erow.data_ptr(), self.xq2.data_ptr(),
                                  self.closest.data_ptr(), self.candq.data_ptr(),
-                                 self.cinfo.data_ptr(), t, self.d, self.n, self.surv.data_ptr(),
-                                 self.exact.data_ptr(), self.counters.data_ptr(), st),
+                                 self.cinfo.data_ptr(), t, self.d, self.n, self.R, self.G,
+                                 self.surv.data_ptr(), self.scount.data_ptr(),
+                                 self.exact.data_ptr(), self.ecount.data_ptr(), st),
                     "kmpp_bound")
             _rc(m.kmpp_exact(self.X.data_ptr(), self.ldx, self.d, self.n, t, cand.data_ptr(),
                              self.closest.data_ptr(), 0 if self.w is None else self.w.data_ptr(),
-                             self.scale, self.exact.data_ptr(), self.counters.data_ptr(),
+                             self.scale, self.exact.data_ptr(), self.ecount.data_ptr(),
                              self.mask[cur].data_ptr(), self.D[cur].data_ptr(),
-                             self.delta.data_ptr(), self.R, st), "kmpp_exact")
+                             self.delta.data_ptr(), self.R, self.G, st), "kmpp_exact")
         return self.delta.sum(0)
 
     def apply(self, best, c):
@@ -909,7 +914,9 @@ class KmppState:
     def list_counts(self):
         """[survivors of the triangle screen, rows of the exact pass] of the
         last trial pass (host read; diagnostics)."""
-        return self.counters[:2].tolist()
+        if not self.prune:
+            return [0, int(self.ecount.sum())]
+        return [int(self.scount.sum()), int(self.ecount.sum())]
 
 
 def _rc(rc, name):

@@ -289,9 +289,9 @@ def test_ipe_pruned_matches_unpruned_law_many_centroids(cuda):
 
 # ------------------------------------------------- hazard-budget screening
 def _fire_case(d=96, K_=64):
-    """Q = 1, M ~ 6-8k bins: pair 0 near, 63 identical competitors (same
-    |c|, same x.c) ~ 800 bins above it: each competitor's hazard ~ 9e-4, so
-    ~5 % of the rows fire at least once; ~0.4 % are won by a competitor."""
+    """Q = 1, eps = 0.001: pair 0 near, 63 identical competitors (same |c|,
+    same x.c) ~ 600+ bins above it: each competitor's hazard ~ 8e-4, so
+    ~5 % of the rows fire at least once; ~0.1 % are won by a competitor."""
     rng = np.random.default_rng(21)
     x = rng.standard_normal(d)
     B = rng.standard_normal((d, K_))
@@ -299,7 +299,7 @@ def _fire_case(d=96, K_=64):
     Qm, _ = np.linalg.qr(B)                      # K_ orthonormal directions, all orthogonal to x
     C = np.empty((K_, d))
     C[0] = x + 0.9 * Qm[:, 0]
-    C[1:] = x[None] - 4.0 * Qm[:, 1:].T
+    C[1:] = x[None] - 6.0 * Qm[:, 1:].T
     return x.astype(np.float32), C.astype(np.float32)
 
 
@@ -344,7 +344,12 @@ def test_ipe_hazard_fire_path_exact_law(cuda, hint):
     st = torch.zeros(5, dtype=torch.int64, device=cuda)
     lab, mind, *_ = _run_rows(x, C, n, eps, 1, cuda, 3, True, hint=hint, stats=st)
     scr, full, fires, exact, p1 = st.tolist()
-    assert fires > 0.01 * n and exact > 0.001 * n, st.tolist()
+    if hint == 5:
+        # a far hint's estimate is a poor threshold: every pair is competitive
+        # with it and takes the full sampler (same law, no pruning)
+        assert full > 0.9 * n * C.shape[0], st.tolist()
+    else:
+        assert fires > 0.01 * n and exact > 0.001 * n, st.tolist()
     assert (p1 > 0) == (hint is None)
     v0, c0, v1, c1 = _competitor_law(x, C, eps)
     vals = np.concatenate([v0, v1])
