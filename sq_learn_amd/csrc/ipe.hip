@@ -902,6 +902,502 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
   }
 }
 
+
+// ------------------------------------------- row-group layout (production)
+// R row groups of 16 rows per workgroup: every B fragment (one L2 load per
+// k-step) feeds R MFMAs (R independent accumulator chains), so the centroid
+// traffic per row drops R-fold; the R A fragments of a k-step are one LDS
+// read (As[(s 64 + l) R + g]).
+template <int D4, int R>
+SQ_DEV void ipe_tile_ipR(const float* __restrict__ As, const float* __restrict__ bf, int lane,
+                         f32x4 (&acc)[R]) {
+  constexpr int B = 8;
+  static_assert(D4 % B == 0, "k-steps in batches of 8");
+  static_assert(R == 1 || R == 2, "one or two row groups");
+#pragma unroll
+  for (int g = 0; g < R; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float a0[B][R], b0[B], a1[B][R], b1[B];
+  auto lda = [&](float (&a)[B][R], int s) {
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      if constexpr (R == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(As + (size_t)((s + u) * 64 + lane) * 2);
+        a[u][0] = v.x;
+        a[u][1] = v.y;
+      } else {
+        a[u][0] = As[(s + u) * 64 + lane];
+      }
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < B; ++u) b0[u] = bf[u * 64];
+  lda(a0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s0 = 0; s0 < D4; s0 += 2 * B) {
+    if (s0 + B < D4) {
+#pragma unroll
+      for (int u = 0; u < B; ++u) b1[u] = bf[(s0 + B + u) * 64];
+      lda(a1, s0 + B);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < B; ++u)
+#pragma unroll
+      for (int g = 0; g < R; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u][g], b0[u], acc[g], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s0 + B < D4) {
+      if (s0 + 2 * B < D4) {
+#pragma unroll
+        for (int u = 0; u < B; ++u) b0[u] = bf[(s0 + 2 * B + u) * 64];
+        lda(a0, s0 + 2 * B);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+#pragma unroll
+        for (int g = 0; g < R; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][g], b1[u], acc[g], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// Row thresholds from label hints, one lane per row (the pre-pass of the
+// row-group kernel): the hint pair's inner product by 16 lanes (the fp32
+// summation order of ipe_fused_kernel's hint path), then every lane samples
+// its row's hint pair in full.  thr = its estimate, hj = the hint centroid;
+// hj = -2 marks an invalid hint (the main kernel's first sweep decides).
+template <bool STATS>
+__global__ void __launch_bounds__(256) ipe_hint_kernel(
+    const float* __restrict__ X, long long ldx, const float* __restrict__ C,
+    const int* __restrict__ hint_labels, const float* __restrict__ xn,
+    const float* __restrict__ cn, float* __restrict__ thr, int* __restrict__ hj, long long n, int d,
+    int k, double eps, int Q, RngKey key, long long row_offset,
+    unsigned long long* __restrict__ stats) {
+  __shared__ float sip[256];
+  __shared__ int slab[256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, q4 = lane >> 4;
+  const long long rb = (long long)blockIdx.x * 256 + wave * 64;
+  for (int it = 0; it < 16; ++it) {
+    const int x = 4 * it + q4;
+    const long long r = rb + x;
+    const int l = r < n ? hint_labels[r] : -1;
+    const bool ok = r < n && l >= 0 && l < k;
+    float s = 0.0f;
+    if (ok)
+      for (int f = c16; f < d; f += 16) s = fmaf(X[(size_t)r * ldx + f], C[(size_t)l * d + f], s);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (c16 == 0) {
+      sip[wave * 64 + x] = s;
+      slab[wave * 64 + x] = ok ? l : -2;
+    }
+  }
+  __syncthreads();
+  const long long r = rb + lane;
+  uint32_t full = 0;
+  if (r < n) {
+    const int l = slab[threadIdx.x];
+    float t = __builtin_inff();
+    if (l >= 0) {
+      const long long g = row_offset + r;
+      t = ipe_distance(sip[threadIdx.x], (double)xn[r], (double)cn[l], eps, Q, key,
+                       (unsigned long long)g * (unsigned long long)k + (unsigned long long)l);
+      full = 1;
+    }
+    thr[r] = t;
+    hj[r] = l;
+  }
+  if (STATS) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) full += (uint32_t)__shfl_xor((int)full, o, 64);
+    if (lane == 0) atomicAdd(stats + 1, (unsigned long long)full);
+  }
+}
+
+// The production IPE kernel: 16 R rows per workgroup, the 4 waves split the
+// centroid tiles (t = wave mod 4, as the streams' classes), register i of
+// row group g of a lane = pair (row 16 g + 4 q4 + i, centroid 16 t + c16).
+// Every (row, class, c16) stream, threshold, hazard, budget block and
+// sampler stream is the one of ipe_fused_kernel above, so the two layouts
+// return the same labels bit for bit.  Pairs that need a sampler are
+// appended to a WAVE-wide LDS list (ballot + mbcnt); a drain runs them 64 at
+// a time, one per lane.  The rows' thresholds come from ipe_hint_kernel
+// (ext_thr / ext_hj) or, for rows without a hint, from a first exact sweep
+// whose hint pairs wave 0 samples for the whole workgroup; what is left in
+// the 4 lists after the last tile is drained as ONE pooled list (64-entry
+// batches dealt to the waves) - the samplers' cost is paid per up-to-64
+// pairs of a workgroup, not per up-to-64 pairs of a wave.  Each row's
+// running best of a wave is held by lane (row) of that wave (registers);
+// drain results reach it through a 64-entry LDS result batch.
+template <int D4, int R, bool STATS>
+__global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
+    const float* __restrict__ X, long long ldx, const float* __restrict__ Cf,
+    const float* __restrict__ ext_thr, const int* __restrict__ ext_hj,
+    const float* __restrict__ xn, const float* __restrict__ cn, int* __restrict__ labels,
+    float* __restrict__ mind, long long n, int d, int k, int n_tiles, double eps, int Q,
+    RngKey key, RngKey tie_key, RngKey skip_key, IpeScreen sc, long long row_offset, int prune,
+    unsigned long long* __restrict__ stats) {
+  constexpr int NR = 16 * R;                   // rows per workgroup
+  constexpr int CAP = D4 >= 256 ? 256 : 512;   // wave list capacity (>= one unit's 256 pushes)
+  extern __shared__ __attribute__((aligned(16))) float As[];   // [D4][64][R]
+  __shared__ uint32_t qe[4][CAP];
+  __shared__ float qip[4][CAP];
+  __shared__ uint32_t re[4][64];
+  __shared__ float rdt[4][64];
+  __shared__ uint32_t nbud[4][256];            // [slot i][thread]: budgets redrawn by a drain
+  __shared__ float r_nx2[NR], r_thr[NR], r_sthr[NR];
+  __shared__ int r_hj[NR];
+  __shared__ float mb[4][NR], mip[4][NR];
+  __shared__ uint32_t mk[4][NR];
+  __shared__ int mj[4][NR];
+  __shared__ int qc[4];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, q4 = lane >> 4;
+  const long long row0 = (long long)blockIdx.x * NR;
+  const float INF = __builtin_inff();
+  uint32_t st_scr = 0, st_full = 0, st_fire = 0, st_exact = 0;
+  // A fragments, row-major reads (coalesced): row rl, feature f ->
+  // As[((f / 4) 64 + (rl mod 16) + 16 (f mod 4)) R + rl / 16]; rows past n clamped
+  for (int e = threadIdx.x; e < NR * D4 * 4; e += 256) {
+    const int rl = e / (D4 * 4), f = e - rl * (D4 * 4);
+    const long long r = row0 + rl < n ? row0 + rl : n - 1;
+    const int l = (rl & 15) + ((f & 3) << 4);
+    As[((f >> 2) * 64 + l) * R + (rl >> 4)] = f < d ? X[(size_t)r * ldx + f] : 0.0f;
+  }
+  // the rows' thresholds: given (hint pre-pass), or hj = -2: the first sweep's
+  int need = 0;
+  for (int rl = threadIdx.x; rl < NR; rl += 256) {
+    const long long r = row0 + rl;
+    r_nx2[rl] = xn[r < n ? r : n - 1];
+    float t = INF;
+    int h = -1;
+    if (prune && r < n) {
+      if (ext_hj) {
+        t = ext_thr[r];
+        h = ext_hj[r];
+      } else {
+        h = -2;
+      }
+    }
+    r_thr[rl] = t;
+    r_hj[rl] = h;
+    need |= h == -2 ? 1 : 0;
+  }
+  const bool need_p1 = __syncthreads_or(need) != 0;
+  if (need_p1) {
+    // ---- pass 1: exact fp32 distance argmin (hint), with its inner product
+    float bd[R][4], bip[R][4], nxr[R][4];
+    int bjj[R][4];
+#pragma unroll
+    for (int g = 0; g < R; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bd[g][i] = INF;
+        bip[g][i] = 0.0f;
+        bjj[g][i] = 0x7fffffff;
+        nxr[g][i] = r_nx2[16 * g + 4 * q4 + i];
+      }
+    for (int t = wave; t < n_tiles; t += 4) {
+      f32x4 acc[R];
+      ipe_tile_ipR<D4, R>(As, Cf + (size_t)t * D4 * 64 + lane, lane, acc);
+      const int j = t * 16 + c16;
+      if (j < k) {
+        const float ny2 = cn[j];
+#pragma unroll
+        for (int g = 0; g < R; ++g)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float Dd = nxr[g][i] + ny2 - 2.0f * acc[g][i];
+            if (Dd < bd[g][i]) { bd[g][i] = Dd; bjj[g][i] = j; bip[g][i] = acc[g][i]; }
+          }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < R; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float b = bd[g][i], p = bip[g][i];
+        int jj = bjj[g][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float ob = __shfl_xor(b, o, 64), op = __shfl_xor(p, o, 64);
+          const int oj = __shfl_xor(jj, o, 64);
+          if (ob < b || (ob == b && oj < jj)) { b = ob; p = op; jj = oj; }
+        }
+        if (c16 == 0) {
+          const int rl = 16 * g + 4 * q4 + i;
+          mb[wave][rl] = b;
+          mj[wave][rl] = jj;
+          mip[wave][rl] = p;
+        }
+      }
+    __syncthreads();
+  }
+  // hazard budgets of this lane's streams (row 16 g + 4 q4 + i, class wave, c16)
+  u32x4 bud[R];
+  auto stream_of = [&](int rl, int w, int c) -> unsigned long long {
+    const long long g = row_offset + row0 + rl;
+    return (unsigned long long)g * 64ull + (unsigned long long)(w * 16 + c);
+  };
+#pragma unroll
+  for (int g = 0; g < R; ++g) {
+    bud[g] = u32x4{0u, 0u, 0u, 0u};
+    if (prune) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        WordStream ws(skip_key, stream_of(16 * g + 4 * q4 + i, wave, c16));
+        const uint32_t w0 = ws.next(), w1 = ws.next();
+        bud[g][i] = ipe_budget(w0, w1);
+      }
+    }
+  }
+  // this wave's running best of row `lane` (lanes < NR)
+  float bestv = INF;
+  int bestj = -1;
+  int qcnt = 0;   // wave-uniform list length
+  auto push = [&](bool p, uint32_t ent, float ip) {
+    const unsigned long long m = __ballot(p);
+    if (m != 0ull) {
+      if (p) {
+        const int pos = qcnt + (int)__builtin_amdgcn_mbcnt_hi(
+                                   (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        qe[wave][pos] = ent;
+        qip[wave][pos] = ip;
+      }
+      qcnt += __popcll(m);
+    }
+  };
+  // entry = j (14 bits) | owner lane << 14 | row << 20 | fired << 26.
+  // mode 0: this wave's list, results to the row owners; 1: the hint pairs
+  // (results are the rows' thresholds); 2: the 4 lists pooled, their 64-entry
+  // batches dealt round-robin to the 4 waves.
+  auto drain = [&](int mode) {
+    const int tot = mode == 2 ? qc[0] + qc[1] + qc[2] + qc[3] : qcnt;
+    const int bstep = mode == 2 ? 256 : 64;
+    for (int b0 = mode == 2 ? 64 * wave : 0; b0 < tot; b0 += bstep) {
+      int e = b0 + lane;
+      if (e < tot) {
+        int w = wave;
+        if (mode == 2) {
+          w = 0;
+          while (e >= qc[w]) e -= qc[w++];
+        }
+        const uint32_t ent = qe[w][e];
+        const float ip = qip[w][e];
+        const int j = (int)(ent & 0x3fffu), ol = (int)((ent >> 14) & 63u);
+        const int rl = (int)((ent >> 20) & 63u);
+        const bool fired = (ent >> 26) & 1u;
+        const long long g = row_offset + row0 + rl;
+        const float nxi = r_nx2[rl];
+        float dt;
+        if (!fired) {
+          if (STATS) ++st_full;
+          dt = ipe_distance(ip, (double)nxi, (double)cn[j], eps, Q, key,
+                            (unsigned long long)g * (unsigned long long)k + (unsigned long long)j);
+        } else {
+          uint32_t hq = 0;
+          float pbar = 1.0f;
+          ipe_hazard(ip, nxi, cn[j], r_sthr[rl], sc, hq, pbar);
+          WordStream ws(skip_key, stream_of(rl, w, ol & 15));
+          ws.b = (uint32_t)(2 * (j >> 6) + 1);   // step (t - class) / 4 = j / 64
+          const uint32_t w0 = ws.next(), w1 = ws.next(), w2 = ws.next(), w3 = ws.next();
+          nbud[rl & 3][w * 64 + ol] = ipe_budget(w0, w1);
+          const double beff = -expm1(-(double)hq * (1.0 / 4294967296.0));
+          const double u = u53(w2, w3) * beff;
+          const int h = (Q + 1) / 2;
+          const double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
+          dt = INF;
+          if (u < pib) {
+            if (STATS) ++st_exact;
+            dt = ipe_pruned_exact((double)ip, (double)nxi + (double)cn[j], eps, Q, r_thr[rl], u, ws);
+          }
+        }
+        if (mode == 1) {
+          r_thr[rl] = dt;
+          r_hj[rl] = j;
+        } else {
+          re[wave][lane] = ent;
+          rdt[wave][lane] = dt;
+        }
+      }
+      if (mode != 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int m = tot - b0 < 64 ? tot - b0 : 64;
+        for (int x = 0; x < m; ++x) {
+          const uint32_t ent = re[wave][x];
+          const float dt = rdt[wave][x];
+          if (lane == (int)((ent >> 20) & 63u)) {
+            const int j = (int)(ent & 0x3fffu);
+            bool take = dt < bestv;
+            if (!take && dt == bestv && dt < INF) {   // tie: the random keys decide (rare)
+              const long long g = row_offset + row0 + lane;
+              const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
+              const uint32_t bk = band_key(tie_key, g, (uint32_t)bestj);
+              take = tk < bk || (tk == bk && j < bestj);
+            }
+            if (take) {
+              bestv = dt;
+              bestj = j;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    qcnt = 0;
+  };
+  // unit -1: the hint pairs of the rows without a threshold (wave 0, lane
+  // = row); units 0 .. nun-1: (tile step, row group) of this wave; unit nun:
+  // the pooled drain (every wave: qcnt = the pooled length)
+  const int ntl = wave < n_tiles ? (n_tiles - wave + 3) / 4 : 0;
+  const int nun = ntl * R;
+  f32x4 accs[R];
+  for (int u = -1; u <= nun; ++u) {
+    bool any_fired = false;
+    int g = 0;
+    uint32_t fmask = 0;
+    int mode = 0;
+    if (u < 0) {
+      mode = 1;
+      if (need_p1 && wave == 0) {
+        const int rl = lane;
+        bool p = false;
+        uint32_t ent = 0;
+        float ip = 0.0f;
+        if (lane < NR && r_hj[rl] == -2) {
+          float b = mb[0][rl];
+          ip = mip[0][rl];
+          int jj = mj[0][rl];
+          for (int w = 1; w < 4; ++w)
+            if (mb[w][rl] < b || (mb[w][rl] == b && mj[w][rl] < jj)) {
+              b = mb[w][rl]; ip = mip[w][rl]; jj = mj[w][rl];
+            }
+          p = jj >= 0 && jj < k;
+          if (!p) r_hj[rl] = -1;
+          ent = (uint32_t)jj | ((uint32_t)rl << 20);
+        }
+        push(p, ent, ip);
+      }
+    } else if (u == nun) {
+      mode = 2;
+      qc[wave] = qcnt;
+      __syncthreads();
+      qcnt = qc[0] + qc[1] + qc[2] + qc[3];
+    } else {
+      const int stp = R == 2 ? u >> 1 : u;
+      g = u - stp * R;
+      const int t = wave + 4 * stp;
+      if (g == 0) ipe_tile_ipR<D4, R>(As, Cf + (size_t)t * D4 * 64 + lane, lane, accs);
+      f32x4 acc = accs[0];
+      u32x4 bd = bud[0];
+      if constexpr (R == 2) {
+        if (g) {
+          acc = accs[1];
+          bd = bud[1];
+        }
+      }
+      const int j = t * 16 + c16;
+      const bool jv = j < k;   // padded centroid columns do nothing
+      const float ny2 = jv ? cn[j] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = 16 * g + 4 * q4 + i;
+        bool p = false, fired = false;
+        if (jv && row0 + rl < n && j != r_hj[rl]) {
+          p = true;
+          if (prune) {
+            uint32_t hq;
+            float pbar;
+            if (ipe_hazard(acc[i], r_nx2[rl], ny2, r_sthr[rl], sc, hq, pbar)) {
+              if (hq > bd[i]) {   // the stream's budget runs out here: the pair fired
+                fired = true;
+                if (STATS) ++st_fire;
+              } else {
+                bd[i] -= hq;
+                p = false;
+                if (STATS) ++st_scr;
+              }
+            }
+          }
+        }
+        fmask |= fired ? 1u << i : 0u;
+        push(p, (uint32_t)j | ((uint32_t)lane << 14) | ((uint32_t)rl << 20) | (fired ? 1u << 26 : 0u),
+             acc[i]);
+      }
+      bud[0] = g == 0 ? bd : bud[0];
+      if constexpr (R == 2) bud[1] = g ? bd : bud[1];
+      any_fired = __ballot(fmask != 0u) != 0ull;
+    }
+    // drain: the hint pairs, after a fire (the stream's next budget is drawn
+    // before its next pair, one tile step later), when the next unit could
+    // overflow the list, the pooled rest
+    if (qcnt > 0 && (u < 0 || u == nun || qcnt > CAP - 256 || any_fired)) {
+      drain(mode);
+      if (fmask) {
+        u32x4 bd = bud[0];
+        if constexpr (R == 2) bd = g ? bud[1] : bud[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (fmask & (1u << i)) bd[i] = nbud[i][threadIdx.x];
+        bud[0] = g == 0 ? bd : bud[0];
+        if constexpr (R == 2) bud[1] = g ? bd : bud[1];
+      }
+    }
+    if (u < 0) {
+      __syncthreads();
+      for (int rl = threadIdx.x; rl < NR; rl += 256) r_sthr[rl] = ipe_sthr(r_thr[rl]);
+      __syncthreads();
+      if (lane < NR) {
+        bestv = r_hj[lane] >= 0 ? r_thr[lane] : INF;
+        bestj = r_hj[lane] >= 0 ? r_hj[lane] : -1;
+      }
+    }
+  }
+  // merge the 4 waves (the order (D~, tie key, j) is total)
+  if (lane < NR) {
+    const long long g = row_offset + row0 + lane;
+    mb[wave][lane] = bestv;
+    mk[wave][lane] = bestj >= 0 ? band_key(tie_key, g, (uint32_t)bestj) : 0xFFFFFFFFu;
+    mj[wave][lane] = bestj >= 0 ? bestj : 0x7fffffff;
+  }
+  __syncthreads();
+  if (threadIdx.x < NR) {
+    const int rr = threadIdx.x;
+    float b = mb[0][rr];
+    uint32_t kk = mk[0][rr];
+    int jj = mj[0][rr];
+    for (int w = 1; w < 4; ++w)
+      if (ipe_better(mb[w][rr], mk[w][rr], mj[w][rr], b, kk, jj)) {
+        b = mb[w][rr];
+        kk = mk[w][rr];
+        jj = mj[w][rr];
+      }
+    const long long r = row0 + rr;
+    if (r < n) {
+      labels[r] = jj < k ? jj : 0;
+      mind[r] = b;
+    }
+  }
+  if (STATS) {
+    const uint32_t v[4] = {st_scr, st_full, st_fire, st_exact};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t s = v[c];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o, 64);
+      if (lane == c) atomicAdd(stats + c, (unsigned long long)s);
+    }
+    if (threadIdx.x == 4 && need_p1) atomicAdd(stats + 4, 1ull);
+  }
+}
+
 }  // namespace sq
 
 using namespace sq;
@@ -912,7 +1408,7 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
                             int Q, unsigned k0, unsigned k1, unsigned s0, unsigned s1, unsigned t0,
                             unsigned t1, unsigned ts0, unsigned ts1, unsigned q0, unsigned q1,
                             unsigned qs0, unsigned qs1, long long row_offset, int prune,
-                            void* stats, void* stream) {
+                            void* stats, void* scratch, void* stream) {
   if (n <= 0) return 0;
   if (Q < 1 || Q > kIpeMaxQ || k < 1 || k_pad % 16 != 0 || k_pad < k || k_pad > 16384 || d < 1 ||
       d > d_pad || ldx < d || !(eps > 0.0) || (hint_labels && !C))
@@ -928,23 +1424,59 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
   sc.cqh = (float)cq * (1.0f + 1e-6f);
   sc.kq = (float)(1.0 / (1.4142135623730951 * eps)) * (1.0f - 1e-6f);
   sc.inv_eps = (float)(1.0 / eps) * (1.0f + 1e-6f);
-  const long long blocks = (n + 15) / 16;
   const int nt = k_pad / 16;
-  const int pr = (prune && (Q & 1)) ? 1 : 0;
-  const dim3 grid((unsigned)blocks);
+  const int pr = (prune & 1) && (Q & 1) ? 1 : 0;
+  // layout (prune bits 1-2): 0 auto, 1 / 2 row groups, 3 the per-lane-queue kernel
+  const int layout = (prune >> 1) & 3;
   hipStream_t hs = (hipStream_t)stream;
+  unsigned long long* stp = (unsigned long long*)stats;
+  // row-group layouts: label hints become thresholds in a pre-pass
+  // (scratch: float thr[n] then int hj[n])
+  float* ext_thr = nullptr;
+  int* ext_hj = nullptr;
+  if (layout != 3 && pr && hint_labels) {
+    if (!scratch) return (int)hipErrorInvalidValue;
+    ext_thr = (float*)scratch;
+    ext_hj = (int*)((float*)scratch + n);
+    const dim3 hg((unsigned)((n + 255) / 256));
+    if (stats)
+      ipe_hint_kernel<true><<<hg, 256, 0, hs>>>(
+          (const float*)X, ldx, (const float*)C, (const int*)hint_labels, (const float*)xn,
+          (const float*)cn, ext_thr, ext_hj, n, d, k, eps, Q, key, row_offset, stp);
+    else
+      ipe_hint_kernel<false><<<hg, 256, 0, hs>>>(
+          (const float*)X, ldx, (const float*)C, (const int*)hint_labels, (const float*)xn,
+          (const float*)cn, ext_thr, ext_hj, n, d, k, eps, Q, key, row_offset, nullptr);
+  }
+#define ARGS                                                                                    \
+  (const float*)X, ldx, (const float*)Cf, (const float*)C, (const int*)hint_labels,             \
+      (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, nt, eps, Q, key, \
+      tie, skip, sc, row_offset, pr
+#define RARGS                                                                                   \
+  (const float*)X, ldx, (const float*)Cf, ext_thr, ext_hj, (const float*)xn, (const float*)cn,  \
+      (int*)labels, (float*)mind, n, d, k, nt, eps, Q, key, tie, skip, sc, row_offset, pr
+#define OLD(DP)                                                                                 \
+  {                                                                                             \
+    const dim3 grid((unsigned)((n + 15) / 16));                                                 \
+    if (stats)                                                                                  \
+      ipe_fused_kernel<DP / 4, true><<<grid, 256, (size_t)DP * 64, hs>>>(ARGS, stp);            \
+    else                                                                                        \
+      ipe_fused_kernel<DP / 4, false><<<grid, 256, (size_t)DP * 64, hs>>>(ARGS, nullptr);       \
+  }
+#define RG(DP, RR)                                                                              \
+  {                                                                                             \
+    const dim3 grid((unsigned)((n + 16 * RR - 1) / (16 * RR)));                                 \
+    const size_t shm = (size_t)DP * 64 * RR;                                                    \
+    if (stats)                                                                                  \
+      ipe_fused_rg_kernel<DP / 4, RR, true><<<grid, 256, shm, hs>>>(RARGS, stp);                \
+    else                                                                                        \
+      ipe_fused_rg_kernel<DP / 4, RR, false><<<grid, 256, shm, hs>>>(RARGS, nullptr);           \
+  }
 #define CASE(DP)                                                                                \
   case DP:                                                                                      \
-    if (stats)                                                                                  \
-      ipe_fused_kernel<DP / 4, true><<<grid, 256, (size_t)DP * 64, hs>>>(                       \
-          (const float*)X, ldx, (const float*)Cf, (const float*)C, (const int*)hint_labels,     \
-          (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, nt, eps, Q,  \
-          key, tie, skip, sc, row_offset, pr, (unsigned long long*)stats);                      \
-    else                                                                                        \
-      ipe_fused_kernel<DP / 4, false><<<grid, 256, (size_t)DP * 64, hs>>>(                      \
-          (const float*)X, ldx, (const float*)Cf, (const float*)C, (const int*)hint_labels,     \
-          (const float*)xn, (const float*)cn, (int*)labels, (float*)mind, n, d, k, nt, eps, Q,  \
-          key, tie, skip, sc, row_offset, pr, nullptr);                                         \
+    if (layout == 3) OLD(DP)                                                                    \
+    else if (layout == 1 || DP > 256) RG(DP, 1)                                                 \
+    else RG(DP, 2)                                                                              \
     break;
   switch (d_pad) {
     CASE(32)
@@ -957,5 +1489,9 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
       return (int)hipErrorInvalidValue;
   }
 #undef CASE
+#undef RG
+#undef OLD
+#undef ARGS
+#undef RARGS
   return (int)hipGetLastError();
 }

@@ -45,7 +45,7 @@ __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, cons
                                        long long, int, int, int, int, double, int, unsigned,
                                        unsigned, unsigned, unsigned, unsigned, unsigned, unsigned,
                                        unsigned, unsigned, unsigned, unsigned, unsigned, long long,
-                                       int, void*, void*);
+                                       int, void*, void*, void*);
 __attribute__((weak)) int sq_centroid_delta(const void*, const void*, const void*, void*, void*,
                                             void*, long long, int, int, int, int, void*, void*,
                                             void*, void*);
@@ -312,17 +312,17 @@ static PyObject* py_xw(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
-  unsigned long long X, Cf, C, hint, xn, cn, lab, mind, stats, st; long long ldx, n, roff;
+  unsigned long long X, Cf, C, hint, xn, cn, lab, mind, stats, scr, st; long long ldx, n, roff;
   int d, dp, k, kp, Q;
   double eps; unsigned k0, k1, s0, s1, t0, t1, ts0, ts1, q0, q1, qs0, qs1; int prune;
-  if (!PyArg_ParseTuple(a, "KLKKKKKKKLiiiidiIIIIIIIIIIIILiKK", &X, &ldx, &Cf, &C, &hint, &xn, &cn,
+  if (!PyArg_ParseTuple(a, "KLKKKKKKKLiiiidiIIIIIIIIIIIILiKKK", &X, &ldx, &Cf, &C, &hint, &xn, &cn,
                         &lab, &mind, &n, &d, &dp, &k, &kp, &eps, &Q, &k0, &k1, &s0, &s1, &t0,
-                        &t1, &ts0, &ts1, &q0, &q1, &qs0, &qs1, &roff, &prune, &stats, &st))
+                        &t1, &ts0, &ts1, &q0, &q1, &qs0, &qs1, &roff, &prune, &stats, &scr, &st))
     return nullptr;
   CHECK(sq_ipe_fused)
   return ret(sq_ipe_fused(P(X), ldx, P(Cf), P(C), P(hint), P(xn), P(cn), P(lab), P(mind), n, d,
                           dp, k, kp, eps, Q, k0, k1, s0, s1, t0, t1, ts0, ts1, q0, q1, qs0, qs1,
-                          roff, prune, P(stats), P(st)));
+                          roff, prune, P(stats), P(scr), P(st)));
 }
 
 static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {

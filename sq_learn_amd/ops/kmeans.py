@@ -258,7 +258,7 @@ def ipe_center_fragments(C, k_pad, d_pad):
 
 def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie_key: RngKey,
                      row_offset, labels, mind, prune=True, C=None, hint_labels=None,
-                     skip_key: RngKey = None, stats=None):
+                     skip_key: RngKey = None, stats=None, layout=0):
     """Fused IPE E-step (csrc/ipe.hip): exact fp32 MFMA inner products, the
     median-of-Q amplitude-estimation distance per pair in the epilogue,
     per-row argmin with random ties; G is never materialised.  ``prune``
@@ -271,7 +271,9 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
     whose budget runs out (thinned to the exact law) or that are competitive
     pay a sampler - same law as prune=False.  ``stats`` (int64[5], optional,
     accumulated): screened pairs, full-sampler pairs, fires, fires reaching
-    the exact branch, workgroups that ran the first sweep."""
+    the exact branch, workgroups that ran the first sweep.  ``layout``
+    (tests): 0 auto, 1 / 2 row groups per workgroup, 3 the per-lane-queue
+    kernel - all return the same labels bit for bit."""
     n, d = X.shape
     assert X.dtype == torch.float32 and X.stride(1) == 1
     assert xn.dtype == torch.float32 and cn.dtype == torch.float32 and xn.numel() >= n
@@ -284,6 +286,10 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
         assert stats.dtype == torch.int64 and stats.numel() >= 5 and stats.is_contiguous()
     if skip_key is None:
         skip_key = key.derive(purpose="ipe_skip")
+    # the row-group layouts turn label hints into thresholds in a pre-pass
+    scratch = None
+    if hint_labels is not None and prune and int(Q) % 2 == 1 and layout != 3:
+        scratch = torch.empty(2 * max(n, 1), dtype=torch.int32, device=X.device)
     rc = nat.native().ipe_fused(X.data_ptr(), X.stride(0), Cfrag.data_ptr(),
                                 0 if C is None else C.data_ptr(),
                                 0 if hint_labels is None else hint_labels.data_ptr(),
@@ -291,8 +297,9 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
                                 d, d_pad, k, k_pad, float(eps), int(Q), key.k0, key.k1, key.s0,
                                 key.s1, tie_key.k0, tie_key.k1, tie_key.s0, tie_key.s1,
                                 skip_key.k0, skip_key.k1, skip_key.s0, skip_key.s1,
-                                int(row_offset), int(bool(prune)),
+                                int(row_offset), int(bool(prune)) | (int(layout) & 3) << 1,
                                 0 if stats is None else stats.data_ptr(),
+                                0 if scratch is None else scratch.data_ptr(),
                                 nat.stream_handle(X.device))
     if rc:
         raise RuntimeError(f"ipe_fused failed (hip error {rc})")

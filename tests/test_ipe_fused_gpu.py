@@ -428,3 +428,43 @@ def test_ipe_pruned_rows_invariant_to_grouping(cuda, with_hint):
     torch.cuda.synchronize()
     assert np.array_equal(outs[0][0][7:], outs[1][0])
     assert np.array_equal(outs[0][1][7:], outs[1][1])
+
+
+@pytest.mark.parametrize("dp,with_hint,prune", [(64, False, True), (64, True, True),
+                                                (256, True, True), (512, False, True),
+                                                (64, False, False)])
+def test_ipe_layouts_bit_identical(cuda, dp, with_hint, prune):
+    """The row-group kernel (1 or 2 groups of 16 rows per workgroup, wave-wide
+    drain lists) and the per-lane-queue kernel share every stream, threshold
+    and sampler: labels, estimates and the screen's counters are identical."""
+    rng = np.random.default_rng(41 + dp)
+    n, d, k, eps, Q = 5003, dp - 5, 200, 0.25, 13
+    ctr = rng.standard_normal((20, d)) * 3
+    X = (ctr[rng.integers(0, 20, n)] + rng.standard_normal((n, d))).astype(np.float32)
+    Cn = (ctr[rng.integers(0, 20, k)] + 0.5 * rng.standard_normal((k, d))).astype(np.float32)
+    Xt = torch.tensor(X, device=cuda)
+    Ct = torch.tensor(Cn, device=cuda)
+    xn = (Xt * Xt).sum(1)
+    cn = (Ct * Ct).sum(1)
+    kp = 208
+    frag = K.ipe_center_fragments(Ct, kp, dp)
+    hint = None
+    if with_hint:   # mostly good hints, some invalid (-> the exact first sweep)
+        hint = torch.tensor(np.where(rng.random(n) < 0.01, -1, rng.integers(0, k, n)).astype(np.int32),
+                            device=cuda)
+    outs = []
+    for layout in (3, 1, 2):
+        lab = torch.empty(n, dtype=torch.int32, device=cuda)
+        mind = torch.empty(n, dtype=torch.float32, device=cuda)
+        st = torch.zeros(5, dtype=torch.int64, device=cuda)
+        K.ipe_fused_native(Xt, frag, xn, cn, k, kp, dp, eps, Q, RngKey(5, "ipe", 2),
+                           RngKey(5, "band_select", 2), 11, lab, mind, prune=prune,
+                           C=Ct if with_hint else None, hint_labels=hint, stats=st, layout=layout)
+        outs.append((lab.cpu().numpy(), mind.cpu().numpy(), st.cpu().numpy()))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0])
+        assert np.array_equal(outs[0][1], o[1])
+        assert np.array_equal(outs[0][2][:4], o[2][:4])
+    if prune:
+        assert outs[0][2][0] > 0

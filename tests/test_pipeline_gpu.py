@@ -3,7 +3,9 @@ E-step is enqueued right after the M-step, before the host reads the
 iteration's scalars.  Same kernels, same Philox keys, same stream order - so
 per-iteration scalars, returned labels and the final centroids must be
 BIT-identical to the unpipelined loop, and a loop that stops (dropping the
-speculative E-step) must leave a final E-step identical too.  QMeans.fit
+speculative E-step) must leave a final E-step identical too.  (Scalar 3, the
+Hamerly filter's kept count, is a scheduling diagnostic: the adaptive filter
+decides on the host's view of it, which lags by one step when pipelined.)  QMeans.fit
 runs pipelined without checkpoints: its result must equal a fit whose loop
 is forced unpipelined."""
 import numpy as np
@@ -42,7 +44,8 @@ def test_pipelined_steps_bit_identical(cuda, delta, d):
                             device=cuda)]
     a = _run(Xt, C0, k, delta, False, 9)
     b = _run(Xt, C0, k, delta, True, 9)
-    assert a[0] == b[0]                                   # inertia / shift / overflow per step
+    # inertia / shift / overflow per step
+    assert [s[:3] for s in a[0]] == [s[:3] for s in b[0]]
     for la, lb in zip(a[1], b[1]):
         assert torch.equal(la, lb)
     assert torch.equal(a[2], b[2])                        # centroids
