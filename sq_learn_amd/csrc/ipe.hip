@@ -432,7 +432,7 @@ struct IpeScreen {
   float kq;       // 1 / (sqrt(2) eps), rounded down
   float inv_eps;  // 1 / eps, rounded up
   float cqh;      // C(Q, h), rounded up
-  int h;
+  float hf;       // h = (Q + 1) / 2
 };
 
 // upper bound on sqrt(x (1 + 2^-23)) (the class-value rounding of thr)
@@ -450,10 +450,12 @@ SQ_DEV float ipe_sthr(float x) { return __builtin_amdgcn_sqrtf(x) * 1.000001f; }
 SQ_DEV bool ipe_hazard(float ip, float nx2, float ny2, float sthr, const IpeScreen& sc,
                        uint32_t& hq, float& pbar) {
 #pragma clang fp contract(off)   // the drain recomputes hq bit for bit
+  // straight-line (every lane evaluates everything; the conditions are
+  // combined at the end): no divergent exits in the tile epilogue
   const float S = nx2 + ny2;
   const float D = fmaf(-2.0f, ip, S);
-  if (!(D >= S * 2.44140625e-4f && D <= S * 1.998046875f)) return false;
-  const float sD = __builtin_amdgcn_sqrtf(D) * (1.0f - 4.8828125e-4f);
+  const bool c1 = (D >= S * 2.44140625e-4f) & (D <= S * 1.998046875f);
+  const float sD = __builtin_amdgcn_sqrtf(fmaxf(D, 0.0f)) * (1.0f - 4.8828125e-4f);
   const float ra = __builtin_amdgcn_rcpf(fmaxf(1.0f, fabsf(ip)));
   const float P = __builtin_amdgcn_sqrtf(S) * ra * sc.kq;
   const float m = (sD - sthr) * P * (1.0f - 3e-6f);
@@ -461,21 +463,21 @@ SQ_DEV bool ipe_hazard(float ip, float nx2, float ny2, float sthr, const IpeScre
   const float tcap = fmaf(1.571f * sthr, P, 2.2f);
   // M below its 2^40 cap
   const float Mq = S * ra * sc.inv_eps;
-  if (!(m >= 3.0f && tcap <= 1048576.0f && Mq < 6.0e10f)) return false;
-  const float rm = __builtin_amdgcn_rcpf(m) * 1.000001f;
-  pbar = fminf(0.5f * rm * (1.0f + rm) * 1.00002f, 1.0f);
-  // C(Q, h) pbar^h by binary powering (h <= 8: at most 6 roundings)
-  const float p2 = pbar * pbar, p4 = p2 * p2;
-  float pw = (sc.h & 1) ? pbar : 1.0f;
-  if (sc.h & 2) pw *= p2;
-  if (sc.h & 4) pw *= p4;
-  if (sc.h & 8) pw *= p4 * p4;
-  const float pu = sc.cqh * pw * 1.00001f;
+  const bool c2 = (m >= 3.0f) & (tcap <= 1048576.0f) & (Mq < 6.0e10f);
+  const float rm = __builtin_amdgcn_rcpf(fmaxf(m, 3.0f)) * 1.000001f;
+  const float pb = fminf(0.5f * rm * (1.0f + rm) * 1.00002f, 1.0f);
+  // C(Q, h) pbar^h = C(Q, h) 2^(h log2 pbar): v_log / v_exp (1 ulp each;
+  // |h log2 pbar| < 2^8 puts the exponent's error below 2^-14 relative to
+  // pw... covered 30x by the 2e-4 margin); an underflow to 0 still gives
+  // hq = 1 >= 2^32 pibar
+  const float pw = __builtin_amdgcn_exp2f(sc.hf * __builtin_amdgcn_logf(pb));
+  const float pu = sc.cqh * pw * 1.0002f;
   // -log(1 - pu) <= pu (1 + pu) <= pu (1 + 2^-10): 2^32 H < 2^22.01, so 256
   // pairs of one stream never exhaust a capped (2^31) budget
-  if (!(pu < 9.765625e-4f)) return false;
-  hq = (uint32_t)(pu * 1.001f * 4294967296.0f) + 1u;
-  return true;
+  const bool c3 = pu < 9.765625e-4f;
+  hq = (uint32_t)(fminf(pu, 9.765625e-4f) * 1.001f * 4294967296.0f) + 1u;
+  pbar = pb;
+  return c1 & c2 & c3;
 }
 
 // 53-bit uniform in (0, 1) from two words
@@ -964,6 +966,41 @@ SQ_DEV void ipe_tile_ipR(const float* __restrict__ As, const float* __restrict__
   }
 }
 
+// The samplers of one list entry (row-group kernel drains), out of line:
+// the tile loop's register allocation does not carry the samplers' fp64
+// state and their parameters (read from LDS here).
+struct IpeDrainArgs {
+  RngKey key, skip;
+  double eps;
+  int Q;
+  IpeScreen sc;
+};
+
+__device__ __attribute__((noinline)) float ipe_entry_sample(
+    float ip, float nxi, float cnj, float sthr, float thr, int j, int fired,
+    unsigned long long sid, unsigned long long stream, const IpeDrainArgs* __restrict__ da,
+    uint32_t* nb, int* exact) {
+  const int Q = da->Q;
+  const double eps = da->eps;
+  if (!fired) return ipe_distance(ip, (double)nxi, (double)cnj, eps, Q, da->key, sid);
+  // the same hazard as at the screen (same inputs, same code)
+  uint32_t hq = 0;
+  float pbar = 1.0f;
+  const IpeScreen sc = da->sc;
+  ipe_hazard(ip, nxi, cnj, sthr, sc, hq, pbar);
+  WordStream ws(da->skip, stream);
+  ws.b = (uint32_t)(2 * (j >> 6) + 1);   // step (t - class) / 4 = j / 64
+  const uint32_t w0 = ws.next(), w1 = ws.next(), w2 = ws.next(), w3 = ws.next();
+  *nb = ipe_budget(w0, w1);   // the stream's next budget
+  const double beff = -expm1(-(double)hq * (1.0 / 4294967296.0));
+  const double u = u53(w2, w3) * beff;
+  const int h = (Q + 1) / 2;
+  const double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
+  if (!(u < pib)) return __builtin_inff();
+  *exact = 1;
+  return ipe_pruned_exact((double)ip, (double)nxi + (double)cnj, eps, Q, thr, u, ws);
+}
+
 // Row thresholds from label hints, one lane per row (the pre-pass of the
 // row-group kernel): the hint pair's inner product by 16 lanes (the fp32
 // summation order of ipe_fused_kernel's hint path), then every lane samples
@@ -1055,12 +1092,26 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
   __shared__ uint32_t mk[4][NR];
   __shared__ int mj[4][NR];
   __shared__ int qc[4];
+  // per row: (|x|^2, sthr, hint centroid bits, row < n) - one LDS read per pair
+  __shared__ float4 rinfo[NR];
+  // the samplers' parameters, read by the drains from LDS (keeps them out of
+  // the tile loop's scalar registers)
+  __shared__ RngKey s_tie;
+  __shared__ IpeDrainArgs s_da;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
   const long long row0 = (long long)blockIdx.x * NR;
   const float INF = __builtin_inff();
   uint32_t st_scr = 0, st_full = 0, st_fire = 0, st_exact = 0;
+  if (threadIdx.x == 0) {
+    s_tie = tie_key;
+    s_da.key = key;
+    s_da.skip = skip_key;
+    s_da.eps = eps;
+    s_da.Q = Q;
+    s_da.sc = sc;
+  }
   // A fragments, row-major reads (coalesced): row rl, feature f ->
   // As[((f / 4) 64 + (rl mod 16) + 16 (f mod 4)) R + rl / 16]; rows past n clamped
   for (int e = threadIdx.x; e < NR * D4 * 4; e += 256) {
@@ -1193,29 +1244,16 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
         const int rl = (int)((ent >> 20) & 63u);
         const bool fired = (ent >> 26) & 1u;
         const long long g = row_offset + row0 + rl;
-        const float nxi = r_nx2[rl];
-        float dt;
-        if (!fired) {
-          if (STATS) ++st_full;
-          dt = ipe_distance(ip, (double)nxi, (double)cn[j], eps, Q, key,
-                            (unsigned long long)g * (unsigned long long)k + (unsigned long long)j);
-        } else {
-          uint32_t hq = 0;
-          float pbar = 1.0f;
-          ipe_hazard(ip, nxi, cn[j], r_sthr[rl], sc, hq, pbar);
-          WordStream ws(skip_key, stream_of(rl, w, ol & 15));
-          ws.b = (uint32_t)(2 * (j >> 6) + 1);   // step (t - class) / 4 = j / 64
-          const uint32_t w0 = ws.next(), w1 = ws.next(), w2 = ws.next(), w3 = ws.next();
-          nbud[rl & 3][w * 64 + ol] = ipe_budget(w0, w1);
-          const double beff = -expm1(-(double)hq * (1.0 / 4294967296.0));
-          const double u = u53(w2, w3) * beff;
-          const int h = (Q + 1) / 2;
-          const double pib = binom_upper_tail((double)pbar, Q, h) * (1.0 + 1e-12);
-          dt = INF;
-          if (u < pib) {
-            if (STATS) ++st_exact;
-            dt = ipe_pruned_exact((double)ip, (double)nxi + (double)cn[j], eps, Q, r_thr[rl], u, ws);
-          }
+        uint32_t nb = 0;
+        int ex = 0;
+        const float dt = ipe_entry_sample(
+            ip, r_nx2[rl], cn[j], r_sthr[rl], r_thr[rl], j, fired ? 1 : 0,
+            (unsigned long long)g * (unsigned long long)k + (unsigned long long)j,
+            stream_of(rl, w, ol & 15), &s_da, &nb, &ex);
+        if (fired) nbud[rl & 3][w * 64 + ol] = nb;
+        if (STATS) {
+          st_full += fired ? 0u : 1u;
+          st_exact += (uint32_t)ex;
         }
         if (mode == 1) {
           r_thr[rl] = dt;
@@ -1238,8 +1276,9 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
             bool take = dt < bestv;
             if (!take && dt == bestv && dt < INF) {   // tie: the random keys decide (rare)
               const long long g = row_offset + row0 + lane;
-              const uint32_t tk = band_key(tie_key, g, (uint32_t)j);
-              const uint32_t bk = band_key(tie_key, g, (uint32_t)bestj);
+              const RngKey tk_ = s_tie;
+              const uint32_t tk = band_key(tk_, g, (uint32_t)j);
+              const uint32_t bk = band_key(tk_, g, (uint32_t)bestj);
               take = tk < bk || (tk == bk && j < bestj);
             }
             if (take) {
@@ -1305,31 +1344,44 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
       }
       const int j = t * 16 + c16;
       const bool jv = j < k;   // padded centroid columns do nothing
-      const float ny2 = jv ? cn[j] : 0.0f;
+      const float ny2 = cn[jv ? j : 0];
+      // straight-line screen of the 4 pairs; one ballot decides whether any
+      // lane appends (full-sampler pairs and fired pairs are rare)
+      bool pp[4];
+      if (prune) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rl = 16 * g + 4 * q4 + i;
-        bool p = false, fired = false;
-        if (jv && row0 + rl < n && j != r_hj[rl]) {
-          p = true;
-          if (prune) {
-            uint32_t hq;
-            float pbar;
-            if (ipe_hazard(acc[i], r_nx2[rl], ny2, r_sthr[rl], sc, hq, pbar)) {
-              if (hq > bd[i]) {   // the stream's budget runs out here: the pair fired
-                fired = true;
-                if (STATS) ++st_fire;
-              } else {
-                bd[i] -= hq;
-                p = false;
-                if (STATS) ++st_scr;
-              }
-            }
+        for (int i = 0; i < 4; ++i) {
+          const float4 ri = rinfo[16 * g + 4 * q4 + i];
+          const bool valid = jv & (ri.w != 0.0f) & (j != __float_as_int(ri.z));
+          uint32_t hq;
+          float pbar;
+          const bool ok = ipe_hazard(acc[i], ri.x, ny2, ri.y, sc, hq, pbar) & valid;
+          const bool fired = ok & (hq > bd[i]);   // the stream's budget runs out here
+          const bool scr = ok & !fired;
+          bd[i] = scr ? bd[i] - hq : bd[i];
+          pp[i] = valid & !scr;
+          fmask |= fired ? 1u << i : 0u;
+          if (STATS) {
+            st_fire += fired ? 1u : 0u;
+            st_scr += scr ? 1u : 0u;
           }
         }
-        fmask |= fired ? 1u << i : 0u;
-        push(p, (uint32_t)j | ((uint32_t)lane << 14) | ((uint32_t)rl << 20) | (fired ? 1u << 26 : 0u),
-             acc[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 ri = rinfo[16 * g + 4 * q4 + i];
+          pp[i] = jv & (ri.w != 0.0f) & (j != __float_as_int(ri.z));
+        }
+      }
+      if (__ballot(pp[0] || pp[1] || pp[2] || pp[3]) != 0ull) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rl = 16 * g + 4 * q4 + i;
+          push(pp[i],
+               (uint32_t)j | ((uint32_t)lane << 14) | ((uint32_t)rl << 20) |
+                   ((fmask >> i) & 1u) << 26,
+               acc[i]);
+        }
       }
       bud[0] = g == 0 ? bd : bud[0];
       if constexpr (R == 2) bud[1] = g ? bd : bud[1];
@@ -1352,7 +1404,12 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
     }
     if (u < 0) {
       __syncthreads();
-      for (int rl = threadIdx.x; rl < NR; rl += 256) r_sthr[rl] = ipe_sthr(r_thr[rl]);
+      for (int rl = threadIdx.x; rl < NR; rl += 256) {
+        const float st = ipe_sthr(r_thr[rl]);
+        r_sthr[rl] = st;
+        rinfo[rl] = make_float4(r_nx2[rl], st, __int_as_float(r_hj[rl]),
+                                row0 + rl < n ? 1.0f : 0.0f);
+      }
       __syncthreads();
       if (lane < NR) {
         bestv = r_hj[lane] >= 0 ? r_thr[lane] : INF;
@@ -1364,7 +1421,7 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
   if (lane < NR) {
     const long long g = row_offset + row0 + lane;
     mb[wave][lane] = bestv;
-    mk[wave][lane] = bestj >= 0 ? band_key(tie_key, g, (uint32_t)bestj) : 0xFFFFFFFFu;
+    mk[wave][lane] = bestj >= 0 ? band_key(s_tie, g, (uint32_t)bestj) : 0xFFFFFFFFu;
     mj[wave][lane] = bestj >= 0 ? bestj : 0x7fffffff;
   }
   __syncthreads();
@@ -1420,7 +1477,7 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
   const int h = (Q + 1) / 2;
   double cq = 1.0;
   for (int i = 0; i < h; ++i) cq = cq * (double)(Q - i) / (double)(i + 1);
-  sc.h = h;
+  sc.hf = (float)h;
   sc.cqh = (float)cq * (1.0f + 1e-6f);
   sc.kq = (float)(1.0 / (1.4142135623730951 * eps)) * (1.0f - 1e-6f);
   sc.inv_eps = (float)(1.0 / eps) * (1.0f + 1e-6f);

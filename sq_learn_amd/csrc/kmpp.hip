@@ -12,9 +12,13 @@
 //     covered), so min(closest_i, D_ij) = closest_i without reading the row.
 //     Rows with a trial left go to the survivor list;
 //  2. certified int8 bound (kmpp_bound_kernel): survivors are read from an
-//     int8 copy (per-row scale s_i, stored error norm e_i >= |x_i - x~_i|):
-//     |x_i - c_j| >= |x~_i - c_j| - e_i with every fp32 rounding of
-//     |x~_i - c_j|^2 bounded; trials still undecided send the row on;
+//     int8 copy (per-row scale s_i, stored error norm e_i >= |x_i - x~_i|);
+//     the candidates are int8 too, as two terms (c~ = s_c (q1 + q2 / 254),
+//     error norm ec_j >= |c_j - c~_j|), so <q_i, q1_j> and <q_i, q2_j> are
+//     EXACT int32 MFMA dot products (v_mfma_i32_16x16x64_i8, 16 rows x 16
+//     trials per instruction) and |x_i - c_j| >= |x~_i - c~_j| - e_i - ec_j
+//     with |x~ - c~|^2 = s^2 |q|^2 + |c~|^2 - 2 s <q, c~> evaluated in fp64
+//     (rounding covered); trials still undecided send the row on;
 //  3. exact pass (kmpp_exact_kernel): the fp32 direct-form distances
 //     sum_f (x_f - c_f)^2 (no norm-expansion cancellation) of the remaining
 //     rows; a trial that improves a row (D_ij < closest_i) records D_ij and
@@ -36,17 +40,15 @@ namespace sq {
 
 constexpr int kKppTile = 32;          // fp32 features per staged tile (128 B of a row)
 constexpr int kKppStride = 36;        // LDS row stride in floats (16-B aligned, skewed banks)
-constexpr int kKqTile = 64;           // int8 features per staged tile (64 B of a row)
-constexpr int kKqStride = 17;         // LDS row stride in dwords (odd: conflict-free)
 
 SQ_DEV double kpp_q(float v, double wi, double scale) { return rint((double)v * wi * scale); }
 
 // ------------------------------------------------------------ int8 copy
-// u = rint(x / s) + 128 (s = max|x| / 127), e = |x - s (u - 128)| rounded up,
-// xq2 = |x~|^2 = s^2 |u - 128|^2
+// q = rint(x / s) (s = max|x| / 127), e = |x - s q| rounded up, q2 = |q|^2
+// (exact int); features d .. dq-1 are zero
 __global__ void __launch_bounds__(256) kmpp_quantize_kernel(
-    const float* __restrict__ X, long long ldx, int d, long long n, uint8_t* __restrict__ Xq,
-    int dq, float* __restrict__ srow, float* __restrict__ erow, float* __restrict__ xq2) {
+    const float* __restrict__ X, long long ldx, int d, long long n, int8_t* __restrict__ Xq,
+    int dq, float* __restrict__ srow, float* __restrict__ erow, int* __restrict__ q2row) {
   const int lane = threadIdx.x & 63;
   const long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
@@ -57,23 +59,25 @@ __global__ void __launch_bounds__(256) kmpp_quantize_kernel(
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     const float s = mx > 0.0f ? mx / 127.0f : 1.0f;
-    double e2 = 0.0, q2 = 0.0;
+    double e2 = 0.0;
+    int q2 = 0;
     for (int f = lane; f < dq; f += 64) {
-      float q = 0.0f;
+      int q = 0;
       if (f < d) {
-        q = fminf(fmaxf(rintf(x[f] / s), -127.0f), 127.0f);
+        q = (int)fminf(fmaxf(rintf(x[f] / s), -127.0f), 127.0f);
         const double r = (double)x[f] - (double)s * (double)q;
         e2 += r * r;
-        q2 += (double)q * (double)q;
+        q2 += q * q;
       }
-      Xq[i * dq + f] = (uint8_t)((int)q + 128);
+      Xq[i * dq + f] = (int8_t)q;
     }
     e2 = wave_sum(e2);
-    q2 = wave_sum(q2);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q2 += __shfl_xor(q2, o, 64);
     if (lane == 0) {
       srow[i] = s;
       erow[i] = (float)(sqrt(e2) * (1.0 + 1e-6)) * 1.000001f;
-      xq2[i] = (float)((double)s * (double)s * q2);
+      q2row[i] = q2;
     }
   }
 }
@@ -134,13 +138,13 @@ __global__ void __launch_bounds__(256) kmpp_block_totals_kernel(
 
 // ------------------------------------------- candidate-centre distances
 // grid (t, ceil(c / 64)): cc[j][m] = |cand_j - C_m|^2 (m < c), one wave per
-// centre; blocks (j, 0) also write cinfo[j] = (|c_j|^2, sum c_j, sum |c_j|)
-// and the zero-padded copy candq[j][dq]; the whole grid zeroes delta_part
-// and the list counters.
+// centre; blocks (j, 0) also write the two-term int8 candidate (candq[j] and
+// candq[16 + j], zero padded to dq) and cinfo[j]; the whole grid zeroes
+// delta_part and the list counters.
 __global__ void __launch_bounds__(256) kmpp_cc_kernel(
     const float* __restrict__ cand, const float* __restrict__ C, int c, int d, int t,
-    float* __restrict__ cc, int ldcc, float* __restrict__ cinfo, float* __restrict__ candq, int dq,
-    double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
+    float* __restrict__ cc, int ldcc, double* __restrict__ cinfo, int8_t* __restrict__ candq,
+    int dq, double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* cj = cand + (size_t)j * d;
@@ -161,29 +165,43 @@ __global__ void __launch_bounds__(256) kmpp_cc_kernel(
     if (lane == 0) cc[(size_t)j * ldcc + m] = acc;
   }
   if (blockIdx.y == 0) {
-    __shared__ float red[3][4];
-    float a = 0.f, s = 0.f, b = 0.f;
-    for (int f = threadIdx.x; f < dq; f += 256) {
-      const float v = f < d ? cj[f] : 0.0f;
-      candq[(size_t)j * dq + f] = v;
-      a = fmaf(v, v, a);
-      s += v;
-      b += fabsf(v);
-    }
+    // two-term int8 candidate: y = c / s_c, q1 = rint(y), q2 = rint(254 (y - q1)),
+    // c~ = s_c (q1 + q2 / 254); cinfo[j] = (s_c, ec >= |c - c~|, |c~|^2, 0) fp64
+    __shared__ float redf[4];
+    __shared__ double redd[2][4];
+    float mx = 0.0f;
+    for (int f = threadIdx.x; f < d; f += 256) mx = fmaxf(mx, fabsf(cj[f]));
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      a += __shfl_xor(a, o, 64);
-      s += __shfl_xor(s, o, 64);
-      b += __shfl_xor(b, o, 64);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    const double sc = mx > 0.0f ? (double)mx / 127.0 : 1.0;
+    double er = 0.0, c2 = 0.0;
+    for (int f = threadIdx.x; f < dq; f += 256) {
+      int q1 = 0, q2 = 0;
+      if (f < d) {
+        const double y = (double)cj[f] / sc;
+        q1 = (int)fmin(fmax(rint(y), -127.0), 127.0);
+        q2 = (int)fmin(fmax(rint((y - (double)q1) * 254.0), -127.0), 127.0);
+        const double ct = sc * ((double)q1 + (double)q2 / 254.0);
+        er += ((double)cj[f] - ct) * ((double)cj[f] - ct);
+        c2 += ct * ct;
+      }
+      candq[(size_t)j * dq + f] = (int8_t)q1;
+      candq[(size_t)(16 + j) * dq + f] = (int8_t)q2;
     }
-    if (lane == 0) { red[0][wave] = a; red[1][wave] = s; red[2][wave] = b; }
+    er = wave_sum(er);
+    c2 = wave_sum(c2);
+    if (lane == 0) { redd[0][wave] = er; redd[1][wave] = c2; }
     __syncthreads();
     if (threadIdx.x == 0) {
-      cinfo[j * 4 + 0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-      cinfo[j * 4 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-      // |sum c| and sum |c| only enter the bound as upper bounds: round up
-      cinfo[j * 4 + 2] = ((red[2][0] + red[2][1]) + (red[2][2] + red[2][3])) * 1.0001f;
-      cinfo[j * 4 + 3] = 0.0f;
+      const double e = (redd[0][0] + redd[0][1]) + (redd[0][2] + redd[0][3]);
+      const double q = (redd[1][0] + redd[1][1]) + (redd[1][2] + redd[1][3]);
+      cinfo[j * 4 + 0] = sc;
+      cinfo[j * 4 + 1] = sqrt(e) * (1.0 + 1e-12) + 1e-12 * sqrt(q);
+      cinfo[j * 4 + 2] = q;
+      cinfo[j * 4 + 3] = 0.0;
     }
   }
 }
@@ -249,95 +267,111 @@ __global__ void __launch_bounds__(256) kmpp_screen_kernel(
 }
 
 // ------------------------------------------------ 2. certified int8 bound
-template <int TMAX>
+typedef int kpp_v4i __attribute__((ext_vector_type(4)));
+
+// <q_row, q1_j> and <q_row, q2_j> for the 16 rows of a group (row slot =
+// lane & 15, -1: none) and the 16 trial slots: lane l supplies 16 bytes of
+// row (l & 15) and of trial (l & 15) at k-block l >> 4 of every 64-feature
+// step; out: lane l = trial l & 15, rows 4 (l >> 4) + i
+SQ_DEV void kpp_i8_dots(const int8_t* __restrict__ Xq, int dq, int row,
+                        const int8_t* __restrict__ cb, int lane, kpp_v4i& hi, kpp_v4i& lo) {
+  const int c16 = lane & 15, kb = lane >> 4;
+  hi = kpp_v4i{0, 0, 0, 0};
+  lo = kpp_v4i{0, 0, 0, 0};
+  const int8_t* xr = Xq + (size_t)(row >= 0 ? row : 0) * dq + 16 * kb;
+  const int8_t* b1 = cb + (size_t)c16 * dq + 16 * kb;
+  const int8_t* b2 = cb + (size_t)(16 + c16) * dq + 16 * kb;
+  for (int s = 0; s < dq; s += 64) {
+    kpp_v4i a = kpp_v4i{0, 0, 0, 0};
+    if (row >= 0) a = *reinterpret_cast<const kpp_v4i*>(xr + s);
+    const kpp_v4i bh = *reinterpret_cast<const kpp_v4i*>(b1 + s);
+    const kpp_v4i bl = *reinterpret_cast<const kpp_v4i*>(b2 + s);
+    hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bh, hi, 0, 0, 0);
+    lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bl, lo, 0, 0, 0);
+  }
+}
+
 __global__ void __launch_bounds__(256) kmpp_bound_kernel(
-    const uint8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
-    const float* __restrict__ erow, const float* __restrict__ xq2,
-    const float* __restrict__ closest, const float* __restrict__ candq,
-    const float* __restrict__ cinfo, int t, int d, long long R, const int* __restrict__ surv,
+    const int8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
+    const float* __restrict__ erow, const int* __restrict__ q2row,
+    const float* __restrict__ closest, const int8_t* __restrict__ candq,
+    const double* __restrict__ cinfo, int t, int d, long long R, const int* __restrict__ surv,
     const int* __restrict__ scount, int* __restrict__ exact, int* __restrict__ ecount) {
-  __shared__ uint32_t tile[4][64 * kKqStride];
+  extern __shared__ __attribute__((aligned(16))) int8_t cb[];   // [2][16][dq]
   __shared__ int lcnt;
+  for (int e = threadIdx.x * 16; e < 32 * dq; e += 256 * 16)
+    *reinterpret_cast<uint4*>(cb + e) = *reinterpret_cast<const uint4*>(candq + e);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* my = tile[wave];
+  const int c16 = lane & 15, kb = lane >> 4;
   const long long r0 = (long long)blockIdx.x * R;
   const int cnt = scount[blockIdx.x];
   const int* sseg = surv + r0;
   int* eseg = exact + r0;
   if (threadIdx.x == 0) lcnt = 0;
   __syncthreads();
-  const long long nb = (cnt + 63) / 64;
-  const int ntiles = dq / kKqTile + (dq % kKqTile ? 1 : 0);
-  // rigorous fp32 error of the int8 dot products: gamma_d = d u / (1 - d u)
-  const float gam = (float)((double)dq * 5.960464477539063e-08 / (1.0 - (double)dq * 5.960464477539063e-08));
-  const float rel = 3.0f * (float)(d + 2) * 5.960464477539063e-08f + 1e-6f;
-  for (long long b = wave; b < nb; b += 4) {
-    const long long e = b * 64 + lane;
+  // the exact pass's fp32 direct-form D carries <= 3 (d + 2) u relative error
+  const double lim_rel = 1.0 + 3.0 * (double)(d + 2) * 5.960464477539063e-08 + 1e-6;
+  const bool jv = c16 < t;
+  const double sc = jv ? cinfo[c16 * 4 + 0] : 1.0;
+  const double ec = jv ? cinfo[c16 * 4 + 1] : 0.0;
+  const double cc2 = jv ? cinfo[c16 * 4 + 2] : 0.0;
+  for (int g0 = wave * 16; g0 < cnt; g0 += 64) {
+    const int e = g0 + c16;
     const int row = e < cnt ? sseg[e] : -1;
-    float acc[TMAX];
+    kpp_v4i hi, lo;
+    kpp_i8_dots(Xq, dq, row, cb, lane, hi, lo);
+    unsigned long long bal[4];
 #pragma unroll
-    for (int j = 0; j < TMAX; ++j) acc[j] = 0.0f;
-    for (int tix = 0; tix < ntiles; ++tix) {
-      // stage: row slot q * 16 + (lane >> 2), 16-B chunk lane & 3
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int slot = q * 16 + (lane >> 2);
-        const int r = __shfl(row, slot, 64);
-        const int f = tix * kKqTile + (lane & 3) * 16;
-        uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
-        if (r >= 0 && f < dq) v = *reinterpret_cast<const uint4*>(Xq + (size_t)r * dq + f);
-        uint32_t* dst = my + slot * kKqStride + (lane & 3) * 4;
-        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-      }
-      const int f0 = tix * kKqTile;
-      const int nw = min(kKqTile, dq - f0) / 4;
-      for (int k4 = 0; k4 < nw; ++k4) {
-        const uint32_t wv = my[lane * kKqStride + k4];
-        // (v_cvt_f32_ubyte0..3)
-        const float u0 = (float)(wv & 0xFFu), u1 = (float)((wv >> 8) & 0xFFu);
-        const float u2 = (float)((wv >> 16) & 0xFFu), u3 = (float)(wv >> 24);
-        const int f = f0 + 4 * k4;
-#pragma unroll
-        for (int j = 0; j < TMAX; ++j) {
-          if (j < t) {
-            const float* cj = candq + (size_t)j * dq + f;
-            float a = acc[j];
-            a = fmaf(u0, cj[0], a);
-            a = fmaf(u1, cj[1], a);
-            a = fmaf(u2, cj[2], a);
-            a = fmaf(u3, cj[3], a);
-            acc[j] = a;
-          }
+    for (int i = 0; i < 4; ++i) {
+      const int rr = __shfl(row, 4 * kb + i, 64);
+      bool need = false;
+      if (jv && rr >= 0) {
+        const double s = (double)srow[rr];
+        const double A = s * s * (double)q2row[rr];
+        const double dot = s * sc * ((double)hi[i] + (double)lo[i] * (1.0 / 254.0));
+        const double Dq = (A + cc2) - 2.0 * dot;
+        const double Dlb = Dq - 1e-13 * (A + cc2 + 2.0 * fabs(dot));
+        double lb = 0.0;
+        if (Dlb > 0.0) {
+          const double r = sqrt(Dlb) * (1.0 - 1e-15) - (double)erow[rr] - ec;
+          lb = r > 0.0 ? r * r * (1.0 - 1e-15) : 0.0;
         }
+        need = !(lb > (double)closest[rr] * lim_rel);
       }
+      bal[i] = __ballot(need);
     }
-    bool need = false;
-    if (row >= 0) {
-      const float cl = closest[row];
-      const float s = srow[row], er = erow[row], q2 = xq2[row];
-      const float lim = cl * (1.0f + rel);
-#pragma unroll
-      for (int j = 0; j < TMAX; ++j) {
-        if (j < t) {
-          const float cn = cinfo[j * 4 + 0], cs = cinfo[j * 4 + 1], ca = cinfo[j * 4 + 2];
-          // x~ . c = s (sum u c - 128 sum c);  |fl - exact| <= s 383 gamma sum|c| + 3 u |.|
-          const float dot = s * (acc[j] - 128.0f * cs);
-          const float Dq = (q2 + cn) - 2.0f * dot;
-          const float E = 2.0f * s * 400.0f * gam * ca + 1e-6f * (q2 + cn + 2.0f * fabsf(dot));
-          const float lb2 = Dq - E;
-          float lb = 0.0f;
-          if (lb2 > 0.0f) {
-            const float r = __builtin_amdgcn_sqrtf(lb2) * (1.0f - 1e-6f) - er;
-            lb = r > 0.0f ? r * r * (1.0f - 1e-6f) : 0.0f;
-          }
-          need |= !(lb > lim);
-        }
-      }
-    }
-    seg_append(need, row, eseg, &lcnt);
+    // row slot c16 (lanes < 16): rows 4 q + i live in lanes [16 q, 16 q + 16) of bal[i]
+    const int q = c16 >> 2, ii = c16 & 3;
+    const unsigned long long bi = ii == 0 ? bal[0] : ii == 1 ? bal[1] : ii == 2 ? bal[2] : bal[3];
+    const bool take = lane < 16 && row >= 0 && ((bi >> (16 * q)) & 0xFFFFull) != 0ull;
+    seg_append(take, row, eseg, &lcnt);
   }
   __syncthreads();
   if (threadIdx.x == 0) ecount[blockIdx.x] = lcnt;
+}
+
+// test hook: out[r][j] = <q_r, q1_j>, out[n + r][j]... (int32 [2][n][16]) for rows 0..n-1
+__global__ void __launch_bounds__(64) kmpp_dots_kernel(const int8_t* __restrict__ Xq, int dq,
+                                                       long long n,
+                                                       const int8_t* __restrict__ candq,
+                                                       int* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) int8_t cb[];
+  for (int e = threadIdx.x * 16; e < 32 * dq; e += 64 * 16)
+    *reinterpret_cast<uint4*>(cb + e) = *reinterpret_cast<const uint4*>(candq + e);
+  __syncthreads();
+  const int lane = threadIdx.x;
+  const long long g0 = (long long)blockIdx.x * 16;
+  const long long r = g0 + (lane & 15);
+  kpp_v4i hi, lo;
+  kpp_i8_dots(Xq, dq, r < n ? (int)r : -1, cb, lane, hi, lo);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long rr = g0 + 4 * (lane >> 4) + i;
+    if (rr < n) {
+      out[rr * 16 + (lane & 15)] = hi[i];
+      out[(n + rr) * 16 + (lane & 15)] = lo[i];
+    }
+  }
 }
 
 // ------------------------------------------------------- 3. exact pass
@@ -507,14 +541,14 @@ static int kpp_grid(long long n) {
   return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
 }
 
-// Xq uint8 [n][dq] (dq = d rounded up to 16), srow / erow / xq2 fp32 [n]
+// Xq int8 [n][dq] (dq = d rounded up to 64), srow / erow fp32 [n], q2row int32 [n]
 int sq_kmpp_quantize(const void* X, long long ldx, int d, long long n, void* Xq, int dq, void* srow,
                      void* erow, void* xq2, void* stream) {
   if (n <= 0) return 0;
-  if (d <= 0 || dq < d || (dq & 15) || ldx < d) return (int)hipErrorInvalidValue;
+  if (d <= 0 || dq < d || (dq & 63) || ldx < d) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmpp_quantize_kernel, dim3(kpp_grid(n * 64 / 256 + 1)), dim3(256), 0,
-                     (hipStream_t)stream, (const float*)X, ldx, d, n, (uint8_t*)Xq, dq,
-                     (float*)srow, (float*)erow, (float*)xq2);
+                     (hipStream_t)stream, (const float*)X, ldx, d, n, (int8_t*)Xq, dq,
+                     (float*)srow, (float*)erow, (int*)xq2);
   return (int)hipGetLastError();
 }
 
@@ -542,11 +576,11 @@ int sq_kmpp_block_totals(const void* closest, const void* w, long long n, long l
 int sq_kmpp_cc(const void* cand, const void* C, int c, int d, int t, void* cc, int ldcc,
                void* cinfo, void* candq, int dq, void* delta_part, long long ndp, void* counters,
                void* stream) {
-  if (t < 1 || t > 16 || c < 0 || c > ldcc || dq < d) return (int)hipErrorInvalidValue;
+  if (t < 1 || t > 16 || c < 0 || c > ldcc || dq < d || (dq & 63)) return (int)hipErrorInvalidValue;
   const int gy = c > 0 ? (c + 63) / 64 : 1;
   hipLaunchKernelGGL(kmpp_cc_kernel, dim3(t, gy), dim3(256), 0, (hipStream_t)stream,
                      (const float*)cand, (const float*)C, c, d, t, (float*)cc, ldcc,
-                     (float*)cinfo, (float*)candq, dq, (double*)delta_part, ndp, (int*)counters);
+                     (double*)cinfo, (int8_t*)candq, dq, (double*)delta_part, ndp, (int*)counters);
   return (int)hipGetLastError();
 }
 
@@ -565,22 +599,28 @@ int sq_kmpp_screen(void* closest, void* nearest, const void* mask_prev, const vo
   return (int)hipGetLastError();
 }
 
+// candq int8 [2][16][dq] (trial slots >= t zero), cinfo fp64 [t][4]
 int sq_kmpp_bound(const void* Xq, int dq, const void* srow, const void* erow, const void* xq2,
                   const void* closest, const void* candq, const void* cinfo, int t, int d,
                   long long n, long long R, int G, const void* surv, const void* scount,
                   void* exact, void* ecount, void* stream) {
   if (n <= 0) return 0;
-  if (t < 1 || t > 16 || (dq & 15) || dq < d || R <= 0 || G <= 0) return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-#define LAUNCH(TM)                                                                              \
-  hipLaunchKernelGGL(kmpp_bound_kernel<TM>, dim3(G), dim3(256), 0, st, (const uint8_t*)Xq,     \
-                     dq, (const float*)srow, (const float*)erow, (const float*)xq2,            \
-                     (const float*)closest, (const float*)candq, (const float*)cinfo, t, d, R, \
-                     (const int*)surv, (const int*)scount, (int*)exact, (int*)ecount)
-  if (t <= 4) LAUNCH(4);
-  else if (t <= 8) LAUNCH(8);
-  else LAUNCH(16);
-#undef LAUNCH
+  if (t < 1 || t > 16 || (dq & 63) || dq < d || R <= 0 || G <= 0 || 32 * dq > 65536)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_bound_kernel, dim3(G), dim3(256), (size_t)32 * dq, (hipStream_t)stream,
+                     (const int8_t*)Xq, dq, (const float*)srow, (const float*)erow,
+                     (const int*)xq2, (const float*)closest, (const int8_t*)candq,
+                     (const double*)cinfo, t, d, R, (const int*)surv, (const int*)scount,
+                     (int*)exact, (int*)ecount);
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_dots(const void* Xq, int dq, long long n, const void* candq, void* out, void* stream) {
+  if (n <= 0) return 0;
+  if ((dq & 63) || 32 * dq > 65536) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_dots_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), (size_t)32 * dq,
+                     (hipStream_t)stream, (const int8_t*)Xq, dq, n, (const int8_t*)candq,
+                     (int*)out);
   return (int)hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ __attribute__((weak)) int sq_kmpp_cc(const void*, const void*, int, int, int, vo
 __attribute__((weak)) int sq_kmpp_screen(void*, void*, const void*, const void*, const void*, int,
                                          const void*, int, int, long long, long long, int, void*,
                                          void*, void*, void*, void*, int, void*);
+__attribute__((weak)) int sq_kmpp_dots(const void*, int, long long, const void*, void*, void*);
 __attribute__((weak)) int sq_kmpp_bound(const void*, int, const void*, const void*, const void*,
                                         const void*, const void*, const void*, int, int,
                                         long long, long long, int, const void*, const void*,
@@ -500,6 +501,13 @@ static PyObject* py_kmpp_exact(PyObject*, PyObject* a) {
                            P(Do), P(dp), R, G, P(st)));
 }
 
+static PyObject* py_kmpp_dots(PyObject*, PyObject* a) {
+  unsigned long long Xq, cq, out, st; int dq; long long n;
+  if (!PyArg_ParseTuple(a, "KiLKKK", &Xq, &dq, &n, &cq, &out, &st)) return nullptr;
+  CHECK(sq_kmpp_dots)
+  return ret(sq_kmpp_dots(P(Xq), dq, n, P(cq), P(out), P(st)));
+}
+
 static PyObject* py_kmpp_pick(PyObject*, PyObject* a) {
   unsigned long long bt, v, cl, m, D, b, w, pos, st; int G, t; long long R, n; double scale;
   if (!PyArg_ParseTuple(a, "KiLLKiKKKKKdKK", &bt, &G, &R, &n, &v, &t, &cl, &m, &D, &b, &w, &scale,
@@ -663,6 +671,7 @@ static PyMethodDef methods[] = {
     {"kmpp_screen", py_kmpp_screen, METH_VARARGS, "k-means++ triangle screen + lazy update"},
     {"kmpp_bound", py_kmpp_bound, METH_VARARGS, "k-means++ certified int8 bound"},
     {"kmpp_exact", py_kmpp_exact, METH_VARARGS, "k-means++ exact fp32 trial distances"},
+    {"kmpp_dots", py_kmpp_dots, METH_VARARGS, "int8 MFMA dots of the k-means++ bound (test hook)"},
     {"kmpp_pick", py_kmpp_pick, METH_VARARGS, "k-means++ two-level potential sampling"},
     {"rows_f64", py_rows_f64, METH_VARARGS, "exact fp64 E-step over a row list (fp64 MFMA)"},
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},

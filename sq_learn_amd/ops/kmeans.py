@@ -792,7 +792,7 @@ class KmppState:
         self.ldx = Xf.stride(0)
         self.w = None if w is None else w.to(device=dev, dtype=torch.float64).contiguous()
         self.prune = bool(prune) and d <= 8192
-        self.dq = -(-d // 16) * 16
+        self.dq = -(-d // 64) * 64
         self.dev = dev
         m = nat.native()
         self.m = m
@@ -801,10 +801,10 @@ class KmppState:
         self.R = max(1, -(-n // G0))
         self.G = max(1, -(-n // self.R))
         if self.prune and n:
-            self.Xq = torch.empty((n, self.dq), dtype=torch.uint8, device=dev)
+            self.Xq = torch.empty((n, self.dq), dtype=torch.int8, device=dev)
             self.srow = torch.empty(n, dtype=torch.float32, device=dev)
             self.erow = torch.empty(n, dtype=torch.float32, device=dev)
-            self.xq2 = torch.empty(n, dtype=torch.float32, device=dev)
+            self.xq2 = torch.empty(n, dtype=torch.int32, device=dev)   # |q|^2 (exact)
             _rc(m.kmpp_quantize(Xf.data_ptr(), self.ldx, d, n, self.Xq.data_ptr(), self.dq,
                                 self.srow.data_ptr(), self.erow.data_ptr(), self.xq2.data_ptr(),
                                 self.st), "kmpp_quantize")
@@ -820,8 +820,9 @@ class KmppState:
         self.ecount = torch.zeros(self.G, dtype=torch.int32, device=dev)
         self.counters = torch.zeros(4, dtype=torch.int32, device=dev)
         self.cc = torch.zeros((t, self.k), dtype=torch.float32, device=dev)
-        self.cinfo = torch.zeros((t, 4), dtype=torch.float32, device=dev)
-        self.candq = torch.zeros((t, self.dq), dtype=torch.float32, device=dev)
+        # two-term int8 candidates [hi / lo][16 trial slots][dq] and (s_c, ec, |c~|^2, 0)
+        self.cinfo = torch.zeros((16, 4), dtype=torch.float64, device=dev)
+        self.candq = torch.zeros((2, 16, self.dq), dtype=torch.int8, device=dev)
         self.delta = torch.zeros((self.G, t), dtype=torch.float64, device=dev)
         self.block_tot = torch.zeros(self.G, dtype=torch.float64, device=dev)
         self.pos = torch.zeros(t, dtype=torch.int64, device=dev)

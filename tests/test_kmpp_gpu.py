@@ -127,3 +127,22 @@ def test_device_kmeans_plusplus_seeding_quality():
         return D.min(1).sum()
     ig, ic = inertia(Cg), inertia(out["cpu"][0])
     assert ig <= 1.5 * ic and ic <= 1.5 * ig
+
+
+@pytest.mark.parametrize("n,dq", [(37, 64), (100, 256), (16, 832)])
+def test_kmpp_int8_mfma_dots_exact(n, dq):
+    """The certified bound's int8 MFMA dot products (v_mfma_i32_16x16x64_i8
+    fragments built by kpp_i8_dots) equal numpy's integer dot products for
+    both candidate terms and every trial slot."""
+    from sq_learn_amd.ops import _native as nat
+    rs = np.random.RandomState(dq)
+    Xq = rs.randint(-127, 128, (n, dq)).astype(np.int8)
+    cq = rs.randint(-127, 128, (2, 16, dq)).astype(np.int8)
+    Xt = torch.from_numpy(Xq).cuda()
+    ct = torch.from_numpy(cq).cuda()
+    out = torch.zeros((2, n, 16), dtype=torch.int32, device="cuda")
+    rc = nat.native().kmpp_dots(Xt.data_ptr(), dq, n, ct.data_ptr(), out.data_ptr(),
+                                nat.stream_handle(Xt.device))
+    assert rc == 0
+    ref = np.einsum("nf,hjf->hnj", Xq.astype(np.int64), cq.astype(np.int64))
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
