@@ -43,79 +43,70 @@ constexpr int kKppStride = 36;        // LDS row stride in floats (16-B aligned,
 
 SQ_DEV double kpp_q(float v, double wi, double scale) { return rint((double)v * wi * scale); }
 
-// ------------------------------------------------------------ int8 copy
-// q = rint(x / s) (s = max|x| / 127), e = |x - s q| rounded up, q2 = |q|^2
-// (exact int); features d .. dq-1 are zero
-__global__ void __launch_bounds__(256) kmpp_quantize_kernel(
-    const float* __restrict__ X, long long ldx, int d, long long n, int8_t* __restrict__ Xq,
-    int dq, float* __restrict__ srow, float* __restrict__ erow, int* __restrict__ q2row) {
-  const int lane = threadIdx.x & 63;
-  const long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long i = w; i < n; i += nw) {
-    const float* x = X + i * ldx;
-    float mx = 0.0f;
-    for (int f = lane; f < d; f += 64) mx = fmaxf(mx, fabsf(x[f]));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-    const float s = mx > 0.0f ? mx / 127.0f : 1.0f;
-    double e2 = 0.0;
-    int q2 = 0;
-    for (int f = lane; f < dq; f += 64) {
-      int q = 0;
-      if (f < d) {
-        q = (int)fminf(fmaxf(rintf(x[f] / s), -127.0f), 127.0f);
-        const double r = (double)x[f] - (double)s * (double)q;
-        e2 += r * r;
-        q2 += q * q;
-      }
-      Xq[i * dq + f] = (int8_t)q;
-    }
-    e2 = wave_sum(e2);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q2 += __shfl_xor(q2, o, 64);
-    if (lane == 0) {
-      srow[i] = s;
-      erow[i] = (float)(sqrt(e2) * (1.0 + 1e-6)) * 1.000001f;
-      q2row[i] = q2;
-    }
-  }
-}
-
-// ------------------------------------------------- first centre + scale
-// closest_i = direct-form |x_i - c0|^2, nearest_i = 0, per-block max of
-// w_i closest_i (the caller turns the global max into the fixed-point scale)
+// ------------------------------------- first centre (+ the int8 copy)
+// One wave per row (coalesced 64-lane reads): closest_i = |x_i - c0|^2
+// (fp32, fixed wave-tree order), nearest_i = 0, the per-block max of
+// w_i closest_i (the caller turns the global max into the fixed-point
+// scale); with Xq: the row's int8 copy in the same pass - q = rint(x / s)
+// (s = max|x| / 127), e = |x - s q| rounded up, q2 = |q|^2 (exact int),
+// features d .. dq-1 zero.
 __global__ void __launch_bounds__(256) kmpp_init_kernel(
     const float* __restrict__ X, long long ldx, int d, long long n, const float* __restrict__ c0,
     const double* __restrict__ w, float* __restrict__ closest, int* __restrict__ nearest,
-    double* __restrict__ bmax) {
-  __shared__ double red[256];
+    double* __restrict__ bmax, int8_t* __restrict__ Xq, int dq, float* __restrict__ srow,
+    float* __restrict__ erow, int* __restrict__ q2row) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long w0 = (long long)blockIdx.x * 4 + wave;
+  const long long nw = (long long)gridDim.x * 4;
   double m = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+  for (long long i = w0; i < n; i += nw) {
     const float* x = X + i * ldx;
-    float acc = 0.0f;
-    for (int f = 0; f < d; f += 4) {
-      const float4 x4 = *reinterpret_cast<const float4*>(x + f);
-      float e = x4.x - c0[f];
+    float acc = 0.0f, mx = 0.0f;
+    for (int f = lane; f < d; f += 64) {
+      const float v = x[f];
+      const float e = v - c0[f];
       acc = fmaf(e, e, acc);
-      e = x4.y - c0[f + 1];
-      acc = fmaf(e, e, acc);
-      e = x4.z - c0[f + 2];
-      acc = fmaf(e, e, acc);
-      e = x4.w - c0[f + 3];
-      acc = fmaf(e, e, acc);
+      mx = fmaxf(mx, fabsf(v));
     }
-    closest[i] = acc;
-    nearest[i] = 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      acc += __shfl_xor(acc, o, 64);
+      mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    }
+    if (lane == 0) {
+      closest[i] = acc;
+      nearest[i] = 0;
+    }
     m = fmax(m, (double)acc * (w ? w[i] : 1.0));
+    if (Xq) {
+      const float s = mx > 0.0f ? mx / 127.0f : 1.0f;
+      double e2 = 0.0;
+      int q2 = 0;
+      for (int f = lane; f < dq; f += 64) {
+        int q = 0;
+        if (f < d) {
+          const float v = x[f];
+          q = (int)fminf(fmaxf(rintf(v / s), -127.0f), 127.0f);
+          const double r = (double)v - (double)s * (double)q;
+          e2 += r * r;
+          q2 += q * q;
+        }
+        Xq[i * dq + f] = (int8_t)q;
+      }
+      e2 = wave_sum(e2);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) q2 += __shfl_xor(q2, o, 64);
+      if (lane == 0) {
+        srow[i] = s;
+        erow[i] = (float)(sqrt(e2) * (1.0 + 1e-6)) * 1.000001f;
+        q2row[i] = q2;
+      }
+    }
   }
-  red[threadIdx.x] = m;
+  if (lane == 0) red[wave] = m;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) bmax[blockIdx.x] = red[0];
+  if (threadIdx.x == 0) bmax[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
 }
 
 // block b of the fixed row partition (rows [b R, b R + R)): exact fixed-point total
@@ -541,27 +532,19 @@ static int kpp_grid(long long n) {
   return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
 }
 
-// Xq int8 [n][dq] (dq = d rounded up to 64), srow / erow fp32 [n], q2row int32 [n]
-int sq_kmpp_quantize(const void* X, long long ldx, int d, long long n, void* Xq, int dq, void* srow,
-                     void* erow, void* xq2, void* stream) {
-  if (n <= 0) return 0;
-  if (d <= 0 || dq < d || (dq & 63) || ldx < d) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmpp_quantize_kernel, dim3(kpp_grid(n * 64 / 256 + 1)), dim3(256), 0,
-                     (hipStream_t)stream, (const float*)X, ldx, d, n, (int8_t*)Xq, dq,
-                     (float*)srow, (float*)erow, (int*)xq2);
-  return (int)hipGetLastError();
-}
-
 // closest fp32 [n], nearest int32 [n], bmax fp64 [grid] with grid = sq_kmpp_grid(n)
 int sq_kmpp_grid(long long n) { return kpp_grid(n); }
 
+// Xq (nullable) int8 [n][dq] (dq = d rounded up to 64), srow / erow fp32 [n], q2row int32 [n]
 int sq_kmpp_init(const void* X, long long ldx, int d, long long n, const void* c0, const void* w,
-                 void* closest, void* nearest, void* bmax, void* stream) {
+                 void* closest, void* nearest, void* bmax, void* Xq, int dq, void* srow,
+                 void* erow, void* q2row, void* stream) {
   if (n <= 0) return 0;
-  if (d <= 0 || (d & 3) || ldx < d || (ldx & 3)) return (int)hipErrorInvalidValue;
+  if (d <= 0 || ldx < d || (Xq && (dq < d || (dq & 63)))) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmpp_init_kernel, dim3(kpp_grid(n)), dim3(256), 0, (hipStream_t)stream,
                      (const float*)X, ldx, d, n, (const float*)c0, (const double*)w,
-                     (float*)closest, (int*)nearest, (double*)bmax);
+                     (float*)closest, (int*)nearest, (double*)bmax, (int8_t*)Xq, dq,
+                     (float*)srow, (float*)erow, (int*)q2row);
   return (int)hipGetLastError();
 }
 

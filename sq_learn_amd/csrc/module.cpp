@@ -104,10 +104,9 @@ __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const
 __attribute__((weak)) int sq_sum_f32(const void*, long long, void*, int, void*, void*);
 // kmpp.hip
 __attribute__((weak)) int sq_kmpp_grid(long long);
-__attribute__((weak)) int sq_kmpp_quantize(const void*, long long, int, long long, void*, int, void*,
-                                           void*, void*, void*);
 __attribute__((weak)) int sq_kmpp_init(const void*, long long, int, long long, const void*,
-                                       const void*, void*, void*, void*, void*);
+                                       const void*, void*, void*, void*, void*, int, void*, void*,
+                                       void*, void*);
 __attribute__((weak)) int sq_kmpp_block_totals(const void*, const void*, long long, long long, int,
                                                double, void*, void*);
 __attribute__((weak)) int sq_kmpp_cc(const void*, const void*, int, int, int, void*, int, void*,
@@ -435,20 +434,14 @@ static PyObject* py_kmpp_grid(PyObject*, PyObject* a) {
   return PyLong_FromLong(sq_kmpp_grid(n));
 }
 
-static PyObject* py_kmpp_quantize(PyObject*, PyObject* a) {
-  unsigned long long X, Xq, sr, er, q2, st; long long ldx, n; int d, dq;
-  if (!PyArg_ParseTuple(a, "KLiLKiKKKK", &X, &ldx, &d, &n, &Xq, &dq, &sr, &er, &q2, &st))
-    return nullptr;
-  CHECK(sq_kmpp_quantize)
-  return ret(sq_kmpp_quantize(P(X), ldx, d, n, P(Xq), dq, P(sr), P(er), P(q2), P(st)));
-}
-
 static PyObject* py_kmpp_init(PyObject*, PyObject* a) {
-  unsigned long long X, c0, w, cl, nr, bm, st; long long ldx, n; int d;
-  if (!PyArg_ParseTuple(a, "KLiLKKKKKK", &X, &ldx, &d, &n, &c0, &w, &cl, &nr, &bm, &st))
+  unsigned long long X, c0, w, cl, nr, bm, Xq, sr, er, q2, st; long long ldx, n; int d, dq;
+  if (!PyArg_ParseTuple(a, "KLiLKKKKKKiKKKK", &X, &ldx, &d, &n, &c0, &w, &cl, &nr, &bm, &Xq, &dq,
+                        &sr, &er, &q2, &st))
     return nullptr;
   CHECK(sq_kmpp_init)
-  return ret(sq_kmpp_init(P(X), ldx, d, n, P(c0), P(w), P(cl), P(nr), P(bm), P(st)));
+  return ret(sq_kmpp_init(P(X), ldx, d, n, P(c0), P(w), P(cl), P(nr), P(bm), P(Xq), dq, P(sr),
+                          P(er), P(q2), P(st)));
 }
 
 static PyObject* py_kmpp_block_totals(PyObject*, PyObject* a) {
@@ -664,7 +657,6 @@ static PyMethodDef methods[] = {
     {"fill_mind", py_fill_mind, METH_VARARGS, "exact distance to the label for marked rows"},
     {"sum_f32", py_sum_f32, METH_VARARGS, "deterministic sum of a float vector"},
     {"kmpp_grid", py_kmpp_grid, METH_VARARGS, "k-means++ trial pass grid size"},
-    {"kmpp_quantize", py_kmpp_quantize, METH_VARARGS, "k-means++ int8 row copy + error norms"},
     {"kmpp_init", py_kmpp_init, METH_VARARGS, "k-means++ first centre distances"},
     {"kmpp_block_totals", py_kmpp_block_totals, METH_VARARGS, "k-means++ fixed-point block totals"},
     {"kmpp_cc", py_kmpp_cc, METH_VARARGS, "k-means++ candidate-centre distances"},

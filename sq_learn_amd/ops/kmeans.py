@@ -805,9 +805,7 @@ class KmppState:
             self.srow = torch.empty(n, dtype=torch.float32, device=dev)
             self.erow = torch.empty(n, dtype=torch.float32, device=dev)
             self.xq2 = torch.empty(n, dtype=torch.int32, device=dev)   # |q|^2 (exact)
-            _rc(m.kmpp_quantize(Xf.data_ptr(), self.ldx, d, n, self.Xq.data_ptr(), self.dq,
-                                self.srow.data_ptr(), self.erow.data_ptr(), self.xq2.data_ptr(),
-                                self.st), "kmpp_quantize")
+            # (filled by first_centre's pass over X)
         nn = max(n, 1)
         self.closest = torch.empty(nn, dtype=torch.float32, device=dev)
         self.nearest = torch.zeros(nn, dtype=torch.int32, device=dev)
@@ -832,15 +830,20 @@ class KmppState:
         self.scale = 1.0
 
     def first_centre(self, c0):
-        """closest / nearest for the first centre; returns the local max of
-        w * closest (device fp64 [1]) for the global fixed-point scale."""
+        """closest / nearest for the first centre (and, pruned, the int8 row
+        copy in the same pass over X); returns the local max of w * closest
+        (device fp64 [1]) for the global fixed-point scale."""
         bmax = torch.zeros(self.m.kmpp_grid(max(self.n, 1)), dtype=torch.float64, device=self.dev)
         if self.n:
             c0 = c0.to(torch.float32).contiguous()
+            q = self.prune
             _rc(self.m.kmpp_init(self.X.data_ptr(), self.ldx, self.d, self.n, c0.data_ptr(),
                                  0 if self.w is None else self.w.data_ptr(),
                                  self.closest.data_ptr(), self.nearest.data_ptr(), bmax.data_ptr(),
-                                 self.st), "kmpp_init")
+                                 self.Xq.data_ptr() if q else 0, self.dq,
+                                 self.srow.data_ptr() if q else 0,
+                                 self.erow.data_ptr() if q else 0,
+                                 self.xq2.data_ptr() if q else 0, self.st), "kmpp_init")
         return bmax.max().reshape(1)
 
     def set_scale(self, max_pot, n_global):

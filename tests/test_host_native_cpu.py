@@ -338,3 +338,29 @@ def test_mt_permutation_head_matches_numpy():
         np.testing.assert_array_equal(ref, got)
         np.testing.assert_array_equal(a.randint(0, 1 << 30, 16), b.randint(0, 1 << 30, 16))
         assert a.rand() == b.rand()
+
+
+def test_stream_handle_makes_the_target_device_current(monkeypatch):
+    """Native launches resolve the null stream against the CURRENT device:
+    ``stream_handle('cuda:1')`` from a thread whose current device is 0 must
+    switch the thread to device 1 before returning the handle (device guard
+    of every ops/ native launch)."""
+    import torch
+    from sq_learn_amd.ops import _native as nat
+    state = {"cur": 0, "set": []}
+
+    class _S:
+        def __init__(self, idx):
+            self.cuda_stream = 1000 + idx
+
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: state["cur"])
+
+    def _set(i):
+        state["set"].append(i)
+        state["cur"] = i
+
+    monkeypatch.setattr(torch.cuda, "set_device", _set)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda idx=None: _S(state["cur"] if idx is None else idx))
+    assert nat.stream_handle("cuda:1") == 1001 and state["set"] == [1] and state["cur"] == 1
+    assert nat.stream_handle(torch.device("cuda", 1)) == 1001 and state["set"] == [1]
+    assert nat.stream_handle("cuda:0") == 1000 and state["set"] == [1, 0]
