@@ -910,11 +910,14 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
 // k-step) feeds R MFMAs (R independent accumulator chains), so the centroid
 // traffic per row drops R-fold; the R A fragments of a k-step are one LDS
 // read (As[(s 64 + l) R + g]).
+#ifndef SQ_IPE_KB
+#define SQ_IPE_KB 16   // k-steps per fragment batch (two batches in flight)
+#endif
 template <int D4, int R>
 SQ_DEV void ipe_tile_ipR(const float* __restrict__ As, const float* __restrict__ bf, int lane,
                          f32x4 (&acc)[R]) {
-  constexpr int B = 8;
-  static_assert(D4 % B == 0, "k-steps in batches of 8");
+  constexpr int B = D4 < SQ_IPE_KB ? D4 : SQ_IPE_KB;
+  static_assert(D4 % B == 0, "k-steps in whole batches");
   static_assert(R == 1 || R == 2, "one or two row groups");
 #pragma unroll
   for (int g = 0; g < R; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1112,13 +1115,18 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
     s_da.Q = Q;
     s_da.sc = sc;
   }
-  // A fragments, row-major reads (coalesced): row rl, feature f ->
-  // As[((f / 4) 64 + (rl mod 16) + 16 (f mod 4)) R + rl / 16]; rows past n clamped
-  for (int e = threadIdx.x; e < NR * D4 * 4; e += 256) {
-    const int rl = e / (D4 * 4), f = e - rl * (D4 * 4);
+  // A fragments: row rl, features 4 s .. 4 s + 3 (one lane: 16 contiguous
+  // bytes) -> As[(s 64 + (rl mod 16) + 16 i) R + rl / 16], i = 0..3; the
+  // lanes of a store take consecutive rows (2-way bank aliasing at most)
+  for (int e = threadIdx.x; e < NR * D4; e += 256) {
+    const int rl = e % NR, s4 = e / NR;
     const long long r = row0 + rl < n ? row0 + rl : n - 1;
-    const int l = (rl & 15) + ((f & 3) << 4);
-    As[((f >> 2) * 64 + l) * R + (rl >> 4)] = f < d ? X[(size_t)r * ldx + f] : 0.0f;
+    const float* xr = X + (size_t)r * ldx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = 4 * s4 + i;
+      As[(s4 * 64 + (rl & 15) + 16 * i) * R + (rl >> 4)] = f < d ? xr[f] : 0.0f;
+    }
   }
   // the rows' thresholds: given (hint pre-pass), or hj = -2: the first sweep's
   int need = 0;
@@ -1298,6 +1306,7 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
   const int ntl = wave < n_tiles ? (n_tiles - wave + 3) / 4 : 0;
   const int nun = ntl * R;
   f32x4 accs[R];
+  float ny2 = 0.0f;   // |c_j|^2 of this lane's centroid of the current tile
   for (int u = -1; u <= nun; ++u) {
     bool any_fired = false;
     int g = 0;
@@ -1333,7 +1342,12 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
       const int stp = R == 2 ? u >> 1 : u;
       g = u - stp * R;
       const int t = wave + 4 * stp;
-      if (g == 0) ipe_tile_ipR<D4, R>(As, Cf + (size_t)t * D4 * 64 + lane, lane, accs);
+      const int j = t * 16 + c16;
+      const bool jv = j < k;   // padded centroid columns do nothing
+      if (g == 0) {
+        ny2 = cn[jv ? j : 0];   // issued before the tile's MFMAs: no exposed L2 latency
+        ipe_tile_ipR<D4, R>(As, Cf + (size_t)t * D4 * 64 + lane, lane, accs);
+      }
       f32x4 acc = accs[0];
       u32x4 bd = bud[0];
       if constexpr (R == 2) {
@@ -1342,9 +1356,6 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
           bd = bud[1];
         }
       }
-      const int j = t * 16 + c16;
-      const bool jv = j < k;   // padded centroid columns do nothing
-      const float ny2 = cn[jv ? j : 0];
       // straight-line screen of the 4 pairs; one ballot decides whether any
       // lane appends (full-sampler pairs and fired pairs are rare)
       bool pp[4];

@@ -128,34 +128,42 @@ __global__ void __launch_bounds__(256) kmpp_block_totals_kernel(
 }
 
 // ------------------------------------------- candidate-centre distances
-// grid (t, ceil(c / 64)): cc[j][m] = |cand_j - C_m|^2 (m < c), one wave per
-// centre; blocks (j, 0) also write the two-term int8 candidate (candq[j] and
-// candq[16 + j], zero padded to dq) and cinfo[j]; the whole grid zeroes
-// delta_part and the list counters.
+// blocks 0 .. t-1: candidate j = blockIdx.x -> its two-term int8 copy
+// (candq[j], candq[16 + j], zero padded to dq) and cinfo[j]; blocks t ..:
+// one wave per chosen centre m < c -> ccmin[m] = min_j |cand_j - C_m|^2
+// (NaN-propagating: a NaN keeps every row of centre m live); the whole grid
+// zeroes delta_part and the list counters.
 __global__ void __launch_bounds__(256) kmpp_cc_kernel(
     const float* __restrict__ cand, const float* __restrict__ C, int c, int d, int t,
-    float* __restrict__ cc, int ldcc, double* __restrict__ cinfo, int8_t* __restrict__ candq,
-    int dq, double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
-  const int j = blockIdx.x;
+    float* __restrict__ ccmin, double* __restrict__ cinfo, int8_t* __restrict__ candq, int dq,
+    double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* cj = cand + (size_t)j * d;
-  const long long gid = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
-  const long long gsz = (long long)gridDim.x * gridDim.y * 256;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long gsz = (long long)gridDim.x * 256;
   for (long long e = gid; e < ndp; e += gsz) delta_part[e] = 0.0;
   if (gid < 4) counters[gid] = 0;
-  const int m0 = blockIdx.y * 64;
-  for (int m = m0 + wave; m < c && m < m0 + 64; m += 4) {
+  if ((int)blockIdx.x >= t) {
+    const int m = 4 * ((int)blockIdx.x - t) + wave;
+    if (m >= c) return;
     const float* cm = C + (size_t)m * d;
-    float acc = 0.0f;
-    for (int f = lane; f < d; f += 64) {
-      const float e = cj[f] - cm[f];
-      acc = fmaf(e, e, acc);
-    }
+    float mn = __builtin_inff();
+    for (int j = 0; j < t; ++j) {
+      const float* cj = cand + (size_t)j * d;
+      float acc = 0.0f;
+      for (int f = lane; f < d; f += 64) {
+        const float e = cj[f] - cm[f];
+        acc = fmaf(e, e, acc);
+      }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (lane == 0) cc[(size_t)j * ldcc + m] = acc;
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      mn = (acc != acc || acc < mn) ? acc : mn;
+    }
+    if (lane == 0) ccmin[m] = mn;
+    return;
   }
-  if (blockIdx.y == 0) {
+  const int j = blockIdx.x;
+  const float* cj = cand + (size_t)j * d;
+  {
     // two-term int8 candidate: y = c / s_c, q1 = rint(y), q2 = rint(254 (y - q1)),
     // c~ = s_c (q1 + q2 / 254); cinfo[j] = (s_c, ec >= |c - c~|, |c~|^2, 0) fp64
     __shared__ float redf[4];
@@ -221,8 +229,8 @@ SQ_DEV void seg_append(bool take, int value, int* __restrict__ seg, int* lcnt) {
 __global__ void __launch_bounds__(256) kmpp_screen_kernel(
     float* __restrict__ closest, int* __restrict__ nearest,
     const uint16_t* __restrict__ mask_prev, const float* __restrict__ Dprev,
-    const int* __restrict__ best_prev, int c_prev, const float* __restrict__ cc, int ldcc, int t,
-    long long n, long long R, uint16_t* __restrict__ mask_out, int* __restrict__ surv,
+    const int* __restrict__ best_prev, int c_prev, const float* __restrict__ ccmin, long long n,
+    long long R, uint16_t* __restrict__ mask_out, int* __restrict__ surv,
     int* __restrict__ exact, int* __restrict__ scount, int* __restrict__ ecount, int prune) {
   __shared__ int lcnt;
   const int bp = best_prev ? *best_prev : -1;
@@ -247,8 +255,7 @@ __global__ void __launch_bounds__(256) kmpp_screen_kernel(
       if (!prune) {
         live = true;
       } else if (cl > 0.0f) {
-        const float lim = 4.01f * cl;
-        for (int j = 0; j < t; ++j) live |= !(cc[(size_t)j * ldcc + a] > lim);
+        live = !(ccmin[a] > 4.01f * cl);   // some trial within 2 sqrt(closest) of C_a
       }
     }
     seg_append(live, (int)i, seg, &lcnt);
@@ -556,14 +563,14 @@ int sq_kmpp_block_totals(const void* closest, const void* w, long long n, long l
   return (int)hipGetLastError();
 }
 
+// cc: ccmin fp32 [>= c] (ldcc: its capacity)
 int sq_kmpp_cc(const void* cand, const void* C, int c, int d, int t, void* cc, int ldcc,
                void* cinfo, void* candq, int dq, void* delta_part, long long ndp, void* counters,
                void* stream) {
   if (t < 1 || t > 16 || c < 0 || c > ldcc || dq < d || (dq & 63)) return (int)hipErrorInvalidValue;
-  const int gy = c > 0 ? (c + 63) / 64 : 1;
-  hipLaunchKernelGGL(kmpp_cc_kernel, dim3(t, gy), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)cand, (const float*)C, c, d, t, (float*)cc, ldcc,
-                     (double*)cinfo, (int8_t*)candq, dq, (double*)delta_part, ndp, (int*)counters);
+  hipLaunchKernelGGL(kmpp_cc_kernel, dim3(t + (c + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)cand, (const float*)C, c, d, t, (float*)cc, (double*)cinfo,
+                     (int8_t*)candq, dq, (double*)delta_part, ndp, (int*)counters);
   return (int)hipGetLastError();
 }
 
@@ -576,8 +583,8 @@ int sq_kmpp_screen(void* closest, void* nearest, const void* mask_prev, const vo
   if (t < 1 || t > 16 || R <= 0 || G <= 0 || (long long)G * R < n) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmpp_screen_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream,
                      (float*)closest, (int*)nearest, (const uint16_t*)mask_prev,
-                     (const float*)Dprev, (const int*)best_prev, c_prev, (const float*)cc, ldcc,
-                     t, n, R, (uint16_t*)mask_out, (int*)surv, (int*)exact, (int*)scount,
+                     (const float*)Dprev, (const int*)best_prev, c_prev, (const float*)cc, n,
+                     R, (uint16_t*)mask_out, (int*)surv, (int*)exact, (int*)scount,
                      (int*)ecount, prune);
   return (int)hipGetLastError();
 }

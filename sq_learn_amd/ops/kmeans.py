@@ -817,7 +817,8 @@ class KmppState:
         self.scount = torch.zeros(self.G, dtype=torch.int32, device=dev)
         self.ecount = torch.zeros(self.G, dtype=torch.int32, device=dev)
         self.counters = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.cc = torch.zeros((t, self.k), dtype=torch.float32, device=dev)
+        # min over the trials of |cand_j - C_m|^2 per chosen centre m (triangle screen)
+        self.cc = torch.zeros(self.k, dtype=torch.float32, device=dev)
         # two-term int8 candidates [hi / lo][16 trial slots][dq] and (s_c, ec, |c~|^2, 0)
         self.cinfo = torch.zeros((16, 4), dtype=torch.float64, device=dev)
         self.candq = torch.zeros((2, 16, self.dq), dtype=torch.int8, device=dev)

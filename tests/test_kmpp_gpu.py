@@ -143,6 +143,6 @@ def test_kmpp_int8_mfma_dots_exact(n, dq):
     out = torch.zeros((2, n, 16), dtype=torch.int32, device="cuda")
     rc = nat.native().kmpp_dots(Xt.data_ptr(), dq, n, ct.data_ptr(), out.data_ptr(),
                                 nat.stream_handle(Xt.device))
-    assert rc == 0
+    assert not rc
     ref = np.einsum("nf,hjf->hnj", Xq.astype(np.int64), cq.astype(np.int64))
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
