@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--center", action="store_true")
     ap.add_argument("--no-unpruned", action="store_true")
+    ap.add_argument("--full-stats", action="store_true",
+                    help="survivor / exact fractions over all k centres (by quarter)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     X, _ = make_blobs_device(a.n, a.d, centers=1024, cluster_std=1.0, seed=1, device=dev,
@@ -40,8 +42,16 @@ def main():
         _, ids[prune] = kmeans_plusplus(data, a.k, np.random.RandomState(0), prune=prune)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        kmeans_plusplus(data, min(a.k, 64), np.random.RandomState(0), prune=prune, stats=stats)
+        kmeans_plusplus(data, a.k if a.full_stats else min(a.k, 64), np.random.RandomState(0),
+                        prune=prune, stats=stats)
         st = np.asarray(stats, dtype=np.float64) / a.n
+        if a.full_stats and len(st) >= 4:
+            q = np.array_split(st, 4)
+            print("survivor / exact frac by quarter of the centres:",
+                  [(round(float(x[:, 0].mean()), 4), round(float(x[:, 1].mean()), 4)) for x in q],
+                  "all:", round(float(st[:, 0].mean()), 4), round(float(st[:, 1].mean()), 4),
+                  flush=True)
+            st = st[:64]
         print(f"k-means++ prune={prune} n={a.n} d={a.d} k={a.k}: {el:.3f} s, "
               f"{el / max(a.k - 1, 1) * 1e3:.3f} ms/centre; first 64 centres: survivor frac "
               f"{st[:, 0].mean():.3f}, exact frac {st[:, 1].mean():.3f}", flush=True)

@@ -289,6 +289,11 @@ SQ_DEV void kpp_i8_dots(const int8_t* __restrict__ Xq, int dq, int row,
   }
 }
 
+// Each wave takes two 16-row groups per iteration: both groups' row ids,
+// then their int8 rows (NS 16-byte loads per lane each, NS = dq / 64 known
+// at compile time up to dq = 256) and per-row scalars are all in flight
+// before the MFMAs - the row gathers, not the int8 MFMAs, bound this pass.
+template <int NS>
 __global__ void __launch_bounds__(256) kmpp_bound_kernel(
     const int8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
     const float* __restrict__ erow, const int* __restrict__ q2row,
@@ -313,36 +318,91 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
   const double sc = jv ? cinfo[c16 * 4 + 0] : 1.0;
   const double ec = jv ? cinfo[c16 * 4 + 1] : 0.0;
   const double cc2 = jv ? cinfo[c16 * 4 + 2] : 0.0;
-  for (int g0 = wave * 16; g0 < cnt; g0 += 64) {
-    const int e = g0 + c16;
-    const int row = e < cnt ? sseg[e] : -1;
-    kpp_v4i hi, lo;
-    kpp_i8_dots(Xq, dq, row, cb, lane, hi, lo);
-    unsigned long long bal[4];
+  const int nsd = NS > 0 ? NS : dq / 64;
+  const int8_t* b1 = cb + (size_t)c16 * dq + 16 * kb;
+  const int8_t* b2 = cb + (size_t)(16 + c16) * dq + 16 * kb;
+  for (int g0 = wave * 32; g0 < cnt; g0 += 128) {
+    int row[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rr = __shfl(row, 4 * kb + i, 64);
-      bool need = false;
-      if (jv && rr >= 0) {
-        const double s = (double)srow[rr];
-        const double A = s * s * (double)q2row[rr];
-        const double dot = s * sc * ((double)hi[i] + (double)lo[i] * (1.0 / 254.0));
-        const double Dq = (A + cc2) - 2.0 * dot;
-        const double Dlb = Dq - 1e-13 * (A + cc2 + 2.0 * fabs(dot));
-        double lb = 0.0;
-        if (Dlb > 0.0) {
-          const double r = sqrt(Dlb) * (1.0 - 1e-15) - (double)erow[rr] - ec;
-          lb = r > 0.0 ? r * r * (1.0 - 1e-15) : 0.0;
-        }
-        need = !(lb > (double)closest[rr] * lim_rel);
-      }
-      bal[i] = __ballot(need);
+    for (int h = 0; h < 2; ++h) {
+      const int e = g0 + 16 * h + c16;
+      row[h] = e < cnt ? sseg[e] : -1;
     }
-    // row slot c16 (lanes < 16): rows 4 q + i live in lanes [16 q, 16 q + 16) of bal[i]
-    const int q = c16 >> 2, ii = c16 & 3;
-    const unsigned long long bi = ii == 0 ? bal[0] : ii == 1 ? bal[1] : ii == 2 ? bal[2] : bal[3];
-    const bool take = lane < 16 && row >= 0 && ((bi >> (16 * q)) & 0xFFFFull) != 0ull;
-    seg_append(take, row, eseg, &lcnt);
+    // per-row scalars of the lane's row slot c16 (all 4 lane copies load them)
+    float rs[2], re_[2], rcl[2];
+    int rq2[2];
+    kpp_v4i hi[2], lo[2];
+    if constexpr (NS > 0) {
+      kpp_v4i a[2][NS > 0 ? NS : 1];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int8_t* xr = Xq + (size_t)(row[h] >= 0 ? row[h] : 0) * dq + 16 * kb;
+#pragma unroll
+        for (int s4 = 0; s4 < NS; ++s4)
+          a[h][s4] = row[h] >= 0 ? *reinterpret_cast<const kpp_v4i*>(xr + 64 * s4)
+                                 : kpp_v4i{0, 0, 0, 0};
+        const int rr = row[h] >= 0 ? row[h] : 0;
+        rs[h] = srow[rr];
+        re_[h] = erow[rr];
+        rq2[h] = q2row[rr];
+        rcl[h] = closest[rr];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        hi[h] = kpp_v4i{0, 0, 0, 0};
+        lo[h] = kpp_v4i{0, 0, 0, 0};
+#pragma unroll
+        for (int s4 = 0; s4 < NS; ++s4) {
+          const kpp_v4i bh = *reinterpret_cast<const kpp_v4i*>(b1 + 64 * s4);
+          const kpp_v4i bl = *reinterpret_cast<const kpp_v4i*>(b2 + 64 * s4);
+          hi[h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[h][s4], bh, hi[h], 0, 0, 0);
+          lo[h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[h][s4], bl, lo[h], 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rr = row[h] >= 0 ? row[h] : 0;
+        rs[h] = srow[rr];
+        re_[h] = erow[rr];
+        rq2[h] = q2row[rr];
+        rcl[h] = closest[rr];
+        kpp_i8_dots(Xq, dq, row[h], cb, lane, hi[h], lo[h]);
+      }
+    }
+    (void)nsd;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned long long bal[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int src = 4 * kb + i;   // the row slot of result register i
+        const int rr = __shfl(row[h], src, 64);
+        const double s = (double)__shfl(rs[h], src, 64);
+        const double er = (double)__shfl(re_[h], src, 64);
+        const double q2 = (double)__shfl(rq2[h], src, 64);
+        const double cl = (double)__shfl(rcl[h], src, 64);
+        bool need = false;
+        if (jv && rr >= 0) {
+          const double A = s * s * q2;
+          const double dot = s * sc * ((double)hi[h][i] + (double)lo[h][i] * (1.0 / 254.0));
+          const double Dq = (A + cc2) - 2.0 * dot;
+          const double Dlb = Dq - 1e-13 * (A + cc2 + 2.0 * fabs(dot));
+          double lb = 0.0;
+          if (Dlb > 0.0) {
+            const double r = sqrt(Dlb) * (1.0 - 1e-15) - er - ec;
+            lb = r > 0.0 ? r * r * (1.0 - 1e-15) : 0.0;
+          }
+          need = !(lb > cl * lim_rel);
+        }
+        bal[i] = __ballot(need);
+      }
+      // row slot c16 (lanes < 16): rows 4 q + i live in lanes [16 q, 16 q + 16) of bal[i]
+      const int q = c16 >> 2, ii = c16 & 3;
+      const unsigned long long bi = ii == 0 ? bal[0] : ii == 1 ? bal[1] : ii == 2 ? bal[2] : bal[3];
+      const bool take = lane < 16 && row[h] >= 0 && ((bi >> (16 * q)) & 0xFFFFull) != 0ull;
+      seg_append(take, row[h], eseg, &lcnt);
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) ecount[blockIdx.x] = lcnt;
@@ -373,6 +433,12 @@ __global__ void __launch_bounds__(64) kmpp_dots_kernel(const int8_t* __restrict_
 }
 
 // ------------------------------------------------------- 3. exact pass
+// One lane per row (64 rows per wave pass), rows staged through LDS in
+// 32-feature tiles (8 lanes x 16 B per row, the next tile's loads in flight
+// during the current tile's FMAs); a row improved by trial j records D_ij
+// and its fixed-point improvement, summed per lane, per wave, then per block
+// (exact integers: any order) and STORED as delta_part[block][j] - one write
+// per block instead of one fp64 atomic per improved (row, trial).
 template <int TMAX>
 __global__ void __launch_bounds__(256) kmpp_exact_kernel(
     const float* __restrict__ X, long long ldx, int d, long long n, int t,
@@ -381,6 +447,7 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
     const int* __restrict__ ecount, uint16_t* __restrict__ mask_out, float* __restrict__ Dout,
     double* __restrict__ delta_part, long long R) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kKppStride];
+  __shared__ double dred[4][TMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* my = tile[wave];
   const int cnt = ecount[blockIdx.x];
@@ -388,23 +455,34 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
   const long long nb = (cnt + 63) / 64;
   const int ntiles = (d + kKppTile - 1) / kKppTile;
   const int lrow = lane >> 3, lchunk = lane & 7;
+  double dsum[TMAX];
+#pragma unroll
+  for (int j = 0; j < TMAX; ++j) dsum[j] = 0.0;
   for (long long b = wave; b < nb; b += 4) {
     const long long e = b * 64 + lane;
     const int row = e < cnt ? eseg[e] : -1;
+    int rq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rq[q] = __shfl(row, q * 8 + lrow, 64);
+    float4 v[8];
+    auto fetch = [&](int tix) {
+      const int f = tix * kKppTile + lchunk * 4;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rq[q] >= 0 && f < d) v[q] = *reinterpret_cast<const float4*>(X + (size_t)rq[q] * ldx + f);
+      }
+    };
     float acc[TMAX];
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) acc[j] = 0.0f;
+    fetch(0);
     for (int tix = 0; tix < ntiles; ++tix) {
       // stage: row slot q * 8 + (lane >> 3), 16-B chunk lane & 7
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int slot = q * 8 + lrow;
-        const int r = __shfl(row, slot, 64);
-        const int f = tix * kKppTile + lchunk * 4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r >= 0 && f < d) v = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + f);
-        *reinterpret_cast<float4*>(my + slot * kKppStride + lchunk * 4) = v;
-      }
+      for (int q = 0; q < 8; ++q)
+        *reinterpret_cast<float4*>(my + (q * 8 + lrow) * kKppStride + lchunk * 4) = v[q];
+      if (tix + 1 < ntiles) fetch(tix + 1);
       const int f0 = tix * kKppTile;
       const int fl = min(kKppTile, d - f0);
 #pragma unroll
@@ -432,19 +510,27 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
       const float cl = closest[row];
       const double wi = w ? w[row] : 1.0;
       const double qcl = kpp_q(cl, wi, scale);
-      const long long blk = (long long)row / R;
       uint32_t m = 0;
 #pragma unroll
       for (int j = 0; j < TMAX; ++j) {
         if (j < t && acc[j] < cl) {
           m |= 1u << j;
           Dout[(size_t)j * n + row] = acc[j];
-          const double dq = qcl - kpp_q(acc[j], wi, scale);
-          if (dq != 0.0) atomicAdd(delta_part + blk * t + j, dq);
+          dsum[j] += qcl - kpp_q(acc[j], wi, scale);
         }
       }
       mask_out[row] = (uint16_t)m;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < TMAX; ++j) {
+    const double s = wave_sum(dsum[j]);
+    if (lane == 0) dred[wave][j] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < t && threadIdx.x < TMAX) {
+    const int j = threadIdx.x;
+    delta_part[(long long)blockIdx.x * t + j] = (dred[0][j] + dred[1][j]) + (dred[2][j] + dred[3][j]);
   }
 }
 
@@ -597,11 +683,20 @@ int sq_kmpp_bound(const void* Xq, int dq, const void* srow, const void* erow, co
   if (n <= 0) return 0;
   if (t < 1 || t > 16 || (dq & 63) || dq < d || R <= 0 || G <= 0 || 32 * dq > 65536)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmpp_bound_kernel, dim3(G), dim3(256), (size_t)32 * dq, (hipStream_t)stream,
-                     (const int8_t*)Xq, dq, (const float*)srow, (const float*)erow,
-                     (const int*)xq2, (const float*)closest, (const int8_t*)candq,
-                     (const double*)cinfo, t, d, R, (const int*)surv, (const int*)scount,
-                     (int*)exact, (int*)ecount);
+#define LAUNCH(NS)                                                                              \
+  hipLaunchKernelGGL(kmpp_bound_kernel<NS>, dim3(G), dim3(256), (size_t)32 * dq,                \
+                     (hipStream_t)stream, (const int8_t*)Xq, dq, (const float*)srow,            \
+                     (const float*)erow, (const int*)xq2, (const float*)closest,                \
+                     (const int8_t*)candq, (const double*)cinfo, t, d, R, (const int*)surv,     \
+                     (const int*)scount, (int*)exact, (int*)ecount)
+  switch (dq / 64) {
+    case 1: LAUNCH(1); break;
+    case 2: LAUNCH(2); break;
+    case 3: LAUNCH(3); break;
+    case 4: LAUNCH(4); break;
+    default: LAUNCH(0); break;
+  }
+#undef LAUNCH
   return (int)hipGetLastError();
 }
 
