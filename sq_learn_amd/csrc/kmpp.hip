@@ -39,6 +39,7 @@
 namespace sq {
 
 constexpr int kKppTile = 32;          // fp32 features per staged tile (128 B of a row)
+constexpr int kKppInitGrid = 16384;   // workgroups of the first-centre pass
 constexpr int kKppStride = 36;        // LDS row stride in floats (16-B aligned, skewed banks)
 
 SQ_DEV double kpp_q(float v, double wi, double scale) { return rint((double)v * wi * scale); }
@@ -542,7 +543,9 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
     const double* __restrict__ block_tot, int G, long long R, long long n,
     const double* __restrict__ vals, const float* __restrict__ closest,
     const uint16_t* __restrict__ mask, const float* __restrict__ D, const int* __restrict__ best,
-    const double* __restrict__ w, double scale, long long* __restrict__ pos) {
+    const double* __restrict__ w, double scale, long long* __restrict__ pos,
+    const float* __restrict__ X, long long ldx, int d, float* __restrict__ cands,
+    long long* __restrict__ cand_ids, long long row_offset, long long n_global) {
   __shared__ double sc[256];
   __shared__ long long found;
   __shared__ double base;
@@ -612,6 +615,63 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
   if (hit >= 0) atomicMin(&found, hit);
   __syncthreads();
   if (tid == 0) pos[blockIdx.x] = found;
+  if (cands) {
+    // the candidate row itself (and its global id), clamped to the shard
+    const long long r = found < 0 ? 0 : (found > n - 1 ? n - 1 : found);
+    for (int f = tid; f < d; f += 256) cands[(size_t)blockIdx.x * d + f] = X[(size_t)r * ldx + f];
+    if (tid == 0) {
+      const long long g = r + row_offset;
+      cand_ids[blockIdx.x] = g < 0 ? 0 : (g > n_global - 1 ? n_global - 1 : g);
+    }
+  }
+}
+
+// ------------------------------------------- winner of one centre (1 rank)
+// Delta_j = sum over blocks of delta_part[b][j] (exact integers), the trial
+// potentials P - Delta_j, the first minimal one wins (torch.argmin's rule):
+// P, the block totals, centres[c], ids[c], the lazily applied winner and the
+// next centre's sampling values draws_next * P - one launch instead of the
+// host-side chain of small tensor ops.
+__global__ void __launch_bounds__(256) kmpp_finish_kernel(
+    const double* __restrict__ delta_part, int G, int t, double* __restrict__ block_tot,
+    double* __restrict__ P, const double* __restrict__ draws_next, double* __restrict__ vals,
+    const float* __restrict__ cands, const long long* __restrict__ cand_ids, int d,
+    float* __restrict__ centers, long long* __restrict__ ids, int c, int* __restrict__ best_out) {
+  __shared__ double red[16][16];
+  __shared__ double dj[16];
+  __shared__ int sb;
+  __shared__ double sP;
+  const int tid = threadIdx.x, j = tid & 15, g = tid >> 4;
+  double s = 0.0;
+  if (j < t)
+    for (int b = g; b < G; b += 16) s += delta_part[(size_t)b * t + j];
+  red[g][j] = s;
+  __syncthreads();
+  if (tid < t) {
+    double a = 0.0;
+    for (int q = 0; q < 16; ++q) a += red[q][tid];
+    dj[tid] = a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double p0 = *P;
+    int bj = 0;
+    double bv = p0 - dj[0];
+    for (int q = 1; q < t; ++q) {
+      const double v = p0 - dj[q];
+      if (v < bv) { bv = v; bj = q; }
+    }
+    sb = bj;
+    sP = bv;
+    *P = bv;
+    *best_out = bj;
+    ids[c] = cand_ids[bj];
+  }
+  __syncthreads();
+  const int bj = sb;
+  if (draws_next && tid < t) vals[tid] = draws_next[tid] * sP;
+  for (int b = tid; b < G; b += 256) block_tot[b] -= delta_part[(size_t)b * t + bj];
+  for (int f = tid; f < d; f += 256) centers[(size_t)c * d + f] = cands[(size_t)bj * d + f];
 }
 
 }  // namespace sq
@@ -625,8 +685,9 @@ static int kpp_grid(long long n) {
   return (int)(b < 2048 ? (b > 0 ? b : 1) : 2048);
 }
 
-// closest fp32 [n], nearest int32 [n], bmax fp64 [grid] with grid = sq_kmpp_grid(n)
-int sq_kmpp_grid(long long n) { return kpp_grid(n); }
+// closest fp32 [n], nearest int32 [n], bmax fp64 [sq_kmpp_grid(-1) = kKppInitGrid] for
+// sq_kmpp_init; sq_kmpp_grid(n >= 0): the workgroups of the per-block passes
+int sq_kmpp_grid(long long n) { return n < 0 ? kKppInitGrid : kpp_grid(n); }
 
 // Xq (nullable) int8 [n][dq] (dq = d rounded up to 64), srow / erow fp32 [n], q2row int32 [n]
 int sq_kmpp_init(const void* X, long long ldx, int d, long long n, const void* c0, const void* w,
@@ -634,7 +695,11 @@ int sq_kmpp_init(const void* X, long long ldx, int d, long long n, const void* c
                  void* erow, void* q2row, void* stream) {
   if (n <= 0) return 0;
   if (d <= 0 || ldx < d || (Xq && (dq < d || (dq & 63)))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmpp_init_kernel, dim3(kpp_grid(n)), dim3(256), 0, (hipStream_t)stream,
+  // one wave per row: enough waves in flight to cover the row loads' latency
+  // (bmax holds kKppInitGrid entries; the caller takes their max)
+  const long long gb = (n + 3) / 4;
+  const int grid = (int)(gb < kKppInitGrid ? gb : kKppInitGrid);
+  hipLaunchKernelGGL(kmpp_init_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      (const float*)X, ldx, d, n, (const float*)c0, (const double*)w,
                      (float*)closest, (int*)nearest, (double*)bmax, (int8_t*)Xq, dq,
                      (float*)srow, (float*)erow, (int*)q2row);
@@ -729,14 +794,31 @@ int sq_kmpp_exact(const void* X, long long ldx, int d, long long n, int t, const
   return (int)hipGetLastError();
 }
 
+// cands (nullable): also copy the picked rows (fp32 [t][d]) and their global ids (int64 [t])
 int sq_kmpp_pick(const void* block_tot, int G, long long R, long long n, const void* vals, int t,
                  const void* closest, const void* mask, const void* D, const void* best,
-                 const void* w, double scale, void* pos, void* stream) {
-  if (t < 1 || G < 1 || n <= 0) return (int)hipErrorInvalidValue;
+                 const void* w, double scale, void* pos, const void* X, long long ldx, int d,
+                 void* cands, void* cand_ids, long long row_offset, long long n_global,
+                 void* stream) {
+  if (t < 1 || G < 1 || n <= 0 || (cands && (!X || !cand_ids || d < 1 || ldx < d)))
+    return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmpp_pick_kernel, dim3(t), dim3(256), 0, (hipStream_t)stream,
                      (const double*)block_tot, G, R, n, (const double*)vals,
                      (const float*)closest, (const uint16_t*)mask, (const float*)D,
-                     (const int*)best, (const double*)w, scale, (long long*)pos);
+                     (const int*)best, (const double*)w, scale, (long long*)pos, (const float*)X,
+                     ldx, d, (float*)cands, (long long*)cand_ids, row_offset, n_global);
+  return (int)hipGetLastError();
+}
+
+int sq_kmpp_finish(const void* delta_part, int G, int t, void* block_tot, void* P,
+                   const void* draws_next, void* vals, const void* cands, const void* cand_ids,
+                   int d, void* centers, void* ids, int c, void* best_out, void* stream) {
+  if (t < 1 || t > 16 || G < 1 || d < 1 || c < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmpp_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                     (const double*)delta_part, G, t, (double*)block_tot, (double*)P,
+                     (const double*)draws_next, (double*)vals, (const float*)cands,
+                     (const long long*)cand_ids, d, (float*)centers, (long long*)ids, c,
+                     (int*)best_out);
   return (int)hipGetLastError();
 }
 

@@ -124,7 +124,11 @@ __attribute__((weak)) int sq_kmpp_exact(const void*, long long, int, long long, 
                                         const void*, void*, void*, void*, long long, int, void*);
 __attribute__((weak)) int sq_kmpp_pick(const void*, int, long long, long long, const void*, int,
                                        const void*, const void*, const void*, const void*,
-                                       const void*, double, void*, void*);
+                                       const void*, double, void*, const void*, long long, int,
+                                       void*, void*, long long, long long, void*);
+__attribute__((weak)) int sq_kmpp_finish(const void*, int, int, void*, void*, const void*, void*,
+                                         const void*, const void*, int, void*, void*, int, void*,
+                                         void*);
 // estep_f32.hip
 __attribute__((weak)) int sq_estep_f32(const void*, const void*, const void*, void*, void*, void*,
                                        void*, void*, int, void*, long long, int, int, double,
@@ -502,13 +506,24 @@ static PyObject* py_kmpp_dots(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_kmpp_pick(PyObject*, PyObject* a) {
-  unsigned long long bt, v, cl, m, D, b, w, pos, st; int G, t; long long R, n; double scale;
-  if (!PyArg_ParseTuple(a, "KiLLKiKKKKKdKK", &bt, &G, &R, &n, &v, &t, &cl, &m, &D, &b, &w, &scale,
-                        &pos, &st))
+  unsigned long long bt, v, cl, m, D, b, w, pos, X, cd, ci, st; int G, t, d;
+  long long R, n, ldx, roff, ng; double scale;
+  if (!PyArg_ParseTuple(a, "KiLLKiKKKKKdKKLiKKLLK", &bt, &G, &R, &n, &v, &t, &cl, &m, &D, &b, &w,
+                        &scale, &pos, &X, &ldx, &d, &cd, &ci, &roff, &ng, &st))
     return nullptr;
   CHECK(sq_kmpp_pick)
   return ret(sq_kmpp_pick(P(bt), G, R, n, P(v), t, P(cl), P(m), P(D), P(b), P(w), scale, P(pos),
-                          P(st)));
+                          P(X), ldx, d, P(cd), P(ci), roff, ng, P(st)));
+}
+
+static PyObject* py_kmpp_finish(PyObject*, PyObject* a) {
+  unsigned long long dp, bt, Pp, dn, v, cd, ci, C, ids, bo, st; int G, t, d, c;
+  if (!PyArg_ParseTuple(a, "KiiKKKKKKiKKiKK", &dp, &G, &t, &bt, &Pp, &dn, &v, &cd, &ci, &d, &C,
+                        &ids, &c, &bo, &st))
+    return nullptr;
+  CHECK(sq_kmpp_finish)
+  return ret(sq_kmpp_finish(P(dp), G, t, P(bt), P(Pp), P(dn), P(v), P(cd), P(ci), d, P(C), P(ids),
+                            c, P(bo), P(st)));
 }
 
 static PyObject* py_sum_f32(PyObject*, PyObject* a) {
@@ -664,6 +679,7 @@ static PyMethodDef methods[] = {
     {"kmpp_bound", py_kmpp_bound, METH_VARARGS, "k-means++ certified int8 bound"},
     {"kmpp_exact", py_kmpp_exact, METH_VARARGS, "k-means++ exact fp32 trial distances"},
     {"kmpp_dots", py_kmpp_dots, METH_VARARGS, "int8 MFMA dots of the k-means++ bound (test hook)"},
+    {"kmpp_finish", py_kmpp_finish, METH_VARARGS, "k-means++ winner of one centre (one rank)"},
     {"kmpp_pick", py_kmpp_pick, METH_VARARGS, "k-means++ two-level potential sampling"},
     {"rows_f64", py_rows_f64, METH_VARARGS, "exact fp64 E-step over a row list (fp64 MFMA)"},
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},

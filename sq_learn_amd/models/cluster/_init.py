@@ -147,6 +147,21 @@ def _kmeans_plusplus_native(data: Data, k, rs, t, w, prune, stats=None):
     g = torch.stack(comm.all_gather(ts))                                  # [W, 2]
     totals, sizes = g[:, 0].contiguous(), g[:, 1].contiguous()
     W = comm.world_size
+    if W == 1 and data.n_local > 0 and X.dtype == torch.float32:
+        # one rank: pick (+ row copy), trial pass, one finishing launch per
+        # centre - no host-side tensor chain
+        Pd = P.clone()
+        vals = (draws[0] * Pd) if k > 1 else torch.zeros(t, dtype=torch.float64, device=dev)
+        cands = torch.empty((t, data.d), dtype=torch.float32, device=dev)
+        cand_ids = torch.empty(t, dtype=torch.int64, device=dev)
+        for c in range(1, k):
+            state.pick(vals, cands, cand_ids, data.row_offset, n)
+            state.trials(cands, centers, c, reduce=False)
+            state.finish(Pd, draws[c] if c < k - 1 else None, vals, cands, cand_ids, centers, ids,
+                         c)
+            if stats is not None:
+                stats.append(state.list_counts())
+        return centers, ids.cpu().numpy()
     zero = torch.zeros(1, dtype=torch.float64, device=dev)
     for c in range(1, k):
         prefix = torch.cat([zero, torch.cumsum(totals, 0)])

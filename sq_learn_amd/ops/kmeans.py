@@ -834,7 +834,7 @@ class KmppState:
         """closest / nearest for the first centre (and, pruned, the int8 row
         copy in the same pass over X); returns the local max of w * closest
         (device fp64 [1]) for the global fixed-point scale."""
-        bmax = torch.zeros(self.m.kmpp_grid(max(self.n, 1)), dtype=torch.float64, device=self.dev)
+        bmax = torch.zeros(self.m.kmpp_grid(-1), dtype=torch.float64, device=self.dev)
         if self.n:
             c0 = c0.to(torch.float32).contiguous()
             q = self.prune
@@ -861,24 +861,32 @@ class KmppState:
                                          self.st), "kmpp_block_totals")
         return self.block_tot.sum().reshape(1)
 
-    def pick(self, vals):
+    def pick(self, vals, cands=None, cand_ids=None, row_offset=0, n_global=None):
         """Local rows of the potential values ``vals`` (device fp64 [t]):
-        first row whose inclusive prefix reaches each value."""
+        first row whose inclusive prefix reaches each value.  With ``cands``
+        (fp32 [t, d]) / ``cand_ids`` (int64 [t]) the same launch also copies
+        the rows and writes their global ids (clamped to the shard)."""
         t = vals.numel()
         if self.n == 0:
             return torch.zeros(t, dtype=torch.int64, device=self.dev)
         assert t <= self.pos.numel()
         vals = vals.to(torch.float64).contiguous()
         prev = 1 - self.cur
+        if cands is not None:
+            assert cands.dtype == torch.float32 and cands.is_contiguous()
+            assert tuple(cands.shape) == (t, self.d) and cand_ids.dtype == torch.int64
         _rc(self.m.kmpp_pick(self.block_tot.data_ptr(), self.G, self.R, self.n, vals.data_ptr(), t,
                              self.closest.data_ptr(), self.mask[prev].data_ptr(),
                              self.D[prev].data_ptr(),
                              0 if self.best is None else self.best.data_ptr(),
                              0 if self.w is None else self.w.data_ptr(), self.scale,
-                             self.pos.data_ptr(), self.st), "kmpp_pick")
+                             self.pos.data_ptr(), self.X.data_ptr(), self.ldx, self.d,
+                             0 if cands is None else cands.data_ptr(),
+                             0 if cand_ids is None else cand_ids.data_ptr(), int(row_offset),
+                             int(self.n if n_global is None else n_global), self.st), "kmpp_pick")
         return self.pos[:t].clone()
 
-    def trials(self, cand, centers, c):
+    def trials(self, cand, centers, c, reduce=True):
         """Trial pass for the candidates ``cand`` [t, d] against the ``c``
         centres chosen so far (``centers[:c]``): returns Delta (device fp64
         [t]), the fixed-point improvement of each trial over this shard."""
@@ -912,7 +920,7 @@ class KmppState:
                              self.scale, self.exact.data_ptr(), self.ecount.data_ptr(),
                              self.mask[cur].data_ptr(), self.D[cur].data_ptr(),
                              self.delta.data_ptr(), self.R, self.G, st), "kmpp_exact")
-        return self.delta.sum(0)
+        return self.delta.sum(0) if reduce else None
 
     def apply(self, best, c):
         """The winning trial (device int64 scalar) of centre ``c``: block
@@ -920,6 +928,22 @@ class KmppState:
         screen / pick."""
         self.block_tot -= self.delta.index_select(1, best.reshape(1))[:, 0]
         self.best = best.reshape(1).to(torch.int32)
+        self.c_last = int(c)
+        self.cur ^= 1
+
+    def finish(self, P, draws_next, vals, cands, cand_ids, centers, ids, c):
+        """Single-rank winner of centre ``c`` in one launch: trial potentials
+        P - Delta_j (exact integers), the first minimum wins; updates ``P``
+        (fp64 [1]), the block totals, ``centers[c]``, ``ids[c]``, the lazily
+        applied winner and ``vals`` = draws_next * P (the next centre's
+        sampling values; ``draws_next`` None: last centre)."""
+        if self.best is None:
+            self.best = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        _rc(self.m.kmpp_finish(self.delta.data_ptr(), self.G, self.t, self.block_tot.data_ptr(),
+                               P.data_ptr(), 0 if draws_next is None else draws_next.data_ptr(),
+                               vals.data_ptr(), cands.data_ptr(), cand_ids.data_ptr(), self.d,
+                               centers.data_ptr(), ids.data_ptr(), int(c), self.best.data_ptr(),
+                               self.st), "kmpp_finish")
         self.c_last = int(c)
         self.cur ^= 1
 
