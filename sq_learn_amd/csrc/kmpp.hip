@@ -40,17 +40,19 @@ namespace sq {
 
 constexpr int kKppTile = 32;          // fp32 features per staged tile (128 B of a row)
 constexpr int kKppInitGrid = 16384;   // workgroups of the first-centre pass
+constexpr int kKppCandLds = 4096;     // fp32 trial features staged in LDS by the exact pass
 constexpr int kKppStride = 36;        // LDS row stride in floats (16-B aligned, skewed banks)
 
 SQ_DEV double kpp_q(float v, double wi, double scale) { return rint((double)v * wi * scale); }
 
 // ------------------------------------- first centre (+ the int8 copy)
-// One wave per row (coalesced 64-lane reads): closest_i = |x_i - c0|^2
-// (fp32, fixed wave-tree order), nearest_i = 0, the per-block max of
-// w_i closest_i (the caller turns the global max into the fixed-point
-// scale); with Xq: the row's int8 copy in the same pass - q = rint(x / s)
-// (s = max|x| / 127), e = |x - s q| rounded up, q2 = |q|^2 (exact int),
-// features d .. dq-1 zero.
+// 16 lanes per row (4 rows per wave; float4 loads, 256 contiguous bytes per
+// row and instruction): closest_i = |x_i - c0|^2 (fp32, fixed lane-tree
+// order), nearest_i = 0, the per-block max of w_i closest_i (the caller
+// turns the global max into the fixed-point scale); with Xq: the row's int8
+// copy in the same pass - q = rint(x / s) (s = max|x| / 127), e = |x - s q|
+// rounded up, q2 = |q|^2 (exact int), features d .. dq-1 zero.  (d, ldx
+// multiples of 4.)
 __global__ void __launch_bounds__(256) kmpp_init_kernel(
     const float* __restrict__ X, long long ldx, int d, long long n, const float* __restrict__ c0,
     const double* __restrict__ w, float* __restrict__ closest, int* __restrict__ nearest,
@@ -58,53 +60,74 @@ __global__ void __launch_bounds__(256) kmpp_init_kernel(
     float* __restrict__ erow, int* __restrict__ q2row) {
   __shared__ double red[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long w0 = (long long)blockIdx.x * 4 + wave;
-  const long long nw = (long long)gridDim.x * 4;
+  const int sub = lane & 15;
+  const long long i0 = ((long long)blockIdx.x * 4 + wave) * 4 + (lane >> 4);
+  const long long stride = (long long)gridDim.x * 16;
   double m = 0.0;
-  for (long long i = w0; i < n; i += nw) {
-    const float* x = X + i * ldx;
+  for (long long ib = i0 - (lane >> 4); ib < n; ib += stride) {   // wave-uniform bound
+    const long long i = ib + (lane >> 4);
+    const bool ok = i < n;
+    const float* x = X + (ok ? i : 0) * ldx;
     float acc = 0.0f, mx = 0.0f;
-    for (int f = lane; f < d; f += 64) {
-      const float v = x[f];
-      const float e = v - c0[f];
+    for (int f = 4 * sub; f < d; f += 64) {
+      const float4 v = *reinterpret_cast<const float4*>(x + f);
+      const float4 c = *reinterpret_cast<const float4*>(c0 + f);
+      float e = v.x - c.x;
       acc = fmaf(e, e, acc);
-      mx = fmaxf(mx, fabsf(v));
+      e = v.y - c.y;
+      acc = fmaf(e, e, acc);
+      e = v.z - c.z;
+      acc = fmaf(e, e, acc);
+      e = v.w - c.w;
+      acc = fmaf(e, e, acc);
+      mx = fmaxf(fmaxf(mx, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = 8; o > 0; o >>= 1) {
       acc += __shfl_xor(acc, o, 64);
       mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     }
-    if (lane == 0) {
+    if (ok && sub == 0) {
       closest[i] = acc;
       nearest[i] = 0;
     }
-    m = fmax(m, (double)acc * (w ? w[i] : 1.0));
+    if (ok) m = fmax(m, (double)acc * (w ? w[i] : 1.0));
     if (Xq) {
       const float s = mx > 0.0f ? mx / 127.0f : 1.0f;
       double e2 = 0.0;
       int q2 = 0;
-      for (int f = lane; f < dq; f += 64) {
-        int q = 0;
-        if (f < d) {
-          const float v = x[f];
-          q = (int)fminf(fmaxf(rintf(v / s), -127.0f), 127.0f);
-          const double r = (double)v - (double)s * (double)q;
-          e2 += r * r;
-          q2 += q * q;
-        }
-        Xq[i * dq + f] = (int8_t)q;
-      }
-      e2 = wave_sum(e2);
+      for (int f = 4 * sub; f < dq; f += 64) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (f < d) v = *reinterpret_cast<const float4*>(x + f);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        uint32_t pk = 0;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) q2 += __shfl_xor(q2, o, 64);
-      if (lane == 0) {
+        for (int u = 0; u < 4; ++u) {
+          int q = 0;
+          if (f + u < d) {
+            q = (int)fminf(fmaxf(rintf(vv[u] / s), -127.0f), 127.0f);
+            const double r = (double)vv[u] - (double)s * (double)q;
+            e2 += r * r;
+            q2 += q * q;
+          }
+          pk |= ((uint32_t)(uint8_t)(int8_t)q) << (8 * u);
+        }
+        if (ok) *reinterpret_cast<uint32_t*>(Xq + i * dq + f) = pk;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        e2 += __shfl_xor(e2, o, 64);
+        q2 += __shfl_xor(q2, o, 64);
+      }
+      if (ok && sub == 0) {
         srow[i] = s;
         erow[i] = (float)(sqrt(e2) * (1.0 + 1e-6)) * 1.000001f;
         q2row[i] = q2;
       }
     }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
   if (lane == 0) red[wave] = m;
   __syncthreads();
   if (threadIdx.x == 0) bmax[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
@@ -449,8 +472,16 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
     double* __restrict__ delta_part, long long R) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kKppStride];
   __shared__ double dred[4][TMAX];
+  // the trials, staged once per block when they fit (read as LDS broadcasts;
+  // scalar-cache loads of them stalled every 4-feature step)
+  __shared__ __attribute__((aligned(16))) float cs[kKppCandLds];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* my = tile[wave];
+  const bool cl_lds = t * d <= kKppCandLds;
+  if (cl_lds)
+    for (int e = threadIdx.x; e < t * d; e += 256) cs[e] = cand[e];
+  const float* cb = cl_lds ? cs : cand;
+  __syncthreads();
   const int cnt = ecount[blockIdx.x];
   const int* eseg = exact + (long long)blockIdx.x * R;
   const long long nb = (cnt + 63) / 64;
@@ -494,7 +525,8 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
 #pragma unroll
         for (int j = 0; j < TMAX; ++j) {
           if (j < t) {
-            const float* c = cand + (size_t)j * d + f;
+            const float4 c4v = *reinterpret_cast<const float4*>(cb + (size_t)j * d + f);
+            const float c[4] = {c4v.x, c4v.y, c4v.z, c4v.w};
             float ev = x4.x - c[0];
             acc[j] = fmaf(ev, ev, acc[j]);
             ev = x4.y - c[1];
@@ -632,24 +664,26 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
 // P, the block totals, centres[c], ids[c], the lazily applied winner and the
 // next centre's sampling values draws_next * P - one launch instead of the
 // host-side chain of small tensor ops.
-__global__ void __launch_bounds__(256) kmpp_finish_kernel(
+__global__ void __launch_bounds__(1024) kmpp_finish_kernel(
     const double* __restrict__ delta_part, int G, int t, double* __restrict__ block_tot,
     double* __restrict__ P, const double* __restrict__ draws_next, double* __restrict__ vals,
     const float* __restrict__ cands, const long long* __restrict__ cand_ids, int d,
     float* __restrict__ centers, long long* __restrict__ ids, int c, int* __restrict__ best_out) {
-  __shared__ double red[16][16];
+  __shared__ double red[64][16];
   __shared__ double dj[16];
   __shared__ int sb;
   __shared__ double sP;
   const int tid = threadIdx.x, j = tid & 15, g = tid >> 4;
   double s = 0.0;
-  if (j < t)
-    for (int b = g; b < G; b += 16) s += delta_part[(size_t)b * t + j];
+  if (j < t) {
+#pragma unroll 8
+    for (int b = g; b < G; b += 64) s += delta_part[(size_t)b * t + j];
+  }
   red[g][j] = s;
   __syncthreads();
   if (tid < t) {
     double a = 0.0;
-    for (int q = 0; q < 16; ++q) a += red[q][tid];
+    for (int q = 0; q < 64; ++q) a += red[q][tid];
     dj[tid] = a;
   }
   __syncthreads();
@@ -670,8 +704,8 @@ __global__ void __launch_bounds__(256) kmpp_finish_kernel(
   __syncthreads();
   const int bj = sb;
   if (draws_next && tid < t) vals[tid] = draws_next[tid] * sP;
-  for (int b = tid; b < G; b += 256) block_tot[b] -= delta_part[(size_t)b * t + bj];
-  for (int f = tid; f < d; f += 256) centers[(size_t)c * d + f] = cands[(size_t)bj * d + f];
+  for (int b = tid; b < G; b += 1024) block_tot[b] -= delta_part[(size_t)b * t + bj];
+  for (int f = tid; f < d; f += 1024) centers[(size_t)c * d + f] = cands[(size_t)bj * d + f];
 }
 
 }  // namespace sq
@@ -694,10 +728,11 @@ int sq_kmpp_init(const void* X, long long ldx, int d, long long n, const void* c
                  void* closest, void* nearest, void* bmax, void* Xq, int dq, void* srow,
                  void* erow, void* q2row, void* stream) {
   if (n <= 0) return 0;
-  if (d <= 0 || ldx < d || (Xq && (dq < d || (dq & 63)))) return (int)hipErrorInvalidValue;
-  // one wave per row: enough waves in flight to cover the row loads' latency
+  if (d <= 0 || (d & 3) || ldx < d || (ldx & 3) || (Xq && (dq < d || (dq & 63))))
+    return (int)hipErrorInvalidValue;
+  // 16 lanes per row: enough waves in flight to cover the row loads' latency
   // (bmax holds kKppInitGrid entries; the caller takes their max)
-  const long long gb = (n + 3) / 4;
+  const long long gb = (n + 15) / 16;   // 16 rows per workgroup pass
   const int grid = (int)(gb < kKppInitGrid ? gb : kKppInitGrid);
   hipLaunchKernelGGL(kmpp_init_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      (const float*)X, ldx, d, n, (const float*)c0, (const double*)w,
@@ -814,7 +849,7 @@ int sq_kmpp_finish(const void* delta_part, int G, int t, void* block_tot, void* 
                    const void* draws_next, void* vals, const void* cands, const void* cand_ids,
                    int d, void* centers, void* ids, int c, void* best_out, void* stream) {
   if (t < 1 || t > 16 || G < 1 || d < 1 || c < 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmpp_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(kmpp_finish_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
                      (const double*)delta_part, G, t, (double*)block_tot, (double*)P,
                      (const double*)draws_next, (double*)vals, (const float*)cands,
                      (const long long*)cand_ids, d, (float*)centers, (long long*)ids, c,
