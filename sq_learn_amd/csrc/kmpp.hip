@@ -40,7 +40,6 @@ namespace sq {
 
 constexpr int kKppTile = 32;          // fp32 features per staged tile (128 B of a row)
 constexpr int kKppInitGrid = 16384;   // workgroups of the first-centre pass
-constexpr int kKppCandLds = 4096;     // fp32 trial features staged in LDS by the exact pass
 constexpr int kKppStride = 36;        // LDS row stride in floats (16-B aligned, skewed banks)
 
 SQ_DEV double kpp_q(float v, double wi, double scale) { return rint((double)v * wi * scale); }
@@ -472,16 +471,8 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
     double* __restrict__ delta_part, long long R) {
   __shared__ __attribute__((aligned(16))) float tile[4][64 * kKppStride];
   __shared__ double dred[4][TMAX];
-  // the trials, staged once per block when they fit (read as LDS broadcasts;
-  // scalar-cache loads of them stalled every 4-feature step)
-  __shared__ __attribute__((aligned(16))) float cs[kKppCandLds];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* my = tile[wave];
-  const bool cl_lds = t * d <= kKppCandLds;
-  if (cl_lds)
-    for (int e = threadIdx.x; e < t * d; e += 256) cs[e] = cand[e];
-  const float* cb = cl_lds ? cs : cand;
-  __syncthreads();
   const int cnt = ecount[blockIdx.x];
   const int* eseg = exact + (long long)blockIdx.x * R;
   const long long nb = (cnt + 63) / 64;
@@ -525,8 +516,7 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
 #pragma unroll
         for (int j = 0; j < TMAX; ++j) {
           if (j < t) {
-            const float4 c4v = *reinterpret_cast<const float4*>(cb + (size_t)j * d + f);
-            const float c[4] = {c4v.x, c4v.y, c4v.z, c4v.w};
+            const float* c = cand + (size_t)j * d + f;   // wave-uniform: scalar loads
             float ev = x4.x - c[0];
             acc[j] = fmaf(ev, ev, acc[j]);
             ev = x4.y - c[1];
