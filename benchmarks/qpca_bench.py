@@ -2,10 +2,13 @@
 fp32, 1 GPU): wall-clock of the second (warm) fit.
 python benchmarks/qpca_bench.py [--n N --d D --bf16 --lowrank --solver full|randomized]"""
 import argparse
+import os
+import sys
 import time
 
 import torch
 
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..")))
 from sq_learn_amd.models.decomposition import QPCA
 from sq_learn_amd.parallel.comm import Comm
 from sq_learn_amd.parallel.sharding import ShardedArray
@@ -18,6 +21,7 @@ def main():
     ap.add_argument("--solver", default="full")
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--true-tomography", action="store_true")
     ap.add_argument("--lowrank", action="store_true",
                     help="BASELINE config 2 data: low rank (32) + tail, as bench.py")
     a = ap.parse_args()
@@ -38,9 +42,14 @@ def main():
         t0 = time.perf_counter()
         q = QPCA(n_components=16, svd_solver=a.solver, random_state=0, device=dev,
                  quantum_truncated=a.solver != "full")
-        q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True)
+        q.fit(sa, eps=1e-3, theta_major=theta, delta=0.1, estimate_all=True,
+              true_tomography=a.true_tomography)
         torch.cuda.synchronize()
         print(rep, f"qPCA {a.solver} fit {time.perf_counter() - t0:.3f} s", flush=True)
+        ph = getattr(q, "fit_phases_", None)
+        if ph:
+            print("  phases (s):", {k: round(v, 4) for k, v in ph.items()},
+                  "sum", round(sum(ph.values()), 4), flush=True)
 
 
 if __name__ == "__main__":

@@ -43,13 +43,16 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--marker", default="estep_kernel")
     ap.add_argument("--last", type=int, default=5)
+    ap.add_argument("--first", type=int, default=None,
+                    help="take --last intervals starting at this one (default: the last ones)")
     a = ap.parse_args()
     rows = load(a.dir)
     marks = [i for i, r in enumerate(rows) if a.marker in r[2]]
     if len(marks) < 2:
         raise SystemExit("not enough marker kernels")
     print("| interval | wall us | busy us | idle us | launches |\n|---|---|---|---|---|")
-    ivs = list(zip(marks[:-1], marks[1:]))[-a.last:]
+    allv = list(zip(marks[:-1], marks[1:]))
+    ivs = allv[-a.last:] if a.first is None else allv[a.first:a.first + a.last]
     for n, (i, j) in enumerate(ivs):
         seg = rows[i:j]
         wall = (rows[j][0] - rows[i][0]) / 1e3

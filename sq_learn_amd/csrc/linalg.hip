@@ -64,7 +64,8 @@ template <typename T, int LPR>
 __global__ void __launch_bounds__(256) mu_sums_kernel(
     const T* __restrict__ X, long long ldx, int col0, int d_total, const float* __restrict__ qs,
     int nq, float* __restrict__ rowmax, float* __restrict__ part, float* __restrict__ rowacc,
-    int final, long long n, int d, long long rows_per_wg, const float* __restrict__ mean) {
+    int final, long long n, int d, long long rows_per_wg, const float* __restrict__ mean,
+    float qstep) {
   constexpr int RPW = 64 / LPR;              // rows per wave step
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -100,6 +101,16 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
     for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(v[e] - mu8[e]) : 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) lg[e] = __builtin_amdgcn_logf(v[e]);   // log2, -inf at 0
+    // qstep > 0: q_i = i qstep - one exp2 per element, then |a|^(i qstep) by
+    // successive products (<= MUQ roundings, ~1e-6 relative)
+    float tb[8], cur[8];
+    if (qstep > 0.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        tb[e] = __builtin_amdgcn_exp2f(qstep * lg[e]);
+        cur[e] = tb[e];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < MUQ; ++i) {
       if (i < nq) {
@@ -107,8 +118,17 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           // |a|^0 counts nonzeros; exp2(q * -inf) = 0 for q > 0
-          const float pw = q[i] == 0.f ? (v[e] != 0.f ? 1.f : 0.f)
-                                        : __builtin_amdgcn_exp2f(q[i] * lg[e]);
+          float pw;
+          if (qstep > 0.f) {
+            if (i == 0) {
+              pw = v[e] != 0.f ? 1.f : 0.f;
+            } else {
+              if (i > 1) cur[e] *= tb[e];
+              pw = cur[e];
+            }
+          } else {
+            pw = q[i] == 0.f ? (v[e] != 0.f ? 1.f : 0.f) : __builtin_amdgcn_exp2f(q[i] * lg[e]);
+          }
           cs[i][e] += pw;
           rs += pw;
         }
@@ -133,11 +153,16 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
     }
   }
   // column sums: reduce the 4*RPW row slots sharing a column group in LDS
-  for (int i = 0; i < nq; ++i) {
+  // (a constant trip count with unconditional barriers, so the loop unrolls:
+  // a runtime-indexed cs would live in scratch)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = cs[i][e];
+  for (int i = 0; i < MUQ; ++i) {
+    if (i < nq) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[tid * 8 + e] = cs[i][e];
+    }
     __syncthreads();
-    if (sg == 0) {               // threads 0..LPR-1: one per column group
+    if (i < nq && sg == 0) {     // threads 0..LPR-1: one per column group
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       for (int s2 = 0; s2 < 4 * RPW; ++s2) {
         const int t = s2 * LPR + vl;
@@ -198,15 +223,50 @@ __global__ void __launch_bounds__(256) row_norms_kernel(const T* __restrict__ X,
   if (lane == 0) out[r] = s;
 }
 
+
+// Column sums and sums of squares in fp64 (global_mean_var): one thread per
+// column (a wave reads 64 consecutive features of a row), 8 rows in flight
+// per thread; per-workgroup partials part[b][2 d] over the fixed row
+// partition, summed in a fixed order by the caller (deterministic).
+template <typename T>
+__global__ void __launch_bounds__(256) col_moments_kernel(const T* __restrict__ X, long long ldx,
+                                                          long long n, int d, long long rpw,
+                                                          double* __restrict__ part) {
+  const long long r0 = (long long)blockIdx.x * rpw;
+  const long long r1 = min(n, r0 + rpw);
+  for (int c = threadIdx.x; c < d; c += 256) {
+    double s = 0.0, ss = 0.0;
+    long long r = r0;
+    for (; r + 8 <= r1; r += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld1<T>(X, (size_t)(r + u) * ldx + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += (double)v[u];
+        ss = fma((double)v[u], (double)v[u], ss);
+      }
+    }
+    for (; r < r1; ++r) {
+      const double v = (double)ld1<T>(X, (size_t)r * ldx + c);
+      s += v;
+      ss = fma(v, v, ss);
+    }
+    part[(size_t)blockIdx.x * 2 * d + c] = s;
+    part[(size_t)blockIdx.x * 2 * d + d + c] = ss;
+  }
+}
+
 }  // namespace sq
 
 using namespace sq;
 
 extern "C" {
 
+// qstep > 0: the exponents are exactly 0, qstep, 2 qstep, ... (qs[i] = i qstep)
 int sq_mu_sums(const void* X, int xdtype, long long ldx, const void* qs, int nq, void* rowmax,
                void* colsum, void* part, int part_wgs, void* rowacc, long long n, int d,
-               const void* mean, void* stream) {
+               const void* mean, float qstep, void* stream) {
   if (n <= 0) return 0;
   if (nq > MUQ || part_wgs < 1 || ldx < d || (d > 512 && !rowacc)) return (int)hipErrorInvalidValue;
   long long wgs = min((long long)part_wgs, max(1LL, (n + 255) / 256));
@@ -223,7 +283,7 @@ int sq_mu_sums(const void* X, int xdtype, long long ldx, const void* qs, int nq,
   case L:                                                                                      \
     hipLaunchKernelGGL((mu_sums_kernel<T, L>), dim3((unsigned)wgs), dim3(256), 0, st,          \
                        (const T*)X, ldx, col0, d, (const float*)qs, nq, (float*)rowmax,        \
-                       (float*)part, racc, final, n, dc, rpw, (const float*)mean);             \
+                       (float*)part, racc, final, n, dc, rpw, (const float*)mean, qstep);      \
     break;
     if (xdtype == 0) {
       switch (lpr) { MU_CASE(float, 1) MU_CASE(float, 2) MU_CASE(float, 4) MU_CASE(float, 8)
@@ -240,6 +300,27 @@ int sq_mu_sums(const void* X, int xdtype, long long ldx, const void* qs, int nq,
   }
   hipLaunchKernelGGL(mu_colsum_kernel, dim3((unsigned)((nq * d + 255) / 256)), dim3(256), 0, st,
                      (const float*)part, (int)wgs, nq, d, (float*)colsum);
+  return (int)hipGetLastError();
+}
+
+// part fp64 [part_wgs][2 d], zero-initialised by the caller (the first wgs <= part_wgs rows
+// are written)
+int sq_col_moments(const void* X, int xdtype, long long ldx, long long n, int d, void* part,
+                   int part_wgs, void* stream) {
+  if (n <= 0 || d <= 0) return 0;
+  if (part_wgs < 1 || ldx < d) return (int)hipErrorInvalidValue;
+  long long wgs = min((long long)part_wgs, max(1LL, (n + 255) / 256));
+  const long long rpw = (n + wgs - 1) / wgs;
+  wgs = (n + rpw - 1) / rpw;
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == 0)
+    hipLaunchKernelGGL(col_moments_kernel<float>, dim3((unsigned)wgs), dim3(256), 0, st,
+                       (const float*)X, ldx, n, d, rpw, (double*)part);
+  else if (xdtype == 2)
+    hipLaunchKernelGGL(col_moments_kernel<uint16_t>, dim3((unsigned)wgs), dim3(256), 0, st,
+                       (const uint16_t*)X, ldx, n, d, rpw, (double*)part);
+  else
+    return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

@@ -149,8 +149,10 @@ __attribute__((weak)) int sq_ipe_estep(const void* G, const void* xn, const void
                  long long m, int k, long long ldG, double eps, int Q, unsigned k0, unsigned k1,
                  unsigned s0, unsigned s1, long long row_offset, void* stream);
 // linalg.hip
+__attribute__((weak)) int sq_col_moments(const void*, int, long long, long long, int, void*, int,
+                                         void*);
 __attribute__((weak)) int sq_mu_sums(const void*, int, long long, const void*, int, void*, void*,
-                                     void*, int, void*, long long, int, const void*, void*);
+                                     void*, int, void*, long long, int, const void*, float, void*);
 __attribute__((weak)) int sq_row_norms(const void* X, int xdtype, void* out, long long n, int d, void* stream);
 // knn.hip
 __attribute__((weak)) int sq_knn_topk(const void* D, void* outd, void* outi, long long m, int nref, long long ldD, int kk,
@@ -606,14 +608,22 @@ static PyObject* py_ipe_estep(PyObject*, PyObject* a) {
                           roff, P(st)));
 }
 
+static PyObject* py_col_moments(PyObject*, PyObject* a) {
+  unsigned long long X, part, st; int xdt, d, pw; long long ldx, n;
+  if (!PyArg_ParseTuple(a, "KiLLiKiK", &X, &xdt, &ldx, &n, &d, &part, &pw, &st)) return nullptr;
+  CHECK(sq_col_moments)
+  return ret(sq_col_moments(P(X), xdt, ldx, n, d, P(part), pw, P(st)));
+}
+
 static PyObject* py_mu_sums(PyObject*, PyObject* a) {
   unsigned long long X, qs, rm, cs, part, racc, mean, st; int xdt, nq, pw, d; long long n, ldx;
-  if (!PyArg_ParseTuple(a, "KiLKiKKKiKLiKK", &X, &xdt, &ldx, &qs, &nq, &rm, &cs, &part, &pw, &racc,
-                        &n, &d, &mean, &st))
+  float qstep;
+  if (!PyArg_ParseTuple(a, "KiLKiKKKiKLiKfK", &X, &xdt, &ldx, &qs, &nq, &rm, &cs, &part, &pw,
+                        &racc, &n, &d, &mean, &qstep, &st))
     return nullptr;
   CHECK(sq_mu_sums)
   return ret(sq_mu_sums(P(X), xdt, ldx, P(qs), nq, P(rm), P(cs), P(part), pw, P(racc), n, d,
-                        P(mean), P(st)));
+                        P(mean), qstep, P(st)));
 }
 
 static PyObject* py_row_norms(PyObject*, PyObject* a) {
@@ -685,6 +695,7 @@ static PyMethodDef methods[] = {
     {"centers_f16_operand", py_centers_f16_operand, METH_VARARGS, "fp16-split centroid operand"},
     {"pack_stats", py_pack_stats, METH_VARARGS, "pack M-step statistics into one fp64 bucket"},
     {"ipe_estep", py_ipe_estep, METH_VARARGS, "IPE-noised distance argmin"},
+    {"col_moments", py_col_moments, METH_VARARGS, "fp64 column sums and sums of squares"},
     {"mu_sums", py_mu_sums, METH_VARARGS, "mu(A) power sums for a p-grid"},
     {"row_norms", py_row_norms, METH_VARARGS, "squared row norms"},
     {"knn_topk", py_knn_topk, METH_VARARGS, "per-row k smallest"},

@@ -81,9 +81,7 @@ def global_sum(data: Data, t):
 def global_mean_var(data: Data):
     """Column mean and (population) variance over all ranks in one collective."""
     X = data.X
-    acc = torch.float64
-    s = X.to(acc).sum(0)
-    ss = (X.to(acc) ** 2).sum(0)
+    s, ss = L.col_moments_local(X)
     buf = torch.cat([s, ss])
     data.comm.all_reduce_(buf)
     d = X.shape[1]

@@ -120,7 +120,7 @@ def _pick_candidates_native(data: Data, state, prefix, sizes, vals, xdtype):
     return packed[:, :d].to(xdtype), ids
 
 
-def _kmeans_plusplus_native(data: Data, k, rs, t, w, prune, stats=None):
+def _kmeans_plusplus_native(data: Data, k, rs, t, w, prune, stats=None, Xf=None):
     """The exact accelerated k-means++ on the device (csrc/kmpp.hip, see
     ``ops.kmeans.KmppState``): per centre one pick (two-level sampling of
     the t candidates), one trial pass that reads only the rows a candidate
@@ -128,7 +128,7 @@ def _kmeans_plusplus_native(data: Data, k, rs, t, w, prune, stats=None):
     exact fixed point (identical results with or without the screens and on
     any number of ranks)."""
     from ...ops.kmeans import KmppState
-    X = data.X
+    X = data.X if Xf is None else Xf     # fp32 rows (a bf16 shard is widened once)
     comm = data.comm
     dev = X.device
     n = data.n_global
@@ -224,7 +224,7 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     if native:
         if prune is None:
             prune = os.environ.get("SQ_KMPP_PRUNE", "1") != "0"
-        return _kmeans_plusplus_native(data, k, rs, t, w, bool(prune), stats)
+        return _kmeans_plusplus_native(data, k, rs, t, w, bool(prune), stats, Xf=Xf)
     if x_squared_norms is None:
         x_squared_norms = L.row_norms_sq(X)
     xn = x_squared_norms.to(Xf.dtype)

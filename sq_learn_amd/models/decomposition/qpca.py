@@ -21,7 +21,10 @@ intended routine (the reference passes invalid kwargs, :944-953);
 import logging
 import math
 import zlib
+import contextlib
 import numbers
+import os
+import time
 import warnings
 
 import numpy as np
@@ -103,6 +106,26 @@ class QPCA(_BasePCA):
 
     def _key(self, purpose, sub=0):
         return RngKey(seed_from_random_state(self.random_state), purpose, sub)
+
+    # ------------------------------------------------------ phase timings
+    @contextlib.contextmanager
+    def _phase(self, name):
+        """Wall-clock of one fit phase into ``fit_phases_`` (seconds) when
+        SQ_QPCA_PHASES=1 (device synchronised at both ends; off: no syncs)."""
+        if os.environ.get("SQ_QPCA_PHASES", "0") != "1":
+            yield
+            return
+        dev = getattr(self, "_device_type", "cpu")
+        if dev == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            if dev == "cuda":
+                torch.cuda.synchronize()
+            ph = self.__dict__.setdefault("fit_phases_", {})
+            ph[name] = ph.get(name, 0.0) + time.perf_counter() - t0
 
     # ---------------------------------------------------------------- fit
     def fit(self, X, y=None, **quantum_kw):
@@ -187,12 +210,16 @@ class QPCA(_BasePCA):
         elif n_components >= 1 and not isinstance(n_components, numbers.Integral):
             raise ValueError(f"n_components={n_components!r} must be of type int when greater "
                              f"than or equal to 1, was of type={type(n_components)!r}")
-        mean, _ = global_mean_var(data)
+        self.__dict__.pop("fit_phases_", None)
+        self._device_type = data.device.type
+        with self._phase("mean"):
+            mean, _ = global_mean_var(data)
         self.mean_ = to_numpy(mean)
         k_left = min(n_samples, n_features)
         if isinstance(n_components, numbers.Integral) and self.n_components_flag:
             k_left = max(int(n_components), 1)
-        res = full_svd(data, mean, k_left)
+        with self._phase("svd"):
+            res = full_svd(data, mean, k_left)
         S, Vt = res.S, res.Vt
         explained_variance_ = (S ** 2) / (n_samples - 1)
         total_var = explained_variance_.sum()
@@ -222,17 +249,19 @@ class QPCA(_BasePCA):
         self.explained_variance_ratio_ = explained_variance_ratio_[:n_components]
         self.singular_values_ = S[:n_components].copy()
         U = res.U_local
-        if U is not None and U.shape[1] < n_components:
-            U = self._left_vectors(data, mean, n_components)
+        with self._phase("left_vectors"):
+            if U is not None and U.shape[1] < n_components:
+                U = self._left_vectors(data, mean, n_components)
         self.left_sv = _as_out(U[:, :n_components].T.contiguous(), data.source_kind) if U is not None else None
         self.spectral_norm = float(self.singular_values_[0]) if n_components else 0.0
         fro = torch.tensor([float((S ** 2).sum())], dtype=torch.float64)
         self.frob_norm = float(np.sqrt(fro.item()))
         # mu(A) of the centred matrix with the mean fused into the power-sum
         # pass (no centred copy of X)
-        self.norm_muA, self.muA = best_mu_distributed(data, start=0, end=1.0, step=0.1,
-                                                      fro_sq_global=float((S ** 2).sum()),
-                                                      mean=mean)
+        with self._phase("mu"):
+            self.norm_muA, self.muA = best_mu_distributed(data, start=0, end=1.0, step=0.1,
+                                                          fro_sq_global=float((S ** 2).sum()),
+                                                          mean=mean)
         self._data_for_tomography = data
         self._quantum_extras()
         return self
@@ -265,13 +294,17 @@ class QPCA(_BasePCA):
             raise ValueError(f"n_components={n_components!r} must be strictly less than "
                              f"min(n_samples, n_features)={min(n_samples, n_features)!r} with "
                              f"svd_solver='{svd_solver}'")
-        mean, var = global_mean_var(data)
+        self.__dict__.pop("fit_phases_", None)
+        self._device_type = data.device.type
+        with self._phase("mean"):
+            mean, var = global_mean_var(data)
         self.mean_ = to_numpy(mean)
         n_iter = self.iterated_power
         if svd_solver == "arpack":
             n_iter = max(7, n_iter if isinstance(n_iter, int) else 7)
-        res = truncated_svd(data, mean, n_components, n_iter=n_iter,
-                            seed=seed_from_random_state(self.random_state))
+        with self._phase("svd"):
+            res = truncated_svd(data, mean, n_components, n_iter=n_iter,
+                                seed=seed_from_random_state(self.random_state))
         S, Vt = res.S, res.Vt
         self.n_samples_, self.n_features_ = n_samples, n_features
         self.components_ = Vt
@@ -299,9 +332,10 @@ class QPCA(_BasePCA):
             self.all_components = Vt
             self.explained_variance_all = self.explained_variance_
             self.explained_variance_ratio_all = self.explained_variance_ratio_
-            self.norm_muA, self.muA = best_mu_distributed(data, start=0, end=1.0, step=0.1,
-                                                          fro_sq_global=self.frob_norm ** 2,
-                                                          mean=mean)
+            with self._phase("mu"):
+                self.norm_muA, self.muA = best_mu_distributed(data, start=0, end=1.0, step=0.1,
+                                                              fro_sq_global=self.frob_norm ** 2,
+                                                              mean=mean)
             self._quantum_extras()
         return self
 
@@ -309,15 +343,23 @@ class QPCA(_BasePCA):
     def _quantum_extras(self):
         k = self._knobs
         if k["condition_number_est"]:
-            self.est_cond_number = self.condition_number_estimation(epsilon=k["eps"], delta=k["delta"])
+            with self._phase("cond_number"):
+                self.est_cond_number = self.condition_number_estimation(epsilon=k["eps"],
+                                                                        delta=k["delta"])
         if k["spectral_norm_est"]:
-            self.est_spectral_norm = self.spectral_norm_estimation(epsilon=k["eps"], delta=k["delta"])
+            with self._phase("spectral_norm"):
+                self.est_spectral_norm = self.spectral_norm_estimation(epsilon=k["eps"],
+                                                                       delta=k["delta"])
         if k["theta_estimate"]:
-            self.est_theta = self.estimate_theta(epsilon=k["eps_theta"], eta=k["eta"], p=self.ret_var)
+            with self._phase("theta"):
+                self.est_theta = self.estimate_theta(epsilon=k["eps_theta"], eta=k["eta"],
+                                                     p=self.ret_var)
         if k["quantum_retained_variance"]:
             # reference attribute ``p`` (estimated retained variance); the
             # constructor parameter p (target variance) is left untouched
-            self.p_ = self.quantum_factor_score_ratio_sum(eps=k["eps"], theta=k["theta_major"], eta=k["eta"])
+            with self._phase("factor_score"):
+                self.p_ = self.quantum_factor_score_ratio_sum(eps=k["eps"], theta=k["theta_major"],
+                                                              eta=k["eta"])
         tkw = dict(true_tomography=k["true_tomography"], norm=k["norm"],
                    stop_when_reached_accuracy=k["stop_when_reached_accuracy"],
                    incremental_measure=k["incremental_measure"],
@@ -496,8 +538,10 @@ class QPCA(_BasePCA):
         self.topk_left_singular_vectors = left
         tk = (true_tomography, norm, stop_when_reached_accuracy, incremental_measure,
               faster_measure_increment)
-        right_est = self._tomography(self.topk_right_singular_vectors, delta, *tk, tag="right")
-        left_est = self._tomography(left, delta, *tk, tag="left", sharded=True)
+        with self._phase("tomography_right"):
+            right_est = self._tomography(self.topk_right_singular_vectors, delta, *tk, tag="right")
+        with self._phase("tomography_left"):
+            left_est = self._tomography(left, delta, *tk, tag="left", sharded=True)
         fro2 = self.frob_norm ** 2
         return (right_est, left_est, sv_est, (sv_est ** 2) / (self.n_samples_ - 1),
                 np.array([fs / fro2 for fs in sv_est ** 2]))

@@ -169,7 +169,8 @@ def gram64_native(X, mean=None):
 
 def cholqr2_r(X, comm, mean=None):
     """R factor of the thin QR of the row-sharded matrix X - mean by
-    CholeskyQR2 in fp64 (two passes over X, one d x d all-reduce each):
+    CholeskyQR2 in fp64 (two passes over X, one d x d all-reduce each; the
+    second pass only when cond(R1) > 100):
     R1 = chol(X^T X), R2 = chol((X R1^-1)^T (X R1^-1)), R = R2 R1.  The
     singular values of R are those of X to ~eps64 * cond(X) relative (the
     Gram eigenvalues alone: eps * cond^2).  Returns None when the first
@@ -181,6 +182,13 @@ def cholqr2_r(X, comm, mean=None):
     R1, info = torch.linalg.cholesky_ex(G1, upper=True)
     if int(info) != 0:
         return None
+    # well-conditioned X (cond(R1) <= 100, estimated from the d x d R1 on the
+    # host): the singular values of R1 are already accurate to
+    # ~eps64 * cond^2 <= 2e-12 relative - the second pass over X (which
+    # brings that to eps64 * cond) is skipped
+    sv = torch.linalg.svdvals(R1)
+    if sv.numel() and float(sv[-1]) > 0.0 and float(sv[0]) <= 100.0 * float(sv[-1]):
+        return R1.to(X.device)
     eye = torch.eye(G1.shape[0], dtype=torch.float64)
     W1 = torch.linalg.solve_triangular(R1, eye, upper=True)
     G2 = comm.all_reduce_(gram64_local(X, mean, W1.to(X.device))).cpu()
@@ -218,6 +226,25 @@ def power_iter_local(X, Q, mean, chunk_rows=None):
     return Z
 
 
+def col_moments_local(X):
+    """(sum over rows, sum of squares over rows) of every column, fp64 [d]
+    each - one pass over X on the GPU (csrc/linalg.hip col_moments, fixed
+    row partition, fixed-order partial sums: deterministic); no fp64 copy
+    of X."""
+    n, d = X.shape
+    if nat.use_native(X) and X.dtype in (torch.float32, torch.bfloat16) and n > 0:
+        wgs = 2048
+        part = torch.zeros((wgs, 2 * d), dtype=torch.float64, device=X.device)
+        rc = nat.native().col_moments(X.data_ptr(), nat.dtype_code(X), X.stride(0), n, d,
+                                      part.data_ptr(), wgs, nat.stream_handle(X.device))
+        if rc:
+            raise RuntimeError(f"col_moments failed (hip error {rc})")
+        tot = part.sum(0)
+        return tot[:d], tot[d:]
+    Xd = X.to(torch.float64)
+    return Xd.sum(0), (Xd * Xd).sum(0)
+
+
 def mu_power_sums_local(X, exponents, mean=None):
     """(row_max [nq], col_sums [nq, d]) local partials for mu(A).
 
@@ -240,9 +267,17 @@ def mu_power_sums_local(X, exponents, mean=None):
         # d > 512: row power sums carried across the 512-column blocks
         racc = torch.zeros((nq, n), dtype=torch.float32, device=X.device) if d > 512 else None
         mu = None if mean is None else mean.to(device=X.device, dtype=torch.float32).contiguous()
+        # an arithmetic grid 0, b, 2b, ... (the p-grid's 2p): one exp2 per element,
+        # the other powers by products
+        qstep = 0.0
+        if nq >= 2 and exponents[0] == 0.0 and exponents[1] > 0.0:
+            b = float(exponents[1])
+            if all(abs(float(e) - i * b) <= 1e-9 * max(1.0, i * b) for i, e in enumerate(exponents)):
+                qstep = b
         rc = nat.native().mu_sums(X.data_ptr(), nat.dtype_code(X), X.stride(0), qd.data_ptr(), nq,
                                   rowmax.data_ptr(), colsum.data_ptr(), part.data_ptr(), wgs,
-                                  nat.ptr(racc), n, d, nat.ptr(mu), nat.stream_handle(X.device))
+                                  nat.ptr(racc), n, d, nat.ptr(mu), qstep,
+                                  nat.stream_handle(X.device))
         if rc:
             raise RuntimeError(f"mu_sums failed (hip error {rc})")
         return rowmax.double(), colsum.double()
