@@ -245,6 +245,9 @@ def _hard_extra(extra, a, comm, dev):
         for _ in range(4):
             eng.step()[1].tolist()
         extra["hard_ms_per_step"] = timed(5)
+        kf = getattr(eng, "_kept_frac", None)
+        if kf is not None:
+            extra["hard_filter_kept_frac"] = round(float(kf), 4)
         cnt = eng.buf.counts.tolist()
         tot = torch.tensor([float(cnt[1]), float(cnt[2])], dtype=torch.float64, device=dev)
         comm.all_reduce_(tot)
