@@ -254,15 +254,27 @@ def _hard_extra(extra, a, comm, dev):
         extra["hard_dense_row_frac"] = float(tot[0]) / n
         extra["hard_multi_row_frac"] = float(tot[1]) / n
         if getattr(eng, "bounds", False):
-            eng.bounds = False
-            eng.step()[1].tolist()
-            extra["hard_unpruned_ms_per_step"] = timed(3)
+            # the same iterations (1 .. 10 from the same centres) with the
+            # Hamerly bounds off, on a fresh engine: like for like
+            C_last = eng.centers().clone()
+            eng2 = LloydEngine(X, a.k, delta=a.delta, true_distance_estimate=False,
+                               intermediate_error=True, true_tomography=False, seed=a.seed,
+                               comm=comm, row_offset=s0, gemm_precision="fp32")
+            eng2.bounds = False
+            eng2.set_centers(C0)
+            eng_b, eng = eng, eng2
+            timed(1)
+            for _ in range(4):
+                eng.step()[1].tolist()
+            extra["hard_unpruned_ms_per_step"] = timed(5)
             cnt = eng.buf.counts.tolist()
             tot = torch.tensor([float(cnt[1]), float(cnt[2])], dtype=torch.float64, device=dev)
             comm.all_reduce_(tot)
             extra["hard_unpruned_dense_row_frac"] = float(tot[0]) / n
             extra["hard_unpruned_multi_row_frac"] = float(tot[1]) / n
-            eng.bounds = True
+            extra["hard_unpruned_same_centres"] = bool(torch.equal(eng.centers(), C_last))
+            del eng
+            eng = eng_b
         if comm.rank == 0:
             m = min(4096, s1 - s0)
             Xs = X[:m].double()

@@ -294,6 +294,8 @@ class LloydEngine:
         self.bounds_valid = False
         self._kept_frac = self._kept_prev = None   # new centres: re-measure the filter
         self._skips = 0
+        self._probe_gap = getattr(self, "probe_every", 2)
+        self._sc_dev = None
         if self.fast:
             self.C.copy_(C.to(torch.float32))
             if self.C_op is not None:
@@ -350,7 +352,16 @@ class LloydEngine:
                 Cp = self.C if self.d == self.d_pad else self._padded_centers()
                 rows = None
                 self._filter_ran = False
-                if self.bounds and self.bounds_valid and not full and self._use_filter():
+                if self.bounds and not full:
+                    mode = self._filter_mode()
+                    if mode == "filter" and not self.bounds_valid:
+                        mode = "bounds"    # no valid bounds to filter with: maintain them now
+                else:
+                    mode = "bounds" if self.bounds else "none"
+                # dormant bounds are not maintained by this sweep: invalid
+                # until a bounds-maintaining sweep (the step before a probe)
+                self._bounds_kept = mode != "none"
+                if mode == "filter":
                     self._filter_ran = True
                     K.ensure_multi_buffers(self.buf, self.n, self.device, True)
                     self.buf.counts.zero_()
@@ -362,7 +373,8 @@ class LloydEngine:
                 lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
                                                self.cmax2, self.k, self.delta, self.alpha, key,
                                                self.row_offset, self.buf,
-                                               bounds=(self.ub, self.lb) if self.bounds else None,
+                                               bounds=(self.ub, self.lb)
+                                               if self.bounds and self._bounds_kept else None,
                                                rows=rows, zero_counts=rows is None,
                                                screen=self.incremental and not full
                                                and os.environ.get("SQ_SCREEN", "1") != "0")
@@ -382,20 +394,32 @@ class LloydEngine:
             return self._estep_ipe(key)
         return self._estep_generic(key)
 
-    def _use_filter(self):
-        """Adaptive Hamerly pruning: run the bounds filter unless the last
-        two measured iterations both kept more than ``keep_max`` of the rows
-        (then the filter's pass and the row-list indirection cost more than
-        they save); re-probe every ``probe_every`` E-steps."""
+    def _filter_mode(self):
+        """Adaptive Hamerly pruning: 'filter' (bounds filter + list-mode
+        sweep), 'bounds' (full sweep that maintains the bounds, so the next
+        E-step can filter) or 'none' (full sweep, bounds dormant).  The filter
+        runs unless the last two measured iterations both kept more than
+        ``keep_max`` of the rows (then its pass and the row-list indirection
+        cost more than they save); it is re-probed after 2, 4, 8, 16 skipped
+        steps while probes keep finding it useless, the step before a probe
+        re-validating the bounds."""
+        sd = getattr(self, "_sc_dev", None)
+        if sd is not None:
+            self._sc_dev = None
+            self._on_scalars(sd.tolist())
         kf, kp = self._kept_frac, self._kept_prev
         if kf is None or kp is None or kf <= self.keep_max or kp <= self.keep_max:
             self._skips = 0
-            return True
+            self._probe_gap = self.probe_every
+            return "filter"
         self._skips += 1
-        if self._skips >= self.probe_every:
+        gap = getattr(self, "_probe_gap", self.probe_every)
+        if self._skips >= gap:
+            # a probe at ~100 % kept costs ~1.2 full sweeps: back off
             self._skips = 0
-            return True
-        return False
+            self._probe_gap = min(2 * gap, 16)
+            return "filter"
+        return "bounds" if self._skips == gap - 1 else "none"
 
     def _on_scalars(self, vals):
         """Host values of an iteration's scalars (called by the pipelined
@@ -648,7 +672,7 @@ class LloydEngine:
                     torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
                     self.shift_s.mul_(1.0 + 1e-12)
                     torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
-                self.bounds_valid = True
+                self.bounds_valid = getattr(self, "_bounds_kept", True)
         return self.scalars
 
     def _padded_centers(self):
@@ -818,4 +842,8 @@ class LloydEngine:
             labels = self._label_snap
             self._pending = self._estep(self._key("band_select"))
             sc = _HostScalars(host, ev, self._on_scalars)
+        elif getattr(self, "bounds", False) and torch.is_tensor(sc) and sc.numel() > 3:
+            # unpipelined: the next E-step reads this iteration's kept count
+            # (the caller has usually synchronised on it already)
+            self._sc_dev = sc
         return labels, sc
