@@ -336,20 +336,31 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
   if (threadIdx.x == 0) lcnt = 0;
   __syncthreads();
   // the exact pass's fp32 direct-form D carries <= 3 (d + 2) u relative error
-  const double lim_rel = 1.0 + 3.0 * (double)(d + 2) * 5.960464477539063e-08 + 1e-6;
+  const float lim_rel = 1.0f + 3.0f * (float)(d + 2) * 5.9604645e-08f + 1e-6f;
   const bool jv = c16 < t;
-  const double sc = jv ? cinfo[c16 * 4 + 0] : 1.0;
-  const double ec = jv ? cinfo[c16 * 4 + 1] : 0.0;
-  const double cc2 = jv ? cinfo[c16 * 4 + 2] : 0.0;
+  // the trial's scale and error norm, rounded UP to fp32 (they only enter as
+  // magnitudes of upper-bounded terms); |c~|^2 to nearest (its rounding is
+  // inside the 1e-6 absolute-sum margin below)
+  const float sc = jv ? (float)cinfo[c16 * 4 + 0] * (1.0f + 1.2e-7f) : 1.0f;
+  const float ec = jv ? (float)cinfo[c16 * 4 + 1] * (1.0f + 1.2e-7f) : 0.0f;
+  const float cc2 = jv ? (float)cinfo[c16 * 4 + 2] : 0.0f;
   const int nsd = NS > 0 ? NS : dq / 64;
   const int8_t* b1 = cb + (size_t)c16 * dq + 16 * kb;
   const int8_t* b2 = cb + (size_t)(16 + c16) * dq + 16 * kb;
+  // the row ids of the next iteration are fetched one iteration ahead
+  int nrow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = wave * 32 + 16 * h + c16;
+    nrow[h] = e < cnt ? sseg[e] : -1;
+  }
   for (int g0 = wave * 32; g0 < cnt; g0 += 128) {
     int row[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int e = g0 + 16 * h + c16;
-      row[h] = e < cnt ? sseg[e] : -1;
+      row[h] = nrow[h];
+      const int e = g0 + 128 + 16 * h + c16;
+      nrow[h] = e < cnt ? sseg[e] : -1;
     }
     // per-row scalars of the lane's row slot c16 (all 4 lane copies load them)
     float rs[2], re_[2], rcl[2];
@@ -401,20 +412,24 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
       for (int i = 0; i < 4; ++i) {
         const int src = 4 * kb + i;   // the row slot of result register i
         const int rr = __shfl(row[h], src, 64);
-        const double s = (double)__shfl(rs[h], src, 64);
-        const double er = (double)__shfl(re_[h], src, 64);
-        const double q2 = (double)__shfl(rq2[h], src, 64);
-        const double cl = (double)__shfl(rcl[h], src, 64);
+        const float s = __shfl(rs[h], src, 64);
+        const float er = __shfl(re_[h], src, 64);
+        const float q2 = (float)__shfl(rq2[h], src, 64);
+        const float cl = __shfl(rcl[h], src, 64);
         bool need = false;
         if (jv && rr >= 0) {
-          const double A = s * s * q2;
-          const double dot = s * sc * ((double)hi[h][i] + (double)lo[h][i] * (1.0 / 254.0));
-          const double Dq = (A + cc2) - 2.0 * dot;
-          const double Dlb = Dq - 1e-13 * (A + cc2 + 2.0 * fabs(dot));
-          double lb = 0.0;
-          if (Dlb > 0.0) {
-            const double r = sqrt(Dlb) * (1.0 - 1e-15) - er - ec;
-            lb = r > 0.0 ? r * r * (1.0 - 1e-15) : 0.0;
+          // fp32 with rigorous margins: every term below carries <= 7 u of
+          // relative rounding (the int32 dots and |q|^2 convert exactly below
+          // 2^24, within u above; the sum Ihi + Ilo / 254 rounds relative to
+          // itself), so |Dq_fl - Dq| <= 1e-6 (A + |c~|^2 + 2 |dot|)
+          const float A = s * s * q2;
+          const float dot = s * sc * ((float)hi[h][i] + (float)lo[h][i] * (1.0f / 254.0f));
+          const float Dq = (A + cc2) - 2.0f * dot;
+          const float Dlb = Dq - 1e-6f * (A + cc2 + 2.0f * fabsf(dot));
+          float lb = 0.0f;
+          if (Dlb > 0.0f) {
+            const float r = __builtin_amdgcn_sqrtf(Dlb) * (1.0f - 1e-6f) - er - ec;
+            lb = r > 0.0f ? r * r * (1.0f - 1e-6f) : 0.0f;
           }
           need = !(lb > cl * lim_rel);
         }
@@ -507,24 +522,35 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
         *reinterpret_cast<float4*>(my + (q * 8 + lrow) * kKppStride + lchunk * 4) = v[q];
       if (tix + 1 < ntiles) fetch(tix + 1);
       const int f0 = tix * kKppTile;
-      const int fl = min(kKppTile, d - f0);
+      // the row's 32 features in registers, then trial by trial: a trial's
+      // 32 wave-uniform features are two 64-byte scalar loads (one wait per
+      // trial, not one per 4 features); a short last tile is zero padded on
+      // both sides (adds 0), so the fmaf chain per trial stays sequential
+      float xv[kKppTile];
 #pragma unroll
       for (int c4 = 0; c4 < kKppTile / 4; ++c4) {
-        if (c4 * 4 >= fl) break;
         const float4 x4 = *reinterpret_cast<const float4*>(my + lane * kKppStride + c4 * 4);
-        const int f = f0 + c4 * 4;
+        xv[4 * c4] = x4.x;
+        xv[4 * c4 + 1] = x4.y;
+        xv[4 * c4 + 2] = x4.z;
+        xv[4 * c4 + 3] = x4.w;
+      }
+      const bool full_tile = f0 + kKppTile <= d;
 #pragma unroll
-        for (int j = 0; j < TMAX; ++j) {
-          if (j < t) {
-            const float* c = cand + (size_t)j * d + f;   // wave-uniform: scalar loads
-            float ev = x4.x - c[0];
-            acc[j] = fmaf(ev, ev, acc[j]);
-            ev = x4.y - c[1];
-            acc[j] = fmaf(ev, ev, acc[j]);
-            ev = x4.z - c[2];
-            acc[j] = fmaf(ev, ev, acc[j]);
-            ev = x4.w - c[3];
-            acc[j] = fmaf(ev, ev, acc[j]);
+      for (int j = 0; j < TMAX; ++j) {
+        if (j < t) {
+          const float* c = cand + (size_t)j * d + f0;   // wave-uniform: scalar loads
+          if (full_tile) {
+#pragma unroll
+            for (int u = 0; u < kKppTile; ++u) {
+              const float ev = xv[u] - c[u];
+              acc[j] = fmaf(ev, ev, acc[j]);
+            }
+          } else {
+            for (int u = 0; u < d - f0; ++u) {
+              const float ev = xv[u] - c[u];
+              acc[j] = fmaf(ev, ev, acc[j]);
+            }
           }
         }
       }
