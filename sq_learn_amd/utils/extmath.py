@@ -156,13 +156,45 @@ def randomized_svd(M, n_components, *, n_oversamples=10, n_iter="auto",
 
 
 # ------------------------------------------------------- distributed path
+def _rsvd_gram(X_local, mean, G, Z, k, n_iter, dev):
+    """The range finder run in the feature domain on the d x d Gram
+    G = (X-mu)^T (X-mu) (all-reduced, on the host): Z <- qr(G Z) n_iter
+    times is the same subspace iteration as the streamed
+    qr((X-mu)^T ((X-mu) Z)).  The range basis Q = (X-mu) Z E lam^-1/2
+    (M = Z^T G Z = E lam E^T, the Gram of (X-mu) Z) is never formed:
+    B = Q^T (X-mu) = lam^-1/2 E^T Z^T G, and U = Q Uhat is ONE xw pass over
+    X with the d x k matrix Z E lam^-1/2 Uhat.  Directions of (X-mu) Z with
+    lam < 1e-6 lam_max (sigma ratio 1e-3, where Q's orthogonality error
+    ~eps64 lam_max / lam would pass 1e-10) are dropped; None when the
+    k-th one is among them (the caller streams instead)."""
+    from ..ops import linalg as L
+    for _ in range(n_iter):
+        Z, _ = torch.linalg.qr(G @ Z)
+    M = Z.T @ G @ Z
+    lam, E = torch.linalg.eigh(0.5 * (M + M.T))
+    lam, E = lam.flip(0), E.flip(1)
+    lmax = float(lam[0]) if lam.numel() else 0.0
+    if not lmax > 0.0 or not float(lam[k - 1]) >= 1e-6 * lmax:
+        return None
+    m = int((lam >= 1e-6 * lmax).sum())
+    T = Z @ (E[:, :m] / torch.sqrt(lam[:m]))          # Q = (X - mu) T
+    Uhat, sv, Vt = torch.linalg.svd(T.T @ G, full_matrices=False)
+    U = L.xw(X_local, (T @ Uhat[:, :k]).contiguous().to(dev), mean=mean)
+    return U, sv, Vt
+
+
 def randomized_svd_distributed(X_local, mean, n_components, comm, *, n_oversamples=10,
-                               n_iter="auto", seed=0, flip_sign=True, n_rows=None, d=None):
+                               n_iter="auto", seed=0, flip_sign=True, n_rows=None, d=None,
+                               method="auto"):
     """Randomized SVD of the centred row-sharded matrix (X - mean)
     (``utils/extmath.py:161-242`` of the reference, Halko et al.).
 
     Every pass over the n rows is an fp64-MFMA tall-skinny kernel
-    (ops/linalg.py xw / xtx -> csrc/tsgemm64.hip on the GPU): power
+    (ops/linalg.py xw / xtx -> csrc/tsgemm64.hip on the GPU).
+    ``method="gram"`` (auto for d <= max(512, 4 l (n_iter + 2)), the
+    flop crossover with margin): one xtx pass forms the d x d Gram, the
+    power iterations and B run on it (:func:`_rsvd_gram`), one xw pass
+    forms U - two reads of X instead of 2 n_iter + 4.  ``"stream"``: power
     iterations Z <- qr((X-mu)^T ((X-mu) Z)), Y = (X-mu) Z, two CholeskyQR
     passes Y <- Y R^-1, B^T = (X-mu)^T Y, U = Y Uhat.  The small d x l / l x l
     factorisations (QR, Cholesky, SVD) run on the host in fp64 LAPACK; one
@@ -181,6 +213,19 @@ def randomized_svd_distributed(X_local, mean, n_components, comm, *, n_oversampl
     if X_local.stride(1) != 1:
         X_local = X_local.contiguous()
     Z = philox_normal((d, l), RngKey(seed, "gaussian", 0), dtype=torch.float64, device="cpu")
+    if method == "auto":
+        method = "gram" if d <= 4096 and d <= max(512, 4 * l * (n_iter + 2)) else "stream"
+    if method == "gram":
+        G = comm.all_reduce_(L.xtx(X_local, mean_a=mean)).cpu()
+        got = _rsvd_gram(X_local, mean, 0.5 * (G + G.T), Z, k, n_iter, dev)
+        if got is not None:
+            U, sv, Vt = got
+            Vt = Vt[:k].to(dev)
+            if flip_sign:
+                U, Vt = svd_flip_distributed(U, Vt, comm)
+            return U, sv[:k].to(dev), Vt
+    elif method != "stream":
+        raise ValueError(f"method must be 'auto', 'gram' or 'stream', got {method!r}")
     for _ in range(n_iter):
         Zn = comm.all_reduce_(L.power_iter_local(X_local, Z.to(dev), mean)).cpu()
         Z, _ = torch.linalg.qr(Zn)

@@ -171,3 +171,33 @@ def test_qpca_randomized_quantum_extras(X):
              quantum_truncated=True).fit(Z, eps=1e-3, theta_major=1e-6, delta=0.2,
                                          estimate_all=True, true_tomography=False)
     assert np.all(np.abs(np.asarray(g.estimate_left_sv) - np.asarray(g.left_sv)) <= 0.2 / np.sqrt(4 * 1500) + 1e-12)
+
+
+@pytest.mark.parametrize("rank", [40, 6])
+def test_randomized_svd_gram_matches_streamed(rank):
+    """The feature-domain range finder (one Gram pass + one U pass) gives the
+    streamed power iterations' factors: same top singular values (exact SVD
+    to 1e-9), orthonormal U, the same singular subspaces; a spectrum whose
+    k-th value falls under 1e-3 sigma_max (rank 6 < k) takes the streamed
+    path and still agrees."""
+    import torch
+    from sq_learn_amd.parallel.comm import Comm
+    from sq_learn_amd.utils.extmath import randomized_svd_distributed
+    g = torch.Generator().manual_seed(rank)
+    n, d, k = 3000, 64, 8
+    U0, _ = torch.linalg.qr(torch.randn(n, rank, generator=g, dtype=torch.float64))
+    V0, _ = torch.linalg.qr(torch.randn(d, rank, generator=g, dtype=torch.float64))
+    X = (U0 * torch.logspace(2, 0, rank, dtype=torch.float64)) @ V0.T + 1.0
+    mu = X.mean(0)
+    ref = torch.linalg.svdvals(X - mu)[:k]
+    out = {}
+    for method in ("gram", "stream"):
+        U, s, Vt = randomized_svd_distributed(X, mu, k, Comm(None), seed=3, method=method)
+        out[method] = (U, s, Vt)
+        torch.testing.assert_close(U.T @ U, torch.eye(k, dtype=torch.float64), atol=1e-9, rtol=0)
+        top = min(k, rank)
+        torch.testing.assert_close(s[:top], ref[:top], rtol=1e-9, atol=0)
+    (Ug, sg, Vg), (Us, ss, Vs) = out["gram"], out["stream"]
+    top = min(k, rank) - 1   # well-separated leading part: same vectors up to sign
+    torch.testing.assert_close(Vg[:top], Vs[:top], atol=1e-7, rtol=0)
+    torch.testing.assert_close(Ug[:, :top], Us[:, :top], atol=1e-7, rtol=0)

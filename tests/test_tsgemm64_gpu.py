@@ -99,11 +99,13 @@ def test_cholqr2_sigma_wide(cuda, d):
     np.testing.assert_allclose(got, ref, rtol=1e-9)
 
 
+@pytest.mark.parametrize("method", ["gram", "stream"])
 @pytest.mark.parametrize("d,dtype", [(512, torch.bfloat16), (784, torch.float32)])
-def test_randomized_svd_wide(cuda, d, dtype):
+def test_randomized_svd_wide(cuda, d, dtype, method):
     """Randomized range finder at d = 512 (BASELINE config 2 dtype) and 784:
     the top singular values of a matrix with a decaying spectrum match the
-    exact fp64 SVD of the same (rounded) data."""
+    exact fp64 SVD of the same (rounded) data, on both the Gram-domain and
+    the streamed range finder."""
     from sq_learn_amd.utils.extmath import randomized_svd_distributed
     n, k = 60_000, 10
     g = torch.Generator().manual_seed(d)
@@ -113,7 +115,8 @@ def test_randomized_svd_wide(cuda, d, dtype):
     X = ((U0 * s0) @ V0.T + 1e-3 * torch.randn(n, d, generator=g, dtype=torch.float64)).to(dtype)
     mu = X.double().mean(0)
     ref = torch.linalg.svdvals(X.double() - mu)[:k]
-    U, s, Vt = randomized_svd_distributed(X.to(cuda), mu.to(cuda), k, Comm(None), seed=0)
+    U, s, Vt = randomized_svd_distributed(X.to(cuda), mu.to(cuda), k, Comm(None), seed=0,
+                                          method=method)
     torch.testing.assert_close(s.cpu(), ref, rtol=1e-7, atol=0)
     # U^T U = I, U S Vt reconstructs the top-k part
     UtU = (U.T @ U).cpu()
