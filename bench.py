@@ -58,6 +58,7 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-hard", action="store_true", help="skip the overlapping-blobs extra")
     ap.add_argument("--no-mnist", action="store_true", help="skip the 70k x 784 (config 4) extra")
+    ap.add_argument("--no-share8", action="store_true", help="skip the N = 8 per-GPU share extra")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the qPCA -> q-means pipeline (config 5) extra")
     ap.add_argument("--pipeline-rows", type=int, default=50_000_000)
@@ -497,7 +498,7 @@ def main(argv=None):
     del eng
     if gpu:
         torch.cuda.empty_cache()
-    if gpu and comm.world_size == 1 and a.n >= 8 * 4096:
+    if gpu and comm.world_size == 1 and a.n >= 8 * 4096 and not a.no_share8:
         _share8_extra(extra, a, X, comm, dev)
     if a.ipe_steps > 0 and gpu:
         _ipe_extra(extra, a, X, comm, dev, start, C0)

@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--last", type=int, default=5)
     ap.add_argument("--first", type=int, default=None,
                     help="take --last intervals starting at this one (default: the last ones)")
+    ap.add_argument("--seq-all", action="store_true",
+                    help="print the kernel sequence of every selected interval")
     a = ap.parse_args()
     rows = load(a.dir)
     marks = [i for i, r in enumerate(rows) if a.marker in r[2]]
@@ -58,12 +60,12 @@ def main():
         wall = (rows[j][0] - rows[i][0]) / 1e3
         busy = sum(e - s for s, e, _ in seg) / 1e3
         print(f"| {n} | {wall:.1f} | {busy:.1f} | {wall - busy:.1f} | {len(seg)} |")
-    i, j = ivs[-1]
-    print("\n| kernel | us | gap before us |\n|---|---|---|")
-    prev = rows[i - 1][1] if i > 0 else rows[i][0]
-    for s, e, nme in rows[i:j]:
-        print(f"| `{nme}` | {(e - s) / 1e3:.1f} | {(s - prev) / 1e3:.1f} |")
-        prev = e
+    for n, (i, j) in enumerate(ivs if a.seq_all else ivs[-1:]):
+        print(f"\ninterval {n if a.seq_all else len(ivs) - 1}\n\n| kernel | us | gap before us |\n|---|---|---|")
+        prev = rows[i - 1][1] if i > 0 else rows[i][0]
+        for s, e, nme in rows[i:j]:
+            print(f"| `{nme}` | {(e - s) / 1e3:.1f} | {(s - prev) / 1e3:.1f} |")
+            prev = e
 
 
 if __name__ == "__main__":

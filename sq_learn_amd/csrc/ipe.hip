@@ -429,10 +429,12 @@ SQ_DEV float ipe_pruned_exact(double ip, double S, double eps, int Q, float thr,
 // grouped into workgroups or sharded over ranks.
 
 struct IpeScreen {
-  float kq;       // 1 / (sqrt(2) eps), rounded down
-  float inv_eps;  // 1 / eps, rounded up
-  float cqh;      // C(Q, h), rounded up
+  float kq;       // (1 - 3e-6) / (sqrt(2) eps), rounded down (the m margin folded in)
+  float smax;     // 6e10 eps, rounded down: S / max(1, |ip|) < smax keeps M below its cap
+  float cqh;      // 1.0002 C(Q, h), rounded up (the pu margin folded in)
   float hf;       // h = (Q + 1) / 2
+  uint32_t cap;   // initial budgets' cap (units 2^-32): 2^23 per pair of a stream
+  double ucap;    // exp(-cap 2^-32): U <= ucap -> the capped budget
 };
 
 // upper bound on sqrt(x (1 + 2^-23)) (the class-value rounding of thr)
@@ -447,37 +449,48 @@ SQ_DEV float ipe_sthr(float x) { return __builtin_amdgcn_sqrtf(x) * 1.000001f; }
 //   (M >= pi / eps_a = pi S / (eps max(1, |ip|)));  D >= S 2^-12 keeps the
 //   fp32 relative error of D below 7.4e-4 (the sqrt(D) margin 4.9e-4 covers
 //   its half); every other product carries its ulps in the 3e-6 margin.
-SQ_DEV bool ipe_hazard(float ip, float nx2, float ny2, float sthr, const IpeScreen& sc,
+SQ_DEV bool ipe_hazard(float ip, float nx2, float ny2, float sthr, float kt, const IpeScreen& sc,
                        uint32_t& hq, float& pbar) {
 #pragma clang fp contract(off)   // the drain recomputes hq bit for bit
   // straight-line (every lane evaluates everything; the conditions are
-  // combined at the end): no divergent exits in the tile epilogue
+  // combined at the end): no divergent exits in the tile epilogue.  Every
+  // constant margin is folded into a per-launch (sc) or per-row (kt =
+  // 1.571 sthr) factor.
   const float S = nx2 + ny2;
   const float D = fmaf(-2.0f, ip, S);
   const bool c1 = (D >= S * 2.44140625e-4f) & (D <= S * 1.998046875f);
   const float sD = __builtin_amdgcn_sqrtf(fmaxf(D, 0.0f)) * (1.0f - 4.8828125e-4f);
   const float ra = __builtin_amdgcn_rcpf(fmaxf(1.0f, fabsf(ip)));
   const float P = __builtin_amdgcn_sqrtf(S) * ra * sc.kq;
-  const float m = (sD - sthr) * P * (1.0f - 3e-6f);
+  const float m = (sD - sthr) * P;
   // t_b <= M sqrt(r) / 2, M <= pi / eps_a + pi + 1: the exact branch's walk
-  const float tcap = fmaf(1.571f * sthr, P, 2.2f);
+  const float tcap = fmaf(kt, P, 2.2f);
   // M below its 2^40 cap
-  const float Mq = S * ra * sc.inv_eps;
-  const bool c2 = (m >= 3.0f) & (tcap <= 1048576.0f) & (Mq < 6.0e10f);
-  const float rm = __builtin_amdgcn_rcpf(fmaxf(m, 3.0f)) * 1.000001f;
-  const float pb = fminf(0.5f * rm * (1.0f + rm) * 1.00002f, 1.0f);
+  const bool c2 = (m >= 3.0f) & (tcap <= 1048576.0f) & (S * ra < sc.smax);
+  // pb >= (r + r^2) / 2 (r = 1 / m): one rounded fma, the rcp's ulp and the
+  // product's rounding inside the 2.4e-5 factor
+  const float rm = __builtin_amdgcn_rcpf(fmaxf(m, 3.0f));
+  // (rm <= 1/3 always: pb < 0.23, no clamp to 1)
+  const float pb = fmaf(rm, rm, rm) * 0.500012f;
   // C(Q, h) pbar^h = C(Q, h) 2^(h log2 pbar): v_log / v_exp (1 ulp each;
   // |h log2 pbar| < 2^8 puts the exponent's error below 2^-14 relative to
-  // pw... covered 30x by the 2e-4 margin); an underflow to 0 still gives
-  // hq = 1 >= 2^32 pibar
-  const float pw = __builtin_amdgcn_exp2f(sc.hf * __builtin_amdgcn_logf(pb));
-  const float pu = sc.cqh * pw * 1.0002f;
+  // pw... covered 30x by the 2e-4 margin in cqh); an underflow to 0 still
+  // gives hq = 1 >= 2^32 pibar
+  const float pu = sc.cqh * __builtin_amdgcn_exp2f(sc.hf * __builtin_amdgcn_logf(pb));
   // -log(1 - pu) <= pu (1 + pu) <= pu (1 + 2^-10): 2^32 H < 2^22.01, so 256
   // pairs of one stream never exhaust a capped (2^31) budget
   const bool c3 = pu < 9.765625e-4f;
-  hq = (uint32_t)(fminf(pu, 9.765625e-4f) * 1.001f * 4294967296.0f) + 1u;
+  // (hq is only spent when c3 holds: no clamp; v_cvt saturates otherwise)
+  hq = (uint32_t)(pu * (1.001f * 4294967296.0f)) + 1u;
   pbar = pb;
   return c1 & c2 & c3;
+}
+
+SQ_DEV float ipe_kt(float sthr) { return 1.571f * sthr; }
+
+SQ_DEV bool ipe_hazard(float ip, float nx2, float ny2, float sthr, const IpeScreen& sc,
+                       uint32_t& hq, float& pbar) {
+  return ipe_hazard(ip, nx2, ny2, sthr, ipe_kt(sthr), sc, hq, pbar);
 }
 
 // 53-bit uniform in (0, 1) from two words
@@ -492,6 +505,70 @@ SQ_DEV uint32_t ipe_budget(uint32_t w0, uint32_t w1) {
   const double U = u53(w0, w1);
   if (U <= 0.6065306597126334) return 0x80000000u;   // exp(-1/2)
   return (uint32_t)(-log(U) * 4294967296.0);
+}
+
+// The initial budgets of a lane's streams: rows gb[t] + i (i < 4, the NG
+// groups' first rows of one parity), class / column cls.  Rows 2m and 2m + 1
+// take words (0, 1) / (2, 3) of one Philox block (stream 64 (2m) + cls,
+// block 0; a fire's redraws use odd blocks) - half the Philox rounds, each
+// stream's words still a function of (key, stream) only.  A stream spends at
+// most (its pairs) x (2^-10 (1.001) + 2^-32) < cap 2^-32 (cap = 2^23 per
+// pair), so a budget E >= cap never runs out - exactly as an uncapped one:
+// only the ~3 % with U > exp(-cap 2^-32) need -log U, and those logs are
+// lane-compacted (one fp64 log per round, each lane's next pending budget).
+template <int NG>
+SQ_DEV void ipe_initial_budgets(const RngKey& key, const long long (&gb)[NG], int cls,
+                                const IpeScreen& sc, u32x4 (&bud)[NG]) {
+  double U[NG][4];
+  const bool odd = (gb[0] & 1) != 0;   // wave-uniform
+#pragma unroll
+  for (int t = 0; t < NG; ++t) {
+    auto block = [&](long long row) -> u4 {
+      WordStream ws(key, (unsigned long long)row * 64ull + (unsigned long long)cls);
+      u4 w;
+      w.x = ws.next();
+      w.y = ws.next();
+      w.z = ws.next();
+      w.w = ws.next();
+      return w;
+    };
+    if (!odd) {
+      const u4 a = block(gb[t]), c = block(gb[t] + 2);
+      U[t][0] = u53(a.x, a.y);
+      U[t][1] = u53(a.z, a.w);
+      U[t][2] = u53(c.x, c.y);
+      U[t][3] = u53(c.z, c.w);
+    } else {
+      const u4 a = block(gb[t] - 1), c = block(gb[t] + 1), e = block(gb[t] + 3);
+      U[t][0] = u53(a.z, a.w);
+      U[t][1] = u53(c.x, c.y);
+      U[t][2] = u53(c.z, c.w);
+      U[t][3] = u53(e.x, e.y);
+    }
+  }
+  uint32_t pend = 0u;
+#pragma unroll
+  for (int t = 0; t < NG; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bud[t][i] = sc.cap;
+      pend |= U[t][i] > sc.ucap ? 1u << (4 * t + i) : 0u;
+    }
+  }
+  while (__ballot(pend != 0u) != 0ull) {
+    const int b = pend ? __builtin_ctz(pend) : 0;
+    double u = 0.5;
+#pragma unroll
+    for (int t = 0; t < NG; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u = b == 4 * t + i ? U[t][i] : u;
+    const uint32_t v = (uint32_t)(-log(u) * 4294967296.0);
+#pragma unroll
+    for (int t = 0; t < NG; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bud[t][i] = (pend && b == 4 * t + i) ? v : bud[t][i];
+    pend &= pend - 1u;
+  }
 }
 
 SQ_DEV bool ipe_better(float ob, uint32_t ok, int oj, float b, uint32_t kk, int jj) {
@@ -672,12 +749,10 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_kernel(
     return (unsigned long long)g * 64ull + (unsigned long long)(wave * 16 + c16);
   };
   if (prune) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      WordStream ws(skip_key, stream_id(i));
-      const uint32_t w0 = ws.next(), w1 = ws.next();
-      bud[i] = ipe_budget(w0, w1);
-    }
+    const long long gb[1] = {row_offset + row0 + 4 * q4};
+    u32x4 b1[1];
+    ipe_initial_budgets<1>(skip_key, gb, wave * 16 + c16, sc, b1);
+    bud = b1[0];
   }
   int qn = 0;
   auto consider = [&](int i, int j, float dt) {
@@ -1204,16 +1279,12 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
     return (unsigned long long)g * 64ull + (unsigned long long)(w * 16 + c);
   };
 #pragma unroll
-  for (int g = 0; g < R; ++g) {
-    bud[g] = u32x4{0u, 0u, 0u, 0u};
-    if (prune) {
+  for (int g = 0; g < R; ++g) bud[g] = u32x4{0u, 0u, 0u, 0u};
+  if (prune) {
+    long long gb[R];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        WordStream ws(skip_key, stream_of(16 * g + 4 * q4 + i, wave, c16));
-        const uint32_t w0 = ws.next(), w1 = ws.next();
-        bud[g][i] = ipe_budget(w0, w1);
-      }
-    }
+    for (int g = 0; g < R; ++g) gb[g] = row_offset + row0 + 16 * g + 4 * q4;
+    ipe_initial_budgets<R>(skip_key, gb, wave * 16 + c16, sc, bud);
   }
   // this wave's running best of row `lane` (lanes < NR)
   float bestv = INF;
@@ -1363,10 +1434,10 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float4 ri = rinfo[16 * g + 4 * q4 + i];
-          const bool valid = jv & (ri.w != 0.0f) & (j != __float_as_int(ri.z));
+          const bool valid = jv & !(ri.w < 0.0f) & (j != __float_as_int(ri.z));
           uint32_t hq;
           float pbar;
-          const bool ok = ipe_hazard(acc[i], ri.x, ny2, ri.y, sc, hq, pbar) & valid;
+          const bool ok = ipe_hazard(acc[i], ri.x, ny2, ri.y, ri.w, sc, hq, pbar) & valid;
           const bool fired = ok & (hq > bd[i]);   // the stream's budget runs out here
           const bool scr = ok & !fired;
           bd[i] = scr ? bd[i] - hq : bd[i];
@@ -1381,7 +1452,7 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float4 ri = rinfo[16 * g + 4 * q4 + i];
-          pp[i] = jv & (ri.w != 0.0f) & (j != __float_as_int(ri.z));
+          pp[i] = jv & !(ri.w < 0.0f) & (j != __float_as_int(ri.z));
         }
       }
       if (__ballot(pp[0] || pp[1] || pp[2] || pp[3]) != 0ull) {
@@ -1418,8 +1489,9 @@ __global__ void __launch_bounds__(256, 2) ipe_fused_rg_kernel(
       for (int rl = threadIdx.x; rl < NR; rl += 256) {
         const float st = ipe_sthr(r_thr[rl]);
         r_sthr[rl] = st;
+        // .w: the row's hazard factor kt (>= 0 or NaN), -1 past the last row
         rinfo[rl] = make_float4(r_nx2[rl], st, __int_as_float(r_hj[rl]),
-                                row0 + rl < n ? 1.0f : 0.0f);
+                                row0 + rl < n ? ipe_kt(st) : -1.0f);
       }
       __syncthreads();
       if (lane < NR) {
@@ -1489,9 +1561,11 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
   double cq = 1.0;
   for (int i = 0; i < h; ++i) cq = cq * (double)(Q - i) / (double)(i + 1);
   sc.hf = (float)h;
-  sc.cqh = (float)cq * (1.0f + 1e-6f);
-  sc.kq = (float)(1.0 / (1.4142135623730951 * eps)) * (1.0f - 1e-6f);
-  sc.inv_eps = (float)(1.0 / eps) * (1.0f + 1e-6f);
+  sc.cqh = (float)(cq * (1.0002 * (1.0 + 1e-6)));
+  sc.kq = (float)((1.0 - 3e-6) * (1.0 - 1e-6) / (1.4142135623730951 * eps));
+  sc.smax = (float)(6.0e10 * eps * (1.0 - 1e-6));
+  sc.cap = (uint32_t)(((k + 63) / 64) * (1u << 23));   // <= 2^31 (k <= 16384)
+  sc.ucap = exp(-(double)sc.cap * 0x1p-32);
   const int nt = k_pad / 16;
   const int pr = (prune & 1) && (Q & 1) ? 1 : 0;
   // layout (prune bits 1-2): 0 auto, 1 / 2 row groups, 3 the per-lane-queue kernel

@@ -1013,7 +1013,13 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
     pstep = 8LL * U;
     ustep = 8;
   } else {
-    const long long waves = min((long long)gridDim.x * 8, (long long)SQ_DSEG_WAVES);
+    // 2048 waves at most while the runs are short (few moved rows: few
+    // flushes); a long list (a first iteration: every row enters) spreads
+    // over the whole grid in runs of >= 512 entries - 2048 waves alone leave
+    // two waves per SIMD on a serial perm -> row gather chain (3.8 ms for
+    // the 10M-row first iteration)
+    const long long waves = min((long long)gridDim.x * 8,
+                                max((long long)SQ_DSEG_WAVES, total / 512));
     const long long rw = max((long long)SQ_DSEG_RUN, (total + waves - 1) / waves);
     p0 = ((long long)blockIdx.x * 8 + wave) * rw;
     p1 = min(total, p0 + rw);
@@ -1042,13 +1048,20 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
       if (q != 0.0) atomicAdd(&qsum[cur], q);
     }
   };
+  // the next batch's entries are loaded while this batch's rows stream in:
+  // one memory latency per batch, not the perm -> row chain of two
+  int2 en[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long q = p0 + ustep * u;
+    en[u] = q < p1 ? perm[q] : make_int2(0, -1);
+  }
   for (long long p = p0; p < p1; p += pstep) {
     int ll[U], out[U];
     float4 v[U][M];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long q = p + ustep * u;
-      const int2 e = q < p1 ? perm[q] : make_int2(0, -1);
+      const int2 e = en[u];
       const int r = e.x;
       ll[u] = e.y < 0 ? -1 : (e.y & 0x3FFFFFFF);
       out[u] = (e.y >> 30) & 1;
@@ -1058,6 +1071,11 @@ __global__ void __launch_bounds__(512) delta_segment_kernel(
         v[u][m] = (ll[u] >= 0 && c0 < d) ? *reinterpret_cast<const float4*>(X + (size_t)r * d + c0)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long q = p + pstep + ustep * u;
+      en[u] = q < p1 ? perm[q] : make_int2(0, -1);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
