@@ -1018,52 +1018,78 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
   const double sm = *smax;
   const long long c0 = (long long)blockIdx.x * kBoundsChunk;
   unsigned long long act = 0, rec = 0;   // bit p: row c0 + p * 256 + tid
-#pragma unroll 4
-  for (int p = 0; p < PER; ++p) {
-    const long long i = c0 + (long long)p * 256 + tid;
-    if (i >= n) break;
-    const int l = labels[i];
-    const double u = (double)ub[i] + (l >= 0 ? shift[l] : 1e300);
-    const int mf = mflag[i];
-    // the moved lower bound lb0 -> w (every centroid except the label)
-    auto wbound = [&](double lb0) -> double {
-      double w = lb0 - sm;
-      // the nf fastest centroids (excluded from sm): the better of Elkan's
-      // bound through the label, |x - c_f'| >= |c_l' - c_f'| - |x - c_l'| >=
-      // cc[l][f] - u, and the moved lower bound lb - s_f
-      if (l >= 0 && nf > 0 && w > 0.0) {   // (w <= 0: active anyway)
-        // cheap form first: every fast centroid is at least cmin[l] from the
-        // label and moved at most s_F = max_f s_f
-        const double wc = fmin(w, fmax((double)cc[(size_t)k * nf + l] - u, lb0 - sf_s[nf]));
-        if (wc > 0.0 && wc * wc - u * u > delta * (1.0 + 1e-9) + 1e-30) {
-          w = wc;
-        } else {   // per fast centroid (tighter)
-          const float* cl = cc + (size_t)l * nf;
-          if ((nf & 3) == 0) {
-            for (int f = 0; f < nf; f += 4) {
-              const float4 c4 = *reinterpret_cast<const float4*>(cl + f);
-              w = fmin(w, fmax((double)c4.x - u, lb0 - sf_s[f]));
-              w = fmin(w, fmax((double)c4.y - u, lb0 - sf_s[f + 1]));
-              w = fmin(w, fmax((double)c4.z - u, lb0 - sf_s[f + 2]));
-              w = fmin(w, fmax((double)c4.w - u, lb0 - sf_s[f + 3]));
+  // rows in batches of 4: every load of a batch (the row's label / bounds /
+  // flag, then the label's shift and Elkan minimum) is issued before any of
+  // the batch's math - a thread's PER rows are 3 dependent-load latencies
+  // per batch, not per row
+  constexpr int B = PER % 4 == 0 ? 4 : 1;
+  for (int p0 = 0; p0 < PER; p0 += B) {
+    int lv[B], mfv[B];
+    float ubv[B], lbv[B];
+    bool inb[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const long long i = c0 + (long long)(p0 + q) * 256 + tid;
+      inb[q] = i < n;
+      const long long ii = inb[q] ? i : 0;
+      lv[q] = inb[q] ? labels[ii] : -1;
+      ubv[q] = ub[ii];
+      lbv[q] = lb[ii];
+      mfv[q] = mflag[ii];
+    }
+    double shv[B];
+    float cmv[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int l = lv[q];
+      shv[q] = l >= 0 ? shift[l] : 1e300;
+      cmv[q] = (l >= 0 && nf > 0) ? cc[(size_t)k * nf + l] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (!inb[q]) continue;
+      const int p = p0 + q;
+      const long long i = c0 + (long long)p * 256 + tid;
+      const int l = lv[q];
+      const double u = (double)ubv[q] + shv[q];
+      // the moved lower bound lb0 -> w (every centroid except the label)
+      auto wbound = [&](double lb0) -> double {
+        double w = lb0 - sm;
+        // the nf fastest centroids (excluded from sm): the better of Elkan's
+        // bound through the label, |x - c_f'| >= |c_l' - c_f'| - |x - c_l'| >=
+        // cc[l][f] - u, and the moved lower bound lb - s_f
+        if (l >= 0 && nf > 0 && w > 0.0) {   // (w <= 0: active anyway)
+          // cheap form first: every fast centroid is at least cmin[l] from the
+          // label and moved at most s_F = max_f s_f
+          const double wc = fmin(w, fmax((double)cmv[q] - u, lb0 - sf_s[nf]));
+          if (wc > 0.0 && wc * wc - u * u > delta * (1.0 + 1e-9) + 1e-30) {
+            w = wc;
+          } else {   // per fast centroid (tighter)
+            const float* cl = cc + (size_t)l * nf;
+            if ((nf & 3) == 0) {
+              for (int f = 0; f < nf; f += 4) {
+                const float4 c4 = *reinterpret_cast<const float4*>(cl + f);
+                w = fmin(w, fmax((double)c4.x - u, lb0 - sf_s[f]));
+                w = fmin(w, fmax((double)c4.y - u, lb0 - sf_s[f + 1]));
+                w = fmin(w, fmax((double)c4.z - u, lb0 - sf_s[f + 2]));
+                w = fmin(w, fmax((double)c4.w - u, lb0 - sf_s[f + 3]));
+              }
+            } else {
+              for (int f = 0; f < nf; ++f) w = fmin(w, fmax((double)cl[f] - u, lb0 - sf_s[f]));
             }
-          } else {
-            for (int f = 0; f < nf; ++f) w = fmin(w, fmax((double)cl[f] - u, lb0 - sf_s[f]));
           }
         }
+        return w;
+      };
+      const double w = wbound((double)lbv[q]);
+      const bool holds = l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30;
+      if (!holds) {
+        act |= 1ull << p;
+      } else {
+        ub[i] = (float)u * (1.0f + 0x1p-22f);
+        lb[i] = (float)w * (1.0f - 0x1p-22f);
+        if (mfv[q]) rec |= 1ull << p;
       }
-      return w;
-    };
-    auto holds = [&](double w) {
-      return l >= 0 && w > 0.0 && w * w - u * u > delta * (1.0 + 1e-9) + 1e-30;
-    };
-    const double w = wbound((double)lb[i]);
-    if (!holds(w)) {
-      act |= 1ull << p;
-    } else {
-      ub[i] = (float)u * (1.0f + 0x1p-22f);
-      lb[i] = (float)w * (1.0f - 0x1p-22f);
-      if (mf) rec |= 1ull << p;
     }
   }
   // block-wide exclusive scan of both per-thread counts (packed 16 | 16 bits:
@@ -1105,6 +1131,8 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
   }
 }
 
+// rcount and multi_count must be zero on entry (the caller clears them with
+// the E-step's other counters in one fill).
 extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const void* shift,
                                 const void* smax, long long n, double delta, void* rlist,
                                 void* rcount, const void* mflag, void* mrows, void* multi_count,
@@ -1113,12 +1141,29 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
   if (!mflag || !mrows || !multi_count) return (int)hipErrorInvalidValue;
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  hipMemsetAsync(rcount, 0, sizeof(int), st);
   // rows per thread: the smallest PER whose grid fits ONE resident round
-  // (8 workgroups of 256 threads per CU at 62 VGPRs, 256 CUs): a second,
-  // mostly empty round doubled the kernel at 10M rows (2442 blocks of 4096)
-  auto pick = [&](int per) { return (n + per * 256LL - 1) / (per * 256LL) <= 2048; };
-  const int per = pick(4) ? 4 : pick(8) ? 8 : pick(16) ? 16 : pick(20) ? 20 : pick(32) ? 32 : 64;
+  // (workgroups per CU from the occupancy query x CUs): a second, mostly
+  // empty round doubled the kernel at 10M rows (2442 blocks of 4096)
+  static long long resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)bounds_filter_kernel<32>,
+                                                 256, 0);
+    resident = (long long)(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 4);
+  }
+  auto pick = [&](int per) { return (n + per * 256LL - 1) / (per * 256LL) <= resident; };
+  static const int per_env = [] {   // SQ_BF_PER: a fixed PER (measurements)
+    const char* e = getenv("SQ_BF_PER");
+    return e ? atoi(e) : 0;
+  }();
+  // (at least 8: the per-workgroup setup and list atomics dominate 4 rows
+  // per thread - measured 38.8 vs 28.4 us on a 1.25M-row shard)
+  int per = pick(8) ? 8 : pick(16) ? 16 : pick(20) ? 20 : pick(32) ? 32 : 64;
+  if (per_env == 4 || per_env == 8 || per_env == 16 || per_env == 20 || per_env == 32 ||
+      per_env == 64)
+    per = per_env;
   const long long blocks = (n + per * 256LL - 1) / (per * 256LL);
   auto kern = per == 4 ? bounds_filter_kernel<4> : per == 8 ? bounds_filter_kernel<8>
             : per == 16 ? bounds_filter_kernel<16> : per == 20 ? bounds_filter_kernel<20>

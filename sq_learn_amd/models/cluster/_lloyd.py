@@ -364,6 +364,8 @@ class LloydEngine:
                 if mode == "filter":
                     self._filter_ran = True
                     K.ensure_multi_buffers(self.buf, self.n, self.device, True)
+                    # one fill clears the E-step counters and the kept count
+                    self.rcount = self.buf.counts[3:4]
                     self.buf.counts.zero_()
                     K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
                                            self.shift_s, self.smax, self.delta, self.rlist,

@@ -178,9 +178,9 @@ class EStepBuffers:
         self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(n, 1))
         self.ovf_rows = torch.empty(self.ovf_cap, dtype=torch.int64, device=device)
         self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
-        # [overflow rows, dense rows, multi-candidate rows] (int32); ovf_count
-        # is a view of slot 0
-        self.counts = torch.zeros(3, dtype=torch.int32, device=device)
+        # [overflow rows, dense rows, multi-candidate rows, rows the bounds
+        # filter kept] (int32); ovf_count is a view of slot 0
+        self.counts = torch.zeros(4, dtype=torch.int32, device=device)
         self.exact_flag = None   # the fp32 screen's hand-off flags (per multi entry)
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
@@ -377,7 +377,9 @@ def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf:
     their candidate set go to ``rlist`` (count in ``rcount``, on the device);
     pruned multi-candidate rows are appended to ``buf``'s multi list (their
     per-row candidate lists stay valid) for the fp64 re-check.
-    ``buf.counts`` must be zeroed before (the multi count accumulates).
+    ``buf.counts`` and ``rcount`` must be zeroed before (the counts
+    accumulate; the E-step keeps rcount in ``buf.counts[3]``, so one fill
+    clears both).
     ``cc`` [k nf + k] fp32 / ``nf``: the fastest centroids' Elkan distances
     (:func:`fast_centroids_native`; ``smax`` then excludes them)."""
     n = labels.numel()

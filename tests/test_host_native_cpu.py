@@ -364,3 +364,9 @@ def test_stream_handle_makes_the_target_device_current(monkeypatch):
     assert nat.stream_handle("cuda:1") == 1001 and state["set"] == [1] and state["cur"] == 1
     assert nat.stream_handle(torch.device("cuda", 1)) == 1001 and state["set"] == [1]
     assert nat.stream_handle("cuda:0") == 1000 and state["set"] == [1, 0]
+    # the fast path (direct torch C calls once CUDA is up) keeps the guard
+    monkeypatch.setattr(nat, "_FAST_STREAM", (lambda: state["cur"], lambda idx: 2000 + idx))
+    assert nat.stream_handle("cuda:1") == 2001 and state["set"] == [1, 0, 1]
+    assert nat.stream_handle(torch.device("cuda", 1)) == 2001 and state["set"] == [1, 0, 1]
+    assert nat.stream_handle(None) == 2001
+    assert nat.stream_handle("cuda:0") == 2000 and state["set"] == [1, 0, 1, 0]
