@@ -1776,7 +1776,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
-                            void* ub, void* lb, void* mflag, void* xflag) {
+                            void* ub, void* lb, void* mflag, void* xflag, int list_rs) {
   // list mode (the rows the bounds could not prune): one row set per wave -
   // half the rows per workgroup, so a short list (the per-GPU share of a
   // strong-scaled run) finishes in one half-length sweep; a full sweep keeps
@@ -1819,7 +1819,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
     const char* e = getenv("SQ_X64_LIST_RS1");
     return !(e && e[0] == '0');
   }();
-  if (rlist && list_rs1)
+  // list_rs (host hint): 1 / 2 row sets in list mode, 0 = the default (1)
+  if (rlist && (list_rs == 1 || (list_rs == 0 && list_rs1)))
     go(std::integral_constant<int, 1>{});
   else
     go(std::integral_constant<int, X64RowSets<KSD>::value>{});
@@ -1907,7 +1908,7 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
                  void* lb, void* mflag, void* xflag, void* counts, void* part, int part_cap, long long n, int d, int d_pad,
                  int k,
                  int k_pad, double alpha, double delta, unsigned k0, unsigned k1, unsigned s0,
-                 unsigned s1, long long row_offset, void* stream) {
+                 unsigned s1, long long row_offset, int list_rs, void* stream) {
   if (n <= 0) return 0;
   if (k_pad % kTileN != 0 || k_pad <= 0 || k_pad > 32768 || k > k_pad || d > d_pad)
     return (int)hipErrorInvalidValue;
@@ -1931,7 +1932,8 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   case KSD * 16:                                                                                 \
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
-                               row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag);        \
+                               row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag,         \
+                               list_rs);                                                         \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, cap, st, dense_rows,       \
@@ -1951,7 +1953,8 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   case KSD * 16:                                                                                 \
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
-                               row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag);        \
+                               row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag,         \
+                               list_rs);                                                         \
     if (rc) return rc;                                                                           \
     rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, dense_rows, cnt + 1, 0, n, labels, mind,      \
                      corr, ub, delta, k0, k1, s0, s1, row_offset, (int)fgrid, stream);           \

@@ -98,7 +98,7 @@ __attribute__((weak)) int sq_estep_x64(const void*, const void*, const void*, co
                                        void*, void*, void*, void*, void*, void*, void*, void*,
                                        void*, void*, int, long long, int, int, int, int, double,
                                        double, unsigned,
-                                       unsigned, unsigned, unsigned, long long, void*);
+                                       unsigned, unsigned, unsigned, long long, int, void*);
 __attribute__((weak)) int sq_fill_mind(const void*, int, const void*, int, const void*, void*,
                                        long long, void*);
 __attribute__((weak)) int sq_sum_f32(const void*, long long, void*, int, void*, void*);
@@ -413,17 +413,19 @@ static PyObject* py_centroid_reduce(PyObject*, PyObject* a) {
 static PyObject* py_estep_x64(PyObject*, PyObject* a) {
   unsigned long long Xh, X, C, Cm, xn, cm2, lab, mind, dr, ovr, mr, mc, corr, rl, rc, ub, lb, ms,
       xr, cnt, part, st;
-  int pcap, d, dp, k, kp; long long n, roff; double alpha, delta; unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKKKKKKKiLiiiiddIIIILK", &Xh, &X, &C, &Cm, &xn, &cm2,
+  int pcap, d, dp, k, kp, list_rs = 0; long long n, roff; double alpha, delta;
+  unsigned k0, k1, s0, s1;
+  if (!PyArg_ParseTuple(a, "KKKKKKKKKKKKKKKKKKKKKiLiiiiddIIIILK|i", &Xh, &X, &C, &Cm, &xn, &cm2,
                         &lab, &mind, &dr, &ovr, &mr, &mc, &corr, &rl, &rc, &ub, &lb, &ms, &xr, &cnt,
                         &part, &pcap,
-                        &n, &d, &dp, &k, &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st))
+                        &n, &d, &dp, &k, &kp, &alpha, &delta, &k0, &k1, &s0, &s1, &roff, &st,
+                        &list_rs))
     return nullptr;
   CHECK(sq_estep_x64)
   return ret(sq_estep_x64(P(Xh), P(X), P(C), P(Cm), P(xn), P(cm2), P(lab), P(mind), P(dr), P(ovr),
                           P(mr), P(mc), P(corr), P(rl), P(rc), P(ub), P(lb), P(ms), P(xr), P(cnt),
                           P(part), pcap,
-                          n, d, dp, k, kp, alpha, delta, k0, k1, s0, s1, roff, P(st)));
+                          n, d, dp, k, kp, alpha, delta, k0, k1, s0, s1, roff, list_rs, P(st)));
 }
 
 static PyObject* py_fill_mind(PyObject*, PyObject* a) {

@@ -220,6 +220,7 @@ class LloydEngine:
         self._kept_frac = None
         self._kept_prev = None
         self._skips = 0
+        self._probing = False
         self._filter_ran = False
         self._minus1 = torch.full((1,), -1, dtype=torch.int32, device=dev)
         if self.bounds:
@@ -294,6 +295,7 @@ class LloydEngine:
         self.bounds_valid = False
         self._kept_frac = self._kept_prev = None   # new centres: re-measure the filter
         self._skips = 0
+        self._probing = False
         self._probe_gap = getattr(self, "probe_every", 2)
         self._sc_dev = None
         if self.fast:
@@ -361,6 +363,13 @@ class LloydEngine:
                 # dormant bounds are not maintained by this sweep: invalid
                 # until a bounds-maintaining sweep (the step before a probe)
                 self._bounds_kept = mode != "none"
+                # a probe (the filter kept > keep_max of the rows twice and was
+                # skipped since) only MEASURES: the filter pass counts the rows
+                # it would keep (the M-step records the fraction), the sweep
+                # stays full and maintains the bounds - a probe costs one
+                # filter pass, not a near-full list sweep
+                probe = mode == "filter" and self._probing
+                zero = True
                 if mode == "filter":
                     self._filter_ran = True
                     K.ensure_multi_buffers(self.buf, self.n, self.device, True)
@@ -371,13 +380,17 @@ class LloydEngine:
                                            self.shift_s, self.smax, self.delta, self.rlist,
                                            self.rcount, self.buf, cc=self.fast_cc,
                                            nf=self.n_fast, fidx=self.fast_idx)
-                    rows = (self.rlist, self.rcount)
+                    if probe:
+                        self.buf.counts[:3].zero_()   # the full sweep lists from scratch
+                    else:
+                        rows = (self.rlist, self.rcount)
+                    zero = False
                 lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
                                                self.cmax2, self.k, self.delta, self.alpha, key,
                                                self.row_offset, self.buf,
                                                bounds=(self.ub, self.lb)
                                                if self.bounds and self._bounds_kept else None,
-                                               rows=rows, zero_counts=rows is None,
+                                               rows=rows, zero_counts=zero,
                                                screen=self.incremental and not full
                                                and os.environ.get("SQ_SCREEN", "1") != "0")
             return lab, mind, self.buf.inertia
@@ -410,6 +423,7 @@ class LloydEngine:
             self._sc_dev = None
             self._on_scalars(sd.tolist())
         kf, kp = self._kept_frac, self._kept_prev
+        self._probing = False
         if kf is None or kp is None or kf <= self.keep_max or kp <= self.keep_max:
             self._skips = 0
             self._probe_gap = self.probe_every
@@ -417,9 +431,11 @@ class LloydEngine:
         self._skips += 1
         gap = getattr(self, "_probe_gap", self.probe_every)
         if self._skips >= gap:
-            # a probe at ~100 % kept costs ~1.2 full sweeps: back off
+            # a probe of a filter that kept > keep_max twice: back off (the
+            # probe measures the kept fraction over a full sweep, see _estep)
             self._skips = 0
             self._probe_gap = min(2 * gap, 16)
+            self._probing = True
             return "filter"
         return "bounds" if self._skips == gap - 1 else "none"
 
@@ -662,9 +678,10 @@ class LloydEngine:
                 if self.bounds:
                     self.shift_part[:self.k].copy_(
                         ((self.C.double() - self.C_new.double()) ** 2).sum(1))
-            if self.bounds:
+            if self.bounds and getattr(self, "_bounds_kept", True):
                 # per-centroid shifts of this update (fp64, rounded up) for the
-                # next E-step's Hamerly bound update
+                # next E-step's Hamerly bound update (after a sweep that left the
+                # bounds dormant nothing reads them: the next E-step rebuilds)
                 if self.n_fast > 0 and self.device.type == "cuda":
                     # sqrt + margin fused into the top-shift select
                     K.fast_centroids_native(self.shift_s, self.C, self.n_fast, self.fast_idx,
@@ -674,6 +691,7 @@ class LloydEngine:
                     torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
                     self.shift_s.mul_(1.0 + 1e-12)
                     torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
+            if self.bounds:
                 self.bounds_valid = getattr(self, "_bounds_kept", True)
         return self.scalars
 

@@ -709,7 +709,7 @@ def rows_f64_native(X, C, labels, mind, delta, key: RngKey, row_offset, rows=Non
 
 def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKey, row_offset,
                      buf: EStepBuffers, stream=None, bounds=None, rows=None, zero_counts=True,
-                     screen=False):
+                     screen=False, list_rs=0):
     """Certified E-step (``estep_x64_kernel``): one fp16 MFMA pass with a
     rigorous error bound, fp64 re-check of the candidate centroids, dense rows
     through the fp32-faithful 3-pass kernel.  Labels are the fp64 delta-band
@@ -723,7 +723,10 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     multi list, so ``zero_counts`` is False).  ``screen``: multi rows go
     through the fp32 screen first (``recheck_fast_kernel``; their ``mind``
     is then fp32 - for steps whose inertia comes from the incremental
-    statistics), the fp64 re-check takes the rest."""
+    statistics), the fp64 re-check takes the rest.  ``list_rs``: row sets
+    per wave of the list-mode sweep (0 = default 1: a short list finishes
+    in one half-length sweep; 2 = the full sweep's tiling, for a list the
+    caller expects to hold nearly every row)."""
     n, d_pad = Xf.shape
     k_pad = C_op.shape[0] * 64
     assert Xf.dtype == torch.float32 and Xf.is_contiguous() and d_pad in X64_D
@@ -753,7 +756,7 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
                            buf.exact_flag.data_ptr() if screen else 0,
                            buf.counts.data_ptr(), buf.inertia_part.data_ptr(), int(buf.part_cap),
                            n, d_pad, d_pad, k, k_pad, float(alpha), float(delta), key.k0, key.k1,
-                           key.s0, key.s1, int(row_offset), st)
+                           key.s0, key.s1, int(row_offset), st, int(list_rs))
     return buf.labels, buf.mind
 
 
