@@ -9,6 +9,6 @@ timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d /tmp/p_head -o r -- \
   --steps 20 --warmup 5 > gpurun_out/prof_head.log 2>&1 || exit 1
 python3 $S $(find /tmp/p_head -name '*.db') --top 30 > gpurun_out/prof_head.md
 python3 scripts/prof_timeline.py /tmp/p_head --marker bounds_filter --first 0 --last 40 > gpurun_out/prof_head_timeline.md
-for i in 44 45; do python3 scripts/prof_timeline.py /tmp/p_head --marker bounds_filter --first $i --last 1 > gpurun_out/prof_head_iv$i.md; done
+for i in 20 21; do python3 scripts/prof_timeline.py /tmp/p_head --marker bounds_filter --first $i --last 1 > gpurun_out/prof_head_iv$i.md; done
 rm -rf /tmp/p_head
 echo done
