@@ -92,3 +92,36 @@ def test_hamerly_pruning_is_exact(cuda, delta, tomo):
             active.append(int(a.rcount.item()))
     if not tomo:   # (shot tomography moves every centroid far each step)
         assert min(active) < 0.5 * 80000, active
+
+
+def test_adaptive_filter_modes_are_exact(cuda):
+    """The adaptive Hamerly policy's every mode - filter, dormant bounds
+    ('none'), bound-maintaining sweeps ('bounds') and measure-only probes -
+    gives labels and centroids BIT-identical to the bounds-off engine
+    (keep_max = 0 treats every measured kept fraction as too high, so the
+    skip / probe cycle runs from the third step on)."""
+    X, _ = make_blobs(60000, 64, centers=30, cluster_std=1.0, random_state=4)
+    Xt = torch.tensor(X, dtype=torch.float32, device=cuda)
+    k = 32
+    C0 = Xt[torch.as_tensor(np.random.RandomState(5).choice(60000, k, replace=False), device=cuda)]
+    a = _engine_b(Xt, k, 0.5, True)
+    b = _engine_b(Xt, k, 0.5, False)
+    a.keep_max = 0.0
+    a.set_centers(C0)
+    b.set_centers(C0)
+    modes = []
+    orig = a._filter_mode
+
+    def spy():
+        m = orig()
+        modes.append("probe" if (m == "filter" and a._probing) else m)
+        return m
+
+    a._filter_mode = spy
+    for it in range(14):
+        la, sa = a.step()
+        lb, sb = b.step()
+        assert torch.equal(la, lb), f"labels differ at iteration {it} ({modes[-1:]})"
+        assert torch.equal(a.C, b.C), f"centroids differ at iteration {it}"
+        assert sa.tolist()[0] == sb.tolist()[0]
+    assert {"none", "bounds", "probe"} <= set(modes), modes
