@@ -212,7 +212,7 @@ def _share8_extra(extra, a, X, comm, dev, C0):
         extra["share8_error"] = repr(e)[:200]
 
 
-def _hard_extra(extra, a, comm, dev):
+def _hard_extra(extra, a, comm, dev, unpruned=True):
     """A hard regime for the certified E-step: 1024 strongly overlapping
     blobs (centres in [-0.1, 0.1]^d, spread 0.4: a mean delta-band of ~3
     members, ~60 % multi-candidate rows) so that most rows have several
@@ -260,7 +260,7 @@ def _hard_extra(extra, a, comm, dev):
         comm.all_reduce_(tot)
         extra["hard_dense_row_frac"] = float(tot[0]) / n
         extra["hard_multi_row_frac"] = float(tot[1]) / n
-        if getattr(eng, "bounds", False):
+        if unpruned and getattr(eng, "bounds", False):
             # the same iterations (1 .. 10 from the same centres) with the
             # Hamerly bounds off, on a fresh engine: like for like
             C_last = eng.centers().clone()

@@ -117,6 +117,14 @@ def _validate_fit_X(est, X):
                              "encoded as NaN natively.")
 
 
+def _current_cuda_device():
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return None
+    return torch.cuda.current_device()
+
+
 def _validating_fit(fit):
     try:
         names = [p for p in inspect.signature(fit).parameters][1:]
@@ -134,7 +142,15 @@ def _validating_fit(fit):
             sw = (args[i_sw] if i_sw is not None and len(args) > i_sw
                   else kwargs.get("sample_weight"))
             _validate_fit_y_sw(self, X, y, sw)
-        return fit(self, *args, **kwargs)
+        # native launches make the data's GPU the thread's current device
+        # (ops._native.stream_handle): give the caller back its own afterwards
+        prev = _current_cuda_device()
+        try:
+            return fit(self, *args, **kwargs)
+        finally:
+            if prev is not None and _current_cuda_device() != prev:
+                import torch
+                torch.cuda.set_device(prev)
     fit_validated._sq_validated = True
     return fit_validated
 

@@ -35,8 +35,8 @@ class ElkanEngine(LloydEngine):
         self.cshift = torch.zeros(self.k, dtype=dt, device=self.device)
         self._fresh = True
 
-    def set_centers(self, C):
-        super().set_centers(C)
+    def set_centers(self, C, reset_hints=True):
+        super().set_centers(C, reset_hints=reset_hints)
         self._fresh = True
 
     def estep(self, C=None):

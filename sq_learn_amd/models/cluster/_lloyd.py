@@ -61,7 +61,9 @@ class _HostScalars:
         self.event.synchronize()
         vals = self.host.tolist()
         if self.sink is not None:
-            self.sink(vals)
+            # one measurement per iteration, however often the caller reads
+            sink, self.sink = self.sink, None
+            sink(vals)
         return vals
 
 
@@ -288,9 +290,15 @@ class LloydEngine:
         bounds, every processed row gets the same label)."""
         self._pending = None
 
-    def set_centers(self, C):
+    def set_centers(self, C, reset_hints=True):
         self._pending = None
         C = C.to(self.device)
+        if reset_hints and getattr(self, "_ipe_lab", None) is not None:
+            # new centres (a restart, the final E-step): the IPE label hints
+            # of the previous trajectory must not seed this one, so every
+            # restart and a resumed fit see the same (empty) hints
+            for h in self._ipe_lab:
+                h.fill_(-1)
         self.inc_valid = False   # the incremental M-step restarts from scratch
         self.bounds_valid = False
         self._kept_frac = self._kept_prev = None   # new centres: re-measure the filter
@@ -323,6 +331,28 @@ class LloydEngine:
         if self.C_op is not None:
             return {"C_op": self.C_op}
         return {"C_bf16": self.C_bf16, "cn": self.cn}
+
+    def checkpoint_local(self):
+        """Per-rank state that must round-trip on resume: the IPE label
+        hints (the previous E-step's labels seed the next one's thresholds,
+        so they pick the realisation - ``ipe.hip`` hazard screen)."""
+        if getattr(self, "_ipe_lab", None) is None:
+            return {}
+        return {"ipe_hint": self._ipe_lab[self._ipe_cur]}
+
+    def restore_local(self, d):
+        t = d.get("ipe_hint") if d else None
+        if t is None or not self.ipe:
+            return
+        self._ipe_buffers()
+        self._ipe_lab[self._ipe_cur].copy_(t.to(self.device).to(torch.int32))
+
+    def _ipe_buffers(self):
+        if getattr(self, "_ipe_lab", None) is None:
+            self._ipe_lab = [torch.full((self.n,), -1, dtype=torch.int32, device=self.device)
+                             for _ in range(2)]
+            self._ipe_cur = 0
+            self._ipe_xn = self.xn.float().contiguous()
 
     def restore_tensors(self, d):
         self._pending = None
@@ -479,11 +509,7 @@ class LloydEngine:
             # buffers alternate, so the labels returned by the last step stay
             # valid through the next one
             n = self.n
-            if getattr(self, "_ipe_lab", None) is None:
-                self._ipe_lab = [torch.full((n,), -1, dtype=torch.int32, device=self.device)
-                                 for _ in range(2)]
-                self._ipe_cur = 0
-                self._ipe_xn = self.xn.float().contiguous()
+            self._ipe_buffers()
             hint = self._ipe_lab[self._ipe_cur]
             self._ipe_cur ^= 1
             labels32 = self._ipe_lab[self._ipe_cur]
@@ -712,7 +738,7 @@ class LloydEngine:
         # a centroid update, not a restart: the incremental statistics stay
         # valid (label based) and the bounds move by the recomputed shifts
         flags = (self.inc_valid, self.bounds_valid)
-        self.set_centers(est.to(self.C.dtype))
+        self.set_centers(est.to(self.C.dtype), reset_hints=False)
         self.inc_valid, self.bounds_valid = flags
 
     # ---------------------------------------------------------- iteration

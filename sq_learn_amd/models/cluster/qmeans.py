@@ -255,7 +255,9 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                 engine.it = int(st["it"])
                 inner = dict(best_inertia=st["r_best_inertia"], best_centers=st["r_best_centers"],
                              best_labels=loc.get("r_best_labels"), shift=float(st["shift"]),
-                             engine={k[7:]: v for k, v in st.items() if k.startswith("engine_")})
+                             engine={k[7:]: v for k, v in st.items() if k.startswith("engine_")},
+                             engine_local={k[7:]: v for k, v in loc.items()
+                                           if k.startswith("engine_")})
             else:
                 C0 = self._init_centroids(data_c, self.init, rs, xn, mean)
                 inner = None
@@ -320,6 +322,7 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         engine.comm.all_reduce_(cnt)   # fit-wide totals, like the attributes
         state["failure_counters"] = cnt
         local = dict(r_best_labels=best_labels.to(torch.int32))
+        local.update({f"engine_{k}": v for k, v in engine.checkpoint_local().items()})
         if outer is not None:
             local["best_labels"] = outer[0].to(torch.int32)
         ctx["ckpt"].save(state, local)
@@ -334,6 +337,7 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         if resume is not None:
             first = engine.it
             engine.restore_tensors(resume["engine"])
+            engine.restore_local(resume.get("engine_local"))
             best_inertia = float(resume["best_inertia"])
             best_centers = resume["best_centers"].to(engine.device).to(engine.centers().dtype)
             best_labels = resume["best_labels"].to(engine.device)

@@ -233,8 +233,13 @@ def col_moments_local(X):
     of X."""
     n, d = X.shape
     if nat.use_native(X) and X.dtype in (torch.float32, torch.bfloat16) and n > 0:
-        wgs = 2048
-        part = torch.zeros((wgs, 2 * d), dtype=torch.float64, device=X.device)
+        # the launcher's own partition (sq_col_moments): every one of its
+        # wgs blocks writes its row of partials, so no zero-fill and no rows
+        # beyond the ones used (ADVICE r4: 2048 x 2d was ~2 GiB at d = 65k)
+        wgs = min(2048, max(1, -(-n // 256)))
+        rpw = -(-n // wgs)
+        wgs = -(-n // rpw)
+        part = torch.empty((wgs, 2 * d), dtype=torch.float64, device=X.device)
         rc = nat.native().col_moments(X.data_ptr(), nat.dtype_code(X), X.stride(0), n, d,
                                       part.data_ptr(), wgs, nat.stream_handle(X.device))
         if rc:

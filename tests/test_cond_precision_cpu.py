@@ -41,3 +41,31 @@ def test_rank_deficient_falls_back():
     A = rng.standard_normal((5000, 6))
     X = np.hstack([A, A[:, :2]])          # rank 6 of 8
     assert sigma_min(as_data(X, device="cpu")) < 1e-5
+
+
+def test_single_pass_cholqr_tolerance_at_cond_100(monkeypatch):
+    """cond(R1) <= 100 skips CholeskyQR2's second pass (ops.linalg.cholqr2_r):
+    the singular values then carry ~eps64 cond^2 <= 2.2e-12 relative error
+    and the right singular vectors ~that over the relative gap.  Pinned here
+    against LAPACK at cond = 90, the worst case the shortcut accepts."""
+    from sq_learn_amd.ops import linalg as L
+    calls = {"n": 0}
+    orig = L.gram64_local
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(L, "gram64_local", counting)
+    X = _matrix(40000, 16, 90.0, 3)
+    d = as_data(X, device="cpu")
+    mean = torch.zeros(16, dtype=torch.float64)
+    res = full_svd(d, mean, 4, method="cholqr2")
+    assert res.method == "cholqr2" and calls["n"] == 1     # one pass over X
+    _, S, Vt = np.linalg.svd(X, full_matrices=False)
+    np.testing.assert_allclose(res.S, S, rtol=3e-12)
+    gap = np.min(np.abs(np.diff(S)) / S[:-1])
+    for i in range(16):
+        c = abs(float(np.dot(res.Vt[i], Vt[i])))
+        assert 1.0 - c <= (3e-12 / gap) ** 2 + 1e-15
+        assert np.linalg.norm(abs(res.Vt[i]) - abs(Vt[i])) <= 3e-11 / gap

@@ -157,3 +157,16 @@ def test_ipe_labels_and_inertia_law_match_reference(R):
     assert (cr > 0).sum() >= 6                     # the labels really vary
     assert _contingency(cr.ravel(), co.ravel()) > P_MIN
     assert stats.ks_2samp(ir, io).pvalue > P_MIN
+
+
+def test_gpu_fixture_is_the_references_output(R):
+    """tests/fixtures/dmeans_ref.npz (what the GPU-box pinned tests compare
+    against) is exactly what the reference functions produce."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures"))
+    import make_dmeans_ref
+    f, z = make_dmeans_ref.load()
+    got = make_dmeans_ref.generate(R)
+    for key in ("cnt1", "inert1", "means2", "cnt3", "inert3"):
+        np.testing.assert_array_equal(got[key], z[key], err_msg=key)

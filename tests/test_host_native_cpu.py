@@ -370,3 +370,23 @@ def test_stream_handle_makes_the_target_device_current(monkeypatch):
     assert nat.stream_handle(torch.device("cuda", 1)) == 2001 and state["set"] == [1, 0, 1]
     assert nat.stream_handle(None) == 2001
     assert nat.stream_handle("cuda:0") == 2000 and state["set"] == [1, 0, 1, 0]
+
+
+def test_fit_restores_the_callers_current_device(monkeypatch):
+    """A fit whose native launches switched the thread to the data's GPU gives
+    the caller its previous current device back (later user
+    allocations on 'cuda' must not land on the fit's device)."""
+    import torch
+    from sq_learn_amd.base import BaseEstimator
+    state = {"cur": 0}
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: state["cur"])
+    monkeypatch.setattr(torch.cuda, "set_device", lambda i: state.update(cur=i))
+
+    class _Est(BaseEstimator):
+        def fit(self, X, y=None):
+            state["cur"] = 1     # what stream_handle('cuda:1') does
+            return self
+
+    _Est().fit([[0.0, 1.0], [1.0, 0.0]])
+    assert state["cur"] == 0

@@ -59,6 +59,65 @@ def test_gpu_fit_checkpoint_resume(cuda, tmp_path):
     assert got.n_failed_rows_ > 0
 
 
+@pytest.mark.parametrize("n_init", [1, 2])
+def test_gpu_ipe_fit_checkpoint_resume(cuda, tmp_path, n_init):
+    """IPE distances (true_distance_estimate=True, delta > 0): the label hints
+    that seed each E-step's thresholds are per-rank checkpoint state and are
+    reset on new centres, so a resumed fit (and every restart) repeats the
+    uninterrupted one bit for bit."""
+    from sq_learn_amd.cluster import QMeans
+    from sq_learn_amd.models.cluster._lloyd import LloydEngine
+    from sq_learn_amd.utils.datasets import make_blobs
+    X, _ = make_blobs(n_samples=20_000, centers=12, n_features=24, cluster_std=2.0,
+                      random_state=3)
+    Xt = torch.as_tensor(X, dtype=torch.float32, device=cuda)
+    kw = dict(n_clusters=12, n_init=n_init, max_iter=6, tol=0.0, delta=0.5, random_state=2,
+              true_distance_estimate=True, intermediate_error=True, true_tomography=False,
+              checkpoint_every=2, compute_prelude=False)
+    ref = QMeans(**kw).fit(Xt)
+    orig = LloydEngine.step
+    calls = {"n": 0}
+
+    def crashing(self):
+        calls["n"] += 1
+        if calls["n"] > 3 + 6 * (n_init - 1):
+            raise KeyboardInterrupt
+        return orig(self)
+
+    ck = str(tmp_path / "ck")
+    LloydEngine.step = crashing
+    try:
+        with pytest.raises(KeyboardInterrupt):
+            QMeans(checkpoint_dir=ck, **kw).fit(Xt)
+    finally:
+        LloydEngine.step = orig
+    got = QMeans(checkpoint_dir=ck, **kw).fit(Xt)
+    assert got.resumed_from_[0] == n_init - 1
+    np.testing.assert_array_equal(got.cluster_centers_, ref.cluster_centers_)
+    np.testing.assert_array_equal(got.labels_, ref.labels_)
+
+
+def test_ipe_hints_reset_by_new_centres(cuda):
+    """set_centers clears the IPE label hints: the same (restart, iteration)
+    from the same centres gives the same labels whatever ran before."""
+    from sq_learn_amd.models.cluster._lloyd import LloydEngine
+    from sq_learn_amd.utils.datasets import make_blobs
+    X, _ = make_blobs(n_samples=30_000, centers=16, n_features=40, cluster_std=2.5,
+                      random_state=5)
+    Xt = torch.as_tensor(X, dtype=torch.float32, device=cuda)
+    C0 = Xt[:16].clone()
+    eng = LloydEngine(Xt, 16, delta=0.5, true_distance_estimate=True, intermediate_error=True,
+                      seed=4)
+    eng.set_centers(C0)
+    first = eng.step()[0].clone()
+    for _ in range(3):
+        eng.step()
+    eng.it = 0
+    eng.set_centers(C0)
+    again = eng.step()[0].clone()
+    assert torch.equal(first, again)
+
+
 def test_tomography_kernel_matches_law(cuda):
     """HIP tomography (K12) vs the torch implementation of the same law."""
     from sq_learn_amd.quantum import device as QD
