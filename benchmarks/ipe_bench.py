@@ -44,20 +44,25 @@ def main():
                       true_tomography=False, seed=a.seed, comm=comm, gemm_precision="fp32")
     eng.set_centers(C0)
     eng.ipe_stats = torch.zeros(5, dtype=torch.int64, device=dev)
+    eng.ipe16_stats = torch.zeros(8, dtype=torch.int64, device=dev)
     out = {"rows": a.rows, "k": a.k, "d": a.d, "center": a.center, "steps": []}
     names = ["screened", "full", "fires", "exact", "pass1_wgs"]
+    names16 = ["near", "fired", "fired_exact", "dense_rows", "flagged_rows", "no_band_rows"]
     for s in range(a.steps + 1):
         eng.ipe_stats.zero_()
+        eng.ipe16_stats.zero_()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         eng.step()[1].tolist()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3
         st = dict(zip(names, eng.ipe_stats.tolist()))
-        out["steps"].append({"ms": round(ms, 2), **st})
+        st16 = dict(zip(names16, eng.ipe16_stats.tolist()))
+        out["steps"].append({"ms": round(ms, 2), **st, **{"i16_" + k: v for k, v in st16.items()}})
         print(json.dumps(out["steps"][-1]), flush=True)
     # timed without stats (the production kernel)
     eng.ipe_stats = None
+    eng.ipe16_stats = None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):

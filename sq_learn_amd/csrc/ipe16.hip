@@ -1,0 +1,1053 @@
+// Certified fp16 screen of the IPE E-step of q-means ("l2-sampled" distance
+// estimates, the reference DEFAULT: sklearn/cluster/_dmeans.py:753-772 ->
+// QuantumUtility/Utility.py:697-737).  Same law as ipe.hip,
+// without an fp32 inner product per (row, centroid) pair.
+//
+// The estimator (ipe.hip header): D~ = 2 S a~, a~ the median of Q amplitude
+// estimations of a = (S - 2 ip) / (2 S), S = |x|^2 + |c|^2; label = argmin_j D~.
+// As in ipe.hip every row first samples its HINT pair (the previous labels,
+// or an approximate argmin) in full: thr = D~_hint.  Every other pair can only
+// matter if its estimate falls at or below thr, and its probability of doing
+// so is bounded by the Fejer tail at m = (sqrt(D) - sqrt(thr)) sqrt(S) /
+// (sqrt2 eps max(1, |ip|)) bins (ipe_hazard).  Here that bound is taken PER
+// ROW over a distance band instead of per pair:
+//
+//  * prep (one lane per row): the hint's exact inner product (the canonical
+//    fp32 dot below), thr, and a band [Dl, Dh] of squared distances such that
+//    every pair whose fp32 law distance lies in it passes ipe_hazard with
+//    hazard <= H_row (a rigorous fp64 bound over S in [Smin, Smax] of the
+//    row, every fp32 rounding of the screen covered), translated into the
+//    certified fp16 filter's units (estep_f32.hip estep_x64: v = alpha^2
+//    (|c|^2 - 2 x.c) with the per-row error bound E_i): far iff
+//    Vlo <= v <= Vhi;
+//  * sweep (fp16 v_mfma_f32_32x32x16_f16 over the fp16 copy of alpha x, the
+//    estep_x64 tile ring): a pair is FAR (per-pair cost: one med3 and one
+//    compare) or NEAR (appended to its row's LDS list).  Far pairs never read
+//    their inner product: each (row, column class) stream spends H_row per
+//    pair from an Exp(1) budget (the memoryless construction of ipe.hip), so
+//    its fire positions are known in advance from the budgets alone - they
+//    are listed at the start of the row block, from per-row budgets drawn
+//    hierarchically (the min of the row's 32 Exp(1) ~ Exp(32) from ONE
+//    uniform; only when that min could run out within the row - a few % of
+//    the rows - are the 32 stream budgets drawn: argmin uniform, the others
+//    min + Exp(1));
+//  * near kernel: every listed pair gets the canonical fp32 inner product;
+//    a near pair is sampled in full (ipe_distance, the pair's own Philox
+//    stream), a fired far pair is thinned to the exact law of "D~ if <= thr"
+//    (u = U (1 - exp(-H_row)) < pibar: ipe_pruned_exact); results merge into
+//    the row's (D~, tie key | j) by one 64-bit atomicMin;
+//  * rows with more than kCapR listed pairs ("dense": no usable band, or a
+//    crowded threshold) are left to the fp32 row-group kernel of ipe.hip in
+//    list mode, with the same hint and threshold.
+// Every decision is a function of the row, its hint, the centroids and the
+// Philox keys (global row index): labels do not depend on blocking, list
+// order or the number of ranks.
+//
+// The canonical inner product of a pair (the one the law uses - the reference
+// uses np.inner in fp64; any fixed fp32 order is within ~d 2^-24 |x||c|):
+// lane c16 of a 16-lane group sums f = c16, c16 + 16, ... by fmaf in order,
+// then an xor tree over the 16 lanes (ipe_hint_kernel's order).
+#include "ipe_law.h"
+#include <utility>
+
+namespace sq {
+namespace i16 {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTileN = 64;    // centroids per LDS tile (estep_x64 operand)
+constexpr int kNW = 4;        // waves per workgroup (one per SIMD)
+constexpr int kRS = 2;        // row sets of 32 per wave
+constexpr int kRows = kNW * 32 * kRS;   // 256 rows per block
+constexpr int kRing = 3;      // centroid-tile LDS slots
+constexpr int kCapR = 64;     // listed pairs per row (more: dense)
+constexpr int kNLS = kCapR + 2;   // LDS row stride of the lists (uint16): no bank aliasing
+constexpr int kFireCap = 7;   // listed fires per row (more: dense); [0] of a row's record = count
+
+SQ_DEV float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+SQ_DEV float and_or(float a, uint32_t m, uint32_t q) {
+  float r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(q));
+  return r;
+}
+SQ_DEV float vmed3(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+template <typename F, int... I>
+SQ_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+SQ_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// the row-sorted packed best: (D~ bits, tie key with the centroid in its low
+// 14 bits) - one u64 min orders by (D~, random key), like ipe_better
+SQ_DEV unsigned long long pack_best(float dt, const RngKey& tie, long long g, int j) {
+  const uint32_t tk = (band_key(tie, g, (uint32_t)j) & ~0x3FFFu) | (uint32_t)j;
+  return ((unsigned long long)__float_as_uint(dt) << 32) | (unsigned long long)tk;
+}
+
+// canonical fp32 inner products of B (row, centroid) pairs (stride-1, d <=
+// 16 U values) by the 16 lanes c16 = 0..15 of a group, every lane returning
+// the totals: lane c16 sums f = c16, c16 + 16, ... by fmaf in order (zeros
+// past d add +0), then an xor tree over the 16 lanes.  All B pairs' loads
+// are issued before the first fma (one memory latency per batch, not one
+// per pair).
+template <int U, int B>
+SQ_DEV void canon_dot_batch(const float* const (&xp)[B], const float* const (&cp)[B], int d,
+                            int c16, float (&out)[B]) {
+  float xv[B][U], cv[B][U];
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = c16 + 16 * u;
+      xv[b][u] = f < d ? xp[b][f] : 0.0f;
+      cv[b][u] = f < d ? cp[b][f] : 0.0f;
+    }
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    float s = 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) s = fmaf(xv[b][u], cv[b][u], s);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+    out[b] = s;
+  }
+}
+
+// the next float above x (finite x)
+SQ_DEV float f32_up(float x) {
+  if (x == 0.0f) return 1.401298464e-45f;
+  const uint32_t b = __float_as_uint(x);
+  return __uint_as_float(x > 0.0f ? b + 1u : b - 1u);
+}
+
+struct Cut {
+  float vlo, vhi, H;
+  int ok;
+};
+
+struct CutParams {
+  double alpha, Ch, sub_rel, mt, min_width;
+  int d;
+};
+
+// The row's far band (see the header).  For a pair at law distance D with
+// S in [Smin, Smax] and ip = (S - D) / 2 (fp32 rounding folded in), the
+// screen's bin distance is m = (c sqrt(D) - sthr) kq sqrt(S) /
+// max(1, |ip|); for fixed D, sqrt(S) / max(1, |S - D| / 2) is unimodal in S,
+// so its minimum is at Smin or Smax, and for each endpoint the set of y =
+// sqrt(D) with m >= m_t is an interval with closed-form ends (one quadratic
+// below S, one above).  The band is the intersection of the two intervals
+// and of ipe_hazard's other conditions; its hazard bound is pu(m_t).  All in
+// fp64, with margins covering every fp32 rounding of ipe_hazard.
+SQ_DEV Cut row_cut(float nx2f, float sthrf, float ktf, float Sminf, float Smaxf, const IpeScreen& sc,
+                   const CutParams& cp) {
+  Cut out{__builtin_inff(), -__builtin_inff(), 0.0f, 0};
+  const double Smin = Sminf, Smax = Smaxf, kq = sc.kq, kt = ktf;
+  const double sthr = (double)sthrf * (1.0 + 1e-7);
+  const double c = (1.0 - 4.8828125e-4) * (1.0 - 1e-6);   // sD = sqrt(D) (1 - 2^-11), rounded
+  const double kqm = kq * (1.0 - 3e-5);                    // sqrt / rcp / products of P and m
+  const double mt = cp.mt * (1.0 + 1e-6);
+  if (!(Smin > 0.0) || !(sthr < 1e300)) return out;
+  const double Pmax = kq * sqrt(Smax) * (1.0 + 1e-5);
+  if (!(kt * Pmax + 2.2 <= 1048576.0 * (1.0 - 1e-6))) return out;    // walk cap (c2)
+  if (!(Smax * (1.0 + 1e-5) < (double)sc.smax)) return out;           // M cap (c2)
+  double ylo = sqrt(Smax * 0x1p-12 * (1.0 + 1e-5));                   // c1
+  double yhi = sqrt(Smin * 1.998046875 * (1.0 - 1e-5));
+  // |ip| <= |S - D| / 2 (1 + 1e-6) + 1e-6 S: m >= mt  <=>
+  //   kqm sqrt(S) (c y - sthr) >= mt max(1, |S - y^2| (1 + 1e-6) / 2 + 1e-6 S)
+  const double e1 = 1.0 + 1e-6;
+  for (int side = 0; side < 2; ++side) {
+    const double S = side ? Smax : Smin;
+    const double rS = sqrt(S);
+    const double B = 2.0 * kqm * rS * c;
+    const double C0 = 2.0 * kqm * rS * sthr;
+    const double a = mt * e1;
+    const double sl = 2e-6 * mt * S;
+    // max(1, .) = 1 part: c y - sthr >= mt / (kqm rS)
+    const double y0 = (mt / (kqm * rS) + sthr) / c;
+    // below S: a y^2 + B y - (a S + sl + C0) >= 0
+    const double cA = a * S + sl + C0;
+    const double yA = (-B + sqrt(B * B + 4.0 * a * cA)) / (2.0 * a);
+    // above S: a y^2 - B y + (C0 + sl - a S) <= 0
+    const double dB = B * B - 4.0 * a * (C0 + sl - a * S);
+    if (!(dB >= 0.0)) return out;
+    const double yB = (B + sqrt(dB)) / (2.0 * a);
+    const double yBm = (B - sqrt(dB)) / (2.0 * a);
+    // m >= mt on {y >= yA} (below-S branch) intersected with [yBm, yB]
+    ylo = fmax(ylo, fmax(y0, fmax(yA, yBm)) * (1.0 + 1e-9));
+    yhi = fmin(yhi, yB * (1.0 - 1e-9));
+  }
+  if (!(ylo <= yhi)) return out;
+  const double Dl = ylo * ylo, Dh = yhi * yhi;
+  // a sliver of a band (a row whose threshold sits among the other
+  // centroids) would list most of its pairs: dense from the start
+  if (Dh - Dl < cp.min_width * Dl) return out;
+  const double m = cp.mt;
+  const double r = (1.0 / m) * (1.0 + 1e-5);
+  const double pb = (r + r * r) * 0.500012 * (1.0 + 1e-5);
+  const double pu = (double)sc.cqh * pow(pb, (double)sc.hf) * (1.0 + 2e-3);
+  if (!(m >= 3.0) || !(pu < 9.765625e-4 * (1.0 - 1e-6))) return out;  // c2, c3
+  const double H = pu * (1.0 + pu) * (1.0 + 1e-6);                     // >= -log(1 - pu)
+  // -> fp16 filter units: v = alpha^2 (D - |x|^2) +- E
+  const double u = 0x1p-24;
+  const double nx2 = nx2f;
+  const double errD = (3.0 * cp.d + 64.0) * u * Smax;                 // law D vs exact D
+  const double x2lo = nx2 * (1.0 - (cp.d + 2) * u), x2hi = nx2 * (1.0 + (cp.d + 2) * u);
+  const double xsv = cp.alpha * sqrt(x2hi) * (1.0 + 0x1p-16);
+  const double E = (1.0625 * 0x1p-10 * xsv * cp.Ch + 0x1p-15 * (0.25 * cp.Ch * cp.Ch + xsv * cp.Ch) +
+                    cp.sub_rel * (xsv + cp.Ch)) * (1.0 + 1e-6);
+  const double a2 = cp.alpha * cp.alpha;
+  const double vlo = a2 * (Dl + errD - x2lo) + E;
+  const double vhi = a2 * (Dh - errD - x2hi) - E;
+  float flo = (float)vlo, fhi = (float)vhi, Hf = (float)H;
+  if ((double)flo < vlo) flo = f32_up(flo);
+  if ((double)fhi > vhi) fhi = -f32_up(-fhi);
+  if ((double)Hf < H) Hf = f32_up(Hf);
+  if (!(flo <= fhi)) return out;
+  out.vlo = flo;
+  out.vhi = fhi;
+  out.H = Hf;
+  out.ok = 1;
+  return out;
+}
+
+// ------------------------------------------------------------------ prep
+// Per row: the hint pair in full (thr), the far band, the row's budget
+// draw.  Outputs (row-indexed, local rows): thr / hj (ipe.hip's ext_thr /
+// ext_hj: the dense fallback reuses them), vlo / vhi / H, rM (min of the 32
+// stream budgets when it can run out within the row, else -1), rst (1: no
+// usable band or hint - dense), best (the hint's packed estimate).
+struct PrepArgs {
+  const float* X;
+  long long ldx;
+  const float* C;
+  const int* hint;
+  const float* xn;
+  const float* cn;
+  float* thr;
+  int* hj;
+  float* vlo;
+  float* vhi;
+  float* H;
+  unsigned char* rst;
+  unsigned long long* best;
+  uint16_t* rfire;          // [n][8]: count, then up to kFireCap fired pairs (j | 0x8000)
+  long long n;
+  int d, k;
+  double eps;
+  int Q;
+  RngKey key, tie, bkey, skey;
+  long long row_offset;
+  IpeScreen sc;
+  CutParams cp;
+  unsigned long long* stats;
+};
+
+template <int KU>
+__global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
+  __shared__ float sip[256];
+  __shared__ int slab[256];
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, q4 = lane >> 4;
+  // min / max of the centroid norms (S range of every pair of a row)
+  float mn = __builtin_inff(), mx = 0.0f;
+  for (int j = threadIdx.x; j < a.k; j += 256) {
+    mn = fminf(mn, a.cn[j]);
+    mx = fmaxf(mx, a.cn[j]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  }
+  if (lane == 0) {
+    red[0][wave] = mn;
+    red[1][wave] = mx;
+  }
+  const long long rb = (long long)blockIdx.x * 256 + wave * 64;
+  // the wave's 64 hint pairs, 4 per lane group: rows 16 g + 4 b + q4
+  constexpr int B = 4;
+#pragma unroll 1
+  for (int g = 0; g < 4; ++g) {
+    const float* xp[B];
+    const float* cp_[B];
+    int lb[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const long long r = rb + 16 * g + 4 * b + q4;
+      const int l = r < a.n ? a.hint[r] : -1;
+      const bool ok = r < a.n && l >= 0 && l < a.k;
+      lb[b] = ok ? l : -2;
+      xp[b] = a.X + (size_t)(ok ? r : 0) * a.ldx;
+      cp_[b] = a.C + (size_t)(ok ? l : 0) * a.d;
+    }
+    float sv[B];
+    canon_dot_batch<KU, B>(xp, cp_, a.d, c16, sv);
+    if (c16 == 0) {
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int x = 16 * g + 4 * b + q4;
+        sip[wave * 64 + x] = sv[b];
+        slab[wave * 64 + x] = lb[b];
+      }
+    }
+  }
+  __syncthreads();
+  const float cmin = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
+  const float cmax = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  const long long r = rb + lane;
+  uint32_t st_flag = 0, st_dense = 0;
+  // C^ = 2 alpha max_j |c_j| of the fp16 filter's bound, from the largest
+  // fp32 norm widened by its summation error
+  CutParams cp = a.cp;
+  cp.Ch = 2.0 * cp.alpha * sqrt((double)cmax * (1.0 + (cp.d + 2) * 0x1p-24)) * (1.0 + 0x1p-16);
+  if (r < a.n) {
+    const int l = slab[threadIdx.x];
+    const long long g = a.row_offset + r;
+    const float nx2 = a.xn[r];
+    float t = __builtin_inff();
+    Cut cut{-__builtin_inff(), __builtin_inff(), 0.0f, 0};
+    uint16_t fire[kFireCap];
+    int nf = 0;
+    if (l >= 0) {
+      t = ipe_distance(sip[threadIdx.x], (double)nx2, (double)a.cn[l], a.eps, a.Q, a.key,
+                       (unsigned long long)g * (unsigned long long)a.k + (unsigned long long)l);
+      const float sthr = ipe_sthr(t);
+      cut = row_cut(nx2, sthr, ipe_kt(sthr), nx2 + cmin, nx2 + cmax, a.sc, cp);
+      a.best[r] = pack_best(t, a.tie, g, l);
+    }
+    if (cut.ok) {
+      // The row's 32 (column class) streams spend H per pair from iid Exp(1)
+      // budgets.  Only budgets below H times the longest stream can run out:
+      // they are drawn in increasing order (Renyi: E_(i+1) = E_(i) +
+      // Exp(1) / (32 - i)), each handed to a uniformly chosen unused stream,
+      // until one exceeds that - ~H 32 k/32 draws per row, not 32.  A stream
+      // fires at pair p = floor(E / H) (j = s + 32 p), then redraws (block
+      // 2 + 2 p of its skey stream, as the near kernel's thinning reads).
+      const double H = (double)cut.H;
+      const int P = (a.k + 31) >> 5;
+      const double Tcap = H * (double)P;
+      WordStream ws(a.bkey, (unsigned long long)g);
+      double E = 0.0;
+      unsigned long long unused = 0xFFFFFFFFull;
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t w0 = ws.next(), w1 = ws.next();
+        E += -log(u53(w0, w1)) / (double)(32 - i);
+        if (!(E < Tcap)) break;
+        // exact uniform on [0, 32 - i) (Lemire: multiply, reject the bias zone)
+        const uint32_t m = (uint32_t)(32 - i);
+        uint32_t wv = ws.next();
+        unsigned long long xm = (unsigned long long)wv * m;
+        const uint32_t thr = (uint32_t)(-m) % m;
+        while ((uint32_t)xm < thr) {
+          wv = ws.next();
+          xm = (unsigned long long)wv * m;
+        }
+        const int sidx = nth_set_bit(unused, (int)(xm >> 32));
+        unused &= ~(1ull << sidx);
+        const int Ps = (a.k - sidx + 31) >> 5;
+        double p = floor(E / H);
+        while (p < (double)Ps) {
+          const int pi = (int)p;
+          if (nf < kFireCap) fire[nf] = (uint16_t)((sidx + 32 * pi) | 0x8000);
+          ++nf;
+          WordStream wr(a.skey, (unsigned long long)g * 32ull + (unsigned long long)sidx);
+          wr.b = (uint32_t)(2 + 2 * pi);
+          const uint32_t r0 = wr.next(), r1 = wr.next();
+          p += 1.0 + floor(-log(u53(r0, r1)) / H);
+        }
+      }
+      st_flag = nf > 0 ? 1 : 0;
+      if (nf > kFireCap) cut.ok = 0;   // a row this hot: dense
+    }
+    if (!cut.ok) {
+      // dense: every pair "far" in the sweep (no list traffic), the whole
+      // row to the fp32 kernel
+      cut.vlo = -__builtin_inff();
+      cut.vhi = __builtin_inff();
+      st_dense = 1;
+    }
+    a.thr[r] = t;
+    a.hj[r] = l >= 0 ? l : -2;
+    a.vlo[r] = cut.vlo;
+    a.vhi[r] = cut.vhi;
+    a.H[r] = cut.H;
+    a.rst[r] = cut.ok ? 0 : 1;
+    uint16_t* fr = a.rfire + (size_t)r * 8;
+    const int nw = cut.ok ? nf : 0;
+    fr[0] = (uint16_t)nw;
+    for (int e = 0; e < nw; ++e) fr[1 + e] = fire[e];
+  }
+  if (a.stats) {
+    uint32_t f = st_flag, dn = st_dense;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      f += (uint32_t)__shfl_xor((int)f, o, 64);
+      dn += (uint32_t)__shfl_xor((int)dn, o, 64);
+    }
+    if (lane == 0) {
+      atomicAdd(a.stats + 4, (unsigned long long)f);
+      atomicAdd(a.stats + 5, (unsigned long long)dn);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ sweep
+// estep_x64's sweep (persistent workgroups of 4 waves x 2 row sets x 32
+// rows, the wave's fp16 A fragments resident in VGPRs, 64-centroid tiles
+// through a 3-slot LDS ring by LDS-DMA with counted vmcnt) with an IPE
+// epilogue.  Register i of a lane (half, r32) holds row (i & 3) + 8 (i >> 2)
+// + 4 half of its row set, column 64 t + 32 h + r32.
+//  ARGMIN: hint = approximate argmin of v (packed (t, h, r32) in the low
+//          14 mantissa bits; any hint is exact for the law);
+//  screen: far iff med3(v, vlo, vhi) == v; near pairs -> the row's LDS list.
+struct SweepArgs {
+  const _Float16* Xh;       // [n][d_pad] fp16(alpha x)
+  const _Float16* C;        // estep_x64 operand (hi region used)
+  const float* vlo;
+  const float* vhi;
+  const unsigned char* rst;
+  const uint16_t* rfire;    // prep's fired pairs per row
+  const int* hj;            // hints (prep's)
+  int* hint_out;            // ARGMIN output
+  unsigned long long* list; // (row << 16) | j | fired << 15
+  int* list_count;
+  long long* dense_rows;
+  int* dense_count;
+  unsigned char* rflag;     // 1: dense (fallback), written per row
+  long long n;
+  int k, k_pad;
+  long long row_offset;
+  unsigned long long* stats;
+};
+
+template <int KSD, bool ARGMIN>
+__global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
+  constexpr int KT = KSD + 1;                 // data k-steps + the norm step
+  constexpr int SLOT = KT * 2048;
+  constexpr int TILE_STRIDE = (2 * KSD + 1) * 2048;
+  constexpr int PIECES = SLOT / 1024;
+  constexpr int PPW = (PIECES + kNW - 1) / kNW;
+  constexpr int DX = KSD * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  auto buf = [&](int g) -> unsigned char* { return smem + (g % kRing) * SLOT; };
+  uint16_t* nl = reinterpret_cast<uint16_t*>(smem + kRing * SLOT);      // [kRows][kNLS]
+  int* ncnt = reinterpret_cast<int*>(nl + kRows * kNLS);                  // [kRows]
+  int* shint = ncnt + kRows;                                              // [kRows]
+  int* wsum = shint + kRows;                                              // [kNW] flush scan
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31;
+  const int half = lane >> 5;
+  const long long n = a.n;
+  const int n_tiles = a.k_pad / kTileN;
+  const long long nblk = (n + kRows - 1) / kRows;
+  long long blk = blockIdx.x;
+  if (blk >= nblk) return;
+  int qbits = 1;
+  while ((1 << qbits) < 2 * n_tiles) ++qbits;
+  const uint32_t keep = ~((1u << (qbits + 5)) - 1u);
+
+  auto stage = [&](int U) {
+    const int t = U % n_tiles;
+    const unsigned char* tile = reinterpret_cast<const unsigned char*>(a.C) + (size_t)t * TILE_STRIDE;
+    unsigned char* dst = buf(U);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wave + kNW * i < PIECES ? wave + kNW * i : PIECES - 1;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(tile + p * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
+    }
+  };
+  auto sync_tile = [&]() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // rows of the block: set st of wave w, row rl of the set's 32
+  auto row_of = [&](long long b, int st, int rl) -> long long {
+    return b * kRows + (wave * kRS + st) * 32 + rl;
+  };
+  f16x8 ah[kRS][KSD];
+  auto load_a = [&](long long b) {
+#pragma unroll
+    for (int st = 0; st < kRS; ++st) {
+      long long r = row_of(b, st, r32);
+      r = r < n ? r : n - 1;
+      const _Float16* xr = a.Xh + (size_t)r * DX + half * 8;
+#pragma unroll
+      for (int ks = 0; ks < KSD; ++ks) ah[st][ks] = *reinterpret_cast<const f16x8*>(xr + ks * 16);
+    }
+  };
+  f16x8 aug = (f16x8)0;
+  if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
+  const int lane_off = (half * 64 + r32) * 16;
+  auto frag = [&](const unsigned char* cur, int g) -> f16x8 {
+    return *reinterpret_cast<const f16x8*>(cur + lane_off + (g / KT) * 512 + (g % KT) * 2048);
+  };
+  // per-lane state: the 16 rows' band edges per set (screen) / running
+  // packed minima (argmin); the near bits of the last epilogue
+  float lo[kRS][16], hi[kRS][16];
+  // near bits: register (st, i) of this lane, bit h' = half-tile index within
+  // the current 1024-column segment (column 32 h' + r32 of the segment)
+  uint32_t mk[kRS][16];
+  auto rl_of = [&](int i) { return (i & 3) + 8 * (i >> 2) + 4 * half; };
+  // one value of the previous half-tile (o), half-tile index q = 2 t + h
+  auto epi = [&](int st, int i, float v, uint32_t q) {
+    if constexpr (ARGMIN) {
+      lo[st][i] = vmin(lo[st][i], and_or(v, keep, (q << 5) | (uint32_t)r32));
+    } else {
+      const bool far = vmed3(v, lo[st][i], hi[st][i]) == v;
+      const uint32_t hb = 1u << (q & 31u);
+      mk[st][i] = far ? mk[st][i] : (mk[st][i] | hb);
+    }
+  };
+  typedef f32x16 Acc[kRS];
+  constexpr int PFD = 2, NB = PFD + 1;
+  f16x8 bq[NB];
+  auto pass = [&](auto H_, const unsigned char* cur, Acc& acc, const Acc& o, uint32_t qo,
+                  bool do_epi) {
+    constexpr int h = decltype(H_)::value;
+#pragma unroll
+    for (int st = 0; st < kRS; ++st) acc[st] = (f32x16){0};
+#pragma unroll
+    for (int ks = 0; ks < KT; ++ks) {
+      const int g = h * KT + ks;
+      if (g + PFD < 2 * KT) bq[(g + PFD) % NB] = frag(cur, g + PFD);
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+        acc[st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ks < KSD ? ah[st][ks] : aug, bq[g % NB],
+                                                         acc[st], 0, 0, 0);
+      if (do_epi) {
+#pragma unroll
+        for (int e = (ks * 16 * kRS) / KT; e < ((ks + 1) * 16 * kRS) / KT; ++e)
+          epi(e / 16, e % 16, o[e / 16][e % 16], qo);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // the near pairs of segment seg (columns 1024 seg ..): each lane walks the
+  // set bits of its 32 registers (the hint, co-located centroids, padding);
+  // a row whose list is already full is skipped (dense)
+  auto flush_masks = [&](long long b, int seg) {
+    if constexpr (!ARGMIN) {
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          uint32_t m = mk[st][i];
+          mk[st][i] = 0u;
+          if (__ballot(m != 0u) != 0ull) {
+            const int rb = (wave * kRS + st) * 32 + rl_of(i);
+            if (row_of(b, st, rl_of(i)) >= n || ncnt[rb] > kCapR) m = 0u;
+            const int hint = shint[rb];
+            while (m) {
+              const int bit = __builtin_ctz(m);
+              m &= m - 1u;
+              const int jc = 1024 * seg + 32 * bit + r32;
+              if (jc < a.k && jc != hint) {
+                const int s = atomicAdd(&ncnt[rb], 1);
+                if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)jc;
+                else m = 0u;
+              }
+            }
+          }
+        }
+    }
+  };
+
+  int U = 0;
+  stage(0);
+  stage(1);
+  load_a(blk);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (; blk < nblk; blk += gridDim.x) {
+    // ---- block prologue: the rows' band edges, hints, listed fires
+    if constexpr (ARGMIN) {
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lo[st][i] = __builtin_inff();
+    } else {
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mk[st][i] = 0u;
+      // the rows' hints and the fires prep listed (thread t: row t)
+      for (int t = tid; t < kRows; t += kNW * 64) {
+        const long long r = blk * kRows + t;
+        int c = 0;
+        if (r < n) {
+          shint[t] = a.hj[r];
+          const uint16_t* fr = a.rfire + (size_t)r * 8;
+          c = fr[0];
+          for (int e = 0; e < c; ++e) nl[t * kNLS + e] = fr[1 + e];
+        } else {
+          shint[t] = -1;
+        }
+        ncnt[t] = c;
+      }
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          long long r = row_of(blk, st, rl_of(i));
+          const bool v = r < n;
+          r = v ? r : n - 1;
+          lo[st][i] = v ? a.vlo[r] : __builtin_inff();
+          hi[st][i] = v ? a.vhi[r] : -__builtin_inff();
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    // ---- the sweep: half 0 of tile t (epilogue of tile t - 1's half 1),
+    // half 1 (epilogue of half 0), one ring slot per tile
+    f32x16 cA[kRS], cB[kRS];
+    for (int t = 0; t < n_tiles; ++t) {
+      stage(U + kRing - 1);
+#pragma unroll
+      for (int j = 0; j < PFD; ++j) bq[j] = frag(buf(U), j);
+      pass(std::integral_constant<int, 0>{}, buf(U), cA, cB, (uint32_t)(2 * t - 1), t > 0);
+      // segment (t - 1) / 16 complete with tile t - 1's half 1
+      if ((t & 15) == 0 && t > 0) flush_masks(blk, (t - 1) >> 4);
+      pass(std::integral_constant<int, 1>{}, buf(U), cB, cA, (uint32_t)(2 * t), true);
+      sync_tile();
+      ++U;
+    }
+    load_a(blk + gridDim.x);   // clamped rows: unconditional
+#pragma unroll
+    for (int st = 0; st < kRS; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) epi(st, i, cB[st][i], (uint32_t)(2 * n_tiles - 1));
+    flush_masks(blk, (n_tiles - 1) >> 4);
+
+    if constexpr (ARGMIN) {
+      // row minimum over the 32 lanes of each half: the packed value holds
+      // the tile-half index and the lane column
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float v = lo[st][i];
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) v = vmin(v, __shfl_xor(v, o, 64));
+          if (r32 == i) {
+            const long long r = row_of(blk, st, rl_of(i));
+            if (r < n) {
+              const uint32_t p = __float_as_uint(v);
+              const uint32_t q = (p >> 5) & ((1u << qbits) - 1u);
+              const int j = (int)((q >> 1) * kTileN + (q & 1u) * 32u + (p & 31u));
+              a.hint_out[r] = j < a.k ? j : 0;
+            }
+          }
+        }
+    } else {
+      // ---- flush the block's lists: dedupe fires against near pairs and the
+      // hint, dense rows to the fallback list, the rest compacted to the
+      // global pair list (one atomic per wave)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const int t = tid;   // kRows == 256 threads: one row each
+      const long long r = blk * kRows + t;
+      int c = 0;
+      bool dense = false;
+      uint16_t* row_l = nl + t * kNLS;
+      if (r < n) {
+        c = ncnt[t];
+        dense = c > kCapR || a.rst[r] != 0;
+        if (dense) {
+          c = 0;
+        } else {
+          const int hj = shint[t];
+          int w = 0;
+          for (int e = 0; e < c; ++e) {
+            const uint16_t v = row_l[e];
+            bool drop = false;
+            if (v & 0x8000) {
+              const int j = v & 0x3FFF;
+              drop = j == hj;
+              for (int f = 0; f < c && !drop; ++f) drop = row_l[f] == (uint16_t)j;
+            }
+            if (!drop) row_l[w++] = v;
+          }
+          c = w;
+        }
+        a.rflag[r] = dense ? 1 : 0;
+      }
+      // wave scan of the counts
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      const int wtot = __shfl(incl, 63, 64);
+      int base = 0;
+      if (lane == 63 && wtot > 0) base = atomicAdd(a.list_count, wtot);
+      base = __shfl(base, 63, 64);
+      const unsigned long long rr = (unsigned long long)(r < n ? r : 0) << 16;
+      for (int e = 0; e < c; ++e) a.list[base + incl - c + e] = rr | (unsigned long long)row_l[e];
+      const unsigned long long dm = __ballot(dense);
+      if (dm) {
+        int db = 0;
+        if (lane == 0) db = atomicAdd(a.dense_count, __popcll(dm));
+        db = __shfl(db, 0, 64);
+        if (dense) a.dense_rows[db + __popcll(dm & ((1ull << lane) - 1ull))] = r;
+      }
+      if (a.stats) {
+        uint32_t nfire = 0, nnear = 0;
+        for (int e = 0; e < c; ++e) {
+          if (row_l[e] & 0x8000) ++nfire; else ++nnear;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          nfire += (uint32_t)__shfl_xor((int)nfire, o, 64);
+          nnear += (uint32_t)__shfl_xor((int)nnear, o, 64);
+        }
+        if (lane == 0) {
+          atomicAdd(a.stats + 0, (unsigned long long)nnear);
+          atomicAdd(a.stats + 1, (unsigned long long)nfire);
+          atomicAdd(a.stats + 3, (unsigned long long)__popcll(dm));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------ near
+// The listed pairs: 16 lanes per canonical dot (4 pairs at a time per wave,
+// 64 per round), then one lane per pair samples and merges.
+struct NearArgs {
+  const unsigned long long* list;
+  const int* list_count;
+  const float* X;
+  long long ldx;
+  const float* C;
+  const float* xn;
+  const float* cn;
+  const float* thr;
+  const float* H;
+  unsigned long long* best;
+  int d, k;
+  double eps;
+  int Q;
+  RngKey key, tie, skey;
+  long long row_offset;
+  IpeScreen sc;
+  unsigned long long* stats;
+};
+
+template <int KU>
+__global__ void __launch_bounds__(256) ipe16_near_kernel(NearArgs a) {
+  __shared__ float sip[256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, q4 = lane >> 4;
+  const long long cnt = *a.list_count;
+  uint32_t st_exact = 0;
+  for (long long base = ((long long)blockIdx.x * 4 + wave) * 64; base < cnt;
+       base += (long long)gridDim.x * 256) {
+    constexpr int B = 4;
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {
+      const float* xp[B];
+      const float* cp_[B];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const long long e = base + 16 * g + 4 * b + q4;
+        long long r = 0;
+        int j = 0;
+        if (e < cnt) {
+          const unsigned long long ent = a.list[e];
+          r = (long long)(ent >> 16);
+          j = (int)(ent & 0x3FFFu);
+        }
+        xp[b] = a.X + (size_t)r * a.ldx;
+        cp_[b] = a.C + (size_t)j * a.d;
+      }
+      float sv[B];
+      canon_dot_batch<KU, B>(xp, cp_, a.d, c16, sv);
+      if (c16 == 0) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) sip[wave * 64 + 16 * g + 4 * b + q4] = sv[b];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const long long e = base + lane;
+    if (e < cnt) {
+      const unsigned long long ent = a.list[e];
+      const long long r = (long long)(ent >> 16);
+      const int j = (int)(ent & 0x3FFFu);
+      const bool fired = (ent & 0x8000u) != 0;
+      const long long g = a.row_offset + r;
+      const float ip = sip[threadIdx.x];
+      const float nx2 = a.xn[r], ny2 = a.cn[j];
+      float dt = __builtin_inff();
+      if (!fired) {
+        dt = ipe_distance(ip, (double)nx2, (double)ny2, a.eps, a.Q, a.key,
+                          (unsigned long long)g * (unsigned long long)a.k + (unsigned long long)j);
+      } else {
+        const float t = a.thr[r];
+        uint32_t hq = 0;
+        float pbar = 1.0f;
+        const bool ok = ipe_hazard(ip, nx2, ny2, ipe_sthr(t), a.sc, hq, pbar);
+        WordStream ws(a.skey, (unsigned long long)g * 32ull + (unsigned long long)(j & 31));
+        ws.b = (uint32_t)(2 + 2 * (j >> 5));
+        (void)ws.next();
+        (void)ws.next();                     // words 0, 1: the stream's next budget (sweep)
+        const uint32_t w2 = ws.next(), w3 = ws.next();
+        const double beff = -expm1(-(double)a.H[r]);
+        const double u = u53(w2, w3) * beff;
+        const int h = (a.Q + 1) / 2;
+        const double pib = ok ? binom_upper_tail((double)pbar, a.Q, h) * (1.0 + 1e-12) : 1.0;
+        if (u < pib) {
+          ++st_exact;
+          dt = ipe_pruned_exact((double)ip, (double)nx2 + (double)ny2, a.eps, a.Q, t, u, ws);
+        }
+      }
+      if (dt < __builtin_inff()) atomicMin(a.best + r, pack_best(dt, a.tie, g, j));
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (a.stats) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) st_exact += (uint32_t)__shfl_xor((int)st_exact, o, 64);
+    if (lane == 0 && st_exact) atomicAdd(a.stats + 2, (unsigned long long)st_exact);
+  }
+}
+
+// labels / mind of the rows the screen resolved (dense rows: the fallback)
+__global__ void __launch_bounds__(256) ipe16_finalize_kernel(const unsigned long long* best,
+                                                            const unsigned char* rflag,
+                                                            int* labels, float* mind,
+                                                            long long n) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n || rflag[r]) return;
+  const unsigned long long b = best[r];
+  labels[r] = (int)(b & 0x3FFFu);
+  mind[r] = __uint_as_float((uint32_t)(b >> 32));
+}
+
+}  // namespace i16
+}  // namespace sq
+
+using namespace sq;
+using namespace sq::i16;
+
+template <int KSD, bool ARGMIN>
+static int launch_sweep(const SweepArgs& a, hipStream_t st) {
+  constexpr int SLOT = (KSD + 1) * 2048;
+  const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 3 * kRows * 4 + 64;
+  auto kern = ipe16_sweep_kernel<KSD, ARGMIN>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kNW * 64, lds);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const long long nblk = (a.n + kRows - 1) / kRows;
+  const unsigned grid = (unsigned)(nblk < resident ? nblk : resident);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kNW * 64), lds, st, a);
+  return (int)hipGetLastError();
+}
+
+static IpeScreen make_screen(int k, double eps, int Q) {
+  IpeScreen sc;
+  const int h = (Q + 1) / 2;
+  double cq = 1.0;
+  for (int i = 0; i < h; ++i) cq = cq * (double)(Q - i) / (double)(i + 1);
+  sc.hf = (float)h;
+  sc.cqh = (float)(cq * (1.0002 * (1.0 + 1e-6)));
+  sc.kq = (float)((1.0 - 3e-6) * (1.0 - 1e-6) / (1.4142135623730951 * eps));
+  sc.smax = (float)(6.0e10 * eps * (1.0 - 1e-6));
+  sc.cap = (uint32_t)(((k + 63) / 64) * (1u << 23));
+  sc.ucap = exp(-(double)sc.cap * 0x1p-32);
+  return sc;
+}
+
+static RngKey key_at(const long long* ia, int i) {
+  return RngKey{(uint32_t)ia[i], (uint32_t)ia[i + 1], (uint32_t)ia[i + 2], (uint32_t)ia[i + 3]};
+}
+
+extern "C" {
+
+// One call per phase (op), arguments in host arrays (ia: integers and device
+// pointers, da: doubles) so the binding stays one signature:
+//   op 0 prep, 1 argmin sweep, 2 screen sweep, 3 near, 4 finalize.
+// ia layout (all ops): [0] X, [1] ldx, [2] C fp32, [3] Xh fp16, [4] C_op,
+//   [5] hint in, [6] hint out (argmin), [7] xn, [8] cn, [9] thr, [10] hj,
+//   [11] vlo, [12] vhi, [13] H, [14] rfire, [15] rst, [16] best, [17] list,
+//   [18] list_count, [19] dense_rows, [20] dense_count, [21] rflag,
+//   [22] labels, [23] mind, [24] stats, [25] n, [26] d, [27] d_pad, [28] k,
+//   [29] k_pad, [30] Q, [31] row_offset, [32..35] key, [36..39] tie,
+//   [40..43] skey, [44..47] bkey
+// da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
+int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = ia[25];
+  if (n <= 0) return 0;
+  const int d = (int)ia[26], d_pad = (int)ia[27], k = (int)ia[28], k_pad = (int)ia[29];
+  const int Q = (int)ia[30];
+  const double eps = da[0];
+  if (Q < 1 || Q > kIpeMaxQ || !(Q & 1) || k < 1 || k > 16384 || k_pad % 64 || k_pad < k ||
+      d < 1 || d > d_pad || d_pad % 16 || d_pad > 256 || !(eps > 0.0))
+    return (int)hipErrorInvalidValue;
+  auto P = [&](int i) -> void* { return (void*)(intptr_t)ia[i]; };
+  const IpeScreen sc = make_screen(k, eps, Q);
+  if (op == 0) {
+    PrepArgs a;
+    a.X = (const float*)P(0);
+    a.ldx = ia[1];
+    a.C = (const float*)P(2);
+    a.hint = (const int*)P(5);
+    a.xn = (const float*)P(7);
+    a.cn = (const float*)P(8);
+    a.thr = (float*)P(9);
+    a.hj = (int*)P(10);
+    a.vlo = (float*)P(11);
+    a.vhi = (float*)P(12);
+    a.H = (float*)P(13);
+    a.rfire = (uint16_t*)P(14);
+    a.rst = (unsigned char*)P(15);
+    a.best = (unsigned long long*)P(16);
+    a.n = n;
+    a.d = d;
+    a.k = k;
+    a.eps = eps;
+    a.Q = Q;
+    a.key = key_at(ia, 32);
+    a.tie = key_at(ia, 36);
+    a.bkey = key_at(ia, 44);
+    a.skey = key_at(ia, 40);
+    a.row_offset = ia[31];
+    a.sc = sc;
+    // the fp16 filter's error-bound constants (estep_x64)
+    a.cp.alpha = da[1];
+    a.cp.Ch = 0.0;   // per block, from the centroid norms
+    a.cp.sub_rel = 0x1p-21 * sqrt((double)d_pad);
+    a.cp.mt = da[2];
+    a.cp.min_width = da[3];
+    a.cp.d = d;
+    a.stats = (unsigned long long*)P(24);
+    const dim3 pg((unsigned)((n + 255) / 256));
+    switch (d_pad) {
+#define CASE(KSD)                                                               \
+  case KSD * 16:                                                                \
+    hipLaunchKernelGGL(ipe16_prep_kernel<KSD>, pg, dim3(256), 0, st, a); break;
+      CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+      default:
+        return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
+  if (op == 1 || op == 2) {
+    SweepArgs a;
+    a.Xh = (const _Float16*)P(3);
+    a.C = (const _Float16*)P(4);
+    a.vlo = (const float*)P(11);
+    a.vhi = (const float*)P(12);
+    a.rfire = (const uint16_t*)P(14);
+    a.rst = (const unsigned char*)P(15);
+    a.hj = (const int*)P(10);
+    a.hint_out = (int*)P(6);
+    a.list = (unsigned long long*)P(17);
+    a.list_count = (int*)P(18);
+    a.dense_rows = (long long*)P(19);
+    a.dense_count = (int*)P(20);
+    a.rflag = (unsigned char*)P(21);
+    a.n = n;
+    a.k = k;
+    a.k_pad = k_pad;
+    a.row_offset = ia[31];
+    a.stats = (unsigned long long*)P(24);
+    const bool am = op == 1;
+    switch (d_pad) {
+#define CASE(KSD)                                                                  \
+  case KSD * 16:                                                                   \
+    return am ? launch_sweep<KSD, true>(a, st) : launch_sweep<KSD, false>(a, st);
+      CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+      default:
+        return (int)hipErrorInvalidValue;
+    }
+  }
+  if (op == 3) {
+    NearArgs a;
+    a.list = (const unsigned long long*)P(17);
+    a.list_count = (const int*)P(18);
+    a.X = (const float*)P(0);
+    a.ldx = ia[1];
+    a.C = (const float*)P(2);
+    a.xn = (const float*)P(7);
+    a.cn = (const float*)P(8);
+    a.thr = (const float*)P(9);
+    a.H = (const float*)P(13);
+    a.best = (unsigned long long*)P(16);
+    a.d = d;
+    a.k = k;
+    a.eps = eps;
+    a.Q = Q;
+    a.key = key_at(ia, 32);
+    a.tie = key_at(ia, 36);
+    a.skey = key_at(ia, 40);
+    a.row_offset = ia[31];
+    a.sc = sc;
+    a.stats = (unsigned long long*)P(24);
+    static int grid = 0;
+    if (grid == 0) {
+      int dev = 0, cus = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      grid = 8 * (cus > 0 ? cus : 256);
+    }
+    switch (d_pad) {
+#define CASE(KSD)                                                                             \
+  case KSD * 16:                                                                              \
+    hipLaunchKernelGGL(ipe16_near_kernel<KSD>, dim3((unsigned)grid), dim3(256), 0, st, a); break;
+      CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
+#undef CASE
+      default:
+        return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
+  if (op == 4) {
+    hipLaunchKernelGGL(ipe16_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (const unsigned long long*)P(16), (const unsigned char*)P(21), (int*)P(22),
+                       (float*)P(23), n);
+    return (int)hipGetLastError();
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+}  // extern "C"

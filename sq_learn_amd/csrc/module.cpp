@@ -45,7 +45,10 @@ __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, cons
                                        long long, int, int, int, int, double, int, unsigned,
                                        unsigned, unsigned, unsigned, unsigned, unsigned, unsigned,
                                        unsigned, unsigned, unsigned, unsigned, unsigned, long long,
-                                       int, void*, void*, void*);
+                                       int, void*, void*, void*, const void*, const void*,
+                                       long long, const void*, const void*);
+// ipe16.hip
+__attribute__((weak)) int sq_ipe16(int, const long long*, const double*, void*);
 __attribute__((weak)) int sq_centroid_delta(const void*, const void*, const void*, void*, void*,
                                             void*, long long, int, int, int, int, void*, void*,
                                             void*, void*);
@@ -318,17 +321,28 @@ static PyObject* py_xw(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
-  unsigned long long X, Cf, C, hint, xn, cn, lab, mind, stats, scr, st; long long ldx, n, roff;
+  unsigned long long X, Cf, C, hint, xn, cn, lab, mind, stats, scr, st, rl = 0, rc = 0, et = 0,
+                                                                       eh = 0;
+  long long ldx, n, roff, ln = 0;
   int d, dp, k, kp, Q;
   double eps; unsigned k0, k1, s0, s1, t0, t1, ts0, ts1, q0, q1, qs0, qs1; int prune;
-  if (!PyArg_ParseTuple(a, "KLKKKKKKKLiiiidiIIIIIIIIIIIILiKKK", &X, &ldx, &Cf, &C, &hint, &xn, &cn,
-                        &lab, &mind, &n, &d, &dp, &k, &kp, &eps, &Q, &k0, &k1, &s0, &s1, &t0,
-                        &t1, &ts0, &ts1, &q0, &q1, &qs0, &qs1, &roff, &prune, &stats, &scr, &st))
+  if (!PyArg_ParseTuple(a, "KLKKKKKKKLiiiidiIIIIIIIIIIIILiKKK|KKLKK", &X, &ldx, &Cf, &C, &hint,
+                        &xn, &cn, &lab, &mind, &n, &d, &dp, &k, &kp, &eps, &Q, &k0, &k1, &s0,
+                        &s1, &t0, &t1, &ts0, &ts1, &q0, &q1, &qs0, &qs1, &roff, &prune, &stats,
+                        &scr, &st, &rl, &rc, &ln, &et, &eh))
     return nullptr;
   CHECK(sq_ipe_fused)
   return ret(sq_ipe_fused(P(X), ldx, P(Cf), P(C), P(hint), P(xn), P(cn), P(lab), P(mind), n, d,
                           dp, k, kp, eps, Q, k0, k1, s0, s1, t0, t1, ts0, ts1, q0, q1, qs0, qs1,
-                          roff, prune, P(stats), P(scr), P(st)));
+                          roff, prune, P(stats), P(scr), P(st), P(rl), P(rc), ln, P(et), P(eh)));
+}
+
+// ipe16: (op, host int64 args pointer, host double args pointer, stream)
+static PyObject* py_ipe16(PyObject*, PyObject* a) {
+  int op; unsigned long long ia, da, st;
+  if (!PyArg_ParseTuple(a, "iKKK", &op, &ia, &da, &st)) return nullptr;
+  CHECK(sq_ipe16)
+  return ret(sq_ipe16(op, (const long long*)(uintptr_t)ia, (const double*)(uintptr_t)da, P(st)));
 }
 
 static PyObject* py_pairwise_reduce(PyObject*, PyObject* a) {
@@ -675,6 +689,7 @@ static PyMethodDef methods[] = {
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},
+    {"ipe16", py_ipe16, METH_VARARGS, "certified fp16 screen of the IPE E-step (op per phase)"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},

@@ -299,6 +299,7 @@ class LloydEngine:
             # restart and a resumed fit see the same (empty) hints
             for h in self._ipe_lab:
                 h.fill_(-1)
+            self._ipe_hint_valid = False
         self.inc_valid = False   # the incremental M-step restarts from scratch
         self.bounds_valid = False
         self._kept_frac = self._kept_prev = None   # new centres: re-measure the filter
@@ -346,6 +347,7 @@ class LloydEngine:
             return
         self._ipe_buffers()
         self._ipe_lab[self._ipe_cur].copy_(t.to(self.device).to(torch.int32))
+        self._ipe_hint_valid = bool((t >= 0).all())
 
     def _ipe_buffers(self):
         if getattr(self, "_ipe_lab", None) is None:
@@ -498,9 +500,67 @@ class LloydEngine:
                                   chunk_rows=self._chunk_rows(), xn=self.xn)
         return lab, mind, mind.double().sum().reshape(1)
 
+    def _ipe16_ok(self):
+        """The certified fp16 IPE screen (csrc/ipe16.hip) covers d <= 256,
+        k <= 16384, odd Q <= 15, fp32 rows; SQ_IPE16=0 disables it."""
+        return (self.device.type == "cuda" and self.Xf.dtype == torch.float32
+                and self.Xf.stride(1) == 1 and self.ipe_Q % 2 == 1 and self.ipe_Q <= 15
+                and K.pad_features(self.d) in K.IPE16_D and self.k <= K.IPE16_MAX_K
+                and os.environ.get("SQ_IPE16", "1") != "0")
+
+    def _estep_ipe16(self, ipe_key):
+        """IPE E-step by the certified fp16 screen: hint pair in full, fp16
+        MFMA band classification of every other pair, canonical fp32 inner
+        products and samplers only for the near / fired pairs (the law of
+        ``_estep_ipe``'s fused kernel, see csrc/ipe16.hip)."""
+        eps = self.delta / 2.0
+        n = self.n
+        self._ipe_buffers()
+        d_pad = K.pad_features(self.d)
+        k_pad = K.pad_clusters(self.k)
+        if getattr(self, "_ipe16", None) is None:
+            mx = (self._ipe_xn.max() if n else torch.zeros((), device=self.device)).double()
+            mx = mx.reshape(1)
+            self.comm.all_reduce_(mx, op="max")
+            margin = self.delta + self._noise_bound() * math.sqrt(self.k * self.d)
+            alpha = K.choose_alpha(float(mx.item()), margin)
+            self._ipe16 = K.Ipe16(self.Xf, self.k, d_pad, k_pad, alpha, self.device)
+        st = self._ipe16
+        hint = self._ipe_lab[self._ipe_cur]
+        self._ipe_cur ^= 1
+        labels32 = self._ipe_lab[self._ipe_cur]
+        first = not getattr(self, "_ipe_hint_valid", False)
+        mind = torch.empty(n, dtype=torch.float32, device=self.device)
+        C32 = self.C.float().contiguous()
+        cn = (C32 * C32).sum(1).contiguous()
+        st.set_centers(C32)
+        tie = self._key("band_select")
+        xn = self._ipe_xn
+        stats = getattr(self, "ipe16_stats", None)
+
+        def fallback(rl, rc, ln, thr, hj, s, e):
+            dp = 32
+            while dp < self.d:
+                dp *= 2
+            kp = -(-self.k // 16) * 16
+            K.ipe_fused_native(self.Xf[s:e], K.ipe_center_fragments(C32, kp, dp), xn[s:e], cn,
+                               self.k, kp, dp, eps, self.ipe_Q, ipe_key, tie,
+                               self.row_offset + s, labels32[s:e], mind[s:e], C=C32,
+                               skip_key=self._key("ipe_skip"), rows=(rl, rc, ln), ext=(thr, hj),
+                               stats=getattr(self, "ipe_stats", None))
+
+        with tracing.range("ipe16"):
+            st.estep(self.Xf, C32, hint, xn, cn, labels32, mind, eps, self.ipe_Q, ipe_key, tie,
+                     self._key("ipe16_skip"), self._key("ipe16_row"), self.row_offset, first,
+                     stats=stats, fallback=fallback)
+        self._ipe_hint_valid = True
+        return labels32, mind, mind.double().sum().reshape(1)
+
     def _estep_ipe(self, key):
         eps = self.delta / 2.0
         ipe_key = self._key("ipe")
+        if self._ipe16_ok():
+            return self._estep_ipe16(ipe_key)
         if self.device.type == "cuda" and self.d <= 1024 and self.Xf.dtype == torch.float32 \
                 and self.Xf.stride(1) == 1 and self.ipe_Q <= 15:
             # fused kernel: fp32 MFMA inner products + per-pair median-of-Q AE.

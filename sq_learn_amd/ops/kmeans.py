@@ -258,7 +258,7 @@ def ipe_center_fragments(C, k_pad, d_pad):
 
 def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie_key: RngKey,
                      row_offset, labels, mind, prune=True, C=None, hint_labels=None,
-                     skip_key: RngKey = None, stats=None, layout=0):
+                     skip_key: RngKey = None, stats=None, layout=0, rows=None, ext=None):
     """Fused IPE E-step (csrc/ipe.hip): exact fp32 MFMA inner products, the
     median-of-Q amplitude-estimation distance per pair in the epilogue,
     per-row argmin with random ties; G is never materialised.  ``prune``
@@ -273,7 +273,10 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
     accumulated): screened pairs, full-sampler pairs, fires, fires reaching
     the exact branch, workgroups that ran the first sweep.  ``layout``
     (tests): 0 auto, 1 / 2 row groups per workgroup, 3 the per-lane-queue
-    kernel - all return the same labels bit for bit."""
+    kernel - all return the same labels bit for bit.  ``rows`` = (rlist
+    int64, rcount int32 [1] on the device, list_n >= count on the host) with
+    ``ext`` = (thr fp32 [n], hj int32 [n]): list mode over the listed rows,
+    with their thresholds / hints given (the dense rows of ``Ipe16``)."""
     n, d = X.shape
     assert X.dtype == torch.float32 and X.stride(1) == 1
     assert xn.dtype == torch.float32 and cn.dtype == torch.float32 and xn.numel() >= n
@@ -288,7 +291,12 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
         skip_key = key.derive(purpose="ipe_skip")
     # the row-group layouts turn label hints into thresholds in a pre-pass
     scratch = None
-    if hint_labels is not None and prune and int(Q) % 2 == 1 and layout != 3:
+    if rows is not None:
+        assert ext is not None and prune and int(Q) % 2 == 1
+        rl, rc, ln = rows
+        assert rl.dtype == torch.int64 and rc.dtype == torch.int32
+        assert ext[0].dtype == torch.float32 and ext[1].dtype == torch.int32
+    elif hint_labels is not None and prune and int(Q) % 2 == 1 and layout != 3:
         scratch = torch.empty(2 * max(n, 1), dtype=torch.int32, device=X.device)
     rc = nat.native().ipe_fused(X.data_ptr(), X.stride(0), Cfrag.data_ptr(),
                                 0 if C is None else C.data_ptr(),
@@ -300,7 +308,10 @@ def ipe_fused_native(X, Cfrag, xn, cn, k, k_pad, d_pad, eps, Q, key: RngKey, tie
                                 int(row_offset), int(bool(prune)) | (int(layout) & 3) << 1,
                                 0 if stats is None else stats.data_ptr(),
                                 0 if scratch is None else scratch.data_ptr(),
-                                nat.stream_handle(X.device))
+                                nat.stream_handle(X.device),
+                                *((rows[0].data_ptr(), rows[1].data_ptr(), int(rows[2]),
+                                   ext[0].data_ptr(), ext[1].data_ptr()) if rows is not None
+                                  else ()))
     if rc:
         raise RuntimeError(f"ipe_fused failed (hip error {rc})")
 
@@ -963,3 +974,158 @@ class KmppState:
 def _rc(rc, name):
     if rc:
         raise RuntimeError(f"{name} failed (hip error {rc})")
+
+
+# ------------------------------------------------ certified fp16 IPE screen
+# (csrc/ipe16.hip): the IPE E-step without a per-pair fp32 inner product.
+
+IPE16_D = FAST_D          # d_pad of the fp16 sweep (one LDS ring slot per tile)
+IPE16_MAX_K = 16384       # centroid ids in 14 bits
+IPE16_CAPR = 64           # listed pairs per row (csrc kCapR)
+IPE16_CHUNK = 1 << 22     # rows per launch group (bounds the pair list: 8 B x 64 per row)
+
+
+class Ipe16:
+    """Buffers and launch sequence of the certified fp16 IPE screen for one
+    engine (rows ``[0, n)`` of a shard).  Per E-step and row chunk: (first
+    step only) the fp16 argmin sweep for the hints, prep (hint pair in full,
+    far band, row budget), the fp16 screen sweep, the near-pair kernel,
+    finalize; rows the screen leaves dense go to the fp32 row-group kernel
+    (``ipe_fused_native`` list mode) with the same hint and threshold."""
+
+    def __init__(self, X, k, d_pad, k_pad, alpha, device):
+        n, d = X.shape
+        self.n, self.d, self.k, self.d_pad, self.k_pad = n, d, int(k), int(d_pad), int(k_pad)
+        self.alpha = float(alpha)
+        dev = device
+        self.Xh = torch.zeros((n, d_pad), dtype=torch.float16, device=dev)
+        step = 1 << 20
+        for s in range(0, n, step):
+            self.Xh[s:s + step, :d] = (X[s:s + step].float() * self.alpha).to(torch.float16)
+        self.C_op = torch.zeros(operand_f16_shape(k_pad, d_pad), dtype=torch.float16, device=dev)
+        self.thr = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.hj = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        self.vlo = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.vhi = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.H = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.rfire = torch.empty((max(n, 1), 8), dtype=torch.int16, device=dev)
+        self.rst = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        self.rflag = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        self.best = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        self.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        cm = min(n, IPE16_CHUNK)
+        self.list = torch.empty(max(cm * IPE16_CAPR, 1), dtype=torch.int64, device=dev)
+        self.nchunks = max(1, -(-n // IPE16_CHUNK))
+        # per chunk: [list count, dense count]
+        self.counts = torch.zeros((self.nchunks, 2), dtype=torch.int32, device=dev)
+        self.counts_host = torch.zeros((self.nchunks, 2), dtype=torch.int32, pin_memory=True)
+        self.ev = torch.cuda.Event()
+        # per-pair hazard of the far band (the band edge's worst case): the
+        # row fires somewhere with probability ~ k * ht; a larger ht narrows
+        # the near set, a smaller one lists fewer fires
+        # (a fired far pair costs one inner product and a thinning test; a
+        # near pair a full median-of-Q sampler: a high target pays)
+        self.ht = float(__import__("os").environ.get("SQ_IPE16_HT", "9e-4"))
+        # bands narrower than this fraction of their lower edge: dense
+        self.min_width = float(__import__("os").environ.get("SQ_IPE16_MINW", "0.5"))
+        self.last_dense = 0
+
+    def relaunch(self, op):
+        """Re-run one phase of the last E-step's last chunk (kernel timing)."""
+        ia, da, st = self._last_args
+        return nat.native().ipe16(op, ia.data_ptr(), da.data_ptr(), st)
+
+    @staticmethod
+    @__import__("functools").lru_cache(maxsize=64)
+    def band_m(Q, ht):
+        """The bin distance m at which the far band's hazard bound (row_cut's
+        pu(m)) equals ``ht``: the band starts where m_lo >= this."""
+        h = (Q + 1) // 2
+        cq = 1.0
+        for i in range(h):
+            cq = cq * (Q - i) / (i + 1)
+        cqh = float(torch.tensor(cq * 1.0002 * (1 + 1e-6), dtype=torch.float32))
+
+        def pu(m):
+            r = (1.0 / m) * (1 + 1e-5)
+            pb = (r + r * r) * 0.500012 * (1 + 1e-5)
+            return cqh * pb ** h * (1 + 2e-3)
+
+        lo, hi = 3.0, 1e9
+        if pu(lo) <= ht:
+            return lo
+        for _ in range(200):
+            mid = math.sqrt(lo * hi)
+            if pu(mid) <= ht:
+                hi = mid
+            else:
+                lo = mid
+        return hi
+
+    def set_centers(self, C32):
+        centers_to_f16_native(C32, self.C_op, self.k, self.d, self.d_pad, self.k_pad, self.alpha)
+
+    def estep(self, X, C32, hint, xn, cn, labels, mind, eps, Q, key: RngKey, tie: RngKey,
+              skey: RngKey, bkey: RngKey, row_offset, first, stats=None, fallback=None):
+        """``hint`` (int32 [n]) is read (and, when ``first``, written by the
+        argmin sweep first); ``fallback(rows, count, list_n, thr, hj, s, e)``
+        runs the fp32 kernel over the dense rows of chunk [s, e)."""
+        n = self.n
+        if n == 0:
+            return
+        m = nat.native()
+        st = nat.stream_handle(X.device)
+        ia = torch.zeros(48, dtype=torch.int64)
+        da = torch.tensor([float(eps), self.alpha, self.band_m(int(Q), min(self.ht, 9.0e-4)),
+                           self.min_width], dtype=torch.float64)
+        ldx = X.stride(0)
+        ia[1] = ldx
+        ia[2] = C32.data_ptr()
+        ia[4] = self.C_op.data_ptr()
+        ia[8] = cn.data_ptr()
+        ia[24] = 0 if stats is None else stats.data_ptr()
+        ia[26], ia[27], ia[28], ia[29], ia[30] = self.d, self.d_pad, self.k, self.k_pad, int(Q)
+        for i, kk in ((32, key), (36, tie), (40, skey), (44, bkey)):
+            ia[i], ia[i + 1], ia[i + 2], ia[i + 3] = kk.k0, kk.k1, kk.s0, kk.s1
+        self.counts.zero_()
+        iap, dap = ia.data_ptr(), da.data_ptr()
+        last = self.nchunks - 1
+
+        def run(op):
+            rc = m.ipe16(op, iap, dap, st)
+            if rc:
+                raise RuntimeError(f"ipe16 op {op} failed (hip error {rc})")
+
+        for c in range(self.nchunks):
+            s, e = c * IPE16_CHUNK, min(n, (c + 1) * IPE16_CHUNK)
+            ia[0] = X.data_ptr() + s * ldx * 4
+            ia[3] = self.Xh.data_ptr() + s * self.d_pad * 2
+            ia[5] = ia[6] = hint.data_ptr() + s * 4
+            ia[7] = xn.data_ptr() + s * 4
+            for i, t in ((9, self.thr), (10, self.hj), (11, self.vlo), (12, self.vhi),
+                         (13, self.H), (14, self.rfire), (15, self.rst), (16, self.best),
+                         (19, self.dense_rows), (21, self.rflag), (22, labels), (23, mind)):
+                ia[i] = t.data_ptr() + s * t.stride(0) * t.element_size()
+            ia[17] = self.list.data_ptr()
+            ia[18] = self.counts[c].data_ptr()
+            ia[20] = self.counts[c].data_ptr() + 4
+            ia[25] = e - s
+            ia[31] = int(row_offset) + s
+            if first:
+                run(1)
+            run(0)
+            run(2)
+            if c == last:
+                self.counts_host.copy_(self.counts, non_blocking=True)
+                self.ev.record()
+            run(3)
+            run(4)
+        self._last_args = (ia, da, st)   # the last chunk's launch arguments (benchmarks)
+        self.ev.synchronize()
+        dense = self.counts_host[:, 1].tolist()
+        self.last_dense = int(sum(dense))
+        for c, nd in enumerate(dense):
+            if nd > 0:
+                s, e = c * IPE16_CHUNK, min(n, (c + 1) * IPE16_CHUNK)
+                fallback(self.dense_rows[s:], self.counts[c, 1:2], int(nd), self.thr[s:e],
+                         self.hj[s:e], s, e)

@@ -45,6 +45,8 @@ PURPOSE = {
     "ipe": 0x000A,           # inner product estimation
     "ipe_skip": 0x000B,      # IPE hazard budgets / thinning of the pruned screen
     "kmpp": 0x000C,          # reserved: k-means++ device streams
+    "ipe16_skip": 0x000D,    # certified fp16 IPE screen: stream budgets / thinning
+    "ipe16_row": 0x000E,     # certified fp16 IPE screen: per-row budget minimum
 }
 
 
