@@ -29,7 +29,7 @@ def main():
                       seed=2024, comm=Comm(None))
     eng.set_centers(C0)
     eng.ipe16_stats = torch.zeros(8, dtype=torch.int64, device=dev)
-    names = ["near", "fired", "fired_exact", "dense", "flagged", "no_band"]
+    names = ["near", "fired", "fired_exact", "dense", "flagged", "no_band", "full"]
     for s in range(steps):
         eng.ipe16_stats.zero_()
         C = eng.centers().clone()

@@ -563,7 +563,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
               const int jc = 1024 * seg + 32 * bit + r32;
               if (jc < a.k && jc != hint) {
                 const int s = atomicAdd(&ncnt[rb], 1);
-                if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)jc;
+                if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)(jc | 0x4000);
                 else m = 0u;
               }
             }
@@ -676,6 +676,9 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
         if (dense) {
           c = 0;
         } else {
+          // a fire on the hint is void; a fire on a near pair is merged into
+          // its entry (bit 15): the near kernel decides from the pair's exact
+          // hazard whether it is sampled in full or treated as far
           const int hj = shint[t];
           int w = 0;
           for (int e = 0; e < c; ++e) {
@@ -684,7 +687,11 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
             if (v & 0x8000) {
               const int j = v & 0x3FFF;
               drop = j == hj;
-              for (int f = 0; f < c && !drop; ++f) drop = row_l[f] == (uint16_t)j;
+              for (int f = 0; f < c && !drop; ++f)
+                if (row_l[f] == (uint16_t)(j | 0x4000)) {
+                  row_l[f] = (uint16_t)(j | 0xC000);
+                  drop = true;
+                }
             }
             if (!drop) row_l[w++] = v;
           }
@@ -715,7 +722,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       if (a.stats) {
         uint32_t nfire = 0, nnear = 0;
         for (int e = 0; e < c; ++e) {
-          if (row_l[e] & 0x8000) ++nfire; else ++nnear;
+          if (row_l[e] & 0x4000) ++nnear; else ++nfire;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -764,7 +771,7 @@ __global__ void __launch_bounds__(256) ipe16_near_kernel(NearArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
   const long long cnt = *a.list_count;
-  uint32_t st_exact = 0;
+  uint32_t st_exact = 0, st_full = 0;
   for (long long base = ((long long)blockIdx.x * 4 + wave) * 64; base < cnt;
        base += (long long)gridDim.x * 256) {
     constexpr int B = 4;
@@ -801,27 +808,34 @@ __global__ void __launch_bounds__(256) ipe16_near_kernel(NearArgs a) {
       const long long r = (long long)(ent >> 16);
       const int j = (int)(ent & 0x3FFFu);
       const bool fired = (ent & 0x8000u) != 0;
+      const bool near = (ent & 0x4000u) != 0;
       const long long g = a.row_offset + r;
       const float ip = sip[threadIdx.x];
       const float nx2 = a.xn[r], ny2 = a.cn[j];
+      const float t = a.thr[r];
       float dt = __builtin_inff();
-      if (!fired) {
+      // the pair's exact hazard (canonical inner product): a near pair the
+      // row's band could not certify may still be far - ipe_hazard passes and
+      // its bound P(D~ <= thr) <= pibar <= 1 - exp(-H_row) - and then it is a
+      // far pair of its stream like the others (fired: thinned; else nothing)
+      uint32_t hq = 0;
+      float pbar = 1.0f;
+      const bool ok = ipe_hazard(ip, nx2, ny2, ipe_sthr(t), a.sc, hq, pbar);
+      const int h = (a.Q + 1) / 2;
+      const double pib = ok ? binom_upper_tail((double)pbar, a.Q, h) * (1.0 + 1e-12) : 1.0;
+      const double beff = -expm1(-(double)a.H[r]);
+      const bool far = !near || (ok && pib <= beff);
+      if (!far) {
+        ++st_full;
         dt = ipe_distance(ip, (double)nx2, (double)ny2, a.eps, a.Q, a.key,
                           (unsigned long long)g * (unsigned long long)a.k + (unsigned long long)j);
-      } else {
-        const float t = a.thr[r];
-        uint32_t hq = 0;
-        float pbar = 1.0f;
-        const bool ok = ipe_hazard(ip, nx2, ny2, ipe_sthr(t), a.sc, hq, pbar);
+      } else if (fired) {
         WordStream ws(a.skey, (unsigned long long)g * 32ull + (unsigned long long)(j & 31));
         ws.b = (uint32_t)(2 + 2 * (j >> 5));
         (void)ws.next();
-        (void)ws.next();                     // words 0, 1: the stream's next budget (sweep)
+        (void)ws.next();                     // words 0, 1: the stream's next budget (prep)
         const uint32_t w2 = ws.next(), w3 = ws.next();
-        const double beff = -expm1(-(double)a.H[r]);
         const double u = u53(w2, w3) * beff;
-        const int h = (a.Q + 1) / 2;
-        const double pib = ok ? binom_upper_tail((double)pbar, a.Q, h) * (1.0 + 1e-12) : 1.0;
         if (u < pib) {
           ++st_exact;
           dt = ipe_pruned_exact((double)ip, (double)nx2 + (double)ny2, a.eps, a.Q, t, u, ws);
@@ -833,8 +847,12 @@ __global__ void __launch_bounds__(256) ipe16_near_kernel(NearArgs a) {
   }
   if (a.stats) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) st_exact += (uint32_t)__shfl_xor((int)st_exact, o, 64);
+    for (int o = 32; o > 0; o >>= 1) {
+      st_exact += (uint32_t)__shfl_xor((int)st_exact, o, 64);
+      st_full += (uint32_t)__shfl_xor((int)st_full, o, 64);
+    }
     if (lane == 0 && st_exact) atomicAdd(a.stats + 2, (unsigned long long)st_exact);
+    if (lane == 0 && st_full) atomicAdd(a.stats + 6, (unsigned long long)st_full);
   }
 }
 

@@ -71,8 +71,9 @@ def test_certified_delta_estep_matches_reference(F):
             assert eng.fast and eng.certified      # the certified filter ran
         assert band[np.arange(n), lo].all()
         co[np.arange(n), lo] += 1
-        # the inertia is the sum of minimum distances: the same every repetition
-        assert io == pytest.approx(float(z["inert1"][s]), rel=1e-9)
+        # the inertia is the sum of minimum distances (fp32 per row on the
+        # GPU, fp64 in the reference): the same every repetition
+        assert io == pytest.approx(float(z["inert1"][s]), rel=2e-7)
     assert _contingency(cr[multi].ravel(), co[multi].ravel()) > P_MIN
 
 
@@ -106,4 +107,11 @@ def test_fused_ipe_estep_law_matches_reference(F):
     io = mind.double().cpu().numpy().reshape(REPS, 4).sum(1)
     assert (cr > 0).sum() >= 6
     assert _contingency(cr.ravel(), co.ravel()) > P_MIN
-    assert stats.ks_2samp(ir, io).pvalue > P_MIN
+    # the estimated inertia takes discrete values (sums of 2 S sin^2 classes),
+    # evaluated in fp32 on the GPU and fp64 in the reference: compare the
+    # laws of the values rounded to 6 significant digits
+    rnd = lambda v: np.round(np.asarray(v, dtype=np.float64), 4)
+    vals, inv = np.unique(np.concatenate([rnd(ir), rnd(io)]), return_inverse=True)
+    ca = np.bincount(inv[:len(ir)], minlength=len(vals))
+    cb = np.bincount(inv[len(ir):], minlength=len(vals))
+    assert _contingency(ca.astype(float), cb.astype(float)) > P_MIN
