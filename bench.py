@@ -162,16 +162,23 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
         extra["ipe_samples_iter_per_s"] = a.n * a.ipe_steps / el
         extra["ipe_ms_per_step"] = el / a.ipe_steps * 1e3
         extra["ipe_pairs_per_s"] = a.n * a.k * a.ipe_steps / el
-        # one more (untimed) step with the screen's pair counters
+        # one more (untimed) step with the screens' pair counters: the fp16
+        # band screen (csrc/ipe16.hip) and the fp32 kernel of its dense rows
         eng.ipe_stats = torch.zeros(5, dtype=torch.int64, device=dev)
+        eng.ipe16_stats = torch.zeros(8, dtype=torch.int64, device=dev)
         eng.step()[1].tolist()
         st = eng.ipe_stats.double()
         comm.all_reduce_(st)
+        s16 = eng.ipe16_stats.double()
+        comm.all_reduce_(s16)
         tot = float(a.n) * a.k
-        extra["ipe_screen"] = {"screened_frac": float(st[0]) / tot,
-                               "full_sampler_frac": float(st[1]) / tot,
-                               "fires": int(st[2]), "fires_exact_branch": int(st[3]),
-                               "first_sweep_wgs": int(st[4])}
+        extra["ipe_screen"] = {
+            "listed_near_per_row": float(s16[0]) / a.n, "listed_fired_per_row": float(s16[1]) / a.n,
+            "full_sampler_per_row": (float(s16[6]) + float(st[1])) / a.n,
+            "fired_exact_branch": int(s16[2]) + int(st[3]),
+            "dense_row_frac": float(s16[3]) / a.n, "no_band_row_frac": float(s16[5]) / a.n,
+            "dense_rows_fp32_screened_frac": float(st[0]) / tot}
+        eng.ipe_stats = eng.ipe16_stats = None
         del eng
         torch.cuda.empty_cache()
     except Exception as e:

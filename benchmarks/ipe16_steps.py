@@ -53,8 +53,8 @@ def main():
         a2 = st.alpha ** 2
         print(json.dumps({"row": int(r), "thr": float(st.thr[r]), "hint": int(st.hj[r]),
                           "D_hint": float(D[int(st.hj[r])]) if st.hj[r] >= 0 else None,
-                          "Dl": float(st.vlo[r]) / a2 + float(xn[r]),
-                          "Dh": float(st.vhi[r]) / a2 + float(xn[r]),
+                          "Dl": float(st.vlo[r, 0]) / a2 + float(xn[r]),
+                          "Dh": float(st.vhi[r, 0]) / a2 + float(xn[r]),
                           "D_sorted": [round(float(v), 1) for v in ds[:6]],
                           "D_q10": float(np.quantile(ds, 0.1)), "D_max": float(ds[-1])}))
 

@@ -63,6 +63,7 @@ constexpr int kRows = kNW * 32 * kRS;   // 256 rows per block
 constexpr int kRing = 3;      // centroid-tile LDS slots
 constexpr int kCapR = 64;     // listed pairs per row (more: dense)
 constexpr int kNLS = kCapR + 2;   // LDS row stride of the lists (uint16): no bank aliasing
+constexpr int kMaxG = 4;      // centroid groups (tiles sorted by |c|^2): one band per group
 constexpr int kFireCap = 7;   // listed fires per row (more: dense); [0] of a row's record = count
 
 SQ_DEV float vmin(float a, float b) {
@@ -245,6 +246,8 @@ struct PrepArgs {
   unsigned char* rst;
   unsigned long long* best;
   uint16_t* rfire;          // [n][8]: count, then up to kFireCap fired pairs (j | 0x8000)
+  const float* gS;          // [G][2] min / max |c|^2 of each centroid group
+  int G;
   long long n;
   int d, k;
   double eps;
@@ -323,11 +326,27 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
     Cut cut{-__builtin_inff(), __builtin_inff(), 0.0f, 0};
     uint16_t fire[kFireCap];
     int nf = 0;
+    float glo[kMaxG], ghi[kMaxG];
     if (l >= 0) {
       t = ipe_distance(sip[threadIdx.x], (double)nx2, (double)a.cn[l], a.eps, a.Q, a.key,
                        (unsigned long long)g * (unsigned long long)a.k + (unsigned long long)l);
       const float sthr = ipe_sthr(t);
-      cut = row_cut(nx2, sthr, ipe_kt(sthr), nx2 + cmin, nx2 + cmax, a.sc, cp);
+      // one band per centroid group (its own S range: the groups are
+      // contiguous in |c|^2); a group without a band lists all its pairs
+      int any = 0;
+      for (int q = 0; q < a.G; ++q) {
+        const Cut cq = row_cut(nx2, sthr, ipe_kt(sthr), nx2 + a.gS[2 * q], nx2 + a.gS[2 * q + 1],
+                               a.sc, cp);
+        // (no band: [+inf, +inf] - med3(v, +inf, +inf) != v, every pair near;
+        // an inverted interval would make med3 return v: far)
+        glo[q] = cq.ok ? cq.vlo : __builtin_inff();
+        ghi[q] = cq.ok ? cq.vhi : __builtin_inff();
+        if (cq.ok) {
+          cut = cq;   // H depends on m_t only: the same for every group
+          any = 1;
+        }
+      }
+      cut.ok = any;
       a.best[r] = pack_best(t, a.tie, g, l);
     }
     if (cut.ok) {
@@ -383,8 +402,10 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
     }
     a.thr[r] = t;
     a.hj[r] = l >= 0 ? l : -2;
-    a.vlo[r] = cut.vlo;
-    a.vhi[r] = cut.vhi;
+    for (int q = 0; q < a.G; ++q) {
+      a.vlo[r * kMaxG + q] = cut.ok ? glo[q] : -__builtin_inff();
+      a.vhi[r * kMaxG + q] = cut.ok ? ghi[q] : __builtin_inff();
+    }
     a.H[r] = cut.H;
     a.rst[r] = cut.ok ? 0 : 1;
     uint16_t* fr = a.rfire + (size_t)r * 8;
@@ -422,6 +443,8 @@ struct SweepArgs {
   const float* vhi;
   const unsigned char* rst;
   const uint16_t* rfire;    // prep's fired pairs per row
+  const int* perm;          // operand column (sorted by |c|^2) -> centroid id
+  int G;
   const int* hj;            // hints (prep's)
   int* hint_out;            // ARGMIN output
   unsigned long long* list; // (row << 16) | j | fired << 15
@@ -448,7 +471,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   uint16_t* nl = reinterpret_cast<uint16_t*>(smem + kRing * SLOT);      // [kRows][kNLS]
   int* ncnt = reinterpret_cast<int*>(nl + kRows * kNLS);                  // [kRows]
   int* shint = ncnt + kRows;                                              // [kRows]
-  int* wsum = shint + kRows;                                              // [kNW] flush scan
+  float* sband = reinterpret_cast<float*>(shint + kRows);                 // [kRows][G][2]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -560,8 +583,9 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
             while (m) {
               const int bit = __builtin_ctz(m);
               m &= m - 1u;
-              const int jc = 1024 * seg + 32 * bit + r32;
-              if (jc < a.k && jc != hint) {
+              const int jp = 1024 * seg + 32 * bit + r32;
+              const int jc = jp < a.k ? a.perm[jp] : -1;
+              if (jc >= 0 && jc != hint) {
                 const int s = atomicAdd(&ncnt[rb], 1);
                 if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)(jc | 0x4000);
                 else m = 0u;
@@ -571,6 +595,21 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
         }
     }
   };
+
+  // the lane's 32 rows' band edges of centroid group q
+  auto load_bands = [&](int q) {
+    if constexpr (!ARGMIN) {
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int e = ((wave * kRS + st) * 32 + rl_of(i)) * kMaxG + q;
+          lo[st][i] = sband[2 * e];
+          hi[st][i] = sband[2 * e + 1];
+        }
+    }
+  };
+  auto group_of = [&](int t) { return (t * a.G) / n_tiles; };
 
   int U = 0;
   stage(0);
@@ -605,18 +644,16 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
         }
         ncnt[t] = c;
       }
-#pragma unroll
-      for (int st = 0; st < kRS; ++st)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          long long r = row_of(blk, st, rl_of(i));
-          const bool v = r < n;
-          r = v ? r : n - 1;
-          lo[st][i] = v ? a.vlo[r] : __builtin_inff();
-          hi[st][i] = v ? a.vhi[r] : -__builtin_inff();
-        }
+      // the block's bands (row, group) -> LDS; a row past n: all far
+      for (int e = tid; e < kRows * kMaxG; e += kNW * 64) {
+        const long long r = blk * kRows + e / kMaxG;
+        const bool v = r < n && (e % kMaxG) < a.G;
+        sband[2 * e] = v ? a.vlo[blk * kRows * kMaxG + e] : -__builtin_inff();
+        sband[2 * e + 1] = v ? a.vhi[blk * kRows * kMaxG + e] : __builtin_inff();
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      load_bands(0);
     }
     // ---- the sweep: half 0 of tile t (epilogue of tile t - 1's half 1),
     // half 1 (epilogue of half 0), one ring slot per tile
@@ -628,6 +665,8 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       pass(std::integral_constant<int, 0>{}, buf(U), cA, cB, (uint32_t)(2 * t - 1), t > 0);
       // segment (t - 1) / 16 complete with tile t - 1's half 1
       if ((t & 15) == 0 && t > 0) flush_masks(blk, (t - 1) >> 4);
+      // tile t's values (epilogues from the next pass on) use its group's bands
+      if (t > 0 && group_of(t) != group_of(t - 1)) load_bands(group_of(t));
       pass(std::integral_constant<int, 1>{}, buf(U), cB, cA, (uint32_t)(2 * t), true);
       sync_tile();
       ++U;
@@ -655,7 +694,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
               const uint32_t p = __float_as_uint(v);
               const uint32_t q = (p >> 5) & ((1u << qbits) - 1u);
               const int j = (int)((q >> 1) * kTileN + (q & 1u) * 32u + (p & 31u));
-              a.hint_out[r] = j < a.k ? j : 0;
+              a.hint_out[r] = a.perm[j < a.k ? j : 0];
             }
           }
         }
@@ -877,7 +916,8 @@ using namespace sq::i16;
 template <int KSD, bool ARGMIN>
 static int launch_sweep(const SweepArgs& a, hipStream_t st) {
   constexpr int SLOT = (KSD + 1) * 2048;
-  const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 3 * kRows * 4 + 64;
+  const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 2 * kRows * 4 +
+                     (size_t)kRows * kMaxG * 2 * 4;
   auto kern = ipe16_sweep_kernel<KSD, ARGMIN>;
   static bool attr = false;
   if (!attr) {
@@ -927,7 +967,8 @@ extern "C" {
 //   [18] list_count, [19] dense_rows, [20] dense_count, [21] rflag,
 //   [22] labels, [23] mind, [24] stats, [25] n, [26] d, [27] d_pad, [28] k,
 //   [29] k_pad, [30] Q, [31] row_offset, [32..35] key, [36..39] tie,
-//   [40..43] skey, [44..47] bkey
+//   [40..43] skey, [44..47] bkey, [48] perm (operand column -> centroid),
+//   [49] group |c|^2 ranges [G][2], [50] G
 // da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
 int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -937,7 +978,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   const int Q = (int)ia[30];
   const double eps = da[0];
   if (Q < 1 || Q > kIpeMaxQ || !(Q & 1) || k < 1 || k > 16384 || k_pad % 64 || k_pad < k ||
-      d < 1 || d > d_pad || d_pad % 16 || d_pad > 256 || !(eps > 0.0))
+      d < 1 || d > d_pad || d_pad % 16 || d_pad > 256 || !(eps > 0.0) || ia[50] < 1 ||
+      ia[50] > kMaxG || ia[50] > k_pad / 64)
     return (int)hipErrorInvalidValue;
   auto P = [&](int i) -> void* { return (void*)(intptr_t)ia[i]; };
   const IpeScreen sc = make_screen(k, eps, Q);
@@ -957,6 +999,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.rfire = (uint16_t*)P(14);
     a.rst = (unsigned char*)P(15);
     a.best = (unsigned long long*)P(16);
+    a.gS = (const float*)P(49);
+    a.G = (int)ia[50];
     a.n = n;
     a.d = d;
     a.k = k;
@@ -997,6 +1041,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.rfire = (const uint16_t*)P(14);
     a.rst = (const unsigned char*)P(15);
     a.hj = (const int*)P(10);
+    a.perm = (const int*)P(48);
+    a.G = (int)ia[50];
     a.hint_out = (int*)P(6);
     a.list = (unsigned long long*)P(17);
     a.list_count = (int*)P(18);

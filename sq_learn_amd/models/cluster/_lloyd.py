@@ -533,7 +533,7 @@ class LloydEngine:
         mind = torch.empty(n, dtype=torch.float32, device=self.device)
         C32 = self.C.float().contiguous()
         cn = (C32 * C32).sum(1).contiguous()
-        st.set_centers(C32)
+        st.set_centers(C32, cn)
         tie = self._key("band_select")
         xn = self._ipe_xn
         stats = getattr(self, "ipe16_stats", None)

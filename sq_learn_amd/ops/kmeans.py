@@ -1005,8 +1005,8 @@ class Ipe16:
         self.C_op = torch.zeros(operand_f16_shape(k_pad, d_pad), dtype=torch.float16, device=dev)
         self.thr = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
         self.hj = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        self.vlo = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
-        self.vhi = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.vlo = torch.empty((max(n, 1), 4), dtype=torch.float32, device=dev)   # [row][group]
+        self.vhi = torch.empty((max(n, 1), 4), dtype=torch.float32, device=dev)
         self.H = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
         self.rfire = torch.empty((max(n, 1), 8), dtype=torch.int16, device=dev)
         self.rst = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
@@ -1062,8 +1062,27 @@ class Ipe16:
                 lo = mid
         return hi
 
-    def set_centers(self, C32):
-        centers_to_f16_native(C32, self.C_op, self.k, self.d, self.d_pad, self.k_pad, self.alpha)
+    def set_centers(self, C32, cn=None):
+        """The fp16 operand of the centroids SORTED by |c|^2 (``perm``: operand
+        column -> centroid id): its tiles fall into G groups of contiguous
+        norms, each with its own band per row (a narrower S range, a tighter
+        band).  ``cn`` = the fp32 |c|^2 the E-step uses."""
+        if cn is None:
+            cn = (C32 * C32).sum(1)
+        nt = self.k_pad // 64
+        G = max(1, min(4, nt))
+        order = torch.argsort(cn, stable=True)
+        self.perm = order.to(torch.int32).contiguous()
+        Cs = C32.index_select(0, order).contiguous()
+        centers_to_f16_native(Cs, self.C_op, self.k, self.d, self.d_pad, self.k_pad, self.alpha)
+        cs = cn.index_select(0, order)
+        lo_t = [(q * nt) // G for q in range(G)]
+        hi_t = [((q + 1) * nt) // G for q in range(G)]
+        first = torch.tensor([min(64 * t, self.k - 1) for t in lo_t], device=cn.device)
+        last = torch.tensor([min(64 * t, self.k) - 1 for t in hi_t], device=cn.device)
+        self.gS = torch.stack([cs.index_select(0, first), cs.index_select(0, last)], 1)
+        self.gS = self.gS.float().contiguous()
+        self.G = G
 
     def estep(self, X, C32, hint, xn, cn, labels, mind, eps, Q, key: RngKey, tie: RngKey,
               skey: RngKey, bkey: RngKey, row_offset, first, stats=None, fallback=None):
@@ -1075,7 +1094,10 @@ class Ipe16:
             return
         m = nat.native()
         st = nat.stream_handle(X.device)
-        ia = torch.zeros(48, dtype=torch.int64)
+        ia = torch.zeros(56, dtype=torch.int64)
+        ia[48] = self.perm.data_ptr()
+        ia[49] = self.gS.data_ptr()
+        ia[50] = self.G
         da = torch.tensor([float(eps), self.alpha, self.band_m(int(Q), min(self.ht, 9.0e-4)),
                            self.min_width], dtype=torch.float64)
         ldx = X.stride(0)

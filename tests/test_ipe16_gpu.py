@@ -239,3 +239,27 @@ def test_ipe16_rows_invariant_to_chunks_and_offsets(cuda, monkeypatch, with_hint
         assert np.array_equal(la[7:], lc) and np.array_equal(ma[7:], mc)
     s = st.tolist()
     assert s[0] > 0, s
+
+
+def test_ipe16_lloyd_trajectory_matches_fp32_kernel(cuda, monkeypatch):
+    """Blob data (256 centroids in 4 norm groups, some groups without a band
+    for some rows): the Lloyd trajectory's inertia with the screen follows
+    the fp32 fused kernel's to within the law's (tiny) sampling noise."""
+    from sq_learn_amd.models.cluster._lloyd import LloydEngine
+    from sq_learn_amd.utils.datasets import make_blobs_device
+    from sq_learn_amd.models._data import Data, gather_rows
+    from sq_learn_amd.parallel.comm import Comm
+    n, d, k = 200_000, 64, 256
+    X, _ = make_blobs_device(n, d, centers=k, cluster_std=1.0, seed=1, device=cuda,
+                             dtype=torch.float32)
+    C0 = gather_rows(Data(X, n, 0, Comm(None), "sharded"),
+                     np.random.RandomState(1).choice(n, k, replace=False))
+    out = {}
+    for use16 in ("0", "1"):
+        monkeypatch.setenv("SQ_IPE16", use16)
+        eng = LloydEngine(X, k, delta=0.5, true_distance_estimate=True, intermediate_error=True,
+                          seed=3)
+        eng.set_centers(C0)
+        out[use16] = [eng.step()[1].tolist()[0] for _ in range(4)]
+    a, b = np.array(out["0"]), np.array(out["1"])
+    assert np.all(np.abs(a - b) <= 2e-3 * a), (a, b)
