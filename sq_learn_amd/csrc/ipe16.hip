@@ -527,9 +527,9 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   // per-lane state: the 16 rows' band edges per set (screen) / running
   // packed minima (argmin); the near bits of the last epilogue
   float lo[kRS][16], hi[kRS][16];
-  // near bits: register (st, i) of this lane, bit h' = half-tile index within
-  // the current 1024-column segment (column 32 h' + r32 of the segment)
-  uint32_t mk[kRS][16];
+  // near bits of the last epilogue (bit 16 st + i: register (st, i)); rows
+  // whose list is full are muted (dense: no more pushes from this lane)
+  uint32_t nb = 0, mute = 0;
   auto rl_of = [&](int i) { return (i & 3) + 8 * (i >> 2) + 4 * half; };
   // one value of the previous half-tile (o), half-tile index q = 2 t + h
   auto epi = [&](int st, int i, float v, uint32_t q) {
@@ -537,8 +537,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       lo[st][i] = vmin(lo[st][i], and_or(v, keep, (q << 5) | (uint32_t)r32));
     } else {
       const bool far = vmed3(v, lo[st][i], hi[st][i]) == v;
-      const uint32_t hb = 1u << (q & 31u);
-      mk[st][i] = far ? mk[st][i] : (mk[st][i] | hb);
+      nb |= far ? 0u : (1u << (16 * st + i));
     }
   };
   typedef f32x16 Acc[kRS];
@@ -565,34 +564,27 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // the near pairs of segment seg (columns 1024 seg ..): each lane walks the
-  // set bits of its 32 registers (the hint, co-located centroids, padding);
-  // a row whose list is already full is skipped (dense)
-  auto flush_masks = [&](long long b, int seg) {
+  // near pairs of the half-tile just screened (operand column jp): each lane
+  // walks its set bits (the hint, co-located centroids, padding)
+  auto flush_near = [&](long long b, int jp) {
     if constexpr (!ARGMIN) {
-#pragma unroll
-      for (int st = 0; st < kRS; ++st)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          uint32_t m = mk[st][i];
-          mk[st][i] = 0u;
-          if (__ballot(m != 0u) != 0ull) {
-            const int rb = (wave * kRS + st) * 32 + rl_of(i);
-            if (row_of(b, st, rl_of(i)) >= n || ncnt[rb] > kCapR) m = 0u;
-            const int hint = shint[rb];
-            while (m) {
-              const int bit = __builtin_ctz(m);
-              m &= m - 1u;
-              const int jp = 1024 * seg + 32 * bit + r32;
-              const int jc = jp < a.k ? a.perm[jp] : -1;
-              if (jc >= 0 && jc != hint) {
-                const int s = atomicAdd(&ncnt[rb], 1);
-                if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)(jc | 0x4000);
-                else m = 0u;
-              }
-            }
+      nb &= ~mute;
+      if (__ballot(nb != 0u) != 0ull) {
+        const int jc = jp < a.k ? a.perm[jp] : -1;
+        uint32_t m = nb;
+        while (m) {
+          const int bit = __builtin_ctz(m);
+          m &= m - 1u;
+          const int st = bit >> 4, i = bit & 15;
+          const int rb = (wave * kRS + st) * 32 + rl_of(i);
+          if (jc >= 0 && jc != shint[rb] && row_of(b, st, rl_of(i)) < n) {
+            const int s = atomicAdd(&ncnt[rb], 1);
+            if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)(jc | 0x4000);
+            else mute |= 1u << bit;   // the row is dense
           }
         }
+      }
+      nb = 0;
     }
   };
 
@@ -626,10 +618,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) lo[st][i] = __builtin_inff();
     } else {
-#pragma unroll
-      for (int st = 0; st < kRS; ++st)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mk[st][i] = 0u;
+      mute = 0;
       // the rows' hints and the fires prep listed (thread t: row t)
       for (int t = tid; t < kRows; t += kNW * 64) {
         const long long r = blk * kRows + t;
@@ -663,11 +652,11 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
 #pragma unroll
       for (int j = 0; j < PFD; ++j) bq[j] = frag(buf(U), j);
       pass(std::integral_constant<int, 0>{}, buf(U), cA, cB, (uint32_t)(2 * t - 1), t > 0);
-      // segment (t - 1) / 16 complete with tile t - 1's half 1
-      if ((t & 15) == 0 && t > 0) flush_masks(blk, (t - 1) >> 4);
+      flush_near(blk, 64 * (t - 1) + 32 + r32);
       // tile t's values (epilogues from the next pass on) use its group's bands
       if (t > 0 && group_of(t) != group_of(t - 1)) load_bands(group_of(t));
       pass(std::integral_constant<int, 1>{}, buf(U), cB, cA, (uint32_t)(2 * t), true);
+      flush_near(blk, 64 * t + r32);
       sync_tile();
       ++U;
     }
@@ -676,7 +665,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     for (int st = 0; st < kRS; ++st)
 #pragma unroll
       for (int i = 0; i < 16; ++i) epi(st, i, cB[st][i], (uint32_t)(2 * n_tiles - 1));
-    flush_masks(blk, (n_tiles - 1) >> 4);
+    flush_near(blk, 64 * (n_tiles - 1) + 32 + r32);
 
     if constexpr (ARGMIN) {
       // row minimum over the 32 lanes of each half: the packed value holds
