@@ -1001,8 +1001,39 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
     long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
     long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
-    const int* __restrict__ fidx, int nf, int k) {
+    const int* __restrict__ fidx, int nf, int k, const float2* __restrict__ mrec,
+    const int* __restrict__ rec_it, const int* __restrict__ mcand, const double* __restrict__ cum,
+    int ring, int it_now, int it_base, int* __restrict__ n_cert) {
   constexpr int kBoundsChunk = PER * 256;   // PER rows per thread (bit masks)
+  const float2* __restrict__ rec_ = mrec;
+  // A multi-candidate row whose last fp32 screen certified the band {argmin}
+  // (recheck_fast_kernel record: sqrt-domain upper bound ha to the argmin,
+  // lower bound lo to every other candidate, at iteration rit) keeps that
+  // band while (ha + acc_a)^2 + delta < (lo - max_j acc_j)^2, acc_j the
+  // accumulated shift of candidate j since rit (cum: per-iteration prefix
+  // sums of the shifts, a ring of `ring` iterations): label, correction (0)
+  // and the exact band are those the screen would find - the row is not read.
+  uint32_t ncert = 0;
+  auto certify = [&](long long i, int l) -> bool {
+    const int rit = rec_it[i];
+    if (rit < it_base || rit < 0 || rit > it_now || it_now - rit >= ring) return false;
+    const float2 r = rec_[i];
+    const int* mc = mcand + i * (kMaxCand + 1);
+    const int c_r = min(max(mc[0], 0), kMaxCand);
+    const double* cn = cum + (size_t)(it_now % ring) * k;
+    const double* cr = cum + (size_t)(rit % ring) * k;
+    double acc_a = -1.0, acc_o = 0.0;
+    for (int c = 0; c < c_r; ++c) {
+      const int j = mc[1 + c];
+      const double acc = (cn[j] - cr[j]) * (1.0 + 1e-12) + 1e-300;
+      if (j == l) acc_a = acc; else acc_o = fmax(acc_o, acc);
+    }
+    if (acc_a < 0.0) return false;
+    const double ha = (double)r.x + acc_a, lo = (double)r.y - acc_o;
+    const bool ok = lo > 0.0 && ha * ha * (1.0 + 1e-7) + delta * (1.0 + 1e-9) < lo * lo * (1.0 - 1e-7);
+    ncert += ok ? 1u : 0u;
+    return ok;
+  };
   __shared__ int wsum[4];
   __shared__ int base_a, base_m;
   __shared__ double sf_s[65];               // shifts of the fast centroids, [nf] = max
@@ -1088,7 +1119,7 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
       } else {
         ub[i] = (float)u * (1.0f + 0x1p-22f);
         lb[i] = (float)w * (1.0f - 0x1p-22f);
-        if (mfv[q]) rec |= 1ull << p;
+        if (mfv[q] && !(rec_ && certify(i, l))) rec |= 1ull << p;
       }
     }
   }
@@ -1129,6 +1160,33 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
       rec &= ~(1ull << p);
     }
   }
+  if (n_cert) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ncert += (uint32_t)__shfl_xor((int)ncert, o, 64);
+    if (lane == 0 && ncert) atomicAdd(n_cert, (int)ncert);
+  }
+}
+
+// the multi-row records of the calling thread's next filter / screen launches
+// (null rec: off) - set by the engine before each E-step
+struct MultiRec {
+  float2* rec = nullptr;
+  int* rec_it = nullptr;
+  const double* cum = nullptr;
+  int ring = 0, it_now = 0, it_base = 0;
+  int* n_cert = nullptr;
+};
+static thread_local MultiRec g_mrec;
+extern "C" int sq_multi_records(void* rec, void* rec_it, const void* cum, int ring, int it_now,
+                                int it_base, void* n_cert) {
+  g_mrec.rec = (float2*)rec;
+  g_mrec.rec_it = (int*)rec_it;
+  g_mrec.cum = (const double*)cum;
+  g_mrec.ring = ring;
+  g_mrec.it_now = it_now;
+  g_mrec.it_base = it_base;
+  g_mrec.n_cert = (int*)n_cert;
+  return (rec && (!rec_it || !cum || ring < 2)) ? (int)hipErrorInvalidValue : 0;
 }
 
 // rcount and multi_count must be zero on entry (the caller clears them with
@@ -1136,8 +1194,10 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
 extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const void* shift,
                                 const void* smax, long long n, double delta, void* rlist,
                                 void* rcount, const void* mflag, void* mrows, void* multi_count,
-                                const void* cc, const void* fidx, int nf, int k, void* stream) {
+                                const void* cc, const void* fidx, int nf, int k, void* stream,
+                                const void* mcand) {
   if (n <= 0) return 0;
+  if (g_mrec.rec && !mcand) return (int)hipErrorInvalidValue;
   if (!mflag || !mrows || !multi_count) return (int)hipErrorInvalidValue;
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -1172,7 +1232,9 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                      dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
                      (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
                      (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
-                     (const float*)cc, (const int*)fidx, nf, k);
+                     (const float*)cc, (const int*)fidx, nf, k, g_mrec.rec, g_mrec.rec_it,
+                     (const int*)mcand, g_mrec.cum, g_mrec.ring, g_mrec.it_now, g_mrec.it_base,
+                     g_mrec.n_cert);
   return (int)hipGetLastError();
 }
 
@@ -1399,7 +1461,8 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
     float* __restrict__ mind, long long cap, double delta, float* __restrict__ ub,
-    unsigned char* __restrict__ xflag, int il) {
+    unsigned char* __restrict__ xflag, int il, float2* __restrict__ rec, int* __restrict__ rec_it,
+    int it_now) {
   constexpr int RPW = 64 / LPR;   // rows per wave step
   constexpr int FPL = DX / LPR;
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
@@ -1551,6 +1614,10 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const int plane = inm ? __ffsll((long long)inm) - 1 : gbase;
     const int pick = __shfl(cur.myj, plane, 64);
     const float hpick = __shfl(hi, plane, 64);
+    // the smallest lower bound of the OTHER candidates (the row's record)
+    float lo_o = (mine && lane != plane) ? lo : __builtin_inff();
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) lo_o = fminf(lo_o, __shfl_xor(lo_o, o, 64));
     fix(nxt);
     // stage 3 for the next step (its first two candidate centroids) BEFORE
     // this step's stores: vmcnt retires in issue order, so a load issued
@@ -1568,6 +1635,15 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     if constexpr (UB) ub[g] = sqrtf(hpick) * (1.0f + 0x1p-20f);
     // the rest -> flagged for the fp64 pass (a per-entry byte: no atomics)
     xflag[e] = done ? 0 : 1;
+    // a row whose band is certainly {argmin}: its record (distance bounds to
+    // the argmin and to the nearest other candidate, sqrt domain) lets later
+    // iterations certify the same band from the centroid shifts alone
+    // (bounds_filter_kernel) without reading the row
+    if (rec) {
+      rec[g] = make_float2(sqrtf(hpick) * (1.0f + 0x1p-20f),
+                           sqrtf(fmaxf(lo_o, 0.0f)) * (1.0f - 0x1p-20f));
+      rec_it[g] = done ? it_now : -1;
+    }
     __builtin_amdgcn_sched_barrier(0);
     g2 = g3;
     g3 = g4;
@@ -1847,7 +1923,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
     hipLaunchKernelGGL(fk, dim3(fgrid2), dim3(256), 0, st, (const float*)X, (const float*)Cm,
                        (const long long*)mrows, (const int*)mcand, (const int*)multi_count,
                        (int*)labels, (float*)mind, n, delta, (float*)ub, (unsigned char*)xflag,
-                       sil);
+                       sil, g_mrec.rec, g_mrec.rec_it, g_mrec.it_now);
   }
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,

@@ -29,7 +29,8 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
                                            unsigned, unsigned, unsigned, const void*, int, void*);
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
                                            long long, double, void*, void*, const void*, void*,
-                                           void*, const void*, const void*, int, int, void*);
+                                           void*, const void*, const void*, int, int, void*, const void*);
+__attribute__((weak)) int sq_multi_records(void*, void*, const void*, int, int, int, void*);
 __attribute__((weak)) int sq_fast_centroids(void*, const void*, const void*, int, int, int, void*,
                                             void*, void*, void*);
 // tsgemm64.hip
@@ -256,14 +257,22 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
-  unsigned long long lab, ub, lb, sh, sm, rl, rc, mf, mr, mcnt, cc, fi, st; long long n;
+  unsigned long long lab, ub, lb, sh, sm, rl, rc, mf, mr, mcnt, cc, fi, st, mc = 0; long long n;
   double delta; int nf, k;
-  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKiiK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc,
-                        &mf, &mr, &mcnt, &cc, &fi, &nf, &k, &st))
+  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKiiK|K", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc,
+                        &mf, &mr, &mcnt, &cc, &fi, &nf, &k, &st, &mc))
     return nullptr;
   CHECK(sq_bounds_filter)
   return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(mf),
-                              P(mr), P(mcnt), P(cc), P(fi), nf, k, P(st)));
+                              P(mr), P(mcnt), P(cc), P(fi), nf, k, P(st), P(mc)));
+}
+
+// the multi-row records of this thread's next certified E-steps (null: off)
+static PyObject* py_multi_records(PyObject*, PyObject* a) {
+  unsigned long long rec, rit, cum, nc; int ring, now, base;
+  if (!PyArg_ParseTuple(a, "KKKiiiK", &rec, &rit, &cum, &ring, &now, &base, &nc)) return nullptr;
+  CHECK(sq_multi_records)
+  return ret(sq_multi_records(P(rec), P(rit), P(cum), ring, now, base, P(nc)));
 }
 
 static PyObject* py_fast_centroids(PyObject*, PyObject* a) {
@@ -685,6 +694,7 @@ static PyMethodDef methods[] = {
     {"xtx_geometry", py_xtx_geometry, METH_VARARGS, "xtx tile sizes and pair count"},
     {"xw", py_xw, METH_VARARGS, "fp64 MFMA (A-mu) W"},
     {"bounds_filter", py_bounds_filter, METH_VARARGS, "Hamerly pruning -> active row list"},
+    {"multi_records", py_multi_records, METH_VARARGS, "multi-row band records for the filter"},
     {"fast_centroids", py_fast_centroids, METH_VARARGS, "fastest centroids + Elkan distances"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},

@@ -238,6 +238,21 @@ class LloydEngine:
             self.fast_idx = torch.zeros(max(self.n_fast, 1), dtype=torch.int32, device=dev)
             self.fast_cc = torch.zeros(max(self.k * (self.n_fast + 1), 1), dtype=torch.float32,
                                        device=dev)
+        # multi-candidate row records (csrc/estep_f32.hip): the fp32 screen
+        # stores, for a row whose band it certified as {argmin}, its distance
+        # bounds; the filter re-certifies that band from the accumulated
+        # centroid shifts (prefix sums over a ring of iterations) without
+        # reading the row.  Opt-in (SQ_MULTI_RECORDS=1): on the headline only
+        # ~16 % of the multi rows certify from the shift-norm bound, and the
+        # filter's extra loads cost more than the screen saves.
+        self.mrec = None
+        if (self.bounds and self.incremental
+                and os.environ.get("SQ_MULTI_RECORDS", "0") != "0"):
+            self.mrec = torch.zeros((max(self.n, 1), 2), dtype=torch.float32, device=dev)
+            self.mrec_it = torch.full((max(self.n, 1),), -1, dtype=torch.int32, device=dev)
+            self.cum = torch.zeros((16, self.k), dtype=torch.float64, device=dev)
+            self._rit = 0
+            self._rbase = 0
         self.bounds_valid = False
 
     def _prepare_reduce(self):
@@ -302,6 +317,7 @@ class LloydEngine:
             self._ipe_hint_valid = False
         self.inc_valid = False   # the incremental M-step restarts from scratch
         self.bounds_valid = False
+        self._records_epoch()
         self._kept_frac = self._kept_prev = None   # new centres: re-measure the filter
         self._skips = 0
         self._probing = False
@@ -356,10 +372,19 @@ class LloydEngine:
             self._ipe_cur = 0
             self._ipe_xn = self.xn.float().contiguous()
 
+    def _records_epoch(self):
+        """New centres not reached by tracked shifts: every multi-row record
+        before this point is void."""
+        if getattr(self, "mrec", None) is not None:
+            self._rit += 1
+            self._rbase = self._rit
+            self.cum[self._rit % self.cum.shape[0]].zero_()
+
     def restore_tensors(self, d):
         self._pending = None
         self.inc_valid = False
         self.bounds_valid = False
+        self._records_epoch()
         if self.fast and self.C_op is not None and "C_op" in d:
             self.C_op.copy_(d["C_op"].to(self.device))
         elif self.fast and self.C_op is None and "C_bf16" in d:
@@ -395,6 +420,11 @@ class LloydEngine:
                 # dormant bounds are not maintained by this sweep: invalid
                 # until a bounds-maintaining sweep (the step before a probe)
                 self._bounds_kept = mode != "none"
+                screen = (self.incremental and not full
+                          and os.environ.get("SQ_SCREEN", "1") != "0")
+                if self.mrec is not None and screen:
+                    K.multi_records(self.mrec, self.mrec_it, self.cum, self._rit, self._rbase,
+                                    self.buf.counts[4:5])
                 # a probe (the filter kept > keep_max of the rows twice and was
                 # skipped since) only MEASURES: the filter pass counts the rows
                 # it would keep (the M-step records the fraction), the sweep
@@ -422,9 +452,13 @@ class LloydEngine:
                                                self.row_offset, self.buf,
                                                bounds=(self.ub, self.lb)
                                                if self.bounds and self._bounds_kept else None,
-                                               rows=rows, zero_counts=zero,
-                                               screen=self.incremental and not full
-                                               and os.environ.get("SQ_SCREEN", "1") != "0")
+                                               rows=rows, zero_counts=zero, screen=screen)
+                if self.mrec is not None:
+                    K.multi_records(None)   # thread-local: never leak into another engine
+                    if not screen:
+                        # the sweep rewrote candidate lists the screen did not
+                        # re-record: every record so far is void
+                        self._records_epoch()
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):
@@ -777,6 +811,14 @@ class LloydEngine:
                     torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
                     self.shift_s.mul_(1.0 + 1e-12)
                     torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
+                if self.mrec is not None:
+                    # prefix sums of the shifts: cum[t + 1] = cum[t] + s_t
+                    R = self.cum.shape[0]
+                    torch.add(self.cum[self._rit % R], self.shift_s,
+                              out=self.cum[(self._rit + 1) % R])
+                    self._rit += 1
+            elif self.bounds:
+                self._records_epoch()   # shifts not tracked this update
             if self.bounds:
                 self.bounds_valid = getattr(self, "_bounds_kept", True)
         return self.scalars

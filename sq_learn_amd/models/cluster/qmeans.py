@@ -20,8 +20,10 @@ Parameters keep the reference's names and defaults.  Intentional deviations
 * ``multiprocess`` is accepted and ignored - every (sample, centroid) pair is
   processed by one batched GPU kernel instead of a process pool.
 
-Framework additions: ``device``, ``gemm_precision`` ('bf16' fused MFMA
-kernel / 'fp32' library GEMM), ``compute_prelude`` (eta, mu(A),
+Framework additions: ``device``, ``gemm_precision`` ('bf16': fused bf16
+MFMA kernel, d <= 256, band edge bf16-accurate; 'fp32': the certified E-step - an
+fp16 MFMA filter whose error bound is certified against fp64, multi-candidate
+rows re-checked in fp32/fp64, csrc/estep_f32.hip), ``compute_prelude`` (eta, mu(A),
 condition number), ``ipe_Q`` (median repetitions of IPE), and
 ShardedArray inputs for multi-GPU fits (one process per GPU).
 """

@@ -180,7 +180,9 @@ class EStepBuffers:
         self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
         # [overflow rows, dense rows, multi-candidate rows, rows the bounds
         # filter kept] (int32); ovf_count is a view of slot 0
-        self.counts = torch.zeros(4, dtype=torch.int32, device=device)
+        # [3-pass overflow rows, dense rows, multi rows, kept rows (filter),
+        #  multi rows certified from their records (filter)]
+        self.counts = torch.zeros(5, dtype=torch.int32, device=device)
         self.exact_flag = None   # the fp32 screen's hand-off flags (per multi entry)
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
@@ -404,7 +406,7 @@ def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf:
                                     0 if cc is None else cc.data_ptr(),
                                     0 if cc is None else fidx.data_ptr(),
                                     int(nf if cc is not None else 0), int(shift.numel()),
-                                    nat.stream_handle(labels.device))
+                                    nat.stream_handle(labels.device), buf.multi_cand.data_ptr())
     if rc:
         raise RuntimeError(f"bounds_filter failed (hip error {rc})")
 
@@ -428,6 +430,20 @@ def fast_centroids_native(shift, C, nf, idx, smax_rest, cc, shift_sq=None):
                                      cc.data_ptr(), nat.stream_handle(C.device))
     if rc:
         raise RuntimeError(f"fast_centroids failed (hip error {rc})")
+
+
+def multi_records(rec=None, rec_it=None, cum=None, it_now=0, it_base=0, n_cert=None):
+    """Set (or clear, rec=None) the multi-candidate row records used by this
+    thread's next certified E-steps (csrc/estep_f32.hip: the fp32 screen writes
+    them, the bounds filter certifies unchanged {argmin} bands from them)."""
+    if rec is None:
+        nat.native().multi_records(0, 0, 0, 0, 0, 0, 0)
+        return
+    rc = nat.native().multi_records(rec.data_ptr(), rec_it.data_ptr(), cum.data_ptr(),
+                                    int(cum.shape[0]), int(it_now), int(it_base),
+                                    0 if n_cert is None else n_cert.data_ptr())
+    if rc:
+        raise RuntimeError(f"multi_records failed (hip error {rc})")
 
 
 def ensure_multi_buffers(buf: EStepBuffers, n, device, bounds=False):
