@@ -376,7 +376,7 @@ def _pipeline_extra(extra, a, comm, dev):
         extra["pipeline_error"] = repr(e)[:200]
 
 
-def _fit_extra(extra, a, sa, comm, dev, init, ipe=False, name=None):
+def _fit_extra(extra, a, sa, comm, dev, init, ipe=False, name=None, n_init=1):
     """Wall-clock of a whole QMeans.fit (prelude: eta, mu(A), condition
     number; centring; initialisation; ``fit_iters`` Lloyd iterations with
     tol = 0; final E-step) on the same matrix (BASELINE: fit wall-clock at a
@@ -386,7 +386,7 @@ def _fit_extra(extra, a, sa, comm, dev, init, ipe=False, name=None):
     try:
         from sq_learn_amd.models.cluster import QMeans
         kw = dict(n_clusters=a.k, delta=a.delta, true_distance_estimate=bool(ipe),
-                  intermediate_error=True, true_tomography=False, init=init, n_init=1,
+                  intermediate_error=True, true_tomography=False, init=init, n_init=n_init,
                   max_iter=a.fit_iters, tol=0.0, random_state=a.seed, device=dev,
                   gemm_precision=a.dtype)
         _sync(dev)
@@ -473,6 +473,10 @@ def main(argv=None):
         cnt = eng.buf.counts.tolist()
         extra["overflow_rows_last"], extra["dense_rows_last"] = int(cnt[0]), int(cnt[1])
         extra["multi_rows_last"] = int(cnt[2])   # rows re-checked over their candidate sets
+        if len(cnt) > 5 and getattr(eng, "mrec", None) is not None:
+            # multi rows whose gap record was moved by the shifts (fp16 row)
+            # and, of those, resolved without the fp32 screen
+            extra["gap_rows_last"], extra["gap_resolved_last"] = int(cnt[5]), int(cnt[4])
         xf = getattr(eng.buf, "exact_flag", None)
         if xf is not None and cnt[2] > 0:   # of which the fp32 screen left to the fp64 pass
             extra["multi_fp64_rows_last"] = int((xf[:int(cnt[2])] != 0).sum())
@@ -529,6 +533,10 @@ def main(argv=None):
             # distances, n_init = 1, fit_iters iterations, tol = 0
             _fit_extra(extra, a, sa, comm, dev, "k-means++", ipe=True,
                        name="fit_wall_s_refdefault")
+            # ... at the reference's default n_init = 10 (best of 10 restarts,
+            # _dmeans.py:1285-1306)
+            _fit_extra(extra, a, sa, comm, dev, "k-means++", ipe=True,
+                       name="fit_wall_s_refdefault_ninit10", n_init=10)
     if not a.no_qpca and gpu:
         # qPCA wall-clock (BASELINE metric part 2) on the same 10M x 256 matrix
         _qpca_extra(extra, "qpca_10Mx256_full_fit_s", sa, comm, dev, "full")

@@ -91,6 +91,10 @@ def run_pipeline(comm, dev, n, d=128, r=32, k=256, iters=10, failure_prob=0.01, 
     times.update(iters=int(km.n_iter_), failed_rows=int(km.n_failed_rows_),
                  estimations=int(km.n_estimations_),
                  qmeans_samples_iter_per_s=n * km.n_iter_ / times["qmeans_fit_s"])
+    # the q-means stage's own phases (setup, prelude, init, Lloyd, final
+    # E-step: QMeans.fit_phase_s_), rank 0's clock
+    for ph, v in getattr(km, "fit_phase_s_", {}).items():
+        times["qmeans_" + ph] = float(v)
     return times
 
 

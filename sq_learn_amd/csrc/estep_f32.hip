@@ -396,6 +396,19 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
 // tile; only the HI region of each operand tile is staged (34 KiB per slot at
 // d = 256).
 constexpr int kMaxCand = 16;
+// Gap record of a multi-candidate row whose band the fp32 screen (or the gap
+// screen) certified as {argmin} in iteration rec_it (csrc: recheck_fast_kernel,
+// gap_screen_kernel): the argmin's squared distance da, the gaps
+// g[c] = D(cand c) - da of its c_r <= kGapCand candidates (mcand order; 0 for
+// the argmin's slot), one error bound err covering da and every g[c], and the
+// candidates themselves (16-bit fields, k <= 16384):
+//   ids[0] = j0 | slot << 14 | j1 << 16 | (c_r - 1) << 30,  ids[1] = j2 | j3 << 16
+constexpr int kGapCand = 4;
+struct __align__(16) GapRec {
+  float da, err;
+  float g[kGapCand];
+  unsigned ids[2];
+};
 #ifndef SQ_X64_NW
 #define SQ_X64_NW 4
 #endif
@@ -1001,41 +1014,17 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
     long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
     long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
-    const int* __restrict__ fidx, int nf, int k, const float2* __restrict__ mrec,
-    const int* __restrict__ rec_it, const int* __restrict__ mcand, const double* __restrict__ cum,
-    int ring, int it_now, int it_base, int* __restrict__ n_cert) {
+    const int* __restrict__ fidx, int nf, int k, int rec_on, int it_now, int it_lo, int ring,
+    long long* __restrict__ mrows_b, int* __restrict__ count_b) {
   constexpr int kBoundsChunk = PER * 256;   // PER rows per thread (bit masks)
-  const float2* __restrict__ rec_ = mrec;
-  // A multi-candidate row whose last fp32 screen certified the band {argmin}
-  // (recheck_fast_kernel record: sqrt-domain upper bound ha to the argmin,
-  // lower bound lo to every other candidate, at iteration rit) keeps that
-  // band while (ha + acc_a)^2 + delta < (lo - max_j acc_j)^2, acc_j the
-  // accumulated shift of candidate j since rit (cum: per-iteration prefix
-  // sums of the shifts, a ring of `ring` iterations): label, correction (0)
-  // and the exact band are those the screen would find - the row is not read.
-  uint32_t ncert = 0;
-  auto certify = [&](long long i, int l) -> bool {
-    const int rit = rec_it[i];
-    if (rit < it_base || rit < 0 || rit > it_now || it_now - rit >= ring) return false;
-    const float2 r = rec_[i];
-    const int* mc = mcand + i * (kMaxCand + 1);
-    const int c_r = min(max(mc[0], 0), kMaxCand);
-    const double* cn = cum + (size_t)(it_now % ring) * k;
-    const double* cr = cum + (size_t)(rit % ring) * k;
-    double acc_a = -1.0, acc_o = 0.0;
-    for (int c = 0; c < c_r; ++c) {
-      const int j = mc[1 + c];
-      const double acc = (cn[j] - cr[j]) * (1.0 + 1e-12) + 1e-300;
-      if (j == l) acc_a = acc; else acc_o = fmax(acc_o, acc);
-    }
-    if (acc_a < 0.0) return false;
-    const double ha = (double)r.x + acc_a, lo = (double)r.y - acc_o;
-    const bool ok = lo > 0.0 && ha * ha * (1.0 + 1e-7) + delta * (1.0 + 1e-9) < lo * lo * (1.0 - 1e-7);
-    ncert += ok ? 1u : 0u;
-    return ok;
-  };
-  __shared__ int wsum[4];
-  __shared__ int base_a, base_m;
+  // A multi row whose bounds hold keeps its candidate set; when its gap
+  // record is current (mflag = 2 + the record's base iteration b, it_lo <= b
+  // < it_now; the sweep stores 1 for a multi row without one) the row goes to
+  // list B - entry g | (b % ring) << 56 | (it_now - b) << 60 - where the
+  // record is moved by the centroid shifts since b (the fp16 row, 512 B),
+  // else to the multi list (fp32 screen of the fp32 row)
+  __shared__ int wsum[4], wsum_b[4];
+  __shared__ int base_a, base_m, base_b;
   __shared__ double sf_s[65];               // shifts of the fast centroids, [nf] = max
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < nf) sf_s[tid] = shift[fidx[tid]];
@@ -1048,7 +1037,7 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
   __syncthreads();
   const double sm = *smax;
   const long long c0 = (long long)blockIdx.x * kBoundsChunk;
-  unsigned long long act = 0, rec = 0;   // bit p: row c0 + p * 256 + tid
+  unsigned long long act = 0, rec = 0, recb = 0;   // bit p: row c0 + p * 256 + tid
   // rows in batches of 4: every load of a batch (the row's label / bounds /
   // flag, then the label's shift and Elkan minimum) is issued before any of
   // the batch's math - a thread's PER rows are 3 dependent-load latencies
@@ -1119,30 +1108,44 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
       } else {
         ub[i] = (float)u * (1.0f + 0x1p-22f);
         lb[i] = (float)w * (1.0f - 0x1p-22f);
-        if (mfv[q] && !(rec_ && certify(i, l))) rec |= 1ull << p;
+        if (mfv[q]) {
+          if (rec_on && mfv[q] >= it_lo + 2 && mfv[q] <= it_now + 1) recb |= 1ull << p;
+          else rec |= 1ull << p;
+        }
       }
     }
   }
   // block-wide exclusive scan of both per-thread counts (packed 16 | 16 bits:
   // a chunk holds 2^14 rows), ONE atomic per list and chunk
   const int mine = __popcll(act) | (__popcll(rec) << 16);
-  int incl = mine;
+  const int mine_b = __popcll(recb);
+  int incl = mine, incl_b = mine_b;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
+    const int vb = __shfl_up(incl_b, o, 64);
+    if (lane >= o) {
+      incl += v;
+      incl_b += vb;
+    }
   }
-  if (lane == 63) wsum[wv] = incl;
+  if (lane == 63) {
+    wsum[wv] = incl;
+    wsum_b[wv] = incl_b;
+  }
   __syncthreads();
-  int before = 0, total = 0;
+  int before = 0, total = 0, before_b = 0, total_b = 0;
 #pragma unroll
   for (int w2 = 0; w2 < 4; ++w2) {
     before += w2 < wv ? wsum[w2] : 0;
     total += wsum[w2];
+    before_b += w2 < wv ? wsum_b[w2] : 0;
+    total_b += wsum_b[w2];
   }
   if (tid == 0) {
     base_a = (total & 0xffff) ? atomicAdd(rcount, total & 0xffff) : 0;
     base_m = (total >> 16) ? atomicAdd(multi_count, total >> 16) : 0;
+    base_b = total_b ? atomicAdd(count_b, total_b) : 0;
   }
   __syncthreads();
   const int ex = before + incl - mine;
@@ -1160,33 +1163,50 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
       rec &= ~(1ull << p);
     }
   }
-  if (n_cert) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ncert += (uint32_t)__shfl_xor((int)ncert, o, 64);
-    if (lane == 0 && ncert) atomicAdd(n_cert, (int)ncert);
+  int bpos = base_b + before_b + incl_b - mine_b;
+  for (int p = 0; p < PER && recb; ++p) {
+    if (recb & (1ull << p)) {
+      const long long i = c0 + (long long)p * 256 + tid;
+      const int b = mflag[i] - 2;   // (an L1 hit: loaded above)
+      mrows_b[bpos++] = i | (long long)(b % ring) << 56 | (long long)(it_now - b) << 60;
+      recb &= ~(1ull << p);
+    }
   }
 }
 
-// the multi-row records of the calling thread's next filter / screen launches
-// (null rec: off) - set by the engine before each E-step
+// the gap records of the calling thread's next filter / screen launches (null
+// rec: off) - set by the engine before each certified E-step
 struct MultiRec {
-  float2* rec = nullptr;
-  int* rec_it = nullptr;
-  const double* cum = nullptr;
-  int ring = 0, it_now = 0, it_base = 0;
-  int* n_cert = nullptr;
+  GapRec* rec = nullptr;
+  int* mflag = nullptr;            // the per-row multi flag (2 + record base)
+  int it_now = 0, it_lo = 0;       // records with base in [it_lo, it_now - 1] are current
+  int ring = 0;                    // shift operands per base iteration b (slot b % ring)
+  const _Float16* dsh = nullptr;   // [ring][k][d_pad] fp16 c(now) - c(b)
+  const float* dq = nullptr;       // [ring][k][8] their per-centroid terms
+  long long dsh_stride = 0;        // halves per ring slot
+  long long* mrows_b = nullptr;    // list B (rows with a current record)
+  int* count_b = nullptr;
+  int* n_done = nullptr;           // list-B rows the gap screen resolved
 };
 static thread_local MultiRec g_mrec;
-extern "C" int sq_multi_records(void* rec, void* rec_it, const void* cum, int ring, int it_now,
-                                int it_base, void* n_cert) {
-  g_mrec.rec = (float2*)rec;
-  g_mrec.rec_it = (int*)rec_it;
-  g_mrec.cum = (const double*)cum;
-  g_mrec.ring = ring;
+extern "C" int sq_multi_records(void* rec, void* mflag, int it_now, int it_lo, int ring,
+                                const void* dsh, const void* dq, long long dsh_stride,
+                                void* mrows_b, void* count_b, void* n_done) {
+  g_mrec.rec = (GapRec*)rec;
+  g_mrec.mflag = (int*)mflag;
   g_mrec.it_now = it_now;
-  g_mrec.it_base = it_base;
-  g_mrec.n_cert = (int*)n_cert;
-  return (rec && (!rec_it || !cum || ring < 2)) ? (int)hipErrorInvalidValue : 0;
+  g_mrec.it_lo = it_lo;
+  g_mrec.ring = ring;
+  g_mrec.dsh = (const _Float16*)dsh;
+  g_mrec.dq = (const float*)dq;
+  g_mrec.dsh_stride = dsh_stride;
+  g_mrec.mrows_b = (long long*)mrows_b;
+  g_mrec.count_b = (int*)count_b;
+  g_mrec.n_done = (int*)n_done;
+  return (rec && (it_now < 1 || it_lo < 1 || it_lo > it_now || ring < 2 || ring > 16 || !mflag ||
+                  !dsh || !dq || !mrows_b || !count_b))
+             ? (int)hipErrorInvalidValue
+             : 0;
 }
 
 // rcount and multi_count must be zero on entry (the caller clears them with
@@ -1197,7 +1217,6 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                                 const void* cc, const void* fidx, int nf, int k, void* stream,
                                 const void* mcand) {
   if (n <= 0) return 0;
-  if (g_mrec.rec && !mcand) return (int)hipErrorInvalidValue;
   if (!mflag || !mrows || !multi_count) return (int)hipErrorInvalidValue;
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -1232,9 +1251,9 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                      dim3(256), 0, st, (const int*)labels, (float*)ub, (float*)lb,
                      (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
                      (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
-                     (const float*)cc, (const int*)fidx, nf, k, g_mrec.rec, g_mrec.rec_it,
-                     (const int*)mcand, g_mrec.cum, g_mrec.ring, g_mrec.it_now, g_mrec.it_base,
-                     g_mrec.n_cert);
+                     (const float*)cc, (const int*)fidx, nf, k,
+                     g_mrec.rec ? 1 : 0, g_mrec.it_now, g_mrec.it_lo, g_mrec.ring,
+                     g_mrec.mrows_b, g_mrec.count_b);
   return (int)hipGetLastError();
 }
 
@@ -1461,7 +1480,7 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ mrows,
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
     float* __restrict__ mind, long long cap, double delta, float* __restrict__ ub,
-    unsigned char* __restrict__ xflag, int il, float2* __restrict__ rec, int* __restrict__ rec_it,
+    unsigned char* __restrict__ xflag, int il, GapRec* __restrict__ rec, int* __restrict__ rec_it,
     int it_now) {
   constexpr int RPW = 64 / LPR;   // rows per wave step
   constexpr int FPL = DX / LPR;
@@ -1640,9 +1659,31 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     // iterations certify the same band from the centroid shifts alone
     // (bounds_filter_kernel) without reading the row
     if (rec) {
-      rec[g] = make_float2(sqrtf(hpick) * (1.0f + 0x1p-20f),
-                           sqrtf(fmaxf(lo_o, 0.0f)) * (1.0f - 0x1p-20f));
-      rec_it[g] = done ? it_now : -1;
+      // the row's gap record (lanes 0..7 of the group: one word each; the
+      // upper half of the group repeats them - identical stores): gaps from
+      // the fp32 distances, each within slack_c + slack_pick (+ the rounding
+      // of the difference)
+      const float dpl = __shfl(dme, plane, 64), spl = __shfl(slack, plane, 64);
+      const float gc = mine ? dme - dpl : 0.0f;
+      float ge = mine ? slack + spl + fabsf(gc) * 0x1p-23f : 0.0f;
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) ge = fmaxf(ge, __shfl_xor(ge, o, 64));
+      const int w = sub & 7;
+      const float gw = __shfl(gc, gbase + min(max(w - 2, 0), LPR - 1), 64);
+      const float v = w == 0 ? dpl : (w == 1 ? ge : gw);
+      // candidate ids (slots past c_r repeat candidate 0)
+      const unsigned i0 = (unsigned)__shfl(cur.myj, gbase, 64) & 0x3FFFu;
+      const unsigned i1 = (unsigned)__shfl(cur.myj, gbase + 1, 64) & 0x3FFFu;
+      const unsigned i2 = (unsigned)__shfl(cur.myj, gbase + 2, 64) & 0x3FFFu;
+      const unsigned i3 = (unsigned)__shfl(cur.myj, gbase + 3, 64) & 0x3FFFu;
+      const unsigned cm1 = (unsigned)min(max(c_r, 1), kGapCand) - 1u;
+      const unsigned id0 = i0 | ((unsigned)(plane - gbase) & 3u) << 14 |
+                           (c_r > 1 ? i1 : i0) << 16 | cm1 << 30;
+      const unsigned id1 = (c_r > 2 ? i2 : i0) | (c_r > 3 ? i3 : i0) << 16;
+      float* rw = reinterpret_cast<float*>(rec + g) + w;
+      if (w < 6) *rw = v;
+      else *reinterpret_cast<unsigned*>(rw) = w == 6 ? id0 : id1;
+      if (sub == 0) rec_it[g] = (done && c_r <= kGapCand) ? it_now + 2 : 1;
     }
     __builtin_amdgcn_sched_barrier(0);
     g2 = g3;
@@ -1653,6 +1694,342 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     if (st + 1 >= nsteps) break;
     step(st + 1, rB, xB, c0B, c1B, rA, xA, c0A, c1A);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Gap screen (list B: multi rows whose candidate set is unchanged and whose
+// gap record is from the previous iteration).  Between two iterations the
+// squared distance to centroid j moves by
+//   D_j(t) - D_j(t-1) = -2 x.S_j + q_j,   S_j = c_j(t) - c_j(t-1),
+//   q_j = |c_j(t)|^2 - |c_j(t-1)|^2,
+// so the record's gaps move by 2 (x.S_a - x.S_c) + q_c - q_a and da by
+// -2 x.S_a + q_a.  x.S_j needs the row, but only to the accuracy of a SHIFT:
+// the fp16 row (the filter's operand, 512 B at d = 256) against the fp16
+// shift operand (shift_operand_kernel) is exact to
+//   E_j = ex |S_j| + |x~| (e_j + gam (|S_j| + e_j)),
+// ex = |x - x~| <= 2^-11 |x| + sqrt(d) 2^-25 / alpha, e_j = |S_j - S~_j| (exact,
+// per centroid), gam the fp32 accumulation of the fp16 products.  The record's
+// err grows by 2 (E_a + max_c E_c) + rounding per iteration; a row whose band
+// is still certainly {argmin} (every other candidate's gap > delta + 2 err) is
+// resolved - label, Hamerly upper bound and a new record - without reading its
+// fp32 row or any centroid row.  The rest are appended to the multi list for
+// the fp32 screen (which re-records them exactly).
+// Layout: a wave takes TWO rows per step (32 lanes each).  The vector
+// memory path is the screen's bound, so every load carries distinct data: the
+// per-row values (the 8-word record, |x|^2, the candidates' 8-word
+// per-centroid terms) come as ONE dword per lane (lane w of a row loads word
+// w) and are broadcast with lane shuffles, the list entries of 32 steps come
+// in one load; the records are read from the previous iteration's buffer and
+// written to the other one.  Three-stage pipeline: a step issues the next
+// step's record / |x|^2 words, computes, then issues the next step's fp16 row,
+// shift rows and per-centroid words (its record has landed meanwhile).
+typedef _Float16 gs_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float gs_dot(const uint4 a, const uint4 b, float acc) {
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(gs_h2, a.x), __builtin_bit_cast(gs_h2, b.x), acc,
+                               false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(gs_h2, a.y), __builtin_bit_cast(gs_h2, b.y), acc,
+                               false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(gs_h2, a.z), __builtin_bit_cast(gs_h2, b.z), acc,
+                               false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(gs_h2, a.w), __builtin_bit_cast(gs_h2, b.w), acc,
+                               false);
+  return acc;
+}
+__device__ __forceinline__ float gs_dot(const uint2 a, const uint2 b, float acc) {
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(gs_h2, a.x), __builtin_bit_cast(gs_h2, b.x), acc,
+                               false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(gs_h2, a.y), __builtin_bit_cast(gs_h2, b.y), acc,
+                               false);
+  return acc;
+}
+__device__ __forceinline__ uint4 gs_zero(uint4) { return make_uint4(0u, 0u, 0u, 0u); }
+template <int CTRL>
+__device__ __forceinline__ float gs_dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF,
+                                                         false));
+}
+__device__ __forceinline__ uint2 gs_zero(uint2) { return make_uint2(0u, 0u); }
+
+template <int DX>
+__global__ void __launch_bounds__(256) gap_screen_kernel(
+    const _Float16* __restrict__ Xh, const float* __restrict__ xn,
+    const long long* __restrict__ mrows_b, const int* __restrict__ count_b,
+    const _Float16* __restrict__ dsh, long long dsh_stride, const float* __restrict__ dq,
+    long long dq_stride, float inv_alpha, float delta, int* __restrict__ labels,
+    GapRec* __restrict__ rec, int* __restrict__ mflag, int it_now, int rebase_age,
+    long long* __restrict__ mrows, int* __restrict__ multi_count, long long cap,
+    int* __restrict__ n_done) {
+  constexpr int LPR = 32;
+  using VT = typename std::conditional<DX % 256 == 0, uint4, uint2>::type;
+  constexpr int HV = (int)sizeof(VT) / 2;   // halves per vector
+  constexpr int V = DX / (LPR * HV);        // vectors per lane per row
+  static_assert(DX % 128 == 0 && V >= 1, "gap screen: d_pad multiple of 128");
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const bool hi = lane >= LPR;
+  const long long cnt = min((long long)*count_b, cap);
+  const long long gw = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+  // a wave owns blocks of 64 list entries (lane r: entry r of the block)
+  const long long nblk = (cnt + 63) / 64;
+  const float sub_err = sqrtf((float)DX) * 0x1p-25f * inv_alpha;
+  constexpr float gam = (float)(DX + 16) * 0x1p-24f;
+  uint32_t done_cnt = 0;
+  auto rl = [](int v, int l) -> int { return __builtin_amdgcn_readlane(v, l); };
+  auto rlf = [](float v, int l) -> float {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+  };
+  for (long long blk = gw; blk < nblk; blk += nw) {
+    // ---- the lane's own row: entry, record, |x|^2, its candidates' terms
+    const long long e = blk * 64 + lane;
+    const bool live = e < cnt;
+    const unsigned long long ent = (unsigned long long)mrows_b[live ? e : cnt - 1];
+    const long long g = (long long)(ent & ((1ull << 56) - 1ull));
+    const int rslot = (int)((ent >> 56) & 15ull), age = (int)(ent >> 60);
+    const float4* rp = reinterpret_cast<const float4*>(rec + g);
+    const float4 r0 = rp[0], r1 = rp[1];
+    const float xq = xn[g];
+    const unsigned id0 = __float_as_uint(r1.z), id1 = __float_as_uint(r1.w);
+    const int c_r = (int)(id0 >> 30) + 1, slot = (int)((id0 >> 14) & 3u);
+    int jc[kGapCand];
+    jc[0] = (int)(id0 & 0x3FFFu);
+    jc[1] = (int)((id0 >> 16) & 0x3FFFu);
+    jc[2] = (int)(id1 & 0x3FFFu);
+    jc[3] = (int)((id1 >> 16) & 0x3FFFu);
+    const float* dqs = dq + (size_t)rslot * dq_stride;
+    float4 d0[kGapCand];
+    float inv[kGapCand];
+#pragma unroll
+    for (int c = 0; c < kGapCand; ++c) {
+      d0[c] = reinterpret_cast<const float4*>(dqs)[2 * jc[c]];
+      inv[c] = dqs[8 * jc[c] + 4];
+    }
+    // ---- x.S for every row of the block: 32 passes of two rows (32 lanes
+    // per row), the fp16 row and its candidates' shift rows double-buffered;
+    // each pass's sums land in the owning lanes (v_writelane)
+    float y[kGapCand] = {0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int NB = 4;   // passes in flight
+    VT xv[NB][V], sv[NB][kGapCand][V];
+    int pcm[NB];   // the pass's widest row (candidate loads past it skipped)
+    auto issue = [&](int p, int b) {
+      const int ra = 2 * p, rb = 2 * p + 1;
+      const long long ga = ((long long)rl((int)(g >> 32), ra) << 32) | (unsigned)rl((int)g, ra);
+      const long long gb = ((long long)rl((int)(g >> 32), rb) << 32) | (unsigned)rl((int)g, rb);
+      const long long gm = hi ? gb : ga;
+      const VT* xr = reinterpret_cast<const VT*>(Xh + (size_t)gm * DX);
+#pragma unroll
+      for (int q = 0; q < V; ++q) xv[b][q] = xr[q * LPR + sub];
+      const int sa = rl(rslot, ra), sb = rl(rslot, rb);
+      const _Float16* ds = dsh + (size_t)(hi ? sb : sa) * dsh_stride;
+      pcm[b] = max(rl(c_r, ra), rl(c_r, rb));
+#pragma unroll
+      for (int c = 0; c < kGapCand; ++c) {
+        if (c < 2 || c < pcm[b]) {   // wave-uniform
+          const int j = hi ? rl(jc[c], rb) : rl(jc[c], ra);
+          const VT* sr = reinterpret_cast<const VT*>(ds + (size_t)j * DX);
+#pragma unroll
+          for (int q = 0; q < V; ++q) sv[b][c][q] = sr[q * LPR + sub];
+        } else {
+#pragma unroll
+          for (int q = 0; q < V; ++q) sv[b][c][q] = gs_zero(VT{});
+        }
+      }
+    };
+    auto consume = [&](int p, int b) {
+#pragma unroll
+      for (int c = 0; c < kGapCand; ++c) {
+        if (c < 2 || c < pcm[b]) {
+          float acc = 0.0f;
+#pragma unroll
+          for (int q = 0; q < V; ++q) acc = gs_dot(xv[b][q], sv[b][c][q], acc);
+          acc = gs_dpp_add<0xB1>(acc);    // quad_perm [1,0,3,2]
+          acc = gs_dpp_add<0x4E>(acc);    // quad_perm [2,3,0,1]
+          acc = gs_dpp_add<0x141>(acc);   // row_half_mirror
+          acc = gs_dpp_add<0x140>(acc);   // row_mirror
+          const float a = rlf(acc, 0) + rlf(acc, 16), bb = rlf(acc, 32) + rlf(acc, 48);
+          y[c] = lane == 2 * p ? a : (lane == 2 * p + 1 ? bb : y[c]);
+        }
+      }
+    };
+#pragma unroll
+    for (int b = 0; b < NB - 1; ++b) issue(b, b);
+#pragma unroll 1
+    for (int p = 0; p < 32; p += NB) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        if (p + b + NB - 1 < 32) issue(p + b + NB - 1, (b + NB - 1) % NB);
+        consume(p + b, b);
+      }
+    }
+    // ---- the lane's own row: move the record, decide
+    const float nx = sqrtf(xq) * (1.0f + 0x1p-16f);
+    const float ex = 0x1p-11f * nx + sub_err, nxh = nx + ex;
+    float yr[kGapCand], E[kGapCand], qv[kGapCand];
+#pragma unroll
+    for (int c = 0; c < kGapCand; ++c) {
+      // dq[j] = {q_j, err(q_j), |S_j| (up), e_j (up)}, inv = 1 / (alpha beta_j)
+      yr[c] = y[c] * inv[c];
+      E[c] = ex * d0[c].z + nxh * (d0[c].w + gam * (d0[c].z + d0[c].w)) + d0[c].y;
+      qv[c] = d0[c].x;
+    }
+    float ya = 0.0f, Ea = 0.0f, qa = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kGapCand; ++c)
+      if (c == slot) {
+        ya = yr[c];
+        Ea = E[c];
+        qa = qv[c];
+      }
+    const float gold[kGapCand] = {r0.z, r0.w, r1.x, r1.y};
+    float gn[kGapCand], gmax = 0.0f, Emax = 0.0f, ymax = fabsf(ya), qmax = fabsf(qa);
+#pragma unroll
+    for (int c = 0; c < kGapCand; ++c) {
+      const bool in = c < c_r;
+      gn[c] = in ? (c == slot ? 0.0f : gold[c] + 2.0f * (ya - yr[c]) + (qv[c] - qa))
+                 : __builtin_inff();
+      if (in) {
+        gmax = fmaxf(gmax, fabsf(gold[c]));
+        Emax = fmaxf(Emax, E[c]);
+        ymax = fmaxf(ymax, fabsf(yr[c]));
+        qmax = fmaxf(qmax, fabsf(qv[c]));
+      }
+    }
+    const float da = r0.x - 2.0f * ya + qa;
+    // propagated error: the record's bound, the x.S estimates (+ the q terms'
+    // bounds) of the argmin and the worst other candidate, and <= 3 fp32
+    // roundings of sums bounded by |g| + 4 max|y| + 2 max|q| (or |da| + ...)
+    float err = r0.y + 2.0f * (Ea + Emax) +
+                0x1p-22f * (fmaxf(gmax, fabsf(r0.x)) + 4.0f * ymax + 2.0f * qmax);
+    err *= 1.0f + 0x1p-20f;
+    int m = 0;
+    float gm = gn[0];
+#pragma unroll
+    for (int c = 1; c < kGapCand; ++c)
+      if (gn[c] < gm) {
+        gm = gn[c];
+        m = c;
+      }
+    // certain: every other candidate more than delta + 2 err above the argmin
+    bool done = live && c_r >= 2 && slot < c_r && err < 0.25f * delta + 1.0f;
+    float gmx = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kGapCand; ++c)
+      if (c < c_r && c != m) {
+        done = done && (gn[c] - gm > delta + 2.0f * err);
+        gmx = fmaxf(gmx, gn[c]);
+      }
+    // a resolved row stores nothing while its label (= the record's argmin
+    // slot) stands and its record is young: the record keeps its base and the
+    // next iteration moves it by the shifts since then.  A label change or an
+    // old base rebases the record on this iteration (err_n covers the moved
+    // values; m != slot: both gaps carry err).
+    if (done && (m != slot || age >= rebase_age)) {
+      const float da_n = da + gm;
+      float err_n =
+          (m == slot ? err : 2.0f * err) + 0x1p-22f * (gmx + fabsf(da_n) + fabsf(gm));
+      err_n *= 1.0f + 0x1p-20f;
+      float gr[kGapCand];
+#pragma unroll
+      for (int c = 0; c < kGapCand; ++c) gr[c] = c < c_r ? gn[c] - gm : 0.0f;
+      float4* wp = reinterpret_cast<float4*>(rec + g);
+      wp[0] = make_float4(da_n, err_n, gr[0], gr[1]);
+      wp[1] = make_float4(gr[2], gr[3],
+                          __uint_as_float((id0 & ~(3u << 14)) | (unsigned)m << 14),
+                          __uint_as_float(id1));
+      if (m != slot) labels[g] = jc[0] * (m == 0) + jc[1] * (m == 1) + jc[2] * (m == 2) +
+                                 jc[3] * (m == 3);
+      mflag[g] = it_now + 2;
+    }
+    // the rest -> the multi list (fp32 screen): one atomic per block
+    const bool fwd = live && !done;
+    const unsigned long long fm = __ballot(fwd);
+    if (fm) {   // wave-uniform
+      int fb = 0;
+      if (lane == 0) fb = atomicAdd(multi_count, __popcll(fm));
+      fb = __shfl(fb, 0, 64);
+      const long long se = (long long)fb + __popcll(fm & ((1ull << lane) - 1ull));
+      if (fwd && se < cap) mrows[se] = g;
+    }
+    done_cnt += __popcll(__ballot(done));
+  }
+  if (n_done && lane == 0 && done_cnt) atomicAdd(n_done, (int)done_cnt);
+}
+
+// The gap screen's shift operands after the update c(t) -> c(t+1): for every
+// ring slot s whose base iteration b (s = b % ring) can still be current at
+// the next E-step (bit s of `valid`), per centroid j (one wave) the
+// accumulated shift S_j = c_j(t+1) - c_j(b) in fp64 (exact: fp32 inputs),
+// fp16 S~_j = rn(beta_j S_j) with beta_j a power of two putting max|S_j| near
+// 2^14, and dq[s][j] = {q_j = |c_j(t+1)|^2 - |c_j(b)|^2 (fp32), its error
+// bound, |S_j| (rounded up), e_j = |S_j - S~_j / beta_j| (rounded up),
+// 1 / (alpha beta_j), 0, 0, 0}.  c(b) comes from the snapshot ring; slot
+// `snew` (b = t) takes c(t) itself, which the kernel also snapshots.  Padded
+// columns d..d_pad are zero.
+__global__ void __launch_bounds__(256) shift_operand_kernel(
+    const float* __restrict__ Cprev, const float* __restrict__ Cnew, int ldc, int d, int d_pad,
+    int k, double alpha, float* __restrict__ snap, _Float16* __restrict__ dsh,
+    float* __restrict__ dq, int snew, unsigned valid) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int sl = blockIdx.y;
+  if (j >= k || !((valid >> sl) & 1u)) return;
+  const size_t rs = (size_t)sl * k + j;
+  const float* cn = Cnew + (size_t)j * ldc;
+  float* sn = snap + rs * d_pad;
+  const bool fresh = sl == snew;
+  const float* co = fresh ? Cprev + (size_t)j * ldc : sn;
+  double amax = 0.0;
+  for (int f = lane; f < d; f += 64) amax = fmax(amax, fabs((double)cn[f] - (double)co[f]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmax(amax, __shfl_xor(amax, o, 64));
+  int ex2 = 0;
+  if (amax > 0.0) frexp(amax, &ex2);   // amax in [2^(ex2-1), 2^ex2)
+  const double beta = amax > 0.0 ? ldexp(1.0, 14 - ex2) : 1.0;
+  double q = 0.0, nrm = 0.0, nd = 0.0, e2 = 0.0;
+  for (int f = lane; f < d_pad; f += 64) {
+    const float a32 = f < d ? co[f] : 0.0f;
+    const double a = (double)a32, b = f < d ? (double)cn[f] : 0.0;
+    const double sft = b - a;
+    const _Float16 h = (_Float16)(float)(beta * sft);
+    dsh[rs * d_pad + f] = h;
+    if (fresh) sn[f] = a32;
+    const double r = sft - (double)h / beta;
+    q += sft * (b + a);
+    nrm += b * b + a * a;
+    nd += sft * sft;
+    e2 += r * r;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    q += __shfl_xor(q, o, 64);
+    nrm += __shfl_xor(nrm, o, 64);
+    nd += __shfl_xor(nd, o, 64);
+    e2 += __shfl_xor(e2, o, 64);
+  }
+  if (lane < 8) {
+    const float qf = (float)q;
+    float v = 0.0f;
+    if (lane == 0) v = qf;
+    // fp64 sums (<= 2d roundings of terms <= |c|^2 each) + the fp32 rounding
+    if (lane == 1) v = (float)(fabs(q - (double)qf) + 1e-13 * nrm + 1e-30) * (1.0f + 0x1p-20f);
+    if (lane == 2) v = (float)sqrt(nd) * (1.0f + 0x1p-20f);
+    if (lane == 3) v = (float)(sqrt(e2) * (1.0 + 1e-12)) * (1.0f + 0x1p-20f) + 1e-30f;
+    if (lane == 4) v = (float)(1.0 / (alpha * beta));
+    dq[rs * 8 + lane] = v;
+  }
+}
+
+extern "C" int sq_shift_operand(const void* Cprev, const void* Cnew, int ldc, int d, int d_pad,
+                                int k, double alpha, void* snap, void* dsh, void* dq, int ring,
+                                int snew, unsigned valid, void* stream) {
+  if (k <= 0 || !valid) return 0;
+  if (d > d_pad || d > ldc || ring < 1 || ring > 16 || snew < 0 || snew >= ring)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(shift_operand_kernel, dim3((unsigned)((k + 3) / 4), (unsigned)ring),
+                     dim3(256), 0, (hipStream_t)stream, (const float*)Cprev, (const float*)Cnew,
+                     ldc, d, d_pad, k, alpha, (float*)snap, (_Float16*)dsh, (float*)dq, snew,
+                     valid);
+  return (int)hipGetLastError();
 }
 
 // Rows resolved by the 3-pass kernel (dense list): corr = mind - exact fp64
@@ -1906,6 +2283,29 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
   // with xrows the fp32 screen first, the fp64 pass over what it left
   const long long rblocks = (n / 16 + 63) / 64;
   const unsigned rgrid = (unsigned)(rblocks < 4096 ? (rblocks > 0 ? rblocks : 1) : 4096);
+  if (xflag && g_mrec.rec && ub) {
+    if constexpr (KSD * 16 % 128 == 0) {
+      // list B first: its uncertain rows join the multi list
+      // one resident round of long-lived waves (each takes blocks of 64 rows)
+      static long long gres = 0;
+      if (gres == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, (const void*)gap_screen_kernel<KSD * 16>, 256, 0);
+        gres = (long long)(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 2);
+      }
+      const unsigned bgrid = (unsigned)min(max(rblocks, 1LL), gres);
+      hipLaunchKernelGGL(gap_screen_kernel<KSD * 16>, dim3(bgrid), dim3(256), 0, st,
+                         (const _Float16*)Xh, (const float*)xn, g_mrec.mrows_b, g_mrec.count_b,
+                         g_mrec.dsh, g_mrec.dsh_stride, g_mrec.dq,
+                         g_mrec.dsh_stride / (KSD * 16) * 8, 1.0f / alpha, (float)delta,
+                         (int*)labels, g_mrec.rec, g_mrec.mflag, g_mrec.it_now,
+                         max(1, g_mrec.ring / 2), (long long*)mrows, (int*)multi_count, n,
+                         g_mrec.n_done);
+    }
+  }
   if (xflag) {
     // one resident round of long-lived waves (each walks its slice with the
     // load pipeline warm) instead of several rounds of short ones
@@ -1923,7 +2323,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
     hipLaunchKernelGGL(fk, dim3(fgrid2), dim3(256), 0, st, (const float*)X, (const float*)Cm,
                        (const long long*)mrows, (const int*)mcand, (const int*)multi_count,
                        (int*)labels, (float*)mind, n, delta, (float*)ub, (unsigned char*)xflag,
-                       sil, g_mrec.rec, g_mrec.rec_it, g_mrec.it_now);
+                       sil, g_mrec.rec, g_mrec.mflag, g_mrec.it_now);
   }
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,

@@ -30,7 +30,10 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
                                            long long, double, void*, void*, const void*, void*,
                                            void*, const void*, const void*, int, int, void*, const void*);
-__attribute__((weak)) int sq_multi_records(void*, void*, const void*, int, int, int, void*);
+__attribute__((weak)) int sq_multi_records(void*, void*, int, int, int, const void*, const void*,
+                                           long long, void*, void*, void*);
+__attribute__((weak)) int sq_shift_operand(const void*, const void*, int, int, int, int, double,
+                                           void*, void*, void*, int, int, unsigned, void*);
 __attribute__((weak)) int sq_fast_centroids(void*, const void*, const void*, int, int, int, void*,
                                             void*, void*, void*);
 // tsgemm64.hip
@@ -269,10 +272,25 @@ static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
 
 // the multi-row records of this thread's next certified E-steps (null: off)
 static PyObject* py_multi_records(PyObject*, PyObject* a) {
-  unsigned long long rec, rit, cum, nc; int ring, now, base;
-  if (!PyArg_ParseTuple(a, "KKKiiiK", &rec, &rit, &cum, &ring, &now, &base, &nc)) return nullptr;
+  unsigned long long rec, mf, dsh, dq, mb, cb, nd; int now, lo, ring; long long ds;
+  if (!PyArg_ParseTuple(a, "KKiiiKKLKKK", &rec, &mf, &now, &lo, &ring, &dsh, &dq, &ds, &mb, &cb,
+                        &nd))
+    return nullptr;
   CHECK(sq_multi_records)
-  return ret(sq_multi_records(P(rec), P(rit), P(cum), ring, now, base, P(nc)));
+  return ret(sq_multi_records(P(rec), P(mf), now, lo, ring, P(dsh), P(dq), ds, P(mb), P(cb),
+                              P(nd)));
+}
+
+// the gap screen's fp16 shift operand of one centroid update
+static PyObject* py_shift_operand(PyObject*, PyObject* a) {
+  unsigned long long co, cn, snap, dsh, dq, st; int ldc, d, dp, k, ring, snew; double alpha;
+  unsigned valid;
+  if (!PyArg_ParseTuple(a, "KKiiiidKKKiiIK", &co, &cn, &ldc, &d, &dp, &k, &alpha, &snap, &dsh,
+                        &dq, &ring, &snew, &valid, &st))
+    return nullptr;
+  CHECK(sq_shift_operand)
+  return ret(sq_shift_operand(P(co), P(cn), ldc, d, dp, k, alpha, P(snap), P(dsh), P(dq), ring,
+                              snew, valid, P(st)));
 }
 
 static PyObject* py_fast_centroids(PyObject*, PyObject* a) {
@@ -694,7 +712,8 @@ static PyMethodDef methods[] = {
     {"xtx_geometry", py_xtx_geometry, METH_VARARGS, "xtx tile sizes and pair count"},
     {"xw", py_xw, METH_VARARGS, "fp64 MFMA (A-mu) W"},
     {"bounds_filter", py_bounds_filter, METH_VARARGS, "Hamerly pruning -> active row list"},
-    {"multi_records", py_multi_records, METH_VARARGS, "multi-row band records for the filter"},
+    {"multi_records", py_multi_records, METH_VARARGS, "gap records of the multi rows (gap screen)"},
+    {"shift_operand", py_shift_operand, METH_VARARGS, "fp16 centroid-shift operand (gap screen)"},
     {"fast_centroids", py_fast_centroids, METH_VARARGS, "fastest centroids + Elkan distances"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},

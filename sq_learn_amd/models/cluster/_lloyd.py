@@ -238,21 +238,27 @@ class LloydEngine:
             self.fast_idx = torch.zeros(max(self.n_fast, 1), dtype=torch.int32, device=dev)
             self.fast_cc = torch.zeros(max(self.k * (self.n_fast + 1), 1), dtype=torch.float32,
                                        device=dev)
-        # multi-candidate row records (csrc/estep_f32.hip): the fp32 screen
-        # stores, for a row whose band it certified as {argmin}, its distance
-        # bounds; the filter re-certifies that band from the accumulated
-        # centroid shifts (prefix sums over a ring of iterations) without
-        # reading the row.  Opt-in (SQ_MULTI_RECORDS=1): on the headline only
-        # ~16 % of the multi rows certify from the shift-norm bound, and the
-        # filter's extra loads cost more than the screen saves.
+        # gap records of the multi-candidate rows (csrc/estep_f32.hip): the
+        # fp32 screen records a row's certain {argmin} band as distance gaps
+        # with an error bound, based on that iteration's centres; while the
+        # row's candidate set is unchanged, later iterations move the gaps by
+        # the centroid shifts since the base (fp16 row x fp16 shift operand,
+        # gap_screen_kernel: 512 B per row at d = 256 instead of the fp32 row
+        # and two fp32 centroid rows; nothing stored while the label stands).
+        # A ring of SQ_GAP_RING base iterations (snapshots + operands).
+        # SQ_MULTI_RECORDS=0 disables them.
         self.mrec = None
-        if (self.bounds and self.incremental
-                and os.environ.get("SQ_MULTI_RECORDS", "0") != "0"):
-            self.mrec = torch.zeros((max(self.n, 1), 2), dtype=torch.float32, device=dev)
-            self.mrec_it = torch.full((max(self.n, 1),), -1, dtype=torch.int32, device=dev)
-            self.cum = torch.zeros((16, self.k), dtype=torch.float64, device=dev)
-            self._rit = 0
-            self._rbase = 0
+        if (self.bounds and self.incremental and self.d_pad % 128 == 0 and self.k <= 16384
+                and os.environ.get("SQ_MULTI_RECORDS", "1") != "0"):
+            R = min(max(int(os.environ.get("SQ_GAP_RING", "8")), 2), 16)
+            self.mrec = torch.zeros((max(self.n, 1), 8), dtype=torch.float32, device=dev)
+            self.rows_b = torch.empty(max(self.n, 1), dtype=torch.int64, device=dev)
+            self.gsnap = torch.zeros((R, self.k, self.d_pad), dtype=torch.float32, device=dev)
+            self.dsh = torch.zeros((R, self.k, self.d_pad), dtype=torch.float16, device=dev)
+            self.dq = torch.zeros((R, self.k, 8), dtype=torch.float32, device=dev)
+            # >= 2: the multi flag stores 2 + a record's base, 1 = no record
+            self._rit = 2
+            self._rlo = 2
         self.bounds_valid = False
 
     def _prepare_reduce(self):
@@ -373,12 +379,11 @@ class LloydEngine:
             self._ipe_xn = self.xn.float().contiguous()
 
     def _records_epoch(self):
-        """New centres not reached by tracked shifts: every multi-row record
-        before this point is void."""
+        """New centres not reached by the shift operands: every gap record
+        written so far is void (current records have a base >= _rlo)."""
         if getattr(self, "mrec", None) is not None:
-            self._rit += 1
-            self._rbase = self._rit
-            self.cum[self._rit % self.cum.shape[0]].zero_()
+            self._rit += 2
+            self._rlo = self._rit
 
     def restore_tensors(self, d):
         self._pending = None
@@ -423,8 +428,12 @@ class LloydEngine:
                 screen = (self.incremental and not full
                           and os.environ.get("SQ_SCREEN", "1") != "0")
                 if self.mrec is not None and screen:
-                    K.multi_records(self.mrec, self.mrec_it, self.cum, self._rit, self._rbase,
-                                    self.buf.counts[4:5])
+                    # the record iteration lives in the multi flag (2 + it)
+                    K.ensure_multi_buffers(self.buf, self.n, self.device, True)
+                    R = self.dsh.shape[0]
+                    K.multi_records(self.mrec, self.buf.mflag, self._rit,
+                                    max(self._rlo, self._rit - R + 1), self.dsh, self.dq,
+                                    self.rows_b, self.buf.counts[5:6], self.buf.counts[4:5])
                 # a probe (the filter kept > keep_max of the rows twice and was
                 # skipped since) only MEASURES: the filter pass counts the rows
                 # it would keep (the M-step records the fraction), the sweep
@@ -443,7 +452,9 @@ class LloydEngine:
                                            self.rcount, self.buf, cc=self.fast_cc,
                                            nf=self.n_fast, fidx=self.fast_idx)
                     if probe:
-                        self.buf.counts[:3].zero_()   # the full sweep lists from scratch
+                        # the full sweep lists from scratch (list B too)
+                        self.buf.counts[:3].zero_()
+                        self.buf.counts[5:6].zero_()
                     else:
                         rows = (self.rlist, self.rcount)
                     zero = False
@@ -811,14 +822,19 @@ class LloydEngine:
                     torch.sqrt(self.shift_part[:self.k], out=self.shift_s)
                     self.shift_s.mul_(1.0 + 1e-12)
                     torch.amax(self.shift_s, dim=0, keepdim=True, out=self.smax)
-                if self.mrec is not None:
-                    # prefix sums of the shifts: cum[t + 1] = cum[t] + s_t
-                    R = self.cum.shape[0]
-                    torch.add(self.cum[self._rit % R], self.shift_s,
-                              out=self.cum[(self._rit + 1) % R])
-                    self._rit += 1
-            elif self.bounds:
-                self._records_epoch()   # shifts not tracked this update
+            if self.mrec is not None:
+                # the gap screen's operands of this update: the E-step centres
+                # (base t, snapshotted) and every older base still current at
+                # the next E-step -> the new centres (after a tomography reset
+                # the records are void anyway)
+                R = self.dsh.shape[0]
+                t = self._rit
+                valid = 0
+                for b in range(max(self._rlo, t + 2 - R), t + 1):
+                    valid |= 1 << (b % R)
+                K.shift_operand_native(self.C_new, self.C, self.alpha, self.gsnap, self.dsh,
+                                       self.dq, t % R, valid)
+                self._rit += 1
             if self.bounds:
                 self.bounds_valid = getattr(self, "_bounds_kept", True)
         return self.scalars

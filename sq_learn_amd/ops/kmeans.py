@@ -181,8 +181,8 @@ class EStepBuffers:
         # [overflow rows, dense rows, multi-candidate rows, rows the bounds
         # filter kept] (int32); ovf_count is a view of slot 0
         # [3-pass overflow rows, dense rows, multi rows, kept rows (filter),
-        #  multi rows certified from their records (filter)]
-        self.counts = torch.zeros(5, dtype=torch.int32, device=device)
+        #  list-B rows resolved by the gap screen, list-B rows (filter)]
+        self.counts = torch.zeros(6, dtype=torch.int32, device=device)
         self.exact_flag = None   # the fp32 screen's hand-off flags (per multi entry)
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
@@ -432,18 +432,44 @@ def fast_centroids_native(shift, C, nf, idx, smax_rest, cc, shift_sq=None):
         raise RuntimeError(f"fast_centroids failed (hip error {rc})")
 
 
-def multi_records(rec=None, rec_it=None, cum=None, it_now=0, it_base=0, n_cert=None):
-    """Set (or clear, rec=None) the multi-candidate row records used by this
-    thread's next certified E-steps (csrc/estep_f32.hip: the fp32 screen writes
-    them, the bounds filter certifies unchanged {argmin} bands from them)."""
+def multi_records(rec=None, mflag=None, it_now=0, it_lo=0, dsh=None, dq=None, rows_b=None,
+                  count_b=None, n_done=None):
+    """Set (or clear, rec=None) the gap records used by this thread's next
+    certified E-steps (csrc/estep_f32.hip): the fp32 screen writes a row's
+    record with base ``it_now`` (mflag = 2 + base), the bounds filter lists
+    rows whose base is in [it_lo, it_now - 1] in ``rows_b`` / ``count_b``,
+    the gap screen moves their records by the shift operand of their base
+    (``dsh`` [ring][k][d_pad] fp16 / ``dq`` [ring][k][8], slot base % ring)."""
     if rec is None:
-        nat.native().multi_records(0, 0, 0, 0, 0, 0, 0)
+        nat.native().multi_records(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
         return
-    rc = nat.native().multi_records(rec.data_ptr(), rec_it.data_ptr(), cum.data_ptr(),
-                                    int(cum.shape[0]), int(it_now), int(it_base),
-                                    0 if n_cert is None else n_cert.data_ptr())
+    assert rec.dtype == torch.float32 and rec.shape[-1] == 8 and mflag.dtype == torch.int32
+    assert dsh.dtype == torch.float16 and dq.dtype == torch.float32 and rows_b.dtype == torch.int64
+    assert dsh.dim() == 3 and dq.shape[:2] == dsh.shape[:2] and dq.shape[2] == 8
+    rc = nat.native().multi_records(rec.data_ptr(), mflag.data_ptr(), int(it_now), int(it_lo),
+                                    int(dsh.shape[0]), dsh.data_ptr(), dq.data_ptr(),
+                                    int(dsh.stride(0)), rows_b.data_ptr(), count_b.data_ptr(),
+                                    0 if n_done is None else n_done.data_ptr())
     if rc:
         raise RuntimeError(f"multi_records failed (hip error {rc})")
+
+
+def shift_operand_native(C_prev, C_new, alpha, snap, dsh, dq, snew, valid):
+    """The gap screen's shift operands of the update C_prev -> C_new (fp32
+    [k][d], same layout) for the ring slots in the bitmask ``valid``: slot
+    ``snew`` against C_prev (which it snapshots into ``snap[snew]``), the
+    others against their snapshots (``snap`` [ring][k][d_pad] fp32)."""
+    k, d = C_new.shape[0], C_new.shape[1]
+    ring, _, d_pad = dsh.shape
+    assert C_prev.dtype == torch.float32 and C_new.dtype == torch.float32
+    assert C_prev.stride() == C_new.stride() and C_new.stride(1) == 1
+    assert tuple(snap.shape) == (ring, k, d_pad) and tuple(dq.shape) == (ring, k, 8)
+    rc = nat.native().shift_operand(C_prev.data_ptr(), C_new.data_ptr(), int(C_new.stride(0)), int(d),
+                                    int(d_pad), int(k), float(alpha), snap.data_ptr(), dsh.data_ptr(),
+                                    dq.data_ptr(), int(ring), int(snew), int(valid),
+                                    nat.stream_handle(C_new.device))
+    if rc:
+        raise RuntimeError(f"shift_operand failed (hip error {rc})")
 
 
 def ensure_multi_buffers(buf: EStepBuffers, n, device, bounds=False):

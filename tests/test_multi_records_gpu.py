@@ -1,9 +1,11 @@
-"""Multi-candidate row records (csrc/estep_f32.hip recheck_fast_kernel /
-bounds_filter_kernel): a row whose fp32 screen certified its delta-band as
-{argmin} is re-certified from the accumulated centroid shifts without being
-read.  The records only skip work: labels, centres and the iteration scalars
-are bit-identical with them on and off, including across a centre reset
-(records before it are void) and with failure injection."""
+"""Gap records of the multi-candidate rows (csrc/estep_f32.hip
+recheck_fast_kernel writes them, bounds_filter_kernel lists rows with a
+current record, gap_screen_kernel moves the gaps by the fp16 shift operand
+and resolves rows whose band stays certainly {argmin} from the fp16 row).
+The records only change which kernel certifies a row: labels, centres and the
+iteration scalars are bit-identical with them on and off, across a centre
+reset (records before it are void), with failure injection and pipelined
+E-steps."""
 import numpy as np
 import pytest
 import torch
@@ -13,7 +15,7 @@ from sq_learn_amd.models.cluster._lloyd import LloydEngine
 pytestmark = pytest.mark.gpu
 
 
-def _data(n=60000, d=64, k=64, seed=0, spread=4.0):
+def _data(n=60000, d=128, k=64, seed=0, spread=3.0):
     rs = np.random.RandomState(seed)
     G = rs.uniform(-spread, spread, (k, d))
     X = (G[rs.randint(k, size=n)] + rs.randn(n, d)).astype(np.float32)
@@ -21,7 +23,7 @@ def _data(n=60000, d=64, k=64, seed=0, spread=4.0):
     return X, C0
 
 
-def _run(monkeypatch, X, C0, on, iters=14, reset_at=None, p=0.0, delta=2.0):
+def _run(monkeypatch, X, C0, on, iters=14, reset_at=None, p=0.0, delta=2.0, pipeline=False):
     monkeypatch.setenv("SQ_MULTI_RECORDS", "1" if on else "0")
     monkeypatch.setenv("SQ_ESTEP_BOUNDS", "1")
     monkeypatch.setenv("SQ_MSTEP_INCREMENTAL", "1")
@@ -32,26 +34,32 @@ def _run(monkeypatch, X, C0, on, iters=14, reset_at=None, p=0.0, delta=2.0):
     assert eng.fast and eng.certified and eng.bounds and eng.incremental
     assert (eng.mrec is not None) == on
     eng.set_centers(torch.from_numpy(C0).cuda())
+    eng.pipeline = pipeline
     out, cert = [], 0
     for it in range(iters):
         if reset_at is not None and it == reset_at:
             # a restart-like reset to perturbed centres: old records are void
             eng.set_centers(eng.centers().clone() * 1.01)
         labels, sc = eng.step()
+        vals = sc.tolist()[:2]
         torch.cuda.synchronize()
-        if on:
+        if on and not pipeline:
             cert += int(eng.buf.counts[4].item())
-        out.append((labels.clone().cpu(), eng.centers().clone().cpu(), sc.tolist()[:2]))
+        out.append((labels.clone().cpu(), eng.centers().clone().cpu(), vals))
+    eng.pipeline = False
+    eng.drop_pending()
     return out, cert
 
 
-@pytest.mark.parametrize("case", ["plain", "reset", "failures"])
+@pytest.mark.parametrize("case", ["plain", "reset", "failures", "pipeline"])
 def test_records_on_off_bit_identical(monkeypatch, case):
-    X, C0 = _data(seed={"plain": 0, "reset": 1, "failures": 2}[case])
-    kw = {"reset": {"reset_at": 7}, "failures": {"p": 0.02}}.get(case, {})
+    X, C0 = _data(seed={"plain": 0, "reset": 1, "failures": 2, "pipeline": 3}[case])
+    kw = {"reset": {"reset_at": 7}, "failures": {"p": 0.02},
+          "pipeline": {"pipeline": True}}.get(case, {})
     a, cert = _run(monkeypatch, X, C0, True, **kw)
     b, _ = _run(monkeypatch, X, C0, False, **kw)
-    assert cert > 0, "no row was certified from its record"
+    if case != "pipeline":
+        assert cert > 0, "no row was resolved by the gap screen"
     for (la, Ca, sa), (lb, Cb, sb) in zip(a, b):
         assert torch.equal(la, lb)
         assert torch.equal(Ca, Cb)
