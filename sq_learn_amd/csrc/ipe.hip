@@ -1101,6 +1101,16 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
     const long long nr_ = rl_p ? list_n : n;                                                    \
     const dim3 grid((unsigned)((nr_ + 16 * RR - 1) / (16 * RR)));                               \
     const size_t shm = (size_t)DP * 64 * RR;                                                    \
+    if (shm > 64 * 1024) {   /* d_pad 2048: 128 KiB of A fragments, one workgroup per CU */     \
+      static bool attr_ = false;                                                                \
+      if (!attr_) {                                                                             \
+        hipFuncSetAttribute((const void*)ipe_fused_rg_kernel<DP / 4, RR, true>,                  \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);              \
+        hipFuncSetAttribute((const void*)ipe_fused_rg_kernel<DP / 4, RR, false>,                 \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);              \
+        attr_ = true;                                                                           \
+      }                                                                                         \
+    }                                                                                           \
     if (stats)                                                                                  \
       ipe_fused_rg_kernel<DP / 4, RR, true><<<grid, 256, shm, hs>>>(RARGS, stp, rl_p, rc_p);    \
     else                                                                                        \
@@ -1119,6 +1129,9 @@ extern "C" int sq_ipe_fused(const void* X, long long ldx, const void* Cf, const 
     CASE(256)
     CASE(512)
     CASE(1024)
+    case 2048:   // the row-group layout only (128 KiB of A fragments)
+      RG(2048, 1)
+      break;
     default:
       return (int)hipErrorInvalidValue;
   }

@@ -19,17 +19,26 @@ constexpr double binom_c(int n, int i) {
   return c;
 }
 
-constexpr int kIpeMaxQ = 15;
+// Q (median repetitions) up to 31: Utility.py:534-572's Q for gamma down to
+// ~1e-4; the draw path keeps the kIpeKeep smallest circular distances (the
+// median of Q <= 31 draws is the (Q/2)-th of them)
+constexpr int kIpeMaxQ = 31;
+constexpr int kIpeKeep = 16;
+static_assert(kIpeMaxQ / 2 + 1 <= kIpeKeep, "the median must be among the kept draws");
 constexpr int kIpeWalkM = 128;
 
-// binomial coefficients C(n, i), n < 16 (uniform indices: scalar loads)
-static __constant__ double kBinom[16][16] = {
-#define R(n) {C_(n,0),C_(n,1),C_(n,2),C_(n,3),C_(n,4),C_(n,5),C_(n,6),C_(n,7),C_(n,8),C_(n,9),C_(n,10),C_(n,11),C_(n,12),C_(n,13),C_(n,14),C_(n,15)}
+// binomial coefficients C(n, i), n < 32 (uniform indices: scalar loads)
+static __constant__ double kBinom[32][32] = {
 #define C_(n, i) ((i) > (n) ? 0.0 : binom_c(n, i))
-    R(0), R(1), R(2), R(3), R(4), R(5), R(6), R(7),
-    R(8), R(9), R(10), R(11), R(12), R(13), R(14), R(15)
-#undef C_
+#define R8(n, b) C_(n, b), C_(n, b + 1), C_(n, b + 2), C_(n, b + 3), C_(n, b + 4), C_(n, b + 5), \
+                 C_(n, b + 6), C_(n, b + 7)
+#define R(n) {R8(n, 0), R8(n, 8), R8(n, 16), R8(n, 24)}
+    R(0),  R(1),  R(2),  R(3),  R(4),  R(5),  R(6),  R(7),  R(8),  R(9),  R(10),
+    R(11), R(12), R(13), R(14), R(15), R(16), R(17), R(18), R(19), R(20), R(21),
+    R(22), R(23), R(24), R(25), R(26), R(27), R(28), R(29), R(30), R(31)
 #undef R
+#undef R8
+#undef C_
 };
 
 // P(Binomial(Q, F) >= h) = F^h sum_{m=0}^{Q-h} C(Q, h+m) F^m G^(Q-h-m),
@@ -151,9 +160,9 @@ SQ_DEV double ce_lo(double a, double b) { return fmin(a, b); }
 SQ_DEV double ce_hi(double a, double b) { return fmax(a, b); }
 
 template <typename K>
-SQ_DEV void insert_sorted(K (&c)[kIpeMaxQ], K x) {
+SQ_DEV void insert_sorted(K (&c)[kIpeKeep], K x) {
 #pragma unroll
-  for (int i = 0; i < kIpeMaxQ; ++i) {
+  for (int i = 0; i < kIpeKeep; ++i) {
     const K lo = ce_lo(c[i], x);
     x = ce_hi(c[i], x);
     c[i] = lo;
@@ -164,9 +173,9 @@ template <typename K>
 SQ_DEV double ae_median_draws(double omega, long long M, int Q, WordStream& ws) {
   const double PI = 3.14159265358979323846;
   const FejerLaw law(omega, M);   // per-pair setup shared by the Q draws
-  K c[kIpeMaxQ];
+  K c[kIpeKeep];   // the kIpeKeep smallest so far, ascending
 #pragma unroll
-  for (int i = 0; i < kIpeMaxQ; ++i) c[i] = sizeof(K) == 4 ? (K)0xFFFFFFFFu : (K)1e300;
+  for (int i = 0; i < kIpeKeep; ++i) c[i] = sizeof(K) == 4 ? (K)0xFFFFFFFFu : (K)1e300;
   auto circ = [&](long long j) -> K { return (K)(j < M - j ? j : M - j); };
   if (law.phi == 0.0 || M <= kFejerSmallM) {
 #pragma nounroll
@@ -210,7 +219,7 @@ SQ_DEV double ae_median_draws(double omega, long long M, int Q, WordStream& ws) 
   }
   double m1 = 0.0, m0 = 0.0;
 #pragma unroll
-  for (int i = 0; i < kIpeMaxQ; ++i) {
+  for (int i = 0; i < kIpeKeep; ++i) {
     if (i == Q / 2) m1 = (double)c[i];
     if (i == Q / 2 - 1) m0 = (double)c[i];
   }

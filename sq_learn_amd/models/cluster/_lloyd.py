@@ -551,9 +551,9 @@ class LloydEngine:
 
     def _ipe16_ok(self):
         """The certified fp16 IPE screen (csrc/ipe16.hip) covers d <= 256,
-        k <= 16384, odd Q <= 15, fp32 rows; SQ_IPE16=0 disables it."""
+        k <= 16384, odd Q <= 31, fp32 rows; SQ_IPE16=0 disables it."""
         return (self.device.type == "cuda" and self.Xf.dtype == torch.float32
-                and self.Xf.stride(1) == 1 and self.ipe_Q % 2 == 1 and self.ipe_Q <= 15
+                and self.Xf.stride(1) == 1 and self.ipe_Q % 2 == 1 and self.ipe_Q <= 31
                 and K.pad_features(self.d) in K.IPE16_D and self.k <= K.IPE16_MAX_K
                 and os.environ.get("SQ_IPE16", "1") != "0")
 
@@ -610,8 +610,8 @@ class LloydEngine:
         ipe_key = self._key("ipe")
         if self._ipe16_ok():
             return self._estep_ipe16(ipe_key)
-        if self.device.type == "cuda" and self.d <= 1024 and self.Xf.dtype == torch.float32 \
-                and self.Xf.stride(1) == 1 and self.ipe_Q <= 15:
+        if self.device.type == "cuda" and self.d <= 2048 and self.Xf.dtype == torch.float32 \
+                and self.Xf.stride(1) == 1 and self.ipe_Q <= 31:
             # fused kernel: fp32 MFMA inner products + per-pair median-of-Q AE.
             # The previous E-step's labels are the hint pairs (their estimates
             # seed the pruned screen; any hint gives the same law): two label

@@ -102,19 +102,21 @@ def _row_and_centroids(seed, d, k, spread, scale=1.5):
     return x, C.astype(np.float32)
 
 
-def test_ipe16_matches_full_sampler_law_many_centroids(cuda):
-    """k = 40 centroids around the row (eps = 0.1, Q = 13: every pair near the
-    hint, all listed and sampled in full): the (label, D~) law equals the
-    full sampler's."""
+@pytest.mark.parametrize("Q", [13, 17])
+def test_ipe16_matches_full_sampler_law_many_centroids(cuda, Q):
+    """k = 40 centroids around the row (eps = 0.1, Q = 13 / 17: every pair
+    near the hint, all listed and sampled in full): the (label, D~) law
+    equals the full sampler's."""
     x, C = _row_and_centroids(12, 40, 40, 1.0)
     n = 400_000
     X = torch.tensor(np.tile(x, (n, 1)), device=cuda)
     Ct = torch.tensor(C, device=cuda)
     st = torch.zeros(8, dtype=torch.int64, device=cuda)
-    la, ma, eng = _run16(X, Ct, 0.1, 13, 1, stats_t=st)
-    lb, mb = _run_full(X, Ct, 0.1, 13, 2)
+    la, ma, eng = _run16(X, Ct, 0.1, Q, 1, stats_t=st)
+    lb, mb = _run_full(X, Ct, 0.1, Q, 2)
     assert eng.last_dense == 0, st.tolist()
-    assert _same_law(la, ma, lb, mb) > 1e-4
+    # (Q = 17 concentrates the median: fewer populated cells)
+    assert _same_law(la, ma, lb, mb, min_cells=3 if Q == 13 else 2) > 1e-4
 
 
 def _fire_case(d=96, K_=301, s=12.0):

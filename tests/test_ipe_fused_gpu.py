@@ -50,7 +50,7 @@ def _run_kernel(x, c, n, eps, Q, cuda, seed=0):
     dp = 32
     while dp < d:
         dp *= 2
-    assert dp <= 1024
+    assert dp <= 2048
     xn = (X.double() ** 2).sum(1).float()
     cn = (C.double() ** 2).sum(1).float()
     lab = torch.empty(n, dtype=torch.int32, device=cuda)
@@ -468,3 +468,52 @@ def test_ipe_layouts_bit_identical(cuda, dp, with_hint, prune):
         assert np.array_equal(outs[0][2][:4], o[2][:4])
     if prune:
         assert outs[0][2][0] > 0
+
+
+# ------------------------------------------------ every shape the reference takes
+@pytest.mark.parametrize("case", ["walk", "draws"])
+def test_ipe_fused_law_exact_q17(cuda, case):
+    """Q = 17 (median_evaluation at gamma = 0.05, Utility.py:564-568): the
+    exact median-of-Q law on the order-statistic walk (M <= 128) and on the
+    draw path (large M: the 16 smallest of the 17 draws kept)."""
+    from sq_learn_amd.quantum.fejer import median_repetitions
+    Q = median_repetitions(0.05)
+    assert Q == 17
+    rng = np.random.default_rng(17)
+    d = 200
+    x = rng.standard_normal(d)
+    c = x + 0.8 * rng.standard_normal(d) if case == "walk" else rng.standard_normal(d)
+    s, nx2, ny2, ip = _run_kernel(x, c, 60000, 0.25, Q, cuda, seed=4)
+    M, vals, pm = _exact_law(ip, nx2, ny2, 0.25, Q)
+    assert (M <= 128) == (case == "walk")
+    assert _gof(s, vals, pm) > 1e-4
+
+
+@pytest.mark.parametrize("Q", [13, 25])
+def test_ipe_fused_law_exact_d1100(cuda, Q):
+    """d = 1100 (d_pad 2048: 128 KiB of A fragments per workgroup): the same
+    exact median law through the fused kernel."""
+    rng = np.random.default_rng(1100)
+    d = 1100
+    x = rng.standard_normal(d)
+    c = x + 0.8 * rng.standard_normal(d)
+    s, nx2, ny2, ip = _run_kernel(x, c, 40000, 0.25, Q, cuda, seed=5)
+    M, vals, pm = _exact_law(ip, nx2, ny2, 0.25, Q)
+    assert M <= 128
+    assert _gof(s, vals, pm) > 1e-4
+
+
+def test_ipe_wide_q17_fit_runs_fused(cuda, monkeypatch):
+    """A QMeans IPE fit at d = 1100, Q = 17 runs the fused kernel - the
+    library-GEMM + sampler fallback is never called - and recovers the blobs."""
+    from sq_learn_amd.models.cluster import QMeans
+    from sq_learn_amd.utils.datasets import make_blobs
+    from sklearn.metrics import adjusted_rand_score
+
+    def boom(*a, **k):
+        raise AssertionError("GEMM + sampler fallback used")
+    monkeypatch.setattr(K, "ipe_estep_native", boom)
+    X, y = make_blobs(3000, 1100, centers=5, cluster_std=1.0, random_state=1)
+    g = QMeans(n_clusters=5, delta=0.5, true_distance_estimate=True, random_state=0, n_init=1,
+               max_iter=8, init="k-means++", ipe_Q=17, device=cuda).fit(X)
+    assert adjusted_rand_score(y, g.labels_) > 0.95
