@@ -1014,15 +1014,14 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     const double* __restrict__ shift, const double* __restrict__ smax, long long n, double delta,
     long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
     long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
-    const int* __restrict__ fidx, int nf, int k, int rec_on, int it_now, int it_lo, int ring,
+    const int* __restrict__ fidx, int nf, int k, int rec_on, int it_now, int it_lo,
     long long* __restrict__ mrows_b, int* __restrict__ count_b) {
   constexpr int kBoundsChunk = PER * 256;   // PER rows per thread (bit masks)
   // A multi row whose bounds hold keeps its candidate set; when its gap
   // record is current (mflag = 2 + the record's base iteration b, it_lo <= b
   // < it_now; the sweep stores 1 for a multi row without one) the row goes to
-  // list B - entry g | (b % ring) << 56 | (it_now - b) << 60 - where the
-  // record is moved by the centroid shifts since b (the fp16 row, 512 B),
-  // else to the multi list (fp32 screen of the fp32 row)
+  // list B, where the record is moved by the centroid shifts since b (the
+  // fp16 row, 512 B), else to the multi list (fp32 screen of the fp32 row)
   __shared__ int wsum[4], wsum_b[4];
   __shared__ int base_a, base_m, base_b;
   __shared__ double sf_s[65];               // shifts of the fast centroids, [nf] = max
@@ -1166,9 +1165,7 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
   int bpos = base_b + before_b + incl_b - mine_b;
   for (int p = 0; p < PER && recb; ++p) {
     if (recb & (1ull << p)) {
-      const long long i = c0 + (long long)p * 256 + tid;
-      const int b = mflag[i] - 2;   // (an L1 hit: loaded above)
-      mrows_b[bpos++] = i | (long long)(b % ring) << 56 | (long long)(it_now - b) << 60;
+      mrows_b[bpos++] = c0 + (long long)p * 256 + tid;
       recb &= ~(1ull << p);
     }
   }
@@ -1252,8 +1249,8 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                      (const double*)shift, (const double*)smax, n, delta, (long long*)rlist,
                      (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
                      (const float*)cc, (const int*)fidx, nf, k,
-                     g_mrec.rec ? 1 : 0, g_mrec.it_now, g_mrec.it_lo, g_mrec.ring,
-                     g_mrec.mrows_b, g_mrec.count_b);
+                     g_mrec.rec ? 1 : 0, g_mrec.it_now, g_mrec.it_lo, g_mrec.mrows_b,
+                     g_mrec.count_b);
   return (int)hipGetLastError();
 }
 
@@ -1756,7 +1753,7 @@ __global__ void __launch_bounds__(256) gap_screen_kernel(
     const long long* __restrict__ mrows_b, const int* __restrict__ count_b,
     const _Float16* __restrict__ dsh, long long dsh_stride, const float* __restrict__ dq,
     long long dq_stride, float inv_alpha, float delta, int* __restrict__ labels,
-    GapRec* __restrict__ rec, int* __restrict__ mflag, int it_now, int rebase_age,
+    GapRec* __restrict__ rec, int* __restrict__ mflag, int it_now, int ring, int rebase_age,
     long long* __restrict__ mrows, int* __restrict__ multi_count, long long cap,
     int* __restrict__ n_done) {
   constexpr int LPR = 32;
@@ -1783,9 +1780,9 @@ __global__ void __launch_bounds__(256) gap_screen_kernel(
     // ---- the lane's own row: entry, record, |x|^2, its candidates' terms
     const long long e = blk * 64 + lane;
     const bool live = e < cnt;
-    const unsigned long long ent = (unsigned long long)mrows_b[live ? e : cnt - 1];
-    const long long g = (long long)(ent & ((1ull << 56) - 1ull));
-    const int rslot = (int)((ent >> 56) & 15ull), age = (int)(ent >> 60);
+    const long long g = mrows_b[live ? e : cnt - 1];
+    const int base_it = mflag[g] - 2;   // the record's base iteration (filter: current)
+    const int rslot = base_it % ring, age = it_now - base_it;
     const float4* rp = reinterpret_cast<const float4*>(rec + g);
     const float4 r0 = rp[0], r1 = rp[1];
     const float xq = xn[g];
@@ -2301,7 +2298,7 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                          (const _Float16*)Xh, (const float*)xn, g_mrec.mrows_b, g_mrec.count_b,
                          g_mrec.dsh, g_mrec.dsh_stride, g_mrec.dq,
                          g_mrec.dsh_stride / (KSD * 16) * 8, 1.0f / alpha, (float)delta,
-                         (int*)labels, g_mrec.rec, g_mrec.mflag, g_mrec.it_now,
+                         (int*)labels, g_mrec.rec, g_mrec.mflag, g_mrec.it_now, g_mrec.ring,
                          max(1, g_mrec.ring / 2), (long long*)mrows, (int*)multi_count, n,
                          g_mrec.n_done);
     }
