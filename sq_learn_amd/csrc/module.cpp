@@ -23,7 +23,7 @@ __attribute__((weak)) int sq_pe_batch(const void*, const void*, void*, long long
 // tomography.hip
 __attribute__((weak)) int sq_tomography(const void*, int, int, const void*, int, int, const void*,
                                         void*, void*, int, unsigned, unsigned, unsigned, unsigned,
-                                        long long, void*);
+                                        long long, void*, double);
 __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, long long,
                                            long long, const void*, void*, long long, unsigned,
                                            unsigned, unsigned, unsigned, const void*, int, void*);
@@ -240,12 +240,13 @@ static PyObject* py_band_select(PyObject*, PyObject* a) {
 static PyObject* py_tomography(PyObject*, PyObject* a) {
   unsigned long long V, sched, first, err, out, st; int r, d, T, mode, ninf; long long roff;
   unsigned k0, k1, s0, s1;
-  if (!PyArg_ParseTuple(a, "KiiKiiKKKiIIIILK", &V, &r, &d, &sched, &T, &mode, &first, &err, &out,
-                        &ninf, &k0, &k1, &s0, &s1, &roff, &st))
+  double stop_err = 0.0;
+  if (!PyArg_ParseTuple(a, "KiiKiiKKKiIIIILK|d", &V, &r, &d, &sched, &T, &mode, &first, &err, &out,
+                        &ninf, &k0, &k1, &s0, &s1, &roff, &st, &stop_err))
     return nullptr;
   CHECK(sq_tomography)
   return ret(sq_tomography(P(V), r, d, P(sched), T, mode, P(first), P(err), P(out), ninf, k0, k1,
-                           s0, s1, roff, P(st)));
+                           s0, s1, roff, P(st), stop_err));
 }
 
 static PyObject* py_mnom_segments(PyObject*, PyObject* a) {

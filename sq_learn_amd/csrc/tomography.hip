@@ -120,18 +120,26 @@ SQ_DEV void multinomial_tree(const double* pre, int M, double N, double* cnt, do
   // leaves now in cnt[0..M)
 }
 
-// 4 waves per workgroup, one (row, checkpoint) pair per wave.
+// 4 waves per workgroup.  mode 0: one (row, checkpoint) pair per wave (the
+// checkpoint's error); mode 1: one row per wave at checkpoint first[row];
+// mode 2 (stop at the first passing checkpoint): one row per wave walks its
+// checkpoints in order and keeps the estimate of the first whose error is
+// <= stop_err (else the last) - the same Philox words per (row, checkpoint)
+// as modes 0 + 1, so the same result, with only the checkpoints up to the
+// first passing one evaluated.
 __global__ void __launch_bounds__(256) tomography_kernel(
     const double* __restrict__ V, int r, int d, const long long* __restrict__ sched, int T,
     int mode, const int* __restrict__ first, double* __restrict__ err, double* __restrict__ out,
-    int norm_inf, RngKey key, long long row_offset) {
+    int norm_inf, RngKey key, long long row_offset, double stop_err) {
   extern __shared__ __attribute__((aligned(16))) double tsm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long pair = (long long)blockIdx.x * 4 + w;
   const long long npairs = mode == 0 ? (long long)r * T : (long long)r;
   if (pair >= npairs) return;
   const int row = (int)(mode == 0 ? pair / T : pair);
-  const int t = mode == 0 ? (int)(pair % T) : first[row];
+  const int t_first = mode == 0 ? (int)(pair % T) : (mode == 1 ? first[row] : 0);
+  const int t_last = mode == 2 ? T - 1 : t_first;
+  for (int t = t_first; t <= t_last; ++t) {
   int M = 1;
   while (M < d + 1) M <<= 1;
   double* pre = tsm + (size_t)w * (4 * kTomoMaxM + 2);     // M + 1
@@ -192,17 +200,22 @@ __global__ void __launch_bounds__(256) tomography_kernel(
   for (int i = lane; i < d; i += 64) {
     const double P = est[i];
     const double s = cnt[i] > 0.4 * P * P * N ? P : -P;
-    if (mode == 1) out[(size_t)row * d + i] = s;
+    if (mode != 0) out[(size_t)row * d + i] = s;
     const double df = v[i] - s;
     e = norm_inf ? fmax(e, fabs(df)) : e + df * df;
   }
-  if (mode == 0) {
+  if (mode != 1) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const double x = __shfl_xor(e, o, 64);
       e = norm_inf ? fmax(e, x) : e + x;
     }
-    if (lane == 0) err[(size_t)row * T + t] = norm_inf ? e : sqrt(e);
+    const double ev = norm_inf ? e : sqrt(e);
+    if (mode == 0 && lane == 0) err[(size_t)row * T + t] = ev;
+    if (mode == 2 && ev <= stop_err) break;   // wave-uniform (the reduced error)
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
 }
 
@@ -276,7 +289,7 @@ using namespace sq;
 extern "C" int sq_tomography(const void* V, int r, int d, const void* sched, int T, int mode,
                              const void* first, void* err, void* out, int norm_inf, unsigned k0,
                              unsigned k1, unsigned s0, unsigned s1, long long row_offset,
-                             void* stream) {
+                             void* stream, double stop_err) {
   if (r <= 0) return 0;
   if (d < 1 || d + 1 > kTomoMaxM || T < 1) return (int)hipErrorInvalidValue;
   RngKey key{k0, k1, s0, s1};
@@ -291,7 +304,7 @@ extern "C" int sq_tomography(const void* V, int r, int d, const void* sched, int
   hipLaunchKernelGGL(tomography_kernel, dim3((unsigned)((npairs + 3) / 4)), dim3(256), lds,
                      (hipStream_t)stream, (const double*)V, r, d, (const long long*)sched, T,
                      mode, (const int*)first, (double*)err, (double*)out, norm_inf, key,
-                     row_offset);
+                     row_offset, stop_err);
   return (int)hipGetLastError();
 }
 

@@ -304,9 +304,11 @@ def tomography_long(A, delta, key: RngKey, norm="L2", N=None, stop_when_reached_
 
 
 def _tomography_rows_native(V, sched, delta, key: RngKey, norm, stop):
-    """HIP path (csrc/tomography.hip): errors of every checkpoint in one
-    launch, first passing checkpoint per row on the device, then the chosen
-    estimates regenerated (same Philox words) in a second launch."""
+    """HIP path (csrc/tomography.hip): with the stop rule, one wave per row
+    walks its checkpoints in order and keeps the first passing estimate
+    (mode 2: only the checkpoints up to it are drawn); SQ_TOMO_ALLPAIRS=1:
+    every checkpoint's error in one launch, then the chosen estimates
+    regenerated (same Philox words, same result) in a second."""
     from ..ops import _native as nat
     r, d = V.shape
     T = len(sched)
@@ -317,6 +319,11 @@ def _tomography_rows_native(V, sched, delta, key: RngKey, norm, stop):
     st = nat.stream_handle(dev)
     ninf = 0 if norm == "L2" else 1
     m = nat.native()
+    import os
+    if stop and T > 1 and os.environ.get("SQ_TOMO_ALLPAIRS", "0") != "1":
+        m.tomography(V.data_ptr(), r, d, sch.data_ptr(), T, 2, 0, 0, out.data_ptr(), ninf,
+                     key.k0, key.k1, key.s0, key.s1, 0, st, float(delta))
+        return out
     if stop and T > 1:
         m.tomography(V.data_ptr(), r, d, sch.data_ptr(), T, 0, 0, err.data_ptr(), 0, ninf,
                      key.k0, key.k1, key.s0, key.s1, 0, st)

@@ -150,6 +150,22 @@ def test_tomography_kernel_matches_law(cuda):
     assert not torch.equal(e_gpu[0], e_gpu[1])
 
 
+@pytest.mark.parametrize("delta", [0.8, 0.1])
+def test_tomography_first_pass_walk_matches_all_checkpoints(cuda, monkeypatch, delta):
+    """The stop rule's one-launch walk (a wave per row, checkpoints in order
+    up to the first passing one) returns the all-checkpoints path's
+    estimates bit for bit (same Philox words per row and checkpoint)."""
+    from sq_learn_amd.quantum import device as QD
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(2000, 61, generator=g, dtype=torch.float64)
+    A /= A.norm(dim=1, keepdim=True)
+    key = RngKey(9, "tomography", 2)
+    walk = QD.tomography_rows_torch(A.to(cuda), delta, key).cpu()
+    monkeypatch.setenv("SQ_TOMO_ALLPAIRS", "1")
+    full = QD.tomography_rows_torch(A.to(cuda), delta, key).cpu()
+    assert torch.equal(walk, full)
+
+
 def test_gpu_fits_are_bit_reproducible(cuda):
     """No float atomics feed any fitted quantity: two fits are identical."""
     from sq_learn_amd.cluster import QMeans
