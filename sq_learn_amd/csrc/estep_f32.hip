@@ -1461,11 +1461,13 @@ __global__ void __launch_bounds__(256) recheck_rows_kernel(
 // each candidate's band membership is CERTAIN when
 //   in : D32_c + B_c <= min_j (D32_j - B_j) + delta,
 //   out: D32_c - B_c >  min_j (D32_j + B_j) + delta.
-// A row whose band is certainly {argmin} is done here (label = argmin,
-// corr = 0 - the memset value, ub from D32 + B; mind is not needed by the
-// incremental steps that run the screen); every other row (a wider band: its
-// kappa pick and correction need the exact values, or an uncertain member)
-// is flagged for recheck_rows_kernel (fp64).
+// A row whose every candidate is certainly in or out of the band is done
+// here: band {argmin} -> label = argmin, corr = 0 (the memset value); a wider
+// band -> the member of kappa rank band_rank(u, |band|) (the fp64 pass's rule
+// and Philox word: the same label) with corr = min - label distance from the
+// fp32 distances; ub from D32 + B (mind is not needed by the incremental
+// steps that run the screen).  Rows with an uncertain member are flagged for
+// recheck_rows_kernel (fp64).
 // The kernel is bound by memory transactions per row (the list entry, the
 // per-row candidate record, the row, the scattered label / bound stores),
 // not by arithmetic: loads are software-pipelined across steps.
@@ -1478,7 +1480,7 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const int* __restrict__ mcand, const int* __restrict__ multi_count, int* __restrict__ labels,
     float* __restrict__ mind, long long cap, double delta, float* __restrict__ ub,
     unsigned char* __restrict__ xflag, int il, GapRec* __restrict__ rec, int* __restrict__ rec_it,
-    int it_now) {
+    int it_now, RngKey key, long long row_offset, float* __restrict__ corr) {
   constexpr int RPW = 64 / LPR;   // rows per wave step
   constexpr int FPL = DX / LPR;
   constexpr int F4 = FPL >= 4 ? FPL / 4 : 1;
@@ -1626,10 +1628,31 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     const unsigned long long gmask = ((1ull << LPR) - 1ull) << gbase;
     const unsigned long long inm = __ballot(cin) & gmask;
     const bool unsure = !fits || (__ballot(mine && !cin && !cout) & gmask) != 0;
-    const bool done = live && !unsure && __popcll(inm) == 1;
-    const int plane = inm ? __ffsll((long long)inm) - 1 : gbase;
+    // every candidate certainly in or out: the band is known, and so is the
+    // label - the member of kappa rank band_rank(u, |band|) (recheck_rows'
+    // rule, the same Philox word); a wider band also needs its correction
+    // min - label distance (fp32 distances here, fp64 in recheck_rows)
+    const int bsz = __popcll(inm);
+    const bool done_any = live && !unsure && bsz >= 1;
+    const bool done = done_any && bsz == 1;   // band {argmin}
+    int plane = inm ? __ffsll((long long)inm) - 1 : gbase;
+    const bool wide = done_any && bsz >= 2;
+    float dmin_w = 0.0f;
+    if (__ballot(wide)) {   // wave-uniform
+      const int kme = cin ? (((cur.myj & 31) << 20) | (cur.myj >> 5)) : 0x7fffffff;
+      int rank = 0;
+#pragma unroll
+      for (int t = 0; t < LPR; ++t) rank += __shfl(kme, gbase + t, 64) < kme ? 1 : 0;
+      const int r = band_rank(band_u(key, row_offset + g), bsz > 0 ? bsz : 1);
+      const unsigned long long pm = __ballot(cin && rank == r) & gmask;
+      if (wide && pm) plane = __ffsll((long long)pm) - 1;
+      dmin_w = mine ? dme : __builtin_inff();
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) dmin_w = fminf(dmin_w, __shfl_xor(dmin_w, o, 64));
+    }
     const int pick = __shfl(cur.myj, plane, 64);
     const float hpick = __shfl(hi, plane, 64);
+    const float dpick = __shfl(dme, plane, 64);
     // the smallest lower bound of the OTHER candidates (the row's record)
     float lo_o = (mine && lane != plane) ? lo : __builtin_inff();
 #pragma unroll
@@ -1649,8 +1672,9 @@ __global__ void __launch_bounds__(256) recheck_fast_kernel(
     // 4-B store is one more memory transaction per row - the kernel's bound)
     labels[g] = pick;
     if constexpr (UB) ub[g] = sqrtf(hpick) * (1.0f + 0x1p-20f);
+    if (wide && sub == 0 && corr) corr[g] = dmin_w - dpick;
     // the rest -> flagged for the fp64 pass (a per-entry byte: no atomics)
-    xflag[e] = done ? 0 : 1;
+    xflag[e] = done_any ? 0 : 1;
     // a row whose band is certainly {argmin}: its record (distance bounds to
     // the argmin and to the nearest other candidate, sqrt domain) lets later
     // iterations certify the same band from the centroid shifts alone
@@ -2320,7 +2344,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
     hipLaunchKernelGGL(fk, dim3(fgrid2), dim3(256), 0, st, (const float*)X, (const float*)Cm,
                        (const long long*)mrows, (const int*)mcand, (const int*)multi_count,
                        (int*)labels, (float*)mind, n, delta, (float*)ub, (unsigned char*)xflag,
-                       sil, g_mrec.rec, g_mrec.mflag, g_mrec.it_now);
+                       sil, g_mrec.rec, g_mrec.mflag, g_mrec.it_now, key, row_offset,
+                       (float*)corr);
   }
   hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
                      (const float*)X, (const float*)Cm, (const long long*)mrows,
