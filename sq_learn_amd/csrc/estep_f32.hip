@@ -1015,7 +1015,7 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
     long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
     const int* __restrict__ fidx, int nf, int k, int rec_on, int it_now, int it_lo,
-    long long* __restrict__ mrows_b, int* __restrict__ count_b) {
+    long long* __restrict__ mrows_b, int* __restrict__ count_b, float* __restrict__ corr) {
   constexpr int kBoundsChunk = PER * 256;   // PER rows per thread (bit masks)
   // A multi row whose bounds hold keeps its candidate set; when its gap
   // record is current (mflag = 2 + the record's base iteration b, it_lo <= b
@@ -1052,6 +1052,9 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
       inb[q] = i < n;
       const long long ii = inb[q] ? i : 0;
       lv[q] = inb[q] ? labels[ii] : -1;
+      // the E-step's per-row corrections start at 0 (this pass visits every
+      // row: the separate memset of the list-mode E-step is not needed)
+      if (corr && inb[q]) corr[ii] = 0.0f;
       ubv[q] = ub[ii];
       lbv[q] = lb[ii];
       mfv[q] = mflag[ii];
@@ -1212,7 +1215,7 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                                 const void* smax, long long n, double delta, void* rlist,
                                 void* rcount, const void* mflag, void* mrows, void* multi_count,
                                 const void* cc, const void* fidx, int nf, int k, void* stream,
-                                const void* mcand) {
+                                void* corr) {
   if (n <= 0) return 0;
   if (!mflag || !mrows || !multi_count) return (int)hipErrorInvalidValue;
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
@@ -1250,7 +1253,7 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                      (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
                      (const float*)cc, (const int*)fidx, nf, k,
                      g_mrec.rec ? 1 : 0, g_mrec.it_now, g_mrec.it_lo, g_mrec.mrows_b,
-                     g_mrec.count_b);
+                     g_mrec.count_b, (float*)corr);
   return (int)hipGetLastError();
 }
 
@@ -2060,20 +2063,32 @@ __global__ void __launch_bounds__(256) dense_corr_kernel(
     const float* __restrict__ X, const float* __restrict__ Cm, const long long* __restrict__ rows,
     const int* __restrict__ count, const int* __restrict__ labels, const float* __restrict__ mind,
     float* __restrict__ corr, long long cap, int d) {
-  const int lane = threadIdx.x & 63;
+  // 16 lanes per row, 4 rows per wave in flight (the row -> label -> row
+  // data chain is three dependent loads: one row per wave left the grid
+  // latency-bound on a 200K-row dense list)
+  const int lane = threadIdx.x & 63, sub = lane & 15, grp = lane >> 4;
   const long long cnt = min((long long)*count, cap);
-  for (long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); e < cnt;
-       e += (long long)gridDim.x * 4) {
-    const long long r = rows[e];
+  const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long long nwv = (long long)gridDim.x * 4;
+  for (long long e0 = wv * 4; e0 < cnt; e0 += nwv * 4) {
+    const long long e = e0 + grp;
+    const bool live = e < cnt;
+    const long long r = rows[live ? e : e0];
     const int l = labels[r];
-    if (l < 0) continue;
+    const bool ok = live && l >= 0;
+    const float* xr = X + (size_t)r * d;
+    const float* cr = Cm + (size_t)(l >= 0 ? l : 0) * d;
     double s = 0.0;
-    for (int f = lane; f < d; f += 64) {
-      const double df = (double)X[(size_t)r * d + f] - (double)Cm[(size_t)l * d + f];
-      s = fma(df, df, s);
+    for (int f = 4 * sub; f < d; f += 64) {
+      const float4 xv = *reinterpret_cast<const float4*>(xr + f);
+      const float4 cv = *reinterpret_cast<const float4*>(cr + f);
+      const double d0 = (double)xv.x - (double)cv.x, d1 = (double)xv.y - (double)cv.y;
+      const double d2 = (double)xv.z - (double)cv.z, d3 = (double)xv.w - (double)cv.w;
+      s = fma(d0, d0, fma(d1, d1, fma(d2, d2, fma(d3, d3, s))));
     }
-    s = wave_sum(s);
-    if (lane == 0) corr[r] = (float)((double)mind[r] - s);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (ok && sub == 0) corr[r] = (float)((double)mind[r] - s);
   }
 }
 
@@ -2419,7 +2434,8 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   const double a2 = alpha * alpha;
   const float fa = (float)alpha, ia2 = (float)(1.0 / a2), ds = (float)(delta * a2);
   int* cnt = (int*)counts;
-  if (corr) hipMemsetAsync(corr, 0, (size_t)n * sizeof(float), st);
+  // list mode follows the bounds filter, which zeroed the corrections
+  if (corr && !rlist) hipMemsetAsync(corr, 0, (size_t)n * sizeof(float), st);
   const int cap = (int)min(n, 2147483647LL);
   const unsigned fgrid = (unsigned)min((n + 15) / 16, 512LL);   // exact fp64 rows kernel
   int rc;
@@ -2438,7 +2454,7 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
                                cnt + 1);                                                         \
     if (rc) return rc;                                                                           \
     if (corr)                                                                                    \
-      hipLaunchKernelGGL(dense_corr_kernel, dim3(256), dim3(256), 0, st, (const float*)X,        \
+      hipLaunchKernelGGL(dense_corr_kernel, dim3(1024), dim3(256), 0, st, (const float*)X,       \
                          (const float*)Cm, (const long long*)dense_rows, (const int*)(cnt + 1),   \
                          (const int*)labels, (const float*)mind, (float*)corr, n, d_pad);        \
     rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, ovf_rows, cnt, 0, n, labels, mind, corr,      \

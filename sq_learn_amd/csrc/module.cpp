@@ -29,7 +29,7 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
                                            unsigned, unsigned, unsigned, const void*, int, void*);
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
                                            long long, double, void*, void*, const void*, void*,
-                                           void*, const void*, const void*, int, int, void*, const void*);
+                                           void*, const void*, const void*, int, int, void*, void*);
 __attribute__((weak)) int sq_multi_records(void*, void*, int, int, int, const void*, const void*,
                                            long long, void*, void*, void*);
 __attribute__((weak)) int sq_shift_operand(const void*, const void*, int, int, int, int, double,

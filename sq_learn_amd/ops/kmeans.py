@@ -394,7 +394,9 @@ def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf:
     accumulate; the E-step keeps rcount in ``buf.counts[3]``, so one fill
     clears both).
     ``cc`` [k nf + k] fp32 / ``nf``: the fastest centroids' Elkan distances
-    (:func:`fast_centroids_native`; ``smax`` then excludes them)."""
+    (:func:`fast_centroids_native`; ``smax`` then excludes them).  The
+    pass also zeroes ``buf.corr`` (the list-mode E-step that follows skips
+    its memset)."""
     n = labels.numel()
     assert ub.dtype == torch.float32 and lb.dtype == torch.float32 and rlist.numel() >= n
     assert shift.dtype == torch.float64 and smax.dtype == torch.float64
@@ -406,7 +408,8 @@ def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf:
                                     0 if cc is None else cc.data_ptr(),
                                     0 if cc is None else fidx.data_ptr(),
                                     int(nf if cc is not None else 0), int(shift.numel()),
-                                    nat.stream_handle(labels.device), buf.multi_cand.data_ptr())
+                                    nat.stream_handle(labels.device),
+                                    0 if buf.corr is None else buf.corr.data_ptr())
     if rc:
         raise RuntimeError(f"bounds_filter failed (hip error {rc})")
 
