@@ -69,7 +69,12 @@ SQ_DEV float vmed3(float a, float b, float c) {
   return r;
 }
 
-template <int KSD>
+// TOP = 2: per lane the two smallest values are band members, a 3rd in the
+// band -> overflow.  TOP = 3 (the overflow rows of a TOP = 2 pass, in list
+// mode): three members per lane, a 4th -> overflow; its rows are loaded at
+// the block start instead of prefetched (the longer lists need the
+// registers).
+template <int KSD, int TOP = 2>
 __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ C, const float* __restrict__ xn,
     int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ ovf_rows,
@@ -139,9 +144,11 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
   f16x8 aug = (f16x8)0;
   if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
 
-  // per-lane top-3 values and the indices of the two smallest
-  float m1[16], m2[16], m3[16];
-  int i1[16], i2[16];
+  static_assert(TOP == 2 || TOP == 3, "two or three members per lane");
+  constexpr bool PREFETCH = TOP == 2;
+  // per-lane top-(TOP + 1) values and the indices of the TOP smallest
+  float m1[16], m2[16], m3[16], m4[TOP == 3 ? 16 : 1];
+  int i1[16], i2[16], i3[TOP == 3 ? 16 : 1];
 
   const int lane_off = (half * 64 + r32) * 16;
   auto ldb = [&](const unsigned char* p) -> f16x8 { return *reinterpret_cast<const f16x8*>(p); };
@@ -157,6 +164,13 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
       const int a1 = i1[i], a2 = i2[i];
       const bool lt1 = v < q1, lt2 = v < q2;
       const int b2 = lt2 ? j : a2;
+      if constexpr (TOP == 3) {
+        const float q3 = m3[i];
+        const int a3 = i3[i];
+        const bool lt3 = v < q3;
+        m4[i] = vmed3(q3, v, m4[i]);
+        i3[i] = lt2 ? a2 : (lt3 ? j : a3);
+      }
       m3[i] = vmed3(q2, v, m3[i]);
       m2[i] = vmed3(q1, v, q2);
       m1[i] = vmin(q1, v);
@@ -228,10 +242,21 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
 
   for (; blk < nblk; blk += gridDim.x) {
     const long long row0 = blk * ROWS + wave * 32;
+    if constexpr (!PREFETCH) {
+      if (blk != (long long)blockIdx.x) {   // the first block's rows came with the prologue
+        load_raw(blk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        split();
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       m1[i] = m2[i] = m3[i] = __builtin_inff();
       i1[i] = i2[i] = 0;
+      if constexpr (TOP == 3) {
+        m4[i] = __builtin_inff();
+        i3[i] = 0;
+      }
     }
     f32x16 pA0, pA1, pB0, pB1;
     stage(G + 1);
@@ -240,7 +265,7 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     int t = 0;
     while (true) {
       if (t + 1 >= n_tiles) {
-        load_raw(blk + gridDim.x);   // clamped rows: unconditional
+        if constexpr (PREFETCH) load_raw(blk + gridDim.x);   // clamped rows: unconditional
         tile_step(smem, pB0, pB1, false, pA0, pA1, t, true);
         break;
       }
@@ -250,7 +275,7 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
       ++t;
       ++G;
       if (t + 1 >= n_tiles) {
-        load_raw(blk + gridDim.x);
+        if constexpr (PREFETCH) load_raw(blk + gridDim.x);
         tile_step(smem, pA0, pA1, false, pB0, pB1, t, true);
         break;
       }
@@ -318,8 +343,15 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         const float u_i = __shfl(urow, src, 64);
         const int c1 = (mine && m1[i] <= thr_i) ? 1 : 0;
         const int c2 = (mine && m2[i] <= thr_i) ? 1 : 0;
-        const bool v3 = mine && m3[i] <= thr_i;
-        const int cl = c1 + c2;
+        int c3 = 0;
+        bool v3;
+        if constexpr (TOP == 3) {
+          c3 = (mine && m3[i] <= thr_i) ? 1 : 0;
+          v3 = mine && m4[i] <= thr_i;
+        } else {
+          v3 = mine && m3[i] <= thr_i;
+        }
+        const int cl = c1 + c2 + c3;
         // inclusive prefix of member counts over the 32 lanes of this half
         int incl = cl;
 #pragma unroll
@@ -333,9 +365,21 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         // the lane whose [incl - cl, incl) range holds rank r supplies the
         // member: its (r - (incl - cl))-th in ascending index order
         const bool hit = cl > 0 && r >= incl - cl && r < incl;
-        const int x1 = i1[i], x2 = i2[i];
-        const int lo_j = min(x1, x2), hi_j = max(x1, x2);
-        const int myj = cl == 1 ? x1 : (r - (incl - cl) == 0 ? lo_j : hi_j);
+        int myj;
+        if constexpr (TOP == 3) {
+          // the lane's members in index (kappa) order
+          const int x1 = i1[i];
+          const int x2 = cl >= 2 ? i2[i] : 0x7fffffff, x3 = cl >= 3 ? i3[i] : 0x7fffffff;
+          const int s_lo = min(x1, min(x2, x3)), s_hi = max(x1, max(x2, x3));
+          const int s_mid = (int)((unsigned)x1 + (unsigned)x2 + (unsigned)x3 - (unsigned)s_lo -
+                                  (unsigned)s_hi);   // (used for cl == 3 only)
+          const int kk = r - (incl - cl);
+          myj = kk == 0 ? s_lo : (kk == 1 ? (cl == 2 ? min(max(x1, x2), s_hi) : s_mid) : s_hi);
+        } else {
+          const int x1 = i1[i], x2 = i2[i];
+          const int lo_j = min(x1, x2), hi_j = max(x1, x2);
+          myj = cl == 1 ? x1 : (r - (incl - cl) == 0 ? lo_j : hi_j);
+        }
         const unsigned long long hb = __ballot(hit) >> (32 * half);
         const int pl = hb ? __ffsll((long long)hb) - 1 : 0;
         const int jsel = __shfl(myj, 32 * half + pl, 64);
@@ -351,7 +395,9 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         }
       }
     }
-    if (blk + gridDim.x < nblk) split();
+    if constexpr (PREFETCH) {
+      if (blk + gridDim.x < nblk) split();
+    }
   }
   my_inertia = wave_sum(my_inertia);
   if (lane == 0) part[(size_t)blockIdx.x * NW + wave] = my_inertia;
@@ -1189,6 +1235,18 @@ struct MultiRec {
   int* n_done = nullptr;           // list-B rows the gap screen resolved
 };
 static thread_local MultiRec g_mrec;
+// second overflow list of the dense-row 3-pass kernel (null: off) - the
+// calling thread's next certified E-steps
+struct Ovf2 {
+  void* rows = nullptr;   // int64 [cap]
+  int* count = nullptr;   // int32 [1], zeroed with the E-step's counters
+};
+static thread_local Ovf2 g_ovf2;
+extern "C" int sq_set_overflow2(void* rows, void* count) {
+  g_ovf2.rows = rows;
+  g_ovf2.count = (int*)count;
+  return (rows != nullptr) != (count != nullptr) ? (int)hipErrorInvalidValue : 0;
+}
 extern "C" int sq_multi_records(void* rec, void* mflag, int it_now, int it_lo, int ring,
                                 const void* dsh, const void* dq, long long dsh_stride,
                                 void* mrows_b, void* count_b, void* n_done) {
@@ -2220,7 +2278,7 @@ extern "C" int sq_rows_f64(const void* X, long long ldx, const void* C, long lon
                            unsigned k0, unsigned k1, unsigned s0, unsigned s1,
                            long long row_offset, int grid, void* stream);
 
-template <int KSD>
+template <int KSD, int TOP = 2>
 static int launch_estep_f32(const void* X, const void* C, const void* xn, void* labels, void* mind,
                             void* ovf_rows, void* ovf_count, void* part, int part_cap,
                             void* inertia, long long n, int k_pad, float alpha, float inv_a2,
@@ -2229,7 +2287,7 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
                             const void* rcount = nullptr) {
   constexpr int NW = 4;
   const size_t lds = 2 * (size_t)((2 * KSD + 1) * 2048);
-  auto kern = estep_f32_kernel<KSD>;
+  auto kern = estep_f32_kernel<KSD, TOP>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2453,11 +2511,20 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
                                n, k_pad, fa, ia2, ds, key, row_offset, cap, st, dense_rows,       \
                                cnt + 1);                                                         \
     if (rc) return rc;                                                                           \
+    if (g_ovf2.rows) {                                                                           \
+      /* the overflow rows once more with 3 members per lane; what still */                      \
+      /* overflows goes to the fp64 rows kernel */                                               \
+      rc = launch_estep_f32<KSD, 3>(X, C, xn, labels, mind, g_ovf2.rows, g_ovf2.count, part,     \
+                                    part_cap, nullptr, n, k_pad, fa, ia2, ds, key, row_offset,   \
+                                    cap, st, ovf_rows, cnt);                                     \
+      if (rc) return rc;                                                                         \
+    }                                                                                            \
     if (corr)                                                                                    \
       hipLaunchKernelGGL(dense_corr_kernel, dim3(1024), dim3(256), 0, st, (const float*)X,       \
                          (const float*)Cm, (const long long*)dense_rows, (const int*)(cnt + 1),   \
                          (const int*)labels, (const float*)mind, (float*)corr, n, d_pad);        \
-    rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, ovf_rows, cnt, 0, n, labels, mind, corr,      \
+    rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, g_ovf2.rows ? g_ovf2.rows : ovf_rows,        \
+                     g_ovf2.rows ? g_ovf2.count : cnt, 0, n, labels, mind, corr,                  \
                      ub, delta, k0, k1, s0, s1, row_offset, (int)fgrid, stream);                 \
     break;
     CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)

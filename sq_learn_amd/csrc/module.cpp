@@ -32,6 +32,7 @@ __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void
                                            void*, const void*, const void*, int, int, void*, void*);
 __attribute__((weak)) int sq_multi_records(void*, void*, int, int, int, const void*, const void*,
                                            long long, void*, void*, void*);
+__attribute__((weak)) int sq_set_overflow2(void*, void*);
 __attribute__((weak)) int sq_shift_operand(const void*, const void*, int, int, int, int, double,
                                            void*, void*, void*, int, int, unsigned, void*);
 __attribute__((weak)) int sq_fast_centroids(void*, const void*, const void*, int, int, int, void*,
@@ -280,6 +281,14 @@ static PyObject* py_multi_records(PyObject*, PyObject* a) {
   CHECK(sq_multi_records)
   return ret(sq_multi_records(P(rec), P(mf), now, lo, ring, P(dsh), P(dq), ds, P(mb), P(cb),
                               P(nd)));
+}
+
+// the second overflow list of the dense-row 3-pass kernel (null: off)
+static PyObject* py_set_overflow2(PyObject*, PyObject* a) {
+  unsigned long long rows, cnt;
+  if (!PyArg_ParseTuple(a, "KK", &rows, &cnt)) return nullptr;
+  CHECK(sq_set_overflow2)
+  return ret(sq_set_overflow2(P(rows), P(cnt)));
 }
 
 // the gap screen's fp16 shift operand of one centroid update
@@ -715,6 +724,7 @@ static PyMethodDef methods[] = {
     {"bounds_filter", py_bounds_filter, METH_VARARGS, "Hamerly pruning -> active row list"},
     {"multi_records", py_multi_records, METH_VARARGS, "gap records of the multi rows (gap screen)"},
     {"shift_operand", py_shift_operand, METH_VARARGS, "fp16 centroid-shift operand (gap screen)"},
+    {"set_overflow2", py_set_overflow2, METH_VARARGS, "second overflow list of the 3-pass kernel"},
     {"fast_centroids", py_fast_centroids, METH_VARARGS, "fastest centroids + Elkan distances"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},

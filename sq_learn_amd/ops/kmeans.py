@@ -181,8 +181,10 @@ class EStepBuffers:
         # [overflow rows, dense rows, multi-candidate rows, rows the bounds
         # filter kept] (int32); ovf_count is a view of slot 0
         # [3-pass overflow rows, dense rows, multi rows, kept rows (filter),
-        #  list-B rows resolved by the gap screen, list-B rows (filter)]
-        self.counts = torch.zeros(6, dtype=torch.int32, device=device)
+        #  list-B rows resolved by the gap screen, list-B rows (filter),
+        #  overflow rows of the second (3 members per lane) 3-pass]
+        self.counts = torch.zeros(7, dtype=torch.int32, device=device)
+        self.ovf2_rows = None
         self.exact_flag = None   # the fp32 screen's hand-off flags (per multi entry)
         self.ovf_count = self.counts[0:1]
         self.dense_rows = None   # allocated by the certified E-step on first use
@@ -799,6 +801,15 @@ def estep_x64_native(Xh, Xf, C_op, C_pad, xn, cmax2, k, delta, alpha, key: RngKe
     if zero_counts:
         buf.counts.zero_()
     buf.ovf_clean = False
+    # dense rows (d_pad <= 256): the 3-pass kernel's overflow rows get a
+    # second pass with 3 band members per lane before the fp64 rows kernel
+    import os
+    if d_pad <= 256 and os.environ.get("SQ_OVF2", "1") != "0":
+        if buf.ovf2_rows is None or buf.ovf2_rows.numel() < n:
+            buf.ovf2_rows = torch.empty(max(n, 1), dtype=torch.int64, device=Xf.device)
+        nat.native().set_overflow2(buf.ovf2_rows.data_ptr(), buf.counts[6:7].data_ptr())
+    else:
+        nat.native().set_overflow2(0, 0)
     nat.native().estep_x64(Xh.data_ptr(), Xf.data_ptr(), C_op.data_ptr(), C_pad.data_ptr(),
                            xn.data_ptr(), cmax2.data_ptr(), buf.labels.data_ptr(),
                            buf.mind.data_ptr(), buf.dense_rows.data_ptr(), buf.ovf_rows.data_ptr(),
