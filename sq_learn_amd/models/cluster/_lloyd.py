@@ -382,6 +382,17 @@ class LloydEngine:
             self._ipe_cur = 0
             self._ipe_xn = self.xn.float().contiguous()
 
+    def _list_rs(self):
+        """Row sets per wave of the list-mode sweep: the full sweep's tiling
+        (2) while the filter is expected to keep most rows (no measurement
+        yet after new centres, or the last one above 30 %), one row set (the
+        short-list default) once it prunes."""
+        force = os.environ.get("SQ_LIST_RS")
+        if force is not None:
+            return int(force)
+        kf = self._kept_frac
+        return 2 if (kf is None or kf > 0.3) else 0
+
     def _records_epoch(self):
         """New centres not reached by the shift operands: every gap record
         written so far is void (current records have a base >= _rlo)."""
@@ -467,7 +478,8 @@ class LloydEngine:
                                                self.row_offset, self.buf,
                                                bounds=(self.ub, self.lb)
                                                if self.bounds and self._bounds_kept else None,
-                                               rows=rows, zero_counts=zero, screen=screen)
+                                               rows=rows, zero_counts=zero, screen=screen,
+                                               list_rs=self._list_rs())
                 if self.mrec is not None:
                     K.multi_records(None)   # thread-local: never leak into another engine
                     if not screen:
