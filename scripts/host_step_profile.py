@@ -1,5 +1,7 @@
-"""Host cost of the pipelined share8 step (1.25M rows, k = 1024): enqueue time
-of eng.step() vs the wait in the scalar read, then a cProfile of 100 steps."""
+"""Host cost of the pipelined Lloyd step (k = 1024): enqueue time of
+eng.step() vs the wait in the scalar read, then a cProfile of 100 steps.
+argv[1]: the share of the 10M x 256 problem (8: the N = 8 per-GPU share of
+1.25M rows, the default; 1: the headline's 10M rows)."""
 import cProfile
 import pstats
 import sys
@@ -20,13 +22,14 @@ X, _ = make_blobs_device(n, d, centers=1024, cluster_std=1.0, seed=2024, device=
                          dtype=torch.float32, row_range=(0, n))
 comm = Comm(None)
 C0 = gather_rows(Data(X, n, 0, comm, "sharded"), np.random.RandomState(2024).choice(n, k, replace=False))
-Xs = X[: n // 8].contiguous()
+share = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+Xs = X[: n // share].contiguous() if share > 1 else X
 del X
 eng = LloydEngine(Xs, k, delta=0.5, true_distance_estimate=False, intermediate_error=True,
                   true_tomography=False, seed=2024, comm=comm, row_offset=0, gemm_precision="fp32")
 eng.set_centers(C0)
 eng.pipeline = True
-for _ in range(10):
+for _ in range(20 if share == 1 else 10):
     eng.step()[1].tolist()
 torch.cuda.synchronize()
 te = tw = 0.0

@@ -1061,7 +1061,8 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
     long long* __restrict__ rlist, int* __restrict__ rcount, const int* __restrict__ mflag,
     long long* __restrict__ mrows, int* __restrict__ multi_count, const float* __restrict__ cc,
     const int* __restrict__ fidx, int nf, int k, int rec_on, int it_now, int it_lo,
-    long long* __restrict__ mrows_b, int* __restrict__ count_b, float* __restrict__ corr) {
+    long long* __restrict__ mrows_b, int* __restrict__ count_b, float* __restrict__ corr,
+    int* __restrict__ rec_count) {
   constexpr int kBoundsChunk = PER * 256;   // PER rows per thread (bit masks)
   // A multi row whose bounds hold keeps its candidate set; when its gap
   // record is current (mflag = 2 + the record's base iteration b, it_lo <= b
@@ -1193,6 +1194,9 @@ __global__ void __launch_bounds__(256) bounds_filter_kernel(
   if (tid == 0) {
     base_a = (total & 0xffff) ? atomicAdd(rcount, total & 0xffff) : 0;
     base_m = (total >> 16) ? atomicAdd(multi_count, total >> 16) : 0;
+    // the multi list's head (this pass's rows, before the sweep appends):
+    // the incremental M-step's second row list
+    if (rec_count && (total >> 16)) atomicAdd(rec_count, total >> 16);
     base_b = total_b ? atomicAdd(count_b, total_b) : 0;
   }
   __syncthreads();
@@ -1273,7 +1277,7 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                                 const void* smax, long long n, double delta, void* rlist,
                                 void* rcount, const void* mflag, void* mrows, void* multi_count,
                                 const void* cc, const void* fidx, int nf, int k, void* stream,
-                                void* corr) {
+                                void* corr, void* rec_count) {
   if (n <= 0) return 0;
   if (!mflag || !mrows || !multi_count) return (int)hipErrorInvalidValue;
   if (nf < 0 || nf > 64 || (nf > 0 && (!cc || !fidx || k <= nf))) return (int)hipErrorInvalidValue;
@@ -1311,7 +1315,7 @@ extern "C" int sq_bounds_filter(const void* labels, void* ub, void* lb, const vo
                      (int*)rcount, (const int*)mflag, (long long*)mrows, (int*)multi_count,
                      (const float*)cc, (const int*)fidx, nf, k,
                      g_mrec.rec ? 1 : 0, g_mrec.it_now, g_mrec.it_lo, g_mrec.mrows_b,
-                     g_mrec.count_b, (float*)corr);
+                     g_mrec.count_b, (float*)corr, (int*)rec_count);
   return (int)hipGetLastError();
 }
 

@@ -975,6 +975,126 @@ __global__ void __launch_bounds__(256) delta_scatter_kernel(const int* __restric
   }
 }
 
+// List form of delta_hist / delta_scatter: after a FILTERED E-step only the
+// rows on its three disjoint row lists can carry a new label (the rows the
+// Hamerly bounds could not prune, the pruned multi-candidate rows re-checked
+// without a record, the rows of list B); every other row kept its label and
+// prev == labels there.  The two passes walk just those rows (the
+// concatenation of the lists, lengths on the device) instead of all n - the
+// same entries, so the same statistics (exact integer arithmetic: any
+// order).  Grid-stride, kDL entries in flight per thread (row -> label /
+// prev are dependent gathers).
+struct RowLists {
+  const long long* L[3];
+  const int* c[3];
+};
+constexpr int kDL = 8;
+struct RowListWalk {
+  long long c0, c01, total;
+  const RowLists& R;
+  SQ_DEV RowListWalk(const RowLists& r, long long n) : R(r) {
+    const long long a = R.L[0] ? min((long long)*R.c[0], n) : 0;
+    const long long b = R.L[1] ? min((long long)*R.c[1], n) : 0;
+    const long long c = R.L[2] ? min((long long)*R.c[2], n) : 0;
+    c0 = a;
+    c01 = a + b;
+    total = a + b + c;
+  }
+  SQ_DEV long long row(long long e) const {
+    return e < c0 ? R.L[0][e] : (e < c01 ? R.L[1][e - c0] : R.L[2][e - c01]);
+  }
+};
+
+__global__ void __launch_bounds__(256) delta_hist_list_kernel(const int* __restrict__ labels,
+                                                              const int* __restrict__ prev,
+                                                              RowLists R, long long n, int k,
+                                                              int* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) int dl[];
+  for (int j = threadIdx.x; j < k; j += 256) dl[j] = 0;
+  __syncthreads();
+  const RowListWalk W(R, n);
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long e0 = (long long)blockIdx.x * 256 + threadIdx.x; e0 < W.total; e0 += kDL * stride) {
+    long long r[kDL];
+    int l[kDL], p[kDL];
+#pragma unroll
+    for (int u = 0; u < kDL; ++u) {
+      const long long e = e0 + u * stride;
+      r[u] = e < W.total ? W.row(e) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kDL; ++u) {
+      l[u] = r[u] >= 0 ? labels[r[u]] : 0;
+      p[u] = r[u] >= 0 ? prev[r[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kDL; ++u) {
+      if (r[u] < 0 || l[u] == p[u]) continue;
+      if (l[u] >= 0 && l[u] < k) atomicAdd(&dl[l[u]], 1);
+      if (p[u] >= 0 && p[u] < k) atomicAdd(&dl[p[u]], 1);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256)
+    if (dl[j]) atomicAdd(&hist[j], dl[j]);
+}
+
+__global__ void __launch_bounds__(256) delta_scatter_list_kernel(const int* __restrict__ labels,
+                                                                 int* __restrict__ prev,
+                                                                 RowLists R, long long n, int k,
+                                                                 int* __restrict__ cursor,
+                                                                 int2* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) int dls[];
+  int* lh = dls;
+  int* base = dls + k;
+  for (int j = threadIdx.x; j < k; j += 256) lh[j] = 0;
+  __syncthreads();
+  const RowListWalk W(R, n);
+  const long long stride = (long long)gridDim.x * 256;
+  // pass 1 counts this block's entries per label, pass 2 places them (the
+  // same entries: the lists do not change in between)
+  for (int pass = 0; pass < 2; ++pass) {
+    for (long long e0 = (long long)blockIdx.x * 256 + threadIdx.x; e0 < W.total;
+         e0 += kDL * stride) {
+      long long r[kDL];
+      int l[kDL], p[kDL];
+#pragma unroll
+      for (int u = 0; u < kDL; ++u) {
+        const long long e = e0 + u * stride;
+        r[u] = e < W.total ? W.row(e) : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kDL; ++u) {
+        l[u] = r[u] >= 0 ? labels[r[u]] : 0;
+        p[u] = r[u] >= 0 ? prev[r[u]] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kDL; ++u) {
+        if (r[u] < 0 || l[u] == p[u]) continue;
+        const bool li = l[u] >= 0 && l[u] < k, pi = p[u] >= 0 && p[u] < k;
+        if (pass == 0) {
+          if (li) atomicAdd(&lh[l[u]], 1);
+          if (pi) atomicAdd(&lh[p[u]], 1);
+        } else {
+          if (li) perm[base[l[u]] + atomicAdd(&lh[l[u]], 1)] = make_int2((int)r[u], l[u]);
+          if (pi)
+            perm[base[p[u]] + atomicAdd(&lh[p[u]], 1)] = make_int2((int)r[u], p[u] | (1 << 30));
+          prev[r[u]] = l[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (pass == 0) {
+      for (int j = threadIdx.x; j < k; j += 256) {
+        const int c = lh[j];
+        base[j] = c ? atomicAdd(&cursor[j], c) : 0;
+        lh[j] = 0;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // one wave per entry (4 fp32 values per lane per 256-column chunk), U entries in
 // flight per wave; the entry count is the scanned total (cursor[k-1]).
 // Each wave takes a run of max(SQ_DSEG_RUN, total / SQ_DSEG_WAVES) entries:
@@ -1978,20 +2098,35 @@ int sq_centroid_reduce(const void* X, int xdtype, const void* labels, const void
 // sums / counts / qsum are UPDATED (not overwritten) by the rows whose label
 // differs from prev, and prev becomes labels; qexp is the quantum of the
 // squared norms; ws_perm holds 2n int2 entries.
-int sq_centroid_delta(const void* X, const void* labels, const void* prev, void* sums,
-                      void* counts, void* qsum, long long n, int d, int k, int xexp, int qexp,
-                      void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
+// lists (nullable): the row lists of the filtered E-step that produced
+// labels - only those rows are walked (delta_hist_list_kernel); null: all n.
+static int centroid_delta_impl(const void* X, const void* labels, const void* prev, void* sums,
+                               void* counts, void* qsum, long long n, int d, int k, int xexp,
+                               int qexp, void* ws_hist, void* ws_cursor, void* ws_perm,
+                               const RowLists* lists, void* stream) {
   if (n <= 0) return 0;
   if (d % 4 != 0 || d > 1024 || k > 16384 || 2 * n > 2147483647LL) return (int)hipErrorInvalidValue;
   if (xexp < -120 || xexp > 120 || qexp < -200 || qexp > 200) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
-  hipLaunchKernelGGL(delta_hist_kernel, dim3(chunks), dim3(256), (size_t)k * 4, st,
-                     (const int*)labels, (const int*)prev, n, k, (int*)ws_hist);
-  hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)ws_hist, k,
-                     (int*)ws_cursor);
-  hipLaunchKernelGGL(delta_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
-                     (const int*)labels, (int*)prev, n, k, (int*)ws_cursor, (int2*)ws_perm);
+  if (lists) {
+    const long long lb = (n + 1023) / 1024;
+    const unsigned lgrid = (unsigned)(lb < 256 ? lb : 256);
+    hipLaunchKernelGGL(delta_hist_list_kernel, dim3(lgrid), dim3(256), (size_t)k * 4, st,
+                       (const int*)labels, (const int*)prev, *lists, n, k, (int*)ws_hist);
+    hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)ws_hist, k,
+                       (int*)ws_cursor);
+    hipLaunchKernelGGL(delta_scatter_list_kernel, dim3(lgrid), dim3(256), (size_t)k * 8, st,
+                       (const int*)labels, (int*)prev, *lists, n, k, (int*)ws_cursor,
+                       (int2*)ws_perm);
+  } else {
+    const unsigned chunks = (unsigned)((n + kHistChunk - 1) / kHistChunk);
+    hipLaunchKernelGGL(delta_hist_kernel, dim3(chunks), dim3(256), (size_t)k * 4, st,
+                       (const int*)labels, (const int*)prev, n, k, (int*)ws_hist);
+    hipLaunchKernelGGL(label_scan_kernel, dim3(1), dim3(1024), 0, st, (int*)ws_hist, k,
+                       (int*)ws_cursor);
+    hipLaunchKernelGGL(delta_scatter_kernel, dim3(chunks), dim3(256), (size_t)k * 8, st,
+                       (const int*)labels, (int*)prev, n, k, (int*)ws_cursor, (int2*)ws_perm);
+  }
   // entries <= 2n, usually far fewer: a fixed grid shares the scanned total
   const long long cap_blocks = (2 * n + 63) / 64;
   const unsigned grid = (unsigned)(cap_blocks < 2048 ? cap_blocks : 2048);
@@ -2003,6 +2138,29 @@ int sq_centroid_delta(const void* X, const void* labels, const void* prev, void*
                      (double*)sums, (double*)counts, (double*)qsum,
                      (const int*)ws_cursor + (k - 1));
   return (int)hipGetLastError();
+}
+
+int sq_centroid_delta(const void* X, const void* labels, const void* prev, void* sums,
+                      void* counts, void* qsum, long long n, int d, int k, int xexp, int qexp,
+                      void* ws_hist, void* ws_cursor, void* ws_perm, void* stream) {
+  return centroid_delta_impl(X, labels, prev, sums, counts, qsum, n, d, k, xexp, qexp, ws_hist,
+                             ws_cursor, ws_perm, nullptr, stream);
+}
+
+// rows: three int64 row lists and their int32 device lengths (a null list
+// is empty); together they must hold every row whose label can differ from
+// prev, each once
+int sq_centroid_delta_lists(const void* X, const void* labels, const void* prev, void* sums,
+                            void* counts, void* qsum, long long n, int d, int k, int xexp,
+                            int qexp, void* ws_hist, void* ws_cursor, void* ws_perm,
+                            const void* L0, const void* c0, const void* L1, const void* c1,
+                            const void* L2, const void* c2, void* stream) {
+  RowLists R{{(const long long*)L0, (const long long*)L1, (const long long*)L2},
+             {(const int*)c0, (const int*)c1, (const int*)c2}};
+  for (int i = 0; i < 3; ++i)
+    if ((R.L[i] != nullptr) != (R.c[i] != nullptr)) return (int)hipErrorInvalidValue;
+  return centroid_delta_impl(X, labels, prev, sums, counts, qsum, n, d, k, xexp, qexp, ws_hist,
+                             ws_cursor, ws_perm, &R, stream);
 }
 
 // part[c] = Q_c - 2 c.S_c + n_c |c|^2 (fp64) for the centroids C the labels

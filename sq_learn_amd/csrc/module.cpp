@@ -29,7 +29,8 @@ __attribute__((weak)) int sq_mnom_segments(const void*, long long, const void*, 
                                            unsigned, unsigned, unsigned, const void*, int, void*);
 __attribute__((weak)) int sq_bounds_filter(const void*, void*, void*, const void*, const void*,
                                            long long, double, void*, void*, const void*, void*,
-                                           void*, const void*, const void*, int, int, void*, void*);
+                                           void*, const void*, const void*, int, int, void*, void*,
+                                           void*);
 __attribute__((weak)) int sq_multi_records(void*, void*, int, int, int, const void*, const void*,
                                            long long, void*, void*, void*);
 __attribute__((weak)) int sq_set_overflow2(void*, void*);
@@ -57,6 +58,11 @@ __attribute__((weak)) int sq_ipe16(int, const long long*, const double*, void*);
 __attribute__((weak)) int sq_centroid_delta(const void*, const void*, const void*, void*, void*,
                                             void*, long long, int, int, int, int, void*, void*,
                                             void*, void*);
+__attribute__((weak)) int sq_centroid_delta_lists(const void*, const void*, const void*, void*,
+                                                  void*, void*, long long, int, int, int, int,
+                                                  void*, void*, void*, const void*, const void*,
+                                                  const void*, const void*, const void*,
+                                                  const void*, void*);
 __attribute__((weak)) int sq_cluster_inertia(const void*, const void*, const void*, const void*,
                                              int, int, int, int, void*, void*);
 // pairwise_fast.hip
@@ -262,14 +268,16 @@ static PyObject* py_mnom_segments(PyObject*, PyObject* a) {
 }
 
 static PyObject* py_bounds_filter(PyObject*, PyObject* a) {
-  unsigned long long lab, ub, lb, sh, sm, rl, rc, mf, mr, mcnt, cc, fi, st, mc = 0; long long n;
+  unsigned long long lab, ub, lb, sh, sm, rl, rc, mf, mr, mcnt, cc, fi, st, mc = 0, rcn = 0;
+  long long n;
   double delta; int nf, k;
-  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKiiK|K", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc,
-                        &mf, &mr, &mcnt, &cc, &fi, &nf, &k, &st, &mc))
+  // optional: corrections to zero, the multi-list head counter
+  if (!PyArg_ParseTuple(a, "KKKKKLdKKKKKKKiiK|KK", &lab, &ub, &lb, &sh, &sm, &n, &delta, &rl, &rc,
+                        &mf, &mr, &mcnt, &cc, &fi, &nf, &k, &st, &mc, &rcn))
     return nullptr;
   CHECK(sq_bounds_filter)
   return ret(sq_bounds_filter(P(lab), P(ub), P(lb), P(sh), P(sm), n, delta, P(rl), P(rc), P(mf),
-                              P(mr), P(mcnt), P(cc), P(fi), nf, k, P(st), P(mc)));
+                              P(mr), P(mcnt), P(cc), P(fi), nf, k, P(st), P(mc), P(rcn)));
 }
 
 // the multi-row records of this thread's next certified E-steps (null: off)
@@ -319,6 +327,18 @@ static PyObject* py_centroid_delta(PyObject*, PyObject* a) {
   CHECK(sq_centroid_delta)
   return ret(sq_centroid_delta(P(X), P(lab), P(prev), P(sums), P(cnts), P(q), n, d, k, xe, qe,
                                P(h), P(c), P(pm), P(st)));
+}
+
+static PyObject* py_centroid_delta_lists(PyObject*, PyObject* a) {
+  unsigned long long X, lab, prev, sums, cnts, q, h, c, pm, l0, c0, l1, c1, l2, c2, st;
+  long long n; int d, k, xe, qe;
+  if (!PyArg_ParseTuple(a, "KKKKKKLiiiiKKKKKKKKKK", &X, &lab, &prev, &sums, &cnts, &q, &n, &d, &k,
+                        &xe, &qe, &h, &c, &pm, &l0, &c0, &l1, &c1, &l2, &c2, &st))
+    return nullptr;
+  CHECK(sq_centroid_delta_lists)
+  return ret(sq_centroid_delta_lists(P(X), P(lab), P(prev), P(sums), P(cnts), P(q), n, d, k, xe,
+                                     qe, P(h), P(c), P(pm), P(l0), P(c0), P(l1), P(c1), P(l2),
+                                     P(c2), P(st)));
 }
 
 static PyObject* py_cluster_inertia(PyObject*, PyObject* a) {
@@ -727,6 +747,8 @@ static PyMethodDef methods[] = {
     {"set_overflow2", py_set_overflow2, METH_VARARGS, "second overflow list of the 3-pass kernel"},
     {"fast_centroids", py_fast_centroids, METH_VARARGS, "fastest centroids + Elkan distances"},
     {"centroid_delta", py_centroid_delta, METH_VARARGS, "incremental fixed-point cluster stats"},
+    {"centroid_delta_lists", py_centroid_delta_lists, METH_VARARGS,
+     "incremental cluster stats over a filtered E-step's row lists"},
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},
     {"ipe16", py_ipe16, METH_VARARGS, "certified fp16 screen of the IPE E-step (op per phase)"},

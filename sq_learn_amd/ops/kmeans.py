@@ -178,12 +178,12 @@ class EStepBuffers:
         self.ovf_cap = int(ovf_cap if ovf_cap is not None else max(n, 1))
         self.ovf_rows = torch.empty(self.ovf_cap, dtype=torch.int64, device=device)
         self.ovf_thr = torch.empty(self.ovf_cap, dtype=torch.float32, device=device)
-        # [overflow rows, dense rows, multi-candidate rows, rows the bounds
-        # filter kept] (int32); ovf_count is a view of slot 0
+        # (int32; ovf_count is a view of slot 0)
         # [3-pass overflow rows, dense rows, multi rows, kept rows (filter),
         #  list-B rows resolved by the gap screen, list-B rows (filter),
-        #  overflow rows of the second (3 members per lane) 3-pass]
-        self.counts = torch.zeros(7, dtype=torch.int32, device=device)
+        #  overflow rows of the second (3 members per lane) 3-pass,
+        #  the filter's own multi-list rows (the list's head)]
+        self.counts = torch.zeros(8, dtype=torch.int32, device=device)
         self.ovf2_rows = None
         self.exact_flag = None   # the fp32 screen's hand-off flags (per multi entry)
         self.ovf_count = self.counts[0:1]
@@ -411,7 +411,8 @@ def bounds_filter_native(labels, ub, lb, shift, smax, delta, rlist, rcount, buf:
                                     0 if cc is None else fidx.data_ptr(),
                                     int(nf if cc is not None else 0), int(shift.numel()),
                                     nat.stream_handle(labels.device),
-                                    0 if buf.corr is None else buf.corr.data_ptr())
+                                    0 if buf.corr is None else buf.corr.data_ptr(),
+                                    buf.counts[7:8].data_ptr())
     if rc:
         raise RuntimeError(f"bounds_filter failed (hip error {rc})")
 
@@ -490,17 +491,39 @@ def ensure_multi_buffers(buf: EStepBuffers, n, device, bounds=False):
 
 
 def centroid_delta_native(X, labels, prev, sums, counts, qsum, k, ws: ReduceWorkspace, perm2,
-                          qexp):
+                          qexp, lists=None):
     """Incremental fixed-point cluster statistics (csrc/kmeans.hip
     delta_segment_kernel): sums / counts / qsum are UPDATED by the rows whose
     label differs from ``prev`` (prev = -1: the row enters), and ``prev``
     becomes ``labels`` in the same pass.  Bit-identical to recomputing them
     from scratch (exact integer arithmetic in fp64).  ``perm2``: int32
-    workspace of 4 n (2 n (row, label) entries)."""
+    workspace of 4 n (2 n (row, label) entries).
+
+    ``lists``: up to three (int64 rows, int32 [1] device length) pairs (None
+    = empty) that together hold, once each, every row whose label can differ
+    from ``prev`` (a filtered E-step's row lists): only those rows are
+    walked - the same statistics."""
     n, d = X.shape
     assert X.dtype == torch.float32 and X.is_contiguous() and d % 4 == 0 and d <= 1024
     assert labels.dtype == torch.int32 and prev.dtype == torch.int32 and perm2.numel() >= 4 * n
     assert sums.dtype == torch.float64 and sums.numel() >= k * d and qsum.numel() >= k
+    if lists is not None:
+        lp = []
+        for ent in list(lists) + [None] * (3 - len(lists)):
+            if ent is None:
+                lp += [0, 0]
+            else:
+                rows, cnt = ent
+                assert rows.dtype == torch.int64 and cnt.dtype == torch.int32
+                lp += [rows.data_ptr(), cnt.data_ptr()]
+        rc = nat.native().centroid_delta_lists(X.data_ptr(), labels.data_ptr(), prev.data_ptr(),
+                                               sums.data_ptr(), counts.data_ptr(),
+                                               qsum.data_ptr(), n, d, k, ws.xexp, int(qexp),
+                                               ws.hist.data_ptr(), ws.cursor.data_ptr(),
+                                               perm2.data_ptr(), *lp, nat.stream_handle(X.device))
+        if rc:
+            raise RuntimeError(f"centroid_delta_lists failed (hip error {rc})")
+        return
     rc = nat.native().centroid_delta(X.data_ptr(), labels.data_ptr(), prev.data_ptr(),
                                      sums.data_ptr(), counts.data_ptr(), qsum.data_ptr(), n, d, k,
                                      ws.xexp, int(qexp), ws.hist.data_ptr(), ws.cursor.data_ptr(),
