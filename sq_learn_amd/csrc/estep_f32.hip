@@ -50,6 +50,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTileN = 64;          // centroids per LDS tile
+constexpr int kMaxCand = 16;        // candidates per multi row (fp64 re-check list)
 
 SQ_DEV float vmin(float a, float b) {
   float r;
@@ -80,9 +81,23 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     int* __restrict__ labels, float* __restrict__ mind, long long* __restrict__ ovf_rows,
     int* __restrict__ ovf_count, double* __restrict__ part, long long n, int k_pad, float alpha,
     float inv_alpha2, float delta_s, RngKey key, long long row_offset, int ovf_cap,
-    const long long* __restrict__ rlist, const int* __restrict__ rcount) {
+    const long long* __restrict__ rlist, const int* __restrict__ rcount,
+    const float* __restrict__ cmax2_p, long long* __restrict__ mrows, int* __restrict__ mcand,
+    int* __restrict__ multi_count, unsigned char* __restrict__ xflag, long long mcap) {
   // list mode (rlist != null): the rows are rlist[0 .. *rcount) - the dense
   // rows handed over by the certified filter kernel (estep_x64_kernel)
+  // cmax2_p (max_j alpha^2 ||c_j||^2, nullable): the band decisions are made
+  // only where the fp32-faithful values are provably on one side of the
+  // band edge.  A row with a tracked value within 2 E of it is settled in
+  // fp64: its candidates (every tracked value <= edge + 2 E; complete when
+  // no lane's last tracked value is that low) go to the multi list for the
+  // fp64 re-check (recheck_rows_kernel, launched after this pass), else the
+  // row overflows to the exact rows kernel.  E bounds |D'~ - alpha^2 D'|:
+  // the hi/lo split drops <= 3 2^-22 |x^| |c^| and the fp32 accumulation of
+  // the 3 (KSD + 1) x 16 products and norm pieces adds <= (3 DX + 48) 2^-24
+  // of the sum of their magnitudes <= 2 |x^| C + C^2 (C = max alpha ||c||).
+  const float Cm = cmax2_p ? sqrtf(*cmax2_p) * (1.0f + 0x1p-16f) : 0.0f;
+  constexpr float kEps3 = (3.0f * 0x1p-22f + (3.0f * KSD * 16 + 48.0f) * 0x1p-24f) * 1.0625f;
   if (rlist) n = min(n, (long long)*rcount);
   auto map_row = [&](long long r) -> long long { return rlist ? rlist[r] : r; };
   constexpr int NW = 4;
@@ -319,18 +334,24 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     const long long grow_local = row0 + rloc;
     const bool owner = ((r32 & 1) == 0) && grow_local < n;
     const float thr = q1 + delta_s;
-    const bool band2 = q2 <= thr;
     const long long gmap = owner ? map_row(grow_local) : 0;
+    const float xnv = owner ? xn[gmap] : 0.0f;
+    // 2 E of this row (the edge moves with q1's own error too)
+    const float e2 = cmax2_p ? 2.0f * kEps3 * (2.0f * alpha * sqrtf(xnv) * Cm + Cm * Cm) : 0.0f;
+    // 2nd value within 2 E of the edge: membership undecidable here
+    const bool unc = cmax2_p && fabsf(q2 - thr) <= e2;
+    const bool band2 = q2 <= thr && !unc;
     if (owner) {
-      const float dist = fmaxf(xn[gmap] + q1 * inv_alpha2, 0.0f);
+      const float dist = fmaxf(xnv + q1 * inv_alpha2, 0.0f);
       mind[gmap] = dist;
-      if (!band2) labels[gmap] = qi;
+      if (!band2 && !unc) labels[gmap] = qi;
       my_inertia += (double)dist;
     }
     // rows with >= 2 band members: the rank rule over the per-lane top-2
     // lists; lane r32 holds the columns j = r32 mod 32, so (lane, index)
     // order is kappa order.  A lane whose 3rd value is in the band -> overflow.
-    const unsigned long long slow = __ballot(owner && band2);
+    // Rows near the edge (unc, or a tracked value within 2 E): fp64 below.
+    const unsigned long long slow = __ballot(owner && (band2 || unc));
     if (slow) {
       const float urow = band_u(key, row_offset + gmap);
 #pragma unroll
@@ -341,23 +362,60 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         const bool mine = (slow >> src) & 1ull;
         const float thr_i = __shfl(thr, src, 64);
         const float u_i = __shfl(urow, src, 64);
+        const float e2_i = __shfl(e2, src, 64);
+        const bool unc_i = __shfl(unc ? 1 : 0, src, 64) != 0;
+        const long long g_i = __shfl(gmap, src, 64);
         const int c1 = (mine && m1[i] <= thr_i) ? 1 : 0;
         const int c2 = (mine && m2[i] <= thr_i) ? 1 : 0;
         int c3 = 0;
         bool v3;
+        // certified mode: a tracked value within 2 E of the edge; the
+        // candidates (tracked values <= edge + 2 E, in index order) and
+        // whether a lane's last tracked value is that low (list incomplete)
+        const float lim = thr_i + e2_i;
+        bool nr = fabsf(m1[i] - thr_i) <= e2_i || fabsf(m2[i] - thr_i) <= e2_i ||
+                  fabsf(m3[i] - thr_i) <= e2_i;
+        int cc = (m1[i] <= lim ? 1 : 0) + (m2[i] <= lim ? 1 : 0);
+        bool last_in;
         if constexpr (TOP == 3) {
           c3 = (mine && m3[i] <= thr_i) ? 1 : 0;
           v3 = mine && m4[i] <= thr_i;
+          nr = nr || fabsf(m4[i] - thr_i) <= e2_i;
+          cc += m3[i] <= lim ? 1 : 0;
+          last_in = m4[i] <= lim;
         } else {
           v3 = mine && m3[i] <= thr_i;
+          last_in = m3[i] <= lim;
         }
+        const bool row_unc =
+            cmax2_p && mine &&
+            (unc_i || ((__ballot(mine && nr) >> (32 * half)) & 0xFFFFFFFFull) != 0ull);
         const int cl = c1 + c2 + c3;
-        // inclusive prefix of member counts over the 32 lanes of this half
-        int incl = cl;
+        // inclusive prefixes of member / candidate counts over the 32 lanes
+        // of this half
+        int incl = cl, cinc = cc;
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) {
           const int v = __shfl_up(incl, o, 32);
-          if (r32 >= o) incl += v;
+          const int w = __shfl_up(cinc, o, 32);
+          if (r32 >= o) {
+            incl += v;
+            cinc += w;
+          }
+        }
+        const int ctot = __shfl(cinc, 32 * half + 31, 64);
+        const bool untr = ((__ballot(mine && last_in) >> (32 * half)) & 0xFFFFFFFFull) != 0ull;
+        // near the edge with a complete list of 2..kMaxCand candidates: fp64
+        // re-check of the candidates (multi list), otherwise overflow
+        const bool to_multi = row_unc && mrows && !untr && ctot >= 2 && ctot <= kMaxCand;
+        if (to_multi) {
+          int* mc = mcand + g_i * (kMaxCand + 1);
+          const int b0 = 1 + cinc - cc;
+          if (cc > 0) mc[b0] = i1[i];
+          if (cc > 1) mc[b0 + 1] = i2[i];
+          if constexpr (TOP == 3) {
+            if (cc > 2) mc[b0 + 2] = i3[i];
+          }
         }
         const int total = __shfl(incl, 32 * half + 31, 64);
         const bool ovf = ((__ballot(v3) >> (32 * half)) & 0xFFFFFFFFull) != 0ull;
@@ -385,11 +443,30 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         const int jsel = __shfl(myj, 32 * half + pl, 64);
         if (mine && r32 == 2 * i) {
           const long long g = gmap;
-          if (ovf) {
+          bool to_ovf = ovf;
+          if (row_unc) {
+            to_ovf = false;
+            if (to_multi) {
+              const long long slot = atomicAdd(multi_count, 1);
+              if (slot < mcap) {
+                mrows[slot] = g;
+                if (xflag) xflag[slot] = 1;
+                mcand[g * (kMaxCand + 1)] = ctot;
+                labels[g] = -1;
+              } else {
+                to_ovf = true;
+              }
+            } else if (ctot == 1 && !untr) {
+              labels[g] = qi;   // every other value certainly beyond the edge
+            } else {
+              to_ovf = true;
+            }
+          }
+          if (to_ovf) {
             const int slot = atomicAdd(ovf_count, 1);
             if (slot < ovf_cap) ovf_rows[slot] = g;
             labels[g] = -1;
-          } else {
+          } else if (!row_unc) {
             labels[g] = jsel;
           }
         }
@@ -441,7 +518,6 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
 // workgroup share each staged
 // tile; only the HI region of each operand tile is staged (34 KiB per slot at
 // d = 256).
-constexpr int kMaxCand = 16;
 // Gap record of a multi-candidate row whose band the fp32 screen (or the gap
 // screen) certified as {argmin} in iteration rec_it (csrc: recheck_fast_kernel,
 // gap_screen_kernel): the argmin's squared distance da, the gaps
@@ -2288,7 +2364,10 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
                             void* inertia, long long n, int k_pad, float alpha, float inv_a2,
                             float delta_s, RngKey key, long long row_offset, int ovf_cap,
                             hipStream_t st, const void* rlist = nullptr,
-                            const void* rcount = nullptr) {
+                            const void* rcount = nullptr, const void* cmax2 = nullptr,
+                            void* mrows = nullptr, void* mcand = nullptr,
+                            void* multi_count = nullptr, void* xflag = nullptr,
+                            long long mcap = 0) {
   constexpr int NW = 4;
   const size_t lds = 2 * (size_t)((2 * KSD + 1) * 2048);
   auto kern = estep_f32_kernel<KSD, TOP>;
@@ -2314,7 +2393,8 @@ static int launch_estep_f32(const void* X, const void* C, const void* xn, void* 
                      (const _Float16*)C, (const float*)xn, (int*)labels, (float*)mind,
                      (long long*)ovf_rows, (int*)ovf_count, (double*)part, n, k_pad, alpha, inv_a2,
                      delta_s, key, row_offset, ovf_cap, (const long long*)rlist,
-                     (const int*)rcount);
+                     (const int*)rcount, (const float*)cmax2, (long long*)mrows, (int*)mcand,
+                     (int*)multi_count, (unsigned char*)xflag, mcap);
   // per-wave inertia partials summed in a fixed order (bit-reproducible)
   if (!inertia) return (int)hipGetLastError();
   return sq_sum_partials(part, (int)grid * NW, inertia, st);
@@ -2327,7 +2407,8 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                             void* multi_count, void* corr, long long n, int k_pad, float alpha,
                             float delta_s, double delta, RngKey key, long long row_offset,
                             int dense_cap, hipStream_t st, const void* rlist, const void* rcount,
-                            void* ub, void* lb, void* mflag, void* xflag, int list_rs) {
+                            void* ub, void* lb, void* mflag, void* xflag, int list_rs,
+                            bool defer_rows = false) {
   // list mode (the rows the bounds could not prune): one row set per wave -
   // half the rows per workgroup, so a short list (the per-GPU share of a
   // strong-scaled run) finishes in one half-length sweep; a full sweep keeps
@@ -2424,11 +2505,14 @@ static int launch_estep_x64(const void* Xh, const void* X, const void* C, const 
                        sil, g_mrec.rec, g_mrec.mflag, g_mrec.it_now, key, row_offset,
                        (float*)corr);
   }
-  hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
-                     (const float*)X, (const float*)Cm, (const long long*)mrows,
-                     (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
-                     delta, key, row_offset, (float*)corr, (float*)ub,
-                     (const unsigned char*)xflag);
+  // (defer_rows: the caller launches it after the dense-row passes, which
+  // append their near-edge rows to the multi list)
+  if (!defer_rows)
+    hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,
+                       (const float*)X, (const float*)Cm, (const long long*)mrows,
+                       (const int*)mcand, (const int*)multi_count, (int*)labels, (float*)mind, n,
+                       delta, key, row_offset, (float*)corr, (float*)ub,
+                       (const unsigned char*)xflag);
   return (int)hipGetLastError();
 }
 
@@ -2500,6 +2584,8 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
   if (corr && !rlist) hipMemsetAsync(corr, 0, (size_t)n * sizeof(float), st);
   const int cap = (int)min(n, 2147483647LL);
   const unsigned fgrid = (unsigned)min((n + 15) / 16, 512LL);   // exact fp64 rows kernel
+  const long long rblocks = (n / 16 + 63) / 64;                  // fp64 re-check (as in launch_estep_x64)
+  const unsigned rgrid = (unsigned)(rblocks < 4096 ? (rblocks > 0 ? rblocks : 1) : 4096);
   int rc;
   switch (d_pad) {
     // d_pad <= 256: dense rows through the fp32-faithful 3-pass kernel (list
@@ -2509,24 +2595,31 @@ int sq_estep_x64(const void* Xh, const void* X, const void* C, const void* Cm, c
     rc = launch_estep_x64<KSD>(Xh, X, C, Cm, xn, cmax2, labels, mind, dense_rows, cnt + 1,       \
                                mrows, mcand, cnt + 2, corr, n, k_pad, fa, ds, delta, key,        \
                                row_offset, cap, st, rlist, rcount, ub, lb, mflag, xflag,         \
-                               list_rs);                                                         \
+                               list_rs, true);                                                   \
     if (rc) return rc;                                                                           \
     rc = launch_estep_f32<KSD>(X, C, xn, labels, mind, ovf_rows, cnt, part, part_cap, nullptr,   \
                                n, k_pad, fa, ia2, ds, key, row_offset, cap, st, dense_rows,       \
-                               cnt + 1);                                                         \
+                               cnt + 1, cmax2, mrows, mcand, cnt + 2, xflag, n);                 \
     if (rc) return rc;                                                                           \
     if (g_ovf2.rows) {                                                                           \
       /* the overflow rows once more with 3 members per lane; what still */                      \
       /* overflows goes to the fp64 rows kernel */                                               \
       rc = launch_estep_f32<KSD, 3>(X, C, xn, labels, mind, g_ovf2.rows, g_ovf2.count, part,     \
                                     part_cap, nullptr, n, k_pad, fa, ia2, ds, key, row_offset,   \
-                                    cap, st, ovf_rows, cnt);                                     \
+                                    cap, st, ovf_rows, cnt, cmax2, mrows, mcand, cnt + 2, xflag, \
+                                    n);                                                          \
       if (rc) return rc;                                                                         \
     }                                                                                            \
     if (corr)                                                                                    \
       hipLaunchKernelGGL(dense_corr_kernel, dim3(1024), dim3(256), 0, st, (const float*)X,       \
                          (const float*)Cm, (const long long*)dense_rows, (const int*)(cnt + 1),   \
                          (const int*)labels, (const float*)mind, (float*)corr, n, d_pad);        \
+    /* the fp64 re-check of the multi list, incl. the near-edge dense rows */                    \
+    hipLaunchKernelGGL(recheck_rows_kernel<KSD * 16>, dim3(rgrid), dim3(256), 0, st,            \
+                       (const float*)X, (const float*)Cm, (const long long*)mrows,               \
+                       (const int*)mcand, (const int*)(cnt + 2), (int*)labels, (float*)mind, n,  \
+                       delta, key, row_offset, (float*)corr, (float*)ub,                         \
+                       (const unsigned char*)xflag);                                             \
     rc = sq_rows_f64(X, d_pad, Cm, d_pad, d_pad, k, g_ovf2.rows ? g_ovf2.rows : ovf_rows,        \
                      g_ovf2.rows ? g_ovf2.count : cnt, 0, n, labels, mind, corr,                  \
                      ub, delta, k0, k1, s0, s1, row_offset, (int)fgrid, stream);                 \
