@@ -93,11 +93,14 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
   // no lane's last tracked value is that low) go to the multi list for the
   // fp64 re-check (recheck_rows_kernel, launched after this pass), else the
   // row overflows to the exact rows kernel.  E bounds |D'~ - alpha^2 D'|:
-  // the hi/lo split drops <= 3 2^-22 |x^| |c^| and the fp32 accumulation of
-  // the 3 (KSD + 1) x 16 products and norm pieces adds <= (3 DX + 48) 2^-24
-  // of the sum of their magnitudes <= 2 |x^| C + C^2 (C = max alpha ||c||).
+  // the hi/lo split drops <= 3 2^-22 |x^| |c^|; the fp32 accumulation of the
+  // DX hi.hi products and 16 norm pieces adds <= (DX + 16) 2^-24, the two
+  // cross-term accumulators (terms <= 2^-10 of them) <= 2 DX 2^-34 and the
+  // final sum 2^-24, of the sum of their magnitudes <= 2 |x^| C + C^2
+  // (C = max alpha ||c||).
   const float Cm = cmax2_p ? sqrtf(*cmax2_p) * (1.0f + 0x1p-16f) : 0.0f;
-  constexpr float kEps3 = (3.0f * 0x1p-22f + (3.0f * KSD * 16 + 48.0f) * 0x1p-24f) * 1.0625f;
+  constexpr float kEps3 =
+      (3.0f * 0x1p-22f + (KSD * 16 + 18.0f) * 0x1p-24f + 2.0f * KSD * 16 * 0x1p-34f) * 1.0625f;
   if (rlist) n = min(n, (long long)*rcount);
   auto map_row = [&](long long r) -> long long { return rlist ? rlist[r] : r; };
   constexpr int NW = 4;
@@ -197,7 +200,10 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
       ins(i, o1[i], j1);
     };
     if (do_mfma) {
-      f32x16 acc0 = {0}, acc1 = {0};
+      // the hi.hi products and the norm step in acc, the two cross terms
+      // (~2^-11 of them) in their own accumulators: the rounding error of the
+      // large partial sums comes from d_pad + 16 adds, not 3 d_pad + 48
+      f32x16 acc0 = {0}, acc1 = {0}, acl0 = {0}, acl1 = {0};
       const unsigned char* hb = cur + lane_off;
       const unsigned char* lb = cur + HI_BYTES + lane_off;
       f16x8 bh0[2], bh1[2], bl0[2], bl1[2];
@@ -216,10 +222,10 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         }
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh0[c], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh1[c], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl0[c], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl1[c], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh0[c], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh1[c], acc1, 0, 0, 0);
+        acl0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl0[c], acl0, 0, 0, 0);
+        acl1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl1[c], acl1, 0, 0, 0);
+        acl0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh0[c], acl0, 0, 0, 0);
+        acl1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh1[c], acl1, 0, 0, 0);
         if (do_epi) {
 #pragma unroll
           for (int i = (ks * 16) / KSD; i < ((ks + 1) * 16) / KSD; ++i) epi_row(i);
@@ -228,8 +234,8 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
       }
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aug, bh0[KSD & 1], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aug, bh1[KSD & 1], acc1, 0, 0, 0);
-      n0 = acc0;
-      n1 = acc1;
+      n0 = acc0 + acl0;
+      n1 = acc1 + acl1;
     } else if (do_epi) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) epi_row(i);
