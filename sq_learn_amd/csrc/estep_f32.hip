@@ -75,6 +75,9 @@ SQ_DEV float vmed3(float a, float b, float c) {
 // mode): three members per lane, a 4th -> overflow; its rows are loaded at
 // the block start instead of prefetched (the longer lists need the
 // registers).
+#ifndef SQ_SPLIT_ACC_ALL
+#define SQ_SPLIT_ACC_ALL 1   // 0: one accumulator in the two-member pass (measured slower overall)
+#endif
 template <int KSD, int TOP = 2>
 __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ C, const float* __restrict__ xn,
@@ -99,8 +102,16 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
   // final sum 2^-24, of the sum of their magnitudes <= 2 |x^| C + C^2
   // (C = max alpha ||c||).
   const float Cm = cmax2_p ? sqrtf(*cmax2_p) * (1.0f + 0x1p-16f) : 0.0f;
+  // (SPLIT_ACC: the cross terms in their own accumulators - the tighter
+  // bound.  The two-member pass then spills (its registers also hold the
+  // next block's prefetched rows: 1.10 vs 0.63 ms on the hard regime's 214K
+  // dense rows), but with one accumulator there its wider window sends more
+  // rows on: hard regime 6.33 vs 5.78 ms per step)
+  constexpr bool SPLIT_ACC = SQ_SPLIT_ACC_ALL || TOP == 3;
   constexpr float kEps3 =
-      (3.0f * 0x1p-22f + (KSD * 16 + 18.0f) * 0x1p-24f + 2.0f * KSD * 16 * 0x1p-34f) * 1.0625f;
+      SPLIT_ACC ? (3.0f * 0x1p-22f + (KSD * 16 + 18.0f) * 0x1p-24f + 2.0f * KSD * 16 * 0x1p-34f) *
+                      1.0625f
+                : (3.0f * 0x1p-22f + (3.0f * KSD * 16 + 48.0f) * 0x1p-24f) * 1.0625f;
   if (rlist) n = min(n, (long long)*rcount);
   auto map_row = [&](long long r) -> long long { return rlist ? rlist[r] : r; };
   constexpr int NW = 4;
@@ -222,10 +233,17 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
         }
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh0[c], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh1[c], acc1, 0, 0, 0);
-        acl0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl0[c], acl0, 0, 0, 0);
-        acl1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl1[c], acl1, 0, 0, 0);
-        acl0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh0[c], acl0, 0, 0, 0);
-        acl1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh1[c], acl1, 0, 0, 0);
+        if constexpr (SPLIT_ACC) {
+          acl0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl0[c], acl0, 0, 0, 0);
+          acl1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl1[c], acl1, 0, 0, 0);
+          acl0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh0[c], acl0, 0, 0, 0);
+          acl1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh1[c], acl1, 0, 0, 0);
+        } else {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl0[c], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl1[c], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh0[c], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh1[c], acc1, 0, 0, 0);
+        }
         if (do_epi) {
 #pragma unroll
           for (int i = (ks * 16) / KSD; i < ((ks + 1) * 16) / KSD; ++i) epi_row(i);
@@ -234,8 +252,13 @@ __global__ void __launch_bounds__(256, 1) estep_f32_kernel(
       }
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aug, bh0[KSD & 1], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(aug, bh1[KSD & 1], acc1, 0, 0, 0);
-      n0 = acc0 + acl0;
-      n1 = acc1 + acl1;
+      if constexpr (SPLIT_ACC) {
+        n0 = acc0 + acl0;
+        n1 = acc1 + acl1;
+      } else {
+        n0 = acc0;
+        n1 = acc1;
+      }
     } else if (do_epi) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) epi_row(i);
