@@ -367,7 +367,7 @@ class ForestRegressor(RegressorMixin, BaseForest):
         oob /= cnt
         self.oob_prediction_ = oob[:, 0] if self.n_outputs_ == 1 else oob
         from ...utils.metrics import r2_score
-        self.oob_score_ = r2_score(y.reshape(self.oob_prediction_.shape), self.oob_prediction_)
+        self.oob_score_ = r2_score(y, self.oob_prediction_)
 
 
 def _forest_init(self, n_estimators, criterion, max_depth, min_samples_split, min_samples_leaf,

@@ -19,15 +19,17 @@ def accuracy_score(y_true, y_pred, *, normalize=True, sample_weight=None):
     return float(score.mean()) if normalize else float(score.sum())
 
 
-def r2_score(y_true, y_pred, *, sample_weight=None):
-    y_true = np.asarray(to_numpy(y_true), dtype=np.float64)
-    y_pred = np.asarray(to_numpy(y_pred), dtype=np.float64)
-    w = np.ones_like(y_true) if sample_weight is None else np.asarray(sample_weight, dtype=np.float64)
-    num = (w * (y_true - y_pred) ** 2).sum()
-    den = (w * (y_true - np.average(y_true, weights=w)) ** 2).sum()
-    if den == 0:
-        return 1.0 if num == 0 else 0.0
-    return float(1 - num / den)
+def r2_score(y_true, y_pred, *, sample_weight=None, multioutput="uniform_average"):
+    """Coefficient of determination with the reference's target handling
+    (``/root/reference/sklearn/metrics/_regression.py`` ``r2_score``, used by
+    ``RegressorMixin.score`` at ``/root/reference/sklearn/base.py:564-566``):
+    1-D targets become one output column, so ``(n,)`` and ``(n, 1)`` agree;
+    per-output scores are combined by ``multioutput`` ('uniform_average' by
+    default, 'raw_values', 'variance_weighted' or an array of weights); a
+    constant output scores 1.0 when predicted exactly, else 0.0."""
+    from .metrics_extra import r2_score_ext
+    return r2_score_ext(to_numpy(y_true), to_numpy(y_pred), sample_weight=sample_weight,
+                        multioutput=multioutput)
 
 
 def confusion_matrix(y_true, y_pred, *, labels=None, sample_weight=None, normalize=None):

@@ -567,6 +567,9 @@ def _reg(y_true, y_pred):
         yt = yt.reshape(-1, 1)
     if yp.ndim == 1:
         yp = yp.reshape(-1, 1)
+    if yt.shape[0] != yp.shape[0]:
+        raise ValueError("Found input variables with inconsistent numbers of samples: "
+                         f"[{yt.shape[0]}, {yp.shape[0]}]")
     if yt.shape != yp.shape:
         raise ValueError("y_true and y_pred have different number of output ({0}!={1})"
                          .format(yt.shape[1], yp.shape[1]))
