@@ -87,6 +87,14 @@ struct MT19937 {
 extern "C" int sqh_mt_permutation_head(uint32_t* key, int* pos, long long n, long long k,
                                                 long long* out) {
   if (n < 0 || k < 0 || k > n || n >= (1LL << 31) || *pos < 0 || *pos > 624) return 1;
+  // the array on 2 MiB pages (transparent huge pages on request): the random
+  // a[j] accesses otherwise miss the TLB nearly every time.  Allocated before
+  // the generator starts, so a failed allocation leaves (key, pos) untouched.
+  const size_t huge = (size_t)2 << 20;
+  const size_t bytes = ((size_t)n * sizeof(int32_t) + huge - 1) & ~(huge - 1);
+  int32_t* a = static_cast<int32_t*>(std::aligned_alloc(huge, bytes > 0 ? bytes : huge));
+  if (!a) return 2;
+  madvise(a, bytes, MADV_HUGEPAGE);
   MT19937 g;
   g.key = key;
   g.pos = *pos;
@@ -112,16 +120,6 @@ extern "C" int sqh_mt_permutation_head(uint32_t* key, int* pos, long long n, lon
       produced.store(c + 1, std::memory_order_release);
     }
   });
-  // the array on 2 MiB pages (transparent huge pages on request): the random
-  // a[j] accesses otherwise miss the TLB nearly every time
-  const size_t huge = (size_t)2 << 20;
-  const size_t bytes = ((size_t)n * sizeof(int32_t) + huge - 1) & ~(huge - 1);
-  int32_t* a = static_cast<int32_t*>(std::aligned_alloc(huge, bytes > 0 ? bytes : huge));
-  if (!a) {
-    producer.join();
-    return 2;
-  }
-  madvise(a, bytes, MADV_HUGEPAGE);
   for (long long i = 0; i < n; ++i) a[(size_t)i] = (int32_t)i;
   constexpr int PF = 48;   // prefetch distance (swaps)
   for (long long c = 0; c < nchunks; ++c) {

@@ -144,6 +144,44 @@ struct CutParams {
   int d;
 };
 
+// The row's exact squared norm range [x2lo, x2hi] (fp32 |x|^2 with its
+// summation error) and the fp16 filter's error bound E on
+// v = alpha^2 (|c|^2 - 2 x.c) (estep_x64's per-row bound).
+struct RowErr {
+  double x2lo, x2hi, E;
+};
+SQ_DEV RowErr row_err(float nx2f, const CutParams& cp) {
+  const double u = 0x1p-24;
+  const double nx2 = nx2f;
+  RowErr r;
+  r.x2lo = nx2 * (1.0 - (cp.d + 2) * u);
+  r.x2hi = nx2 * (1.0 + (cp.d + 2) * u);
+  const double xsv = cp.alpha * sqrt(r.x2hi) * (1.0 + 0x1p-16);
+  r.E = (1.0625 * 0x1p-10 * xsv * cp.Ch + 0x1p-15 * (0.25 * cp.Ch * cp.Ch + xsv * cp.Ch) +
+         cp.sub_rel * (xsv + cp.Ch)) * (1.0 + 1e-6);
+  return r;
+}
+
+// fp64 -> fp32 rounded down / up (finite x)
+SQ_DEV float f32_dn(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = -f32_up(-f);
+  return f;
+}
+SQ_DEV float f32_upd(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = f32_up(f);
+  return f;
+}
+
+// Lower bound on sqrt(D) of a pair from its canonical fp32 inner product
+// (law D vs exact D within (3 d + 64) 2^-24 S, as in row_cut).
+SQ_DEV float pair_dist_lo(float ip, float nx2, float ny2, int d) {
+  const double S = (double)nx2 + (double)ny2;
+  const double D = S - 2.0 * (double)ip - (3.0 * d + 64.0) * 0x1p-24 * S * (1.0 + 1e-6);
+  return D > 0.0 ? f32_dn(sqrt(D) * (1.0 - 1e-12)) : 0.0f;
+}
+
 // The row's far band (see the header).  For a pair at law distance D with
 // S in [Smin, Smax] and ip = (S - D) / 2 (fp32 rounding folded in), the
 // screen's bin distance is m = (c sqrt(D) - sthr) kq sqrt(S) /
@@ -203,16 +241,11 @@ SQ_DEV Cut row_cut(float nx2f, float sthrf, float ktf, float Sminf, float Smaxf,
   if (!(m >= 3.0) || !(pu < 9.765625e-4 * (1.0 - 1e-6))) return out;  // c2, c3
   const double H = pu * (1.0 + pu) * (1.0 + 1e-6);                     // >= -log(1 - pu)
   // -> fp16 filter units: v = alpha^2 (D - |x|^2) +- E
-  const double u = 0x1p-24;
-  const double nx2 = nx2f;
-  const double errD = (3.0 * cp.d + 64.0) * u * Smax;                 // law D vs exact D
-  const double x2lo = nx2 * (1.0 - (cp.d + 2) * u), x2hi = nx2 * (1.0 + (cp.d + 2) * u);
-  const double xsv = cp.alpha * sqrt(x2hi) * (1.0 + 0x1p-16);
-  const double E = (1.0625 * 0x1p-10 * xsv * cp.Ch + 0x1p-15 * (0.25 * cp.Ch * cp.Ch + xsv * cp.Ch) +
-                    cp.sub_rel * (xsv + cp.Ch)) * (1.0 + 1e-6);
+  const double errD = (3.0 * cp.d + 64.0) * 0x1p-24 * Smax;           // law D vs exact D
+  const RowErr re = row_err(nx2f, cp);
   const double a2 = cp.alpha * cp.alpha;
-  const double vlo = a2 * (Dl + errD - x2lo) + E;
-  const double vhi = a2 * (Dh - errD - x2hi) - E;
+  const double vlo = a2 * (Dl + errD - re.x2lo) + re.E;
+  const double vhi = a2 * (Dh - errD - re.x2hi) - re.E;
   float flo = (float)vlo, fhi = (float)vhi, Hf = (float)H;
   if ((double)flo < vlo) flo = f32_up(flo);
   if ((double)fhi > vhi) fhi = -f32_up(-fhi);
@@ -231,6 +264,20 @@ SQ_DEV Cut row_cut(float nx2f, float sthrf, float ktf, float Sminf, float Smaxf,
 // ext_hj: the dense fallback reuses them), vlo / vhi / H, rM (min of the 32
 // stream budgets when it can run out within the row, else -1), rst (1: no
 // usable band or hint - dense), best (the hint's packed estimate).
+//
+// Row skip (lb given).  lb[r] is a lower bound on |x - c_j| for every
+// centroid j other than the row's label of the previous E-step (= this
+// step's hint), at that step's centres; moved by the largest centroid shift
+// since (Hamerly).  With ub = |x - c_hint| + max_j |c_hint - c_j| an upper
+// bound on every other distance, a row whose [lb^2, ub^2] lies inside
+// EVERY group's far band - with the fp16 filter's error E and the |x|^2
+// range folded in, i.e. where the sweep would provably classify every
+// non-hint pair far - needs no sweep: its only listed pairs would be its
+// fires (prep's own list, the hint's dropped).  Prep finishes such a row
+// itself: canonical fp32 dots of its fired pairs, the near kernel's
+// thinning of a fired far pair (same streams, same arithmetic), the packed
+// minimum -> labels / mind; so the labels are bit-identical with the skip
+// on or off.  Every other row goes to the sweep's row list.
 struct PrepArgs {
   const float* X;
   long long ldx;
@@ -257,13 +304,31 @@ struct PrepArgs {
   IpeScreen sc;
   CutParams cp;
   unsigned long long* stats;
+  // row skip / bound upkeep (lb == nullptr: off)
+  float* lb;                // [n] lower bound on sqrt(D) to every non-label centroid
+  int lb_ok;                // lb is relative to `hint` (the previous labels)
+  const float* smax;        // [1] largest centroid shift since lb's centres (rounded up)
+  const float* Rc;          // [k] max_j |c_l - c_j| (rounded up)
+  float* lbo;               // [n] x2lo - E / alpha^2: the sweep's v -> D lower bound
+  float* dhint;             // [n] lower bound on sqrt(D) of the hint pair
+  int* rows;                // rows left to the sweep (all of them when lb is off)
+  int* rows_count;
+  int* labels;              // skipped rows' results
+  float* mind;
+  unsigned char* rflag;     // skipped rows: 2 (finalize leaves them)
+  float* ea2;               // [n] E / alpha^2 (the sweep's pair certificate)
 };
 
 template <int KU>
 __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
+  constexpr int kWF = 64 * kFireCap;   // a wave's fired pairs of skipped rows
   __shared__ float sip[256];
   __shared__ int slab[256];
   __shared__ float red[2][4];
+  __shared__ uint32_t fpair[4][kWF];   // (lane << 16) | j
+  __shared__ float fip[4][kWF];
+  __shared__ unsigned long long sbest[256];
+  __shared__ float s_t[256], s_H[256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c16 = lane & 15, q4 = lane >> 4;
   // min / max of the centroid norms (S range of every pair of a row)
@@ -312,28 +377,35 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
   __syncthreads();
   const float cmin = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
   const float cmax = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  (void)cmin;
   const long long r = rb + lane;
-  uint32_t st_flag = 0, st_dense = 0;
+  uint32_t st_flag = 0, st_dense = 0, st_skip = 0, st_exact = 0;
   // C^ = 2 alpha max_j |c_j| of the fp16 filter's bound, from the largest
   // fp32 norm widened by its summation error
   CutParams cp = a.cp;
   cp.Ch = 2.0 * cp.alpha * sqrt((double)cmax * (1.0 + (cp.d + 2) * 0x1p-24)) * (1.0 + 0x1p-16);
+  const double a2 = cp.alpha * cp.alpha;
+  bool skip = false;
+  int nfs = 0;                 // fired pairs prep finishes itself (skipped rows)
+  uint16_t fire[kFireCap];
+  int l = -2;
+  float t = __builtin_inff();
+  float lbe_f = 0.0f, dh_lo = 0.0f;
+  long long g = 0;
   if (r < a.n) {
-    const int l = slab[threadIdx.x];
-    const long long g = a.row_offset + r;
+    l = slab[threadIdx.x];
+    g = a.row_offset + r;
     const float nx2 = a.xn[r];
-    float t = __builtin_inff();
     Cut cut{-__builtin_inff(), __builtin_inff(), 0.0f, 0};
-    uint16_t fire[kFireCap];
     int nf = 0;
     float glo[kMaxG], ghi[kMaxG];
+    int nok = 0;
     if (l >= 0) {
       t = ipe_distance(sip[threadIdx.x], (double)nx2, (double)a.cn[l], a.eps, a.Q, a.key,
                        (unsigned long long)g * (unsigned long long)a.k + (unsigned long long)l);
       const float sthr = ipe_sthr(t);
       // one band per centroid group (its own S range: the groups are
       // contiguous in |c|^2); a group without a band lists all its pairs
-      int any = 0;
       for (int q = 0; q < a.G; ++q) {
         const Cut cq = row_cut(nx2, sthr, ipe_kt(sthr), nx2 + a.gS[2 * q], nx2 + a.gS[2 * q + 1],
                                a.sc, cp);
@@ -343,11 +415,10 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
         ghi[q] = cq.ok ? cq.vhi : __builtin_inff();
         if (cq.ok) {
           cut = cq;   // H depends on m_t only: the same for every group
-          any = 1;
+          ++nok;
         }
       }
-      cut.ok = any;
-      a.best[r] = pack_best(t, a.tie, g, l);
+      cut.ok = nok > 0;
     }
     if (cut.ok) {
       // The row's 32 (column class) streams spend H per pair from iid Exp(1)
@@ -393,38 +464,211 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       st_flag = nf > 0 ? 1 : 0;
       if (nf > kFireCap) cut.ok = 0;   // a row this hot: dense
     }
-    if (!cut.ok) {
-      // dense: every pair "far" in the sweep (no list traffic), the whole
-      // row to the fp32 kernel
-      cut.vlo = -__builtin_inff();
-      cut.vhi = __builtin_inff();
-      st_dense = 1;
+    const RowErr re = row_err(nx2, cp);
+    a.ea2[r] = f32_upd(re.E / a2);
+    if (a.lb && l >= 0) {
+      const double S = (double)nx2 + (double)a.cn[l];
+      const double errH = (3.0 * cp.d + 64.0) * 0x1p-24 * S * (1.0 + 1e-6);
+      const double Dc = S - 2.0 * (double)sip[threadIdx.x];
+      dh_lo = Dc - errH > 0.0 ? f32_dn(sqrt(Dc - errH) * (1.0 - 1e-12)) : 0.0f;
+      if (a.lb_ok && cut.ok && nok == a.G) {
+        const double lbe = (double)a.lb[r] - (double)a.smax[0];
+        if (lbe > 0.0) {
+          // every non-hint pair provably far in the sweep: its exact D in
+          // [need_lo, need_hi] of its group puts v = alpha^2 (D - |x|^2) +- E
+          // inside [vlo, vhi]
+          double need_lo = -__builtin_inf(), need_hi = __builtin_inf();
+          for (int q = 0; q < a.G; ++q) {
+            need_lo = fmax(need_lo, ((double)glo[q] + re.E) / a2 + re.x2hi);
+            need_hi = fmin(need_hi, ((double)ghi[q] - re.E) / a2 + re.x2lo);
+          }
+          need_lo += 1e-12 * fabs(need_lo);
+          need_hi -= 1e-12 * fabs(need_hi);
+          const double ub = sqrt(fmax(Dc + errH, 0.0)) * (1.0 + 1e-12) + (double)a.Rc[l];
+          skip = lbe * lbe * (1.0 - 1e-12) >= need_lo && ub * ub * (1.0 + 1e-12) <= need_hi;
+          lbe_f = f32_dn(lbe);
+        }
+      }
+      if (!skip) a.lbo[r] = f32_dn(re.x2lo - re.E / a2);
+      if (!skip) a.dhint[r] = dh_lo;
     }
-    a.thr[r] = t;
-    a.hj[r] = l >= 0 ? l : -2;
-    for (int q = 0; q < a.G; ++q) {
-      a.vlo[r * kMaxG + q] = cut.ok ? glo[q] : -__builtin_inff();
-      a.vhi[r * kMaxG + q] = cut.ok ? ghi[q] : __builtin_inff();
+    if (skip) {
+      // the fires prep finishes: a fire on the hint is void
+      for (int e = 0; e < nf; ++e)
+        if ((fire[e] & 0x3FFF) != l) fire[nfs++] = fire[e];
+      st_skip = 1;
+      s_t[threadIdx.x] = t;
+      s_H[threadIdx.x] = cut.H;
+    } else {
+      if (!cut.ok) {
+        // dense: every pair "far" in the sweep (no list traffic), the whole
+        // row to the fp32 kernel
+        cut.vlo = -__builtin_inff();
+        cut.vhi = __builtin_inff();
+        st_dense = 1;
+      }
+      if (l >= 0) a.best[r] = pack_best(t, a.tie, g, l);
+      a.thr[r] = t;
+      a.hj[r] = l >= 0 ? l : -2;
+      for (int q = 0; q < a.G; ++q) {
+        a.vlo[r * kMaxG + q] = cut.ok ? glo[q] : -__builtin_inff();
+        a.vhi[r * kMaxG + q] = cut.ok ? ghi[q] : __builtin_inff();
+      }
+      a.H[r] = cut.H;
+      a.rst[r] = cut.ok ? 0 : 1;
+      uint16_t* fr = a.rfire + (size_t)r * 8;
+      const int nw = cut.ok ? nf : 0;
+      fr[0] = (uint16_t)nw;
+      for (int e = 0; e < nw; ++e) fr[1 + e] = fire[e];
     }
-    a.H[r] = cut.H;
-    a.rst[r] = cut.ok ? 0 : 1;
-    uint16_t* fr = a.rfire + (size_t)r * 8;
-    const int nw = cut.ok ? nf : 0;
-    fr[0] = (uint16_t)nw;
-    for (int e = 0; e < nw; ++e) fr[1 + e] = fire[e];
+  }
+  // the sweep's row list (one atomic per wave)
+  {
+    const bool lst = r < a.n && !skip;
+    const unsigned long long m = __ballot(lst);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(a.rows_count, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (lst) a.rows[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)r;
+  }
+  if (__ballot(skip) != 0ull) {
+    // the skipped rows' fired pairs: canonical dots 16 at a time (4 per
+    // 16-lane group, the rows' X just read), then one lane per pair
+    int incl = nfs;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int tot = __shfl(incl, 63, 64);
+    for (int e = 0; e < nfs; ++e) fpair[wave][incl - nfs + e] = ((uint32_t)lane << 16) | (fire[e] & 0x3FFFu);
+    if (skip) sbest[threadIdx.x] = pack_best(t, a.tie, g, l);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (int base = 0; base < tot; base += 16) {
+      const float* xp[B];
+      const float* cp_[B];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const int e = base + 4 * b + q4;
+        const uint32_t pr = e < tot ? fpair[wave][e] : fpair[wave][0];
+        xp[b] = a.X + (size_t)(rb + (pr >> 16)) * a.ldx;
+        cp_[b] = a.C + (size_t)(pr & 0xFFFFu) * a.d;
+      }
+      float sv[B];
+      canon_dot_batch<KU, B>(xp, cp_, a.d, c16, sv);
+      if (c16 == 0) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          const int e = base + 4 * b + q4;
+          if (e < tot) fip[wave][e] = sv[b];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ipe16_near_kernel's fired far pair, verbatim: the exact hazard, the
+    // thinning word of the stream's fire block, the exact branch
+    for (int e = lane; e < tot; e += 64) {
+      const uint32_t pr = fpair[wave][e];
+      const int ln = (int)(pr >> 16), j = (int)(pr & 0xFFFFu);
+      const long long rr = rb + ln;
+      const long long gg = a.row_offset + rr;
+      const float ip = fip[wave][e];
+      const float nx2 = a.xn[rr], ny2 = a.cn[j];
+      const float tt = s_t[wave * 64 + ln];
+      uint32_t hq = 0;
+      float pbar = 1.0f;
+      const bool ok = ipe_hazard(ip, nx2, ny2, ipe_sthr(tt), a.sc, hq, pbar);
+      const int h = (a.Q + 1) / 2;
+      const double pib = ok ? binom_upper_tail((double)pbar, a.Q, h) * (1.0 + 1e-12) : 1.0;
+      const double beff = -expm1(-(double)s_H[wave * 64 + ln]);
+      WordStream ws(a.skey, (unsigned long long)gg * 32ull + (unsigned long long)(j & 31));
+      ws.b = (uint32_t)(2 + 2 * (j >> 5));
+      (void)ws.next();
+      (void)ws.next();
+      const uint32_t w2 = ws.next(), w3 = ws.next();
+      const double u = u53(w2, w3) * beff;
+      if (u < pib) {
+        ++st_exact;
+        const float dt = ipe_pruned_exact((double)ip, (double)nx2 + (double)ny2, a.eps, a.Q, tt, u, ws);
+        if (dt < __builtin_inff()) atomicMin(&sbest[wave * 64 + ln], pack_best(dt, a.tie, gg, j));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (skip) {
+      const unsigned long long bb = sbest[threadIdx.x];
+      const int lab = (int)(bb & 0x3FFFu);
+      a.labels[r] = lab;
+      a.mind[r] = __uint_as_float((uint32_t)(bb >> 32));
+      a.rflag[r] = 2;
+      // the bound for the next step (relative to this label): the hint
+      // joins the non-label set when the label moved
+      a.lb[r] = lab == l ? lbe_f : fminf(lbe_f, dh_lo);
+    }
   }
   if (a.stats) {
-    uint32_t f = st_flag, dn = st_dense;
+    uint32_t f = st_flag, dn = st_dense, sk = st_skip, ex = st_exact;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       f += (uint32_t)__shfl_xor((int)f, o, 64);
       dn += (uint32_t)__shfl_xor((int)dn, o, 64);
+      sk += (uint32_t)__shfl_xor((int)sk, o, 64);
+      ex += (uint32_t)__shfl_xor((int)ex, o, 64);
     }
     if (lane == 0) {
       atomicAdd(a.stats + 4, (unsigned long long)f);
       atomicAdd(a.stats + 5, (unsigned long long)dn);
+      if (sk) atomicAdd(a.stats + 7, (unsigned long long)sk);
+      if (ex) atomicAdd(a.stats + 2, (unsigned long long)ex);
     }
   }
+}
+
+// ------------------------------------------------------------------ pair certificate
+// A pair the row's group band flags near may still be provably far: its own
+// S = |x|^2 + |c|^2 (not the group's range) and the inner-product interval
+// the fp16 value v = alpha^2 (|c|^2 - 2 x.c) +- E gives.  With ip_c the
+// canonical fp32 inner product (the law's), 2 ip_c lies in cv +- w,
+// cv = |c|^2 - v / alpha^2, w = (d + 2) u |c|^2 (fp32 |c|^2) + E / alpha^2
+// (fp16 filter) + d u S (canonical dot) + the fp32 roundings here; so the
+// law's D = S - 2 ip_c >= S - cv - w and ipe_hazard's bin distance
+// m >= (sqrt(D_lo) (1 - 2^-11) - sthr) sqrt(S) kq / max(1, |ip|_max).  When
+// that is >= m_t (the row's band hazard: pu(m) <= pu(m_t) <= 1 - exp(-H))
+// and a = D / 2S stays inside ipe_hazard's range over the whole interval,
+// the pair's P(D~ <= thr) is covered by its stream's budget exactly like a
+// band-far pair's: it is not listed (a fire on it stays a plain fired pair,
+// thinned with its exact hazard by the near kernel).
+struct CertParams {
+  float inv_a2;   // 1 / alpha^2 (a power of two)
+  float kq;       // IpeScreen::kq
+  float mt;       // m_t of the band hazard
+  float smax;     // IpeScreen::smax
+  float du;       // d 2^-24
+};
+
+SQ_DEV bool cert_far(float v, float ny2, float nx2, float sthr, float ea2, const CertParams& p) {
+  constexpr float u = 5.9604645e-8f;   // 2^-24
+  const float S = nx2 + ny2;
+  const float vs = v * p.inv_a2;
+  const float cv = ny2 - vs;
+  const float w = (p.du * (ny2 + S) + 2.0f * u * ny2 + ea2 + 4.0f * u * (fabsf(ny2) + fabsf(vs))) *
+                  1.001f;
+  const float Dlo = (S - cv - w) - 4.0f * u * (S + fabsf(cv) + w);
+  const float Dhi = (S - cv + w) + 4.0f * u * (S + fabsf(cv) + w);
+  const float aip = fmaxf(1.0f, 0.5f * (fabsf(cv) + w) * 1.0001f);
+  const float num = __builtin_sqrtf(fmaxf(Dlo, 0.0f)) * ((1.0f - 4.8828125e-4f) * (1.0f - 1e-5f)) - sthr;
+  const float m = num * __builtin_sqrtf(S) * p.kq * (1.0f - 1e-5f) / aip;
+  const float kt = 1.571f * sthr;
+  return (Dlo >= S * (2.44140625e-4f * 1.0001f)) & (Dhi <= S * (1.998046875f * 0.9999f)) &
+         (num > 0.0f) & (m >= p.mt * 1.0001f) &
+         (fmaf(kt, __builtin_sqrtf(S) * p.kq, 2.2f) <= 1048576.0f * 0.9999f) &
+         (S < p.smax * 0.9999f);
 }
 
 // ------------------------------------------------------------------ sweep
@@ -456,9 +700,24 @@ struct SweepArgs {
   int k, k_pad;
   long long row_offset;
   unsigned long long* stats;
+  // list mode (screen): the rows prep left to the sweep, positions [0, *rows_count)
+  const int* rows;
+  const int* rows_count;
+  // bound upkeep (screen, lb given): lb[r] <- sqrt of min over the row's far
+  // values v / alpha^2 + lbo[r] (a lower bound on D of every far pair); the
+  // near kernel folds in the listed pairs, finalize the hint
+  float* lb;
+  const float* lbo;
+  double inv_a2;
+  // the pair certificate of near-flagged pairs (cert_far)
+  const float* cns;         // [k_pad] fp32 |c|^2 (the law's) by operand column
+  const float* xn;          // [n] fp32 |x|^2
+  const float* thr;         // [n] the hint's estimate
+  const float* ea2;         // [n] E / alpha^2 (rounded up)
+  CertParams cert;
 };
 
-template <int KSD, bool ARGMIN>
+template <int KSD, bool ARGMIN, bool LB>
 __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   constexpr int KT = KSD + 1;                 // data k-steps + the norm step
   constexpr int SLOT = KT * 2048;
@@ -472,13 +731,19 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   int* ncnt = reinterpret_cast<int*>(nl + kRows * kNLS);                  // [kRows]
   int* shint = ncnt + kRows;                                              // [kRows]
   float* sband = reinterpret_cast<float*>(shint + kRows);                 // [kRows][G][2]
+  float* sfm = sband + kRows * kMaxG * 2;                                 // [kRows]
+  float* s_nx2 = sfm + kRows;                                             // [kRows]
+  float* s_sthr = s_nx2 + kRows;                                          // [kRows]
+  float* s_ea2 = s_sthr + kRows;                                          // [kRows]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31;
   const int half = lane >> 5;
-  const long long n = a.n;
+  // positions [0, n): rows 0.. n - 1, or list entries (screen in list mode)
+  const long long n = a.rows ? (long long)*a.rows_count : a.n;
+  auto R = [&](long long p) -> long long { return a.rows ? (long long)a.rows[p] : p; };
   const int n_tiles = a.k_pad / kTileN;
   const long long nblk = (n + kRows - 1) / kRows;
   long long blk = blockIdx.x;
@@ -512,7 +777,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
 #pragma unroll
     for (int st = 0; st < kRS; ++st) {
       long long r = row_of(b, st, r32);
-      r = r < n ? r : n - 1;
+      r = R(r < n ? r : n - 1);
       const _Float16* xr = a.Xh + (size_t)r * DX + half * 8;
 #pragma unroll
       for (int ks = 0; ks < KSD; ++ks) ah[st][ks] = *reinterpret_cast<const f16x8*>(xr + ks * 16);
@@ -527,6 +792,8 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   // per-lane state: the 16 rows' band edges per set (screen) / running
   // packed minima (argmin); the near bits of the last epilogue
   float lo[kRS][16], hi[kRS][16];
+  // (screen, LB) per register the minimum far value: the row's bound upkeep
+  float fm[kRS][LB ? 16 : 1];
   // near bits of the last epilogue (bit 16 st + i: register (st, i)); rows
   // whose list is full are muted (dense: no more pushes from this lane)
   uint32_t nb = 0, mute = 0;
@@ -538,6 +805,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     } else {
       const bool far = vmed3(v, lo[st][i], hi[st][i]) == v;
       nb |= far ? 0u : (1u << (16 * st + i));
+      if constexpr (LB) fm[st][i] = vmin(fm[st][i], far ? v : __builtin_inff());
     }
   };
   typedef f32x16 Acc[kRS];
@@ -566,21 +834,31 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   };
   // near pairs of the half-tile just screened (operand column jp): each lane
   // walks its set bits (the hint, co-located centroids, padding)
-  auto flush_near = [&](long long b, int jp) {
+  // (o: the accumulators of that half-tile, still live; jc / ny2: its
+  // lane column's centroid and |c|^2, loaded a tile ahead - a global load
+  // here would wait for the in-flight tile DMA as well)
+  auto flush_near = [&](long long b, int jc, float ny2, const Acc& o) {
     if constexpr (!ARGMIN) {
       nb &= ~mute;
       if (__ballot(nb != 0u) != 0ull) {
-        const int jc = jp < a.k ? a.perm[jp] : -1;
-        uint32_t m = nb;
-        while (m) {
-          const int bit = __builtin_ctz(m);
-          m &= m - 1u;
-          const int st = bit >> 4, i = bit & 15;
-          const int rb = (wave * kRS + st) * 32 + rl_of(i);
-          if (jc >= 0 && jc != shint[rb] && row_of(b, st, rl_of(i)) < n) {
-            const int s = atomicAdd(&ncnt[rb], 1);
-            if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)(jc | 0x4000);
-            else mute |= 1u << bit;   // the row is dense
+#pragma unroll
+        for (int st = 0; st < kRS; ++st) {
+          uint32_t m = (nb >> (16 * st)) & 0xFFFFu;
+          while (m) {
+            const int i = __builtin_ctz(m);
+            m &= m - 1u;
+            const int rb = (wave * kRS + st) * 32 + rl_of(i);
+            if (jc >= 0 && jc != shint[rb] && row_of(b, st, rl_of(i)) < n) {
+              // the flagged value: a branch-free select of register i
+              float v = o[st][0];
+#pragma unroll
+              for (int e = 1; e < 16; ++e) v = i == e ? o[st][e] : v;
+              if (!cert_far(v, ny2, s_nx2[rb], s_sthr[rb], s_ea2[rb], a.cert)) {
+                const int s = atomicAdd(&ncnt[rb], 1);
+                if (s < kCapR) nl[rb * kNLS + s] = (uint16_t)(jc | 0x4000);
+                else mute |= 1u << (16 * st + i);   // the row is dense
+              }
+            }
           }
         }
       }
@@ -619,12 +897,22 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
         for (int i = 0; i < 16; ++i) lo[st][i] = __builtin_inff();
     } else {
       mute = 0;
+      if constexpr (LB) {
+#pragma unroll
+        for (int st = 0; st < kRS; ++st)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) fm[st][i] = __builtin_inff();
+      }
       // the rows' hints and the fires prep listed (thread t: row t)
       for (int t = tid; t < kRows; t += kNW * 64) {
-        const long long r = blk * kRows + t;
+        const long long p = blk * kRows + t;
         int c = 0;
-        if (r < n) {
+        if (p < n) {
+          const long long r = R(p);
           shint[t] = a.hj[r];
+          s_nx2[t] = a.xn[r];
+          s_sthr[t] = ipe_sthr(a.thr[r]);
+          s_ea2[t] = a.ea2[r];
           const uint16_t* fr = a.rfire + (size_t)r * 8;
           c = fr[0];
           for (int e = 0; e < c; ++e) nl[t * kNLS + e] = fr[1 + e];
@@ -635,10 +923,11 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       }
       // the block's bands (row, group) -> LDS; a row past n: all far
       for (int e = tid; e < kRows * kMaxG; e += kNW * 64) {
-        const long long r = blk * kRows + e / kMaxG;
-        const bool v = r < n && (e % kMaxG) < a.G;
-        sband[2 * e] = v ? a.vlo[blk * kRows * kMaxG + e] : -__builtin_inff();
-        sband[2 * e + 1] = v ? a.vhi[blk * kRows * kMaxG + e] : __builtin_inff();
+        const long long p = blk * kRows + e / kMaxG;
+        const bool v = p < n && (e % kMaxG) < a.G;
+        const long long idx = v ? R(p) * kMaxG + e % kMaxG : 0;
+        sband[2 * e] = v ? a.vlo[idx] : -__builtin_inff();
+        sband[2 * e + 1] = v ? a.vhi[idx] : __builtin_inff();
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -647,25 +936,37 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     // ---- the sweep: half 0 of tile t (epilogue of tile t - 1's half 1),
     // half 1 (epilogue of half 0), one ring slot per tile
     f32x16 cA[kRS], cB[kRS];
+    // the lane columns' centroids / norms of the two flushes of a tile
+    auto colc = [&](int jp, int& jc, float& ny2) {
+      if constexpr (!ARGMIN) {
+        jc = jp < a.k ? a.perm[jp] : -1;
+        ny2 = a.cns[jp];
+      }
+    };
+    int jcA = -1, jcB = -1;
+    float nyA = 0.0f, nyB = 0.0f;
     for (int t = 0; t < n_tiles; ++t) {
+      if (t > 0) colc(64 * (t - 1) + 32 + r32, jcA, nyA);
+      colc(64 * t + r32, jcB, nyB);
       stage(U + kRing - 1);
 #pragma unroll
       for (int j = 0; j < PFD; ++j) bq[j] = frag(buf(U), j);
       pass(std::integral_constant<int, 0>{}, buf(U), cA, cB, (uint32_t)(2 * t - 1), t > 0);
-      flush_near(blk, 64 * (t - 1) + 32 + r32);
+      flush_near(blk, jcA, nyA, cB);
       // tile t's values (epilogues from the next pass on) use its group's bands
       if (t > 0 && group_of(t) != group_of(t - 1)) load_bands(group_of(t));
       pass(std::integral_constant<int, 1>{}, buf(U), cB, cA, (uint32_t)(2 * t), true);
-      flush_near(blk, 64 * t + r32);
+      flush_near(blk, jcB, nyB, cA);
       sync_tile();
       ++U;
     }
+    colc(64 * (n_tiles - 1) + 32 + r32, jcA, nyA);
     load_a(blk + gridDim.x);   // clamped rows: unconditional
 #pragma unroll
     for (int st = 0; st < kRS; ++st)
 #pragma unroll
       for (int i = 0; i < 16; ++i) epi(st, i, cB[st][i], (uint32_t)(2 * n_tiles - 1));
-    flush_near(blk, 64 * (n_tiles - 1) + 32 + r32);
+    flush_near(blk, jcA, nyA, cB);
 
     if constexpr (ARGMIN) {
       // row minimum over the 32 lanes of each half: the packed value holds
@@ -688,17 +989,30 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
           }
         }
     } else {
+      // the rows' minimum far values (over the 32 columns of a half)
+      if constexpr (LB) {
+#pragma unroll
+        for (int st = 0; st < kRS; ++st)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float v = fm[st][i];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) v = vmin(v, __shfl_xor(v, o, 64));
+            if (r32 == i) sfm[(wave * kRS + st) * 32 + rl_of(i)] = v;
+          }
+      }
       // ---- flush the block's lists: dedupe fires against near pairs and the
       // hint, dense rows to the fallback list, the rest compacted to the
       // global pair list (one atomic per wave)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       const int t = tid;   // kRows == 256 threads: one row each
-      const long long r = blk * kRows + t;
+      const long long p = blk * kRows + t;
+      const long long r = p < n ? R(p) : 0;
       int c = 0;
       bool dense = false;
       uint16_t* row_l = nl + t * kNLS;
-      if (r < n) {
+      if (p < n) {
         c = ncnt[t];
         dense = c > kCapR || a.rst[r] != 0;
         if (dense) {
@@ -726,6 +1040,17 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
           c = w;
         }
         a.rflag[r] = dense ? 1 : 0;
+        if (LB && a.lb) {
+          // far pairs: exact D >= v / alpha^2 + x2lo - E / alpha^2 (lbo);
+          // a dense row (fallback) keeps no bound
+          const float fmv = sfm[t];
+          float lbv = 0.0f;
+          if (!dense) {
+            const double D = (double)fmv * a.inv_a2 + (double)a.lbo[r];
+            lbv = fmv == __builtin_inff() ? fmv : (D > 0.0 ? f32_dn(sqrt(D) * (1.0 - 1e-12)) : 0.0f);
+          }
+          a.lb[r] = lbv;
+        }
       }
       // wave scan of the counts
       int incl = c;
@@ -738,7 +1063,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       int base = 0;
       if (lane == 63 && wtot > 0) base = atomicAdd(a.list_count, wtot);
       base = __shfl(base, 63, 64);
-      const unsigned long long rr = (unsigned long long)(r < n ? r : 0) << 16;
+      const unsigned long long rr = (unsigned long long)r << 16;
       for (int e = 0; e < c; ++e) a.list[base + incl - c + e] = rr | (unsigned long long)row_l[e];
       const unsigned long long dm = __ballot(dense);
       if (dm) {
@@ -791,6 +1116,7 @@ struct NearArgs {
   long long row_offset;
   IpeScreen sc;
   unsigned long long* stats;
+  float* lb;                // bound upkeep: every listed pair is a non-hint pair
 };
 
 template <int KU>
@@ -842,6 +1168,8 @@ __global__ void __launch_bounds__(256) ipe16_near_kernel(NearArgs a) {
       const float nx2 = a.xn[r], ny2 = a.cn[j];
       const float t = a.thr[r];
       float dt = __builtin_inff();
+      if (a.lb) atomicMin(reinterpret_cast<unsigned int*>(a.lb + r),
+                          __float_as_uint(pair_dist_lo(ip, nx2, ny2, a.d)));
       // the pair's exact hazard (canonical inner product): a near pair the
       // row's band could not certify may still be far - ipe_hazard passes and
       // its bound P(D~ <= thr) <= pibar <= 1 - exp(-H_row) - and then it is a
@@ -885,15 +1213,20 @@ __global__ void __launch_bounds__(256) ipe16_near_kernel(NearArgs a) {
 }
 
 // labels / mind of the rows the screen resolved (dense rows: the fallback)
+// (skipped rows: prep's own; lb given: a row whose label left its hint
+// adds the hint pair to its non-label bound)
 __global__ void __launch_bounds__(256) ipe16_finalize_kernel(const unsigned long long* best,
                                                             const unsigned char* rflag,
                                                             int* labels, float* mind,
-                                                            long long n) {
+                                                            long long n, const int* hj, float* lb,
+                                                            const float* dhint) {
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r >= n || rflag[r]) return;
   const unsigned long long b = best[r];
-  labels[r] = (int)(b & 0x3FFFu);
+  const int lab = (int)(b & 0x3FFFu);
+  labels[r] = lab;
   mind[r] = __uint_as_float((uint32_t)(b >> 32));
+  if (lb && lab != hj[r]) lb[r] = fminf(lb[r], dhint[r]);
 }
 
 }  // namespace i16
@@ -902,12 +1235,12 @@ __global__ void __launch_bounds__(256) ipe16_finalize_kernel(const unsigned long
 using namespace sq;
 using namespace sq::i16;
 
-template <int KSD, bool ARGMIN>
+template <int KSD, bool ARGMIN, bool LB>
 static int launch_sweep(const SweepArgs& a, hipStream_t st) {
   constexpr int SLOT = (KSD + 1) * 2048;
   const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 2 * kRows * 4 +
-                     (size_t)kRows * kMaxG * 2 * 4;
-  auto kern = ipe16_sweep_kernel<KSD, ARGMIN>;
+                     (size_t)kRows * kMaxG * 2 * 4 + (size_t)kRows * 4 * 4;
+  auto kern = ipe16_sweep_kernel<KSD, ARGMIN, LB>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -957,7 +1290,10 @@ extern "C" {
 //   [22] labels, [23] mind, [24] stats, [25] n, [26] d, [27] d_pad, [28] k,
 //   [29] k_pad, [30] Q, [31] row_offset, [32..35] key, [36..39] tie,
 //   [40..43] skey, [44..47] bkey, [48] perm (operand column -> centroid),
-//   [49] group |c|^2 ranges [G][2], [50] G
+//   [49] group |c|^2 ranges [G][2], [50] G, [51] lb (0: no row skip / bound
+//   upkeep), [52] lb valid (skip allowed), [53] smax [1], [54] Rc [k],
+//   [55] lbo, [56] dhint, [57] sweep rows, [58] sweep row count, [59] ea2,
+//   [60] |c|^2 by operand column [k_pad]
 // da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
 int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -1009,6 +1345,20 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.cp.min_width = da[3];
     a.cp.d = d;
     a.stats = (unsigned long long*)P(24);
+    a.lb = (float*)P(51);
+    a.lb_ok = (int)ia[52];
+    a.smax = (const float*)P(53);
+    a.Rc = (const float*)P(54);
+    a.lbo = (float*)P(55);
+    a.dhint = (float*)P(56);
+    a.rows = (int*)P(57);
+    a.rows_count = (int*)P(58);
+    a.labels = (int*)P(22);
+    a.mind = (float*)P(23);
+    a.rflag = (unsigned char*)P(21);
+    a.ea2 = (float*)P(59);
+    if (!a.ea2 || !a.rows || !a.rows_count || (a.lb && (!a.lbo || !a.dhint || (a.lb_ok && (!a.smax || !a.Rc)))))
+      return (int)hipErrorInvalidValue;
     const dim3 pg((unsigned)((n + 255) / 256));
     switch (d_pad) {
 #define CASE(KSD)                                                               \
@@ -1044,10 +1394,28 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.row_offset = ia[31];
     a.stats = (unsigned long long*)P(24);
     const bool am = op == 1;
+    // the argmin sweep (hints) runs over all rows; the screen over prep's list
+    a.rows = am ? nullptr : (const int*)P(57);
+    a.rows_count = am ? nullptr : (const int*)P(58);
+    a.lb = am ? nullptr : (float*)P(51);
+    a.lbo = (const float*)P(55);
+    a.inv_a2 = 1.0 / (da[1] * da[1]);
+    a.cns = (const float*)P(60);
+    a.xn = (const float*)P(7);
+    a.thr = (const float*)P(9);
+    a.ea2 = (const float*)P(59);
+    a.cert.inv_a2 = (float)a.inv_a2;
+    a.cert.kq = sc.kq;
+    a.cert.mt = (float)da[2];
+    a.cert.smax = sc.smax;
+    a.cert.du = (float)d * 0x1p-24f;
+    if (!am && (!a.rows || !a.ea2 || !a.cns || (double)a.cert.inv_a2 != a.inv_a2))
+      return (int)hipErrorInvalidValue;
     switch (d_pad) {
 #define CASE(KSD)                                                                  \
   case KSD * 16:                                                                   \
-    return am ? launch_sweep<KSD, true>(a, st) : launch_sweep<KSD, false>(a, st);
+    return am ? launch_sweep<KSD, true, false>(a, st)                                \
+              : (a.lb ? (int)hipErrorNotSupported : launch_sweep<KSD, false, false>(a, st));
       CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
 #undef CASE
       default:
@@ -1076,6 +1444,7 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.row_offset = ia[31];
     a.sc = sc;
     a.stats = (unsigned long long*)P(24);
+    a.lb = (float*)P(51);
     static int grid = 0;
     if (grid == 0) {
       int dev = 0, cus = 0;
@@ -1097,7 +1466,7 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   if (op == 4) {
     hipLaunchKernelGGL(ipe16_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                        (const unsigned long long*)P(16), (const unsigned char*)P(21), (int*)P(22),
-                       (float*)P(23), n);
+                       (float*)P(23), n, (const int*)P(10), (float*)P(51), (const float*)P(56));
     return (int)hipGetLastError();
   }
   return (int)hipErrorInvalidValue;

@@ -374,6 +374,8 @@ class LloydEngine:
         self._ipe_buffers()
         self._ipe_lab[self._ipe_cur].copy_(t.to(self.device).to(torch.int32))
         self._ipe_hint_valid = bool((t >= 0).all())
+        if getattr(self, "_ipe16", None) is not None:
+            self._ipe16.invalidate_bounds()   # restored hints: no skip until a full sweep
 
     def _ipe_buffers(self):
         if getattr(self, "_ipe_lab", None) is None:
@@ -452,49 +454,56 @@ class LloydEngine:
                     K.multi_records(self.mrec, self.buf.mflag, self._rit,
                                     max(self._rlo, self._rit - R + 1), self.dsh, self.dq,
                                     self.rows_b, self.buf.counts[5:6], self.buf.counts[4:5])
-                # a probe (the filter kept > keep_max of the rows twice and was
-                # skipped since) only MEASURES: the filter pass counts the rows
-                # it would keep (the M-step records the fraction), the sweep
-                # stays full and maintains the bounds - a probe costs one
-                # filter pass, not a near-full list sweep
-                probe = mode == "filter" and self._probing
-                zero = True
-                if mode == "filter":
-                    self._filter_ran = True
-                    K.ensure_multi_buffers(self.buf, self.n, self.device, True)
-                    # one fill clears the E-step counters and the kept count
-                    self.rcount = self.buf.counts[3:4]
-                    self.buf.counts.zero_()
-                    K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
-                                           self.shift_s, self.smax, self.delta, self.rlist,
-                                           self.rcount, self.buf, cc=self.fast_cc,
-                                           nf=self.n_fast, fidx=self.fast_idx)
-                    if probe:
-                        # the full sweep lists from scratch (list B too)
-                        self.buf.counts[:3].zero_()
-                        self.buf.counts[5:6].zero_()
-                    else:
-                        rows = (self.rlist, self.rcount)
-                        # disjoint: unpruned rows, the filter's multi rows
-                        # (the multi list's head), list B
-                        self._dlists = ((self.rlist, self.rcount),
-                                        (self.buf.multi_rows, self.buf.counts[7:8]),
-                                        (self.rows_b, self.buf.counts[5:6])
-                                        if self.mrec is not None and screen else None)
-                    zero = False
-                lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
-                                               self.cmax2, self.k, self.delta, self.alpha, key,
-                                               self.row_offset, self.buf,
-                                               bounds=(self.ub, self.lb)
-                                               if self.bounds and self._bounds_kept else None,
-                                               rows=rows, zero_counts=zero, screen=screen,
-                                               list_rs=self._list_rs())
-                if self.mrec is not None:
-                    K.multi_records(None)   # thread-local: never leak into another engine
-                    if not screen:
-                        # the sweep rewrote candidate lists the screen did not
-                        # re-record: every record so far is void
-                        self._records_epoch()
+                else:
+                    # thread-local: a previous engine's records never leak in
+                    K.multi_records(None)
+                try:
+                    # a probe (the filter kept > keep_max of the rows twice and was
+                    # skipped since) only MEASURES: the filter pass counts the rows
+                    # it would keep (the M-step records the fraction), the sweep
+                    # stays full and maintains the bounds - a probe costs one
+                    # filter pass, not a near-full list sweep
+                    probe = mode == "filter" and self._probing
+                    zero = True
+                    if mode == "filter":
+                        self._filter_ran = True
+                        K.ensure_multi_buffers(self.buf, self.n, self.device, True)
+                        # one fill clears the E-step counters and the kept count
+                        self.rcount = self.buf.counts[3:4]
+                        self.buf.counts.zero_()
+                        K.bounds_filter_native(self.buf.labels[:self.n], self.ub, self.lb,
+                                               self.shift_s, self.smax, self.delta, self.rlist,
+                                               self.rcount, self.buf, cc=self.fast_cc,
+                                               nf=self.n_fast, fidx=self.fast_idx)
+                        if probe:
+                            # the full sweep lists from scratch (list B too)
+                            self.buf.counts[:3].zero_()
+                            self.buf.counts[5:6].zero_()
+                        else:
+                            rows = (self.rlist, self.rcount)
+                            # disjoint: unpruned rows, the filter's multi rows
+                            # (the multi list's head), list B
+                            self._dlists = ((self.rlist, self.rcount),
+                                            (self.buf.multi_rows, self.buf.counts[7:8]),
+                                            (self.rows_b, self.buf.counts[5:6])
+                                            if self.mrec is not None and screen else None)
+                        zero = False
+                    lab, mind = K.estep_x64_native(self.Xh16, self.Xf32, self.C_op, Cp, self.xn,
+                                                   self.cmax2, self.k, self.delta, self.alpha, key,
+                                                   self.row_offset, self.buf,
+                                                   bounds=(self.ub, self.lb)
+                                                   if self.bounds and self._bounds_kept else None,
+                                                   rows=rows, zero_counts=zero, screen=screen,
+                                                   list_rs=self._list_rs())
+                finally:
+                    if self.mrec is not None:
+                        # thread-local: never leak into another engine, even
+                        # when the native E-step raised
+                        K.multi_records(None)
+                if self.mrec is not None and not screen:
+                    # the sweep rewrote candidate lists the screen did not
+                    # re-record: every record so far is void
+                    self._records_epoch()
             return lab, mind, self.buf.inertia
         if self.fast and self.C_op is not None:
             with tracing.range("estep_f32"):
@@ -985,6 +994,8 @@ class LloydEngine:
             labels[li] = newlab.to(labels.dtype)
             if getattr(self, "bounds", False):
                 self.lb[li] = 0.0   # label moved: re-evaluate next E-step
+            if getattr(self, "_ipe16", None) is not None:
+                self._ipe16.lb[li] = 0.0   # the IPE row skip's bound too
         self.n_relocated += e
         return labels
 

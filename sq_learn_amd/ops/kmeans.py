@@ -1095,9 +1095,24 @@ class Ipe16:
         cm = min(n, IPE16_CHUNK)
         self.list = torch.empty(max(cm * IPE16_CAPR, 1), dtype=torch.int64, device=dev)
         self.nchunks = max(1, -(-n // IPE16_CHUNK))
-        # per chunk: [list count, dense count]
-        self.counts = torch.zeros((self.nchunks, 2), dtype=torch.int32, device=dev)
-        self.counts_host = torch.zeros((self.nchunks, 2), dtype=torch.int32, pin_memory=True)
+        # per chunk: [list count, dense count, sweep row count]
+        self.counts = torch.zeros((self.nchunks, 3), dtype=torch.int32, device=dev)
+        self.counts_host = torch.zeros((self.nchunks, 3), dtype=torch.int32, pin_memory=True)
+        # row skip (csrc/ipe16.hip prep): per-row lower bound on the distance
+        # to every non-label centroid, kept across E-steps (valid while the
+        # hints are the previous E-step's labels), the bound's conversion
+        # offset and the hint pair's distance bound, the sweep's row list
+        self.lb = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        self.lbo = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.dhint = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        self.ea2 = torch.empty(max(n, 1), dtype=torch.float32, device=dev)   # E / alpha^2
+        self.rows = torch.empty(max(cm, 1), dtype=torch.int32, device=dev)
+        self.smax = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.Rc = torch.zeros(max(int(k), 1), dtype=torch.float32, device=dev)
+        self.C_prev = None
+        self.lb_valid = False
+        # (off: the sweep's bound upkeep does not fit its register budget yet)
+        self.skip = __import__("os").environ.get("SQ_IPE16_SKIP", "0") == "1"
         self.ev = torch.cuda.Event()
         # per-pair hazard of the far band (the band edge's worst case): the
         # row fires somewhere with probability ~ k * ht; a larger ht narrows
@@ -1110,8 +1125,14 @@ class Ipe16:
         self.last_dense = 0
 
     def relaunch(self, op):
-        """Re-run one phase of the last E-step's last chunk (kernel timing)."""
+        """Re-run one phase of the last E-step's last chunk (kernel timing;
+        prep re-lists the sweep rows from scratch, the screen sweep re-lists
+        its pairs, so their counters restart)."""
         ia, da, st = self._last_args
+        if op == 0:
+            self.counts[-1, 2].zero_()
+        if op == 2:
+            self.counts[-1, :2].zero_()
         return nat.native().ipe16(op, ia.data_ptr(), da.data_ptr(), st)
 
     @staticmethod
@@ -1141,6 +1162,26 @@ class Ipe16:
                 lo = mid
         return hi
 
+    def invalidate_bounds(self):
+        """The hints no longer are the labels the bounds were kept for
+        (new centres, restored hints): no row skip until a full sweep."""
+        self.lb_valid = False
+
+    def _skip_bounds(self, C32):
+        """Device scalars of the row skip for centres C32 (fp32, the E-step's):
+        smax = max_j |c_j - c_j(prev)| since the last E-step's centres and
+        Rc[a] = max_j |c_a - c_j|, both fp64 then rounded up to fp32."""
+        C64 = C32.double()
+        inf = torch.tensor(float("inf"), device=C32.device)
+        if self.C_prev is not None and self.C_prev.shape == C32.shape:
+            sh = (C64 - self.C_prev.double()).pow(2).sum(1).max().sqrt() * (1.0 + 1e-9)
+            self.smax.copy_(torch.nextafter(sh.float(), inf).reshape(1))
+        nrm = (C64 * C64).sum(1)
+        D2 = (nrm[:, None] + nrm[None, :] - 2.0 * (C64 @ C64.T)).amax(1).clamp_min(0.0)
+        R = (D2 + 2e-12 * nrm.max()).sqrt() * (1.0 + 1e-9)
+        self.Rc[:C32.shape[0]].copy_(torch.nextafter(R.float(), inf))
+        self.C_prev = C32.clone()
+
     def set_centers(self, C32, cn=None):
         """The fp16 operand of the centroids SORTED by |c|^2 (``perm``: operand
         column -> centroid id): its tiles fall into G groups of contiguous
@@ -1155,6 +1196,9 @@ class Ipe16:
         Cs = C32.index_select(0, order).contiguous()
         centers_to_f16_native(Cs, self.C_op, self.k, self.d, self.d_pad, self.k_pad, self.alpha)
         cs = cn.index_select(0, order)
+        # the law's |c|^2 by operand column (the sweep's pair certificate)
+        self.cns = torch.zeros(self.k_pad, dtype=torch.float32, device=cn.device)
+        self.cns[:self.k].copy_(cs.float())
         lo_t = [(q * nt) // G for q in range(G)]
         hi_t = [((q + 1) * nt) // G for q in range(G)]
         first = torch.tensor([min(64 * t, self.k - 1) for t in lo_t], device=cn.device)
@@ -1173,8 +1217,14 @@ class Ipe16:
             return
         m = nat.native()
         st = nat.stream_handle(X.device)
-        ia = torch.zeros(56, dtype=torch.int64)
+        if first:
+            self.lb_valid = False
+        skip = self.skip
+        if skip:
+            self._skip_bounds(C32)
+        ia = torch.zeros(64, dtype=torch.int64)
         ia[48] = self.perm.data_ptr()
+        ia[60] = self.cns.data_ptr()
         ia[49] = self.gS.data_ptr()
         ia[50] = self.G
         da = torch.tensor([float(eps), self.alpha, self.band_m(int(Q), min(self.ht, 9.0e-4)),
@@ -1185,6 +1235,9 @@ class Ipe16:
         ia[4] = self.C_op.data_ptr()
         ia[8] = cn.data_ptr()
         ia[24] = 0 if stats is None else stats.data_ptr()
+        ia[52] = 1 if (skip and self.lb_valid) else 0
+        ia[53] = self.smax.data_ptr()
+        ia[54] = self.Rc.data_ptr()
         ia[26], ia[27], ia[28], ia[29], ia[30] = self.d, self.d_pad, self.k, self.k_pad, int(Q)
         for i, kk in ((32, key), (36, tie), (40, skey), (44, bkey)):
             ia[i], ia[i + 1], ia[i + 2], ia[i + 3] = kk.k0, kk.k1, kk.s0, kk.s1
@@ -1205,11 +1258,16 @@ class Ipe16:
             ia[7] = xn.data_ptr() + s * 4
             for i, t in ((9, self.thr), (10, self.hj), (11, self.vlo), (12, self.vhi),
                          (13, self.H), (14, self.rfire), (15, self.rst), (16, self.best),
-                         (19, self.dense_rows), (21, self.rflag), (22, labels), (23, mind)):
+                         (19, self.dense_rows), (21, self.rflag), (22, labels), (23, mind),
+                         (51, self.lb), (55, self.lbo), (56, self.dhint), (59, self.ea2)):
                 ia[i] = t.data_ptr() + s * t.stride(0) * t.element_size()
+            if not skip:
+                ia[51] = 0
             ia[17] = self.list.data_ptr()
             ia[18] = self.counts[c].data_ptr()
             ia[20] = self.counts[c].data_ptr() + 4
+            ia[57] = self.rows.data_ptr()
+            ia[58] = self.counts[c].data_ptr() + 8
             ia[25] = e - s
             ia[31] = int(row_offset) + s
             if first:
@@ -1221,6 +1279,8 @@ class Ipe16:
                 self.ev.record()
             run(3)
             run(4)
+        # the bounds now hold for these labels (the next E-step's hints)
+        self.lb_valid = skip
         self._last_args = (ia, da, st)   # the last chunk's launch arguments (benchmarks)
         self.ev.synchronize()
         dense = self.counts_host[:, 1].tolist()
