@@ -662,13 +662,14 @@ SQ_DEV bool cert_far(float v, float ny2, float nx2, float sthr, float ea2, const
   const float Dlo = (S - cv - w) - 4.0f * u * (S + fabsf(cv) + w);
   const float Dhi = (S - cv + w) + 4.0f * u * (S + fabsf(cv) + w);
   const float aip = fmaxf(1.0f, 0.5f * (fabsf(cv) + w) * 1.0001f);
-  const float num = __builtin_sqrtf(fmaxf(Dlo, 0.0f)) * ((1.0f - 4.8828125e-4f) * (1.0f - 1e-5f)) - sthr;
-  const float m = num * __builtin_sqrtf(S) * p.kq * (1.0f - 1e-5f) / aip;
+  // (v_sqrt_f32: 1 ulp, inside the 1e-5 factors; m >= m_t as a product)
+  const float rS = __builtin_amdgcn_sqrtf(S);
+  const float num = __builtin_amdgcn_sqrtf(fmaxf(Dlo, 0.0f)) * ((1.0f - 4.8828125e-4f) * (1.0f - 1e-5f)) -
+                    sthr;
   const float kt = 1.571f * sthr;
   return (Dlo >= S * (2.44140625e-4f * 1.0001f)) & (Dhi <= S * (1.998046875f * 0.9999f)) &
-         (num > 0.0f) & (m >= p.mt * 1.0001f) &
-         (fmaf(kt, __builtin_sqrtf(S) * p.kq, 2.2f) <= 1048576.0f * 0.9999f) &
-         (S < p.smax * 0.9999f);
+         (num > 0.0f) & (num * rS * p.kq * (1.0f - 1e-5f) >= p.mt * 1.0001f * aip) &
+         (fmaf(kt, rS * p.kq * 1.00001f, 2.2f) <= 1048576.0f * 0.9999f) & (S < p.smax * 0.9999f);
 }
 
 // ------------------------------------------------------------------ sweep
@@ -689,6 +690,7 @@ struct SweepArgs {
   const uint16_t* rfire;    // prep's fired pairs per row
   const int* perm;          // operand column (sorted by |c|^2) -> centroid id
   int G;
+  int gb[3];                 // first tile of groups 1..3 (n_tiles: none)
   const int* hj;            // hints (prep's)
   int* hint_out;            // ARGMIN output
   unsigned long long* list; // (row << 16) | j | fired << 15
@@ -879,7 +881,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
         }
     }
   };
-  auto group_of = [&](int t) { return (t * a.G) / n_tiles; };
+  auto group_of = [&](int t) { return (t >= a.gb[0]) + (t >= a.gb[1]) + (t >= a.gb[2]); };
 
   int U = 0;
   stage(0);
@@ -1293,7 +1295,7 @@ extern "C" {
 //   [49] group |c|^2 ranges [G][2], [50] G, [51] lb (0: no row skip / bound
 //   upkeep), [52] lb valid (skip allowed), [53] smax [1], [54] Rc [k],
 //   [55] lbo, [56] dhint, [57] sweep rows, [58] sweep row count, [59] ea2,
-//   [60] |c|^2 by operand column [k_pad]
+//   [60] |c|^2 by operand column [k_pad], [61..63] first tile of groups 1..3
 // da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
 int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -1382,6 +1384,7 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.hj = (const int*)P(10);
     a.perm = (const int*)P(48);
     a.G = (int)ia[50];
+    for (int q = 0; q < 3; ++q) a.gb[q] = (int)ia[61 + q];
     a.hint_out = (int*)P(6);
     a.list = (unsigned long long*)P(17);
     a.list_count = (int*)P(18);

@@ -759,8 +759,27 @@ class LloydEngine:
                                            device=self.device)
                 self._g_counts = torch.zeros(self.k, dtype=torch.float64, device=self.device)
                 self._g_w = w.to(torch.float32).contiguous() if w is not None else None
-            K.centroid_reduce_native(self.Xf, labels.to(torch.int32), self._g_w, self._g_sums,
-                                     self._g_counts, self.k, self._g_rws)
+                # incremental statistics (unweighted, contiguous rows of <= 1024
+                # features - the IPE path): only the rows whose label moved are
+                # re-read (csrc/kmeans.hip delta_segment_kernel; exact fixed
+                # point, bit-identical to the full reduce below)
+                self._g_inc = (w is None and self.Xf.is_contiguous() and self.d <= 1024
+                               and os.environ.get("SQ_MSTEP_INCREMENTAL", "1") != "0")
+                if self._g_inc:
+                    self._g_prev = torch.full((max(self.n, 1),), -1, dtype=torch.int32,
+                                              device=self.device)
+                    self._g_qsum = torch.zeros(self.k, dtype=torch.float64, device=self.device)
+                    self._g_perm2 = torch.empty(max(4 * self.n, 1), dtype=torch.int32,
+                                                device=self.device)
+                    self._g_qexp = K.fixed_point_exp(mxl[0] ** 2 * self.d, int(nr.item()))
+            if self._g_inc:
+                K.centroid_delta_native(self.Xf, labels.to(torch.int32).contiguous(),
+                                        self._g_prev[:self.n], self._g_sums, self._g_counts,
+                                        self._g_qsum, self.k, self._g_rws, self._g_perm2,
+                                        self._g_qexp)
+            else:
+                K.centroid_reduce_native(self.Xf, labels.to(torch.int32), self._g_w, self._g_sums,
+                                         self._g_counts, self.k, self._g_rws)
             packed = torch.empty(self.k * self.d + self.k + 1, dtype=torch.float64,
                                  device=self.device)
             K.pack_stats_native(self._g_sums, self._g_counts, inertia.double().reshape(1), packed,

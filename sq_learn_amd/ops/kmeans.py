@@ -1199,13 +1199,49 @@ class Ipe16:
         # the law's |c|^2 by operand column (the sweep's pair certificate)
         self.cns = torch.zeros(self.k_pad, dtype=torch.float32, device=cn.device)
         self.cns[:self.k].copy_(cs.float())
-        lo_t = [(q * nt) // G for q in range(G)]
-        hi_t = [((q + 1) * nt) // G for q in range(G)]
+        lo_t = self.group_tiles(cs.double().cpu().numpy(), self.k, nt, G)
+        hi_t = lo_t[1:] + [nt]
         first = torch.tensor([min(64 * t, self.k - 1) for t in lo_t], device=cn.device)
         last = torch.tensor([min(64 * t, self.k) - 1 for t in hi_t], device=cn.device)
         self.gS = torch.stack([cs.index_select(0, first), cs.index_select(0, last)], 1)
         self.gS = self.gS.float().contiguous()
         self.G = G
+        self.gstart = lo_t + [nt] * (4 - G)   # first tile of each group (unused: n_tiles)
+
+    @staticmethod
+    def group_tiles(cs, k, nt, G):
+        """First tile of each of the G norm groups: contiguous tile ranges of
+        the sorted norms ``cs`` minimising sum_g (centroids in g) x (|c|^2
+        range of g) - a row's band loses about its group's S range, so a few
+        outlying norms get a small group of their own instead of widening a
+        quarter of the centroids' range (dynamic programme over tile cuts)."""
+        import numpy as np
+        if G <= 1:
+            return [0]
+        lo = np.array([cs[min(64 * t, k - 1)] for t in range(nt)])
+        hi = np.array([cs[min(64 * t + 63, k - 1)] for t in range(nt)])
+        cnt = np.array([max(0, min(64, k - 64 * t)) for t in range(nt)], dtype=np.float64)
+        ccnt = np.concatenate([[0.0], np.cumsum(cnt)])
+
+        def cost(a, b):   # tiles [a, b)
+            return (ccnt[b] - ccnt[a]) * (hi[b - 1] - lo[a])
+
+        inf = float("inf")
+        best = np.full((G + 1, nt + 1), inf)
+        arg = np.zeros((G + 1, nt + 1), dtype=np.int64)
+        best[0, 0] = 0.0
+        for g in range(1, G + 1):
+            for b in range(g, nt + 1):
+                for a in range(g - 1, b):
+                    c = best[g - 1, a] + cost(a, b)
+                    if c < best[g, b]:
+                        best[g, b], arg[g, b] = c, a
+        cuts, b = [], nt
+        for g in range(G, 0, -1):
+            a = int(arg[g, b])
+            cuts.append(a)
+            b = a
+        return sorted(cuts)
 
     def estep(self, X, C32, hint, xn, cn, labels, mind, eps, Q, key: RngKey, tie: RngKey,
               skey: RngKey, bkey: RngKey, row_offset, first, stats=None, fallback=None):
@@ -1227,6 +1263,7 @@ class Ipe16:
         ia[60] = self.cns.data_ptr()
         ia[49] = self.gS.data_ptr()
         ia[50] = self.G
+        ia[61], ia[62], ia[63] = self.gstart[1], self.gstart[2], self.gstart[3]
         da = torch.tensor([float(eps), self.alpha, self.band_m(int(Q), min(self.ht, 9.0e-4)),
                            self.min_width], dtype=torch.float64)
         ldx = X.stride(0)

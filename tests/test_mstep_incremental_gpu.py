@@ -125,3 +125,30 @@ def test_adaptive_filter_modes_are_exact(cuda):
         assert torch.equal(a.C, b.C), f"centroids differ at iteration {it}"
         assert sa.tolist()[0] == sb.tolist()[0]
     assert {"none", "bounds", "probe"} <= set(modes), modes
+
+
+@pytest.mark.parametrize("d", [64, 100])
+def test_ipe_incremental_mstep_bit_identical(cuda, monkeypatch, d):
+    """The IPE E-step's Lloyd loop (generic M-step): the incremental
+    statistics (moved rows only) give bit-identical centroids and scalars to
+    the full fixed-point reduce."""
+    X, _ = make_blobs(40000, d, centers=30, cluster_std=1.5, random_state=2)
+    Xt = torch.tensor(X, dtype=torch.float32, device=cuda)
+    k = 32
+    C0 = Xt[torch.as_tensor(np.random.RandomState(3).choice(Xt.shape[0], k, replace=False),
+                            device=cuda)]
+    out = {}
+    for inc in ("1", "0"):
+        monkeypatch.setenv("SQ_MSTEP_INCREMENTAL", inc)
+        eng = LloydEngine(Xt, k, delta=0.5, true_distance_estimate=True, intermediate_error=True,
+                          seed=5)
+        eng.set_centers(C0)
+        tr = []
+        for _ in range(5):
+            lab, sc = eng.step()
+            tr.append((sc.tolist(), eng.centers().cpu().numpy().copy()))
+        assert eng._g_inc == (inc == "1")
+        out[inc] = tr
+    for (sa, ca), (sb, cb) in zip(out["1"], out["0"]):
+        assert sa == sb
+        assert np.array_equal(ca, cb)
