@@ -62,7 +62,8 @@ def main():
         need_lo = (vlo.max(1).values) / a2 + (X[sub].double() ** 2).sum(1)
         need_hi = (vhi.min(1).values) / a2 + (X[sub].double() ** 2).sum(1)
         dh = D.gather(1, hint.clamp_min(0)[:, None])[:, 0].clamp_min(0).sqrt()
-        ub = dh + st.Rc[hint.clamp_min(0)].double()
+        ub = dh + st.Rc[hint.clamp_min(0)].double().amax(1)
+        mwv = st.mw[hint.clamp_min(0)].double() - dh
         rec = {"step": s, "smax": float(st.smax), "skipped": int(eng.ipe16_stats[7]),
                "Rc_q": q(st.Rc[:k]), "lb_over_true_q": q((lbv / dmin)[lbv > 0]),
                "lb_zero_frac": float((lbv == 0).double().mean()),
@@ -70,7 +71,9 @@ def main():
                "swept_need_lo_sqrt_q": q(need_lo[swept].clamp_min(0).sqrt()),
                "swept_lb_minus_needlo_q": q((lbv - need_lo.clamp_min(0).sqrt())[swept]),
                "swept_ub_q": q(ub[swept]), "swept_need_hi_sqrt_q": q(need_hi[swept].clamp_min(0).sqrt()),
-               "lab_eq_hint": float((lab_s == hint).double().mean())}
+               "lab_eq_hint": float((lab_s == hint).double().mean()),
+               "mw_minus_dh_q": q(mwv), "n_wild": st.n_wild,
+               "lbdecayed_minus_needlo_q(swept)": q((lbv - float(st.smax) - need_lo.clamp_min(0).sqrt())[swept])}
         print(json.dumps(rec), flush=True)
 
 

@@ -47,7 +47,8 @@ def main():
     eng.ipe16_stats = torch.zeros(8, dtype=torch.int64, device=dev)
     out = {"rows": a.rows, "k": a.k, "d": a.d, "center": a.center, "steps": []}
     names = ["screened", "full", "fires", "exact", "pass1_wgs"]
-    names16 = ["near", "fired", "fired_exact", "dense_rows", "flagged_rows", "no_band_rows", "full"]
+    names16 = ["near", "fired", "fired_exact", "dense_rows", "flagged_rows", "no_band_rows", "full",
+               "skipped"]
     for s in range(a.steps + 1):
         eng.ipe_stats.zero_()
         eng.ipe16_stats.zero_()

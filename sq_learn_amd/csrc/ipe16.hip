@@ -307,8 +307,10 @@ struct PrepArgs {
   // row skip / bound upkeep (lb == nullptr: off)
   float* lb;                // [n] lower bound on sqrt(D) to every non-label centroid
   int lb_ok;                // lb is relative to `hint` (the previous labels)
-  const float* smax;        // [1] largest centroid shift since lb's centres (rounded up)
-  const float* Rc;          // [k] max_j |c_l - c_j| (rounded up)
+  const float* smax;        // [1] tau: the largest shift of a non-wild centroid since
+                            //     lb's centres (rounded up; the W largest are "wild")
+  const float* Rc;          // [k][4] max over group g of |c_l - c_j| (rounded up)
+  const float* mw;          // [k] min over the wild j != l of |c_l - c_j| (rounded down)
   float* lbo;               // [n] x2lo - E / alpha^2: the sweep's v -> D lower bound
   float* dhint;             // [n] lower bound on sqrt(D) of the hint pair
   int* rows;                // rows left to the sweep (all of them when lb is off)
@@ -472,20 +474,26 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       const double Dc = S - 2.0 * (double)sip[threadIdx.x];
       dh_lo = Dc - errH > 0.0 ? f32_dn(sqrt(Dc - errH) * (1.0 - 1e-12)) : 0.0f;
       if (a.lb_ok && cut.ok && nok == a.G) {
-        const double lbe = (double)a.lb[r] - (double)a.smax[0];
+        // non-wild centroids moved by <= tau since the bound; the wild ones
+        // by the triangle inequality through the hint's centre
+        const double dhi0 = sqrt(fmax(Dc + errH, 0.0)) * (1.0 + 1e-12);
+        const double lbe = fmin((double)a.lb[r] - (double)a.smax[0], (double)a.mw[l] - dhi0);
         if (lbe > 0.0) {
           // every non-hint pair provably far in the sweep: its exact D in
           // [need_lo, need_hi] of its group puts v = alpha^2 (D - |x|^2) +- E
           // inside [vlo, vhi]
-          double need_lo = -__builtin_inf(), need_hi = __builtin_inf();
-          for (int q = 0; q < a.G; ++q) {
-            need_lo = fmax(need_lo, ((double)glo[q] + re.E) / a2 + re.x2hi);
-            need_hi = fmin(need_hi, ((double)ghi[q] - re.E) / a2 + re.x2lo);
-          }
+          double need_lo = -__builtin_inf();
+          for (int q = 0; q < a.G; ++q) need_lo = fmax(need_lo, ((double)glo[q] + re.E) / a2 + re.x2hi);
           need_lo += 1e-12 * fabs(need_lo);
-          need_hi -= 1e-12 * fabs(need_hi);
-          const double ub = sqrt(fmax(Dc + errH, 0.0)) * (1.0 + 1e-12) + (double)a.Rc[l];
-          skip = lbe * lbe * (1.0 - 1e-12) >= need_lo && ub * ub * (1.0 + 1e-12) <= need_hi;
+          // upper side per group: |x - c_j| <= |x - c_hint| + |c_hint - c_j|
+          const double dhi = sqrt(fmax(Dc + errH, 0.0)) * (1.0 + 1e-12);
+          bool up = true;
+          for (int q = 0; q < a.G; ++q) {
+            const double nh = ((double)ghi[q] - re.E) / a2 + re.x2lo;
+            const double ub = dhi + (double)a.Rc[4 * l + q];
+            up = up && ub * ub * (1.0 + 1e-12) <= nh - 1e-12 * fabs(nh);
+          }
+          skip = lbe * lbe * (1.0 - 1e-12) >= need_lo && up;
           lbe_f = f32_dn(lbe);
         }
       }
@@ -793,7 +801,11 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   };
   // per-lane state: the 16 rows' band edges per set (screen) / running
   // packed minima (argmin); the near bits of the last epilogue
-  float lo[kRS][16], hi[kRS][16];
+  // lower band edge per register (row); the upper edge per row set: the
+  // smallest of the lane half's 16 rows (a row with a higher edge flags a
+  // few more pairs, which the pair certificate then clears) - 30 VGPRs for
+  // the bound upkeep
+  float lo[kRS][16], hi[kRS];
   // (screen, LB) per register the minimum far value: the row's bound upkeep
   float fm[kRS][LB ? 16 : 1];
   // near bits of the last epilogue (bit 16 st + i: register (st, i)); rows
@@ -805,7 +817,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     if constexpr (ARGMIN) {
       lo[st][i] = vmin(lo[st][i], and_or(v, keep, (q << 5) | (uint32_t)r32));
     } else {
-      const bool far = vmed3(v, lo[st][i], hi[st][i]) == v;
+      const bool far = (v >= lo[st][i]) & (v <= hi[st]);
       nb |= far ? 0u : (1u << (16 * st + i));
       if constexpr (LB) fm[st][i] = vmin(fm[st][i], far ? v : __builtin_inff());
     }
@@ -877,7 +889,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
         for (int i = 0; i < 16; ++i) {
           const int e = ((wave * kRS + st) * 32 + rl_of(i)) * kMaxG + q;
           lo[st][i] = sband[2 * e];
-          hi[st][i] = sband[2 * e + 1];
+          hi[st] = i == 0 ? sband[2 * e + 1] : fminf(hi[st], sband[2 * e + 1]);
         }
     }
   };
@@ -1243,11 +1255,15 @@ static int launch_sweep(const SweepArgs& a, hipStream_t st) {
   const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 2 * kRows * 4 +
                      (size_t)kRows * kMaxG * 2 * 4 + (size_t)kRows * 4 * 4;
   auto kern = ipe16_sweep_kernel<KSD, ARGMIN, LB>;
-  static bool attr = false;
+  static int attr = 0;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+    // the tile ring counts its own vmcnt: a register spill (scratch memory
+    // ops between the DMA and its wait) would break that count
+    hipFuncAttributes fa;
+    attr = (hipFuncGetAttributes(&fa, (const void*)kern) == hipSuccess && fa.localSizeBytes > 0) ? 2 : 1;
   }
+  if (attr == 2) return (int)hipErrorNotSupported;
   static int resident = 0;
   if (resident == 0) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -1295,7 +1311,8 @@ extern "C" {
 //   [49] group |c|^2 ranges [G][2], [50] G, [51] lb (0: no row skip / bound
 //   upkeep), [52] lb valid (skip allowed), [53] smax [1], [54] Rc [k],
 //   [55] lbo, [56] dhint, [57] sweep rows, [58] sweep row count, [59] ea2,
-//   [60] |c|^2 by operand column [k_pad], [61..63] first tile of groups 1..3
+//   [60] |c|^2 by operand column [k_pad], [61..63] first tile of groups 1..3,
+//   [64] mw [k] (row skip: nearest wild centroid)
 // da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
 int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -1351,6 +1368,7 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.lb_ok = (int)ia[52];
     a.smax = (const float*)P(53);
     a.Rc = (const float*)P(54);
+    a.mw = (const float*)P(64);
     a.lbo = (float*)P(55);
     a.dhint = (float*)P(56);
     a.rows = (int*)P(57);
@@ -1359,7 +1377,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.mind = (float*)P(23);
     a.rflag = (unsigned char*)P(21);
     a.ea2 = (float*)P(59);
-    if (!a.ea2 || !a.rows || !a.rows_count || (a.lb && (!a.lbo || !a.dhint || (a.lb_ok && (!a.smax || !a.Rc)))))
+    if (!a.ea2 || !a.rows || !a.rows_count ||
+        (a.lb && (!a.lbo || !a.dhint || (a.lb_ok && (!a.smax || !a.Rc || !a.mw)))))
       return (int)hipErrorInvalidValue;
     const dim3 pg((unsigned)((n + 255) / 256));
     switch (d_pad) {
@@ -1418,7 +1437,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
 #define CASE(KSD)                                                                  \
   case KSD * 16:                                                                   \
     return am ? launch_sweep<KSD, true, false>(a, st)                                \
-              : (a.lb ? (int)hipErrorNotSupported : launch_sweep<KSD, false, false>(a, st));
+              : (a.lb ? launch_sweep<KSD, false, true>(a, st)                      \
+                      : launch_sweep<KSD, false, false>(a, st));
       CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
 #undef CASE
       default:

@@ -1107,12 +1107,13 @@ class Ipe16:
         self.dhint = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
         self.ea2 = torch.empty(max(n, 1), dtype=torch.float32, device=dev)   # E / alpha^2
         self.rows = torch.empty(max(cm, 1), dtype=torch.int32, device=dev)
-        self.smax = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.Rc = torch.zeros(max(int(k), 1), dtype=torch.float32, device=dev)
+        self.smax = torch.zeros(1, dtype=torch.float32, device=dev)        # tau
+        self.Rc = torch.zeros((max(int(k), 1), 4), dtype=torch.float32, device=dev)
+        self.mw = torch.zeros(max(int(k), 1), dtype=torch.float32, device=dev)
+        self.n_wild = 16
         self.C_prev = None
         self.lb_valid = False
-        # (off: the sweep's bound upkeep does not fit its register budget yet)
-        self.skip = __import__("os").environ.get("SQ_IPE16_SKIP", "0") == "1"
+        self.skip = __import__("os").environ.get("SQ_IPE16_SKIP", "1") != "0"
         self.ev = torch.cuda.Event()
         # per-pair hazard of the far band (the band edge's worst case): the
         # row fires somewhere with probability ~ k * ht; a larger ht narrows
@@ -1168,18 +1169,43 @@ class Ipe16:
         self.lb_valid = False
 
     def _skip_bounds(self, C32):
-        """Device scalars of the row skip for centres C32 (fp32, the E-step's):
-        smax = max_j |c_j - c_j(prev)| since the last E-step's centres and
-        Rc[a] = max_j |c_a - c_j|, both fp64 then rounded up to fp32."""
+        """Device inputs of the row skip for centres C32 (fp32, the E-step's;
+        after ``set_centers``), fp64 then rounded outward to fp32: the
+        centroids' shifts since the last E-step's centres - the n_wild
+        largest are "wild", tau (smax) bounds every other one, so a kept
+        bound decays by tau only; mw[a] = min over the wild j != a of
+        |c_a - c_j| (the wild centroids are bounded through the hint's
+        centre instead); Rc[a][g] = max over norm group g of |c_a - c_j|
+        (the upper side)."""
+        k = C32.shape[0]
+        dev = C32.device
         C64 = C32.double()
-        inf = torch.tensor(float("inf"), device=C32.device)
-        if self.C_prev is not None and self.C_prev.shape == C32.shape:
-            sh = (C64 - self.C_prev.double()).pow(2).sum(1).max().sqrt() * (1.0 + 1e-9)
-            self.smax.copy_(torch.nextafter(sh.float(), inf).reshape(1))
+        inf = torch.tensor(float("inf"), device=dev)
         nrm = (C64 * C64).sum(1)
-        D2 = (nrm[:, None] + nrm[None, :] - 2.0 * (C64 @ C64.T)).amax(1).clamp_min(0.0)
-        R = (D2 + 2e-12 * nrm.max()).sqrt() * (1.0 + 1e-9)
-        self.Rc[:C32.shape[0]].copy_(torch.nextafter(R.float(), inf))
+        D2 = nrm[:, None] + nrm[None, :] - 2.0 * (C64 @ C64.T)
+        marg = 1e-12 * nrm.max()
+        Dlo = (D2 - marg).clamp_min(0.0).sqrt() * (1.0 - 1e-9)
+        Dhi = (D2 + marg).clamp_min(0.0).sqrt() * (1.0 + 1e-9)
+        W = min(self.n_wild, k)
+        if self.C_prev is not None and self.C_prev.shape == C32.shape:
+            sh = (C64 - self.C_prev.double()).pow(2).sum(1).sqrt() * (1.0 + 1e-9)
+            top = torch.topk(sh, min(W + 1, k)).values
+            tau = top[W] if k > W else torch.zeros((), dtype=torch.float64, device=dev)
+            self.smax.copy_(torch.nextafter(tau.float(), inf).reshape(1))
+            wild = sh > tau
+        else:
+            wild = torch.zeros(k, dtype=torch.bool, device=dev)
+        Dw = torch.where(wild[None, :] & ~torch.eye(k, dtype=torch.bool, device=dev), Dlo,
+                         torch.full_like(Dlo, float("inf")))
+        self.mw[:k].copy_(torch.nextafter(Dw.amin(1).float(), -inf))
+        # centroid -> norm group (operand column order: perm, group starts)
+        col = torch.empty(k, dtype=torch.int64, device=dev)
+        col[self.perm.long()] = torch.arange(k, device=dev)
+        gs = torch.tensor(self.gstart[1:4], device=dev)
+        grp = ((col // 64)[:, None] >= gs[None, :]).sum(1)
+        Rc = torch.full((k, 4), 0.0, dtype=torch.float64, device=dev)
+        Rc.scatter_reduce_(1, grp[None, :].expand(k, k), Dhi, reduce="amax", include_self=True)
+        self.Rc[:k].copy_(torch.nextafter(Rc.float(), inf))
         self.C_prev = C32.clone()
 
     def set_centers(self, C32, cn=None):
@@ -1258,7 +1284,7 @@ class Ipe16:
         skip = self.skip
         if skip:
             self._skip_bounds(C32)
-        ia = torch.zeros(64, dtype=torch.int64)
+        ia = torch.zeros(72, dtype=torch.int64)
         ia[48] = self.perm.data_ptr()
         ia[60] = self.cns.data_ptr()
         ia[49] = self.gS.data_ptr()
@@ -1275,6 +1301,7 @@ class Ipe16:
         ia[52] = 1 if (skip and self.lb_valid) else 0
         ia[53] = self.smax.data_ptr()
         ia[54] = self.Rc.data_ptr()
+        ia[64] = self.mw.data_ptr()
         ia[26], ia[27], ia[28], ia[29], ia[30] = self.d, self.d_pad, self.k, self.k_pad, int(Q)
         for i, kk in ((32, key), (36, tie), (40, skey), (44, bkey)):
             ia[i], ia[i + 1], ia[i + 2], ia[i + 3] = kk.k0, kk.k1, kk.s0, kk.s1

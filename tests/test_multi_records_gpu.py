@@ -64,3 +64,21 @@ def test_records_on_off_bit_identical(monkeypatch, case):
         assert torch.equal(la, lb)
         assert torch.equal(Ca, Cb)
         assert sa == sb
+
+
+def test_screen_wide_band_inertia_close_to_fp64_path(monkeypatch):
+    """The fp32 screen settles wide bands whose membership is certain
+    (recheck_fast_kernel) and writes their min-vs-label correction from its
+    fp32 distances, where the fp64 re-check (SQ_SCREEN=0) uses fp64 ones:
+    labels and centres are identical, and the iteration inertia stays within
+    a stated tolerance of the fp64 path's (1e-6 relative: fp32 rounding of
+    the corrections of the screen-settled rows)."""
+    X, C0 = _data(n=80000, d=64, k=96, seed=3, spread=1.2)
+    res = {}
+    for scr in ("1", "0"):
+        monkeypatch.setenv("SQ_SCREEN", scr)
+        res[scr], _ = _run(monkeypatch, X, C0, False, iters=8, delta=2.0)
+    for (la, ca, va), (lb, cb, vb) in zip(res["1"], res["0"]):
+        assert torch.equal(la, lb)
+        assert torch.equal(ca, cb)
+        assert abs(va[0] - vb[0]) <= 1e-6 * abs(vb[0]), (va, vb)
