@@ -6,10 +6,12 @@
 //              (Utility.py:196-231).
 // row_norms  : ||x_i||^2 for bf16/fp32 rows.
 #include "common.h"
+#include <type_traits>
 
 namespace sq {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;   // packed fp32 (v_pk_*_f32)
 
 template <typename T> SQ_DEV float ld1(const T* p, size_t i);
 template <> SQ_DEV float ld1<float>(const float* p, size_t i) { return p[i]; }
@@ -57,6 +59,56 @@ SQ_DEV void ld8raw<float>(const float* p, bool full, int valid, float v[8]) {
   }
 }
 
+// Transposing butterfly over the LPR (>= 16) lanes of a row: 16 values per
+// lane in, the LPR-lane sum of value butterfly_index(lane) out in v[0].  A
+// halving step at lane bit o (while more than one value is left) keeps the
+// upper half of the values on lanes with the bit set, the lower half on the
+// others, and adds the partner's copy of the kept half; the remaining steps
+// (LPR > 16) add the partner's single value.
+template <int LPR>
+SQ_DEV int butterfly_index(int lane) {
+  int j = 0;
+#pragma unroll
+  for (int s = 0, o = LPR / 2, c = 16; o >= 1; ++s, o >>= 1) {
+    if (c > 1 && o >= LPR / 16) {
+      if (lane & o) j += c / 2;
+      c /= 2;
+    }
+  }
+  return j;
+}
+
+// The butterfly partner at lane bit O
+// (measured: DPP moves for the low bits - quad_perm / row mirrors, with
+// their VALU-to-DPP wait states - made the kernel 2.3x slower than
+// ds_bpermute at 10M x 256)
+template <int O>
+SQ_DEV float xpart(float x) {
+  return __shfl_xor(x, O, 64);
+}
+
+template <int LPR>
+SQ_DEV void rowsum_butterfly(float (&v)[16], int lane) {
+  // halving steps on the high lane bits (LPR/2 down to LPR/16), then plain
+  // adds on the low bits
+  auto halve = [&](auto C_, auto O_) {
+    constexpr int c = decltype(C_)::value, o = decltype(O_)::value;
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int t = 0; t < c / 2; ++t) {
+      const float send = hi ? v[t] : v[t + c / 2];
+      const float keep = hi ? v[t + c / 2] : v[t];
+      v[t] = keep + xpart<o>(send);
+    }
+  };
+  halve(std::integral_constant<int, 16>{}, std::integral_constant<int, LPR / 2>{});
+  halve(std::integral_constant<int, 8>{}, std::integral_constant<int, LPR / 4>{});
+  halve(std::integral_constant<int, 4>{}, std::integral_constant<int, LPR / 8>{});
+  halve(std::integral_constant<int, 2>{}, std::integral_constant<int, LPR / 16>{});
+  if constexpr (LPR >= 64) v[0] += xpart<LPR / 32>(v[0]);
+  if constexpr (LPR >= 32) v[0] += xpart<1>(v[0]);
+}
+
 // d > 512: one launch per 512-column block (col0); the row power sums of the
 // earlier blocks are carried in rowacc[nq][n] and the maxima taken by the
 // last block (final = 1).
@@ -81,75 +133,131 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
   float q[MUQ];
 #pragma unroll
   for (int i = 0; i < MUQ; ++i) q[i] = i < nq ? qs[i] : 0.f;
-  float cs[MUQ][8], rmax[MUQ];
+  f32x2 cs[MUQ][4];   // column sums, packed pairs of the lane's 8 columns
+  float rmax[MUQ];
+  // (LPR >= 16) the exponent whose row sums this lane ends with, and the
+  // lane bits that hold duplicates of it (the butterfly's plain steps)
+  float rmax1 = 0.f;
+  const int rjl = butterfly_index<LPR>(lane);
+  constexpr int rj_dup = LPR > 16 ? (LPR / 16 - 1) : 0;
 #pragma unroll
   for (int i = 0; i < MUQ; ++i) {
     rmax[i] = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) cs[i][e] = 0.f;
+    for (int e = 0; e < 4; ++e) cs[i][e] = (f32x2){0.f, 0.f};
   }
   const long long r_beg = (long long)blockIdx.x * rows_per_wg;
   const long long r_end = min(n, r_beg + rows_per_wg);
-  for (long long r = r_beg + sg; r < r_end; r += 4 * RPW) {
-    float v[8], lg[8];
-    if (c0 < d) ld8raw<T>(X + (size_t)r * ldx + col0 + c0, vec, valid, v);
+  // the next row step's 8 values are loaded before this step's arithmetic
+  // (the loop is otherwise one dependent load per step: latency-bound)
+  float vn[8];
+  auto load8 = [&](long long rr, float (&dst)[8]) {
+    if (c0 < d && rr < r_end) ld8raw<T>(X + (size_t)rr * ldx + col0 + c0, vec, valid, dst);
     else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      for (int e = 0; e < 8; ++e) dst[e] = 0.f;
     }
+  };
+  load8(r_beg + sg, vn);
+  for (long long r = r_beg + sg; r < r_end; r += 4 * RPW) {
+    float v[8], lg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = vn[e];
+    load8(r + 4 * RPW, vn);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = e < valid ? fabsf(v[e] - mu8[e]) : 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) lg[e] = __builtin_amdgcn_logf(v[e]);   // log2, -inf at 0
     // qstep > 0: q_i = i qstep - one exp2 per element, then |a|^(i qstep) by
     // successive products (<= MUQ roundings, ~1e-6 relative)
-    float tb[8], cur[8];
+    // (arithmetic grid: packed pairs - one v_pk_mul / v_pk_add per 2 columns)
+    f32x2 tb[4], cur[4];
     if (qstep > 0.f) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        tb[e] = __builtin_amdgcn_exp2f(qstep * lg[e]);
+      for (int e = 0; e < 4; ++e) {
+        tb[e] = (f32x2){__builtin_amdgcn_exp2f(qstep * lg[2 * e]),
+                        __builtin_amdgcn_exp2f(qstep * lg[2 * e + 1])};
         cur[e] = tb[e];
       }
     }
+    // per exponent: the lane's column sums and its partial row sum (LPR >=
+    // 16: collected for the butterfly; else reduced right away)
+    float rsv[LPR >= 16 ? 16 : 1];
+#pragma unroll
+    for (int i = 0; i < (LPR >= 16 ? 16 : 1); ++i) rsv[i] = 0.f;
 #pragma unroll
     for (int i = 0; i < MUQ; ++i) {
       if (i < nq) {
-        float rs = 0.f;
+        f32x2 rs2 = (f32x2){0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < 4; ++e) {
           // |a|^0 counts nonzeros; exp2(q * -inf) = 0 for q > 0
-          float pw;
+          f32x2 pw;
           if (qstep > 0.f) {
             if (i == 0) {
-              pw = v[e] != 0.f ? 1.f : 0.f;
+              pw = (f32x2){v[2 * e] != 0.f ? 1.f : 0.f, v[2 * e + 1] != 0.f ? 1.f : 0.f};
             } else {
               if (i > 1) cur[e] *= tb[e];
               pw = cur[e];
             }
           } else {
-            pw = q[i] == 0.f ? (v[e] != 0.f ? 1.f : 0.f) : __builtin_amdgcn_exp2f(q[i] * lg[e]);
+            pw.x = q[i] == 0.f ? (v[2 * e] != 0.f ? 1.f : 0.f)
+                               : __builtin_amdgcn_exp2f(q[i] * lg[2 * e]);
+            pw.y = q[i] == 0.f ? (v[2 * e + 1] != 0.f ? 1.f : 0.f)
+                               : __builtin_amdgcn_exp2f(q[i] * lg[2 * e + 1]);
           }
           cs[i][e] += pw;
-          rs += pw;
+          rs2 += pw;
         }
+        float rs = rs2.x + rs2.y;
+        if constexpr (LPR >= 16) {
+          rsv[i] = rs;
+        } else {
 #pragma unroll
-        for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
-        if (rowacc) {   // column blocks: carry the row sum to the next block
-          rs += rowacc[(size_t)i * n + r];
-          if (!final && vl == 0) rowacc[(size_t)i * n + r] = rs;
+          for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
+          if (rowacc) {   // column blocks: carry the row sum to the next block
+            rs += rowacc[(size_t)i * n + r];
+            if (!final && vl == 0) rowacc[(size_t)i * n + r] = rs;
+          }
+          rmax[i] = fmaxf(rmax[i], rs);
         }
-        rmax[i] = fmaxf(rmax[i], rs);
+      }
+    }
+    if constexpr (LPR >= 16) {
+      // the row sums of all exponents at once: a transposing butterfly over
+      // the LPR lanes of the row - each halving step keeps half of the
+      // values (by the lane bit) and adds the partner's copy of them, so 16
+      // values cost 16 lane exchanges instead of 16 log2(LPR); each lane ends
+      // with the full row sum of ONE exponent (rs_j, j = rjl)
+      rowsum_butterfly<LPR>(rsv, lane);
+      float rs = rsv[0];
+      if (rjl < nq) {
+        if (rowacc) {   // column blocks: carry the row sum to the next block
+          rs += rowacc[(size_t)rjl * n + r];
+          if (!final && (lane & rj_dup) == 0) rowacc[(size_t)rjl * n + r] = rs;
+        }
+        rmax1 = fmaxf(rmax1, rs);
       }
     }
   }
   // row maxima: one atomic per exponent per wave (max is order-independent)
+  if constexpr (LPR >= 16) {
+    // lanes holding the same exponent: those differing in the bits the
+    // butterfly did not halve on (rj_dup) and in the row-slot bits
+    float m = rmax1;
 #pragma unroll
-  for (int i = 0; i < MUQ; ++i) {
-    if (i < nq && final) {
-      float m = rmax[i];
+    for (int o = 1; o < 64; o <<= 1)
+      if ((o & rj_dup) || o >= LPR) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (final && rjl < nq && (lane & (rj_dup | ~(LPR - 1) & 63)) == 0) atomic_max_pos(&rowmax[rjl], m);
+  } else {
 #pragma unroll
-      for (int o = LPR; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      if (lane == 0) atomic_max_pos(&rowmax[i], m);
+    for (int i = 0; i < MUQ; ++i) {
+      if (i < nq && final) {
+        float m = rmax[i];
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (lane == 0) atomic_max_pos(&rowmax[i], m);
+      }
     }
   }
   // column sums: reduce the 4*RPW row slots sharing a column group in LDS
@@ -159,7 +267,10 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
   for (int i = 0; i < MUQ; ++i) {
     if (i < nq) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) red[tid * 8 + e] = cs[i][e];
+      for (int e = 0; e < 4; ++e) {
+        red[tid * 8 + 2 * e] = cs[i][e].x;
+        red[tid * 8 + 2 * e + 1] = cs[i][e].y;
+      }
     }
     __syncthreads();
     if (i < nq && sg == 0) {     // threads 0..LPR-1: one per column group

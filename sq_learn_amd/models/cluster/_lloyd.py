@@ -534,18 +534,24 @@ class LloydEngine:
             self._sc_dev = None
             self._on_scalars(sd.tolist())
         kf, kp = self._kept_frac, self._kept_prev
+        was_probe = self._probing
         self._probing = False
         if kf is None or kp is None or kf <= self.keep_max or kp <= self.keep_max:
             self._skips = 0
             self._probe_gap = self.probe_every
             return "filter"
+        if was_probe and kf >= 0.98 and kp >= 0.98:
+            # the probe found (almost) nothing to prune: the rows are crowded
+            # by the centres, not moving - probe rarely (a probe and the
+            # bound-maintaining sweep before it cost more than the full sweep)
+            self._probe_gap = 64
         self._skips += 1
         gap = getattr(self, "_probe_gap", self.probe_every)
         if self._skips >= gap:
             # a probe of a filter that kept > keep_max twice: back off (the
             # probe measures the kept fraction over a full sweep, see _estep)
             self._skips = 0
-            self._probe_gap = min(2 * gap, 16)
+            self._probe_gap = min(2 * gap, 16) if gap < 16 else gap
             self._probing = True
             return "filter"
         return "bounds" if self._skips == gap - 1 else "none"
