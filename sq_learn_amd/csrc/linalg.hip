@@ -112,7 +112,10 @@ SQ_DEV void rowsum_butterfly(float (&v)[16], int lane) {
 // d > 512: one launch per 512-column block (col0); the row power sums of the
 // earlier blocks are carried in rowacc[nq][n] and the maxima taken by the
 // last block (final = 1).
-template <typename T, int LPR>
+// ARITH: the exponents are the arithmetic grid 0, qstep, 2 qstep, ... (the
+// p-grid of mu(A)).  Every exponent slot is computed (slots >= nq are
+// dropped at the end): one basic block per row step, no per-exponent branch.
+template <typename T, int LPR, bool ARITH>
 __global__ void __launch_bounds__(256) mu_sums_kernel(
     const T* __restrict__ X, long long ldx, int col0, int d_total, const float* __restrict__ qs,
     int nq, float* __restrict__ rowmax, float* __restrict__ part, float* __restrict__ rowacc,
@@ -172,7 +175,7 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
     // successive products (<= MUQ roundings, ~1e-6 relative)
     // (arithmetic grid: packed pairs - one v_pk_mul / v_pk_add per 2 columns)
     f32x2 tb[4], cur[4];
-    if (qstep > 0.f) {
+    if constexpr (ARITH) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         tb[e] = (f32x2){__builtin_amdgcn_exp2f(qstep * lg[2 * e]),
@@ -187,13 +190,13 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
     for (int i = 0; i < (LPR >= 16 ? 16 : 1); ++i) rsv[i] = 0.f;
 #pragma unroll
     for (int i = 0; i < MUQ; ++i) {
-      if (i < nq) {
+      {
         f32x2 rs2 = (f32x2){0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           // |a|^0 counts nonzeros; exp2(q * -inf) = 0 for q > 0
           f32x2 pw;
-          if (qstep > 0.f) {
+          if constexpr (ARITH) {
             if (i == 0) {
               pw = (f32x2){v[2 * e] != 0.f ? 1.f : 0.f, v[2 * e + 1] != 0.f ? 1.f : 0.f};
             } else {
@@ -215,7 +218,7 @@ __global__ void __launch_bounds__(256) mu_sums_kernel(
         } else {
 #pragma unroll
           for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
-          if (rowacc) {   // column blocks: carry the row sum to the next block
+          if (rowacc && i < nq) {   // column blocks: carry the row sum to the next block
             rs += rowacc[(size_t)i * n + r];
             if (!final && vl == 0) rowacc[(size_t)i * n + r] = rs;
           }
@@ -392,7 +395,12 @@ int sq_mu_sums(const void* X, int xdtype, long long ldx, const void* qs, int nq,
     while (lpr * 8 < dc) lpr <<= 1;
 #define MU_CASE(T, L)                                                                          \
   case L:                                                                                      \
-    hipLaunchKernelGGL((mu_sums_kernel<T, L>), dim3((unsigned)wgs), dim3(256), 0, st,          \
+    if (qstep > 0.f)                                                                           \
+      hipLaunchKernelGGL((mu_sums_kernel<T, L, true>), dim3((unsigned)wgs), dim3(256), 0, st,  \
+                         (const T*)X, ldx, col0, d, (const float*)qs, nq, (float*)rowmax,      \
+                         (float*)part, racc, final, n, dc, rpw, (const float*)mean, qstep);    \
+    else                                                                                       \
+    hipLaunchKernelGGL((mu_sums_kernel<T, L, false>), dim3((unsigned)wgs), dim3(256), 0, st,   \
                        (const T*)X, ldx, col0, d, (const float*)qs, nq, (float*)rowmax,        \
                        (float*)part, racc, final, n, dc, rpw, (const float*)mean, qstep);      \
     break;
