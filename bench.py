@@ -55,6 +55,8 @@ def parse(argv=None):
     ap.add_argument("--ipe-steps", type=int, default=3,
                     help="timed steady-state Lloyd steps of the IPE (true_distance_estimate) "
                          "extra, after its first two (separately timed) steps; 0 = skip")
+    ap.add_argument("--ipe-warm", type=int, default=3,
+                    help="untimed IPE steps between the second step and the timed ones")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-hard", action="store_true", help="skip the overlapping-blobs extra")
     ap.add_argument("--no-mnist", action="store_true", help="skip the 70k x 784 (config 4) extra")
@@ -132,8 +134,14 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
     """Lloyd throughput with the reference's DEFAULT distance mode,
     true_distance_estimate=True (``_dmeans.py:753-772``): every (row,
     centroid) distance is |x|^2 + |c|^2 - 2 IPE(x, c), IPE = median of 13
-    amplitude estimations (csrc/ipe.hip, fused with the fp32 MFMA inner
-    products).  Same data, k and delta as the headline."""
+    amplitude estimations, drawn from its exact law.  The certified fp16
+    screen (csrc/ipe16.hip: hint pair in full, fp16 MFMA band
+    classification + per-pair certificate, row skip by Hamerly-style bounds,
+    canonical fp32 dots and samplers only for near / fired pairs; rows it
+    cannot certify through the fp32 kernel of csrc/ipe.hip).  Same data, k
+    and delta as the headline.  First and second steps timed on their own;
+    then ``--ipe-warm`` untimed steps and ``--ipe-steps`` timed ones (the
+    steady state, like the headline's warmup)."""
     try:
         from sq_learn_amd.models.cluster._lloyd import LloydEngine
         eng = LloydEngine(X, a.k, delta=a.delta, true_distance_estimate=True,
@@ -153,6 +161,10 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
         _sync(dev)
         comm.barrier()
         extra["ipe_second_step_ms"] = _max_over_ranks(comm, dev, (time.perf_counter() - t0) * 1e3)
+        for _ in range(a.ipe_warm):
+            eng.step()[1].tolist()
+        _sync(dev)
+        comm.barrier()
         t0 = time.perf_counter()
         for _ in range(a.ipe_steps):
             eng.step()[1].tolist()

@@ -880,16 +880,28 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     }
   };
 
-  // the lane's 32 rows' band edges of centroid group q
+  // the lane's 32 rows' band edges of centroid group q.  A row without a
+  // band in a group wider than one tile is dense right away (muted, its count
+  // past the cap): certifying 64+ pairs per tile would only delay that (the
+  // first steps after a random init); in a one-tile group - the DP
+  // grouping's outlying norms - its pairs go through the certificate
   auto load_bands = [&](int q) {
     if constexpr (!ARGMIN) {
+      const int qs = q == 0 ? 0 : a.gb[q - 1];
+      const int qe = q == 3 ? n_tiles : (a.gb[q] < n_tiles ? a.gb[q] : n_tiles);
+      const bool wide = qe - qs > 1;
 #pragma unroll
       for (int st = 0; st < kRS; ++st)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int e = ((wave * kRS + st) * 32 + rl_of(i)) * kMaxG + q;
+          const int rb = (wave * kRS + st) * 32 + rl_of(i);
+          const int e = rb * kMaxG + q;
           lo[st][i] = sband[2 * e];
           hi[st] = i == 0 ? sband[2 * e + 1] : fminf(hi[st], sband[2 * e + 1]);
+          if (wide && lo[st][i] == __builtin_inff()) {
+            mute |= 1u << (16 * st + i);
+            ncnt[rb] = kCapR + 1;
+          }
         }
     }
   };

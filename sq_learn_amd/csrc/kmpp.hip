@@ -156,17 +156,17 @@ __global__ void __launch_bounds__(256) kmpp_block_totals_kernel(
 // one wave per chosen centre m < c -> ccmin[m] = min_j |cand_j - C_m|^2
 // (NaN-propagating: a NaN keeps every row of centre m live); the whole grid
 // zeroes delta_part and the list counters.
-__global__ void __launch_bounds__(256) kmpp_cc_kernel(
+SQ_DEV void kmpp_cc_body(int blk, int nblk, 
     const float* __restrict__ cand, const float* __restrict__ C, int c, int d, int t,
     float* __restrict__ ccmin, double* __restrict__ cinfo, int8_t* __restrict__ candq, int dq,
     double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long gsz = (long long)gridDim.x * 256;
+  const long long gid = (long long)blk * 256 + threadIdx.x;
+  const long long gsz = (long long)nblk * 256;
   for (long long e = gid; e < ndp; e += gsz) delta_part[e] = 0.0;
   if (gid < 4) counters[gid] = 0;
-  if ((int)blockIdx.x >= t) {
-    const int m = 4 * ((int)blockIdx.x - t) + wave;
+  if ((int)blk >= t) {
+    const int m = 4 * ((int)blk - t) + wave;
     if (m >= c) return;
     const float* cm = C + (size_t)m * d;
     float mn = __builtin_inff();
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(256) kmpp_cc_kernel(
     if (lane == 0) ccmin[m] = mn;
     return;
   }
-  const int j = blockIdx.x;
+  const int j = blk;
   const float* cj = cand + (size_t)j * d;
   {
     // two-term int8 candidate: y = c / s_c, q1 = rint(y), q2 = rint(254 (y - q1)),
@@ -249,7 +249,7 @@ SQ_DEV void seg_append(bool take, int value, int* __restrict__ seg, int* lcnt) {
 // lazy update of the previous step's winner (best_prev < 0: none), mask_out
 // cleared, rows with a live trial appended to this block's segment of surv
 // (prune) or of exact (!prune); scount / ecount[b] = the segment length.
-__global__ void __launch_bounds__(256) kmpp_screen_kernel(
+SQ_DEV void kmpp_screen_body(int blk, 
     float* __restrict__ closest, int* __restrict__ nearest,
     const uint16_t* __restrict__ mask_prev, const float* __restrict__ Dprev,
     const int* __restrict__ best_prev, int c_prev, const float* __restrict__ ccmin, long long n,
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(256) kmpp_screen_kernel(
     int* __restrict__ exact, int* __restrict__ scount, int* __restrict__ ecount, int prune) {
   __shared__ int lcnt;
   const int bp = best_prev ? *best_prev : -1;
-  const long long r0 = (long long)blockIdx.x * R;
+  const long long r0 = (long long)blk * R;
   const long long r1 = r0 + R < n ? r0 + R : n;
   int* seg = (prune ? surv : exact) + r0;
   if (threadIdx.x == 0) lcnt = 0;
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256) kmpp_screen_kernel(
     seg_append(live, (int)i, seg, &lcnt);
   }
   __syncthreads();
-  if (threadIdx.x == 0) (prune ? scount : ecount)[blockIdx.x] = lcnt;
+  if (threadIdx.x == 0) (prune ? scount : ecount)[blk] = lcnt;
 }
 
 // ------------------------------------------------ 2. certified int8 bound
@@ -317,7 +317,7 @@ SQ_DEV void kpp_i8_dots(const int8_t* __restrict__ Xq, int dq, int row,
 // at compile time up to dq = 256) and per-row scalars are all in flight
 // before the MFMAs - the row gathers, not the int8 MFMAs, bound this pass.
 template <int NS>
-__global__ void __launch_bounds__(256) kmpp_bound_kernel(
+SQ_DEV void kmpp_bound_body(int blk, 
     const int8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
     const float* __restrict__ erow, const int* __restrict__ q2row,
     const float* __restrict__ closest, const int8_t* __restrict__ candq,
@@ -329,8 +329,8 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
     *reinterpret_cast<uint4*>(cb + e) = *reinterpret_cast<const uint4*>(candq + e);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c16 = lane & 15, kb = lane >> 4;
-  const long long r0 = (long long)blockIdx.x * R;
-  const int cnt = scount[blockIdx.x];
+  const long long r0 = (long long)blk * R;
+  const int cnt = scount[blk];
   const int* sseg = surv + r0;
   int* eseg = exact + r0;
   if (threadIdx.x == 0) lcnt = 0;
@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(256) kmpp_bound_kernel(
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) ecount[blockIdx.x] = lcnt;
+  if (threadIdx.x == 0) ecount[blk] = lcnt;
 }
 
 // test hook: out[r][j] = <q_r, q1_j>, out[n + r][j]... (int32 [2][n][16]) for rows 0..n-1
@@ -478,7 +478,7 @@ __global__ void __launch_bounds__(64) kmpp_dots_kernel(const int8_t* __restrict_
 // (exact integers: any order) and STORED as delta_part[block][j] - one write
 // per block instead of one fp64 atomic per improved (row, trial).
 template <int TMAX>
-__global__ void __launch_bounds__(256) kmpp_exact_kernel(
+SQ_DEV void kmpp_exact_body(int blk, 
     const float* __restrict__ X, long long ldx, int d, long long n, int t,
     const float* __restrict__ cand, const float* __restrict__ closest,
     const double* __restrict__ w, double scale, const int* __restrict__ exact,
@@ -488,8 +488,8 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
   __shared__ double dred[4][TMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* my = tile[wave];
-  const int cnt = ecount[blockIdx.x];
-  const int* eseg = exact + (long long)blockIdx.x * R;
+  const int cnt = ecount[blk];
+  const int* eseg = exact + (long long)blk * R;
   const long long nb = (cnt + 63) / 64;
   const int ntiles = (d + kKppTile - 1) / kKppTile;
   const int lrow = lane >> 3, lchunk = lane & 7;
@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
   __syncthreads();
   if (threadIdx.x < t && threadIdx.x < TMAX) {
     const int j = threadIdx.x;
-    delta_part[(long long)blockIdx.x * t + j] = (dred[0][j] + dred[1][j]) + (dred[2][j] + dred[3][j]);
+    delta_part[(long long)blk * t + j] = (dred[0][j] + dred[1][j]) + (dred[2][j] + dred[3][j]);
   }
 }
 
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256) kmpp_exact_kernel(
 // One workgroup per value v: the first row (in row order) whose inclusive
 // fixed-point prefix reaches v - np.searchsorted(stable_cumsum, v) on the
 // current potentials (after the winning trial of mask / D / best).
-__global__ void __launch_bounds__(256) kmpp_pick_kernel(
+SQ_DEV void kmpp_pick_body(int blk, 
     const double* __restrict__ block_tot, int G, long long R, long long n,
     const double* __restrict__ vals, const float* __restrict__ closest,
     const uint16_t* __restrict__ mask, const float* __restrict__ D, const int* __restrict__ best,
@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
   __shared__ double sc[256];
   __shared__ long long found;
   __shared__ double base;
-  const double v = vals[blockIdx.x];
+  const double v = vals[blk];
   const int tid = threadIdx.x;
   const int bp = best ? *best : -1;
   // ---- block: per-thread chunk sums, WG exclusive scan, first crossing
@@ -662,14 +662,14 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
   }
   if (hit >= 0) atomicMin(&found, hit);
   __syncthreads();
-  if (tid == 0) pos[blockIdx.x] = found;
+  if (tid == 0) pos[blk] = found;
   if (cands) {
     // the candidate row itself (and its global id), clamped to the shard
     const long long r = found < 0 ? 0 : (found > n - 1 ? n - 1 : found);
-    for (int f = tid; f < d; f += 256) cands[(size_t)blockIdx.x * d + f] = X[(size_t)r * ldx + f];
+    for (int f = tid; f < d; f += 256) cands[(size_t)blk * d + f] = X[(size_t)r * ldx + f];
     if (tid == 0) {
       const long long g = r + row_offset;
-      cand_ids[blockIdx.x] = g < 0 ? 0 : (g > n_global - 1 ? n_global - 1 : g);
+      cand_ids[blk] = g < 0 ? 0 : (g > n_global - 1 ? n_global - 1 : g);
     }
   }
 }
@@ -680,7 +680,7 @@ __global__ void __launch_bounds__(256) kmpp_pick_kernel(
 // P, the block totals, centres[c], ids[c], the lazily applied winner and the
 // next centre's sampling values draws_next * P - one launch instead of the
 // host-side chain of small tensor ops.
-__global__ void __launch_bounds__(1024) kmpp_finish_kernel(
+SQ_DEV void kmpp_finish_body(
     const double* __restrict__ delta_part, int G, int t, double* __restrict__ block_tot,
     double* __restrict__ P, const double* __restrict__ draws_next, double* __restrict__ vals,
     const float* __restrict__ cands, const long long* __restrict__ cand_ids, int d,
@@ -722,6 +722,172 @@ __global__ void __launch_bounds__(1024) kmpp_finish_kernel(
   if (draws_next && tid < t) vals[tid] = draws_next[tid] * sP;
   for (int b = tid; b < G; b += 1024) block_tot[b] -= delta_part[(size_t)b * t + bj];
   for (int f = tid; f < d; f += 1024) centers[(size_t)c * d + f] = cands[(size_t)bj * d + f];
+}
+
+
+// ---------------------------------------------- single-restart kernels
+__global__ void __launch_bounds__(256) kmpp_cc_kernel(
+    const float* __restrict__ cand, const float* __restrict__ C, int c, int d, int t,
+    float* __restrict__ ccmin, double* __restrict__ cinfo, int8_t* __restrict__ candq, int dq,
+    double* __restrict__ delta_part, long long ndp, int* __restrict__ counters) {
+  kmpp_cc_body(blockIdx.x, gridDim.x, cand, C, c, d, t, ccmin, cinfo, candq, dq, delta_part, ndp,
+               counters);
+}
+__global__ void __launch_bounds__(256) kmpp_screen_kernel(
+    float* __restrict__ closest, int* __restrict__ nearest, const uint16_t* __restrict__ mask_prev,
+    const float* __restrict__ Dprev, const int* __restrict__ best_prev, int c_prev,
+    const float* __restrict__ ccmin, long long n, long long R, uint16_t* __restrict__ mask_out,
+    int* __restrict__ surv, int* __restrict__ exact, int* __restrict__ scount,
+    int* __restrict__ ecount, int prune) {
+  kmpp_screen_body(blockIdx.x, closest, nearest, mask_prev, Dprev, best_prev, c_prev, ccmin, n, R,
+                   mask_out, surv, exact, scount, ecount, prune);
+}
+template <int NS>
+__global__ void __launch_bounds__(256) kmpp_bound_kernel(
+    const int8_t* __restrict__ Xq, int dq, const float* __restrict__ srow,
+    const float* __restrict__ erow, const int* __restrict__ q2row,
+    const float* __restrict__ closest, const int8_t* __restrict__ candq,
+    const double* __restrict__ cinfo, int t, int d, long long R, const int* __restrict__ surv,
+    const int* __restrict__ scount, int* __restrict__ exact, int* __restrict__ ecount) {
+  kmpp_bound_body<NS>(blockIdx.x, Xq, dq, srow, erow, q2row, closest, candq, cinfo, t, d, R, surv,
+                      scount, exact, ecount);
+}
+template <int TMAX>
+__global__ void __launch_bounds__(256) kmpp_exact_kernel(
+    const float* __restrict__ X, long long ldx, int d, long long n, int t,
+    const float* __restrict__ cand, const float* __restrict__ closest,
+    const double* __restrict__ w, double scale, const int* __restrict__ exact,
+    const int* __restrict__ ecount, uint16_t* __restrict__ mask_out, float* __restrict__ Dout,
+    double* __restrict__ delta_part, long long R) {
+  kmpp_exact_body<TMAX>(blockIdx.x, X, ldx, d, n, t, cand, closest, w, scale, exact, ecount,
+                        mask_out, Dout, delta_part, R);
+}
+__global__ void __launch_bounds__(256) kmpp_pick_kernel(
+    const double* __restrict__ block_tot, int G, long long R, long long n,
+    const double* __restrict__ vals, const float* __restrict__ closest,
+    const uint16_t* __restrict__ mask, const float* __restrict__ D, const int* __restrict__ best,
+    const double* __restrict__ w, double scale, long long* __restrict__ pos,
+    const float* __restrict__ X, long long ldx, int d, float* __restrict__ cands,
+    long long* __restrict__ cand_ids, long long row_offset, long long n_global) {
+  kmpp_pick_body(blockIdx.x, block_tot, G, R, n, vals, closest, mask, D, best, w, scale, pos, X,
+                 ldx, d, cands, cand_ids, row_offset, n_global);
+}
+__global__ void __launch_bounds__(1024) kmpp_finish_kernel(
+    const double* __restrict__ delta_part, int G, int t, double* __restrict__ block_tot,
+    double* __restrict__ P, const double* __restrict__ draws_next, double* __restrict__ vals,
+    const float* __restrict__ cands, const long long* __restrict__ cand_ids, int d,
+    float* __restrict__ centers, long long* __restrict__ ids, int c, int* __restrict__ best_out) {
+  kmpp_finish_body(delta_part, G, t, block_tot, P, draws_next, vals, cands, cand_ids, d, centers,
+                   ids, c, best_out);
+}
+
+// ---------------------------------------------- batched restarts
+// NR independent k-means++ runs (the restarts of one fit, their draws taken
+// up front in the reference's order) advance through their centres in
+// lockstep, one launch per phase for all of them.  Per-restart state through
+// a device table [NR][kKppNF] of pointers (and the fixed-point scale); the
+// rows (X, its int8 copy) are shared.  The row passes (screen / bound /
+// exact) order their workgroups row block first, restart second, so the NR
+// restarts' workgroups of one row block run side by side and a row two of
+// them need is read from HBM once (the L2 / MALL serves the rest).
+constexpr int kKppNF = 32;
+enum KppField {
+  F_CLOSEST = 0, F_NEAREST, F_MASK0, F_MASK1, F_D0, F_D1, F_SURV, F_EXACT, F_SCOUNT, F_ECOUNT,
+  F_CC, F_CINFO, F_CANDQ, F_DELTA, F_BTOT, F_POS, F_CANDS, F_CANDIDS, F_CENTERS, F_IDS, F_P,
+  F_VALS, F_DRAWS, F_BEST, F_COUNTERS, F_SCALE
+};
+struct KppArgs {
+  const long long* tab;
+  int nr;
+  const float* X;
+  long long ldx;
+  int d;
+  long long n;
+  int t, k, dq;
+  const int8_t* Xq;
+  const float* srow;
+  const float* erow;
+  const int* q2row;
+  const double* w;
+  long long R;
+  int G;
+  int c, c_prev, cur, prune;
+  long long row_offset, n_global, doff, ndp;
+  int per;   // workgroups per restart of the cc phase
+};
+// Row-pass workgroup -> (row block b, restart r), XCD-aware: workgroups are
+// dealt to the 8 XCDs round robin (id % 8), so the nr restarts of row block
+// b take ids with the same residue - one XCD, one L2 for that block's rows
+// (read by nr workgroups close in time).  Grid: ceil(G / 8) * 8 * nr.
+SQ_DEV bool kpp_decode(int id, int nr, int G, int& b, int& r) {
+  const int x = id & 7, q = id >> 3;
+  b = (q / nr) * 8 + x;
+  r = q % nr;
+  return b < G;
+}
+template <typename P_>
+SQ_DEV P_ kf(const KppArgs& a, int r, int f) {
+  return reinterpret_cast<P_>(a.tab[(size_t)r * kKppNF + f]);
+}
+SQ_DEV double kscale(const KppArgs& a, int r) {
+  return __longlong_as_double(a.tab[(size_t)r * kKppNF + F_SCALE]);
+}
+
+__global__ void __launch_bounds__(256) kmpp_cc_batch_kernel(KppArgs a) {
+  const int r = blockIdx.x / a.per, b = blockIdx.x % a.per;
+  kmpp_cc_body(b, a.per, kf<const float*>(a, r, F_CANDS), kf<const float*>(a, r, F_CENTERS), a.c,
+               a.d, a.t, kf<float*>(a, r, F_CC), kf<double*>(a, r, F_CINFO),
+               kf<int8_t*>(a, r, F_CANDQ), a.dq, kf<double*>(a, r, F_DELTA), a.ndp,
+               kf<int*>(a, r, F_COUNTERS));
+}
+__global__ void __launch_bounds__(256) kmpp_screen_batch_kernel(KppArgs a) {
+  int b, r;
+  if (!kpp_decode(blockIdx.x, a.nr, a.G, b, r)) return;
+  const int prev = 1 - a.cur;
+  kmpp_screen_body(b, kf<float*>(a, r, F_CLOSEST), kf<int*>(a, r, F_NEAREST),
+                   kf<const uint16_t*>(a, r, F_MASK0 + prev), kf<const float*>(a, r, F_D0 + prev),
+                   a.c_prev >= 0 ? kf<const int*>(a, r, F_BEST) : nullptr, a.c_prev,
+                   kf<const float*>(a, r, F_CC), a.n, a.R, kf<uint16_t*>(a, r, F_MASK0 + a.cur),
+                   kf<int*>(a, r, F_SURV), kf<int*>(a, r, F_EXACT), kf<int*>(a, r, F_SCOUNT),
+                   kf<int*>(a, r, F_ECOUNT), a.prune);
+}
+template <int NS>
+__global__ void __launch_bounds__(256) kmpp_bound_batch_kernel(KppArgs a) {
+  int b, r;
+  if (!kpp_decode(blockIdx.x, a.nr, a.G, b, r)) return;
+  kmpp_bound_body<NS>(b, a.Xq, a.dq, a.srow, a.erow, a.q2row, kf<const float*>(a, r, F_CLOSEST),
+                      kf<const int8_t*>(a, r, F_CANDQ), kf<const double*>(a, r, F_CINFO), a.t, a.d,
+                      a.R, kf<const int*>(a, r, F_SURV), kf<const int*>(a, r, F_SCOUNT),
+                      kf<int*>(a, r, F_EXACT), kf<int*>(a, r, F_ECOUNT));
+}
+template <int TMAX>
+__global__ void __launch_bounds__(256) kmpp_exact_batch_kernel(KppArgs a) {
+  int b, r;
+  if (!kpp_decode(blockIdx.x, a.nr, a.G, b, r)) return;
+  kmpp_exact_body<TMAX>(b, a.X, a.ldx, a.d, a.n, a.t, kf<const float*>(a, r, F_CANDS),
+                        kf<const float*>(a, r, F_CLOSEST), a.w, kscale(a, r),
+                        kf<const int*>(a, r, F_EXACT), kf<const int*>(a, r, F_ECOUNT),
+                        kf<uint16_t*>(a, r, F_MASK0 + a.cur), kf<float*>(a, r, F_D0 + a.cur),
+                        kf<double*>(a, r, F_DELTA), a.R);
+}
+__global__ void __launch_bounds__(256) kmpp_pick_batch_kernel(KppArgs a) {
+  const int r = blockIdx.x / a.t, b = blockIdx.x % a.t;
+  const int prev = 1 - a.cur;
+  kmpp_pick_body(b, kf<const double*>(a, r, F_BTOT), a.G, a.R, a.n, kf<const double*>(a, r, F_VALS),
+                 kf<const float*>(a, r, F_CLOSEST), kf<const uint16_t*>(a, r, F_MASK0 + prev),
+                 kf<const float*>(a, r, F_D0 + prev),
+                 a.c_prev >= 0 ? kf<const int*>(a, r, F_BEST) : nullptr, a.w, kscale(a, r),
+                 kf<long long*>(a, r, F_POS), a.X, a.ldx, a.d, kf<float*>(a, r, F_CANDS),
+                 kf<long long*>(a, r, F_CANDIDS), a.row_offset, a.n_global);
+}
+__global__ void __launch_bounds__(1024) kmpp_finish_batch_kernel(KppArgs a) {
+  const int r = blockIdx.x;
+  const double* dr = kf<const double*>(a, r, F_DRAWS);
+  kmpp_finish_body(kf<const double*>(a, r, F_DELTA), a.G, a.t, kf<double*>(a, r, F_BTOT),
+                   kf<double*>(a, r, F_P), a.doff >= 0 ? dr + a.doff : nullptr,
+                   kf<double*>(a, r, F_VALS), kf<const float*>(a, r, F_CANDS),
+                   kf<const long long*>(a, r, F_CANDIDS), a.d, kf<float*>(a, r, F_CENTERS),
+                   kf<long long*>(a, r, F_IDS), a.c, kf<int*>(a, r, F_BEST));
 }
 
 }  // namespace sq
@@ -870,6 +1036,89 @@ int sq_kmpp_finish(const void* delta_part, int G, int t, void* block_tot, void* 
                      (const double*)draws_next, (double*)vals, (const float*)cands,
                      (const long long*)cand_ids, d, (float*)centers, (long long*)ids, c,
                      (int*)best_out);
+  return (int)hipGetLastError();
+}
+
+// Batched restarts: op 1 cc, 2 screen, 3 bound, 4 exact, 5 pick, 6 finish.
+// ia: [0] table (device int64 [nr][32]), [1] nr, [2] X, [3] ldx, [4] d,
+// [5] n, [6] t, [7] k, [8] dq, [9] Xq, [10] srow, [11] erow, [12] q2row,
+// [13] w, [14] R, [15] G, [16] c (centre being chosen), [17] c_prev (the
+// lazily applied winner's centre, -1: none), [18] cur (mask / D pair this
+// step writes), [19] prune, [20] row_offset, [21] n_global, [22] draws
+// offset of the next centre (elements, -1: last centre), [23] delta_part
+// entries per restart.
+int sq_kmpp_batch(int op, const long long* ia, void* stream) {
+  KppArgs a;
+  a.tab = (const long long*)ia[0];
+  a.nr = (int)ia[1];
+  a.X = (const float*)ia[2];
+  a.ldx = ia[3];
+  a.d = (int)ia[4];
+  a.n = ia[5];
+  a.t = (int)ia[6];
+  a.k = (int)ia[7];
+  a.dq = (int)ia[8];
+  a.Xq = (const int8_t*)ia[9];
+  a.srow = (const float*)ia[10];
+  a.erow = (const float*)ia[11];
+  a.q2row = (const int*)ia[12];
+  a.w = (const double*)ia[13];
+  a.R = ia[14];
+  a.G = (int)ia[15];
+  a.c = (int)ia[16];
+  a.c_prev = (int)ia[17];
+  a.cur = (int)ia[18];
+  a.prune = (int)ia[19];
+  a.row_offset = ia[20];
+  a.n_global = ia[21];
+  a.doff = ia[22];
+  a.ndp = ia[23];
+  a.per = 1;
+  hipStream_t st = (hipStream_t)stream;
+  if (!a.tab || a.nr < 1 || a.nr > 64 || a.t < 1 || a.t > 16 || a.n <= 0 || a.d < 1 ||
+      (a.d & 3) || a.ldx < a.d || (a.ldx & 3) || a.R <= 0 || a.G <= 0 ||
+      (long long)a.G * a.R < a.n || (a.cur & ~1))
+    return (int)hipErrorInvalidValue;
+  const unsigned rows_grid = (unsigned)((long long)((a.G + 7) / 8) * 8 * a.nr);
+  switch (op) {
+    case 1: {
+      if (a.c < 0 || a.c > a.k || a.dq < a.d || (a.dq & 63)) return (int)hipErrorInvalidValue;
+      a.per = a.t + (a.c + 3) / 4;
+      hipLaunchKernelGGL(kmpp_cc_batch_kernel, dim3((unsigned)(a.per * a.nr)), dim3(256), 0, st, a);
+      break;
+    }
+    case 2:
+      hipLaunchKernelGGL(kmpp_screen_batch_kernel, dim3(rows_grid), dim3(256), 0, st, a);
+      break;
+    case 3: {
+      if (!a.Xq || (a.dq & 63) || a.dq < a.d || 32 * a.dq > 65536) return (int)hipErrorInvalidValue;
+#define LAUNCH(NS)                                                                              \
+  hipLaunchKernelGGL(kmpp_bound_batch_kernel<NS>, dim3(rows_grid), dim3(256), (size_t)32 * a.dq, st, a)
+      switch (a.dq / 64) {
+        case 1: LAUNCH(1); break;
+        case 2: LAUNCH(2); break;
+        case 3: LAUNCH(3); break;
+        case 4: LAUNCH(4); break;
+        default: LAUNCH(0); break;
+      }
+#undef LAUNCH
+      break;
+    }
+    case 4:
+      if (a.t <= 4) hipLaunchKernelGGL(kmpp_exact_batch_kernel<4>, dim3(rows_grid), dim3(256), 0, st, a);
+      else if (a.t <= 8) hipLaunchKernelGGL(kmpp_exact_batch_kernel<8>, dim3(rows_grid), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL(kmpp_exact_batch_kernel<16>, dim3(rows_grid), dim3(256), 0, st, a);
+      break;
+    case 5:
+      hipLaunchKernelGGL(kmpp_pick_batch_kernel, dim3((unsigned)(a.t * a.nr)), dim3(256), 0, st, a);
+      break;
+    case 6:
+      if (a.c < 0) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL(kmpp_finish_batch_kernel, dim3((unsigned)a.nr), dim3(1024), 0, st, a);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }
 

@@ -55,6 +55,8 @@ __attribute__((weak)) int sq_ipe_fused(const void*, long long, const void*, cons
                                        long long, const void*, const void*);
 // ipe16.hip
 __attribute__((weak)) int sq_ipe16(int, const long long*, const double*, void*);
+// kmpp.hip, batched restarts
+__attribute__((weak)) int sq_kmpp_batch(int, const long long*, void*);
 __attribute__((weak)) int sq_centroid_delta(const void*, const void*, const void*, void*, void*,
                                             void*, long long, int, int, int, int, void*, void*,
                                             void*, void*);
@@ -392,6 +394,15 @@ static PyObject* py_ipe_fused(PyObject*, PyObject* a) {
   return ret(sq_ipe_fused(P(X), ldx, P(Cf), P(C), P(hint), P(xn), P(cn), P(lab), P(mind), n, d,
                           dp, k, kp, eps, Q, k0, k1, s0, s1, t0, t1, ts0, ts1, q0, q1, qs0, qs1,
                           roff, prune, P(stats), P(scr), P(st), P(rl), P(rc), ln, P(et), P(eh)));
+}
+
+// kmpp_batch: (op, host int64 args pointer, stream)
+static PyObject* py_kmpp_batch(PyObject*, PyObject* a) {
+  int op;
+  unsigned long long ia, st;
+  if (!PyArg_ParseTuple(a, "iKK", &op, &ia, &st)) return nullptr;
+  CHECK(sq_kmpp_batch)
+  return ret(sq_kmpp_batch(op, (const long long*)(uintptr_t)ia, P(st)));
 }
 
 // ipe16: (op, host int64 args pointer, host double args pointer, stream)
@@ -752,6 +763,7 @@ static PyMethodDef methods[] = {
     {"cluster_inertia", py_cluster_inertia, METH_VARARGS, "per-cluster inertia from the stats"},
     {"ipe_fused", py_ipe_fused, METH_VARARGS, "fused fp32-MFMA + amplitude-estimation IPE E-step"},
     {"ipe16", py_ipe16, METH_VARARGS, "certified fp16 screen of the IPE E-step (op per phase)"},
+    {"kmpp_batch", py_kmpp_batch, METH_VARARGS, "batched k-means++ restarts (op per phase)"},
     {"centroid_accumulate", py_centroid_accumulate, METH_VARARGS, "label-segmented row sums"},
     {"centroid_reduce", py_centroid_reduce, METH_VARARGS, "counting-sort segmented row sums"},
     {"centroid_finalize", py_centroid_finalize, METH_VARARGS, "centroid average + noise + shift"},

@@ -268,6 +268,58 @@ def kmeans_plusplus(data: Data, n_clusters, random_state, x_squared_norms=None,
     return centers, ids.cpu().numpy()
 
 
+def kmeans_plusplus_restarts(data: Data, n_clusters, random_state, n_restarts,
+                             n_local_trials=None, prune=None):
+    """The k-means++ initialisations of ``n_restarts`` consecutive restarts
+    (reference: ``_dmeans.py:1285-1306`` runs ``_init_centroids`` once per
+    restart, and its Lloyd loop never draws from ``random_state``): every
+    restart's draws - ``randint(n)`` then ``random_sample((k - 1, t))``
+    (``_dmeans.py:153-247``) - are taken up front in that order, then the
+    restarts run together on the device (``ops.kmeans.KmppBatch``: one
+    launch per phase for all of them, rows shared).  Returns a list of
+    [k, d] centre tensors identical to sequential ``kmeans_plusplus`` calls,
+    or None where the batched device path does not apply (one rank, fp32
+    rows on the GPU, no sample weights)."""
+    import os
+    from ...ops.kmeans import KmppBatch
+    X = data.X
+    dev = X.device
+    k = int(n_clusters)
+    if n_local_trials is None:
+        n_local_trials = 2 + int(np.log(k))
+    t = int(n_local_trials)
+    Xf = X if X.dtype in (torch.float32, torch.float64) else X.float()
+    if not (dev.type == "cuda" and data.comm.world_size == 1 and Xf.dtype == torch.float32
+            and Xf.dim() == 2 and Xf.stride(1) == 1 and Xf.stride(0) % 4 == 0
+            and data.d % 4 == 0 and Xf.data_ptr() % 16 == 0 and 1 <= t <= 16 and k >= 2
+            and n_restarts >= 1 and data.n_local > 0):
+        return None
+    if prune is None:
+        prune = os.environ.get("SQ_KMPP_PRUNE", "1") != "0"
+    rs = random_state
+    n = data.n_global
+    # device memory per restart (closest, nearest, 2 masks, 2 x t distances,
+    # 2 row lists): restarts run in groups that fit half the free memory
+    per = data.n_local * (4 + 4 + 4 + 8 * t + 8) + k * data.d * 4
+    free = torch.cuda.mem_get_info(dev)[0]
+    group = max(1, min(int(n_restarts), int(0.5 * free // max(per, 1))))
+    out = []
+    for g0 in range(0, int(n_restarts), group):
+        nr = min(group, int(n_restarts) - g0)
+        ids0, draws = [], []
+        for _ in range(nr):
+            ids0.append(int(rs.randint(n)))
+            draws.append(rs.random_sample((k - 1, t)))
+        c0s = torch.stack([gather_rows(data, [i]).to(torch.float32)[0] for i in ids0])
+        batch = KmppBatch(Xf, k, t, nr, prune=bool(prune))
+        centers, _ = batch.run(c0s, torch.as_tensor(np.stack(draws), dtype=torch.float64),
+                               torch.tensor(ids0, dtype=torch.int64, device=dev), n,
+                               row_offset=data.row_offset)
+        out += [centers[r].clone() for r in range(nr)]
+        del batch
+    return out
+
+
 def kmeans_parallel(data: Data, n_clusters, random_state, x_squared_norms=None, seed=0,
                     oversampling=2.0, rounds=5):
     """k-means|| initialisation (see the module docstring).  Returns

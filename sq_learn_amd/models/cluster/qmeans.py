@@ -41,7 +41,7 @@ from ...runtime.device import to_numpy
 from ..._config import get_config
 from .._data import as_data, check_n_features, global_mean_var, prelude_stats
 from ...utils.checkpoint import Checkpointer, rs_state_from_tensors, rs_state_to_tensors
-from ._init import kmeans_plusplus, kmeans_parallel, random_init
+from ._init import kmeans_parallel, kmeans_plusplus, kmeans_plusplus_restarts, random_init
 from ._lloyd import LloydEngine
 from ...ops import kmeans as K
 from ...quantum.fejer import median_repetitions
@@ -248,6 +248,16 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             self.resumed_from_ = (start_restart, int(st["it"]))
         self._ckpt_ctx = dict(ckpt=ckpt, fingerprint=fingerprint, rs=rs)
         phase("setup_s")
+        # the k-means++ initialisations of every restart at once (the draws
+        # in the reference order: the Lloyd loop never touches rs), one
+        # device pass per centre for all restarts; not with checkpoints
+        # (they save rs at restart boundaries)
+        pre = None
+        restart_inertias = []
+        if (isinstance(self.init, str) and self.init == "k-means++" and resume is None
+                and self._n_init - start_restart > 1 and self.checkpoint_dir is None):
+            pre = kmeans_plusplus_restarts(data_c, self.n_clusters, rs,
+                                           self._n_init - start_restart)
         for restart in range(start_restart, self._n_init):
             engine.restart = restart
             engine.it = 0
@@ -260,6 +270,9 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
                              engine={k[7:]: v for k, v in st.items() if k.startswith("engine_")},
                              engine_local={k[7:]: v for k, v in loc.items()
                                            if k.startswith("engine_")})
+            elif pre is not None:
+                C0 = pre[restart - start_restart]
+                inner = None
             else:
                 C0 = self._init_centroids(data_c, self.init, rs, xn, mean)
                 inner = None
@@ -267,6 +280,7 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
             self._ckpt_ctx["outer_best"] = best
             labels, inertia, centers, n_iter = self._run_lloyd(engine, C0, resume=inner)
             phase("lloyd_s")
+            restart_inertias.append(float(inertia))
             if best is None or inertia < best[1]:
                 best = (labels, inertia, centers, n_iter)
         ckpt.clear()
@@ -285,6 +299,9 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         self.n_iter_ = int(n_iter)
         phase("finish_s")
         self.fit_phase_s_ = phases
+        # the inertia each restart ended with (this run's restarts; the best
+        # one is inertia_)
+        self.fit_restart_inertias_ = restart_inertias
         self._mean = to_numpy(mean)
         self._engine_comm = comm
         distinct = self._count_distinct(labels, comm)

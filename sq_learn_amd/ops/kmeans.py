@@ -878,7 +878,9 @@ class KmppState:
     through the exact pass (same results: the screens only skip rows whose
     minimum provably stays the same)."""
 
-    def __init__(self, Xf, k, t, w=None, prune=True):
+    def __init__(self, Xf, k, t, w=None, prune=True, shared=None):
+        """``shared``: another state over the same rows whose int8 row copy
+        (and its scales / error norms) this one reads instead of its own."""
         n, d = Xf.shape
         dev = Xf.device
         assert Xf.dtype == torch.float32 and Xf.stride(1) == 1 and d % 4 == 0
@@ -895,7 +897,11 @@ class KmppState:
         G0 = m.kmpp_grid(max(n, 1))
         self.R = max(1, -(-n // G0))
         self.G = max(1, -(-n // self.R))
-        if self.prune and n:
+        self.owns_q = shared is None
+        if self.prune and n and shared is not None:
+            assert shared.prune and shared.X is Xf
+            self.Xq, self.srow, self.erow, self.xq2 = shared.Xq, shared.srow, shared.erow, shared.xq2
+        elif self.prune and n:
             self.Xq = torch.empty((n, self.dq), dtype=torch.int8, device=dev)
             self.srow = torch.empty(n, dtype=torch.float32, device=dev)
             self.erow = torch.empty(n, dtype=torch.float32, device=dev)
@@ -932,7 +938,7 @@ class KmppState:
         bmax = torch.zeros(self.m.kmpp_grid(-1), dtype=torch.float64, device=self.dev)
         if self.n:
             c0 = c0.to(torch.float32).contiguous()
-            q = self.prune
+            q = self.prune and self.owns_q
             _rc(self.m.kmpp_init(self.X.data_ptr(), self.ldx, self.d, self.n, c0.data_ptr(),
                                  0 if self.w is None else self.w.data_ptr(),
                                  self.closest.data_ptr(), self.nearest.data_ptr(), bmax.data_ptr(),
@@ -1049,6 +1055,94 @@ class KmppState:
             return [0, int(self.ecount.sum())]
         return [int(self.scount.sum()), int(self.ecount.sum())]
 
+
+
+class KmppBatch:
+    """NR restarts of the exact accelerated k-means++ (one rank), advanced
+    through their centres in lockstep: per phase one launch for all of them
+    (csrc/kmpp.hip ``sq_kmpp_batch``; the row passes interleave the
+    restarts' workgroups of a row block, so rows two restarts need are read
+    from HBM once).  Each restart is a ``KmppState`` (its own closest /
+    nearest / masks / lists / fixed-point scale) over the shared int8 row
+    copy; the results are those of NR sequential runs with the same draws."""
+
+    NF = 32
+
+    def __init__(self, Xf, k, t, nr, w=None, prune=True):
+        self.states = [KmppState(Xf, k, t, w=w, prune=prune)]
+        for _ in range(1, nr):
+            self.states.append(KmppState(Xf, k, t, w=w, prune=prune, shared=self.states[0]))
+        self.X, self.k, self.t, self.nr = Xf, int(k), int(t), int(nr)
+        self.n, self.d = Xf.shape
+        dev = Xf.device
+        self.dev = dev
+        self.cands = torch.empty((nr, t, self.d), dtype=torch.float32, device=dev)
+        self.cand_ids = torch.empty((nr, t), dtype=torch.int64, device=dev)
+        self.centers = torch.empty((nr, self.k, self.d), dtype=torch.float32, device=dev)
+        self.ids = torch.empty((nr, self.k), dtype=torch.int64, device=dev)
+        self.P = torch.zeros((nr, 1), dtype=torch.float64, device=dev)
+        self.vals = torch.zeros((nr, t), dtype=torch.float64, device=dev)
+        self.best = torch.zeros((nr, 1), dtype=torch.int32, device=dev)
+
+    def run(self, c0s, draws, ids0, n_global, row_offset=0):
+        """``c0s`` fp32 [nr, d] (first centres), ``draws`` fp64 [nr, k - 1, t]
+        (device), ``ids0`` int64 [nr] (the first centres' global ids):
+        returns (centers [nr, k, d], ids [nr, k])."""
+        st0 = self.states[0]
+        m, stream = st0.m, st0.st
+        nr, k, t = self.nr, self.k, self.t
+        draws = draws.to(device=self.dev, dtype=torch.float64).contiguous()
+        self.centers[:, 0].copy_(c0s)
+        self.ids[:, 0].copy_(ids0)
+        for r, s_ in enumerate(self.states):
+            mx = s_.first_centre(c0s[r])
+            self.P[r].copy_(s_.set_scale(mx.item(), n_global))
+        if k > 1:
+            self.vals.copy_(draws[:, 0] * self.P)
+        F = self.NF
+        tab = torch.zeros((nr, F), dtype=torch.int64)
+        for r, s_ in enumerate(self.states):
+            row = {0: s_.closest, 1: s_.nearest, 2: s_.mask[0], 3: s_.mask[1], 4: s_.D[0],
+                   5: s_.D[1], 6: s_.surv, 7: s_.exact, 8: s_.scount, 9: s_.ecount, 10: s_.cc,
+                   11: s_.cinfo, 12: s_.candq, 13: s_.delta, 14: s_.block_tot, 15: s_.pos,
+                   16: self.cands[r], 17: self.cand_ids[r], 18: self.centers[r], 19: self.ids[r],
+                   20: self.P[r], 21: self.vals[r], 22: draws[r], 23: self.best[r],
+                   24: s_.counters}
+            for f, ten in row.items():
+                tab[r, f] = ten.data_ptr()
+            tab[r, 25] = torch.tensor([s_.scale], dtype=torch.float64).view(torch.int64)[0]
+        self._tab = tab.to(self.dev)
+        ia = torch.zeros(32, dtype=torch.int64)
+        ia[0], ia[1] = self._tab.data_ptr(), nr
+        ia[2], ia[3], ia[4], ia[5] = self.X.data_ptr(), st0.ldx, self.d, self.n
+        ia[6], ia[7], ia[8] = t, k, st0.dq
+        if st0.prune and self.n:
+            ia[9], ia[10], ia[11], ia[12] = (st0.Xq.data_ptr(), st0.srow.data_ptr(),
+                                             st0.erow.data_ptr(), st0.xq2.data_ptr())
+        ia[13] = 0 if st0.w is None else st0.w.data_ptr()
+        ia[14], ia[15] = st0.R, st0.G
+        ia[19] = int(st0.prune)
+        ia[20], ia[21] = int(row_offset), int(n_global)
+        ia[23] = st0.delta.numel()
+        iap = ia.data_ptr()
+
+        def run_op(op):
+            _rc(m.kmpp_batch(op, iap, stream), f"kmpp_batch op {op}")
+
+        cur, c_prev = 0, -1
+        for c in range(1, k):
+            ia[16], ia[17], ia[18] = c, c_prev, cur
+            ia[22] = c * t if c < k - 1 else -1
+            run_op(5)                       # pick (+ candidate rows)
+            run_op(1)                       # candidate quantisation, centre distances
+            if self.n:
+                run_op(2)                   # triangle screen (+ lazy winner)
+                if st0.prune:
+                    run_op(3)               # certified int8 bound
+                run_op(4)                   # exact pass
+            run_op(6)                       # winners, next sampling values
+            c_prev, cur = c, cur ^ 1
+        return self.centers, self.ids
 
 def _rc(rc, name):
     if rc:
