@@ -185,7 +185,7 @@ def _ipe_extra(extra, a, X, comm, dev, start, C0):
         comm.all_reduce_(s16)
         tot = float(a.n) * a.k
         extra["ipe_screen"] = {
-            "listed_near_per_row": float(s16[0]) / a.n, "listed_fired_per_row": float(s16[1]) / a.n,
+            "listed_near_per_row": float(s16[0]) / a.n, "fired_per_row": float(s16[1]) / a.n,
             "full_sampler_per_row": (float(s16[6]) + float(st[1])) / a.n,
             "fired_exact_branch": int(s16[2]) + int(st[3]),
             "dense_row_frac": float(s16[3]) / a.n, "no_band_row_frac": float(s16[5]) / a.n,

@@ -59,7 +59,10 @@ def main():
         ms = (time.perf_counter() - t0) * 1e3
         st = dict(zip(names, eng.ipe_stats.tolist()))
         st16 = dict(zip(names16, eng.ipe16_stats.tolist()))
-        out["steps"].append({"ms": round(ms, 2), **st, **{"i16_" + k: v for k, v in st16.items()}})
+        i16 = getattr(eng, "_ipe16", None)
+        tau = float(i16.smax.item()) if i16 is not None and i16.skip else None
+        out["steps"].append({"ms": round(ms, 2), "tau": tau, **st,
+                             **{"i16_" + k: v for k, v in st16.items()}})
         print(json.dumps(out["steps"][-1]), flush=True)
     # timed without stats (the production kernel)
     eng.ipe_stats = None

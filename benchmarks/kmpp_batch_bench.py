@@ -17,6 +17,7 @@ from sq_learn_amd.utils.datasets import make_blobs_device  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+RS = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2, 4, 10]
 dev = torch.device("cuda")
 X, _ = make_blobs_device(n, 256, centers=1024, cluster_std=1.0, seed=2024, device=dev,
                          dtype=torch.float32)
@@ -28,7 +29,7 @@ t0 = time.perf_counter()
 I.kmeans_plusplus(data, k, np.random.RandomState(1))
 torch.cuda.synchronize()
 out = {"sequential_s_per_restart": time.perf_counter() - t0}
-for R in (2, 4, 10):
+for R in RS:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     I.kmeans_plusplus_restarts(data, k, np.random.RandomState(1), R)

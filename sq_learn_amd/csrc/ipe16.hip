@@ -56,6 +56,15 @@ namespace i16 {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Timing-only variant builds (benchmarks/ipe16_prep_variants.py): bits of
+// SQ_IPE16_DIAG drop parts of prep - 1: the hint's sampler (thr = the fp32
+// distance), 2: the budget / fire listing, 4: the fired pairs' evaluation,
+// 8: the per-group bands (group 0's for all).  Results are NOT the law's;
+// never set in the production build.
+#ifndef SQ_IPE16_DIAG
+#define SQ_IPE16_DIAG 0
+#endif
+
 constexpr int kTileN = 64;    // centroids per LDS tile (estep_x64 operand)
 constexpr int kNW = 4;        // waves per workgroup (one per SIMD)
 constexpr int kRS = 2;        // row sets of 32 per wave
@@ -381,7 +390,7 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
   const float cmax = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
   (void)cmin;
   const long long r = rb + lane;
-  uint32_t st_flag = 0, st_dense = 0, st_skip = 0, st_exact = 0;
+  uint32_t st_flag = 0, st_dense = 0, st_skip = 0, st_exact = 0, st_full = 0;
   // C^ = 2 alpha max_j |c_j| of the fp16 filter's bound, from the largest
   // fp32 norm widened by its summation error
   CutParams cp = a.cp;
@@ -403,14 +412,23 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
     float glo[kMaxG], ghi[kMaxG];
     int nok = 0;
     if (l >= 0) {
+#if SQ_IPE16_DIAG & 1
+      t = fmaxf(nx2 + a.cn[l] - 2.0f * sip[threadIdx.x], 0.0f);
+#else
       t = ipe_distance(sip[threadIdx.x], (double)nx2, (double)a.cn[l], a.eps, a.Q, a.key,
                        (unsigned long long)g * (unsigned long long)a.k + (unsigned long long)l);
+#endif
       const float sthr = ipe_sthr(t);
       // one band per centroid group (its own S range: the groups are
       // contiguous in |c|^2); a group without a band lists all its pairs
       for (int q = 0; q < a.G; ++q) {
+#if SQ_IPE16_DIAG & 8
+        const Cut cq = row_cut(nx2, sthr, ipe_kt(sthr), nx2 + a.gS[0], nx2 + a.gS[2 * a.G - 1],
+                               a.sc, cp);
+#else
         const Cut cq = row_cut(nx2, sthr, ipe_kt(sthr), nx2 + a.gS[2 * q], nx2 + a.gS[2 * q + 1],
                                a.sc, cp);
+#endif
         // (no band: [+inf, +inf] - med3(v, +inf, +inf) != v, every pair near;
         // an inverted interval would make med3 return v: far)
         glo[q] = cq.ok ? cq.vlo : __builtin_inff();
@@ -432,7 +450,7 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       // 2 + 2 p of its skey stream, as the near kernel's thinning reads).
       const double H = (double)cut.H;
       const int P = (a.k + 31) >> 5;
-      const double Tcap = H * (double)P;
+      const double Tcap = (SQ_IPE16_DIAG & 2) ? 0.0 : H * (double)P;
       WordStream ws(a.bkey, (unsigned long long)g);
       double E = 0.0;
       unsigned long long unused = 0xFFFFFFFFull;
@@ -500,13 +518,18 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       if (!skip) a.lbo[r] = f32_dn(re.x2lo - re.E / a2);
       if (!skip) a.dhint[r] = dh_lo;
     }
-    if (skip) {
-      // the fires prep finishes: a fire on the hint is void
+    // every row's fired pairs are finished here (the row's X was just read
+    // for the hint pair): a fire on the hint is void (dense rows: the
+    // fallback samples the whole row)
+    if (cut.ok && !(SQ_IPE16_DIAG & 4))
       for (int e = 0; e < nf; ++e)
         if ((fire[e] & 0x3FFF) != l) fire[nfs++] = fire[e];
-      st_skip = 1;
+    if (skip || nfs > 0) {
       s_t[threadIdx.x] = t;
       s_H[threadIdx.x] = cut.H;
+    }
+    if (skip) {
+      st_skip = 1;
     } else {
       if (!cut.ok) {
         // dense: every pair "far" in the sweep (no list traffic), the whole
@@ -515,7 +538,7 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
         cut.vhi = __builtin_inff();
         st_dense = 1;
       }
-      if (l >= 0) a.best[r] = pack_best(t, a.tie, g, l);
+      if (l >= 0 && nfs == 0) a.best[r] = pack_best(t, a.tie, g, l);
       a.thr[r] = t;
       a.hj[r] = l >= 0 ? l : -2;
       for (int q = 0; q < a.G; ++q) {
@@ -524,10 +547,8 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       }
       a.H[r] = cut.H;
       a.rst[r] = cut.ok ? 0 : 1;
-      uint16_t* fr = a.rfire + (size_t)r * 8;
-      const int nw = cut.ok ? nf : 0;
-      fr[0] = (uint16_t)nw;
-      for (int e = 0; e < nw; ++e) fr[1 + e] = fire[e];
+      // (the sweep lists no fires: prep finished them)
+      a.rfire[(size_t)r * 8] = 0;
     }
   }
   // the sweep's row list (one atomic per wave)
@@ -539,9 +560,9 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
     base = __shfl(base, 0, 64);
     if (lst) a.rows[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)r;
   }
-  if (__ballot(skip) != 0ull) {
-    // the skipped rows' fired pairs: canonical dots 16 at a time (4 per
-    // 16-lane group, the rows' X just read), then one lane per pair
+  if (__ballot(skip || nfs > 0) != 0ull) {
+    // the rows' fired pairs: canonical dots 16 at a time (4 per 16-lane
+    // group, the rows' X just read), then one lane per pair
     int incl = nfs;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -550,7 +571,7 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
     }
     const int tot = __shfl(incl, 63, 64);
     for (int e = 0; e < nfs; ++e) fpair[wave][incl - nfs + e] = ((uint32_t)lane << 16) | (fire[e] & 0x3FFFu);
-    if (skip) sbest[threadIdx.x] = pack_best(t, a.tie, g, l);
+    if (skip || nfs > 0) sbest[threadIdx.x] = pack_best(t, a.tie, g, l);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -578,8 +599,11 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ipe16_near_kernel's fired far pair, verbatim: the exact hazard, the
-    // thinning word of the stream's fire block, the exact branch
+    // a fired pair: its exact hazard (canonical inner product) certifies it
+    // far - P(D~ <= thr) <= pibar <= 1 - exp(-H_row) - and it is thinned
+    // (the thinning word of the stream's fire block, the exact branch), or
+    // it is sampled in full (ipe16_near_kernel's rule for a fired near pair;
+    // a band-far pair is certified by construction)
     for (int e = lane; e < tot; e += 64) {
       const uint32_t pr = fpair[wave][e];
       const int ln = (int)(pr >> 16), j = (int)(pr & 0xFFFFu);
@@ -594,17 +618,24 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       const int h = (a.Q + 1) / 2;
       const double pib = ok ? binom_upper_tail((double)pbar, a.Q, h) * (1.0 + 1e-12) : 1.0;
       const double beff = -expm1(-(double)s_H[wave * 64 + ln]);
-      WordStream ws(a.skey, (unsigned long long)gg * 32ull + (unsigned long long)(j & 31));
-      ws.b = (uint32_t)(2 + 2 * (j >> 5));
-      (void)ws.next();
-      (void)ws.next();
-      const uint32_t w2 = ws.next(), w3 = ws.next();
-      const double u = u53(w2, w3) * beff;
-      if (u < pib) {
-        ++st_exact;
-        const float dt = ipe_pruned_exact((double)ip, (double)nx2 + (double)ny2, a.eps, a.Q, tt, u, ws);
-        if (dt < __builtin_inff()) atomicMin(&sbest[wave * 64 + ln], pack_best(dt, a.tie, gg, j));
+      float dt = __builtin_inff();
+      if (ok && pib <= beff) {
+        WordStream ws(a.skey, (unsigned long long)gg * 32ull + (unsigned long long)(j & 31));
+        ws.b = (uint32_t)(2 + 2 * (j >> 5));
+        (void)ws.next();
+        (void)ws.next();
+        const uint32_t w2 = ws.next(), w3 = ws.next();
+        const double u = u53(w2, w3) * beff;
+        if (u < pib) {
+          ++st_exact;
+          dt = ipe_pruned_exact((double)ip, (double)nx2 + (double)ny2, a.eps, a.Q, tt, u, ws);
+        }
+      } else {
+        ++st_full;
+        dt = ipe_distance(ip, (double)nx2, (double)ny2, a.eps, a.Q, a.key,
+                          (unsigned long long)gg * (unsigned long long)a.k + (unsigned long long)j);
       }
+      if (dt < __builtin_inff()) atomicMin(&sbest[wave * 64 + ln], pack_best(dt, a.tie, gg, j));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -618,22 +649,30 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       // the bound for the next step (relative to this label): the hint
       // joins the non-label set when the label moved
       a.lb[r] = lab == l ? lbe_f : fminf(lbe_f, dh_lo);
+    } else if (nfs > 0) {
+      // the near kernel merges the sweep's near pairs into this
+      a.best[r] = sbest[threadIdx.x];
     }
   }
   if (a.stats) {
-    uint32_t f = st_flag, dn = st_dense, sk = st_skip, ex = st_exact;
+    uint32_t f = st_flag, dn = st_dense, sk = st_skip, ex = st_exact, fu = st_full;
+    uint32_t nfired = (uint32_t)nfs;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       f += (uint32_t)__shfl_xor((int)f, o, 64);
       dn += (uint32_t)__shfl_xor((int)dn, o, 64);
       sk += (uint32_t)__shfl_xor((int)sk, o, 64);
       ex += (uint32_t)__shfl_xor((int)ex, o, 64);
+      fu += (uint32_t)__shfl_xor((int)fu, o, 64);
+      nfired += (uint32_t)__shfl_xor((int)nfired, o, 64);
     }
     if (lane == 0) {
       atomicAdd(a.stats + 4, (unsigned long long)f);
       atomicAdd(a.stats + 5, (unsigned long long)dn);
       if (sk) atomicAdd(a.stats + 7, (unsigned long long)sk);
       if (ex) atomicAdd(a.stats + 2, (unsigned long long)ex);
+      if (fu) atomicAdd(a.stats + 6, (unsigned long long)fu);
+      if (nfired) atomicAdd(a.stats + 1, (unsigned long long)nfired);
     }
   }
 }

@@ -814,6 +814,11 @@ struct KppArgs {
   int c, c_prev, cur, prune;
   long long row_offset, n_global, doff, ndp;
   int per;   // workgroups per restart of the cc phase
+  // fused screen / bound (ops 7, 8): the union of the restarts' survivors
+  int* useg;          // per-block segments of row ids (any restart live)
+  uint16_t* umask;    // the restarts live for useg[i] (bit r)
+  int* ucount;        // [G] segment lengths
+  int tp;             // trial columns per restart (t rounded up to a power of two)
 };
 // Row-pass workgroup -> (row block b, restart r), XCD-aware: workgroups are
 // dealt to the 8 XCDs round robin (id % 8), so the nr restarts of row block
@@ -888,6 +893,346 @@ __global__ void __launch_bounds__(1024) kmpp_finish_batch_kernel(KppArgs a) {
                    kf<double*>(a, r, F_VALS), kf<const float*>(a, r, F_CANDS),
                    kf<const long long*>(a, r, F_CANDIDS), a.d, kf<float*>(a, r, F_CENTERS),
                    kf<long long*>(a, r, F_IDS), a.c, kf<int*>(a, r, F_BEST));
+}
+
+// ---------------------------------------------- fused restart passes
+// The per-restart bound pass reads every survivor's int8 row once per
+// restart: NR x ~50 % of X per centre step, and the restarts' workgroups of
+// one row block do not meet in L2 (measured: 0.487 -> 0.451 s per restart
+// only).  The fused passes read a row ONCE per step for all restarts:
+//  7. screen: one workgroup per row block walks its rows for every restart
+//     (the lazy winner update and the triangle test of kmpp_screen_body,
+//     unchanged) and lists the rows live in ANY restart, with the bit mask
+//     of the restarts they are live in;
+//  8. bound: the listed rows' int8 copies meet every restart's trials in one
+//     MFMA sweep - the nr x t trial columns side by side (tp = t rounded up
+//     to a power of two columns per restart, so a 16-column MFMA block holds
+//     whole restarts) - and each (row, restart) pair live in the mask takes
+//     the certified test of kmpp_bound_body; undecided rows go to that
+//     restart's exact segment.  The same rows reach each restart's exact
+//     pass as in the per-restart passes (set equality; the exact pass's
+//     block sums are order-free), so the ids are unchanged.
+SQ_DEV int seg_append_pos(bool take, int value, int* __restrict__ seg, int* lcnt) {
+  const unsigned long long b = __ballot(take);
+  if (b == 0ull) return -1;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(lcnt, (int)__popcll(b));
+  base = __shfl(base, 0, 64);
+  if (!take) return -1;
+  const int p = base + (int)__popcll(b & ((1ull << lane) - 1ull));
+  seg[p] = value;
+  return p;
+}
+
+__global__ void __launch_bounds__(256) kmpp_screen_fused_kernel(KppArgs a) {
+  __shared__ int lcnt;
+  const int blk = blockIdx.x;
+  const int prev = 1 - a.cur;
+  const long long r0 = (long long)blk * a.R;
+  const long long r1 = r0 + a.R < a.n ? r0 + a.R : a.n;
+  if (threadIdx.x == 0) lcnt = 0;
+  __syncthreads();
+  for (long long i0 = r0; i0 < r1; i0 += 256) {
+    const long long i = i0 + threadIdx.x;
+    unsigned bits = 0;
+    if (i < r1) {
+      // all restarts' loads first (independent), then the dependent ones
+      float cl[16];
+      int c[16], bp[16];
+      uint16_t mp[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < a.nr) {
+          bp[r] = a.c_prev >= 0 ? *kf<const int*>(a, r, F_BEST) : -1;
+          cl[r] = kf<const float*>(a, r, F_CLOSEST)[i];
+          c[r] = kf<const int*>(a, r, F_NEAREST)[i];
+          mp[r] = bp[r] >= 0 ? kf<const uint16_t*>(a, r, F_MASK0 + prev)[i] : (uint16_t)0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < a.nr) {
+          if (bp[r] >= 0 && ((mp[r] >> bp[r]) & 1u)) {
+            cl[r] = kf<const float*>(a, r, F_D0 + prev)[(size_t)bp[r] * a.n + i];
+            c[r] = a.c_prev;
+            kf<float*>(a, r, F_CLOSEST)[i] = cl[r];
+            kf<int*>(a, r, F_NEAREST)[i] = c[r];
+          }
+          kf<uint16_t*>(a, r, F_MASK0 + a.cur)[i] = 0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < a.nr && cl[r] > 0.0f && !(kf<const float*>(a, r, F_CC)[c[r]] > 4.01f * cl[r]))
+          bits |= 1u << r;
+      }
+    }
+    const int p = seg_append_pos(bits != 0u, (int)i, a.useg + r0, &lcnt);
+    if (p >= 0) a.umask[r0 + p] = (uint16_t)bits;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.ucount[blk] = lcnt;
+}
+
+// kScol: trial columns (nr x tp <= 128); LDS: the two-term int8 trials
+// [2][kScol][dq] and per column (s_c, ec, |c~|^2)
+constexpr int kScol = 128;
+// Exact pass, batched restarts (op 9): one lane per (row, trial) instead of
+// one lane per row - the per-block exact lists are short (~1-5 % of a
+// block's rows), so a lane per row left most of each wave idle and each
+// trial's candidate features came through the scalar cache, which the
+// restarts' different candidates thrash.  Here the block's candidates sit in
+// LDS ([t][d + 4] fp32, padded rows: conflict-free 16-B reads), RW = 256 / tp
+// rows at a time are staged ([RW][d + 4]; the next RW rows' loads in flight
+// during the current FMAs), and lane (row slot s, trial j) runs the SAME
+// sequential fmaf chain over f = 0 .. d - 1 as kmpp_exact_body - identical
+// D, masks and improvement sums.  d <= 256.
+constexpr int kExRowsMax = 32;
+__global__ void __launch_bounds__(256) kmpp_exact2_batch_kernel(KppArgs a) {
+  int blk, r;
+  if (!kpp_decode(blockIdx.x, a.nr, a.G, blk, r)) return;
+  extern __shared__ __attribute__((aligned(16))) float exs[];
+  __shared__ double dred[4][16];
+  const int d = a.d, ds = a.d + 4, t = a.t, tp = a.tp;
+  const int RW = 256 / tp < kExRowsMax ? 256 / tp : kExRowsMax;
+  float* cs = exs;                    // [t][ds]
+  float* xs = exs + (size_t)t * ds;   // [RW][ds]
+  const float* cand = kf<const float*>(a, r, F_CANDS);
+  const float* closest = kf<const float*>(a, r, F_CLOSEST);
+  uint16_t* mask_out = kf<uint16_t*>(a, r, F_MASK0 + a.cur);
+  float* Dout = kf<float*>(a, r, F_D0 + a.cur);
+  const double scale = kscale(a, r);
+  const int cnt = kf<const int*>(a, r, F_ECOUNT)[blk];
+  const int* eseg = kf<const int*>(a, r, F_EXACT) + (long long)blk * a.R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int d4 = d >> 2;
+  for (int e = tid; e < t * d4; e += 256) {
+    const int j = e / d4, f4 = e % d4;
+    *reinterpret_cast<float4*>(cs + (size_t)j * ds + 4 * f4) =
+        *reinterpret_cast<const float4*>(cand + (size_t)j * d + 4 * f4);
+  }
+  const int rs = tid / tp, j = tid % tp;
+  double dsum = 0.0;
+  // row staging: RW d4 float4 per chunk, kExRowsMax * 64 / 256 = 8 per thread at most
+  constexpr int kPer = kExRowsMax * 64 / 256;
+  float4 v[kPer];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < RW * d4) {
+        const int s = e / d4, f4 = e % d4;
+        const int p = c0 + s;
+        if (p < cnt) v[i] = *reinterpret_cast<const float4*>(a.X + (size_t)eseg[p] * a.ldx + 4 * f4);
+      }
+    }
+  };
+  fetch(0);
+  for (int c0 = 0; c0 < cnt; c0 += RW) {
+    __syncthreads();   // the previous chunk's reads of xs are done (and cs staged)
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
+      if (e < RW * d4) *reinterpret_cast<float4*>(xs + (size_t)(e / d4) * ds + 4 * (e % d4)) = v[i];
+    }
+    __syncthreads();
+    if (c0 + RW < cnt) fetch(c0 + RW);
+    const int p = rs < RW ? c0 + rs : cnt;
+    const bool live = p < cnt && j < t;
+    float acc = 0.0f;
+    if (live) {
+      const float* xr = xs + (size_t)rs * ds;
+      const float* cr = cs + (size_t)j * ds;
+      for (int f = 0; f < d; f += 4) {
+        const float4 x4 = *reinterpret_cast<const float4*>(xr + f);
+        const float4 c4 = *reinterpret_cast<const float4*>(cr + f);
+        float ev = x4.x - c4.x;
+        acc = fmaf(ev, ev, acc);
+        ev = x4.y - c4.y;
+        acc = fmaf(ev, ev, acc);
+        ev = x4.z - c4.z;
+        acc = fmaf(ev, ev, acc);
+        ev = x4.w - c4.w;
+        acc = fmaf(ev, ev, acc);
+      }
+    }
+    const int row = p < cnt ? eseg[p] : 0;
+    uint32_t m = 0;
+    if (live) {
+      const float cl = closest[row];
+      if (acc < cl) {
+        const double wi = a.w ? a.w[row] : 1.0;
+        m = 1u << j;
+        Dout[(size_t)j * a.n + row] = acc;
+        dsum += kpp_q(cl, wi, scale) - kpp_q(acc, wi, scale);
+      }
+    }
+    // the row's mask over its tp lanes
+    for (int o = 1; o < tp; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o, 64);
+    if (j == 0 && p < cnt) mask_out[row] = (uint16_t)m;
+  }
+  // improvement sums per trial (exact integers: any order)
+  for (int o = tp; o < 64; o <<= 1) dsum += __shfl_xor(dsum, o, 64);
+  if (lane < tp) dred[wave][lane] = dsum;
+  __syncthreads();
+  if (tid < t) {
+    double* dp = kf<double*>(a, r, F_DELTA);
+    dp[(long long)blk * t + tid] = (dred[0][tid] + dred[1][tid]) + (dred[2][tid] + dred[3][tid]);
+  }
+}
+
+constexpr int kBfThreads = 512;   // 8 waves share one staging of the trials
+template <int NS>
+__global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a) {
+  constexpr int DQ = NS * 64;
+  constexpr int NWV = kBfThreads / 64;
+  // dynamic LDS: [2][ncb 16][DQ] int8 (sized to the columns in use: occupancy)
+  extern __shared__ __attribute__((aligned(16))) int8_t cbs[];
+  __shared__ float cpar[kScol][3];
+  __shared__ int lcnt[16];
+  __shared__ float sclo[NWV * 256];
+  const int blk = blockIdx.x;
+  const int tp = a.tp, t = a.t, nr = a.nr;
+  const int ncol = nr * tp, ncb = (ncol + 15) / 16;
+  auto cb = [&](int hl, int col) -> int8_t* { return cbs + ((size_t)hl * ncb * 16 + col) * DQ; };
+  // stage every restart's trials: column c = r tp + j (j >= t: zero)
+  for (int e = threadIdx.x; e < 2 * ncb * 16 * (DQ / 16); e += kBfThreads) {
+    const int hl = e / (ncb * 16 * (DQ / 16));
+    const int rem = e % (ncb * 16 * (DQ / 16));
+    const int col = rem / (DQ / 16), piece = rem % (DQ / 16);
+    const int r = col / tp, j = col % tp;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < nr && j < t)
+      v = *reinterpret_cast<const uint4*>(kf<const int8_t*>(a, r, F_CANDQ) +
+                                          ((size_t)(hl * 16 + j) * a.dq + piece * 16));
+    *reinterpret_cast<uint4*>(cb(hl, col) + piece * 16) = v;
+  }
+  for (int col = threadIdx.x; col < ncb * 16; col += kBfThreads) {
+    const int r = col / tp, j = col % tp;
+    const bool jv = r < nr && j < t;
+    const double* ci = jv ? kf<const double*>(a, r, F_CINFO) + j * 4 : nullptr;
+    // scale and error norm rounded UP to fp32, |c~|^2 to nearest (kmpp_bound_body)
+    cpar[col][0] = jv ? (float)ci[0] * (1.0f + 1.2e-7f) : 1.0f;
+    cpar[col][1] = jv ? (float)ci[1] * (1.0f + 1.2e-7f) : 0.0f;
+    cpar[col][2] = jv ? (float)ci[2] : 0.0f;
+  }
+  if (threadIdx.x < 16) lcnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, kb = lane >> 4;
+  const long long r0 = (long long)blk * a.R;
+  const int cnt = a.ucount[blk];
+  const int* useg = a.useg + r0;
+  const uint16_t* umask = a.umask + r0;
+  const float lim_rel = 1.0f + 3.0f * (float)(a.d + 2) * 5.9604645e-08f + 1e-6f;
+  const int rpb = 16 / tp;   // restarts per 16-column block
+  // one group ahead in registers: the group's row ids / masks, int8 rows,
+  // per-row scalars and the rows' closest values of the restarts they are
+  // live in (lane (kb, c16): restarts kb, kb + 4, kb + 8, kb + 12 of row
+  // slot c16); the current group's closest values go through LDS
+  float* scl = sclo + wave * 256;   // [16 row slots][16 restarts]
+  int nrow = -1;
+  unsigned nbits = 0u;
+  kpp_v4i nav[NS];
+  float nrs = 0.f, nre = 0.f, ncl[4];
+  int nq2 = 0;
+  auto prefetch = [&](int g) {
+    const int e = g + c16;
+    nrow = e < cnt ? useg[e] : -1;
+    nbits = e < cnt ? umask[e] : 0u;
+    const int rr0 = nrow >= 0 ? nrow : 0;
+    const int8_t* xr = a.Xq + (size_t)rr0 * a.dq + 16 * kb;
+#pragma unroll
+    for (int s4 = 0; s4 < NS; ++s4)
+      nav[s4] = nrow >= 0 ? *reinterpret_cast<const kpp_v4i*>(xr + 64 * s4) : kpp_v4i{0, 0, 0, 0};
+    nrs = a.srow[rr0];
+    nre = a.erow[rr0];
+    nq2 = a.q2row[rr0];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rr = kb + 4 * u;
+      ncl[u] = (nrow >= 0 && rr < nr && ((nbits >> rr) & 1u))
+                   ? kf<const float*>(a, rr, F_CLOSEST)[nrow] : 0.0f;
+    }
+  };
+  prefetch(wave * 16);
+  for (int g0 = wave * 16; g0 < cnt; g0 += 16 * NWV) {
+    const int row = nrow;
+    const unsigned bits = nbits;
+    kpp_v4i av[NS];
+#pragma unroll
+    for (int s4 = 0; s4 < NS; ++s4) av[s4] = nav[s4];
+    const float rs = nrs, re_ = nre;
+    const int rq2 = nq2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) scl[c16 * 16 + kb + 4 * u] = ncl[u];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    prefetch(g0 + 16 * NWV);
+    // restarts live in any row of the group
+    unsigned gbits = row >= 0 ? bits : 0u;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) gbits |= (unsigned)__shfl_xor((int)gbits, o, 64);
+    gbits = (unsigned)__builtin_amdgcn_readfirstlane((int)gbits);
+    for (int cbk = 0; cbk < ncb; ++cbk) {
+      const unsigned bm = ((1u << rpb) - 1u) << (cbk * rpb);
+      if (!(gbits & bm)) continue;
+      kpp_v4i hi = kpp_v4i{0, 0, 0, 0}, lo = kpp_v4i{0, 0, 0, 0};
+#pragma unroll
+      for (int s4 = 0; s4 < NS; ++s4) {
+        const kpp_v4i bh = *reinterpret_cast<const kpp_v4i*>(cb(0, cbk * 16 + c16) + 64 * s4 + 16 * kb);
+        const kpp_v4i bl = *reinterpret_cast<const kpp_v4i*>(cb(1, cbk * 16 + c16) + 64 * s4 + 16 * kb);
+        hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s4], bh, hi, 0, 0, 0);
+        lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s4], bl, lo, 0, 0, 0);
+      }
+      const int col = cbk * 16 + c16;
+      const int r = col / tp, j = col % tp;
+      const bool jv = r < nr && j < t;
+      const float sc = cpar[col][0], ec = cpar[col][1], cc2 = cpar[col][2];
+      unsigned long long bal[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int src = 4 * kb + i;   // the row slot of result register i
+        const int rr = __shfl(row, src, 64);
+        const unsigned rb = (unsigned)__shfl((int)bits, src, 64);
+        const float s = __shfl(rs, src, 64);
+        const float er = __shfl(re_, src, 64);
+        const float q2 = (float)__shfl(rq2, src, 64);
+        bool need = false;
+        if (jv && rr >= 0 && ((rb >> r) & 1u)) {
+          const float cl = scl[src * 16 + r];
+          const float A = s * s * q2;
+          const float dot = s * sc * ((float)hi[i] + (float)lo[i] * (1.0f / 254.0f));
+          const float Dq = (A + cc2) - 2.0f * dot;
+          const float Dlb = Dq - 1e-6f * (A + cc2 + 2.0f * fabsf(dot));
+          float lb = 0.0f;
+          if (Dlb > 0.0f) {
+            const float rt = __builtin_amdgcn_sqrtf(Dlb) * (1.0f - 1e-6f) - er - ec;
+            lb = rt > 0.0f ? rt * rt * (1.0f - 1e-6f) : 0.0f;
+          }
+          need = !(lb > cl * lim_rel);
+        }
+        bal[i] = __ballot(need);
+      }
+      // row slot c16 (lanes < 16): rows 4 q + i live in lanes [16 q, 16 q + 16) of bal[i];
+      // restart p of this block: lanes [p tp, p tp + tp) of that 16-lane group
+      const int q = c16 >> 2, ii = c16 & 3;
+      const unsigned long long bi = ii == 0 ? bal[0] : ii == 1 ? bal[1] : ii == 2 ? bal[2] : bal[3];
+      const unsigned tmask = tp >= 16 ? 0xFFFFu : ((1u << tp) - 1u);
+      for (int p = 0; p < rpb; ++p) {
+        const int rp = cbk * rpb + p;
+        if (rp >= nr) break;
+        const bool take = lane < 16 && row >= 0 &&
+                          (((unsigned)(bi >> (16 * q + p * tp))) & tmask) != 0u;
+        seg_append(take, row, kf<int*>(a, rp, F_EXACT) + r0, &lcnt[rp]);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nr) kf<int*>(a, threadIdx.x, F_ECOUNT)[blk] = lcnt[threadIdx.x];
 }
 
 }  // namespace sq
@@ -1046,7 +1391,8 @@ int sq_kmpp_finish(const void* delta_part, int G, int t, void* block_tot, void* 
 // lazily applied winner's centre, -1: none), [18] cur (mask / D pair this
 // step writes), [19] prune, [20] row_offset, [21] n_global, [22] draws
 // offset of the next centre (elements, -1: last centre), [23] delta_part
-// entries per restart.
+// entries per restart; ops 7 (fused screen) / 8 (fused bound): [24] useg
+// (int32 [G R]), [25] umask (uint16 [G R]), [26] ucount (int32 [G]), [27] tp.
 int sq_kmpp_batch(int op, const long long* ia, void* stream) {
   KppArgs a;
   a.tab = (const long long*)ia[0];
@@ -1074,6 +1420,10 @@ int sq_kmpp_batch(int op, const long long* ia, void* stream) {
   a.doff = ia[22];
   a.ndp = ia[23];
   a.per = 1;
+  a.useg = (int*)ia[24];
+  a.umask = (uint16_t*)ia[25];
+  a.ucount = (int*)ia[26];
+  a.tp = (int)ia[27];
   hipStream_t st = (hipStream_t)stream;
   if (!a.tab || a.nr < 1 || a.nr > 64 || a.t < 1 || a.t > 16 || a.n <= 0 || a.d < 1 ||
       (a.d & 3) || a.ldx < a.d || (a.ldx & 3) || a.R <= 0 || a.G <= 0 ||
@@ -1116,6 +1466,37 @@ int sq_kmpp_batch(int op, const long long* ia, void* stream) {
       if (a.c < 0) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL(kmpp_finish_batch_kernel, dim3((unsigned)a.nr), dim3(1024), 0, st, a);
       break;
+    case 9: {
+      // exact pass, lane per (row, trial): d <= 256, tp a power of two >= t
+      if (a.d > 256 || a.tp < a.t || a.tp > 16 || (a.tp & (a.tp - 1))) return (int)hipErrorInvalidValue;
+      const int RW = 256 / a.tp < kExRowsMax ? 256 / a.tp : kExRowsMax;
+      const size_t lds = (size_t)(a.t + RW) * (a.d + 4) * sizeof(float);
+      hipLaunchKernelGGL(kmpp_exact2_batch_kernel, dim3(rows_grid), dim3(256), lds, st, a);
+      break;
+    }
+    case 7:
+    case 8: {
+      // fused passes: <= 16 restarts (uint16 masks), nr tp <= kScol columns, dq <= 256
+      if (!a.useg || !a.umask || !a.ucount || a.nr > 16 || a.tp < a.t || a.tp > 16 ||
+          (a.tp & (a.tp - 1)) || a.nr * a.tp > kScol || !a.prune)
+        return (int)hipErrorInvalidValue;
+      if (op == 7) {
+        hipLaunchKernelGGL(kmpp_screen_fused_kernel, dim3((unsigned)a.G), dim3(256), 0, st, a);
+        break;
+      }
+      if (!a.Xq || (a.dq & 63) || a.dq < a.d || a.dq > 256) return (int)hipErrorInvalidValue;
+      const size_t lds = (size_t)2 * ((a.nr * a.tp + 15) / 16) * 16 * a.dq;
+#define LAUNCH(NS)                                                                               \
+  hipLaunchKernelGGL(kmpp_bound_fused_kernel<NS>, dim3((unsigned)a.G), dim3(kBfThreads), lds, st, a)
+      switch (a.dq / 64) {
+        case 1: LAUNCH(1); break;
+        case 2: LAUNCH(2); break;
+        case 3: LAUNCH(3); break;
+        default: LAUNCH(4); break;
+      }
+#undef LAUNCH
+      break;
+    }
     default:
       return (int)hipErrorInvalidValue;
   }

@@ -303,6 +303,10 @@ def kmeans_plusplus_restarts(data: Data, n_clusters, random_state, n_restarts,
     per = data.n_local * (4 + 4 + 4 + 8 * t + 8) + k * data.d * 4
     free = torch.cuda.mem_get_info(dev)[0]
     group = max(1, min(int(n_restarts), int(0.5 * free // max(per, 1))))
+    if prune:
+        # the fused screen / bound hold <= 16 restarts and <= 128 trial columns
+        tp = 1 << max(0, (t - 1).bit_length())
+        group = min(group, 16, max(1, 128 // tp))
     out = []
     for g0 in range(0, int(n_restarts), group):
         nr = min(group, int(n_restarts) - g0)

@@ -7,6 +7,7 @@ Philox keys (reference ``_dmeans.py:732-830``).
 """
 
 import math
+import os
 
 import torch
 
@@ -1083,6 +1084,22 @@ class KmppBatch:
         self.P = torch.zeros((nr, 1), dtype=torch.float64, device=dev)
         self.vals = torch.zeros((nr, t), dtype=torch.float64, device=dev)
         self.best = torch.zeros((nr, 1), dtype=torch.int32, device=dev)
+        # fused screen / bound (ops 7 / 8): one read of a row per centre step
+        # for all restarts (nr <= 16 restarts, nr tp <= 128 trial columns,
+        # dq <= 256); SQ_KMPP_FUSED=0: the per-restart passes (same ids)
+        st0 = self.states[0]
+        self.tp = 1 << max(0, (self.t - 1).bit_length())
+        self.fused = (prune and self.n > 0 and nr <= 16 and nr * self.tp <= 128
+                      and st0.dq <= 256 and os.environ.get("SQ_KMPP_FUSED", "1") != "0")
+        # exact pass with a lane per (row, trial) (op 9; d <= 256);
+        # SQ_KMPP_EXACT2=0: a lane per row (op 4, same results)
+        self.exact2 = (self.d <= 256 and self.t <= 16
+                       and os.environ.get("SQ_KMPP_EXACT2", "1") != "0")
+        if self.fused:
+            GR = max(st0.G * st0.R, 1)
+            self.useg = torch.empty(GR, dtype=torch.int32, device=dev)
+            self.umask = torch.empty(GR, dtype=torch.int16, device=dev)
+            self.ucount = torch.zeros(st0.G, dtype=torch.int32, device=dev)
 
     def run(self, c0s, draws, ids0, n_global, row_offset=0):
         """``c0s`` fp32 [nr, d] (first centres), ``draws`` fp64 [nr, k - 1, t]
@@ -1124,6 +1141,10 @@ class KmppBatch:
         ia[19] = int(st0.prune)
         ia[20], ia[21] = int(row_offset), int(n_global)
         ia[23] = st0.delta.numel()
+        ia[27] = self.tp
+        if self.fused:
+            ia[24], ia[25], ia[26] = (self.useg.data_ptr(), self.umask.data_ptr(),
+                                      self.ucount.data_ptr())
         iap = ia.data_ptr()
 
         def run_op(op):
@@ -1135,11 +1156,15 @@ class KmppBatch:
             ia[22] = c * t if c < k - 1 else -1
             run_op(5)                       # pick (+ candidate rows)
             run_op(1)                       # candidate quantisation, centre distances
-            if self.n:
+            if self.n and self.fused:
+                run_op(7)                   # triangle screen, all restarts: union list
+                run_op(8)                   # certified int8 bound, one row read
+                run_op(9 if self.exact2 else 4)   # exact pass
+            elif self.n:
                 run_op(2)                   # triangle screen (+ lazy winner)
                 if st0.prune:
                     run_op(3)               # certified int8 bound
-                run_op(4)                   # exact pass
+                run_op(9 if self.exact2 else 4)   # exact pass
             run_op(6)                       # winners, next sampling values
             c_prev, cur = c, cur ^ 1
         return self.centers, self.ids

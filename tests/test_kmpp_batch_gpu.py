@@ -24,10 +24,15 @@ def _data(cuda, n=120_000, d=64, blobs=40, seed=0):
     return Data(Xt, n, 0, Comm(None), "sharded")
 
 
-@pytest.mark.parametrize("prune,d", [(True, 64), (False, 64), (True, 256)])
-def test_batched_restarts_equal_sequential(cuda, prune, d):
-    data = _data(cuda, d=d)
-    k, R = 48, 4
+# (the pruned cases run the fused screen / bound: t = 5 -> 8 columns per
+# restart; k = 3000: t = 10 -> 16 columns, one restart per MFMA block; R = 16
+# x 8 = 128 columns, the limit)
+@pytest.mark.parametrize("prune,d,k,R,n", [(True, 64, 48, 4, 120_000), (False, 64, 48, 4, 120_000),
+                                           (True, 256, 48, 4, 120_000),
+                                           (True, 128, 48, 16, 60_000),
+                                           (True, 64, 3000, 3, 40_000)])
+def test_batched_restarts_equal_sequential(cuda, prune, d, k, R, n):
+    data = _data(cuda, d=d, n=n)
     rs1 = np.random.RandomState(7)
     seq = [I.kmeans_plusplus(data, k, rs1, prune=prune) for _ in range(R)]
     rs2 = np.random.RandomState(7)
@@ -51,3 +56,13 @@ def test_qmeans_fit_n_init_batched_matches_sequential(cuda, monkeypatch):
     assert a.fit_restart_inertias_ == b.fit_restart_inertias_
     assert np.array_equal(a.labels_, b.labels_)
     assert a.inertia_ == b.inertia_
+
+
+def test_fused_passes_equal_per_restart_passes(cuda, monkeypatch):
+    """SQ_KMPP_FUSED=0 (per-restart screen / bound) gives the same centres."""
+    data = _data(cuda, n=100_000, d=96, blobs=30, seed=3)
+    a = I.kmeans_plusplus_restarts(data, 64, np.random.RandomState(11), 6)
+    monkeypatch.setenv("SQ_KMPP_FUSED", "0")
+    b = I.kmeans_plusplus_restarts(data, 64, np.random.RandomState(11), 6)
+    for Ca, Cb in zip(a, b):
+        assert torch.equal(Ca, Cb)
