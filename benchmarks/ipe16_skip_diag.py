@@ -41,12 +41,14 @@ def main():
     eng.set_centers(C0)
     eng.ipe16_stats = torch.zeros(8, dtype=torch.int64, device=dev)
     sub = torch.arange(0, n, max(1, n // 20000), device=dev)[:20000]
+    prev_skip = None
     for s in range(steps):
         C = eng.centers().clone().double()
         eng.ipe16_stats.zero_()
         lab, sc = eng.step()
         sc.tolist()
         st = eng._ipe16
+        skipped = st.rflag[sub] == 2
         lab_s = lab[sub].long()
         hint = eng._ipe_lab[eng._ipe_cur ^ 1][sub].long()
         Xs = X[sub].double()
@@ -64,7 +66,22 @@ def main():
         dh = D.gather(1, hint.clamp_min(0)[:, None])[:, 0].clamp_min(0).sqrt()
         ub = dh + st.Rc[hint.clamp_min(0)].double().amax(1)
         mwv = st.mw[hint.clamp_min(0)].double() - dh
+        # per-group upper condition (need_hi per group vs dh + Rc[hint][g])
+        Rcg = st.Rc[hint.clamp_min(0)].double()[:, :st.G]
+        up_ok = ((dh[:, None] + Rcg) ** 2 <= vhi / a2 + (X[sub].double() ** 2).sum(1)[:, None]).all(1)
+        lo_ok = (lbv - float(st.smax)).clamp_min(0) ** 2 >= need_lo
+        mw_ok = mwv.clamp_min(0) ** 2 >= need_lo
+        trans = {}
+        if prev_skip is not None:
+            for nm, m in (("after_skip", prev_skip), ("after_sweep", ~prev_skip)):
+                trans[nm] = {"rows": int(m.sum()), "skip_now": float(skipped[m].double().mean()),
+                             "lo_ok": float(lo_ok[m].double().mean()),
+                             "mw_ok": float(mw_ok[m].double().mean()),
+                             "up_ok": float(up_ok[m].double().mean()),
+                             "lbe_minus_needlo_q": q((lbv - float(st.smax) - need_lo.clamp_min(0).sqrt())[m])}
+        prev_skip = skipped
         rec = {"step": s, "smax": float(st.smax), "skipped": int(eng.ipe16_stats[7]),
+               "trans": trans,
                "Rc_q": q(st.Rc[:k]), "lb_over_true_q": q((lbv / dmin)[lbv > 0]),
                "lb_zero_frac": float((lbv == 0).double().mean()),
                "lb_q": q(lbv), "dmin_q": q(dmin),

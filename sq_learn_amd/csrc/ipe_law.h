@@ -73,37 +73,18 @@ SQ_DEV double rcp64(double x) {
 // The median of Q (odd) iid draws T_1..T_Q with CDF F is F^-1(U_(h)), h =
 // (Q + 1) / 2, U_(h) the h-th order statistic of Q uniforms ~ Beta(h, h):
 // P(U_(h) <= x) = G(x) = P(Binomial(Q, x) >= h).  One uniform u gives
-// x* = G^-1(u) (safeguarded Newton in fp64 from the normal approximation;
-// G' = Q C(Q-1, h-1) x^(h-1) (1-x)^(Q-h)), after which the draw is ONE
-// inverse-CDF walk of F to x* - no binomial tail per step, no per-draw
-// sorting (Utility.py:534-572's median over Q repetitions, exact law).
-SQ_DEV double median_order_stat(double u, int Q) {
-  const int h = (Q + 1) / 2;
-  if (Q == 1) return u;
-  double cq = (double)Q;                  // Q C(Q-1, h-1)
-  for (int i = 1; i < h; ++i) cq = cq * (double)(Q - i) / (double)i;
-  double lo = 0.0, hi = 1.0;
-  // start: the normal approximation (fp32 erfinv: only the Newton start)
-  double x = 0.5 + 0.7071067811865476 / sqrt((double)Q + 2.0) * (double)erfinvf((float)(2.0 * u - 1.0));
-  x = fmin(fmax(x, 1e-9), 1.0 - 1e-9);
-  for (int it = 0; it < 40; ++it) {
-    const double g = binom_upper_tail(x, Q, h) - u;
-    if (g > 0.0) hi = x; else lo = x;
-    double dens = cq;
-    for (int i = 0; i < h - 1; ++i) dens *= x * (1.0 - x);   // Q = 2h - 1: x^(h-1) (1-x)^(h-1)
-    double xn = dens > 0.0 ? x - g / dens : 0.5 * (lo + hi);
-    if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-    const bool done = fabs(xn - x) <= 1e-15 * fmax(fmin(x, 1.0 - x), 1e-300) || hi - lo <= 1e-16;
-    x = xn;
-    if (done) break;
-  }
-  return x;
-}
+// x* = G^-1(u), after which the draw is ONE inverse-CDF walk of F to x* - no
+// per-draw sorting (Utility.py:534-572's median over Q repetitions, exact
+// law).
 
 // exact draw of the median of Q (odd) iid AE estimates for small M: the
 // value classes t = min(j, M - j) in increasing sin^2 order, their masses
 // p(t) + p(M - t) accumulated until F(t) >= x* (fp64 angle-addition
-// recurrence, no transcendental per step)
+// recurrence, no transcendental per step).  F(t) >= x* = G^-1(u) iff
+// G(F(t)) >= u (G increasing), so the walk tests G(F(t)) >= u directly: one
+// binomial tail per class step instead of a Newton solve for x* (~5-8 tail
+// + density evaluations and a division per lane, divergent) - the walk to
+// the median's class is short (its value is near the pair's a).
 SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
   const double PI = 3.14159265358979323846;
   const double fl = floor(omega);
@@ -115,7 +96,7 @@ SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
     const double v = sin(PI * (double)j / Md);
     return v * v;
   }
-  const double xs = median_order_stat(u, Q);
+  const int h = (Q + 1) / 2;
   const double sp = sin(PI * phi);
   const double num = sp * sp / (Md * Md);
   const double alpha = PI / Md, beta = PI * omega / Md;
@@ -135,7 +116,7 @@ SQ_DEV double ae_median_walk(double omega, long long M, int Q, double u) {
     }
     F += mass;
     v = st * st;
-    if (F >= xs) return v;
+    if (binom_upper_tail(F, Q, h) >= u) return v;
     const double nst = st * ca + ct * sa;
     ct = ct * ca - st * sa;
     st = nst;

@@ -925,47 +925,75 @@ SQ_DEV int seg_append_pos(bool take, int value, int* __restrict__ seg, int* lcnt
   return p;
 }
 
+// The restarts' pointers, staged once per workgroup in LDS and moved to
+// SGPRs at each use (reading them from the pointer table in the row loop
+// re-loads them after every global store - the compiler cannot rule out
+// that a store aliases the table - and a lane-varying table read puts a
+// dependent load in front of every row access).
+template <typename P_>
+SQ_DEV P_ uni_ptr(unsigned long long v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+  return reinterpret_cast<P_>(((unsigned long long)hi << 32) | lo);
+}
+enum ScrPtr { S_CL = 0, S_NEAR, S_MPREV, S_DPREV, S_MCUR, S_CC, S_BP, S_NP };
+
 __global__ void __launch_bounds__(256) kmpp_screen_fused_kernel(KppArgs a) {
   __shared__ int lcnt;
+  __shared__ unsigned long long sp[16][S_NP];
   const int blk = blockIdx.x;
   const int prev = 1 - a.cur;
   const long long r0 = (long long)blk * a.R;
   const long long r1 = r0 + a.R < a.n ? r0 + a.R : a.n;
   if (threadIdx.x == 0) lcnt = 0;
+  if (threadIdx.x < a.nr) {
+    const int r = threadIdx.x;
+    sp[r][S_CL] = (unsigned long long)a.tab[(size_t)r * kKppNF + F_CLOSEST];
+    sp[r][S_NEAR] = (unsigned long long)a.tab[(size_t)r * kKppNF + F_NEAREST];
+    sp[r][S_MPREV] = (unsigned long long)a.tab[(size_t)r * kKppNF + F_MASK0 + prev];
+    sp[r][S_DPREV] = (unsigned long long)a.tab[(size_t)r * kKppNF + F_D0 + prev];
+    sp[r][S_MCUR] = (unsigned long long)a.tab[(size_t)r * kKppNF + F_MASK0 + a.cur];
+    sp[r][S_CC] = (unsigned long long)a.tab[(size_t)r * kKppNF + F_CC];
+    sp[r][S_BP] = (unsigned long long)(long long)(a.c_prev >= 0 ? *kf<const int*>(a, r, F_BEST) : -1);
+  }
   __syncthreads();
   for (long long i0 = r0; i0 < r1; i0 += 256) {
     const long long i = i0 + threadIdx.x;
     unsigned bits = 0;
     if (i < r1) {
-      // all restarts' loads first (independent), then the dependent ones
-      float cl[16];
-      int c[16], bp[16];
-      uint16_t mp[16];
+      // four restarts at a time: their loads first (no store in between:
+      // all in flight), then the lazy winner's rows, the stores and the
+      // triangle tests
+      for (int r4 = 0; r4 < a.nr; r4 += 4) {
+        float cl[4];
+        int c[4];
+        unsigned mp[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (r < a.nr) {
-          bp[r] = a.c_prev >= 0 ? *kf<const int*>(a, r, F_BEST) : -1;
-          cl[r] = kf<const float*>(a, r, F_CLOSEST)[i];
-          c[r] = kf<const int*>(a, r, F_NEAREST)[i];
-          mp[r] = bp[r] >= 0 ? kf<const uint16_t*>(a, r, F_MASK0 + prev)[i] : (uint16_t)0;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (r < a.nr) {
-          if (bp[r] >= 0 && ((mp[r] >> bp[r]) & 1u)) {
-            cl[r] = kf<const float*>(a, r, F_D0 + prev)[(size_t)bp[r] * a.n + i];
-            c[r] = a.c_prev;
-            kf<float*>(a, r, F_CLOSEST)[i] = cl[r];
-            kf<int*>(a, r, F_NEAREST)[i] = c[r];
+        for (int u = 0; u < 4; ++u) {
+          const int r = r4 + u;
+          if (r < a.nr) {
+            const int bp = (int)(long long)sp[r][S_BP];
+            cl[u] = uni_ptr<const float*>(sp[r][S_CL])[i];
+            c[u] = uni_ptr<const int*>(sp[r][S_NEAR])[i];
+            mp[u] = bp >= 0 ? uni_ptr<const uint16_t*>(sp[r][S_MPREV])[i] : 0u;
           }
-          kf<uint16_t*>(a, r, F_MASK0 + a.cur)[i] = 0;
         }
-      }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (r < a.nr && cl[r] > 0.0f && !(kf<const float*>(a, r, F_CC)[c[r]] > 4.01f * cl[r]))
-          bits |= 1u << r;
+        for (int u = 0; u < 4; ++u) {
+          const int r = r4 + u;
+          if (r < a.nr) {
+            const int bp = (int)(long long)sp[r][S_BP];
+            if (bp >= 0 && ((mp[u] >> bp) & 1u)) {
+              cl[u] = uni_ptr<const float*>(sp[r][S_DPREV])[(size_t)bp * a.n + i];
+              c[u] = a.c_prev;
+              uni_ptr<float*>(sp[r][S_CL])[i] = cl[u];
+              uni_ptr<int*>(sp[r][S_NEAR])[i] = c[u];
+            }
+            uni_ptr<uint16_t*>(sp[r][S_MCUR])[i] = 0;
+            if (cl[u] > 0.0f && !(uni_ptr<const float*>(sp[r][S_CC])[c[u]] > 4.01f * cl[u]))
+              bits |= 1u << r;
+          }
+        }
       }
     }
     const int p = seg_append_pos(bits != 0u, (int)i, a.useg + r0, &lcnt);
@@ -1093,8 +1121,13 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
   __shared__ float cpar[kScol][3];
   __shared__ int lcnt[16];
   __shared__ float sclo[NWV * 256];
+  __shared__ unsigned long long spc[16], spe[16];   // closest / exact of each restart
   const int blk = blockIdx.x;
   const int tp = a.tp, t = a.t, nr = a.nr;
+  if (threadIdx.x < nr) {
+    spc[threadIdx.x] = (unsigned long long)a.tab[(size_t)threadIdx.x * kKppNF + F_CLOSEST];
+    spe[threadIdx.x] = (unsigned long long)a.tab[(size_t)threadIdx.x * kKppNF + F_EXACT];
+  }
   const int ncol = nr * tp, ncb = (ncol + 15) / 16;
   auto cb = [&](int hl, int col) -> int8_t* { return cbs + ((size_t)hl * ncb * 16 + col) * DQ; };
   // stage every restart's trials: column c = r tp + j (j >= t: zero)
@@ -1154,7 +1187,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
     for (int u = 0; u < 4; ++u) {
       const int rr = kb + 4 * u;
       ncl[u] = (nrow >= 0 && rr < nr && ((nbits >> rr) & 1u))
-                   ? kf<const float*>(a, rr, F_CLOSEST)[nrow] : 0.0f;
+                   ? reinterpret_cast<const float*>(spc[rr])[nrow] : 0.0f;
     }
   };
   prefetch(wave * 16);
@@ -1177,6 +1210,21 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) gbits |= (unsigned)__shfl_xor((int)gbits, o, 64);
     gbits = (unsigned)__builtin_amdgcn_readfirstlane((int)gbits);
+    // the row of each result register (row slot 4 kb + i) and its scalars,
+    // the same for every column block
+    int rrv[4];
+    unsigned rbv[4];
+    float sv[4], erv[4], Av[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int src = 4 * kb + i;
+      rrv[i] = __shfl(row, src, 64);
+      rbv[i] = (unsigned)__shfl((int)bits, src, 64);
+      sv[i] = __shfl(rs, src, 64);
+      erv[i] = __shfl(re_, src, 64);
+      const float q2 = (float)__shfl(rq2, src, 64);
+      Av[i] = sv[i] * sv[i] * q2;
+    }
     for (int cbk = 0; cbk < ncb; ++cbk) {
       const unsigned bm = ((1u << rpb) - 1u) << (cbk * rpb);
       if (!(gbits & bm)) continue;
@@ -1196,15 +1244,11 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int src = 4 * kb + i;   // the row slot of result register i
-        const int rr = __shfl(row, src, 64);
-        const unsigned rb = (unsigned)__shfl((int)bits, src, 64);
-        const float s = __shfl(rs, src, 64);
-        const float er = __shfl(re_, src, 64);
-        const float q2 = (float)__shfl(rq2, src, 64);
+        const int rr = rrv[i];
+        const float s = sv[i], er = erv[i], A = Av[i];
         bool need = false;
-        if (jv && rr >= 0 && ((rb >> r) & 1u)) {
+        if (jv && rr >= 0 && ((rbv[i] >> r) & 1u)) {
           const float cl = scl[src * 16 + r];
-          const float A = s * s * q2;
           const float dot = s * sc * ((float)hi[i] + (float)lo[i] * (1.0f / 254.0f));
           const float Dq = (A + cc2) - 2.0f * dot;
           const float Dlb = Dq - 1e-6f * (A + cc2 + 2.0f * fabsf(dot));
@@ -1227,7 +1271,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
         if (rp >= nr) break;
         const bool take = lane < 16 && row >= 0 &&
                           (((unsigned)(bi >> (16 * q + p * tp))) & tmask) != 0u;
-        seg_append(take, row, kf<int*>(a, rp, F_EXACT) + r0, &lcnt[rp]);
+        seg_append(take, row, uni_ptr<int*>(spe[rp]) + r0, &lcnt[rp]);
       }
     }
   }
