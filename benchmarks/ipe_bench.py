@@ -61,7 +61,8 @@ def main():
         st16 = dict(zip(names16, eng.ipe16_stats.tolist()))
         i16 = getattr(eng, "_ipe16", None)
         tau = float(i16.smax.item()) if i16 is not None and i16.skip else None
-        out["steps"].append({"ms": round(ms, 2), "tau": tau, **st,
+        wild = getattr(i16, "last_wild", None) if i16 is not None else None
+        out["steps"].append({"ms": round(ms, 2), "tau": tau, "wild": wild, **st,
                              **{"i16_" + k: v for k, v in st16.items()}})
         print(json.dumps(out["steps"][-1]), flush=True)
     # timed without stats (the production kernel)

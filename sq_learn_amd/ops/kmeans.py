@@ -1308,10 +1308,19 @@ class Ipe16:
         W = min(self.n_wild, k)
         if self.C_prev is not None and self.C_prev.shape == C32.shape:
             sh = (C64 - self.C_prev.double()).pow(2).sum(1).sqrt() * (1.0 + 1e-9)
+            # adaptive wild set: at least n_wild, and every centroid that moved
+            # more than 1 % of the median nearest-centroid distance (up to
+            # k / 2) - a few hundred centroids contesting unclaimed blobs jump
+            # by ~10 units per IPE step at 10M x 256 while the rest barely
+            # move, and a kept bound decays by tau every step
+            Dn = Dlo + torch.diag(torch.full((k,), float("inf"), dtype=torch.float64, device=dev))
+            tgt = 0.01 * Dn.amin(1).median()
+            W = int(min(max(W, int((sh > tgt).sum())), max(k // 2, 1)))
             top = torch.topk(sh, min(W + 1, k)).values
             tau = top[W] if k > W else torch.zeros((), dtype=torch.float64, device=dev)
             self.smax.copy_(torch.nextafter(tau.float(), inf).reshape(1))
             wild = sh > tau
+            self.last_wild = W
         else:
             wild = torch.zeros(k, dtype=torch.bool, device=dev)
         Dw = torch.where(wild[None, :] & ~torch.eye(k, dtype=torch.bool, device=dev), Dlo,
