@@ -44,6 +44,8 @@ def main():
     prev_skip = None
     for s in range(steps):
         C = eng.centers().clone().double()
+        st0 = getattr(eng, "_ipe16", None)
+        lb_before = st0.lb[sub].double().clone() if st0 is not None else None
         eng.ipe16_stats.zero_()
         lab, sc = eng.step()
         sc.tolist()
@@ -69,7 +71,16 @@ def main():
         # per-group upper condition (need_hi per group vs dh + Rc[hint][g])
         Rcg = st.Rc[hint.clamp_min(0)].double()[:, :st.G]
         up_ok = ((dh[:, None] + Rcg) ** 2 <= vhi / a2 + (X[sub].double() ** 2).sum(1)[:, None]).all(1)
-        lo_ok = (lbv - float(st.smax)).clamp_min(0) ** 2 >= need_lo
+        lbb = lb_before if lb_before is not None else lbv
+        lo_ok = (lbb - float(st.smax)).clamp_min(0) ** 2 >= need_lo
+        sw = ~skipped
+        fails = {"swept": int(sw.sum()),
+                 "lo_fail_only": float((sw & ~lo_ok & up_ok).double().sum() / max(int(sw.sum()), 1)),
+                 "up_fail_only": float((sw & lo_ok & ~up_ok).double().sum() / max(int(sw.sum()), 1)),
+                 "both_fail": float((sw & ~lo_ok & ~up_ok).double().sum() / max(int(sw.sum()), 1)),
+                 "neither_fail": float((sw & lo_ok & up_ok).double().sum() / max(int(sw.sum()), 1)),
+                 "up_ratio_q(swept)": q(((dh[:, None] + Rcg).amax(1) ** 2 /
+                                        (vhi / a2 + (X[sub].double() ** 2).sum(1)[:, None]).amin(1))[sw])}
         mw_ok = mwv.clamp_min(0) ** 2 >= need_lo
         trans = {}
         if prev_skip is not None:
@@ -81,7 +92,7 @@ def main():
                              "lbe_minus_needlo_q": q((lbv - float(st.smax) - need_lo.clamp_min(0).sqrt())[m])}
         prev_skip = skipped
         rec = {"step": s, "smax": float(st.smax), "skipped": int(eng.ipe16_stats[7]),
-               "trans": trans,
+               "trans": trans, "fails": fails,
                "Rc_q": q(st.Rc[:k]), "lb_over_true_q": q((lbv / dmin)[lbv > 0]),
                "lb_zero_frac": float((lbv == 0).double().mean()),
                "lb_q": q(lbv), "dmin_q": q(dmin),

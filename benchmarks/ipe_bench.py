@@ -62,6 +62,7 @@ def main():
         i16 = getattr(eng, "_ipe16", None)
         tau = float(i16.smax.item()) if i16 is not None and i16.skip else None
         wild = getattr(i16, "last_wild", None) if i16 is not None else None
+        wild = int(wild) if wild is not None else None
         out["steps"].append({"ms": round(ms, 2), "tau": tau, "wild": wild, **st,
                              **{"i16_" + k: v for k, v in st16.items()}})
         print(json.dumps(out["steps"][-1]), flush=True)

@@ -23,14 +23,11 @@
 //  * sweep (fp16 v_mfma_f32_32x32x16_f16 over the fp16 copy of alpha x, the
 //    estep_x64 tile ring): a pair is FAR (per-pair cost: one med3 and one
 //    compare) or NEAR (appended to its row's LDS list).  Far pairs never read
-//    their inner product: each (row, column class) stream spends H_row per
-//    pair from an Exp(1) budget (the memoryless construction of ipe.hip), so
-//    its fire positions are known in advance from the budgets alone - they
-//    are listed at the start of the row block, from per-row budgets drawn
-//    hierarchically (the min of the row's 32 Exp(1) ~ Exp(32) from ONE
-//    uniform; only when that min could run out within the row - a few % of
-//    the rows - are the 32 stream budgets drawn: argmin uniform, the others
-//    min + Exp(1));
+//    their inner product: each fires with probability 1 - exp(-H_row),
+//    independently (the memoryless budget construction of ipe.hip), so the
+//    fire positions are known in advance - prep draws them per row (a
+//    binomial count, then a uniform subset of the pairs) and evaluates the
+//    fired pairs itself;
 //  * near kernel: every listed pair gets the canonical fp32 inner product;
 //    a near pair is sampled in full (ipe_distance, the pair's own Philox
 //    stream), a fired far pair is thinned to the exact law of "D~ if <= thr"
@@ -441,45 +438,46 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       cut.ok = nok > 0;
     }
     if (cut.ok) {
-      // The row's 32 (column class) streams spend H per pair from iid Exp(1)
-      // budgets.  Only budgets below H times the longest stream can run out:
-      // they are drawn in increasing order (Renyi: E_(i+1) = E_(i) +
-      // Exp(1) / (32 - i)), each handed to a uniformly chosen unused stream,
-      // until one exceeds that - ~H 32 k/32 draws per row, not 32.  A stream
-      // fires at pair p = floor(E / H) (j = s + 32 p), then redraws (block
-      // 2 + 2 p of its skey stream, as the near kernel's thinning reads).
+      // Each far pair fires with probability b = 1 - exp(-H), independently
+      // (a stream spending H per pair from a memoryless Exp(1) budget):
+      // the row's fires are N ~ Binomial(k, b) by inversion (P(0) =
+      // exp(-k H), P(n + 1) / P(n) = (k - n) / (n + 1) (e^H - 1)) and, given
+      // N, a uniform N-subset of the k pairs (Lemire integers, duplicates
+      // redrawn) - one exp and ~N Philox words per row, no per-fire log.
+      // More than kFireCap fires: the row is dense.
       const double H = (double)cut.H;
-      const int P = (a.k + 31) >> 5;
-      const double Tcap = (SQ_IPE16_DIAG & 2) ? 0.0 : H * (double)P;
-      WordStream ws(a.bkey, (unsigned long long)g);
-      double E = 0.0;
-      unsigned long long unused = 0xFFFFFFFFull;
-      for (int i = 0; i < 32; ++i) {
+      if (!(SQ_IPE16_DIAG & 2)) {
+        WordStream ws(a.bkey, (unsigned long long)g);
         const uint32_t w0 = ws.next(), w1 = ws.next();
-        E += -log(u53(w0, w1)) / (double)(32 - i);
-        if (!(E < Tcap)) break;
-        // exact uniform on [0, 32 - i) (Lemire: multiply, reject the bias zone)
-        const uint32_t m = (uint32_t)(32 - i);
-        uint32_t wv = ws.next();
-        unsigned long long xm = (unsigned long long)wv * m;
-        const uint32_t thr = (uint32_t)(-m) % m;
-        while ((uint32_t)xm < thr) {
-          wv = ws.next();
-          xm = (unsigned long long)wv * m;
+        const double u = u53(w0, w1);
+        double pn = exp(-(double)a.k * H);
+        double cdf = pn;
+        const double rat = expm1(H);
+        int N = 0;
+        while (u > cdf && N <= kFireCap) {
+          pn *= (double)(a.k - N) / (double)(N + 1) * rat;
+          cdf += pn;
+          ++N;
         }
-        const int sidx = nth_set_bit(unused, (int)(xm >> 32));
-        unused &= ~(1ull << sidx);
-        const int Ps = (a.k - sidx + 31) >> 5;
-        double p = floor(E / H);
-        while (p < (double)Ps) {
-          const int pi = (int)p;
-          if (nf < kFireCap) fire[nf] = (uint16_t)((sidx + 32 * pi) | 0x8000);
-          ++nf;
-          WordStream wr(a.skey, (unsigned long long)g * 32ull + (unsigned long long)sidx);
-          wr.b = (uint32_t)(2 + 2 * pi);
-          const uint32_t r0 = wr.next(), r1 = wr.next();
-          p += 1.0 + floor(-log(u53(r0, r1)) / H);
+        const uint32_t km = (uint32_t)a.k;
+        const uint32_t kthr = (uint32_t)(-km) % km;
+        for (int e = 0; e < N && e < kFireCap; ++e) {
+          uint32_t j = 0;
+          bool dup = true;
+          while (dup) {
+            uint32_t wv = ws.next();
+            unsigned long long xm = (unsigned long long)wv * km;
+            while ((uint32_t)xm < kthr) {
+              wv = ws.next();
+              xm = (unsigned long long)wv * km;
+            }
+            j = (uint32_t)(xm >> 32);
+            dup = false;
+            for (int f = 0; f < e; ++f) dup = dup || (fire[f] & 0x3FFFu) == j;
+          }
+          fire[e] = (uint16_t)(j | 0x8000u);
         }
+        nf = N;
       }
       st_flag = nf > 0 ? 1 : 0;
       if (nf > kFireCap) cut.ok = 0;   // a row this hot: dense

@@ -1313,26 +1313,30 @@ class Ipe16:
             # k / 2) - a few hundred centroids contesting unclaimed blobs jump
             # by ~10 units per IPE step at 10M x 256 while the rest barely
             # move, and a kept bound decays by tau every step
+            # (device-side: no host read of the count)
             Dn = Dlo + torch.diag(torch.full((k,), float("inf"), dtype=torch.float64, device=dev))
             tgt = 0.01 * Dn.amin(1).median()
-            W = int(min(max(W, int((sh > tgt).sum())), max(k // 2, 1)))
-            top = torch.topk(sh, min(W + 1, k)).values
-            tau = top[W] if k > W else torch.zeros((), dtype=torch.float64, device=dev)
+            Wd = (sh > tgt).sum().clamp(min=W, max=max(k // 2, 1)).clamp(max=k - 1)
+            srt = torch.sort(sh, descending=True).values
+            tau = srt.gather(0, Wd.reshape(1))[0] if k > W else torch.zeros(
+                (), dtype=torch.float64, device=dev)
             self.smax.copy_(torch.nextafter(tau.float(), inf).reshape(1))
             wild = sh > tau
-            self.last_wild = W
+            self.last_wild = Wd
         else:
             wild = torch.zeros(k, dtype=torch.bool, device=dev)
         Dw = torch.where(wild[None, :] & ~torch.eye(k, dtype=torch.bool, device=dev), Dlo,
                          torch.full_like(Dlo, float("inf")))
         self.mw[:k].copy_(torch.nextafter(Dw.amin(1).float(), -inf))
         # centroid -> norm group (operand column order: perm, group starts)
-        col = torch.empty(k, dtype=torch.int64, device=dev)
-        col[self.perm.long()] = torch.arange(k, device=dev)
-        gs = torch.tensor(self.gstart[1:4], device=dev)
-        grp = ((col // 64)[:, None] >= gs[None, :]).sum(1)
-        Rc = torch.full((k, 4), 0.0, dtype=torch.float64, device=dev)
-        Rc.scatter_reduce_(1, grp[None, :].expand(k, k), Dhi, reduce="amax", include_self=True)
+        # (operand column order = the groups' contiguous tile ranges)
+        Dp = Dhi.index_select(1, self.perm.long())
+        Rc = torch.zeros((k, 4), dtype=torch.float64, device=dev)
+        for g in range(self.G):
+            c0 = min(64 * self.gstart[g], k)
+            c1 = min(64 * self.gstart[g + 1], k) if g + 1 < self.G else k
+            if c1 > c0:
+                Rc[:, g] = Dp[:, c0:c1].amax(1)
         self.Rc[:k].copy_(torch.nextafter(Rc.float(), inf))
         self.C_prev = C32.clone()
 
