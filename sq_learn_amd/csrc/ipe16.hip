@@ -45,6 +45,7 @@
 // lane c16 of a 16-lane group sums f = c16, c16 + 16, ... by fmaf in order,
 // then an xor tree over the 16 lanes (ipe_hint_kernel's order).
 #include "ipe_law.h"
+#include <cmath>
 #include <utility>
 
 namespace sq {
@@ -148,6 +149,12 @@ struct Cut {
 struct CutParams {
   double alpha, Ch, sub_rel, mt, min_width;
   int d;
+  // per-launch constants of row_cut (host: cut_constants): the per-row
+  // band then costs 6 fp64 sqrt and 2 divisions per group instead of 8
+  // sqrt, 8 divisions and a pow
+  double c, inv_c, kqm, mt_e, a, inv2a, mtk, klo, khi;
+  float Hf;
+  int band_ok;
 };
 
 // The row's exact squared norm range [x2lo, x2hi] (fp32 |x|^2 with its
@@ -200,37 +207,39 @@ SQ_DEV float pair_dist_lo(float ip, float nx2, float ny2, int d) {
 SQ_DEV Cut row_cut(float nx2f, float sthrf, float ktf, float Sminf, float Smaxf, const IpeScreen& sc,
                    const CutParams& cp) {
   Cut out{__builtin_inff(), -__builtin_inff(), 0.0f, 0};
+  if (!cp.band_ok) return out;                                        // c2, c3 (m_t, pu)
   const double Smin = Sminf, Smax = Smaxf, kq = sc.kq, kt = ktf;
   const double sthr = (double)sthrf * (1.0 + 1e-7);
-  const double c = (1.0 - 4.8828125e-4) * (1.0 - 1e-6);   // sD = sqrt(D) (1 - 2^-11), rounded
-  const double kqm = kq * (1.0 - 3e-5);                    // sqrt / rcp / products of P and m
-  const double mt = cp.mt * (1.0 + 1e-6);
   if (!(Smin > 0.0) || !(sthr < 1e300)) return out;
-  const double Pmax = kq * sqrt(Smax) * (1.0 + 1e-5);
+  const double rSmin = sqrt(Smin), rSmax = sqrt(Smax);
+  const double Pmax = kq * rSmax * (1.0 + 1e-5);
   if (!(kt * Pmax + 2.2 <= 1048576.0 * (1.0 - 1e-6))) return out;    // walk cap (c2)
   if (!(Smax * (1.0 + 1e-5) < (double)sc.smax)) return out;           // M cap (c2)
-  double ylo = sqrt(Smax * 0x1p-12 * (1.0 + 1e-5));                   // c1
-  double yhi = sqrt(Smin * 1.998046875 * (1.0 - 1e-5));
+  // sqrt(Smax 2^-12 (1 + 1e-5)) and sqrt(Smin 1.998046875 (1 - 1e-5)) (c1)
+  // as products with constants (the few-ulp differences are inside the
+  // 1e-9 margins below)
+  double ylo = rSmax * cp.klo;
+  double yhi = rSmin * cp.khi;
   // |ip| <= |S - D| / 2 (1 + 1e-6) + 1e-6 S: m >= mt  <=>
   //   kqm sqrt(S) (c y - sthr) >= mt max(1, |S - y^2| (1 + 1e-6) / 2 + 1e-6 S)
-  const double e1 = 1.0 + 1e-6;
+  const double a = cp.a;
   for (int side = 0; side < 2; ++side) {
     const double S = side ? Smax : Smin;
-    const double rS = sqrt(S);
-    const double B = 2.0 * kqm * rS * c;
-    const double C0 = 2.0 * kqm * rS * sthr;
-    const double a = mt * e1;
-    const double sl = 2e-6 * mt * S;
+    const double rS = side ? rSmax : rSmin;
+    const double B = 2.0 * cp.kqm * rS * cp.c;
+    const double C0 = 2.0 * cp.kqm * rS * sthr;
+    const double sl = 2e-6 * cp.mt_e * S;
     // max(1, .) = 1 part: c y - sthr >= mt / (kqm rS)
-    const double y0 = (mt / (kqm * rS) + sthr) / c;
+    const double y0 = (cp.mtk / rS + sthr) * cp.inv_c;
     // below S: a y^2 + B y - (a S + sl + C0) >= 0
     const double cA = a * S + sl + C0;
-    const double yA = (-B + sqrt(B * B + 4.0 * a * cA)) / (2.0 * a);
+    const double yA = (-B + sqrt(B * B + 4.0 * a * cA)) * cp.inv2a;
     // above S: a y^2 - B y + (C0 + sl - a S) <= 0
     const double dB = B * B - 4.0 * a * (C0 + sl - a * S);
     if (!(dB >= 0.0)) return out;
-    const double yB = (B + sqrt(dB)) / (2.0 * a);
-    const double yBm = (B - sqrt(dB)) / (2.0 * a);
+    const double sdB = sqrt(dB);
+    const double yB = (B + sdB) * cp.inv2a;
+    const double yBm = (B - sdB) * cp.inv2a;
     // m >= mt on {y >= yA} (below-S branch) intersected with [yBm, yB]
     ylo = fmax(ylo, fmax(y0, fmax(yA, yBm)) * (1.0 + 1e-9));
     yhi = fmin(yhi, yB * (1.0 - 1e-9));
@@ -240,28 +249,45 @@ SQ_DEV Cut row_cut(float nx2f, float sthrf, float ktf, float Sminf, float Smaxf,
   // a sliver of a band (a row whose threshold sits among the other
   // centroids) would list most of its pairs: dense from the start
   if (Dh - Dl < cp.min_width * Dl) return out;
-  const double m = cp.mt;
-  const double r = (1.0 / m) * (1.0 + 1e-5);
-  const double pb = (r + r * r) * 0.500012 * (1.0 + 1e-5);
-  const double pu = (double)sc.cqh * pow(pb, (double)sc.hf) * (1.0 + 2e-3);
-  if (!(m >= 3.0) || !(pu < 9.765625e-4 * (1.0 - 1e-6))) return out;  // c2, c3
-  const double H = pu * (1.0 + pu) * (1.0 + 1e-6);                     // >= -log(1 - pu)
   // -> fp16 filter units: v = alpha^2 (D - |x|^2) +- E
   const double errD = (3.0 * cp.d + 64.0) * 0x1p-24 * Smax;           // law D vs exact D
   const RowErr re = row_err(nx2f, cp);
   const double a2 = cp.alpha * cp.alpha;
   const double vlo = a2 * (Dl + errD - re.x2lo) + re.E;
   const double vhi = a2 * (Dh - errD - re.x2hi) - re.E;
-  float flo = (float)vlo, fhi = (float)vhi, Hf = (float)H;
+  float flo = (float)vlo, fhi = (float)vhi;
   if ((double)flo < vlo) flo = f32_up(flo);
   if ((double)fhi > vhi) fhi = -f32_up(-fhi);
-  if ((double)Hf < H) Hf = f32_up(Hf);
   if (!(flo <= fhi)) return out;
   out.vlo = flo;
   out.vhi = fhi;
-  out.H = Hf;
+  out.H = cp.Hf;   // depends on m_t only
   out.ok = 1;
   return out;
+}
+
+// row_cut's per-launch constants (the margins of the per-row version they
+// replace: c, kqm, mt's (1 + 1e-6); pu(m_t) and H >= -log(1 - pu) rounded up)
+static void cut_constants(CutParams& cp, const IpeScreen& sc) {
+  const double e1 = 1.0 + 1e-6;
+  cp.c = (1.0 - 4.8828125e-4) * (1.0 - 1e-6);   // sD = sqrt(D) (1 - 2^-11), rounded
+  cp.inv_c = (1.0 / cp.c) * (1.0 + 1e-15);
+  cp.kqm = (double)sc.kq * (1.0 - 3e-5);         // sqrt / rcp / products of P and m
+  cp.mt_e = cp.mt * (1.0 + 1e-6);
+  cp.a = cp.mt_e * e1;
+  cp.inv2a = (1.0 / (2.0 * cp.a)) * (1.0 + 1e-15);
+  cp.mtk = cp.mt_e / cp.kqm * (1.0 + 1e-15);
+  cp.klo = sqrt(0x1p-12 * (1.0 + 1e-5)) * (1.0 + 1e-15);
+  cp.khi = sqrt(1.998046875 * (1.0 - 1e-5)) * (1.0 - 1e-15);
+  const double m = cp.mt;
+  const double r = (1.0 / m) * (1.0 + 1e-5);
+  const double pb = (r + r * r) * 0.500012 * (1.0 + 1e-5);
+  const double pu = (double)sc.cqh * pow(pb, (double)sc.hf) * (1.0 + 2e-3);
+  cp.band_ok = (m >= 3.0 && pu < 9.765625e-4 * (1.0 - 1e-6)) ? 1 : 0;   // c2, c3
+  const double H = pu * (1.0 + pu) * (1.0 + 1e-6);                       // >= -log(1 - pu)
+  float Hf = (float)H;
+  if ((double)Hf < H) Hf = std::nextafter(Hf, 1e30f);
+  cp.Hf = Hf;
 }
 
 // ------------------------------------------------------------------ prep
@@ -1412,6 +1438,7 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.cp.mt = da[2];
     a.cp.min_width = da[3];
     a.cp.d = d;
+    cut_constants(a.cp, sc);
     a.stats = (unsigned long long*)P(24);
     a.lb = (float*)P(51);
     a.lb_ok = (int)ia[52];

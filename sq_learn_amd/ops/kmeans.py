@@ -1237,9 +1237,10 @@ class Ipe16:
         # per-pair hazard of the far band (the band edge's worst case): the
         # row fires somewhere with probability ~ k * ht; a larger ht narrows
         # the near set, a smaller one lists fewer fires
-        # (a fired far pair costs one inner product and a thinning test; a
-        # near pair a full median-of-Q sampler: a high target pays)
-        self.ht = float(__import__("os").environ.get("SQ_IPE16_HT", "9e-4"))
+        # (a fired far pair costs one inner product and a thinning test in
+        # prep; a near pair the sweep's listing and a full sampler).  10M x
+        # 256, k = 1024: 2e-4 / 4e-4 / 9e-4 -> 13.4 / 13.1 / 13.7 ms per step
+        self.ht = float(os.environ.get("SQ_IPE16_HT", "4e-4"))
         # bands narrower than this fraction of their lower edge: dense
         self.min_width = float(__import__("os").environ.get("SQ_IPE16_MINW", "0.5"))
         self.last_dense = 0
