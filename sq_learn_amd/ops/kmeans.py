@@ -1382,19 +1382,23 @@ class Ipe16:
         cnt = np.array([max(0, min(64, k - 64 * t)) for t in range(nt)], dtype=np.float64)
         ccnt = np.concatenate([[0.0], np.cumsum(cnt)])
 
-        def cost(a, b):   # tiles [a, b)
-            return (ccnt[b] - ccnt[a]) * (hi[b - 1] - lo[a])
-
+        # cost[a, b] of tiles [a, b) (a < b), vectorised (a Python triple
+        # loop cost ~0.2 ms of host time per IPE step)
         inf = float("inf")
+        A = np.arange(nt + 1)
+        valid = A[:, None] < A[None, :]
+        hib = np.concatenate([[0.0], hi])          # hi[b - 1] at index b
+        lo1 = np.concatenate([lo, [0.0]])
+        cost = np.where(valid, (ccnt[None, :] - ccnt[:, None]) * (hib[None, :] - lo1[:, None]), inf)
         best = np.full((G + 1, nt + 1), inf)
         arg = np.zeros((G + 1, nt + 1), dtype=np.int64)
         best[0, 0] = 0.0
         for g in range(1, G + 1):
-            for b in range(g, nt + 1):
-                for a in range(g - 1, b):
-                    c = best[g - 1, a] + cost(a, b)
-                    if c < best[g, b]:
-                        best[g, b], arg[g, b] = c, a
+            tot = best[g - 1][:, None] + cost          # [a, b]
+            tot[: g - 1, :] = inf                      # a >= g - 1
+            arg[g] = np.argmin(tot, axis=0)            # first minimum: the loop's a order
+            best[g] = tot[arg[g], A]
+            best[g, :g] = inf
         cuts, b = [], nt
         for g in range(G, 0, -1):
             a = int(arg[g, b])
