@@ -1,7 +1,8 @@
 """Where ipe16_prep_kernel's time goes: timing-only variant libraries built
 with SQ_IPE16_DIAG bits (csrc/ipe16.hip: 1 no hint sampler, 2 no fire
-listing, 4 no fired-pair evaluation, 8 one band for all groups - results
-not the law's), each the production objects relinked with one recompiled
+listing, 4 no fired-pair evaluation, 8 one band for all groups, 16 no
+near-pair flush in the sweep, 32 no far-minimum upkeep - results not the
+law's), each the production objects relinked with one recompiled
 ipe16.hip.
 
     python benchmarks/ipe16_prep_variants.py --build    (CPU)
@@ -13,7 +14,7 @@ import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "benchmarks", "_ipev")
-VARIANTS = {"d0": 0, "d1": 1, "d2": 2, "d4": 4, "d8": 8, "d15": 15}
+VARIANTS = {"d0": 0, "d16": 16, "d32": 32, "d48": 48}
 
 
 def build():

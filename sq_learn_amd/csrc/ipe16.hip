@@ -57,7 +57,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // Timing-only variant builds (benchmarks/ipe16_prep_variants.py): bits of
 // SQ_IPE16_DIAG drop parts of prep - 1: the hint's sampler (thr = the fp32
 // distance), 2: the budget / fire listing, 4: the fired pairs' evaluation,
-// 8: the per-group bands (group 0's for all).  Results are NOT the law's;
+// 8: the per-group bands (group 0's for all), 16: the sweep's near-pair
+// flush (flagged values dropped), 32: the sweep's far-minimum upkeep.
+// Results are NOT the law's;
 // never set in the production build.
 #ifndef SQ_IPE16_DIAG
 #define SQ_IPE16_DIAG 0
@@ -882,7 +884,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     } else {
       const bool far = (v >= lo[st][i]) & (v <= hi[st]);
       nb |= far ? 0u : (1u << (16 * st + i));
-      if constexpr (LB) fm[st][i] = vmin(fm[st][i], far ? v : __builtin_inff());
+      if constexpr (LB && !(SQ_IPE16_DIAG & 32)) fm[st][i] = vmin(fm[st][i], far ? v : __builtin_inff());
     }
   };
   typedef f32x16 Acc[kRS];
@@ -916,6 +918,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   // here would wait for the in-flight tile DMA as well)
   auto flush_near = [&](long long b, int jc, float ny2, const Acc& o) {
     if constexpr (!ARGMIN) {
+      if (SQ_IPE16_DIAG & 16) nb = 0;
       nb &= ~mute;
       if (__ballot(nb != 0u) != 0ull) {
 #pragma unroll
