@@ -573,8 +573,7 @@ __global__ void __launch_bounds__(256) ipe16_prep_kernel(PrepArgs a) {
       }
       a.H[r] = cut.H;
       a.rst[r] = cut.ok ? 0 : 1;
-      // (the sweep lists no fires: prep finished them)
-      a.rfire[(size_t)r * 8] = 0;
+
     }
   }
   // the sweep's row list (one atomic per wave)
@@ -810,6 +809,8 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   float* s_nx2 = sfm + kRows;                                             // [kRows]
   float* s_sthr = s_nx2 + kRows;                                          // [kRows]
   float* s_ea2 = s_sthr + kRows;                                          // [kRows]
+  float* s_lbo = s_ea2 + kRows;                                           // [kRows]
+  int* s_rr = reinterpret_cast<int*>(s_lbo + kRows);                      // [kRows] row | rst << 31
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -995,31 +996,39 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) fm[st][i] = __builtin_inff();
       }
-      // the rows' hints and the fires prep listed (thread t: row t)
-      for (int t = tid; t < kRows; t += kNW * 64) {
+      // the rows' hints, norms, thresholds and bands (thread t: row t; a
+      // row past n: all far).  The row id first, then every load of the row
+      // in flight together (one wait instead of one per load); prep
+      // finishes the fires, so the lists start empty
+      static_assert(kRows == kNW * 64, "one row per thread");
+      {
+        const int t = tid;
         const long long p = blk * kRows + t;
-        int c = 0;
-        if (p < n) {
-          const long long r = R(p);
-          shint[t] = a.hj[r];
-          s_nx2[t] = a.xn[r];
-          s_sthr[t] = ipe_sthr(a.thr[r]);
-          s_ea2[t] = a.ea2[r];
-          const uint16_t* fr = a.rfire + (size_t)r * 8;
-          c = fr[0];
-          for (int e = 0; e < c; ++e) nl[t * kNLS + e] = fr[1 + e];
-        } else {
-          shint[t] = -1;
+        const bool pv = p < n;
+        const long long r = pv ? R(p) : 0;
+        const int hj = a.hj[r];
+        const float xn = a.xn[r], th = a.thr[r], e2 = a.ea2[r];
+        const unsigned char rs = a.rst[r];
+        const float lo_r = (LB && a.lb) ? a.lbo[r] : 0.0f;
+        float blo[kMaxG], bhi[kMaxG];
+#pragma unroll
+        for (int q = 0; q < kMaxG; ++q) {
+          const bool v = pv && q < a.G;
+          blo[q] = v ? a.vlo[r * kMaxG + q] : -__builtin_inff();
+          bhi[q] = v ? a.vhi[r * kMaxG + q] : __builtin_inff();
         }
-        ncnt[t] = c;
-      }
-      // the block's bands (row, group) -> LDS; a row past n: all far
-      for (int e = tid; e < kRows * kMaxG; e += kNW * 64) {
-        const long long p = blk * kRows + e / kMaxG;
-        const bool v = p < n && (e % kMaxG) < a.G;
-        const long long idx = v ? R(p) * kMaxG + e % kMaxG : 0;
-        sband[2 * e] = v ? a.vlo[idx] : -__builtin_inff();
-        sband[2 * e + 1] = v ? a.vhi[idx] : __builtin_inff();
+        shint[t] = pv ? hj : -1;
+        s_nx2[t] = xn;
+        s_sthr[t] = ipe_sthr(th);
+        s_ea2[t] = e2;
+        s_lbo[t] = lo_r;
+        s_rr[t] = (int)r | (rs != 0 ? (int)0x80000000u : 0);
+        ncnt[t] = 0;
+#pragma unroll
+        for (int q = 0; q < kMaxG; ++q) {
+          sband[2 * (t * kMaxG + q)] = blo[q];
+          sband[2 * (t * kMaxG + q) + 1] = bhi[q];
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1100,13 +1109,14 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       __builtin_amdgcn_s_barrier();
       const int t = tid;   // kRows == 256 threads: one row each
       const long long p = blk * kRows + t;
-      const long long r = p < n ? R(p) : 0;
+      const int rrw = s_rr[t];   // (the prologue's row id and dense flag)
+      const long long r = p < n ? (long long)(rrw & 0x7FFFFFFF) : 0;
       int c = 0;
       bool dense = false;
       uint16_t* row_l = nl + t * kNLS;
       if (p < n) {
         c = ncnt[t];
-        dense = c > kCapR || a.rst[r] != 0;
+        dense = c > kCapR || rrw < 0;
         if (dense) {
           c = 0;
         } else {
@@ -1138,7 +1148,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
           const float fmv = sfm[t];
           float lbv = 0.0f;
           if (!dense) {
-            const double D = (double)fmv * a.inv_a2 + (double)a.lbo[r];
+            const double D = (double)fmv * a.inv_a2 + (double)s_lbo[t];
             lbv = fmv == __builtin_inff() ? fmv : (D > 0.0 ? f32_dn(sqrt(D) * (1.0 - 1e-12)) : 0.0f);
           }
           a.lb[r] = lbv;
@@ -1331,7 +1341,7 @@ template <int KSD, bool ARGMIN, bool LB>
 static int launch_sweep(const SweepArgs& a, hipStream_t st) {
   constexpr int SLOT = (KSD + 1) * 2048;
   const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 2 * kRows * 4 +
-                     (size_t)kRows * kMaxG * 2 * 4 + (size_t)kRows * 4 * 4;
+                     (size_t)kRows * kMaxG * 2 * 4 + (size_t)kRows * 6 * 4;
   auto kern = ipe16_sweep_kernel<KSD, ARGMIN, LB>;
   static int attr = 0;
   if (!attr) {
