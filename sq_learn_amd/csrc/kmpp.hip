@@ -1111,6 +1111,115 @@ __global__ void __launch_bounds__(256) kmpp_exact2_batch_kernel(KppArgs a) {
   }
 }
 
+// Exact pass over (row, trial) PAIRS (op 10, after the fused bound): the
+// bound leaves ~1-2 of a listed row's t trials undecided, and records them
+// (the entry's trial mask, in the restart's surv segment); the lane-per-
+// (row, trial) pass above computed all t.  Here each wave expands 64 list
+// entries into their undecided pairs (wave scan of the mask popcounts) and
+// runs one lane per pair: the row straight from global memory (float4, a
+// few loads ahead), the trial's features from LDS, the same sequential
+// fmaf chain - identical D for every pair it computes; a decided trial
+// provably does not improve its row, so the masks, D and block sums equal
+// the full pass's (mask bits set by 32-bit atomicOr: the screen cleared
+// every row's mask; the per-trial sums by LDS fp64 atomics of exact
+// fixed-point integers).
+__global__ void __launch_bounds__(256) kmpp_exact3_batch_kernel(KppArgs a) {
+  int blk, r;
+  if (!kpp_decode(blockIdx.x, a.nr, a.G, blk, r)) return;
+  extern __shared__ __attribute__((aligned(16))) float exs3[];
+  __shared__ double dsum[16];
+  __shared__ int srow[4][64];
+  __shared__ uint16_t spair[4][64 * 16];
+  const int d = a.d, ds = a.d + 4, t = a.t;
+  float* cs = exs3;                    // [t][ds]
+  const float* cand = kf<const float*>(a, r, F_CANDS);
+  const float* closest = kf<const float*>(a, r, F_CLOSEST);
+  uint16_t* mask_out = kf<uint16_t*>(a, r, F_MASK0 + a.cur);
+  float* Dout = kf<float*>(a, r, F_D0 + a.cur);
+  const double scale = kscale(a, r);
+  const int cnt = kf<const int*>(a, r, F_ECOUNT)[blk];
+  const int* eseg = kf<const int*>(a, r, F_EXACT) + (long long)blk * a.R;
+  const int* mseg = kf<const int*>(a, r, F_SURV) + (long long)blk * a.R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int d4 = d >> 2;
+  for (int e = tid; e < t * d4; e += 256) {
+    const int j = e / d4, f4 = e % d4;
+    *reinterpret_cast<float4*>(cs + (size_t)j * ds + 4 * f4) =
+        *reinterpret_cast<const float4*>(cand + (size_t)j * d + 4 * f4);
+  }
+  if (tid < 16) dsum[tid] = 0.0;
+  __syncthreads();
+  for (int e0 = wave * 64; e0 < cnt; e0 += 256) {
+    const int e = e0 + lane;
+    const int row = e < cnt ? eseg[e] : -1;
+    const unsigned m = e < cnt ? (unsigned)mseg[e] & ((1u << t) - 1u) : 0u;
+    const int np = __popc(m);
+    int incl = np;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int tot = __shfl(incl, 63, 64);
+    srow[wave][lane] = row;
+    {
+      int w = incl - np;
+      unsigned mm = m;
+      while (mm) {
+        const int j = __builtin_ctz(mm);
+        mm &= mm - 1u;
+        spair[wave][w++] = (uint16_t)((lane << 4) | j);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int b = 0; b < tot; b += 64) {
+      const bool live = b + lane < tot;
+      const uint16_t pr = live ? spair[wave][b + lane] : (uint16_t)0;
+      const int rr = srow[wave][pr >> 4];
+      const int j = pr & 15;
+      float acc = 0.0f;
+      if (live) {
+        const float* xr = a.X + (size_t)rr * a.ldx;
+        const float* cr = cs + (size_t)j * ds;
+        constexpr int U = 8;   // float4 row loads in flight
+        for (int f0 = 0; f0 < d; f0 += 4 * U) {
+          float4 xv[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            xv[u] = f0 + 4 * u < d ? *reinterpret_cast<const float4*>(xr + f0 + 4 * u)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (f0 + 4 * u < d) {
+              const float4 c4 = *reinterpret_cast<const float4*>(cr + f0 + 4 * u);
+              float ev = xv[u].x - c4.x;
+              acc = fmaf(ev, ev, acc);
+              ev = xv[u].y - c4.y;
+              acc = fmaf(ev, ev, acc);
+              ev = xv[u].z - c4.z;
+              acc = fmaf(ev, ev, acc);
+              ev = xv[u].w - c4.w;
+              acc = fmaf(ev, ev, acc);
+            }
+          }
+        }
+        const float cl = closest[rr];
+        if (acc < cl) {
+          const double wi = a.w ? a.w[rr] : 1.0;
+          Dout[(size_t)j * a.n + rr] = acc;
+          atomicOr(reinterpret_cast<unsigned int*>(mask_out + (rr & ~1)), (1u << j) << (16 * (rr & 1)));
+          atomicAdd(&dsum[j], kpp_q(cl, wi, scale) - kpp_q(acc, wi, scale));
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (tid < t) kf<double*>(a, r, F_DELTA)[(long long)blk * t + tid] = dsum[tid];
+}
+
 constexpr int kBfThreads = 512;   // 8 waves share one staging of the trials
 template <int NS>
 __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a) {
@@ -1121,12 +1230,13 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
   __shared__ float cpar[kScol][3];
   __shared__ int lcnt[16];
   __shared__ float sclo[NWV * 256];
-  __shared__ unsigned long long spc[16], spe[16];   // closest / exact of each restart
+  __shared__ unsigned long long spc[16], spe[16], sps[16];   // closest / exact / surv
   const int blk = blockIdx.x;
   const int tp = a.tp, t = a.t, nr = a.nr;
   if (threadIdx.x < nr) {
     spc[threadIdx.x] = (unsigned long long)a.tab[(size_t)threadIdx.x * kKppNF + F_CLOSEST];
     spe[threadIdx.x] = (unsigned long long)a.tab[(size_t)threadIdx.x * kKppNF + F_EXACT];
+    sps[threadIdx.x] = (unsigned long long)a.tab[(size_t)threadIdx.x * kKppNF + F_SURV];
   }
   const int ncol = nr * tp, ncb = (ncol + 15) / 16;
   auto cb = [&](int hl, int col) -> int8_t* { return cbs + ((size_t)hl * ncb * 16 + col) * DQ; };
@@ -1269,9 +1379,12 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
       for (int p = 0; p < rpb; ++p) {
         const int rp = cbk * rpb + p;
         if (rp >= nr) break;
-        const bool take = lane < 16 && row >= 0 &&
-                          (((unsigned)(bi >> (16 * q + p * tp))) & tmask) != 0u;
-        seg_append(take, row, uni_ptr<int*>(spe[rp]) + r0, &lcnt[rp]);
+        const unsigned tm = ((unsigned)(bi >> (16 * q + p * tp))) & tmask;
+        const bool take = lane < 16 && row >= 0 && tm != 0u;
+        const int pos = seg_append_pos(take, row, uni_ptr<int*>(spe[rp]) + r0, &lcnt[rp]);
+        // the undecided trials of the entry (the surv segments are free in
+        // the fused passes): op 10 computes only those
+        if (pos >= 0) uni_ptr<int*>(sps[rp])[r0 + pos] = (int)tm;
       }
     }
   }
@@ -1510,6 +1623,13 @@ int sq_kmpp_batch(int op, const long long* ia, void* stream) {
       if (a.c < 0) return (int)hipErrorInvalidValue;
       hipLaunchKernelGGL(kmpp_finish_batch_kernel, dim3((unsigned)a.nr), dim3(1024), 0, st, a);
       break;
+    case 10: {
+      // exact pass over the fused bound's undecided pairs: d <= 256
+      if (a.d > 256 || !a.prune) return (int)hipErrorInvalidValue;
+      const size_t lds = (size_t)a.t * (a.d + 4) * sizeof(float);
+      hipLaunchKernelGGL(kmpp_exact3_batch_kernel, dim3(rows_grid), dim3(256), lds, st, a);
+      break;
+    }
     case 9: {
       // exact pass, lane per (row, trial): d <= 256, tp a power of two >= t
       if (a.d > 256 || a.tp < a.t || a.tp > 16 || (a.tp & (a.tp - 1))) return (int)hipErrorInvalidValue;

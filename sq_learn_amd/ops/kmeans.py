@@ -1095,6 +1095,8 @@ class KmppBatch:
         # SQ_KMPP_EXACT2=0: a lane per row (op 4, same results)
         self.exact2 = (self.d <= 256 and self.t <= 16
                        and os.environ.get("SQ_KMPP_EXACT2", "1") != "0")
+        # after the fused bound: only the undecided (row, trial) pairs (op 10)
+        self.pairs = self.exact2 and os.environ.get("SQ_KMPP_PAIRS", "1") != "0"
         if self.fused:
             GR = max(st0.G * st0.R, 1)
             self.useg = torch.empty(GR, dtype=torch.int32, device=dev)
@@ -1159,7 +1161,7 @@ class KmppBatch:
             if self.n and self.fused:
                 run_op(7)                   # triangle screen, all restarts: union list
                 run_op(8)                   # certified int8 bound, one row read
-                run_op(9 if self.exact2 else 4)   # exact pass
+                run_op(10 if self.pairs else (9 if self.exact2 else 4))   # exact pass
             elif self.n:
                 run_op(2)                   # triangle screen (+ lazy winner)
                 if st0.prune:

@@ -58,11 +58,13 @@ def test_qmeans_fit_n_init_batched_matches_sequential(cuda, monkeypatch):
     assert a.inertia_ == b.inertia_
 
 
-def test_fused_passes_equal_per_restart_passes(cuda, monkeypatch):
-    """SQ_KMPP_FUSED=0 (per-restart screen / bound) gives the same centres."""
+@pytest.mark.parametrize("env", ["SQ_KMPP_FUSED", "SQ_KMPP_PAIRS"])
+def test_fused_passes_equal_per_restart_passes(cuda, monkeypatch, env):
+    """SQ_KMPP_FUSED=0 (per-restart screen / bound) and SQ_KMPP_PAIRS=0 (the
+    exact pass over every trial of a listed row) give the same centres."""
     data = _data(cuda, n=100_000, d=96, blobs=30, seed=3)
     a = I.kmeans_plusplus_restarts(data, 64, np.random.RandomState(11), 6)
-    monkeypatch.setenv("SQ_KMPP_FUSED", "0")
+    monkeypatch.setenv(env, "0")
     b = I.kmeans_plusplus_restarts(data, 64, np.random.RandomState(11), 6)
     for Ca, Cb in zip(a, b):
         assert torch.equal(Ca, Cb)
