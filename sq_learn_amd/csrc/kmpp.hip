@@ -1281,10 +1281,19 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
   kpp_v4i nav[NS];
   float nrs = 0.f, nre = 0.f, ncl[4];
   int nq2 = 0;
-  auto prefetch = [&](int g) {
+  // the list entries (row id, restart mask) run one group further ahead:
+  // the row loads of group g + 1 need them, and waiting for them right
+  // before issuing those loads exposed a full memory latency per group
+  int irow = -1;
+  unsigned ibits = 0u;
+  auto load_ids = [&](int g) {
     const int e = g + c16;
-    nrow = e < cnt ? useg[e] : -1;
-    nbits = e < cnt ? umask[e] : 0u;
+    irow = e < cnt ? useg[e] : -1;
+    ibits = e < cnt ? umask[e] : 0u;
+  };
+  auto prefetch = [&]() {
+    nrow = irow;
+    nbits = ibits;
     const int rr0 = nrow >= 0 ? nrow : 0;
     const int8_t* xr = a.Xq + (size_t)rr0 * a.dq + 16 * kb;
 #pragma unroll
@@ -1300,7 +1309,9 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
                    ? reinterpret_cast<const float*>(spc[rr])[nrow] : 0.0f;
     }
   };
-  prefetch(wave * 16);
+  load_ids(wave * 16);
+  prefetch();
+  load_ids(wave * 16 + 16 * NWV);
   for (int g0 = wave * 16; g0 < cnt; g0 += 16 * NWV) {
     const int row = nrow;
     const unsigned bits = nbits;
@@ -1314,7 +1325,8 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    prefetch(g0 + 16 * NWV);
+    prefetch();
+    load_ids(g0 + 32 * NWV);
     // restarts live in any row of the group
     unsigned gbits = row >= 0 ? bits : 0u;
 #pragma unroll
