@@ -1488,8 +1488,25 @@ class Ipe16:
         self.ev.synchronize()
         dense = self.counts_host[:, 1].tolist()
         self.last_dense = int(sum(dense))
-        for c, nd in enumerate(dense):
-            if nd > 0:
-                s, e = c * IPE16_CHUNK, min(n, (c + 1) * IPE16_CHUNK)
-                fallback(self.dense_rows[s:], self.counts[c, 1:2], int(nd), self.thr[s:e],
-                         self.hj[s:e], s, e)
+        parts = [(c, int(nd)) for c, nd in enumerate(dense) if nd > 0]
+        if len(parts) == 1:
+            c, nd = parts[0]
+            s, e = c * IPE16_CHUNK, min(n, (c + 1) * IPE16_CHUNK)
+            fallback(self.dense_rows[s:], self.counts[c, 1:2], nd, self.thr[s:e], self.hj[s:e],
+                     s, e)
+        elif parts:
+            # the chunks' dense rows in ONE fallback launch over the shard (the
+            # fp32 row-group kernel is latency-bound on a few rows: one launch
+            # per chunk cost ~90 us each at steady state)
+            tot = sum(nd for _, nd in parts)
+            if getattr(self, "_dense_all", None) is None or self._dense_all.numel() < tot:
+                self._dense_all = torch.empty(max(tot, 1024), dtype=self.dense_rows.dtype,
+                                              device=self.dense_rows.device)
+                self._dense_cnt = torch.zeros(1, dtype=torch.int32, device=self.dense_rows.device)
+            off = 0
+            for c, nd in parts:
+                s = c * IPE16_CHUNK
+                torch.add(self.dense_rows[s:s + nd], s, out=self._dense_all[off:off + nd])
+                off += nd
+            self._dense_cnt.fill_(tot)
+            fallback(self._dense_all, self._dense_cnt, tot, self.thr[:n], self.hj[:n], 0, n)
