@@ -273,7 +273,7 @@ class LloydEngine:
         mx = torch.stack([self.Xm.abs().max().float() if self.n else torch.zeros((), device=dev),
                           (self.sample_weight.abs().max().float() if self.sample_weight is not None
                            and self.n else torch.zeros((), device=dev))]).double()
-        nrows = torch.tensor([float(self.n)], dtype=torch.float64, device=dev)
+        nrows = torch.full((1,), float(self.n), dtype=torch.float64, device=dev)
         self.comm.all_reduce_(mx, op="max")
         self.comm.all_reduce_(nrows)
         mxl = mx.tolist()
@@ -755,7 +755,7 @@ class LloydEngine:
             if not hasattr(self, "_g_rws"):
                 mx = torch.stack([self.Xf.abs().max(), w.abs().max().float() if w is not None
                                   else torch.zeros((), device=self.device)]).double()
-                nr = torch.tensor([float(self.n)], dtype=torch.float64, device=self.device)
+                nr = torch.full((1,), float(self.n), dtype=torch.float64, device=self.device)
                 self.comm.all_reduce_(mx, op="max")
                 self.comm.all_reduce_(nr)
                 mxl = mx.tolist()

@@ -1302,7 +1302,11 @@ class Ipe16:
         k = C32.shape[0]
         dev = C32.device
         C64 = C32.double()
-        inf = torch.tensor(float("inf"), device=dev)
+        # (outward fp32 rounding by a 2^-20 relative margin - plain products,
+        # not nextafter / pow / median: every distinct torch kernel costs
+        # 30-130 ms of lazy loading at its first use in a process, which the
+        # first IPE step paid)
+        up, dn = 1.0 + 2.0 ** -20, 1.0 - 2.0 ** -20
         nrm = (C64 * C64).sum(1)
         D2 = nrm[:, None] + nrm[None, :] - 2.0 * (C64 @ C64.T)
         marg = 1e-12 * nrm.max()
@@ -1310,7 +1314,8 @@ class Ipe16:
         Dhi = (D2 + marg).clamp_min(0.0).sqrt() * (1.0 + 1e-9)
         W = min(self.n_wild, k)
         if self.C_prev is not None and self.C_prev.shape == C32.shape:
-            sh = (C64 - self.C_prev.double()).pow(2).sum(1).sqrt() * (1.0 + 1e-9)
+            dd = C64 - self.C_prev.double()
+            sh = (dd * dd).sum(1).sqrt() * (1.0 + 1e-9)
             # adaptive wild set: at least n_wild, and every centroid that moved
             # more than 1 % of the median nearest-centroid distance (up to
             # k / 2) - a few hundred centroids contesting unclaimed blobs jump
@@ -1318,19 +1323,19 @@ class Ipe16:
             # move, and a kept bound decays by tau every step
             # (device-side: no host read of the count)
             Dn = Dlo + torch.diag(torch.full((k,), float("inf"), dtype=torch.float64, device=dev))
-            tgt = 0.01 * Dn.amin(1).median()
+            tgt = 0.01 * torch.sort(Dn.amin(1)).values[(k - 1) // 2]   # the median
             Wd = (sh > tgt).sum().clamp(min=W, max=max(k // 2, 1)).clamp(max=k - 1)
             srt = torch.sort(sh, descending=True).values
             tau = srt.gather(0, Wd.reshape(1))[0] if k > W else torch.zeros(
                 (), dtype=torch.float64, device=dev)
-            self.smax.copy_(torch.nextafter(tau.float(), inf).reshape(1))
+            self.smax.copy_((tau * up).float().reshape(1))
             wild = sh > tau
             self.last_wild = Wd
         else:
             wild = torch.zeros(k, dtype=torch.bool, device=dev)
         Dw = torch.where(wild[None, :] & ~torch.eye(k, dtype=torch.bool, device=dev), Dlo,
                          torch.full_like(Dlo, float("inf")))
-        self.mw[:k].copy_(torch.nextafter(Dw.amin(1).float(), -inf))
+        self.mw[:k].copy_((Dw.amin(1) * dn).float())
         # centroid -> norm group (operand column order: perm, group starts)
         # (operand column order = the groups' contiguous tile ranges)
         Dp = Dhi.index_select(1, self.perm.long())
@@ -1340,7 +1345,7 @@ class Ipe16:
             c1 = min(64 * self.gstart[g + 1], k) if g + 1 < self.G else k
             if c1 > c0:
                 Rc[:, g] = Dp[:, c0:c1].amax(1)
-        self.Rc[:k].copy_(torch.nextafter(Rc.float(), inf))
+        self.Rc[:k].copy_((Rc * up).float())
         self.C_prev = C32.clone()
 
     def set_centers(self, C32, cn=None):
@@ -1362,9 +1367,11 @@ class Ipe16:
         self.cns[:self.k].copy_(cs.float())
         lo_t = self.group_tiles(cs.double().cpu().numpy(), self.k, nt, G)
         hi_t = lo_t[1:] + [nt]
-        first = torch.tensor([min(64 * t, self.k - 1) for t in lo_t], device=cn.device)
-        last = torch.tensor([min(64 * t, self.k) - 1 for t in hi_t], device=cn.device)
-        self.gS = torch.stack([cs.index_select(0, first), cs.index_select(0, last)], 1)
+        # (views and a cat: no host -> device copy of the group indices)
+        first = [min(64 * t, self.k - 1) for t in lo_t]
+        last = [min(64 * t, self.k) - 1 for t in hi_t]
+        self.gS = torch.stack([torch.cat([cs[f:f + 1] for f in first]),
+                               torch.cat([cs[l:l + 1] for l in last])], 1)
         self.gS = self.gS.float().contiguous()
         self.G = G
         self.gstart = lo_t + [nt] * (4 - G)   # first tile of each group (unused: n_tiles)
