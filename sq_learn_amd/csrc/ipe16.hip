@@ -1331,6 +1331,177 @@ __global__ void __launch_bounds__(256) ipe16_finalize_kernel(const unsigned long
   if (lb && lab != hj[r]) lb[r] = fminf(lb[r], dhint[r]);
 }
 
+// ------------------------------------------------------------------ skip bounds
+// The row skip's per-step centroid quantities (ops.kmeans.Ipe16._skip_bounds
+// in three launches instead of ~45 small torch ops - each ~8 us of launch
+// gap, and each distinct torch kernel 30-130 ms of lazy loading at its first
+// use).  G = C C^T (fp64, the caller's GEMM), nrm = |c|^2.
+// |c|^2 is G's diagonal, the margin 1e-12 max |c|^2 (each workgroup takes the
+// max itself: no host read).
+//  1. per centroid a (one workgroup): Dlo / Dhi of every pair from the
+//     expansion with its margin (as the torch version), the nearest other
+//     centroid nn[a] (Dlo), and a's shift sh[a] since the previous centres;
+//  2. one workgroup: the median of nn (bitonic sort in LDS), the wild count
+//     W = clamp(#{sh > 0.01 median}, n_wild, k / 2) and tau = the (W+1)-th
+//     largest shift -> smax (rounded up);
+//  3. per centroid a: mw[a] = min over the wild j != a of Dlo (rounded down),
+//     Rc[a][g] = max over norm group g (operand columns) of Dhi (rounded up).
+struct BoundsArgs {
+  const float* C;
+  const float* Cprev;     // nullable: no shifts (first call)
+  const double* G;        // [k][k]
+  const int* perm;        // operand column -> centroid
+  int k, d, Gn, n_wild;
+  int gs[4];              // first tile of each group
+  double mrel;            // margin / max |c|^2
+  double* sh;             // [k] work
+  double* nn;             // [k] work
+  double* tau;            // [1] work
+  int* wild_n;            // [1] out
+  float* smax;            // [1] out
+  float* mw;              // [k] out
+  float* Rc;              // [k][4] out
+};
+SQ_DEV double sb_d2(const BoundsArgs& a, int i, int j) {
+  return (a.G[(size_t)i * (a.k + 1)] + a.G[(size_t)j * (a.k + 1)]) - 2.0 * a.G[(size_t)i * a.k + j];
+}
+SQ_DEV double sb_lo(double D2, double marg) { return sqrt(fmax(D2 - marg, 0.0)) * (1.0 - 1e-9); }
+SQ_DEV double sb_hi(double D2, double marg) { return sqrt(fmax(D2 + marg, 0.0)) * (1.0 + 1e-9); }
+SQ_DEV double wave_max_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// the margin, in every thread of a 256-thread block
+SQ_DEV double sb_margin(const BoundsArgs& a, double* red4) {
+  double m = 0.0;
+  for (int j = threadIdx.x; j < a.k; j += 256) m = fmax(m, a.G[(size_t)j * (a.k + 1)]);
+  m = wave_max_d(m);
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+  __syncthreads();
+  return a.mrel * fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+}
+SQ_DEV double wave_min_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+SQ_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__global__ void __launch_bounds__(256) skip_bounds_rows_kernel(BoundsArgs a) {
+  __shared__ double red[3][4];
+  const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double marg = sb_margin(a, red[2]);
+  double m = __builtin_inf();
+  for (int j = tid; j < a.k; j += 256)
+    if (j != i) m = fmin(m, sb_lo(sb_d2(a, i, j), marg));
+  double s2 = 0.0;
+  if (a.Cprev)
+    for (int f = tid; f < a.d; f += 256) {
+      const double dd = (double)a.C[(size_t)i * a.d + f] - (double)a.Cprev[(size_t)i * a.d + f];
+      s2 += dd * dd;
+    }
+  m = wave_min_d(m);
+  s2 = wave_sum_d(s2);
+  if (lane == 0) {
+    red[0][wave] = m;
+    red[1][wave] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    a.nn[i] = fmin(fmin(red[0][0], red[0][1]), fmin(red[0][2], red[0][3]));
+    a.sh[i] = sqrt((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * (1.0 + 1e-9);
+  }
+}
+constexpr int kSbMaxK = 4096;
+SQ_DEV void lds_bitonic(double* v, int np2) {
+  for (int size = 2; size <= np2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < np2 / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const double x = v[lo], y = v[hi];
+        if ((x > y) == asc) {
+          v[lo] = y;
+          v[hi] = x;
+        }
+      }
+    }
+  __syncthreads();
+}
+__global__ void __launch_bounds__(1024) skip_bounds_tau_kernel(BoundsArgs a) {
+  __shared__ double v[kSbMaxK];
+  __shared__ int cnt;
+  int np2 = 1;
+  while (np2 < a.k) np2 <<= 1;
+  for (int j = threadIdx.x; j < np2; j += blockDim.x) v[j] = j < a.k ? a.nn[j] : __builtin_inf();
+  if (threadIdx.x == 0) cnt = 0;
+  lds_bitonic(v, np2);
+  const double tgt = 0.01 * v[(a.k - 1) / 2];
+  __syncthreads();
+  int c = 0;
+  for (int j = threadIdx.x; j < a.k; j += blockDim.x) c += a.sh[j] > tgt ? 1 : 0;
+  atomicAdd(&cnt, c);
+  // descending shifts: ascending sort of -sh
+  for (int j = threadIdx.x; j < np2; j += blockDim.x) v[j] = j < a.k ? -a.sh[j] : __builtin_inf();
+  lds_bitonic(v, np2);
+  if (threadIdx.x == 0) {
+    const int W0 = a.n_wild < a.k ? a.n_wild : a.k;
+    int W = cnt;
+    W = W < W0 ? W0 : W;
+    const int half = a.k / 2 > 1 ? a.k / 2 : 1;
+    W = W > half ? half : W;
+    W = W > a.k - 1 ? a.k - 1 : W;
+    const double t = a.k > W0 ? -v[W] : 0.0;
+    a.tau[0] = t;
+    a.wild_n[0] = W;
+    a.smax[0] = (float)(t * (1.0 + 0x1p-20));
+  }
+}
+__global__ void __launch_bounds__(256) skip_bounds_cols_kernel(BoundsArgs a) {
+  __shared__ double red[6][4];
+  const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double marg = sb_margin(a, red[5]);
+  const double tau = a.Cprev ? a.tau[0] : __builtin_inf();
+  double mw = __builtin_inf();
+  double rc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int c = tid; c < a.k; c += 256) {
+    const int j = a.perm[c];
+    const double D2 = sb_d2(a, i, j);
+    if (j != i && a.Cprev && a.sh[j] > tau) mw = fmin(mw, sb_lo(D2, marg));
+    const int t = c >> 6;
+    const int g = (t >= a.gs[1] && a.Gn > 1) + (t >= a.gs[2] && a.Gn > 2) + (t >= a.gs[3] && a.Gn > 3);
+    const double h = sb_hi(D2, marg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rc[q] = q == g ? fmax(rc[q], h) : rc[q];
+  }
+  mw = wave_min_d(mw);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) rc[q] = fmax(rc[q], __shfl_xor(rc[q], o, 64));
+  if (lane == 0) {
+    red[0][wave] = mw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[1 + q][wave] = rc[q];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double m = fmin(fmin(red[0][0], red[0][1]), fmin(red[0][2], red[0][3]));
+    a.mw[i] = (float)(m * (1.0 - 0x1p-20));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double r = fmax(fmax(red[1 + q][0], red[1 + q][1]), fmax(red[1 + q][2], red[1 + q][3]));
+      a.Rc[(size_t)i * 4 + q] = q < a.Gn ? (float)(r * (1.0 + 0x1p-20)) : 0.0f;
+    }
+  }
+}
+
 }  // namespace i16
 }  // namespace sq
 
@@ -1404,6 +1575,38 @@ extern "C" {
 // da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
 int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (op == 5) {
+    // skip bounds (own layout): ia [0] C fp32 [k][d], [1] C_prev (0: none),
+    // [2] G = C C^T fp64 [k][k], [4] perm int32, [5] k, [6] d,
+    // [7] G groups, [8] n_wild, [9..12] first tile of groups 0..3, [13] sh,
+    // [14] nn (fp64 [k] work), [15] tau (fp64 [1]), [16] wild count (int32
+    // [1]), [17] smax, [18] mw, [19] Rc [k][4]; da [0] the D2 margin relative to max |c|^2
+    BoundsArgs b;
+    b.C = (const float*)ia[0];
+    b.Cprev = (const float*)ia[1];
+    b.G = (const double*)ia[2];
+    b.perm = (const int*)ia[4];
+    b.k = (int)ia[5];
+    b.d = (int)ia[6];
+    b.Gn = (int)ia[7];
+    b.n_wild = (int)ia[8];
+    for (int q = 0; q < 4; ++q) b.gs[q] = (int)ia[9 + q];
+    b.sh = (double*)ia[13];
+    b.nn = (double*)ia[14];
+    b.tau = (double*)ia[15];
+    b.wild_n = (int*)ia[16];
+    b.smax = (float*)ia[17];
+    b.mw = (float*)ia[18];
+    b.Rc = (float*)ia[19];
+    b.mrel = da[0];
+    if (b.k < 1 || b.k > kSbMaxK || b.d < 1 || b.Gn < 1 || b.Gn > 4 || !b.C || !b.G ||
+        !b.perm || !b.sh || !b.nn || !b.tau || !b.wild_n || !b.smax || !b.mw || !b.Rc)
+      return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(skip_bounds_rows_kernel, dim3(b.k), dim3(256), 0, st, b);
+    if (b.Cprev) hipLaunchKernelGGL(skip_bounds_tau_kernel, dim3(1), dim3(1024), 0, st, b);
+    hipLaunchKernelGGL(skip_bounds_cols_kernel, dim3(b.k), dim3(256), 0, st, b);
+    return (int)hipGetLastError();
+  }
   const long long n = ia[25];
   if (n <= 0) return 0;
   const int d = (int)ia[26], d_pad = (int)ia[27], k = (int)ia[28], k_pad = (int)ia[29];

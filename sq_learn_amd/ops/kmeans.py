@@ -1232,6 +1232,7 @@ class Ipe16:
         self.Rc = torch.zeros((max(int(k), 1), 4), dtype=torch.float32, device=dev)
         self.mw = torch.zeros(max(int(k), 1), dtype=torch.float32, device=dev)
         self.n_wild = 16
+        self.native_bounds = os.environ.get("SQ_IPE16_NATIVE_BOUNDS", "1") != "0"
         self.C_prev = None
         self.lb_valid = False
         self.skip = __import__("os").environ.get("SQ_IPE16_SKIP", "1") != "0"
@@ -1302,6 +1303,36 @@ class Ipe16:
         k = C32.shape[0]
         dev = C32.device
         C64 = C32.double()
+        if k <= 4096 and self.native_bounds:
+            # csrc/ipe16.hip op 5: the same quantities in three launches after
+            # the fp64 GEMM (each torch op below is a launch of its own)
+            G = C64 @ C64.T
+            if not hasattr(self, "_sb_work") or self._sb_work[0].shape[0] != k:
+                self._sb_work = (torch.empty(k, dtype=torch.float64, device=dev),
+                                 torch.empty(k, dtype=torch.float64, device=dev),
+                                 torch.zeros(1, dtype=torch.float64, device=dev),
+                                 torch.zeros(1, dtype=torch.int32, device=dev))
+            sh, nn, tau, wn = self._sb_work
+            prev = self.C_prev is not None and self.C_prev.shape == C32.shape
+            C32c = C32.contiguous()
+            ia = torch.zeros(20, dtype=torch.int64)
+            ia[0] = C32c.data_ptr()
+            ia[1] = self.C_prev.data_ptr() if prev else 0
+            ia[2], ia[4] = G.data_ptr(), self.perm.data_ptr()
+            ia[5], ia[6], ia[7], ia[8] = k, C32.shape[1], self.G, self.n_wild
+            for g in range(4):
+                ia[9 + g] = self.gstart[g]
+            ia[13], ia[14], ia[15], ia[16] = sh.data_ptr(), nn.data_ptr(), tau.data_ptr(), wn.data_ptr()
+            ia[17], ia[18], ia[19] = self.smax.data_ptr(), self.mw.data_ptr(), self.Rc.data_ptr()
+            da = torch.tensor([1e-12], dtype=torch.float64)
+            rc = nat.native().ipe16(5, ia.data_ptr(), da.data_ptr(),
+                                    nat.stream_handle(dev))
+            if rc != 0:
+                raise RuntimeError(f"sq_ipe16 skip bounds failed ({rc})")
+            if prev:
+                self.last_wild = wn
+            self.C_prev = C32c.clone()
+            return
         # (outward fp32 rounding by a 2^-20 relative margin - plain products,
         # not nextafter / pow / median: every distinct torch kernel costs
         # 30-130 ms of lazy loading at its first use in a process, which the

@@ -141,3 +141,37 @@ def test_ipe16_skip_law_at_band_edge(cuda):
     la, ma = out[1]
     lb, mb = _run_full(X, Ct, 0.25, 13, 9)
     assert _same_law(la, ma, lb, mb, min_cells=2) > 1e-4
+
+
+@pytest.mark.parametrize("k", [40, 200, 1000, 3000])
+def test_ipe16_native_skip_bounds_match_torch(cuda, k):
+    """csrc/ipe16.hip op 5 (the skip bounds in three launches) against the
+    torch formulation of ``Ipe16._skip_bounds``: the same wild count, tau,
+    wild minimum and per-group upper distances (fp32, up to the fp64
+    rounding order)."""
+    d = 64
+    g = torch.Generator().manual_seed(k)
+    C0 = (torch.randn(k, d, generator=g) * 3).to(cuda)
+    C1 = C0 + 1e-3 * torch.randn(k, d, generator=g).to(cuda)
+    jump = torch.randperm(k, generator=g)[:max(k // 20, 1)].to(cuda)
+    C1[jump] += 2.0 * torch.randn(len(jump), d, generator=g).to(cuda)
+    X = torch.randn(256, d, device=cuda)
+    outs = []
+    for native in (True, False):
+        st = K.Ipe16(X, k, K.pad_features(d), K.pad_clusters(k), 1.0, cuda)
+        st.native_bounds = native
+        for C in (C0, C1):
+            st.set_centers(C)
+            st._skip_bounds(C)
+            if C is C0:
+                first = (st.mw[:k].clone(), st.Rc[:k].clone())
+        torch.cuda.synchronize()
+        outs.append((first, int(st.last_wild), st.smax.clone(), st.mw[:k].clone(),
+                     st.Rc[:k].clone()))
+    (fa, wa, sa, ma, ra), (fb, wb, sb, mb, rb) = outs
+    assert torch.isinf(fa[0]).all() and torch.isinf(fb[0]).all()
+    torch.testing.assert_close(fa[1], fb[1], rtol=1e-6, atol=0)
+    assert wa == wb and wa >= min(16, k // 2)
+    torch.testing.assert_close(sa, sb, rtol=1e-6, atol=0)
+    torch.testing.assert_close(ma, mb, rtol=1e-6, atol=0)
+    torch.testing.assert_close(ra, rb, rtol=1e-6, atol=0)
