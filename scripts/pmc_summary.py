@@ -11,6 +11,7 @@ per-dispatch mean of every counter plus derived metrics:
 import argparse
 import collections
 import sqlite3
+import re
 
 
 def short(name, n=70):
@@ -47,7 +48,7 @@ def main():
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         durs = collections.defaultdict(dict)
         for kn, did, cn, val, dur in cc:
-            if a.match and a.match not in kn:
+            if a.match and not re.search(a.match, kn):
                 continue
             per[(kn, did)][cn] += val
             durs[kn][did] = dur
