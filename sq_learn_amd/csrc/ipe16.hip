@@ -113,26 +113,36 @@ SQ_DEV unsigned long long pack_best(float dt, const RngKey& tie, long long g, in
 // past d add +0), then an xor tree over the 16 lanes.  All B pairs' loads
 // are issued before the first fma (one memory latency per batch, not one
 // per pair).
+// (U > 16, wide rows: 16 values per pair at a time, the same fmaf order)
 template <int U, int B>
 SQ_DEV void canon_dot_batch(const float* const (&xp)[B], const float* const (&cp)[B], int d,
                             int c16, float (&out)[B]) {
-  float xv[B][U], cv[B][U];
+  constexpr int UC = U < 16 ? U : 16;
+  static_assert(U % UC == 0, "chunked canonical dot");
+  float s[B];
 #pragma unroll
-  for (int b = 0; b < B; ++b)
+  for (int b = 0; b < B; ++b) s[b] = 0.0f;
+  for (int u0 = 0; u0 < U; u0 += UC) {
+    float xv[B][UC], cv[B][UC];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int f = c16 + 16 * u;
-      xv[b][u] = f < d ? xp[b][f] : 0.0f;
-      cv[b][u] = f < d ? cp[b][f] : 0.0f;
-    }
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const int f = c16 + 16 * (u0 + u);
+        xv[b][u] = f < d ? xp[b][f] : 0.0f;
+        cv[b][u] = f < d ? cp[b][f] : 0.0f;
+      }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+      for (int u = 0; u < UC; ++u) s[b] = fmaf(xv[b][u], cv[b][u], s[b]);
+  }
 #pragma unroll
   for (int b = 0; b < B; ++b) {
-    float s = 0.0f;
+    float t = s[b];
 #pragma unroll
-    for (int u = 0; u < U; ++u) s = fmaf(xv[b][u], cv[b][u], s);
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-    out[b] = s;
+    for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+    out[b] = t;
   }
 }
 
@@ -789,9 +799,12 @@ struct SweepArgs {
   const float* thr;         // [n] the hint's estimate
   const float* ea2;         // [n] E / alpha^2 (rounded up)
   CertParams cert;
+  // wide rows (GV): the pass values of every position, [n][k_pad] in the
+  // accumulator layout, from ipe16_values_kernel (the same MFMA sequence)
+  const float* V;
 };
 
-template <int KSD, bool ARGMIN, bool LB>
+template <int KSD, bool ARGMIN, bool LB, bool GV = false>
 __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   constexpr int KT = KSD + 1;                 // data k-steps + the norm step
   constexpr int SLOT = KT * 2048;
@@ -801,7 +814,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   constexpr int DX = KSD * 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   auto buf = [&](int g) -> unsigned char* { return smem + (g % kRing) * SLOT; };
-  uint16_t* nl = reinterpret_cast<uint16_t*>(smem + kRing * SLOT);      // [kRows][kNLS]
+  uint16_t* nl = reinterpret_cast<uint16_t*>(smem + (GV ? 0 : kRing * SLOT));   // [kRows][kNLS]
   int* ncnt = reinterpret_cast<int*>(nl + kRows * kNLS);                  // [kRows]
   int* shint = ncnt + kRows;                                              // [kRows]
   float* sband = reinterpret_cast<float*>(shint + kRows);                 // [kRows][G][2]
@@ -829,6 +842,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   const uint32_t keep = ~((1u << (qbits + 5)) - 1u);
 
   auto stage = [&](int U) {
+    if constexpr (GV) return;
     const int t = U % n_tiles;
     const unsigned char* tile = reinterpret_cast<const unsigned char*>(a.C) + (size_t)t * TILE_STRIDE;
     unsigned char* dst = buf(U);
@@ -841,6 +855,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     }
   };
   auto sync_tile = [&]() {
+    if constexpr (GV) return;
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -850,6 +865,7 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   };
   f16x8 ah[kRS][KSD];
   auto load_a = [&](long long b) {
+    if constexpr (GV) return;
 #pragma unroll
     for (int st = 0; st < kRS; ++st) {
       long long r = row_of(b, st, r32);
@@ -894,6 +910,24 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   auto pass = [&](auto H_, const unsigned char* cur, Acc& acc, const Acc& o, uint32_t qo,
                   bool do_epi) {
     constexpr int h = decltype(H_)::value;
+    if constexpr (GV) {
+      // this half-tile's values (half-tile index qo + 1) of the block's rows,
+      // then the previous half-tile's epilogue
+      const int col = 32 * (int)(qo + 1u) + r32;
+#pragma unroll
+      for (int st = 0; st < kRS; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          long long p = row_of(blk, st, rl_of(i));
+          p = p < n ? p : n - 1;
+          acc[st][i] = a.V[(size_t)p * a.k_pad + col];
+        }
+      if (do_epi) {
+#pragma unroll
+        for (int e = 0; e < 16 * kRS; ++e) epi(e / 16, e % 16, o[e / 16][e % 16], qo);
+      }
+      return;
+    }
 #pragma unroll
     for (int st = 0; st < kRS; ++st) acc[st] = (f32x16){0};
 #pragma unroll
@@ -975,11 +1009,13 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
   auto group_of = [&](int t) { return (t >= a.gb[0]) + (t >= a.gb[1]) + (t >= a.gb[2]); };
 
   int U = 0;
-  stage(0);
-  stage(1);
-  load_a(blk);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  if constexpr (!GV) {
+    stage(0);
+    stage(1);
+    load_a(blk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
 
   for (; blk < nblk; blk += gridDim.x) {
     // ---- block prologue: the rows' band edges, hints, listed fires
@@ -1050,8 +1086,10 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
       if (t > 0) colc(64 * (t - 1) + 32 + r32, jcA, nyA);
       colc(64 * t + r32, jcB, nyB);
       stage(U + kRing - 1);
+      if constexpr (!GV) {
 #pragma unroll
-      for (int j = 0; j < PFD; ++j) bq[j] = frag(buf(U), j);
+        for (int j = 0; j < PFD; ++j) bq[j] = frag(buf(U), j);
+      }
       pass(std::integral_constant<int, 0>{}, buf(U), cA, cB, (uint32_t)(2 * t - 1), t > 0);
       flush_near(blk, jcA, nyA, cB);
       // tile t's values (epilogues from the next pass on) use its group's bands
@@ -1195,6 +1233,58 @@ __global__ void __launch_bounds__(kNW * 64) ipe16_sweep_kernel(SweepArgs a) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ------------------------------------------------------------------ values
+// Wide rows (d_pad > 256: the A fragments of a row set no longer fit in
+// VGPRs next to the sweep's epilogue state): the sweep's pass values are
+// computed here first - per wave 32 positions x one 64-centroid tile, the
+// SAME operands in the same k-step order through the same MFMA from zero, so
+// every value equals the resident-fragment sweep's bit for bit - and the
+// GV sweep reads them instead of running its MFMAs.  V [n][k_pad] fp32, in
+// the accumulator layout (register i of lane (half, r32): row (i & 3) +
+// 8 (i >> 2) + 4 half of the wave's 32, column 64 t + 32 h + r32).
+struct ValuesArgs {
+  const _Float16* Xh;
+  const _Float16* C;
+  const int* rows;          // list mode: positions -> rows
+  const int* rows_count;
+  long long n;              // positions (upper bound in list mode)
+  int ksd, k_pad;
+  float* V;
+};
+__global__ void __launch_bounds__(256) ipe16_values_kernel(ValuesArgs a) {
+  const long long n = a.rows ? (long long)*a.rows_count : a.n;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r32 = lane & 31, half = lane >> 5;
+  const long long p0 = ((long long)blockIdx.x * 4 + wave) * 32;
+  if (p0 >= n) return;
+  const int t = blockIdx.y;
+  const long long p = p0 + r32 < n ? p0 + r32 : n - 1;
+  const long long r = a.rows ? (long long)a.rows[p] : p;
+  const int KT = a.ksd + 1;
+  const _Float16* xr = a.Xh + (size_t)r * (a.ksd * 16) + half * 8;
+  const unsigned char* tile = reinterpret_cast<const unsigned char*>(a.C) +
+                              (size_t)t * (2 * a.ksd + 1) * 2048 + (half * 64 + r32) * 16;
+  f16x8 aug = (f16x8)0;
+  if (half == 0) { aug[0] = aug[1] = aug[2] = (_Float16)1.0f; }
+  f32x16 c0 = (f32x16){0}, c1 = (f32x16){0};
+  for (int ks = 0; ks < KT; ++ks) {
+    const f16x8 av = ks < a.ksd ? *reinterpret_cast<const f16x8*>(xr + ks * 16) : aug;
+    const f16x8 b0 = *reinterpret_cast<const f16x8*>(tile + ks * 2048);
+    const f16x8 b1 = *reinterpret_cast<const f16x8*>(tile + 512 + ks * 2048);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, b0, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, b1, c1, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const long long q = p0 + (i & 3) + 8 * (i >> 2) + 4 * half;
+    if (q < n) {
+      float* vr = a.V + (size_t)q * a.k_pad + 64 * t + r32;
+      vr[0] = c0[i];
+      vr[32] = c1[i];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ near
@@ -1508,12 +1598,12 @@ __global__ void __launch_bounds__(256) skip_bounds_cols_kernel(BoundsArgs a) {
 using namespace sq;
 using namespace sq::i16;
 
-template <int KSD, bool ARGMIN, bool LB>
+template <int KSD, bool ARGMIN, bool LB, bool GV = false>
 static int launch_sweep(const SweepArgs& a, hipStream_t st) {
   constexpr int SLOT = (KSD + 1) * 2048;
-  const size_t lds = kRing * (size_t)SLOT + (size_t)kRows * kNLS * 2 + 2 * kRows * 4 +
+  const size_t lds = (GV ? 0 : kRing * (size_t)SLOT) + (size_t)kRows * kNLS * 2 + 2 * kRows * 4 +
                      (size_t)kRows * kMaxG * 2 * 4 + (size_t)kRows * 6 * 4;
-  auto kern = ipe16_sweep_kernel<KSD, ARGMIN, LB>;
+  auto kern = ipe16_sweep_kernel<KSD, ARGMIN, LB, GV>;
   static int attr = 0;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1571,7 +1661,8 @@ extern "C" {
 //   upkeep), [52] lb valid (skip allowed), [53] smax [1], [54] Rc [k],
 //   [55] lbo, [56] dhint, [57] sweep rows, [58] sweep row count, [59] ea2,
 //   [60] |c|^2 by operand column [k_pad], [61..63] first tile of groups 1..3,
-//   [64] mw [k] (row skip: nearest wild centroid)
+//   [64] mw [k] (row skip: nearest wild centroid), [65] V (0: the sweep's own
+//   MFMAs; required for d_pad > 256), [66] rows of V
 // da: [0] eps, [1] alpha, [2] m_t, [3] min band width (relative to Dl)
 int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -1613,7 +1704,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
   const int Q = (int)ia[30];
   const double eps = da[0];
   if (Q < 1 || Q > kIpeMaxQ || !(Q & 1) || k < 1 || k > 16384 || k_pad % 64 || k_pad < k ||
-      d < 1 || d > d_pad || d_pad % 16 || d_pad > 256 || !(eps > 0.0) || ia[50] < 1 ||
+      d < 1 || d > d_pad || d_pad % 16 || d_pad > 1024 || (d_pad > 256 && !ia[65]) ||
+      !(eps > 0.0) || ia[50] < 1 ||
       ia[50] > kMaxG || ia[50] > k_pad / 64)
     return (int)hipErrorInvalidValue;
   auto P = [&](int i) -> void* { return (void*)(intptr_t)ia[i]; };
@@ -1679,8 +1771,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     hipLaunchKernelGGL(ipe16_prep_kernel<KSD>, pg, dim3(256), 0, st, a); break;
       CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
 #undef CASE
-      default:
-        return (int)hipErrorInvalidValue;
+      default:   // wide rows: chunked canonical dots (zeros past d add +0)
+        hipLaunchKernelGGL(ipe16_prep_kernel<64>, pg, dim3(256), 0, st, a);
     }
     return (int)hipGetLastError();
   }
@@ -1725,6 +1817,26 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     a.cert.du = (float)d * 0x1p-24f;
     if (!am && (!a.rows || !a.ea2 || !a.cns || (double)a.cert.inv_a2 != a.inv_a2))
       return (int)hipErrorInvalidValue;
+    a.V = (const float*)P(65);
+    if (a.V) {
+      // wide rows (or forced): the values first, then the sweep without MFMA;
+      // ia[66] = the rows V holds (>= the positions of this launch)
+      if (ia[66] < n) return (int)hipErrorInvalidValue;
+      ValuesArgs v;
+      v.Xh = a.Xh;
+      v.C = a.C;
+      v.rows = a.rows;
+      v.rows_count = a.rows_count;
+      v.n = n;
+      v.ksd = d_pad / 16;
+      v.k_pad = k_pad;
+      v.V = (float*)P(65);
+      hipLaunchKernelGGL(ipe16_values_kernel, dim3((unsigned)((n + 127) / 128), (unsigned)(k_pad / 64)),
+                         dim3(256), 0, st, v);
+      return am ? launch_sweep<1, true, false, true>(a, st)
+                : (a.lb ? launch_sweep<1, false, true, true>(a, st)
+                        : launch_sweep<1, false, false, true>(a, st));
+    }
     switch (d_pad) {
 #define CASE(KSD)                                                                  \
   case KSD * 16:                                                                   \
@@ -1773,8 +1885,8 @@ int sq_ipe16(int op, const long long* ia, const double* da, void* stream) {
     hipLaunchKernelGGL(ipe16_near_kernel<KSD>, dim3((unsigned)grid), dim3(256), 0, st, a); break;
       CASE(1) CASE(2) CASE(4) CASE(8) CASE(16)
 #undef CASE
-      default:
-        return (int)hipErrorInvalidValue;
+      default:   // wide rows
+        hipLaunchKernelGGL(ipe16_near_kernel<64>, dim3((unsigned)grid), dim3(256), 0, st, a);
     }
     return (int)hipGetLastError();
   }

@@ -1179,7 +1179,7 @@ def _rc(rc, name):
 # ------------------------------------------------ certified fp16 IPE screen
 # (csrc/ipe16.hip): the IPE E-step without a per-pair fp32 inner product.
 
-IPE16_D = FAST_D          # d_pad of the fp16 sweep (one LDS ring slot per tile)
+IPE16_D = X64_D           # d_pad of the fp16 sweep (> 256: values pass first, see Ipe16.gv)
 IPE16_MAX_K = 16384       # centroid ids in 14 bits
 IPE16_CAPR = 64           # listed pairs per row (csrc kCapR)
 IPE16_CHUNK = 1 << 22     # rows per launch group (bounds the pair list: 8 B x 64 per row)
@@ -1213,9 +1213,18 @@ class Ipe16:
         self.rflag = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
         self.best = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         self.dense_rows = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-        cm = min(n, IPE16_CHUNK)
+        # wide rows (d_pad > 256; SQ_IPE16_GV=1 forces it): the sweep's
+        # values [chunk rows][k_pad] fp32 come from a separate MFMA pass
+        # (csrc/ipe16.hip ipe16_values_kernel, bit-identical values), the
+        # chunk sized so that buffer stays <= 2 GiB
+        self.gv = self.d_pad > 256 or os.environ.get("SQ_IPE16_GV", "0") == "1"
+        self.chunk = (min(IPE16_CHUNK, max(4096, (1 << 29) // self.k_pad)) if self.gv
+                      else IPE16_CHUNK)
+        cm = min(n, self.chunk)
+        self.V = (torch.empty((max(cm, 1), self.k_pad), dtype=torch.float32, device=dev)
+                  if self.gv else None)
         self.list = torch.empty(max(cm * IPE16_CAPR, 1), dtype=torch.int64, device=dev)
-        self.nchunks = max(1, -(-n // IPE16_CHUNK))
+        self.nchunks = max(1, -(-n // self.chunk))
         # per chunk: [list count, dense count, sweep row count]
         self.counts = torch.zeros((self.nchunks, 3), dtype=torch.int32, device=dev)
         self.counts_host = torch.zeros((self.nchunks, 3), dtype=torch.int32, pin_memory=True)
@@ -1459,6 +1468,8 @@ class Ipe16:
         if skip:
             self._skip_bounds(C32)
         ia = torch.zeros(72, dtype=torch.int64)
+        if self.gv:
+            ia[65], ia[66] = self.V.data_ptr(), self.V.shape[0]
         ia[48] = self.perm.data_ptr()
         ia[60] = self.cns.data_ptr()
         ia[49] = self.gS.data_ptr()
@@ -1489,7 +1500,7 @@ class Ipe16:
                 raise RuntimeError(f"ipe16 op {op} failed (hip error {rc})")
 
         for c in range(self.nchunks):
-            s, e = c * IPE16_CHUNK, min(n, (c + 1) * IPE16_CHUNK)
+            s, e = c * self.chunk, min(n, (c + 1) * self.chunk)
             ia[0] = X.data_ptr() + s * ldx * 4
             ia[3] = self.Xh.data_ptr() + s * self.d_pad * 2
             ia[5] = ia[6] = hint.data_ptr() + s * 4
@@ -1526,7 +1537,7 @@ class Ipe16:
         parts = [(c, int(nd)) for c, nd in enumerate(dense) if nd > 0]
         if len(parts) == 1:
             c, nd = parts[0]
-            s, e = c * IPE16_CHUNK, min(n, (c + 1) * IPE16_CHUNK)
+            s, e = c * self.chunk, min(n, (c + 1) * self.chunk)
             fallback(self.dense_rows[s:], self.counts[c, 1:2], nd, self.thr[s:e], self.hj[s:e],
                      s, e)
         elif parts:
@@ -1540,7 +1551,7 @@ class Ipe16:
                 self._dense_cnt = torch.zeros(1, dtype=torch.int32, device=self.dense_rows.device)
             off = 0
             for c, nd in parts:
-                s = c * IPE16_CHUNK
+                s = c * self.chunk
                 torch.add(self.dense_rows[s:s + nd], s, out=self._dense_all[off:off + nd])
                 off += nd
             self._dense_cnt.fill_(tot)
