@@ -356,6 +356,27 @@ def _mnist_extra(extra, a, comm, dev):
         extra["mnist70kx784_qmeans_fit_s"] = t
         extra["mnist70kx784_qmeans_lloyd_ms_per_step"] = round(
             1e3 * getattr(qm, "fit_phase_s_", {}).get("lloyd_s", float("nan")) / max(qm.n_iter_, 1), 4)
+        # the reference default distance mode (IPE) at this shape: d_pad 896
+        # runs the certified fp16 screen with its values pass (ops.kmeans.
+        # Ipe16.gv), the fp32 IPE kernel only for the screen's dense rows
+        t, qm = wall(lambda: QMeans(n_clusters=k, delta=a.delta, true_distance_estimate=True,
+                                    intermediate_error=True, true_tomography=False, n_init=1,
+                                    max_iter=20, tol=0.0, random_state=0, device=dev).fit(sa))
+        extra["mnist70kx784_qmeans_ipe_fit_s"] = t
+        extra["mnist70kx784_qmeans_ipe_lloyd_ms_per_step"] = round(
+            1e3 * getattr(qm, "fit_phase_s_", {}).get("lloyd_s", float("nan")) / max(qm.n_iter_, 1), 4)
+        from sq_learn_amd.models.cluster._lloyd import LloydEngine
+        eng = LloydEngine(X, k, delta=a.delta, true_distance_estimate=True,
+                          intermediate_error=True, true_tomography=False, seed=a.seed, comm=comm,
+                          row_offset=s0)
+        eng.set_centers(torch.as_tensor(qm.cluster_centers_, dtype=torch.float32, device=dev))
+        for _ in range(3):
+            eng.step()[1].tolist()
+        i16 = getattr(eng, "_ipe16", None)
+        extra["mnist70kx784_ipe16_screen"] = bool(i16 is not None and i16.gv)
+        extra["mnist70kx784_ipe16_dense_row_frac"] = (
+            round(i16.last_dense / max(X.shape[0], 1), 6) if i16 is not None else None)
+        del eng
         del X, sa
         torch.cuda.empty_cache()
         if comm.world_size == 1:
