@@ -1225,7 +1225,11 @@ template <int NS>
 __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a) {
   constexpr int DQ = NS * 64;
   constexpr int NWV = kBfThreads / 64;
-  // dynamic LDS: [2][ncb 16][DQ] int8 (sized to the columns in use: occupancy)
+  // dynamic LDS: [2][ncb 16][DQ + 16] int8 (sized to the columns in use:
+  // occupancy).  The 16-B pad per column: a ds_read_b128 lane group reads 8
+  // columns at one offset, which a DQ (multiple of 256 B) stride put on one
+  // bank slot - 8-way conflicts, ~10 LDS cycles per read in the PMC
+  constexpr int CS = DQ + 16;
   extern __shared__ __attribute__((aligned(16))) int8_t cbs[];
   __shared__ float cpar[kScol][3];
   __shared__ int lcnt[16];
@@ -1239,7 +1243,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
     sps[threadIdx.x] = (unsigned long long)a.tab[(size_t)threadIdx.x * kKppNF + F_SURV];
   }
   const int ncol = nr * tp, ncb = (ncol + 15) / 16;
-  auto cb = [&](int hl, int col) -> int8_t* { return cbs + ((size_t)hl * ncb * 16 + col) * DQ; };
+  auto cb = [&](int hl, int col) -> int8_t* { return cbs + ((size_t)hl * ncb * 16 + col) * CS; };
   // stage every restart's trials: column c = r tp + j (j >= t: zero)
   for (int e = threadIdx.x; e < 2 * ncb * 16 * (DQ / 16); e += kBfThreads) {
     const int hl = e / (ncb * 16 * (DQ / 16));
@@ -1661,9 +1665,19 @@ int sq_kmpp_batch(int op, const long long* ia, void* stream) {
         break;
       }
       if (!a.Xq || (a.dq & 63) || a.dq < a.d || a.dq > 256) return (int)hipErrorInvalidValue;
-      const size_t lds = (size_t)2 * ((a.nr * a.tp + 15) / 16) * 16 * a.dq;
+      const size_t lds = (size_t)2 * ((a.nr * a.tp + 15) / 16) * 16 * (a.dq + 16);
+      // (the padded columns can pass 64 KiB at kScol columns)
 #define LAUNCH(NS)                                                                               \
-  hipLaunchKernelGGL(kmpp_bound_fused_kernel<NS>, dim3((unsigned)a.G), dim3(kBfThreads), lds, st, a)
+  do {                                                                                           \
+    static bool attr = false;                                                                    \
+    if (!attr) {                                                                                 \
+      (void)hipFuncSetAttribute((const void*)kmpp_bound_fused_kernel<NS>,                        \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);        \
+      attr = true;                                                                               \
+    }                                                                                            \
+    hipLaunchKernelGGL(kmpp_bound_fused_kernel<NS>, dim3((unsigned)a.G), dim3(kBfThreads), lds, \
+                       st, a);                                                                   \
+  } while (0)
       switch (a.dq / 64) {
         case 1: LAUNCH(1); break;
         case 2: LAUNCH(2); break;
