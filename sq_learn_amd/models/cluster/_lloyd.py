@@ -586,8 +586,9 @@ class LloydEngine:
         return lab, mind, mind.double().sum().reshape(1)
 
     def _ipe16_ok(self):
-        """The certified fp16 IPE screen (csrc/ipe16.hip) covers d <= 256,
-        k <= 16384, odd Q <= 31, fp32 rows; SQ_IPE16=0 disables it."""
+        """The certified fp16 IPE screen (csrc/ipe16.hip) covers d <= 1024
+        (above d_pad 256 through its values pass), k <= 16384, odd Q <= 31,
+        fp32 rows; SQ_IPE16=0 disables it."""
         return (self.device.type == "cuda" and self.Xf.dtype == torch.float32
                 and self.Xf.stride(1) == 1 and self.ipe_Q % 2 == 1 and self.ipe_Q <= 31
                 and K.pad_features(self.d) in K.IPE16_D and self.k <= K.IPE16_MAX_K
