@@ -804,7 +804,10 @@ class LloydEngine:
         self._C_prev = self.C
         tot_inertia = packed[-1]
         old = self.C
-        new = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1e-300)[:, None],
+        # (no clamp of the counts: where() discards the empty clusters' 0/0, and
+        # every distinct torch kernel costs 30-130 ms of lazy loading at its
+        # first use in a process - the first IPE step paid for clamp and pow)
+        new = torch.where(counts[:, None] > 0, sums / counts[:, None],
                           old.double() if self.empty_policy == 0 else torch.zeros_like(sums))
         new = new.to(old.dtype).contiguous()
         b = self._noise_bound()
@@ -814,7 +817,8 @@ class LloydEngine:
         self.C = new
         if self.intermediate_error and self.true_tomography and self.delta > 0:
             self._true_tomography_centers()
-        shift = ((self.C.double() - old.double()) ** 2).sum()
+        dd = self.C.double() - old.double()
+        shift = (dd * dd).sum()
         return torch.stack([tot_inertia, shift, torch.zeros((), dtype=torch.float64,
                                                             device=self.device)])
 
