@@ -1182,7 +1182,11 @@ def _rc(rc, name):
 IPE16_D = X64_D           # d_pad of the fp16 sweep (> 256: values pass first, see Ipe16.gv)
 IPE16_MAX_K = 16384       # centroid ids in 14 bits
 IPE16_CAPR = 64           # listed pairs per row (csrc kCapR)
-IPE16_CHUNK = 1 << 22     # rows per launch group (bounds the pair list: 8 B x 64 per row)
+# rows per launch group at most (bounds the pair list: 8 B x 64 per row, 8.6 GB
+# at 2^24 rows of 288 GB); the groups of a shard are balanced.  10M x 256,
+# k = 1024: 3 / 2 / 1 groups -> 11.87 / 11.66 / 11.39 ms per IPE step (every
+# launch's tail is paid once per group)
+IPE16_CHUNK = int(os.environ.get("SQ_IPE16_CHUNK", 1 << 24))
 
 
 class Ipe16:
@@ -1218,8 +1222,10 @@ class Ipe16:
         # (csrc/ipe16.hip ipe16_values_kernel, bit-identical values), the
         # chunk sized so that buffer stays <= 2 GiB
         self.gv = self.d_pad > 256 or os.environ.get("SQ_IPE16_GV", "0") == "1"
-        self.chunk = (min(IPE16_CHUNK, max(4096, (1 << 29) // self.k_pad)) if self.gv
-                      else IPE16_CHUNK)
+        cap = (min(IPE16_CHUNK, max(4096, (1 << 29) // self.k_pad)) if self.gv
+               else IPE16_CHUNK)
+        nch = max(1, -(-n // cap))
+        self.chunk = min(cap, ((-(-n // nch) + 255) // 256) * 256) if n > 0 else cap
         cm = min(n, self.chunk)
         self.V = (torch.empty((max(cm, 1), self.k_pad), dtype=torch.float32, device=dev)
                   if self.gv else None)
