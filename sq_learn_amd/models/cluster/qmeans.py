@@ -250,12 +250,13 @@ class QMeans(TransformerMixin, ClusterMixin, BaseEstimator):
         phase("setup_s")
         # the k-means++ initialisations of every restart at once (the draws
         # in the reference order: the Lloyd loop never touches rs), one
-        # device pass per centre for all restarts; not with checkpoints
-        # (they save rs at restart boundaries)
+        # device pass per centre for all restarts - also for one restart (its
+        # fused passes: 0.449 vs 0.466 s sequentially at 10M x 256, k = 1024);
+        # not with checkpoints (they save rs at restart boundaries)
         pre = None
         restart_inertias = []
         if (isinstance(self.init, str) and self.init == "k-means++" and resume is None
-                and self._n_init - start_restart > 1 and self.checkpoint_dir is None):
+                and self._n_init - start_restart >= 1 and self.checkpoint_dir is None):
             pre = kmeans_plusplus_restarts(data_c, self.n_clusters, rs,
                                            self._n_init - start_restart)
         for restart in range(start_restart, self._n_init):
