@@ -1220,9 +1220,9 @@ class Ipe16:
         # wide rows (d_pad > 256; SQ_IPE16_GV=1 forces it): the sweep's
         # values [chunk rows][k_pad] fp32 come from a separate MFMA pass
         # (csrc/ipe16.hip ipe16_values_kernel, bit-identical values), the
-        # chunk sized so that buffer stays <= 2 GiB
+        # chunk sized so that buffer stays <= 8 GiB
         self.gv = self.d_pad > 256 or os.environ.get("SQ_IPE16_GV", "0") == "1"
-        cap = (min(IPE16_CHUNK, max(4096, (1 << 29) // self.k_pad)) if self.gv
+        cap = (min(IPE16_CHUNK, max(4096, (1 << 31) // self.k_pad)) if self.gv
                else IPE16_CHUNK)
         nch = max(1, -(-n // cap))
         self.chunk = min(cap, ((-(-n // nch) + 255) // 256) * 256) if n > 0 else cap
