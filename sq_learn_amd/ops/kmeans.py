@@ -9,6 +9,8 @@ Philox keys (reference ``_dmeans.py:732-830``).
 import math
 import os
 
+import numpy as np
+
 import torch
 
 from ..runtime.rng import RngKey, philox4x32, MASK32
@@ -1272,7 +1274,7 @@ class Ipe16:
             self.counts[-1, 2].zero_()
         if op == 2:
             self.counts[-1, :2].zero_()
-        return nat.native().ipe16(op, ia.data_ptr(), da.data_ptr(), st)
+        return nat.native().ipe16(op, ia.ctypes.data, da.ctypes.data, st)
 
     @staticmethod
     @__import__("functools").lru_cache(maxsize=64)
@@ -1330,7 +1332,9 @@ class Ipe16:
             sh, nn, tau, wn = self._sb_work
             prev = self.C_prev is not None and self.C_prev.shape == C32.shape
             C32c = C32.contiguous()
-            ia = torch.zeros(20, dtype=torch.int64)
+            # (host argument arrays in numpy: a torch CPU tensor costs a few us
+            # per element assignment, on the step boundary's critical path)
+            ia = np.zeros(20, dtype=np.int64)
             ia[0] = C32c.data_ptr()
             ia[1] = self.C_prev.data_ptr() if prev else 0
             ia[2], ia[4] = G.data_ptr(), self.perm.data_ptr()
@@ -1339,8 +1343,8 @@ class Ipe16:
                 ia[9 + g] = self.gstart[g]
             ia[13], ia[14], ia[15], ia[16] = sh.data_ptr(), nn.data_ptr(), tau.data_ptr(), wn.data_ptr()
             ia[17], ia[18], ia[19] = self.smax.data_ptr(), self.mw.data_ptr(), self.Rc.data_ptr()
-            da = torch.tensor([1e-12], dtype=torch.float64)
-            nat.native().ipe16(5, ia.data_ptr(), da.data_ptr(), nat.stream_handle(dev))
+            da = np.array([1e-12], dtype=np.float64)
+            nat.native().ipe16(5, ia.ctypes.data, da.ctypes.data, nat.stream_handle(dev))
             if prev:
                 self.last_wild = wn
             self.C_prev = C32c.clone()
@@ -1473,7 +1477,8 @@ class Ipe16:
         skip = self.skip
         if skip:
             self._skip_bounds(C32)
-        ia = torch.zeros(72, dtype=torch.int64)
+        # (numpy host arrays: see _skip_bounds)
+        ia = np.zeros(72, dtype=np.int64)
         if self.gv:
             ia[65], ia[66] = self.V.data_ptr(), self.V.shape[0]
         ia[48] = self.perm.data_ptr()
@@ -1481,8 +1486,8 @@ class Ipe16:
         ia[49] = self.gS.data_ptr()
         ia[50] = self.G
         ia[61], ia[62], ia[63] = self.gstart[1], self.gstart[2], self.gstart[3]
-        da = torch.tensor([float(eps), self.alpha, self.band_m(int(Q), min(self.ht, 9.0e-4)),
-                           self.min_width], dtype=torch.float64)
+        da = np.array([float(eps), self.alpha, self.band_m(int(Q), min(self.ht, 9.0e-4)),
+                       self.min_width], dtype=np.float64)
         ldx = X.stride(0)
         ia[1] = ldx
         ia[2] = C32.data_ptr()
@@ -1497,7 +1502,7 @@ class Ipe16:
         for i, kk in ((32, key), (36, tie), (40, skey), (44, bkey)):
             ia[i], ia[i + 1], ia[i + 2], ia[i + 3] = kk.k0, kk.k1, kk.s0, kk.s1
         self.counts.zero_()
-        iap, dap = ia.data_ptr(), da.data_ptr()
+        iap, dap = ia.ctypes.data, da.ctypes.data
         last = self.nchunks - 1
 
         def run(op):
