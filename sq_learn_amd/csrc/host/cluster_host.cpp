@@ -6,6 +6,7 @@
 //   * expected mutual information of a contingency table under the
 //     hypergeometric model (reference
 //     ``metrics/cluster/_expected_mutual_info_fast.pyx``), OpenMP over rows.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <vector>
@@ -137,4 +138,58 @@ extern "C" void sqh_optics_order(const double* X, int64_t n, int64_t d, const do
       if (rd < reach[j]) { reach[j] = rd; pred[j] = pt; }
     }
   }
+}
+
+// Norm groups of the ipe16 IPE screen (ops.kmeans.Ipe16.group_tiles): the
+// first tile of each of G contiguous tile ranges of the |c|^2-sorted
+// centroids minimising sum_g (centroids in g) x (|c|^2 range of g), by a DP
+// over tile cuts - the same fp64 expressions and first-minimum ties as the
+// numpy version, once per IPE step on the host (the numpy form cost ~0.1 ms
+// of the step boundary, where the GPU waits for it).
+extern "C" int sqh_group_tiles(const double* cs, int64_t k, int nt, int G, int* out) {
+  if (nt < 1 || k < 1 || G < 1) return 1;
+  if (G == 1) {
+    out[0] = 0;
+    return 0;
+  }
+  const double inf = INFINITY;
+  std::vector<double> lo1(nt + 1, 0.0), hib(nt + 1, 0.0), cc(nt + 1, 0.0);
+  for (int t = 0; t < nt; ++t) {
+    const int64_t a = 64 * (int64_t)t < k - 1 ? 64 * (int64_t)t : k - 1;
+    const int64_t b = 64 * (int64_t)t + 63 < k - 1 ? 64 * (int64_t)t + 63 : k - 1;
+    lo1[t] = cs[a];
+    hib[t + 1] = cs[b];
+    const int64_t c = k - 64 * (int64_t)t;
+    cc[t + 1] = cc[t] + (double)(c < 0 ? 0 : (c > 64 ? 64 : c));
+  }
+  std::vector<double> best((size_t)(G + 1) * (nt + 1), inf);
+  std::vector<int> arg((size_t)(G + 1) * (nt + 1), 0);
+  best[0] = 0.0;
+  for (int g = 1; g <= G; ++g) {
+    const double* bp = &best[(size_t)(g - 1) * (nt + 1)];
+    for (int b = 0; b <= nt; ++b) {
+      double m = inf;
+      int am = 0;
+      for (int a = 0; a <= nt; ++a) {
+        double tv = inf;
+        if (a >= g - 1 && a < b) tv = bp[a] + (cc[b] - cc[a]) * (hib[b] - lo1[a]);
+        if (tv < m) {
+          m = tv;
+          am = a;
+        }
+      }
+      arg[(size_t)g * (nt + 1) + b] = am;
+      best[(size_t)g * (nt + 1) + b] = b < g ? inf : m;
+    }
+  }
+  std::vector<int> cuts;
+  int b = nt;
+  for (int g = G; g >= 1; --g) {
+    const int a = arg[(size_t)g * (nt + 1) + b];
+    cuts.push_back(a);
+    b = a;
+  }
+  std::sort(cuts.begin(), cuts.end());
+  for (int g = 0; g < G; ++g) out[g] = cuts[g];
+  return 0;
 }

@@ -40,6 +40,7 @@ _SIGS = {
     "sqh_svml_copy": (None, [_P, _P, _P, _P, _P, _P, _P]),
     "sqh_svml_free": (None, [_P]),
     "sqh_dbscan_inner": (None, [_P, _P, _P, _LL, _P]),
+    "sqh_group_tiles": (_I, [_P, _LL, _I, _I, _P]),
     "sqh_expected_mutual_info": (_D, [_P, _LL, _P, _LL, _LL]),
     "sqh_sparse_manhattan": (None, [_P, _P, _P, _P, _P, _P, _LL, _LL, _P]),
     "sqh_cholesky_delete": (None, [_P, _LL, _LL, _LL]),

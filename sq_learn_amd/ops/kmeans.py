@@ -1425,6 +1425,20 @@ class Ipe16:
 
     @staticmethod
     def group_tiles(cs, k, nt, G):
+        """``group_tiles_np`` in the host library (``sqh_group_tiles``, the same
+        fp64 expressions and ties): called once per IPE step while the GPU
+        waits at the step boundary."""
+        import ctypes
+        from . import _host
+        c = np.ascontiguousarray(cs, dtype=np.float64)
+        out = (ctypes.c_int * max(int(G), 1))()
+        rc = _host.lib().sqh_group_tiles(c.ctypes.data, int(k), int(nt), int(G), out)
+        if rc:
+            raise ValueError(f"sqh_group_tiles: bad arguments (k={k}, nt={nt}, G={G})")
+        return [int(v) for v in out[:max(int(G), 1)]]
+
+    @staticmethod
+    def group_tiles_np(cs, k, nt, G):
         """First tile of each of the G norm groups: contiguous tile ranges of
         the sorted norms ``cs`` minimising sum_g (centroids in g) x (|c|^2
         range of g) - a row's band loses about its group's S range, so a few
