@@ -1226,15 +1226,19 @@ template <int NS>
 __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a) {
   constexpr int DQ = NS * 64;
   constexpr int NWV = kBfThreads / 64;
-  // dynamic LDS: [2][ncb 16][DQ + 16] int8 (sized to the columns in use:
-  // occupancy).  The 16-B pad per column: a ds_read_b128 lane group reads 8
-  // columns at one offset, which a DQ (multiple of 256 B) stride put on one
-  // bank slot - 8-way conflicts, ~10 LDS cycles per read in the PMC
-  constexpr int CS = DQ + 16;
+  // dynamic LDS: [2][ncb 16][CS] int8 (sized to the columns in use:
+  // occupancy).  A ds_read_b128 lane group reads 8 columns at one offset,
+  // which a DQ (multiple of 256 B) stride put on one bank slot - 8-way
+  // conflicts, ~10 LDS cycles per read in the PMC.  NS = 4 (16 pieces per
+  // column): piece p of column c is stored at p ^ (c & 15), so the group's
+  // two 8-lane halves (kb 0 / 1, complementary c16 sets) hit 16 distinct
+  // slots; other NS: a 16-B pad per column
+  constexpr int CS = NS == 4 ? DQ : DQ + 16;
+  auto swz = [](int p, int c) { return NS == 4 ? (p ^ (c & 15)) : p; };
   extern __shared__ __attribute__((aligned(16))) int8_t cbs[];
   __shared__ float cpar[kScol][3];
   __shared__ int lcnt[16];
-  __shared__ float sclo[NWV * 256];
+  __shared__ float sclo[NWV * 16 * 17];   // row stride 17: no ds_write_b32 bank aliasing
   __shared__ unsigned long long spc[16], spe[16], sps[16];   // closest / exact / surv
   const int blk = blockIdx.x;
   const int tp = a.tp, t = a.t, nr = a.nr;
@@ -1255,7 +1259,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
     if (r < nr && j < t)
       v = *reinterpret_cast<const uint4*>(kf<const int8_t*>(a, r, F_CANDQ) +
                                           ((size_t)(hl * 16 + j) * a.dq + piece * 16));
-    *reinterpret_cast<uint4*>(cb(hl, col) + piece * 16) = v;
+    *reinterpret_cast<uint4*>(cb(hl, col) + swz(piece, col) * 16) = v;
   }
   for (int col = threadIdx.x; col < ncb * 16; col += kBfThreads) {
     const int r = col / tp, j = col % tp;
@@ -1280,7 +1284,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
   // per-row scalars and the rows' closest values of the restarts they are
   // live in (lane (kb, c16): restarts kb, kb + 4, kb + 8, kb + 12 of row
   // slot c16); the current group's closest values go through LDS
-  float* scl = sclo + wave * 256;   // [16 row slots][16 restarts]
+  float* scl = sclo + wave * 16 * 17;   // [16 row slots][16 restarts (+1 pad)]
   int nrow = -1;
   unsigned nbits = 0u;
   kpp_v4i nav[NS];
@@ -1326,7 +1330,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
     const float rs = nrs, re_ = nre;
     const int rq2 = nq2;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) scl[c16 * 16 + kb + 4 * u] = ncl[u];
+    for (int u = 0; u < 4; ++u) scl[c16 * 17 + kb + 4 * u] = ncl[u];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1358,8 +1362,9 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
       kpp_v4i hi = kpp_v4i{0, 0, 0, 0}, lo = kpp_v4i{0, 0, 0, 0};
 #pragma unroll
       for (int s4 = 0; s4 < NS; ++s4) {
-        const kpp_v4i bh = *reinterpret_cast<const kpp_v4i*>(cb(0, cbk * 16 + c16) + 64 * s4 + 16 * kb);
-        const kpp_v4i bl = *reinterpret_cast<const kpp_v4i*>(cb(1, cbk * 16 + c16) + 64 * s4 + 16 * kb);
+        const int pc = swz(4 * s4 + kb, c16) * 16;
+        const kpp_v4i bh = *reinterpret_cast<const kpp_v4i*>(cb(0, cbk * 16 + c16) + pc);
+        const kpp_v4i bl = *reinterpret_cast<const kpp_v4i*>(cb(1, cbk * 16 + c16) + pc);
         hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s4], bh, hi, 0, 0, 0);
         lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s4], bl, lo, 0, 0, 0);
       }
@@ -1375,7 +1380,7 @@ __global__ void __launch_bounds__(kBfThreads) kmpp_bound_fused_kernel(KppArgs a)
         const float s = sv[i], er = erv[i], A = Av[i];
         bool need = false;
         if (jv && rr >= 0 && ((rbv[i] >> r) & 1u)) {
-          const float cl = scl[src * 16 + r];
+          const float cl = scl[src * 17 + r];
           const float dot = s * sc * ((float)hi[i] + (float)lo[i] * (1.0f / 254.0f));
           const float Dq = (A + cc2) - 2.0f * dot;
           const float Dlb = Dq - 1e-6f * (A + cc2 + 2.0f * fabsf(dot));
@@ -1668,7 +1673,7 @@ int sq_kmpp_batch(int op, const long long* ia, void* stream) {
         break;
       }
       if (!a.Xq || (a.dq & 63) || a.dq < a.d || a.dq > 256) return (int)hipErrorInvalidValue;
-      const size_t lds = (size_t)2 * ((a.nr * a.tp + 15) / 16) * 16 * (a.dq + 16);
+      const size_t lds = (size_t)2 * ((a.nr * a.tp + 15) / 16) * 16 * (a.dq == 256 ? 256 : a.dq + 16);
       // (the padded columns can pass 64 KiB at kScol columns)
 #define LAUNCH(NS)                                                                               \
   do {                                                                                           \
